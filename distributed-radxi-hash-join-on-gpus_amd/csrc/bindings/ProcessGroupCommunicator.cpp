@@ -1,0 +1,57 @@
+#include "ProcessGroupCommunicator.h"
+
+#include <cstring>
+
+#include "../utils/Debug.h"
+
+namespace hpcjoin {
+namespace comm {
+
+ProcessGroupCommunicator::ProcessGroupCommunicator(c10::intrusive_ptr<c10d::ProcessGroup> pg) : pg_(std::move(pg)) {
+  utils::setDebugRank(pg_->getRank());
+}
+
+static at::Tensor hostWords(const uint64_t *p, size_t n) {
+  at::Tensor t = at::empty({(int64_t)n}, at::TensorOptions().dtype(at::kLong));
+  if (n) std::memcpy(t.data_ptr(), p, n * 8);
+  return t;
+}
+
+void ProcessGroupCommunicator::allGatherHost(const uint64_t *send, uint64_t *recv, size_t count) {
+  std::vector<at::Tensor> in{hostWords(send, count)};
+  std::vector<std::vector<at::Tensor>> out(1);
+  for (uint32_t r = 0; r < size(); ++r) out[0].push_back(at::empty({(int64_t)count}, at::kLong));
+  pg_->allgather(out, in)->wait();
+  for (uint32_t r = 0; r < size(); ++r) std::memcpy(recv + r * count, out[0][r].data_ptr(), count * 8);
+}
+
+void ProcessGroupCommunicator::allReduceSumHost(uint64_t *data, size_t count) {
+  std::vector<at::Tensor> t{hostWords(data, count)};
+  pg_->allreduce(t)->wait();
+  std::memcpy(data, t[0].data_ptr(), count * 8);
+}
+
+void ProcessGroupCommunicator::barrier() { pg_->barrier()->wait(); }
+
+void ProcessGroupCommunicator::allToAllV(const uint64_t *send, const uint64_t *sendCounts,
+                                         const uint64_t *sendDispls, uint64_t *recv, const uint64_t *recvCounts,
+                                         const uint64_t *recvDispls, Location loc, hipStream_t) {
+  JOIN_ASSERT(loc == Location::Host, "PGComm", "ProcessGroupCommunicator moves host buffers only");
+  const uint32_t N = size();
+  std::vector<int64_t> ss(N), rs(N);
+  uint64_t st = 0, rt = 0;
+  for (uint32_t p = 0; p < N; ++p) {
+    JOIN_ASSERT(sendDispls[p] == sendDispls[0] + st && recvDispls[p] == recvDispls[0] + rt, "PGComm",
+                "all-to-allv regions must be contiguous and peer-ordered");
+    ss[p] = (int64_t)sendCounts[p];
+    rs[p] = (int64_t)recvCounts[p];
+    st += sendCounts[p];
+    rt += recvCounts[p];
+  }
+  at::Tensor in = at::from_blob(const_cast<uint64_t *>(send) + sendDispls[0], {(int64_t)st}, at::kLong);
+  at::Tensor out = at::from_blob(recv + recvDispls[0], {(int64_t)rt}, at::kLong);
+  pg_->alltoall_base(out, in, rs, ss)->wait();
+}
+
+}  // namespace comm
+}  // namespace hpcjoin

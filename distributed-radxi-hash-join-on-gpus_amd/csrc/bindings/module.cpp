@@ -1,0 +1,628 @@
+// pybind11 bindings of the native engine (built in-tree as hpcjoin/_C*.so).
+// The C++ core is the source of truth; Python adds launch/bootstrap glue,
+// the oracle and the benchmark harness.
+#include <torch/extension.h>
+
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <vector>
+
+#include "../comm/RcclCommunicator.h"
+#include "../comm/World.h"
+#include "../core/ExecContext.h"
+#include "../core/JoinConfig.h"
+#include "../data/Relation.h"
+#include "../host/HostOps.h"
+#include "../kernels/kernels.h"
+#include "../memory/Arena.h"
+#include "../memory/Pool.h"
+#include "../operators/HashJoin.h"
+#include "../performance/Measurements.h"
+#include "../utils/Hip.h"
+#include "ProcessGroupCommunicator.h"
+
+namespace py = pybind11;
+using namespace hpcjoin;
+
+namespace {
+
+Location locOf(const at::Tensor &t) { return t.is_cuda() ? Location::Device : Location::Host; }
+
+void syncIfDevice(Location l) {
+  if (l == Location::Device) HIP_CHECK(hipDeviceSynchronize());
+}
+
+void checkTuples(const at::Tensor &t, const char *name) {
+  TORCH_CHECK(t.dim() == 2 && t.size(1) == 2 && t.scalar_type() == at::kLong && t.is_contiguous(), name,
+              " must be a contiguous int64 tensor of shape [n, 2] (key, rid)");
+}
+
+void checkWords(const at::Tensor &t, const char *name) {
+  TORCH_CHECK(t.dim() == 1 && t.scalar_type() == at::kLong && t.is_contiguous(), name,
+              " must be a contiguous 1-D int64 tensor");
+}
+
+template <typename T>
+T *ptr(const at::Tensor &t) {
+  return reinterpret_cast<T *>(t.data_ptr());
+}
+
+at::TensorOptions like(const at::Tensor &t, at::ScalarType st = at::kLong) {
+  return at::TensorOptions().dtype(st).device(t.device());
+}
+
+void setDevice(const at::Tensor &t) {
+  if (t.is_cuda()) HIP_CHECK(hipSetDevice(t.get_device()));
+}
+
+// ---- single-relation network pass (one "rank", all partitions local) ------
+std::tuple<at::Tensor, at::Tensor> opNetPartition(const at::Tensor &tuples, int64_t bits, int64_t keyShift,
+                                                  bool wide, int64_t maxBlocks) {
+  checkTuples(tuples, "tuples");
+  setDevice(tuples);
+  const uint64_t n = tuples.size(0);
+  const uint32_t F = 1u << bits;
+  const Location l = locOf(tuples);
+  const auto g = kernels::partitionGeometry(n, (uint32_t)maxBlocks);
+  at::Tensor blockHist = at::empty({(int64_t)F * g.blocks}, like(tuples, at::kInt));
+  at::Tensor totals = at::empty({(int64_t)F}, like(tuples));
+  at::Tensor cursors = at::empty({(int64_t)F * g.blocks}, like(tuples));
+  at::Tensor out = wide ? at::empty({(int64_t)n, 2}, like(tuples)) : at::empty({(int64_t)n}, like(tuples));
+  const data::Tuple *in = ptr<const data::Tuple>(tuples);
+  if (l == Location::Device) {
+    kernels::netHistogram(in, n, bits, g, ptr<uint32_t>(blockHist), nullptr);
+    kernels::digitTotals(ptr<uint32_t>(blockHist), F, g.blocks, g.blocks, 1, ptr<uint64_t>(totals), nullptr);
+  } else {
+    host::netHistogram(in, n, bits, g, ptr<uint32_t>(blockHist));
+    host::digitTotals(ptr<uint32_t>(blockHist), F, g.blocks, g.blocks, 1, ptr<uint64_t>(totals));
+  }
+  at::Tensor begin = at::zeros({(int64_t)F + 1}, at::kLong);
+  at::Tensor totalsH = totals.cpu();
+  for (uint32_t d = 0; d < F; ++d) begin[d + 1] = begin[d].item<int64_t>() + totalsH[d].item<int64_t>();
+  at::Tensor base = begin.slice(0, 0, F).to(tuples.device()).contiguous();
+  if (l == Location::Device) {
+    kernels::netCursors(ptr<uint32_t>(blockHist), F, g.blocks, g.blocks, ptr<uint64_t>(base), ptr<uint64_t>(cursors),
+                        nullptr);
+    if (wide)
+      kernels::netScatterWide(in, n, bits, g, 0, g.blocks, ptr<uint64_t>(cursors), ptr<data::Tuple>(out), nullptr);
+    else
+      kernels::netScatter(in, n, bits, (uint32_t)keyShift, g, 0, g.blocks, ptr<uint64_t>(cursors), ptr<uint64_t>(out),
+                          nullptr);
+  } else {
+    host::netCursors(ptr<uint32_t>(blockHist), F, g.blocks, g.blocks, ptr<uint64_t>(base), ptr<uint64_t>(cursors));
+    host::netScatter(in, n, bits, (uint32_t)keyShift, g, 0, g.blocks, ptr<uint64_t>(cursors), out.data_ptr(), wide);
+  }
+  syncIfDevice(l);
+  return {out, begin};
+}
+
+at::Tensor opNetHistogram(const at::Tensor &tuples, int64_t bits, int64_t maxBlocks) {
+  checkTuples(tuples, "tuples");
+  setDevice(tuples);
+  const uint64_t n = tuples.size(0);
+  const uint32_t F = 1u << bits;
+  const auto g = kernels::partitionGeometry(n, (uint32_t)maxBlocks);
+  at::Tensor blockHist = at::empty({(int64_t)F * g.blocks}, like(tuples, at::kInt));
+  at::Tensor totals = at::empty({(int64_t)F}, like(tuples));
+  if (tuples.is_cuda()) {
+    kernels::netHistogram(ptr<data::Tuple>(tuples), n, bits, g, ptr<uint32_t>(blockHist), nullptr);
+    kernels::digitTotals(ptr<uint32_t>(blockHist), F, g.blocks, g.blocks, 1, ptr<uint64_t>(totals), nullptr);
+    HIP_CHECK(hipDeviceSynchronize());
+  } else {
+    host::netHistogram(ptr<data::Tuple>(tuples), n, bits, g, ptr<uint32_t>(blockHist));
+    host::digitTotals(ptr<uint32_t>(blockHist), F, g.blocks, g.blocks, 1, ptr<uint64_t>(totals));
+  }
+  return totals;
+}
+
+// ---- local pass over a partition-major buffer (each input partition = one lp)
+std::tuple<at::Tensor, at::Tensor> opLocalPartition(const at::Tensor &values, const at::Tensor &partBeginIn,
+                                                    int64_t shift, int64_t bits, bool wide) {
+  if (wide)
+    checkTuples(values, "values");
+  else
+    checkWords(values, "values");
+  setDevice(values);
+  at::Tensor pbIn = partBeginIn.cpu().contiguous();
+  const uint32_t owned = (uint32_t)pbIn.size(0) - 1;
+  const uint32_t F = 1u << bits;
+  std::vector<kernels::LocalItem> items;
+  std::vector<uint32_t> lb(owned + 1);
+  std::vector<uint64_t> base(owned + 1);
+  for (uint32_t lp = 0; lp < owned; ++lp) {
+    lb[lp] = (uint32_t)items.size();
+    const uint64_t b = pbIn[lp].item<int64_t>(), e = pbIn[lp + 1].item<int64_t>();
+    base[lp] = b;
+    for (uint64_t o = b; o < e; o += kernels::LOCAL_ITEM_MAX)
+      items.push_back({o, (uint32_t)std::min<uint64_t>(kernels::LOCAL_ITEM_MAX, e - o), lp});
+  }
+  lb[owned] = (uint32_t)items.size();
+  base[owned] = owned ? (uint64_t)pbIn[owned].item<int64_t>() : 0;
+  const uint32_t nItems = (uint32_t)items.size();
+  at::Tensor out = at::empty_like(values);
+  at::Tensor partBegin = at::empty({(int64_t)owned * F + 1}, like(values));
+  at::Tensor itemHist = at::empty({std::max<int64_t>(1, (int64_t)nItems * F)}, like(values, at::kInt));
+  at::Tensor itemCursors = at::empty({std::max<int64_t>(1, (int64_t)nItems * F)}, like(values));
+  if (values.is_cuda()) {
+    at::Tensor dItems = at::empty({std::max<int64_t>(1, (int64_t)nItems * 2)}, like(values));
+    at::Tensor dLb = at::empty({(int64_t)owned + 1}, like(values, at::kInt));
+    at::Tensor dBase = at::empty({(int64_t)owned + 1}, like(values));
+    HIP_CHECK(hipMemcpy(dItems.data_ptr(), items.data(), nItems * sizeof(kernels::LocalItem), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dLb.data_ptr(), lb.data(), (owned + 1) * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dBase.data_ptr(), base.data(), (owned + 1) * 8, hipMemcpyHostToDevice));
+    const auto *di = ptr<const kernels::LocalItem>(dItems);
+    kernels::localHistogram(values.data_ptr(), wide, di, nItems, (uint32_t)shift, (uint32_t)bits, ptr<uint32_t>(itemHist),
+                            nullptr);
+    kernels::localCursors(ptr<uint32_t>(itemHist), ptr<uint32_t>(dLb), owned, (uint32_t)bits, ptr<uint64_t>(dBase),
+                          ptr<uint64_t>(itemCursors), ptr<uint64_t>(partBegin), nullptr);
+    kernels::localScatter(values.data_ptr(), wide, di, nItems, (uint32_t)shift, (uint32_t)bits,
+                          ptr<uint64_t>(itemCursors), out.data_ptr(), nullptr);
+    HIP_CHECK(hipDeviceSynchronize());
+  } else {
+    host::localHistogram(values.data_ptr(), wide, items.data(), nItems, (uint32_t)shift, (uint32_t)bits,
+                         ptr<uint32_t>(itemHist));
+    host::localCursors(ptr<uint32_t>(itemHist), lb.data(), owned, (uint32_t)bits, base.data(),
+                       ptr<uint64_t>(itemCursors), ptr<uint64_t>(partBegin));
+    host::localScatter(values.data_ptr(), wide, items.data(), nItems, (uint32_t)shift, (uint32_t)bits,
+                       ptr<uint64_t>(itemCursors), out.data_ptr());
+  }
+  return {out, partBegin};
+}
+
+// ---- build/probe over partition-major inputs -----------------------------
+py::dict opBuildProbe(const at::Tensor &R, const at::Tensor &S, const at::Tensor &partR, const at::Tensor &partS,
+                      int64_t fragShift, int64_t keyShift, bool wide, bool materialize, int64_t rChunk,
+                      int64_t sChunk, int64_t outCapacity) {
+  setDevice(R);
+  kernels::BPArgs a;
+  a.R = R.data_ptr();
+  a.S = S.data_ptr();
+  at::Tensor pr = partR.to(R.device()).contiguous(), ps = partS.to(R.device()).contiguous();
+  a.partR = ptr<uint64_t>(pr);
+  a.partS = ptr<uint64_t>(ps);
+  a.P = (uint32_t)pr.size(0) - 1;
+  a.rChunk = (uint32_t)rChunk;
+  a.sChunk = (uint32_t)sChunk;
+  a.fragShift = (uint32_t)fragShift;
+  a.keyShift = (uint32_t)keyShift;
+  a.wide = wide;
+  a.materialize = materialize;
+  at::Tensor pairs = at::empty({std::max<int64_t>(outCapacity, 1), 2}, like(R));
+  a.outPairs = reinterpret_cast<ulonglong2 *>(pairs.data_ptr());
+  a.outCapacity = materialize ? (uint64_t)outCapacity : 0;
+  py::dict d;
+  if (R.is_cuda()) {
+    at::Tensor ctr = at::zeros({4}, like(R));
+    a.result = reinterpret_cast<unsigned long long *>(ctr.data_ptr());
+    a.outCursor = a.result + 1;
+    uint32_t *nItems = reinterpret_cast<uint32_t *>(a.result + 2);
+    at::Tensor counts = at::empty({std::max<int64_t>(a.P, 1)}, like(R, at::kInt));
+    at::Tensor offsets = at::empty({std::max<int64_t>(a.P, 1)}, like(R, at::kInt));
+    at::Tensor scanWs = at::empty({(int64_t)kernels::scanWorkspaceBytes(a.P) / 4 + 1}, like(R, at::kInt));
+    uint32_t capacity = 2 * a.P + (uint32_t)(S.size(0) / a.sChunk + R.size(0) / a.rChunk) + 1024;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      at::Tensor items = at::empty({(int64_t)capacity * 2}, like(R));
+      ctr.zero_();
+      kernels::bpPlanCounts(a, ptr<uint32_t>(counts), nullptr);
+      kernels::scanExclusiveU32(ptr<uint32_t>(counts), ptr<uint32_t>(offsets), a.P, nItems, scanWs.data_ptr(), nullptr);
+      kernels::bpEmit(a, ptr<uint32_t>(counts), ptr<uint32_t>(offsets), ptr<kernels::BPItem>(items), capacity, nullptr);
+      kernels::buildProbe(a, ptr<kernels::BPItem>(items), nItems, capacity, nullptr);
+      HIP_CHECK(hipDeviceSynchronize());
+      at::Tensor h = ctr.cpu();
+      const uint32_t need = (uint32_t)(h[2].item<int64_t>() & 0xFFFFFFFF);
+      d["matches"] = (uint64_t)h[0].item<int64_t>();
+      d["output_count"] = (uint64_t)h[1].item<int64_t>();
+      d["work_items"] = need;
+      if (need <= capacity) break;
+      capacity = need;
+    }
+  } else {
+    uint64_t cursor = 0;
+    a.outCursor = reinterpret_cast<unsigned long long *>(&cursor);
+    d["matches"] = host::buildProbe(a);
+    d["output_count"] = cursor;
+    d["work_items"] = a.P;
+  }
+  d["pairs"] = pairs;
+  return d;
+}
+
+at::Tensor opGenerate(int64_t n, int64_t globalOffset, int64_t globalSize, const data::GenSpec &spec,
+                      const std::string &device) {
+  at::Tensor out = at::empty({n, 2}, at::TensorOptions().dtype(at::kLong).device(device));
+  setDevice(out);
+  const uint64_t domain = spec.domain ? spec.domain : (uint64_t)globalSize;
+  kernels::GenParams p;
+  p.dist = spec.distribution;
+  p.globalOffset = globalOffset;
+  p.ridOffset = globalOffset;
+  p.keyOffset = spec.keyOffset;
+  p.domain = domain;
+  p.modulo = domain;
+  p.seed = spec.seed;
+  p.perm = kernels::FeistelPermutation::make(domain, spec.seed);
+  if (spec.distribution == kernels::KeyDistribution::Zipf) p.zipf = host::makeZipf(domain, spec.zipfTheta);
+  if (out.is_cuda()) {
+    kernels::generate(ptr<data::Tuple>(out), n, p, nullptr);
+    HIP_CHECK(hipDeviceSynchronize());
+  } else {
+    host::generate(ptr<data::Tuple>(out), n, p);
+  }
+  return out;
+}
+
+at::Tensor opScan(const at::Tensor &in) {
+  TORCH_CHECK(in.is_cuda() && in.scalar_type() == at::kInt && in.dim() == 1, "scan expects a 1-D int32 HIP tensor");
+  setDevice(in);
+  const uint64_t n = in.size(0);
+  at::Tensor out = at::empty({(int64_t)n + 1}, like(in, at::kInt));
+  at::Tensor ws = at::empty({(int64_t)kernels::scanWorkspaceBytes(n) / 4 + 1}, like(in, at::kInt));
+  kernels::scanExclusiveU32(ptr<uint32_t>(in), ptr<uint32_t>(out), n, ptr<uint32_t>(out) + n, ws.data_ptr(), nullptr);
+  HIP_CHECK(hipDeviceSynchronize());
+  return out;
+}
+
+uint64_t opNpjCount(const at::Tensor &R, const at::Tensor &S) {
+  checkTuples(R, "R");
+  checkTuples(S, "S");
+  setDevice(R);
+  if (!R.is_cuda()) return host::npjJoin(ptr<data::Tuple>(R), R.size(0), ptr<data::Tuple>(S), S.size(0));
+  const uint64_t slots = kernels::npjTableSlots(R.size(0));
+  at::Tensor table = at::empty({(int64_t)slots}, like(R));
+  at::Tensor res = at::zeros({1}, like(R));
+  kernels::npjBuild(ptr<data::Tuple>(R), R.size(0), ptr<unsigned long long>(table), slots, nullptr);
+  kernels::npjProbe(ptr<data::Tuple>(S), S.size(0), ptr<unsigned long long>(table), slots, ptr<unsigned long long>(res),
+                    nullptr);
+  HIP_CHECK(hipDeviceSynchronize());
+  return (uint64_t)res.cpu()[0].item<int64_t>();
+}
+
+at::Tensor opNetScatterGlobalAtomic(const at::Tensor &tuples, int64_t bits, int64_t keyShift,
+                                    const at::Tensor &partBegin) {
+  checkTuples(tuples, "tuples");
+  TORCH_CHECK(tuples.is_cuda(), "global-atomic scatter is a device ablation");
+  setDevice(tuples);
+  at::Tensor cur = partBegin.slice(0, 0, partBegin.size(0) - 1).to(tuples.device()).contiguous().clone();
+  at::Tensor out = at::empty({tuples.size(0)}, like(tuples));
+  kernels::netScatterGlobalAtomic(ptr<data::Tuple>(tuples), tuples.size(0), bits, keyShift, ptr<uint64_t>(cur),
+                                  ptr<uint64_t>(out), nullptr);
+  HIP_CHECK(hipDeviceSynchronize());
+  return out;
+}
+
+// Timed device micro-benchmarks: returns milliseconds per call (median of iters).
+double timeDevice(const std::function<void(hipStream_t)> &fn, int iters) {
+  hipEvent_t a, b;
+  HIP_CHECK(hipEventCreate(&a));
+  HIP_CHECK(hipEventCreate(&b));
+  std::vector<float> ms;
+  fn(nullptr);  // warm
+  for (int i = 0; i < iters; ++i) {
+    HIP_CHECK(hipEventRecord(a, nullptr));
+    fn(nullptr);
+    HIP_CHECK(hipEventRecord(b, nullptr));
+    HIP_CHECK(hipEventSynchronize(b));
+    float m;
+    HIP_CHECK(hipEventElapsedTime(&m, a, b));
+    ms.push_back(m);
+  }
+  HIP_CHECK(hipEventDestroy(a));
+  HIP_CHECK(hipEventDestroy(b));
+  std::sort(ms.begin(), ms.end());
+  return ms[ms.size() / 2];
+}
+
+double benchCopy(const at::Tensor &src, const at::Tensor &dst, int iters) {
+  setDevice(src);
+  const uint64_t n16 = src.numel() * src.element_size() / 16;
+  return timeDevice(
+      [&](hipStream_t s) {
+        kernels::copyKernel(ptr<const ulonglong2>(src), ptr<ulonglong2>(dst), n16, s);
+      },
+      iters);
+}
+
+double benchRead(const at::Tensor &src, int iters) {
+  setDevice(src);
+  const uint64_t n16 = src.numel() * src.element_size() / 16;
+  at::Tensor sink = at::zeros({1}, like(src));
+  return timeDevice(
+      [&](hipStream_t s) { kernels::readKernel(ptr<const ulonglong2>(src), n16, ptr<unsigned long long>(sink), s); },
+      iters);
+}
+
+py::dict resultToDict(const operators::JoinResult &r) {
+  py::dict d;
+  d["local_matches"] = r.localMatches;
+  d["global_matches"] = r.globalMatches;
+  d["output_pairs"] = r.outputPairs;
+  d["output_overflow"] = r.outputOverflow;
+  d["reruns"] = r.reruns;
+  d["join_ms"] = r.joinMs;
+  d["histogram_ms"] = r.histogramMs;
+  d["window_ms"] = r.windowMs;
+  d["network_ms"] = r.networkMs;
+  d["local_ms"] = r.localMs;
+  d["dev_histogram_ms"] = r.devHistogramMs;
+  d["dev_network_ms"] = r.devNetworkMs;
+  d["dev_local_partition_ms"] = r.devLocalPartitionMs;
+  d["dev_build_probe_ms"] = r.devBuildProbeMs;
+  d["inner_received"] = r.innerReceived;
+  d["outer_received"] = r.outerReceived;
+  d["local_items"] = r.localItems;
+  d["build_probe_items"] = r.buildProbeItems;
+  d["inner_local"] = r.innerLocal;
+  d["outer_local"] = r.outerLocal;
+  return d;
+}
+
+// Relation wrapper that can keep a torch tensor alive for views.
+struct PyRelation {
+  std::shared_ptr<data::Relation> rel;
+  py::object keepAlive;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "MI355X-native distributed radix hash join engine (native core)";
+  m.attr("ARCH") = "gfx950";
+
+  m.def("device_count", []() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+  });
+
+  py::enum_<kernels::KeyDistribution>(m, "KeyDistribution")
+      .value("UNIQUE", kernels::KeyDistribution::Unique)
+      .value("MODULO", kernels::KeyDistribution::Modulo)
+      .value("UNIFORM", kernels::KeyDistribution::Uniform)
+      .value("ZIPF", kernels::KeyDistribution::Zipf)
+      .value("DENSE", kernels::KeyDistribution::Dense);
+  py::enum_<core::AssignmentPolicy>(m, "AssignmentPolicy")
+      .value("ROUND_ROBIN", core::AssignmentPolicy::RoundRobin)
+      .value("LPT", core::AssignmentPolicy::LPT);
+  py::enum_<core::TupleFormat>(m, "TupleFormat")
+      .value("COMPRESSED", core::TupleFormat::Compressed)
+      .value("WIDE", core::TupleFormat::Wide);
+
+  py::class_<core::JoinConfig>(m, "JoinConfig")
+      .def(py::init<>())
+      .def_readwrite("network_bits", &core::JoinConfig::networkBits)
+      .def_readwrite("local_bits", &core::JoinConfig::localBits)
+      .def_readwrite("two_level", &core::JoinConfig::twoLevel)
+      .def_readwrite("key_shift", &core::JoinConfig::keyShift)
+      .def_readwrite("assignment", &core::JoinConfig::assignment)
+      .def_readwrite("format", &core::JoinConfig::format)
+      .def_readwrite("materialize", &core::JoinConfig::materialize)
+      .def_readwrite("output_capacity", &core::JoinConfig::outputCapacity)
+      .def_readwrite("build_target", &core::JoinConfig::buildTarget)
+      .def_readwrite("r_chunk", &core::JoinConfig::rChunk)
+      .def_readwrite("s_chunk", &core::JoinConfig::sChunk)
+      .def_readwrite("chunks", &core::JoinConfig::chunks)
+      .def_readwrite("checks", &core::JoinConfig::checks)
+      .def_readwrite("max_partition_blocks", &core::JoinConfig::maxPartitionBlocks)
+      .def("__repr__", &core::JoinConfig::describe);
+
+  py::class_<core::JoinPlan>(m, "JoinPlan")
+      .def_readonly("number_of_nodes", &core::JoinPlan::numberOfNodes)
+      .def_readonly("network_bits", &core::JoinPlan::networkBits)
+      .def_readonly("local_bits", &core::JoinPlan::localBits)
+      .def_readonly("key_shift", &core::JoinPlan::keyShift)
+      .def_readonly("frag_shift", &core::JoinPlan::fragShift)
+      .def_readonly("r_chunk", &core::JoinPlan::rChunk)
+      .def_readonly("s_chunk", &core::JoinPlan::sChunk)
+      .def_readonly("chunks", &core::JoinPlan::chunks)
+      .def_readonly("two_level", &core::JoinPlan::twoLevel)
+      .def_readonly("wide", &core::JoinPlan::wide)
+      .def_readonly("materialize", &core::JoinPlan::materialize)
+      .def("__repr__", &core::JoinPlan::describe);
+  m.def("make_plan", &core::makePlan, py::arg("config"), py::arg("number_of_nodes"), py::arg("global_inner"),
+        py::arg("global_outer"), py::arg("max_key"), py::arg("max_rid"));
+
+  py::class_<comm::Communicator, std::shared_ptr<comm::Communicator>>(m, "Communicator")
+      .def("rank", &comm::Communicator::rank)
+      .def("size", &comm::Communicator::size)
+      .def("name", &comm::Communicator::name)
+      .def("barrier", &comm::Communicator::barrier, py::call_guard<py::gil_scoped_release>())
+      .def("all_gather", [](comm::Communicator &c, std::vector<uint64_t> v) {
+        std::vector<uint64_t> out(v.size() * c.size());
+        {
+          py::gil_scoped_release nogil;
+          c.allGatherHost(v.data(), out.data(), v.size());
+        }
+        return out;
+      })
+      .def("all_reduce_sum", [](comm::Communicator &c, std::vector<uint64_t> v) {
+        {
+          py::gil_scoped_release nogil;
+          c.allReduceSumHost(v.data(), v.size());
+        }
+        return v;
+      });
+  py::class_<comm::LocalCommunicator, comm::Communicator, std::shared_ptr<comm::LocalCommunicator>>(
+      m, "LocalCommunicator")
+      .def(py::init<>());
+  py::class_<comm::RcclCommunicator, comm::Communicator, std::shared_ptr<comm::RcclCommunicator>>(m,
+                                                                                                   "RcclCommunicator")
+      .def(py::init([](py::bytes id, uint32_t rank, uint32_t size, int device) {
+             std::string s = id;
+             std::vector<uint8_t> v(s.begin(), s.end());
+             py::gil_scoped_release nogil;
+             return std::make_shared<comm::RcclCommunicator>(v, rank, size, device);
+           }),
+           py::arg("unique_id"), py::arg("rank"), py::arg("size"), py::arg("device"));
+  m.def("rccl_unique_id", []() {
+    auto v = comm::RcclCommunicator::uniqueId();
+    return py::bytes(reinterpret_cast<const char *>(v.data()), v.size());
+  });
+  py::class_<comm::ProcessGroupCommunicator, comm::Communicator, std::shared_ptr<comm::ProcessGroupCommunicator>>(
+      m, "ProcessGroupCommunicator")
+      .def(py::init<c10::intrusive_ptr<c10d::ProcessGroup>>(), py::arg("process_group"));
+  m.def("set_world", [](std::shared_ptr<comm::Communicator> c) {
+    static std::shared_ptr<comm::Communicator> keep;
+    keep = c;
+    comm::setWorld(c.get());
+  });
+
+  py::class_<core::ExecContext, std::shared_ptr<core::ExecContext>>(m, "ExecContext")
+      .def(py::init([](const std::string &loc, int device, std::shared_ptr<comm::Communicator> c) {
+             auto ctx = std::shared_ptr<core::ExecContext>(
+                 new core::ExecContext(loc == "device" ? Location::Device : Location::Host, device, c.get()),
+                 [c](core::ExecContext *p) { delete p; });
+             return ctx;
+           }),
+           py::arg("location"), py::arg("device"), py::arg("communicator"))
+      .def_property_readonly("on_device", &core::ExecContext::onDevice)
+      .def_property_readonly("device", &core::ExecContext::device)
+      .def_property_readonly("node_id", &core::ExecContext::nodeId)
+      .def_property_readonly("number_of_nodes", &core::ExecContext::numberOfNodes)
+      .def("workspace_capacity", [](core::ExecContext &c) { return c.workspace().capacity(); })
+      .def("workspace_peak", [](core::ExecContext &c) { return c.workspace().peak(); })
+      .def("reserve_workspace", [](core::ExecContext &c, uint64_t b) { c.workspace().reserve(b); })
+      .def("synchronize", &core::ExecContext::synchronize);
+
+  py::class_<data::GenSpec>(m, "GenSpec")
+      .def(py::init<>())
+      .def(py::init([](kernels::KeyDistribution d, uint64_t seed, uint64_t domain, uint64_t keyOffset, double theta) {
+             data::GenSpec s;
+             s.distribution = d;
+             s.seed = seed;
+             s.domain = domain;
+             s.keyOffset = keyOffset;
+             s.zipfTheta = theta;
+             return s;
+           }),
+           py::arg("distribution") = kernels::KeyDistribution::Unique, py::arg("seed") = 1234, py::arg("domain") = 0,
+           py::arg("key_offset") = 0, py::arg("zipf_theta") = 0.75)
+      .def_readwrite("distribution", &data::GenSpec::distribution)
+      .def_readwrite("seed", &data::GenSpec::seed)
+      .def_readwrite("domain", &data::GenSpec::domain)
+      .def_readwrite("key_offset", &data::GenSpec::keyOffset)
+      .def_readwrite("zipf_theta", &data::GenSpec::zipfTheta);
+
+  py::class_<PyRelation>(m, "Relation")
+      .def(py::init([](uint64_t localSize, uint64_t globalSize, const std::string &loc, int device) {
+             PyRelation r;
+             r.rel = std::make_shared<data::Relation>(localSize, globalSize,
+                                                      loc == "device" ? Location::Device : Location::Host, device);
+             return r;
+           }),
+           py::arg("local_size"), py::arg("global_size"), py::arg("location") = "device", py::arg("device") = 0)
+      .def_static(
+          "from_tensor",
+          [](at::Tensor t, uint64_t globalSize) {
+            checkTuples(t, "tuples");
+            if (t.is_cuda()) HIP_CHECK(hipDeviceSynchronize());
+            PyRelation r;
+            r.rel = std::make_shared<data::Relation>(ptr<data::Tuple>(t), t.size(0), globalSize, locOf(t),
+                                                     t.is_cuda() ? t.get_device() : 0);
+            r.keepAlive = py::cast(t);
+            return r;
+          },
+          py::arg("tuples"), py::arg("global_size"))
+      .def("local_size", [](PyRelation &r) { return r.rel->getLocalSize(); })
+      .def("global_size", [](PyRelation &r) { return r.rel->getGlobalSize(); })
+      .def("location", [](PyRelation &r) { return std::string(locationName(r.rel->location())); })
+      .def("fill_unique_values", [](PyRelation &r, uint64_t k, uint64_t rid) { r.rel->fillUniqueValues(k, rid); })
+      .def("fill_modulo_values",
+           [](PyRelation &r, uint64_t k, uint64_t rid, uint64_t inner) { r.rel->fillModuloValues(k, rid, inner); })
+      .def("generate", [](PyRelation &r, const data::GenSpec &s, uint64_t off) { r.rel->generate(s, off); },
+           py::arg("spec"), py::arg("global_offset"))
+      .def("distribute",
+           [](PyRelation &r, uint32_t node, uint32_t n, std::shared_ptr<comm::Communicator> c) {
+             py::gil_scoped_release nogil;
+             r.rel->distribute(node, n, c.get());
+           })
+      .def("to_tensor",
+           [](PyRelation &r) {
+             const auto &rel = r.rel;
+             auto opts = at::TensorOptions().dtype(at::kLong);
+             if (rel->location() == Location::Device) opts = opts.device(at::kCUDA, rel->device());
+             at::Tensor out = at::empty({(int64_t)rel->getLocalSize(), 2}, opts);
+             if (rel->location() == Location::Device)
+               HIP_CHECK(hipMemcpy(out.data_ptr(), rel->getData(), rel->getLocalSize() * 16, hipMemcpyDeviceToDevice));
+             else
+               std::memcpy(out.data_ptr(), rel->getData(), rel->getLocalSize() * 16);
+             return out;
+           })
+      .def_static("local_size_for", &data::Relation::localSizeFor)
+      .def_static("local_offset_for", &data::Relation::localOffsetFor)
+      .def_static("expected_matches", [](const data::GenSpec &i, uint64_t gi, const data::GenSpec &o, uint64_t go) {
+        uint64_t v = data::Relation::expectedMatches(i, gi, o, go);
+        return v == UINT64_MAX ? py::object(py::none()) : py::object(py::int_(v));
+      });
+
+  py::class_<operators::HashJoin, std::shared_ptr<operators::HashJoin>>(m, "HashJoin")
+      .def(py::init([](PyRelation &inner, PyRelation &outer, std::shared_ptr<core::ExecContext> ctx,
+                       const core::JoinConfig &cfg) {
+             py::gil_scoped_release nogil;
+             return std::make_shared<operators::HashJoin>(inner.rel.get(), outer.rel.get(), ctx.get(), cfg);
+           }),
+           py::arg("inner"), py::arg("outer"), py::arg("context"), py::arg("config") = core::JoinConfig(),
+           py::keep_alive<1, 2>(), py::keep_alive<1, 3>(), py::keep_alive<1, 4>())
+      .def("run",
+           [](operators::HashJoin &j) {
+             operators::JoinResult r;
+             {
+               py::gil_scoped_release nogil;
+               r = j.run();
+             }
+             return resultToDict(r);
+           })
+      .def("join", [](operators::HashJoin &j) {
+        py::gil_scoped_release nogil;
+        j.join();
+      })
+      .def_property_readonly("plan", &operators::HashJoin::getPlan)
+      .def("output", [](operators::HashJoin &j) {
+        const auto &r = j.lastResult();
+        const uint64_t n = std::min<uint64_t>(r.outputPairs, r.outputPairs);
+        at::Tensor out = at::empty({(int64_t)n, 2}, at::kLong);
+        if (n && j.getOutput()) {
+          hipPointerAttribute_t attr;
+          bool dev = hipPointerGetAttributes(&attr, j.getOutput()) == hipSuccess && attr.type == hipMemoryTypeDevice;
+          if (dev)
+            HIP_CHECK(hipMemcpy(out.data_ptr(), j.getOutput(), n * 16, hipMemcpyDeviceToHost));
+          else
+            std::memcpy(out.data_ptr(), j.getOutput(), n * 16);
+        }
+        (void)hipGetLastError();
+        return out;
+      });
+  m.def("result_counter", []() { return operators::HashJoin::RESULT_COUNTER; });
+
+  auto meas = m.def_submodule("measurements");
+  meas.def("init", &performance::Measurements::init, py::arg("node_id"), py::arg("number_of_nodes"),
+           py::arg("tag") = "experiment", py::arg("directory") = "");
+  meas.def("write_meta", [](const std::string &k, const std::string &v) {
+    performance::Measurements::writeMetaData(k.c_str(), v.c_str());
+  });
+  meas.def("print_measurements", [](std::shared_ptr<comm::Communicator> c) {
+    py::gil_scoped_release nogil;
+    performance::Measurements::printMeasurements(c.get());
+  });
+  meas.def("store_all", &performance::Measurements::storeAllMeasurements);
+  meas.def("snapshot", &performance::Measurements::snapshot);
+  meas.def("serialize", &performance::Measurements::serializeResults);
+
+  auto ops = m.def_submodule("ops", "kernel-level entry points on torch tensors (device or host)");
+  ops.def("net_histogram", &opNetHistogram, py::arg("tuples"), py::arg("bits"), py::arg("max_blocks") = 2048);
+  ops.def("net_partition", &opNetPartition, py::arg("tuples"), py::arg("bits"), py::arg("key_shift") = 32,
+          py::arg("wide") = false, py::arg("max_blocks") = 2048);
+  ops.def("local_partition", &opLocalPartition, py::arg("values"), py::arg("part_begin"), py::arg("shift"),
+          py::arg("bits"), py::arg("wide") = false);
+  ops.def("build_probe", &opBuildProbe, py::arg("R"), py::arg("S"), py::arg("part_r"), py::arg("part_s"),
+          py::arg("frag_shift"), py::arg("key_shift"), py::arg("wide") = false, py::arg("materialize") = false,
+          py::arg("r_chunk") = 4096, py::arg("s_chunk") = 65536, py::arg("out_capacity") = 0);
+  ops.def("generate", &opGenerate, py::arg("n"), py::arg("global_offset"), py::arg("global_size"), py::arg("spec"),
+          py::arg("device") = "cpu");
+  ops.def("scan_u32", &opScan);
+  ops.def("npj_count", &opNpjCount);
+  ops.def("net_scatter_global_atomic", &opNetScatterGlobalAtomic);
+  ops.def("bench_copy_ms", &benchCopy, py::arg("src"), py::arg("dst"), py::arg("iters") = 10);
+  ops.def("bench_read_ms", &benchRead, py::arg("src"), py::arg("iters") = 10);
+  ops.def("partition_tile", []() { return kernels::PART_TILE; });
+}

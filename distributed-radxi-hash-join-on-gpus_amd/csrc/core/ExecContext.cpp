@@ -1,0 +1,60 @@
+#include "ExecContext.h"
+
+#include <cstring>
+
+#include "../comm/Communicator.h"
+#include "../memory/Arena.h"
+#include "../utils/Hip.h"
+
+namespace hpcjoin {
+namespace core {
+
+ExecContext::ExecContext(Location loc, int device, comm::Communicator *comm)
+    : loc_(loc), device_(device < 0 ? 0 : device), comm_(comm) {
+  JOIN_ASSERT(comm_ != nullptr, "ExecContext", "a communicator is required");
+  JOIN_ASSERT(comm_->size() == 1 || comm_->supports(loc), "ExecContext", "communicator %s cannot move %s buffers",
+              comm_->name().c_str(), locationName(loc));
+  utils::setDebugRank((int)comm_->rank());
+  workspace_.reset(new memory::Arena(loc, device_));
+  staging_.reset(new memory::Arena(Location::Host, device_));
+  if (onDevice()) {
+    HIP_CHECK(hipSetDevice(device_));
+    HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    HIP_CHECK(hipStreamCreateWithFlags(&commStream_, hipStreamNonBlocking));
+  }
+}
+
+ExecContext::~ExecContext() {
+  workspace_.reset();
+  staging_.reset();
+  if (stream_) (void)hipStreamDestroy(stream_);
+  if (commStream_) (void)hipStreamDestroy(commStream_);
+}
+
+uint32_t ExecContext::nodeId() const { return comm_->rank(); }
+uint32_t ExecContext::numberOfNodes() const { return comm_->size(); }
+
+void ExecContext::synchronize() const {
+  if (!onDevice()) return;
+  HIP_CHECK(hipStreamSynchronize(commStream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+void ExecContext::copy(void *dst, const void *src, uint64_t bytes, bool toDevice, bool fromDevice) const {
+  if (bytes == 0) return;
+  if (!onDevice()) {
+    std::memcpy(dst, src, bytes);
+    return;
+  }
+  hipMemcpyKind k = toDevice ? (fromDevice ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice)
+                             : (fromDevice ? hipMemcpyDeviceToHost : hipMemcpyHostToHost);
+  HIP_CHECK(hipMemcpyAsync(dst, src, bytes, k, stream_));
+}
+
+void ExecContext::resetScratch() {
+  workspace_->reset();
+  staging_->reset();
+}
+
+}  // namespace core
+}  // namespace hpcjoin

@@ -1,0 +1,57 @@
+// Per-engine execution state shared by the tasks of one HashJoin: where the
+// data lives, the HIP streams, the communicator and the workspace arenas.
+// The reference has none of this (everything is a static or an MPI global).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <memory>
+
+#include "JoinConfig.h"
+#include "Types.h"
+
+namespace hpcjoin {
+namespace comm {
+class Communicator;
+}
+namespace memory {
+class Arena;
+}
+
+namespace core {
+
+class ExecContext {
+ public:
+  // device < 0 selects the host reference path.
+  ExecContext(Location loc, int device, comm::Communicator *comm);
+  ~ExecContext();
+  ExecContext(const ExecContext &) = delete;
+  ExecContext &operator=(const ExecContext &) = delete;
+
+  Location location() const { return loc_; }
+  bool onDevice() const { return loc_ == Location::Device; }
+  int device() const { return device_; }
+  hipStream_t stream() const { return stream_; }          // compute stream
+  hipStream_t commStream() const { return commStream_; }  // exchange stream (overlaps compute)
+  comm::Communicator *comm() const { return comm_; }
+  uint32_t nodeId() const;
+  uint32_t numberOfNodes() const;
+  memory::Arena &workspace() { return *workspace_; }  // data-side scratch (HBM or host), reset per join
+  memory::Arena &staging() { return *staging_; }      // pinned host scratch for plans/results, reset per join
+
+  void synchronize() const;                 // compute + comm streams
+  void copy(void *dst, const void *src, uint64_t bytes, bool toDevice, bool fromDevice) const;  // async on stream()
+  void resetScratch();
+
+ private:
+  Location loc_;
+  int device_;
+  comm::Communicator *comm_;
+  hipStream_t stream_ = nullptr;
+  hipStream_t commStream_ = nullptr;
+  std::unique_ptr<memory::Arena> workspace_;
+  std::unique_ptr<memory::Arena> staging_;
+};
+
+}  // namespace core
+}  // namespace hpcjoin

@@ -1,0 +1,95 @@
+#include "JoinConfig.h"
+
+#include <algorithm>
+
+#include "../utils/Debug.h"
+
+namespace hpcjoin {
+namespace core {
+
+std::string JoinConfig::describe() const {
+  return utils::format("JoinConfig(networkBits=%u localBits=%u twoLevel=%d keyShift=%u assignment=%s format=%s "
+                       "materialize=%d buildTarget=%lu rChunk=%u sChunk=%u chunks=%u)",
+                       networkBits, localBits, (int)twoLevel, keyShift,
+                       assignment == AssignmentPolicy::LPT ? "lpt" : "round_robin",
+                       format == TupleFormat::Wide ? "wide" : "compressed", (int)materialize,
+                       (unsigned long)buildTarget, rChunk, sChunk, chunks);
+}
+
+std::string JoinPlan::describe() const {
+  return utils::format("JoinPlan(nodes=%u networkBits=%u localBits=%u twoLevel=%d keyShift=%u fragShift=%u "
+                       "rChunk=%u sChunk=%u chunks=%u wide=%d materialize=%d assignment=%s)",
+                       numberOfNodes, networkBits, localBits, (int)twoLevel, keyShift, fragShift, rChunk, sChunk,
+                       chunks, (int)wide, (int)materialize,
+                       assignment == AssignmentPolicy::LPT ? "lpt" : "round_robin");
+}
+
+JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t globalInner, uint64_t globalOuter,
+                  uint64_t maxKey, uint64_t maxRid) {
+  JoinPlan p;
+  p.numberOfNodes = numberOfNodes;
+  p.twoLevel = cfg.twoLevel;
+  p.wide = cfg.format == TupleFormat::Wide;
+  p.materialize = cfg.materialize;
+  p.assignment = cfg.assignment;
+  p.chunks = std::max<uint32_t>(1, cfg.chunks);
+  p.sChunk = std::max<uint32_t>(1024, cfg.sChunk);
+
+  const uint32_t maxBits = Configuration::GPU_MAX_FANOUT_BITS - 1;  // 1024-way per pass
+  const uint64_t target = std::max<uint64_t>(256, cfg.buildTarget);
+  const uint32_t totalBits = ceilLog2(ceilDiv(std::max<uint64_t>(globalInner, 1), target));
+  // >= 8 network partitions per node so LPT has room to balance.
+  const uint32_t minNet = std::max<uint32_t>(4, ceilLog2(numberOfNodes) + 3);
+
+  if (cfg.networkBits) {
+    p.networkBits = cfg.networkBits;
+  } else if (p.twoLevel) {
+    p.networkBits = std::min(maxBits, std::max(minNet, (totalBits + 1) / 2));
+  } else {
+    p.networkBits = std::min(maxBits, std::max(minNet, totalBits));
+  }
+  if (!p.twoLevel) {
+    p.localBits = 0;
+  } else if (cfg.localBits) {
+    p.localBits = cfg.localBits;
+  } else {
+    p.localBits = totalBits > p.networkBits ? std::min(maxBits, totalBits - p.networkBits) : 1;
+  }
+  JOIN_ASSERT(p.networkBits >= 1 && p.networkBits <= Configuration::GPU_MAX_FANOUT_BITS, "Plan",
+              "networkBits=%u out of range", p.networkBits);
+  JOIN_ASSERT(p.localBits <= Configuration::GPU_MAX_FANOUT_BITS, "Plan", "localBits=%u out of range", p.localBits);
+
+  const uint32_t ridBits = ceilLog2(maxRid + 1);
+  const uint32_t keyBits = ceilLog2(maxKey + 1);
+  if (p.wide) {
+    p.keyShift = 64;
+    p.fragShift = 64;
+    JOIN_ASSERT(maxKey != ~0ull, "Plan", "wide format reserves key 0xFFFFFFFFFFFFFFFF as the empty slot");
+  } else {
+    p.keyShift = cfg.keyShift ? cfg.keyShift : std::max<uint32_t>(32, ridBits);
+    JOIN_ASSERT(ridBits <= p.keyShift, "Plan", "rids need %u bits but keyShift=%u", ridBits, p.keyShift);
+    const uint32_t keyHighBits = keyBits > p.networkBits ? keyBits - p.networkBits : 0;
+    JOIN_ASSERT(keyHighBits <= 64 - p.keyShift, "Plan",
+                "keys need %u bits: %u above the %u network bits do not fit the %u bits of a CompressedTuple above "
+                "keyShift=%u; use TupleFormat::Wide",
+                keyBits, keyHighBits, p.networkBits, 64 - p.keyShift, p.keyShift);
+    p.fragShift = p.keyShift + (p.twoLevel ? p.localBits : 0);
+    // The LDS table uses 0xFFFFFFFF as its empty marker: fragments must stay below it.
+    JOIN_ASSERT(keyHighBits <= 31 + (p.twoLevel ? p.localBits : 0), "Plan",
+                "key fragment (%u bits) would reach the LDS empty marker 0xFFFFFFFF", keyHighBits);
+  }
+
+  // LDS budget: a 32 KiB table (counting, 4-byte fragments) lets 5 workgroups
+  // (20 wave64s) share a CU; 8- and 16-byte entries get 64 KiB (2 per CU).
+  if (cfg.rChunk) {
+    p.rChunk = cfg.rChunk;
+  } else {
+    const uint32_t entry = p.wide ? (p.materialize ? 16 : 8) : (p.materialize ? 8 : 4);
+    const uint32_t budget = entry == 4 ? 32 * 1024 : 64 * 1024;
+    p.rChunk = (budget / entry) / 2;
+  }
+  return p;
+}
+
+}  // namespace core
+}  // namespace hpcjoin

@@ -1,0 +1,68 @@
+// Runtime configuration of one join (the reference is compile-time only:
+// core/Configuration.h + CMake -D macros, SURVEY §5 "Config / flag system").
+// JoinPlan is what the engine actually runs with once sizes are known.
+#pragma once
+
+#include <cstdint>
+#include <string>
+
+#include "Configuration.h"
+#include "Types.h"
+
+namespace hpcjoin {
+namespace core {
+
+enum class AssignmentPolicy : int {
+  RoundRobin = 0,  // partition p -> node p % N (reference AssignmentMap.cpp:41-43)
+  LPT = 1,         // longest-processing-time greedy on |R_p| + |S_p| (skew-aware)
+};
+
+enum class TupleFormat : int {
+  Compressed = 0,  // 8-byte CompressedTuple after the network pass (reference format)
+  Wide = 1,        // 16-byte Tuple end to end: full 64-bit keys (the RCD / AoS path)
+};
+
+struct JoinConfig {
+  uint32_t networkBits = 0;   // radix bits of the network pass (0 = auto)
+  uint32_t localBits = 0;     // radix bits of the local pass (0 = auto; ignored if !twoLevel)
+  bool twoLevel = true;       // run the local (second) partitioning pass
+  uint32_t keyShift = 0;      // CompressedTuple key position (0 = auto: max(32, rid bits))
+  AssignmentPolicy assignment = AssignmentPolicy::LPT;
+  TupleFormat format = TupleFormat::Compressed;
+  bool materialize = false;   // also write (rid_inner, rid_outer) pairs
+  uint64_t outputCapacity = 0;  // materialize: pair capacity (0 = auto from oracle bound)
+  uint64_t buildTarget = 3072;  // target inner tuples per final partition
+  uint32_t rChunk = 0;          // max inner tuples per LDS table (0 = auto from LDS budget)
+  uint32_t sChunk = 65536;      // max outer tuples per build/probe work item
+  uint32_t chunks = 1;          // exchange pipeline slices per relation (>1: scatter(k+1) || all-to-all(k))
+  bool checks = true;           // cheap always-on invariants (all tuples written, sizes)
+  uint32_t maxPartitionBlocks = 2048;  // network-pass grid cap (~8 WGs per CU)
+
+  std::string describe() const;
+};
+
+// Fully resolved plan for a given pair of relations.
+struct JoinPlan {
+  uint32_t numberOfNodes = 1;
+  uint32_t networkBits = 5;
+  uint32_t localBits = 0;
+  uint32_t keyShift = 32;
+  uint32_t fragShift = 32;    // compressed: key fragment shift after both passes
+  uint32_t rChunk = 4096;
+  uint32_t sChunk = 65536;
+  uint32_t chunks = 1;
+  bool twoLevel = true;
+  bool wide = false;
+  bool materialize = false;
+  AssignmentPolicy assignment = AssignmentPolicy::LPT;
+  uint64_t networkPartitions() const { return uint64_t(1) << networkBits; }
+  uint64_t localPartitions() const { return twoLevel ? (uint64_t(1) << localBits) : 1; }
+  std::string describe() const;
+};
+
+// maxKey / maxRid: upper bounds over both relations (all ranks).
+JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t globalInner, uint64_t globalOuter,
+                  uint64_t maxKey, uint64_t maxRid);
+
+}  // namespace core
+}  // namespace hpcjoin

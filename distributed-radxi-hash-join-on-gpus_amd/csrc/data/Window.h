@@ -1,0 +1,78 @@
+// Receive window of one relation.  Reference: /root/reference/data/Window.cpp
+// (MPI_Win over MPI_Alloc_mem, lock_all / Put / flush_local / unlock_all).
+//
+// On MI355X the window is an HBM buffer carved from the engine arena, sized
+// exactly from the exchange plan, and filled by stream-ordered RCCL
+// all-to-allv chunks on the exchange stream.  start()/stop()/flush() keep
+// the reference's epoch API: stop() makes the compute stream wait for every
+// exchange of this window (the MPI_Win_unlock_all + MPI_Barrier analog),
+// without a host round trip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "../core/ExecContext.h"
+#include "../histograms/AssignmentMap.h"
+#include "../histograms/ExchangePlan.h"
+#include "../histograms/GlobalHistogram.h"
+#include "CompressedTuple.h"
+#include "Tuple.h"
+
+namespace hpcjoin {
+namespace data {
+
+class Window {
+ public:
+  Window(const histograms::ExchangePlan &plan, histograms::GlobalHistogram *globalHistogram,
+         histograms::AssignmentMap *assignment, core::ExecContext *ctx, bool wide);
+  ~Window();
+  Window(const Window &) = delete;
+  Window &operator=(const Window &) = delete;
+
+  void start();
+  void stop();
+  void flush();
+  // Enqueue the all-to-allv of one chunk once the compute stream reaches this
+  // point (the chunk's scatter kernel is already enqueued on it).
+  void exchange(const void *sendBuffer, uint32_t chunk);
+
+  CompressedTuple *getPartition(uint32_t partitionId);  // partition-major (after local partitioning)
+  Tuple *getWidePartition(uint32_t partitionId);
+  uint64_t getPartitionSize(uint32_t partitionId);
+  uint64_t computeLocalWindowSize();
+  uint64_t computeWindowSize(uint32_t nodeId);
+  void assertAllTuplesWritten();
+
+  void *getData() { return data; }
+  uint32_t tupleBytes() const { return wide ? 16 : 8; }
+  bool isWide() const { return wide; }
+  const histograms::ExchangePlan &getPlan() const { return plan; }
+  // Local partitioning hands back its partition-major output.
+  void setPartitioned(void *partitioned, const uint64_t *partBegin, uint32_t localBits);
+  void *getPartitionedData() const { return partitioned; }
+  const uint64_t *getPartitionBegin() const { return partBegin; }  // [owned * 2^localBits + 1] (ctx location)
+  uint32_t getLocalBits() const { return localBits; }
+
+ protected:
+  uint64_t localWindowSize;
+  void *data;
+
+ private:
+  const histograms::ExchangePlan &plan;
+  histograms::GlobalHistogram *globalHistogram;
+  histograms::AssignmentMap *assignment;
+  core::ExecContext *ctx;
+  bool wide;
+  bool open = false;
+  std::vector<hipEvent_t> ready, done;
+  std::vector<bool> exchanged;
+  void *partitioned = nullptr;
+  const uint64_t *partBegin = nullptr;
+  uint32_t localBits = 0;
+};
+
+}  // namespace data
+}  // namespace hpcjoin

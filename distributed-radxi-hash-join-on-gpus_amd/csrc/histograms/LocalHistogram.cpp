@@ -1,0 +1,65 @@
+#include "LocalHistogram.h"
+
+#include <algorithm>
+
+#include "../comm/World.h"
+#include "../core/Configuration.h"
+#include "../host/HostOps.h"
+#include "../memory/Arena.h"
+#include "../utils/Hip.h"
+
+namespace hpcjoin {
+namespace histograms {
+
+LocalHistogram::LocalHistogram(data::Relation *relation)
+    : relation(relation), ctx(nullptr), bits((uint32_t)core::Configuration::NETWORK_PARTITIONING_FANOUT), chunks(1) {
+  ownedComm.reset(new comm::LocalCommunicator());
+  ownedCtx.reset(new core::ExecContext(relation->location(), relation->device(), ownedComm.get()));
+  ctx = ownedCtx.get();
+  geom = kernels::partitionGeometry(relation->getLocalSize());
+  bpc = geom.blocks;
+}
+
+LocalHistogram::LocalHistogram(data::Relation *relation, core::ExecContext *ctx, uint32_t bits, uint32_t chunks,
+                               uint32_t maxBlocks)
+    : relation(relation), ctx(ctx), bits(bits), chunks(std::max<uint32_t>(1, chunks)) {
+  geom = kernels::partitionGeometry(relation->getLocalSize(), std::max<uint32_t>(maxBlocks, this->chunks));
+  if (this->chunks > geom.blocks) this->chunks = geom.blocks;
+  bpc = (uint32_t)ceilDiv(geom.blocks, this->chunks);
+  this->chunks = (uint32_t)ceilDiv(geom.blocks, bpc);
+}
+
+LocalHistogram::~LocalHistogram() {}
+
+void LocalHistogram::computeLocalHistogram() {
+  const uint32_t F = 1u << bits;
+  values.assign(F, 0);
+  chunkValues.assign((size_t)chunks * F, 0);
+  summed = false;
+  blockHist = ctx->workspace().getArray<uint32_t>((uint64_t)F * geom.blocks);
+  if (ctx->onDevice()) {
+    totalsDev = ctx->workspace().getArray<uint64_t>((uint64_t)chunks * F);
+    kernels::netHistogram(relation->getData(), relation->getLocalSize(), bits, geom, blockHist, ctx->stream());
+    kernels::digitTotals(blockHist, F, geom.blocks, bpc, chunks, totalsDev, ctx->stream());
+    ctx->copy(chunkValues.data(), totalsDev, chunkValues.size() * 8, false, true);
+  } else {
+    host::netHistogram(relation->getData(), relation->getLocalSize(), bits, geom, blockHist);
+    host::digitTotals(blockHist, F, geom.blocks, bpc, chunks, chunkValues.data());
+  }
+}
+
+uint64_t *LocalHistogram::getChunkHistograms() { return chunkValues.data(); }
+
+uint64_t *LocalHistogram::getLocalHistogram() {
+  if (!summed) {
+    const uint32_t F = 1u << bits;
+    values.assign(F, 0);
+    for (uint32_t c = 0; c < chunks; ++c)
+      for (uint32_t d = 0; d < F && !chunkValues.empty(); ++d) values[d] += chunkValues[(size_t)c * F + d];
+    summed = true;
+  }
+  return values.data();
+}
+
+}  // namespace histograms
+}  // namespace hpcjoin

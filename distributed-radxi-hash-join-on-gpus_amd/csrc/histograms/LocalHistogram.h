@@ -1,0 +1,55 @@
+// Per-rank radix histogram of the network partition bits.  Reference:
+// /root/reference/histograms/LocalHistogram.cpp:35-53 (a host loop over key & 31).
+// On MI355X it is the netHistogram kernel (LDS wave-private histograms,
+// digit-major per-workgroup output) followed by a per-digit reduction; the
+// per-workgroup histogram stays in HBM and is reused by NetworkPartitioning
+// to derive every workgroup's scatter cursors.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "../core/ExecContext.h"
+#include "../data/Relation.h"
+#include "../kernels/kernels.h"
+
+namespace hpcjoin {
+namespace histograms {
+
+class LocalHistogram {
+ public:
+  explicit LocalHistogram(data::Relation *relation);  // reference: host, Configuration fan-out, 1 chunk
+  LocalHistogram(data::Relation *relation, core::ExecContext *ctx, uint32_t bits, uint32_t chunks,
+                 uint32_t maxBlocks = 2048);
+  ~LocalHistogram();
+
+  void computeLocalHistogram();  // device: enqueued; host values valid after ctx->synchronize()
+  uint64_t *getLocalHistogram();  // [F], summed over chunks
+  uint64_t *getChunkHistograms();  // [chunks][F]
+
+  uint32_t getPartitionBits() const { return bits; }
+  uint32_t getPartitionCount() const { return 1u << bits; }
+  uint32_t getChunkCount() const { return chunks; }
+  uint32_t blocksPerChunk() const { return bpc; }
+  const kernels::PartitionGeometry &geometry() const { return geom; }
+  const uint32_t *blockHistogram() const { return blockHist; }  // [F][blocks] (ctx location)
+  data::Relation *getRelation() const { return relation; }
+
+ protected:
+  data::Relation *relation;
+  std::vector<uint64_t> values;   // [F]
+  std::vector<uint64_t> chunkValues;  // [chunks][F]
+
+ private:
+  core::ExecContext *ctx;
+  std::unique_ptr<core::ExecContext> ownedCtx;
+  std::unique_ptr<comm::Communicator> ownedComm;
+  uint32_t bits, chunks, bpc;
+  kernels::PartitionGeometry geom;
+  uint32_t *blockHist = nullptr;
+  uint64_t *totalsDev = nullptr;
+  bool summed = false;
+};
+
+}  // namespace histograms
+}  // namespace hpcjoin

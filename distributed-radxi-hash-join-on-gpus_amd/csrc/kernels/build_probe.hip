@@ -1,0 +1,260 @@
+// LDS hash build/probe over (partition, R-chunk, S-chunk) work items.
+//
+// Replaces the reference's CPU bucket-chained build/probe
+// (/root/reference/tasks/BuildProbe.cpp:47-121) and its GPU offload
+// (/root/reference/operators/gpu/eth.cu:25-109, which only had 16 buckets per
+// partition and a build/probe stride mismatch), plus the
+// dormant probe / probe_skew / probe_count / probe_match_rate kernels
+// (kernels_optimized.cu:127-848).
+//
+// MI355X design:
+//  * After two radix passes a final partition's inner side fits an LDS open
+//    addressing table (load factor <= 0.5, linear probing, LDS CAS inserts).
+//  * Skew: a partition whose inner side exceeds rChunk, or whose outer side
+//    exceeds sChunk, is expanded into several work items (the
+//    skew_detect -> generate_block_mapping idea of kernels_optimized.cu:301-457,
+//    without CUDA dynamic parallelism, which HIP does not have).  Items are
+//    materialised by a count -> scan -> emit sequence on the device.
+//  * Persistent-style grid: a fixed grid (<= 8 WGs/CU) grid-strides over the
+//    item list so the LDS table is carved once per workgroup.
+//  * Counting: per-lane counters -> wave64 reduction -> one 64-bit global
+//    atomic per workgroup.  Materialisation: per-lane register slots, one
+//    wave-aggregated reservation per 64 probes (not one atomic per match).
+#include "kernels.h"
+#include "device_common.h"
+
+#include <type_traits>
+
+namespace hpcjoin {
+namespace kernels {
+
+constexpr int BPT = 256;
+constexpr uint32_t EMPTY32 = 0xFFFFFFFFu;
+constexpr unsigned long long EMPTY64 = ~0ull;
+constexpr int MAT_SLOTS = 2;  // register-held matches per probe before the overflow path
+
+enum BPMode : int { BP_CCOUNT = 0, BP_CMAT = 1, BP_WCOUNT = 2, BP_WMAT = 3 };
+
+static int bpMode(const BPArgs &a) { return (a.wide ? 2 : 0) + (a.materialize ? 1 : 0); }
+
+static size_t bpEntryBytes(int mode) {
+  switch (mode) {
+    case BP_CCOUNT: return 4;
+    case BP_CMAT: return 8;
+    case BP_WCOUNT: return 8;
+    default: return 16;
+  }
+}
+
+size_t bpLdsBytes(const BPArgs &a) {
+  const uint64_t slots = uint64_t(1) << ceilLog2(2ull * a.rChunk);
+  return slots * bpEntryBytes(bpMode(a)) + 64;
+}
+
+__device__ __forceinline__ uint32_t hash32(uint32_t frag, uint32_t tbits) {
+  return (frag * 2654435761u) >> (32 - tbits);
+}
+__device__ __forceinline__ uint32_t hash64(uint64_t key, uint32_t tbits) {
+  return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - tbits));
+}
+
+__global__ __launch_bounds__(BPT) void bpPlanCountsKernel(const uint64_t *__restrict__ partR,
+                                                          const uint64_t *__restrict__ partS, uint32_t P, uint32_t rc,
+                                                          uint32_t sc, uint32_t *counts) {
+  const uint32_t p = blockIdx.x * BPT + threadIdx.x;
+  if (p >= P) return;
+  const uint64_t nr = partR[p + 1] - partR[p], ns = partS[p + 1] - partS[p];
+  counts[p] = (nr == 0 || ns == 0) ? 0u : (uint32_t)(ceilDiv(nr, rc) * ceilDiv(ns, sc));
+}
+
+void bpPlanCounts(const BPArgs &a, uint32_t *counts, hipStream_t s) {
+  if (a.P == 0) return;
+  hipLaunchKernelGGL(bpPlanCountsKernel, dim3(ceilDiv(a.P, BPT)), dim3(BPT), 0, s, a.partR, a.partS, a.P, a.rChunk,
+                     a.sChunk, counts);
+  HIP_CHECK_LAUNCH();
+}
+
+__global__ __launch_bounds__(BPT) void bpEmitKernel(const uint64_t *__restrict__ partS, uint32_t P, uint32_t sc,
+                                                    const uint32_t *__restrict__ counts,
+                                                    const uint32_t *__restrict__ offsets, BPItem *items,
+                                                    uint32_t capacity) {
+  const uint32_t p = blockIdx.x * BPT + threadIdx.x;
+  if (p >= P) return;
+  const uint32_t c = counts[p];
+  if (c == 0) return;
+  const uint32_t nsChunks = (uint32_t)ceilDiv(partS[p + 1] - partS[p], sc);
+  const uint32_t o = offsets[p];
+  for (uint32_t i = 0; i < c && o + i < capacity; ++i) {
+    BPItem it;
+    it.part = p;
+    it.rChunk = i / nsChunks;
+    it.sChunk = i % nsChunks;
+    it.pad = 0;
+    items[o + i] = it;
+  }
+}
+
+void bpEmit(const BPArgs &a, const uint32_t *counts, const uint32_t *offsets, BPItem *items, uint32_t capacity,
+            hipStream_t s) {
+  if (a.P == 0) return;
+  hipLaunchKernelGGL(bpEmitKernel, dim3(ceilDiv(a.P, BPT)), dim3(BPT), 0, s, a.partS, a.P, a.sChunk, counts, offsets,
+                     items, capacity);
+  HIP_CHECK_LAUNCH();
+}
+
+// Wave-aggregated output reservation: every lane of the (converged) wave calls
+// this with its number of register-held matches; returns the lane's base slot.
+__device__ __forceinline__ unsigned long long reserveOutput(uint32_t mine, unsigned long long *cursor) {
+  const uint32_t incl = waveInclusiveScan<uint32_t>(mine);
+  const uint32_t total = __shfl(incl, WAVE - 1, WAVE);
+  unsigned long long base = 0;
+  if ((threadIdx.x & (WAVE - 1)) == WAVE - 1 && total) base = atomicAdd(cursor, (unsigned long long)total);
+  base = __shfl(base, WAVE - 1, WAVE);
+  return base + (incl - mine);
+}
+
+__device__ __forceinline__ void emitPair(const BPArgs &a, unsigned long long pos, uint64_t ridR, uint64_t ridS) {
+  if (pos < a.outCapacity) a.outPairs[pos] = make_ulonglong2(ridR, ridS);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(BPT) void buildProbeKernel(BPArgs a, const BPItem *__restrict__ items,
+                                                        const uint32_t *__restrict__ nItemsPtr, uint32_t capacity) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr bool WIDE = (MODE >= BP_WCOUNT);
+  constexpr bool MAT = (MODE == BP_CMAT || MODE == BP_WMAT);
+  using Entry = typename std::conditional<MODE == BP_CCOUNT, uint32_t, unsigned long long>::type;
+  const uint64_t maxSlots = uint64_t(1) << ceilLog2(2ull * a.rChunk);
+  Entry *table = reinterpret_cast<Entry *>(smem);
+  unsigned long long *ridTable = reinterpret_cast<unsigned long long *>(smem) + maxSlots;  // WMAT only
+  constexpr size_t EB = MODE == BP_CCOUNT ? 4 : (MODE == BP_WMAT ? 16 : 8);
+  unsigned long long *wsum = reinterpret_cast<unsigned long long *>(smem + maxSlots * EB);
+  const uint32_t t = threadIdx.x;
+  const uint64_t ridMask = a.keyShift >= 64 ? ~0ull : ((1ull << a.keyShift) - 1);
+  uint64_t matches = 0;
+  const uint32_t nItems = min(*nItemsPtr, capacity);
+
+  for (uint32_t w = blockIdx.x; w < nItems; w += gridDim.x) {
+    const BPItem it = items[w];
+    const uint64_t rb = a.partR[it.part] + (uint64_t)it.rChunk * a.rChunk;
+    const uint64_t re = min(a.partR[it.part + 1], rb + a.rChunk);
+    const uint64_t sb = a.partS[it.part] + (uint64_t)it.sChunk * a.sChunk;
+    const uint64_t se = min(a.partS[it.part + 1], sb + a.sChunk);
+    const uint32_t nr = (uint32_t)(re - rb), ns = (uint32_t)(se - sb);
+    uint32_t tbits = ceilLog2(2ull * nr);
+    if (tbits < 6) tbits = 6;
+    const uint32_t slots = 1u << tbits, mask = slots - 1;
+
+    for (uint32_t i = t; i < slots; i += BPT) table[i] = (Entry)(MODE == BP_CCOUNT ? EMPTY32 : EMPTY64);
+    __syncthreads();
+
+    // ---- build
+    for (uint32_t i = t; i < nr; i += BPT) {
+      if constexpr (!WIDE) {
+        const uint64_t v = reinterpret_cast<const uint64_t *>(a.R)[rb + i];
+        const uint32_t frag = (uint32_t)(v >> a.fragShift);
+        uint32_t h = hash32(frag, tbits);
+        if constexpr (MODE == BP_CCOUNT) {
+          while (atomicCAS(&table[h], EMPTY32, frag) != EMPTY32) h = (h + 1) & mask;
+        } else {
+          while (atomicCAS(&table[h], EMPTY64, (unsigned long long)v) != EMPTY64) h = (h + 1) & mask;
+        }
+      } else {
+        const ulonglong2 v = reinterpret_cast<const ulonglong2 *>(a.R)[rb + i];
+        uint32_t h = hash64(v.x, tbits);
+        while (atomicCAS(&table[h], EMPTY64, (unsigned long long)v.x) != EMPTY64) h = (h + 1) & mask;
+        if constexpr (MAT) ridTable[h] = v.y;
+      }
+    }
+    __syncthreads();
+
+    // ---- probe
+    for (uint32_t i0 = 0; i0 < ns; i0 += BPT) {
+      const uint32_t i = i0 + t;
+      const bool active = i < ns;
+      uint32_t found = 0;
+      uint64_t m0 = 0, m1 = 0, sRid = 0;
+      if (active) {
+        if constexpr (!WIDE) {
+          const uint64_t v = reinterpret_cast<const uint64_t *>(a.S)[sb + i];
+          const uint32_t frag = (uint32_t)(v >> a.fragShift);
+          uint32_t h = hash32(frag, tbits);
+          if constexpr (MODE == BP_CCOUNT) {
+            uint32_t e;
+            while ((e = table[h]) != EMPTY32) {
+              found += (e == frag);
+              h = (h + 1) & mask;
+            }
+          } else {
+            sRid = v & ridMask;
+            unsigned long long e;
+            while ((e = table[h]) != EMPTY64) {
+              if ((uint32_t)(e >> a.fragShift) == frag) {
+                const uint64_t rr = e & ridMask;
+                if (found == 0) m0 = rr;
+                else if (found == 1) m1 = rr;
+                else emitPair(a, atomicAdd(a.outCursor, 1ull), rr, sRid);  // overflow path
+                ++found;
+              }
+              h = (h + 1) & mask;
+            }
+          }
+        } else {
+          const ulonglong2 v = reinterpret_cast<const ulonglong2 *>(a.S)[sb + i];
+          uint32_t h = hash64(v.x, tbits);
+          sRid = v.y;
+          unsigned long long e;
+          while ((e = table[h]) != EMPTY64) {
+            if (e == v.x) {
+              if constexpr (MAT) {
+                const uint64_t rr = ridTable[h];
+                if (found == 0) m0 = rr;
+                else if (found == 1) m1 = rr;
+                else emitPair(a, atomicAdd(a.outCursor, 1ull), rr, sRid);
+              }
+              ++found;
+            }
+            h = (h + 1) & mask;
+          }
+        }
+      }
+      matches += found;
+      if constexpr (MAT) {
+        const uint32_t mine = found < MAT_SLOTS ? found : MAT_SLOTS;
+        const unsigned long long pos = reserveOutput(mine, a.outCursor);
+        if (mine > 0) emitPair(a, pos, m0, sRid);
+        if (mine > 1) emitPair(a, pos + 1, m1, sRid);
+      }
+    }
+    __syncthreads();
+  }
+  const unsigned long long total = blockReduceSum<BPT, unsigned long long>((unsigned long long)matches, wsum);
+  if (t == 0 && total) atomicAdd(a.result, total);
+}
+
+void buildProbe(const BPArgs &a, const BPItem *items, const uint32_t *nItems, uint32_t capacity, hipStream_t s) {
+  if (capacity == 0) return;
+  const size_t lds = bpLdsBytes(a);
+  HJ_CHECK(lds <= 160 * 1024, "buildProbe: LDS request %zu exceeds 160 KiB (rChunk=%u)", lds, a.rChunk);
+  const uint32_t perCu = (uint32_t)((160 * 1024) / lds);
+  const uint32_t maxBlocks = 256 * (perCu < 8 ? (perCu ? perCu : 1) : 8);
+  const uint32_t blocks = capacity < maxBlocks ? capacity : maxBlocks;
+  switch (bpMode(a)) {
+    case BP_CCOUNT:
+      hipLaunchKernelGGL(buildProbeKernel<BP_CCOUNT>, dim3(blocks), dim3(BPT), lds, s, a, items, nItems, capacity);
+      break;
+    case BP_CMAT:
+      hipLaunchKernelGGL(buildProbeKernel<BP_CMAT>, dim3(blocks), dim3(BPT), lds, s, a, items, nItems, capacity);
+      break;
+    case BP_WCOUNT:
+      hipLaunchKernelGGL(buildProbeKernel<BP_WCOUNT>, dim3(blocks), dim3(BPT), lds, s, a, items, nItems, capacity);
+      break;
+    default:
+      hipLaunchKernelGGL(buildProbeKernel<BP_WMAT>, dim3(blocks), dim3(BPT), lds, s, a, items, nItems, capacity);
+      break;
+  }
+  HIP_CHECK_LAUNCH();
+}
+
+}  // namespace kernels
+}  // namespace hpcjoin

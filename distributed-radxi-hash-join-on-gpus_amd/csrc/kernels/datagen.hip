@@ -1,0 +1,59 @@
+// Device relation generators (replace the sequential generators and the MPI
+// pairwise shuffle of /root/reference/data/Relation.cpp:63-141).
+//
+// Every element is a pure function of (params, global index), so each rank
+// writes its slice of one global relation straight into HBM with 16-byte
+// stores and no communication.  Bit-identical host versions live in
+// host/HostOps.cpp (used by the CPU reference path and the tests).
+#include "kernels.h"
+#include "device_common.h"
+
+namespace hpcjoin {
+namespace kernels {
+
+__device__ __forceinline__ uint64_t zipfRank(const ZipfParams &z, double u) {
+  double uz = u * z.zetan;
+  if (uz < 1.0) return 0;
+  if (uz < 1.0 + z.half_pow_theta) return 1;
+  uint64_t r = (uint64_t)((double)z.n * pow(z.eta * u - z.eta + 1.0, z.alpha));
+  return r >= z.n ? z.n - 1 : r;
+}
+
+__device__ __forceinline__ uint64_t genKey(const GenParams &p, uint64_t gi) {
+  switch (p.dist) {
+    case KeyDistribution::Unique:
+      return p.keyOffset + p.perm(gi);
+    case KeyDistribution::Dense:
+      return p.keyOffset + gi;
+    case KeyDistribution::Modulo:
+      return p.keyOffset + p.perm(gi % p.modulo);
+    case KeyDistribution::Uniform:
+      return p.keyOffset + (uint64_t)(uniform01(p.seed, gi) * (double)p.domain) % p.domain;
+    case KeyDistribution::Zipf:
+    default:
+      return p.keyOffset + p.perm(zipfRank(p.zipf, uniform01(p.seed, gi)));
+  }
+}
+
+__global__ __launch_bounds__(256) void generateKernel(ulonglong2 *__restrict__ out, uint64_t n, GenParams p) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t gi = p.globalOffset + i;
+    ulonglong2 t;
+    t.x = genKey(p, gi);
+    t.y = p.ridOffset + i;
+    out[i] = t;
+  }
+}
+
+void generate(data::Tuple *out, uint64_t n, const GenParams &p, hipStream_t s) {
+  if (n == 0) return;
+  const uint32_t threads = 256;
+  const uint64_t want = ceilDiv(n, threads);
+  const uint32_t blocks = (uint32_t)(want < 8192 ? want : 8192);
+  hipLaunchKernelGGL(generateKernel, dim3(blocks), dim3(threads), 0, s, reinterpret_cast<ulonglong2 *>(out), n, p);
+  HIP_CHECK_LAUNCH();
+}
+
+}  // namespace kernels
+}  // namespace hpcjoin

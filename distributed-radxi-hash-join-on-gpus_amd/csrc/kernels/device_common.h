@@ -1,0 +1,81 @@
+// Device-side building blocks shared by the gfx950 kernels: wave64 scans and
+// reductions and LDS block scans.  Wave width is hard-coded to 64 (CDNA).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../utils/Hip.h"
+
+namespace hpcjoin {
+namespace kernels {
+
+constexpr int WAVE = 64;
+
+template <typename T>
+__device__ __forceinline__ T waveInclusiveScan(T x) {
+  const int lane = threadIdx.x & (WAVE - 1);
+#pragma unroll
+  for (int o = 1; o < WAVE; o <<= 1) {
+    T y = __shfl_up(x, o, WAVE);
+    if (lane >= o) x += y;
+  }
+  return x;
+}
+
+template <typename T>
+__device__ __forceinline__ T waveReduceSum(T x) {
+#pragma unroll
+  for (int o = WAVE / 2; o > 0; o >>= 1) x += __shfl_xor(x, o, WAVE);
+  return x;
+}
+
+// Exclusive scan of an LDS array data[0..n) into out[0..n) (may alias) by a
+// workgroup of NT threads; each thread owns a contiguous run of entries.
+// waveTot must hold NT/64 entries of T.  Contains the barriers it needs; all
+// threads of the block must call it.
+template <int NT, typename T, typename U>
+__device__ __forceinline__ T blockExclusiveScanLds(const U *data, T *out, int n, T *waveTot) {
+  const int t = threadIdx.x, lane = t & (WAVE - 1), wid = t / WAVE;
+  const int per = (n + NT - 1) / NT;
+  const int b = t * per;
+  T local = 0;
+  for (int i = 0; i < per; ++i)
+    if (b + i < n) local += T(data[b + i]);
+  T incl = waveInclusiveScan<T>(local);
+  if (lane == WAVE - 1) waveTot[wid] = incl;
+  __syncthreads();
+  T prefix = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < NT / WAVE; ++w) {
+    T v = waveTot[w];
+    if (w < wid) prefix += v;
+    total += v;
+  }
+  T run = prefix + incl - local;
+  for (int i = 0; i < per; ++i)
+    if (b + i < n) {
+      T v = T(data[b + i]);
+      out[b + i] = run;
+      run += v;
+    }
+  __syncthreads();
+  return total;
+}
+
+template <int NT, typename T>
+__device__ __forceinline__ T blockReduceSum(T x, T *waveTot) {
+  const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+  x = waveReduceSum<T>(x);
+  __syncthreads();
+  if (lane == 0) waveTot[wid] = x;
+  __syncthreads();
+  T total = 0;
+#pragma unroll
+  for (int w = 0; w < NT / WAVE; ++w) total += waveTot[w];
+  return total;
+}
+
+}  // namespace kernels
+}  // namespace hpcjoin

@@ -1,0 +1,158 @@
+// Host-side launch API of every hand-written CDNA4 (gfx950) kernel.
+//
+// Kernel map vs the reference GPU library:
+//   datagen.hip      device relation generators (replace Relation.cpp:63-141)
+//   partition.hip    LDS radix histogram + LDS write-combining scatter, both
+//                    radix passes (network pass = NetworkPartitioning.cpp:74-222,
+//                    local pass = LocalPartitioning.cpp:138-250; supersede the
+//                    dormant histogram_build_L1/L2 + reorder_L1/L2 families of
+//                    kernels.cu / kernels_optimized.cu / kernels_tile.cu)
+//   build_probe.hip  LDS hash build/probe over (partition, R-chunk, S-chunk)
+//                    work items (BuildProbe.cpp:47-121, eth.cu:25-109, and the
+//                    probe / probe_skew / probe_count / probe_match_rate family)
+//   scan.hip         wave64 LDS exclusive scans (replaces thrust::exclusive_scan)
+//   npj.hip          no-partitioning join baseline (build_kernel/probe_kernel)
+//   microbench.hip   bandwidth / ablation micro-benchmarks
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "../core/Types.h"
+#include "../data/Tuple.h"
+#include "Random.h"
+
+namespace hpcjoin {
+namespace kernels {
+
+// ---------------------------------------------------------------- geometry
+constexpr uint32_t PART_THREADS = 256;   // 4 wave64s per partitioning workgroup
+constexpr uint32_t PART_ITEMS = 16;      // tuples per thread per tile
+constexpr uint32_t PART_TILE = PART_THREADS * PART_ITEMS;  // 4096 tuples per LDS tile
+constexpr uint32_t MAX_PART_BITS = 11;   // LDS cursor/count arrays sized for 2048 digits
+
+struct PartitionGeometry {
+  uint32_t blocks = 0;         // workgroups of the pass (each owns a contiguous tile range)
+  uint32_t tilesPerBlock = 0;  // tiles per workgroup
+  uint64_t tuplesPerBlock() const { return uint64_t(tilesPerBlock) * PART_TILE; }
+};
+// Cap the grid at ~8 workgroups per CU (2048) and give each workgroup a
+// contiguous run of tiles so its per-digit output runs stay contiguous.
+PartitionGeometry partitionGeometry(uint64_t n, uint32_t maxBlocks = 2048);
+
+size_t netScatterLdsBytes(uint32_t bits, bool wide);
+
+// ----------------------------------------------------------------- datagen
+enum class KeyDistribution : int { Unique = 0, Modulo = 1, Uniform = 2, Zipf = 3, Dense = 4 };
+
+struct GenParams {
+  KeyDistribution dist = KeyDistribution::Unique;
+  uint64_t globalOffset = 0;  // global index of local element 0
+  uint64_t ridOffset = 0;     // rid of local element 0
+  uint64_t domain = 0;        // key domain: keys in [keyOffset, keyOffset + domain)
+  uint64_t keyOffset = 0;
+  uint64_t modulo = 0;        // Modulo: key = perm(gi % modulo)
+  FeistelPermutation perm{};  // Unique/Modulo/Zipf rank -> key bijection
+  uint64_t seed = 0;
+  ZipfParams zipf{};
+};
+void generate(data::Tuple *out, uint64_t n, const GenParams &p, hipStream_t s);
+
+// ------------------------------------------------- pass 1: network partition
+// blockHist is digit-major [F][blocks] (u32).
+void netHistogram(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
+                  uint32_t *blockHist, hipStream_t s);
+// totals[c][F] = sum of blockHist over the blocks of chunk c (blocksPerChunk each).
+void digitTotals(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint32_t blocksPerChunk,
+                 uint32_t chunks, uint64_t *totals, hipStream_t s);
+// cursors[d][b] = base[chunk(b)][d] + sum_{b' in chunk(b), b' < b} blockHist[d][b'].
+void netCursors(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint32_t blocksPerChunk,
+                const uint64_t *base, uint64_t *cursors, hipStream_t s);
+// Compressed (8 B) and wide (16 B, full-range keys) scatter into the send buffer.
+// Scatters the tiles of workgroups [blockBegin, blockEnd) (one exchange chunk).
+void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift, const PartitionGeometry &g,
+                uint32_t blockBegin, uint32_t blockEnd, const uint64_t *cursors, uint64_t *out, hipStream_t s);
+void netScatterWide(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
+                    uint32_t blockBegin, uint32_t blockEnd, const uint64_t *cursors, data::Tuple *out,
+                    hipStream_t s);
+// Ablation baseline: one global atomic per tuple, no LDS staging
+// (reference histogram_build_global / reorder_global, kernels.cu:256-298).
+void netScatterGlobalAtomic(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift,
+                            uint64_t *digitCursor, uint64_t *out, hipStream_t s);
+
+// --------------------------------------------------- pass 2: local partition
+// One work item = a contiguous run (<= LOCAL_ITEM_MAX tuples) of one received
+// segment that belongs to owned partition `lp`.  Items are sorted by lp.
+struct LocalItem {
+  uint64_t begin;
+  uint32_t len;
+  uint32_t lp;
+};
+constexpr uint32_t LOCAL_ITEM_TILES = 16;
+constexpr uint32_t LOCAL_ITEM_MAX = LOCAL_ITEM_TILES * PART_TILE;  // 65536
+
+// digit = (word >> shift) & (2^bits - 1).  For compressed tuples word = value,
+// shift = keyShift; for wide tuples word = key, shift = networkBits.
+void localHistogram(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift,
+                    uint32_t bits, uint32_t *itemHist, hipStream_t s);
+void localCursors(const uint32_t *itemHist, const uint32_t *lpItemBegin, uint32_t owned, uint32_t bits,
+                  const uint64_t *lpBase, uint64_t *itemCursors, uint64_t *partBegin, hipStream_t s);
+void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift,
+                  uint32_t bits, const uint64_t *itemCursors, void *out, hipStream_t s);
+
+// --------------------------------------------------------------- build/probe
+struct BPItem {
+  uint32_t part;
+  uint32_t rChunk;
+  uint32_t sChunk;
+  uint32_t pad;
+};
+struct BPArgs {
+  const void *R = nullptr;        // partitioned inner (u64 compressed or Tuple)
+  const void *S = nullptr;        // partitioned outer
+  const uint64_t *partR = nullptr;  // [P+1] partition begin offsets
+  const uint64_t *partS = nullptr;
+  uint32_t P = 0;
+  uint32_t rChunk = 4096;   // max inner tuples per LDS table
+  uint32_t sChunk = 65536;  // max outer tuples per work item
+  uint32_t fragShift = 0;   // compressed: key fragment = value >> fragShift
+  uint32_t keyShift = 32;   // compressed: rid = value & (2^keyShift - 1)
+  bool wide = false;
+  bool materialize = false;
+  unsigned long long *result = nullptr;     // match counter (device)
+  unsigned long long *outCursor = nullptr;  // materialize: pair cursor (device)
+  ulonglong2 *outPairs = nullptr;           // materialize: (rid_inner, rid_outer)
+  uint64_t outCapacity = 0;
+};
+size_t bpLdsBytes(const BPArgs &a);
+void bpPlanCounts(const BPArgs &a, uint32_t *counts, hipStream_t s);
+void bpEmit(const BPArgs &a, const uint32_t *counts, const uint32_t *offsets, BPItem *items,
+            uint32_t capacity, hipStream_t s);
+// Grid-strides over min(*nItems, capacity) items; nItems is a device word
+// written by the scan, so no host round trip sits between plan and probe.
+void buildProbe(const BPArgs &a, const BPItem *items, const uint32_t *nItems, uint32_t capacity, hipStream_t s);
+
+// ------------------------------------------------------------------- scans
+size_t scanWorkspaceBytes(uint64_t n);
+// out[i] = sum_{j<i} in[j]; *total = sum of all (device pointer, may be null).
+void scanExclusiveU32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *total, void *workspace,
+                      hipStream_t s);
+
+// --------------------------------------------------- no-partitioning join
+uint64_t npjTableSlots(uint64_t innerSize);
+void npjBuild(const data::Tuple *R, uint64_t nR, unsigned long long *table, uint64_t slots, hipStream_t s);
+void npjProbe(const data::Tuple *S, uint64_t nS, const unsigned long long *table, uint64_t slots,
+              unsigned long long *result, hipStream_t s);
+
+// ---------------------------------------------------------- micro-benchmarks
+void copyKernel(const ulonglong2 *in, ulonglong2 *out, uint64_t n16, hipStream_t s);
+void readKernel(const ulonglong2 *in, uint64_t n16, unsigned long long *sink, hipStream_t s);
+
+}  // namespace kernels
+}  // namespace hpcjoin
+
+namespace hpcjoin {
+namespace kernels {
+// out[0] = max key, out[1] = max rid over n tuples (device); out must be zeroed.
+void keyRidMax(const data::Tuple *in, uint64_t n, unsigned long long *out, hipStream_t s);
+}  // namespace kernels
+}  // namespace hpcjoin

@@ -1,0 +1,69 @@
+// Streaming micro-kernels used by the phase micro-benchmarks (the analog of
+// the reference's UVA_benchmark / shared_memory_PT drivers,
+// /root/reference/operators/gpu/small_data_optimized.cu:254-399,1664-1729):
+// 16-byte-per-lane copy and read give the HBM ceiling the partition kernels
+// are judged against.
+#include "kernels.h"
+#include "device_common.h"
+
+namespace hpcjoin {
+namespace kernels {
+
+__global__ __launch_bounds__(256) void copyKernelImpl(const ulonglong2 *__restrict__ in, ulonglong2 *__restrict__ out,
+                                                      uint64_t n) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) out[i] = in[i];
+}
+
+__global__ __launch_bounds__(256) void readKernelImpl(const ulonglong2 *__restrict__ in, uint64_t n,
+                                                      unsigned long long *sink) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  unsigned long long acc = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const ulonglong2 v = in[i];
+    acc ^= v.x ^ v.y;
+  }
+  if (acc == 0x9E3779B97F4A7C15ull) *sink = acc;  // keeps the loads live
+}
+
+__global__ __launch_bounds__(256) void keyRidMaxKernel(const ulonglong2 *__restrict__ in, uint64_t n,
+                                                       unsigned long long *out) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  unsigned long long k = 0, r = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const ulonglong2 v = in[i];
+    k = v.x > k ? v.x : k;
+    r = v.y > r ? v.y : r;
+  }
+#pragma unroll
+  for (int o = WAVE / 2; o > 0; o >>= 1) {
+    const unsigned long long k2 = __shfl_xor(k, o, WAVE), r2 = __shfl_xor(r, o, WAVE);
+    k = k2 > k ? k2 : k;
+    r = r2 > r ? r2 : r;
+  }
+  if ((threadIdx.x & (WAVE - 1)) == 0) {
+    atomicMax(&out[0], k);
+    atomicMax(&out[1], r);
+  }
+}
+
+void keyRidMax(const data::Tuple *in, uint64_t n, unsigned long long *out, hipStream_t s) {
+  if (n == 0) return;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>(ceilDiv(n, 256), 2048);
+  hipLaunchKernelGGL(keyRidMaxKernel, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const ulonglong2 *>(in), n,
+                     out);
+  HIP_CHECK_LAUNCH();
+}
+
+void copyKernel(const ulonglong2 *in, ulonglong2 *out, uint64_t n16, hipStream_t s) {
+  hipLaunchKernelGGL(copyKernelImpl, dim3(4096), dim3(256), 0, s, in, out, n16);
+  HIP_CHECK_LAUNCH();
+}
+
+void readKernel(const ulonglong2 *in, uint64_t n16, unsigned long long *sink, hipStream_t s) {
+  hipLaunchKernelGGL(readKernelImpl, dim3(4096), dim3(256), 0, s, in, n16, sink);
+  HIP_CHECK_LAUNCH();
+}
+
+}  // namespace kernels
+}  // namespace hpcjoin

@@ -1,0 +1,67 @@
+// Device exclusive scan (u32) built from wave64 shuffles and LDS block scans.
+// Replaces the thrust::exclusive_scan calls of the reference GPU drivers
+// (/root/reference/operators/gpu/small_data.cu:95-155).  Three launches:
+// per-block reduce -> single-block scan of block sums -> per-block downsweep.
+#include "kernels.h"
+#include "device_common.h"
+
+namespace hpcjoin {
+namespace kernels {
+
+constexpr int SCAN_T = 256;
+constexpr int SCAN_PER = 8;
+constexpr uint32_t SCAN_TILE = SCAN_T * SCAN_PER;
+
+size_t scanWorkspaceBytes(uint64_t n) { return (ceilDiv(n, SCAN_TILE) + 16) * sizeof(uint32_t); }
+
+__global__ __launch_bounds__(SCAN_T) void scanReduceKernel(const uint32_t *__restrict__ in, uint64_t n,
+                                                           uint32_t *__restrict__ sums) {
+  __shared__ uint32_t wt[SCAN_T / WAVE];
+  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_PER; ++i) {
+    const uint64_t idx = base + (uint64_t)i * SCAN_T + threadIdx.x;
+    if (idx < n) s += in[idx];
+  }
+  s = blockReduceSum<SCAN_T, uint32_t>(s, wt);
+  if (threadIdx.x == 0) sums[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(SCAN_T) void scanSumsKernel(uint32_t *sums, uint32_t nb, uint32_t *total) {
+  __shared__ uint32_t wt[SCAN_T / WAVE];
+  const uint32_t t = blockExclusiveScanLds<SCAN_T, uint32_t, uint32_t>(sums, sums, (int)nb, wt);
+  if (threadIdx.x == 0 && total) *total = t;
+}
+
+__global__ __launch_bounds__(SCAN_T) void scanDownKernel(const uint32_t *__restrict__ in, uint64_t n,
+                                                         const uint32_t *__restrict__ sums, uint32_t *__restrict__ out) {
+  __shared__ uint32_t tile[SCAN_TILE];
+  __shared__ uint32_t wt[SCAN_T / WAVE];
+  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
+  const uint32_t cnt = (uint32_t)min((uint64_t)SCAN_TILE, n - base);
+  for (uint32_t i = threadIdx.x; i < SCAN_TILE; i += SCAN_T) tile[i] = i < cnt ? in[base + i] : 0;
+  __syncthreads();
+  blockExclusiveScanLds<SCAN_T, uint32_t, uint32_t>(tile, tile, (int)SCAN_TILE, wt);
+  const uint32_t off = sums[blockIdx.x];
+  for (uint32_t i = threadIdx.x; i < cnt; i += SCAN_T) out[base + i] = tile[i] + off;
+}
+
+void scanExclusiveU32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *total, void *workspace,
+                      hipStream_t s) {
+  if (n == 0) {
+    if (total) HIP_CHECK(hipMemsetAsync(total, 0, sizeof(uint32_t), s));
+    return;
+  }
+  const uint32_t nb = (uint32_t)ceilDiv(n, SCAN_TILE);
+  uint32_t *sums = reinterpret_cast<uint32_t *>(workspace);
+  hipLaunchKernelGGL(scanReduceKernel, dim3(nb), dim3(SCAN_T), 0, s, in, n, sums);
+  HIP_CHECK_LAUNCH();
+  hipLaunchKernelGGL(scanSumsKernel, dim3(1), dim3(SCAN_T), 0, s, sums, nb, total);
+  HIP_CHECK_LAUNCH();
+  hipLaunchKernelGGL(scanDownKernel, dim3(nb), dim3(SCAN_T), 0, s, in, n, sums, out);
+  HIP_CHECK_LAUNCH();
+}
+
+}  // namespace kernels
+}  // namespace hpcjoin

@@ -1,0 +1,94 @@
+#include "Arena.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+
+#include "../utils/Hip.h"
+
+namespace hpcjoin {
+namespace memory {
+
+void *Arena::rawAlloc(Location loc, uint64_t bytes, int device) {
+  if (bytes == 0) bytes = ALIGNMENT;
+  void *p = nullptr;
+  if (loc == Location::Device) {
+    HIP_CHECK(hipSetDevice(device));
+    HIP_CHECK(hipMalloc(&p, bytes));
+  } else {
+    int r = posix_memalign(&p, ALIGNMENT, bytes);
+    JOIN_ASSERT(r == 0 && p, "Arena", "posix_memalign(%lu) failed", (unsigned long)bytes);
+  }
+  return p;
+}
+
+void Arena::rawFree(Location loc, void *p) {
+  if (!p) return;
+  if (loc == Location::Device)
+    (void)hipFree(p);  // never throw from a destructor path
+  else
+    std::free(p);
+}
+
+Arena::~Arena() { releaseAll(); }
+
+void Arena::releaseAll() {
+  for (auto &f : fallbacks_) rawFree(loc_, f.first);
+  fallbacks_.clear();
+  fallbackBytes_ = 0;
+  rawFree(loc_, base_);
+  base_ = nullptr;
+  capacity_ = used_ = 0;
+}
+
+void Arena::reserve(uint64_t bytes) {
+  releaseAll();
+  bytes = ceilDiv(bytes, ALIGNMENT) * ALIGNMENT;
+  if (bytes) base_ = static_cast<uint8_t *>(rawAlloc(loc_, bytes, device_));
+  capacity_ = bytes;
+  used_ = 0;
+}
+
+void *Arena::get(uint64_t bytes) {
+  const uint64_t sz = ceilDiv(bytes ? bytes : 1, ALIGNMENT) * ALIGNMENT;
+  if (base_ && used_ + sz <= capacity_) {
+    void *p = base_ + used_;
+    used_ += sz;
+    if (used_ + fallbackBytes_ > peak_) peak_ = used_ + fallbackBytes_;
+    return p;
+  }
+  void *p = rawAlloc(loc_, sz, device_);
+  fallbacks_.emplace_back(p, sz);
+  fallbackBytes_ += sz;
+  if (used_ + fallbackBytes_ > peak_) peak_ = used_ + fallbackBytes_;
+  return p;
+}
+
+void Arena::reset() {
+  if (!fallbacks_.empty()) {
+    const uint64_t want = peak_ + peak_ / 8;
+    for (auto &f : fallbacks_) rawFree(loc_, f.first);
+    fallbacks_.clear();
+    fallbackBytes_ = 0;
+    reserve(want);
+  }
+  used_ = 0;
+}
+
+bool Arena::owns(const void *p) const {
+  const uint8_t *q = static_cast<const uint8_t *>(p);
+  return base_ && q >= base_ && q < base_ + capacity_;
+}
+
+void Arena::freeFallback(void *p) {
+  for (size_t i = 0; i < fallbacks_.size(); ++i)
+    if (fallbacks_[i].first == p) {
+      rawFree(loc_, p);
+      fallbackBytes_ -= fallbacks_[i].second;
+      fallbacks_.erase(fallbacks_.begin() + i);
+      return;
+    }
+}
+
+}  // namespace memory
+}  // namespace hpcjoin

@@ -1,0 +1,216 @@
+#include "HashJoin.h"
+
+#include <algorithm>
+
+#include "../comm/Communicator.h"
+#include "../comm/World.h"
+#include "../data/Window.h"
+#include "../memory/Arena.h"
+#include "../performance/Clock.h"
+#include "../performance/Measurements.h"
+#include "../tasks/BuildProbe.h"
+#include "../tasks/HistogramComputation.h"
+#include "../tasks/LocalPartitioning.h"
+#include "../tasks/NetworkPartitioning.h"
+#include "../utils/Hip.h"
+
+namespace hpcjoin {
+namespace operators {
+
+uint64_t HashJoin::RESULT_COUNTER = 0;
+std::queue<tasks::Task *> HashJoin::TASK_QUEUE;
+
+using performance::Measurements;
+using performance::nowUs;
+
+HashJoin::HashJoin(uint32_t numberOfNodes, uint32_t nodeId, data::Relation *innerRelation,
+                   data::Relation *outerRelation)
+    : numberOfNodes(numberOfNodes), nodeId(nodeId), innerRelation(innerRelation), outerRelation(outerRelation) {
+  comm::Communicator *c = comm::world();
+  JOIN_ASSERT(c->size() == numberOfNodes && c->rank() == nodeId, "HashJoin",
+              "world communicator is rank %u of %u, caller says %u of %u", c->rank(), c->size(), nodeId,
+              numberOfNodes);
+  ownedCtx.reset(new core::ExecContext(innerRelation->location(), innerRelation->device(), c));
+  ctx = ownedCtx.get();
+  makeJoinPlan();
+}
+
+HashJoin::HashJoin(data::Relation *innerRelation, data::Relation *outerRelation, core::ExecContext *ctx,
+                   const core::JoinConfig &config)
+    : numberOfNodes(ctx->numberOfNodes()), nodeId(ctx->nodeId()), innerRelation(innerRelation),
+      outerRelation(outerRelation), ctx(ctx), config(config) {
+  makeJoinPlan();
+}
+
+HashJoin::~HashJoin() {
+  for (auto &e : ev)
+    if (e) (void)hipEventDestroy(e);
+}
+
+void HashJoin::makeJoinPlan() {
+  JOIN_ASSERT(innerRelation->location() == ctx->location() && outerRelation->location() == ctx->location(),
+              "HashJoin", "relations must live where the engine runs (%s)", locationName(ctx->location()));
+  // Max key / rid over both relations and all ranks (the plan must be identical everywhere).
+  uint64_t mx[2] = {0, 0};
+  for (data::Relation *r : {innerRelation, outerRelation}) {
+    if (ctx->onDevice()) {
+      unsigned long long *d = ctx->workspace().getArray<unsigned long long>(2);
+      HIP_CHECK(hipMemsetAsync(d, 0, 16, ctx->stream()));
+      kernels::keyRidMax(r->getData(), r->getLocalSize(), d, ctx->stream());
+      unsigned long long h[2];
+      HIP_CHECK(hipMemcpyAsync(h, d, 16, hipMemcpyDeviceToHost, ctx->stream()));
+      HIP_CHECK(hipStreamSynchronize(ctx->stream()));
+      mx[0] = std::max<uint64_t>(mx[0], h[0]);
+      mx[1] = std::max<uint64_t>(mx[1], h[1]);
+    } else {
+      const data::Tuple *t = r->getData();
+      for (uint64_t i = 0; i < r->getLocalSize(); ++i) {
+        mx[0] = std::max(mx[0], t[i].key);
+        mx[1] = std::max(mx[1], t[i].rid);
+      }
+    }
+  }
+  ctx->workspace().reset();
+  std::vector<uint64_t> all(2 * numberOfNodes);
+  ctx->comm()->allGatherHost(mx, all.data(), 2);
+  for (uint32_t r = 0; r < numberOfNodes; ++r) {
+    mx[0] = std::max(mx[0], all[2 * r]);
+    mx[1] = std::max(mx[1], all[2 * r + 1]);
+  }
+  plan = core::makePlan(config, numberOfNodes, innerRelation->getGlobalSize(), outerRelation->getGlobalSize(), mx[0],
+                        mx[1]);
+  JOIN_DEBUG("HashJoin", "%s", plan.describe().c_str());
+  if (ctx->onDevice())
+    for (auto &e : ev) HIP_CHECK(hipEventCreate(&e));
+}
+
+void HashJoin::join() {
+  run();
+  RESULT_COUNTER = result.localMatches;
+}
+
+JoinResult HashJoin::run() {
+  result = JoinResult();
+  result.innerLocal = innerRelation->getLocalSize();
+  result.outerLocal = outerRelation->getLocalSize();
+  ctx->resetScratch();
+  const bool dev = ctx->onDevice();
+  if (dev) HIP_CHECK(hipSetDevice(ctx->device()));
+
+  Measurements::startJoin();
+  const uint64_t t0 = nowUs();
+  if (dev) HIP_CHECK(hipEventRecord(ev[0], ctx->stream()));
+
+  // ---------------------------------------------------------------- histogram
+  Measurements::startHistogramComputation();
+  tasks::HistogramComputation hc(numberOfNodes, nodeId, innerRelation, outerRelation, ctx, plan,
+                                 config.maxPartitionBlocks);
+  hc.execute();
+  if (dev) HIP_CHECK(hipEventRecord(ev[1], ctx->stream()));
+  Measurements::stopHistogramComputation();
+  Measurements::storeHistogramDetails(hc.localUs, innerRelation->getLocalSize(), outerRelation->getLocalSize(),
+                                      hc.globalUs, hc.assignUs, hc.offsetUs);
+  const uint64_t t1 = nowUs();
+
+  // ------------------------------------------------------------------ windows
+  Measurements::startWindowAllocation();
+  data::Window innerWindow(hc.innerOffsetMap()->getExchangePlan(), hc.innerGlobal(), hc.assignmentMap(), ctx,
+                           plan.wide);
+  data::Window outerWindow(hc.outerOffsetMap()->getExchangePlan(), hc.outerGlobal(), hc.assignmentMap(), ctx,
+                           plan.wide);
+  Measurements::stopWindowAllocation();
+  const uint64_t t2 = nowUs();
+
+  // ------------------------------------------------------------------ network
+  Measurements::startNetworkPartitioning();
+  {
+    tasks::NetworkPartitioning np(nodeId, innerRelation, outerRelation, &innerWindow, &outerWindow, &hc, ctx, plan);
+    np.execute();
+  }
+  Measurements::stopNetworkPartitioning();
+  Measurements::storeNetworkDetails(innerRelation->getLocalSize(), outerRelation->getLocalSize(),
+                                    hc.innerLocal()->getChunkCount());
+  Measurements::startWaitingForNetworkCompletion();
+  innerWindow.stop();
+  outerWindow.stop();
+  if (config.checks) {
+    innerWindow.assertAllTuplesWritten();
+    outerWindow.assertAllTuplesWritten();
+  }
+  if (dev) HIP_CHECK(hipEventRecord(ev[2], ctx->stream()));
+  Measurements::stopWaitingForNetworkCompletion();
+  const uint64_t t3 = nowUs();
+
+  // -------------------------------------------------------------------- local
+  Measurements::startLocalProcessingPreparations();
+  auto *lp = new tasks::LocalPartitioning(&innerWindow, &outerWindow, ctx, plan);
+  TASK_QUEUE.push(lp);
+  Measurements::stopLocalProcessingPreparations();
+  Measurements::startLocalProcessing();
+  tasks::BuildProbe *bp = nullptr;
+  while (!TASK_QUEUE.empty()) {
+    tasks::Task *t = TASK_QUEUE.front();
+    TASK_QUEUE.pop();
+    t->execute();
+    if (t->getType() == TASK_PARTITION) {
+      if (dev) HIP_CHECK(hipEventRecord(ev[3], ctx->stream()));
+      result.localItems = lp->workItems();
+      bp = new tasks::BuildProbe(&innerWindow, &outerWindow, ctx, plan, config.outputCapacity);
+      TASK_QUEUE.push(bp);
+      delete t;
+    }
+  }
+  if (dev) HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
+  ctx->synchronize();
+  while (bp->collect()) {  // rare: item list or output buffer overflowed -> exact re-run
+    ++result.reruns;
+    bp->execute();
+    if (dev) HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
+    ctx->synchronize();
+  }
+  Measurements::stopLocalProcessing();
+  const uint64_t t4 = nowUs();
+
+  result.localMatches = bp->getMatches();
+  result.outputPairs = plan.materialize ? std::min<uint64_t>(bp->getOutputCount(), UINT64_MAX) : 0;
+  result.outputOverflow = bp->outputOverflowed();
+  result.buildProbeItems = bp->getWorkItems();
+  output = bp->getOutput();
+  delete bp;
+  result.innerReceived = innerWindow.computeLocalWindowSize();
+  result.outerReceived = outerWindow.computeLocalWindowSize();
+  Measurements::storeLocalPartitioningDetails(result.innerReceived + result.outerReceived, result.localItems);
+  Measurements::storeBuildProbeDetails(result.innerReceived, result.outerReceived, result.buildProbeItems);
+  Measurements::storeResultTuples(result.localMatches);
+  Measurements::stopJoin();
+
+  result.joinMs = (t4 - t0) / 1000.0;
+  result.histogramMs = (t1 - t0) / 1000.0;
+  result.windowMs = (t2 - t1) / 1000.0;
+  result.networkMs = (t3 - t2) / 1000.0;
+  result.localMs = (t4 - t3) / 1000.0;
+  if (dev) {
+    float ms;
+    HIP_CHECK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+    result.devHistogramMs = ms;
+    HIP_CHECK(hipEventElapsedTime(&ms, ev[1], ev[2]));
+    result.devNetworkMs = ms;
+    HIP_CHECK(hipEventElapsedTime(&ms, ev[2], ev[3]));
+    result.devLocalPartitionMs = ms;
+    HIP_CHECK(hipEventElapsedTime(&ms, ev[3], ev[4]));
+    result.devBuildProbeMs = ms;
+    Measurements::storeDevicePhase("DHIST", result.devHistogramMs);
+    Measurements::storeDevicePhase("DNET", result.devNetworkMs);
+    Measurements::storeDevicePhase("DLOCPART", result.devLocalPartitionMs);
+    Measurements::storeDevicePhase("DBP", result.devBuildProbeMs);
+  }
+
+  uint64_t g = result.localMatches;
+  ctx->comm()->allReduceSumHost(&g, 1);
+  result.globalMatches = g;
+  RESULT_COUNTER = result.localMatches;
+  return result;
+}
+
+}  // namespace operators
+}  // namespace hpcjoin

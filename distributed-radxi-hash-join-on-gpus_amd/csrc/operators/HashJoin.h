@@ -1,0 +1,80 @@
+// The distributed radix hash join operator.  Same entry points as
+// /root/reference/operators/HashJoin.h:19-45 (constructor(numberOfNodes,
+// nodeId, inner, outer), join(), RESULT_COUNTER, TASK_QUEUE), plus the
+// MI355X-native constructor that takes an execution context and a runtime
+// JoinConfig, and run() which returns a JoinResult.
+//
+// Phase structure (reference HashJoin.cpp:45-220):
+//   histogram   LocalHistogram kernels -> fused all-gather -> AssignmentMap -> OffsetMap
+//   windows     exact-size receive buffers from the engine arena (no hipMalloc in steady state)
+//   network     cursor + LDS scatter kernels per chunk, RCCL all-to-allv per chunk on the exchange stream
+//   local       TASK_QUEUE: LocalPartitioning (second radix pass), BuildProbe (LDS hash join)
+//   result      one sync, counters read back, all-reduce of the match count
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <queue>
+
+#include "../core/ExecContext.h"
+#include "../core/JoinConfig.h"
+#include "../data/Relation.h"
+#include "../tasks/Task.h"
+
+namespace hpcjoin {
+namespace operators {
+
+struct JoinResult {
+  uint64_t localMatches = 0;
+  uint64_t globalMatches = 0;
+  uint64_t outputPairs = 0;        // materialize: pairs written on this rank
+  bool outputOverflow = false;
+  uint32_t reruns = 0;             // build/probe re-launches after an item/output overflow
+  double joinMs = 0;               // host wall: histogram start -> local result available
+  double histogramMs = 0, windowMs = 0, networkMs = 0, localMs = 0;  // host phases
+  double devHistogramMs = 0, devNetworkMs = 0, devLocalPartitionMs = 0, devBuildProbeMs = 0;  // hipEvents
+  uint64_t innerReceived = 0, outerReceived = 0;
+  uint64_t localItems = 0, buildProbeItems = 0;
+  uint64_t innerLocal = 0, outerLocal = 0;
+};
+
+class HashJoin {
+ public:
+  // Reference constructor: world communicator, default JoinConfig, relation location.
+  HashJoin(uint32_t numberOfNodes, uint32_t nodeId, data::Relation *innerRelation, data::Relation *outerRelation);
+  HashJoin(data::Relation *innerRelation, data::Relation *outerRelation, core::ExecContext *ctx,
+           const core::JoinConfig &config);
+  ~HashJoin();
+
+  void join();        // reference API: runs, updates RESULT_COUNTER (local matches)
+  JoinResult run();   // one full join
+  const JoinResult &lastResult() const { return result; }
+  const core::JoinPlan &getPlan() const { return plan; }
+  const core::JoinConfig &getConfig() const { return config; }
+  // Materialized (rid_inner, rid_outer) pairs of the last run, in ctx memory
+  // (valid until the next run on this context).
+  const ulonglong2 *getOutput() const { return output; }
+
+ protected:
+  uint32_t numberOfNodes;
+  uint32_t nodeId;
+  data::Relation *innerRelation;
+  data::Relation *outerRelation;
+
+ public:
+  static uint64_t RESULT_COUNTER;
+  static std::queue<tasks::Task *> TASK_QUEUE;
+
+ private:
+  void makeJoinPlan();
+  core::ExecContext *ctx;
+  std::unique_ptr<core::ExecContext> ownedCtx;
+  core::JoinConfig config;
+  core::JoinPlan plan;
+  JoinResult result;
+  const ulonglong2 *output = nullptr;
+  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+};
+
+}  // namespace operators
+}  // namespace hpcjoin

@@ -1,0 +1,193 @@
+#include "Measurements.h"
+
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <mutex>
+
+#include "../comm/Communicator.h"
+#include "Clock.h"
+
+namespace hpcjoin {
+namespace performance {
+
+namespace {
+struct State {
+  uint32_t nodeId = 0, numberOfNodes = 1;
+  std::string tag = "experiment", dir;
+  std::map<std::string, std::string> meta;
+  std::map<std::string, std::pair<double, std::string>> values;
+  uint64_t joinStart = 0, joinStop = 0;
+  uint64_t phaseStart[8] = {0};
+  uint64_t phaseTime[8] = {0};
+  uint64_t tuples = 0;
+};
+State &st() {
+  static State s;
+  return s;
+}
+enum Phase { HIST = 0, WINALLOC, NET, NETWAIT, LOCPREP, LOCAL, NPHASE };
+void begin(int p) { st().phaseStart[p] = nowUs(); }
+void end(int p) { st().phaseTime[p] = nowUs() - st().phaseStart[p]; }
+}  // namespace
+
+void Measurements::put(const std::string &key, double v, const char *unit) { st().values[key] = {v, unit}; }
+
+void Measurements::init(uint32_t nodeId, uint32_t numberOfNodes, const std::string &tag, const std::string &dir) {
+  State &s = st();
+  s = State();
+  s.nodeId = nodeId;
+  s.numberOfNodes = numberOfNodes;
+  s.tag = tag;
+  s.dir = dir;
+  if (!dir.empty()) mkdir(dir.c_str(), 0755);
+  writeMetaData("NUMNODES", numberOfNodes);
+  writeMetaData("NODEID", nodeId);
+  char host[256] = {0};
+  gethostname(host, sizeof(host) - 1);
+  writeMetaData("HOST", host);
+}
+
+void Measurements::writeMetaData(const char *key, const char *value) { st().meta[key] = value; }
+void Measurements::writeMetaData(const char *key, uint64_t value) { st().meta[key] = std::to_string(value); }
+
+void Measurements::startJoin() { st().joinStart = nowUs(); }
+void Measurements::stopJoin() {
+  State &s = st();
+  s.joinStop = nowUs();
+  put("JTOTAL", (double)(s.joinStop - s.joinStart), "us");
+  put("JHIST", (double)s.phaseTime[HIST], "us");
+  put("JMPI", (double)(s.phaseTime[WINALLOC] + s.phaseTime[NET] + s.phaseTime[NETWAIT]), "us");
+  put("JPROC", (double)(s.phaseTime[LOCPREP] + s.phaseTime[LOCAL]), "us");
+  put("SWINALLOC", (double)s.phaseTime[WINALLOC], "us");
+  put("SNETCOMPL", (double)s.phaseTime[NETWAIT], "us");
+  put("SLOCPREP", (double)s.phaseTime[LOCPREP], "us");
+}
+uint64_t Measurements::joinUs() { return st().joinStop - st().joinStart; }
+
+void Measurements::startHistogramComputation() { begin(HIST); }
+void Measurements::stopHistogramComputation() { end(HIST); }
+void Measurements::startWindowAllocation() { begin(WINALLOC); }
+void Measurements::stopWindowAllocation() { end(WINALLOC); }
+void Measurements::startNetworkPartitioning() { begin(NET); }
+void Measurements::stopNetworkPartitioning() { end(NET); }
+void Measurements::startWaitingForNetworkCompletion() { begin(NETWAIT); }
+void Measurements::stopWaitingForNetworkCompletion() { end(NETWAIT); }
+void Measurements::startLocalProcessingPreparations() { begin(LOCPREP); }
+void Measurements::stopLocalProcessingPreparations() { end(LOCPREP); }
+void Measurements::startLocalProcessing() { begin(LOCAL); }
+void Measurements::stopLocalProcessing() { end(LOCAL); }
+
+void Measurements::storeHistogramDetails(uint64_t localUs, uint64_t innerElements, uint64_t outerElements,
+                                         uint64_t globalUs, uint64_t assignUs, uint64_t offsetUs) {
+  // The device computes both relations' histograms in one enqueue + sync; the
+  // time is split by element count for the per-relation keys.
+  const double tot = (double)(innerElements + outerElements);
+  const double fi = tot > 0 ? innerElements / tot : 0.5;
+  put("HILOCAL", localUs * fi, "us");
+  put("HILOCELEM", (double)innerElements, "tuples");
+  put("HILOCRATE", localUs ? innerElements * 16.0 / (localUs * fi) : 0, "Mbytes/sec");
+  put("HOLOCAL", localUs * (1 - fi), "us");
+  put("HOLOCELEM", (double)outerElements, "tuples");
+  put("HOLOCRATE", localUs ? outerElements * 16.0 / (localUs * (1 - fi)) : 0, "Mbytes/sec");
+  put("HIGLOBAL", (double)globalUs, "us");
+  put("HOGLOBAL", 0, "us");  // fused into HIGLOBAL (one all-gather for both relations)
+  put("HASSIGN", (double)assignUs, "us");
+  put("HIOFFCOMP", offsetUs / 2.0, "us");
+  put("HOOFFCOMP", offsetUs / 2.0, "us");
+}
+
+void Measurements::storeNetworkDetails(uint64_t innerElements, uint64_t outerElements, uint64_t chunks) {
+  put("MIMAINPART", (double)st().phaseTime[NET], "us");
+  put("MWINPUTCNT", (double)chunks, "calls");
+  put("MIELEM", (double)innerElements, "tuples");
+  put("MOELEM", (double)outerElements, "tuples");
+}
+
+void Measurements::storeLocalPartitioningDetails(uint64_t elements, uint64_t items) {
+  put("LPELEMENTS", (double)elements, "tuples");
+  put("LPTASKCOUNT", (double)items, "tasks");
+}
+
+void Measurements::storeBuildProbeDetails(uint64_t buildElements, uint64_t probeElements, uint64_t items) {
+  put("BPBUILDELEM", (double)buildElements, "tuples");
+  put("BPPROBEELEM", (double)probeElements, "tuples");
+  put("BPTASKCOUNT", (double)items, "tasks");
+}
+
+void Measurements::storeDevicePhase(const std::string &key, double ms) { put(key, ms * 1000.0, "us"); }
+
+void Measurements::storeResultTuples(uint64_t tuples) {
+  st().tuples = tuples;
+  put("RTUPLES", (double)tuples, "tuples");
+}
+
+std::vector<uint64_t> Measurements::serializeResults() {
+  State &s = st();
+  auto dev = [&](const char *k) -> uint64_t {
+    auto it = s.values.find(k);
+    return it == s.values.end() ? 0 : (uint64_t)it->second.first;
+  };
+  return {s.tuples,
+          s.joinStop - s.joinStart,
+          s.phaseTime[HIST],
+          s.phaseTime[WINALLOC] + s.phaseTime[NET] + s.phaseTime[NETWAIT],
+          s.phaseTime[LOCPREP] + s.phaseTime[LOCAL],
+          s.phaseTime[WINALLOC],
+          s.phaseTime[NETWAIT],
+          s.phaseTime[LOCPREP],
+          dev("DLOCPART"),
+          dev("DBP")};
+}
+
+void Measurements::printMeasurements(comm::Communicator *comm) {
+  std::vector<uint64_t> mine = serializeResults();
+  const uint32_t N = comm->size();
+  std::vector<uint64_t> all(mine.size() * N);
+  comm->allGatherHost(mine.data(), all.data(), mine.size());
+  if (comm->rank() != 0) return;
+  const char *names[] = {"Tuples", "Join", "Histogram", "Network", "Local",
+                         "WinAlloc", "PartWait", "LocalPrep", "LocalPart", "LocalBP"};
+  uint64_t totalTuples = 0;
+  for (size_t k = 0; k < mine.size(); ++k) {
+    std::printf("[RESULTS] %s:\t", names[k]);
+    for (uint32_t r = 0; r < N; ++r) {
+      const uint64_t v = all[r * mine.size() + k];
+      if (k == 0) {
+        std::printf("%lu\t", (unsigned long)v);
+        totalTuples += v;
+      } else {
+        std::printf("%.3f\t", v / 1000.0);
+      }
+    }
+    std::printf("\n");
+  }
+  uint64_t maxJoin = 0;
+  for (uint32_t r = 0; r < N; ++r) maxJoin = std::max(maxJoin, all[r * mine.size() + 1]);
+  std::printf("[RESULTS] Summary:\t%lu\t%.3f\n", (unsigned long)totalTuples, maxJoin / 1000.0);
+  std::fflush(stdout);
+}
+
+void Measurements::storeAllMeasurements() {
+  State &s = st();
+  if (s.dir.empty()) return;
+  const std::string base = s.dir + "/" + std::to_string(s.nodeId);
+  if (FILE *f = std::fopen((base + ".perf").c_str(), "w")) {
+    for (auto &kv : s.values) std::fprintf(f, "%s\t%.3f\t%s\n", kv.first.c_str(), kv.second.first, kv.second.second.c_str());
+    std::fclose(f);
+  }
+  if (FILE *f = std::fopen((base + ".info").c_str(), "w")) {
+    for (auto &kv : s.meta) std::fprintf(f, "%s\t%s\n", kv.first.c_str(), kv.second.c_str());
+    std::fclose(f);
+  }
+}
+
+std::map<std::string, double> Measurements::snapshot() {
+  std::map<std::string, double> m;
+  for (auto &kv : st().values) m[kv.first] = kv.second.first;
+  return m;
+}
+
+}  // namespace performance
+}  // namespace hpcjoin

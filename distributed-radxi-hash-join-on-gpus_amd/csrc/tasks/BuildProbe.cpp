@@ -1,0 +1,122 @@
+#include "BuildProbe.h"
+
+#include <cstring>
+
+#include "../host/HostOps.h"
+#include "../memory/Arena.h"
+#include "../operators/HashJoin.h"
+#include "../utils/Hip.h"
+
+namespace hpcjoin {
+namespace tasks {
+
+BuildProbe::BuildProbe(uint64_t innerPartitionSize, data::CompressedTuple *innerPartition,
+                       uint64_t outerPartitionSize, data::CompressedTuple *outerPartition)
+    : innerPartitionSize(innerPartitionSize), innerPartition(innerPartition), outerPartitionSize(outerPartitionSize),
+      outerPartition(outerPartition), reference(true) {
+  refBounds = {0, innerPartitionSize, 0, outerPartitionSize};
+  args.R = innerPartition;
+  args.S = outerPartition;
+  args.partR = &refBounds[0];
+  args.partS = &refBounds[2];
+  args.P = 1;
+  args.keyShift = core::Configuration::NETWORK_PARTITIONING_FANOUT + core::Configuration::PAYLOAD_BITS;  // 32
+  args.fragShift = args.keyShift + core::Configuration::LOCAL_PARTITIONING_FANOUT;                      // 37
+}
+
+BuildProbe::BuildProbe(data::Window *innerWindow, data::Window *outerWindow, core::ExecContext *ctx,
+                       const core::JoinPlan &plan, uint64_t outputCapacity)
+    : innerPartitionSize(innerWindow->computeLocalWindowSize()), innerPartition(nullptr),
+      outerPartitionSize(outerWindow->computeLocalWindowSize()), outerPartition(nullptr), ctx(ctx), plan(plan),
+      outputCapacity(outputCapacity) {
+  windows[0] = innerWindow;
+  windows[1] = outerWindow;
+}
+
+BuildProbe::~BuildProbe() {}
+
+void BuildProbe::configure() {
+  data::Window *wi = windows[0], *wo = windows[1];
+  const uint32_t owned = (uint32_t)wi->getPlan().owned.size();
+  args = kernels::BPArgs();
+  args.R = wi->getPartitionedData();
+  args.S = wo->getPartitionedData();
+  args.partR = wi->getPartitionBegin();
+  args.partS = wo->getPartitionBegin();
+  args.P = owned << wi->getLocalBits();
+  args.rChunk = plan.rChunk;
+  args.sChunk = plan.sChunk;
+  args.fragShift = plan.wide ? 64 : plan.keyShift + wi->getLocalBits();
+  args.keyShift = plan.keyShift;
+  args.wide = plan.wide;
+  args.materialize = plan.materialize;
+  if (capacity == 0)
+    capacity = (uint32_t)std::min<uint64_t>(
+        0xFFFFFFF0ull, 2ull * args.P + outerPartitionSize / args.sChunk + innerPartitionSize / args.rChunk + 1024);
+}
+
+void BuildProbe::execute() {
+  if (reference) {
+    args.result = nullptr;
+    matches = host::buildProbe(args);
+    operators::HashJoin::RESULT_COUNTER += matches;
+    return;
+  }
+  configure();
+  const bool dev = ctx->onDevice();
+  memory::Arena &ws = ctx->workspace();
+  if (plan.materialize) {
+    if (outputCapacity == 0) outputCapacity = outerPartitionSize + 1024;
+    outPairs = static_cast<ulonglong2 *>(ws.get(outputCapacity * sizeof(ulonglong2)));
+    args.outPairs = outPairs;
+    args.outCapacity = outputCapacity;
+  }
+  if (!dev) {
+    hostCursor = 0;
+    args.outCursor = reinterpret_cast<unsigned long long *>(&hostCursor);
+    matches = host::buildProbe(args);
+    outputCount = hostCursor;
+    workItems = args.P;
+    return;
+  }
+  counters = ws.getArray<unsigned long long>(4);
+  HIP_CHECK(hipMemsetAsync(counters, 0, 4 * sizeof(unsigned long long), ctx->stream()));
+  args.result = counters;
+  args.outCursor = counters + 1;
+  uint32_t *nItems = reinterpret_cast<uint32_t *>(counters + 2);
+  uint32_t *counts = ws.getArray<uint32_t>(std::max<uint32_t>(args.P, 1));
+  uint32_t *offsets = ws.getArray<uint32_t>(std::max<uint32_t>(args.P, 1));
+  void *scanWs = ws.get(kernels::scanWorkspaceBytes(args.P));
+  kernels::BPItem *items = ws.getArray<kernels::BPItem>(capacity);
+  kernels::bpPlanCounts(args, counts, ctx->stream());
+  kernels::scanExclusiveU32(counts, offsets, args.P, nItems, scanWs, ctx->stream());
+  kernels::bpEmit(args, counts, offsets, items, capacity, ctx->stream());
+  kernels::buildProbe(args, items, nItems, capacity, ctx->stream());
+}
+
+bool BuildProbe::collect() {
+  if (reference || !ctx->onDevice()) {
+    overflowOut = plan.materialize && outputCount > outputCapacity;
+    return false;
+  }
+  unsigned long long h[4];
+  HIP_CHECK(hipMemcpy(h, counters, sizeof(h), hipMemcpyDeviceToHost));
+  matches = h[0];
+  outputCount = h[1];
+  uint32_t items;
+  std::memcpy(&items, &h[2], sizeof(items));
+  workItems = items;
+  bool again = false;
+  if (items > capacity) {
+    capacity = items;
+    again = true;
+  }
+  if (plan.materialize && outputCount > outputCapacity) {
+    outputCapacity = outputCount;
+    again = true;
+  }
+  return again;
+}
+
+}  // namespace tasks
+}  // namespace hpcjoin

@@ -1,0 +1,68 @@
+// Build/probe phase.  Reference: /root/reference/tasks/BuildProbe.cpp:47-121
+// (host bucket chaining per partition pair) and the GPU offload of
+// tasks/gpu/GPUWrapper.cu + operators/gpu/eth.cu (whose result was never
+// read back).  Device flow, all stream-ordered:
+//   plan counts -> wave64 scan (item count stays on the device) -> emit items
+//   -> persistent LDS build/probe kernel -> one 64-bit atomic per workgroup.
+// The host reads the counters once, after the join's single final sync.
+#pragma once
+
+#include <vector>
+
+#include "../core/ExecContext.h"
+#include "../data/CompressedTuple.h"
+#include "../data/Window.h"
+#include "../kernels/kernels.h"
+#include "Task.h"
+
+namespace hpcjoin {
+namespace tasks {
+
+class BuildProbe : public Task {
+ public:
+  // Reference-compatible: one (inner, outer) partition pair in host memory,
+  // reference bit layout (compare value >> 32, hash bits from 37).
+  BuildProbe(uint64_t innerPartitionSize, data::CompressedTuple *innerPartition, uint64_t outerPartitionSize,
+             data::CompressedTuple *outerPartition);
+  BuildProbe(data::Window *innerWindow, data::Window *outerWindow, core::ExecContext *ctx, const core::JoinPlan &plan,
+             uint64_t outputCapacity);
+  ~BuildProbe();
+
+  void execute();
+  task_type_t getType() { return TASK_BUILD_PROBE; }
+
+  // After the caller synchronised the streams: pull the counters; returns
+  // true if the work-item list or the output buffer overflowed and
+  // execute() must run again (it then sizes both exactly).
+  bool collect();
+  uint64_t getMatches() const { return matches; }
+  uint64_t getOutputCount() const { return outputCount; }
+  uint32_t getWorkItems() const { return workItems; }
+  const ulonglong2 *getOutput() const { return outPairs; }
+  bool outputOverflowed() const { return overflowOut; }
+
+ protected:
+  uint64_t innerPartitionSize;
+  data::CompressedTuple *innerPartition;
+  uint64_t outerPartitionSize;
+  data::CompressedTuple *outerPartition;
+
+ private:
+  void configure();
+  core::ExecContext *ctx = nullptr;
+  core::JoinPlan plan;
+  data::Window *windows[2] = {nullptr, nullptr};
+  kernels::BPArgs args;
+  uint32_t capacity = 0;
+  uint64_t outputCapacity = 0;
+  unsigned long long *counters = nullptr;  // [0] matches [1] out cursor [2] item count (u32)
+  ulonglong2 *outPairs = nullptr;
+  std::vector<uint64_t> refBounds;  // reference ctor: partition begin arrays
+  uint64_t matches = 0, outputCount = 0;
+  uint32_t workItems = 0;
+  bool reference = false, overflowOut = false;
+  uint64_t hostCursor = 0;
+};
+
+}  // namespace tasks
+}  // namespace hpcjoin

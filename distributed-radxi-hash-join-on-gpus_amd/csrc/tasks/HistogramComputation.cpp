@@ -1,0 +1,66 @@
+#include "HistogramComputation.h"
+
+#include "../performance/Clock.h"
+
+namespace hpcjoin {
+namespace tasks {
+
+HistogramComputation::HistogramComputation(uint32_t numberOfNodes, uint32_t nodeId, data::Relation *innerRelation,
+                                           data::Relation *outerRelation, core::ExecContext *ctx,
+                                           const core::JoinPlan &plan, uint32_t maxBlocks)
+    : nodeId(nodeId), numberOfNodes(numberOfNodes), innerRelation(innerRelation), outerRelation(outerRelation),
+      ctx(ctx) {
+  innerRelationLocalHistogram.reset(
+      new histograms::LocalHistogram(innerRelation, ctx, plan.networkBits, plan.chunks, maxBlocks));
+  outerRelationLocalHistogram.reset(
+      new histograms::LocalHistogram(outerRelation, ctx, plan.networkBits, plan.chunks, maxBlocks));
+  innerRelationGlobalHistogram.reset(new histograms::GlobalHistogram(innerRelationLocalHistogram.get(), ctx->comm()));
+  outerRelationGlobalHistogram.reset(new histograms::GlobalHistogram(outerRelationLocalHistogram.get(), ctx->comm()));
+  assignment.reset(new histograms::AssignmentMap(numberOfNodes, innerRelationGlobalHistogram.get(),
+                                                 outerRelationGlobalHistogram.get(), plan.assignment));
+  innerOffsets.reset(new histograms::OffsetMap(numberOfNodes, nodeId, innerRelationLocalHistogram.get(),
+                                               innerRelationGlobalHistogram.get(), assignment.get()));
+  outerOffsets.reset(new histograms::OffsetMap(numberOfNodes, nodeId, outerRelationLocalHistogram.get(),
+                                               outerRelationGlobalHistogram.get(), assignment.get()));
+}
+
+HistogramComputation::~HistogramComputation() {}
+
+void HistogramComputation::execute() {
+  computeLocalHistograms();
+  computeGlobalInformation();
+}
+
+void HistogramComputation::computeLocalHistograms() {
+  const uint64_t t0 = performance::nowUs();
+  innerRelationLocalHistogram->computeLocalHistogram();
+  outerRelationLocalHistogram->computeLocalHistogram();
+  ctx->synchronize();  // the host needs the totals for the collective
+  localUs = performance::nowUs() - t0;
+}
+
+void HistogramComputation::computeGlobalInformation() {
+  uint64_t t0 = performance::nowUs();
+  histograms::GlobalHistogram::computeGlobalHistograms(*innerRelationGlobalHistogram, *outerRelationGlobalHistogram);
+  globalUs = performance::nowUs() - t0;
+  t0 = performance::nowUs();
+  assignment->computePartitionAssignment();
+  assignUs = performance::nowUs() - t0;
+  t0 = performance::nowUs();
+  innerOffsets->computeOffsets();
+  outerOffsets->computeOffsets();
+  offsetUs = performance::nowUs() - t0;
+}
+
+uint32_t *HistogramComputation::getAssignment() { return assignment->getPartitionAssignment(); }
+uint64_t *HistogramComputation::getInnerRelationLocalHistogram() { return innerRelationLocalHistogram->getLocalHistogram(); }
+uint64_t *HistogramComputation::getOuterRelationLocalHistogram() { return outerRelationLocalHistogram->getLocalHistogram(); }
+uint64_t *HistogramComputation::getInnerRelationGlobalHistogram() { return innerRelationGlobalHistogram->getGlobalHistogram(); }
+uint64_t *HistogramComputation::getOuterRelationGlobalHistogram() { return outerRelationGlobalHistogram->getGlobalHistogram(); }
+uint64_t *HistogramComputation::getInnerRelationBaseOffsets() { return innerOffsets->getBaseOffsets(); }
+uint64_t *HistogramComputation::getOuterRelationBaseOffsets() { return outerOffsets->getBaseOffsets(); }
+uint64_t *HistogramComputation::getInnerRelationWriteOffsets() { return innerOffsets->getAbsoluteWriteOffsets(); }
+uint64_t *HistogramComputation::getOuterRelationWriteOffsets() { return outerOffsets->getAbsoluteWriteOffsets(); }
+
+}  // namespace tasks
+}  // namespace hpcjoin

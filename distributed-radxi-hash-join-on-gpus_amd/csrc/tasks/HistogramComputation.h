@@ -1,0 +1,72 @@
+// Histogram phase: local histograms (HIP kernels) -> one fused all-gather ->
+// assignment -> offsets / exchange plans.  Reference:
+// /root/reference/tasks/HistogramComputation.cpp:63-76.
+#pragma once
+
+#include <memory>
+
+#include "../core/ExecContext.h"
+#include "../data/Relation.h"
+#include "../histograms/AssignmentMap.h"
+#include "../histograms/GlobalHistogram.h"
+#include "../histograms/LocalHistogram.h"
+#include "../histograms/OffsetMap.h"
+#include "Task.h"
+
+namespace hpcjoin {
+namespace tasks {
+
+class HistogramComputation : public Task {
+ public:
+  HistogramComputation(uint32_t numberOfNodes, uint32_t nodeId, data::Relation *innerRelation,
+                       data::Relation *outerRelation, core::ExecContext *ctx, const core::JoinPlan &plan,
+                       uint32_t maxBlocks);
+  ~HistogramComputation();
+
+  void execute();
+  task_type_t getType() { return TASK_HISTOGRAM; }
+
+  uint32_t *getAssignment();
+  uint64_t *getInnerRelationLocalHistogram();
+  uint64_t *getOuterRelationLocalHistogram();
+  uint64_t *getInnerRelationGlobalHistogram();
+  uint64_t *getOuterRelationGlobalHistogram();
+  uint64_t *getInnerRelationBaseOffsets();
+  uint64_t *getOuterRelationBaseOffsets();
+  uint64_t *getInnerRelationWriteOffsets();
+  uint64_t *getOuterRelationWriteOffsets();
+
+  histograms::LocalHistogram *innerLocal() { return innerRelationLocalHistogram.get(); }
+  histograms::LocalHistogram *outerLocal() { return outerRelationLocalHistogram.get(); }
+  histograms::GlobalHistogram *innerGlobal() { return innerRelationGlobalHistogram.get(); }
+  histograms::GlobalHistogram *outerGlobal() { return outerRelationGlobalHistogram.get(); }
+  histograms::AssignmentMap *assignmentMap() { return assignment.get(); }
+  histograms::OffsetMap *innerOffsetMap() { return innerOffsets.get(); }
+  histograms::OffsetMap *outerOffsetMap() { return outerOffsets.get(); }
+
+  // Sub-phase host times (µs) for Measurements.
+  uint64_t localUs = 0, globalUs = 0, assignUs = 0, offsetUs = 0;
+
+ protected:
+  void computeLocalHistograms();
+  void computeGlobalInformation();
+
+ protected:
+  uint32_t nodeId;
+  uint32_t numberOfNodes;
+  data::Relation *innerRelation;
+  data::Relation *outerRelation;
+  std::unique_ptr<histograms::LocalHistogram> innerRelationLocalHistogram;
+  std::unique_ptr<histograms::LocalHistogram> outerRelationLocalHistogram;
+  std::unique_ptr<histograms::GlobalHistogram> innerRelationGlobalHistogram;
+  std::unique_ptr<histograms::GlobalHistogram> outerRelationGlobalHistogram;
+  std::unique_ptr<histograms::AssignmentMap> assignment;
+  std::unique_ptr<histograms::OffsetMap> innerOffsets;
+  std::unique_ptr<histograms::OffsetMap> outerOffsets;
+
+ private:
+  core::ExecContext *ctx;
+};
+
+}  // namespace tasks
+}  // namespace hpcjoin

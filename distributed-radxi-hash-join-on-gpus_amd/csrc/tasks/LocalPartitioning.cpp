@@ -1,0 +1,85 @@
+#include "LocalPartitioning.h"
+
+#include "../host/HostOps.h"
+#include "../memory/Arena.h"
+#include "../utils/Hip.h"
+
+namespace hpcjoin {
+namespace tasks {
+
+LocalPartitioning::LocalPartitioning(data::Window *innerWindow, data::Window *outerWindow, core::ExecContext *ctx,
+                                     const core::JoinPlan &plan)
+    : ctx(ctx), plan(plan) {
+  windows[0] = innerWindow;
+  windows[1] = outerWindow;
+}
+
+LocalPartitioning::~LocalPartitioning() {}
+
+void LocalPartitioning::execute() {
+  partition(windows[0], 0);
+  partition(windows[1], 1);
+}
+
+void LocalPartitioning::partition(data::Window *w, int which) {
+  w->stop();  // compute stream now waits for this window's exchanges
+  const histograms::ExchangePlan &xp = w->getPlan();
+  const uint32_t owned = (uint32_t)xp.owned.size();
+  const bool wide = w->isWide();
+  const uint32_t tb = w->tupleBytes();
+  elements += xp.recvTotal;
+
+  if (!plan.twoLevel && xp.windowIsPartitionMajor()) {
+    uint64_t *pb = ctx->workspace().getArray<uint64_t>(owned + 1);
+    ctx->copy(pb, xp.lpBase.data(), (owned + 1) * 8, ctx->onDevice(), false);
+    w->setPartitioned(w->getData(), pb, 0);
+    return;
+  }
+  const uint32_t bits = plan.twoLevel ? plan.localBits : 0, F = 1u << bits;
+  std::vector<kernels::LocalItem> &it = items[which];
+  std::vector<uint32_t> &lb = lpItemBegin[which];
+  it.clear();
+  lb.assign(owned + 1, 0);
+  size_t seg = 0;
+  for (uint32_t lp = 0; lp < owned; ++lp) {
+    lb[lp] = (uint32_t)it.size();
+    for (; seg < xp.segments.size() && xp.segments[seg].lp == lp; ++seg)
+      for (uint64_t off = 0; off < xp.segments[seg].len; off += kernels::LOCAL_ITEM_MAX) {
+        const uint64_t len = std::min<uint64_t>(kernels::LOCAL_ITEM_MAX, xp.segments[seg].len - off);
+        it.push_back(kernels::LocalItem{xp.segments[seg].begin + off, (uint32_t)len, lp});
+      }
+  }
+  lb[owned] = (uint32_t)it.size();
+  const uint32_t nItems = (uint32_t)it.size();
+  const uint32_t shift = wide ? plan.networkBits : plan.keyShift;
+
+  void *out = ctx->workspace().get(std::max<uint64_t>(xp.recvTotal, 1) * tb);
+  uint32_t *itemHist = ctx->workspace().getArray<uint32_t>(std::max<uint64_t>(1, (uint64_t)nItems * F));
+  uint64_t *itemCursors = ctx->workspace().getArray<uint64_t>(std::max<uint64_t>(1, (uint64_t)nItems * F));
+  uint64_t *partBegin = ctx->workspace().getArray<uint64_t>((uint64_t)owned * F + 1);
+
+  if (ctx->onDevice()) {
+    kernels::LocalItem *dItems = ctx->workspace().getArray<kernels::LocalItem>(std::max<uint32_t>(nItems, 1));
+    uint32_t *dLb = ctx->workspace().getArray<uint32_t>(owned + 1);
+    uint64_t *dBase = ctx->workspace().getArray<uint64_t>(owned + 1);
+    ctx->copy(dItems, it.data(), (uint64_t)nItems * sizeof(kernels::LocalItem), true, false);
+    ctx->copy(dLb, lb.data(), (owned + 1) * 4ull, true, false);
+    ctx->copy(dBase, xp.lpBase.data(), (owned + 1) * 8ull, true, false);
+    if (owned == 0) {
+      zero.assign(1, 0);
+      ctx->copy(partBegin, zero.data(), 8, true, false);
+    }
+    kernels::localHistogram(w->getData(), wide, dItems, nItems, shift, bits, itemHist, ctx->stream());
+    kernels::localCursors(itemHist, dLb, owned, bits, dBase, itemCursors, partBegin, ctx->stream());
+    kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, itemCursors, out, ctx->stream());
+  } else {
+    if (owned == 0) partBegin[0] = 0;
+    host::localHistogram(w->getData(), wide, it.data(), nItems, shift, bits, itemHist);
+    host::localCursors(itemHist, lb.data(), owned, bits, xp.lpBase.data(), itemCursors, partBegin);
+    host::localScatter(w->getData(), wide, it.data(), nItems, shift, bits, itemCursors, out);
+  }
+  w->setPartitioned(out, partBegin, bits);
+}
+
+}  // namespace tasks
+}  // namespace hpcjoin

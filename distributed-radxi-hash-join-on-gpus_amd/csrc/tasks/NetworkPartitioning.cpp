@@ -1,0 +1,62 @@
+#include "NetworkPartitioning.h"
+
+#include "../host/HostOps.h"
+#include "../memory/Arena.h"
+#include "../utils/Hip.h"
+
+namespace hpcjoin {
+namespace tasks {
+
+NetworkPartitioning::NetworkPartitioning(uint32_t nodeId, data::Relation *innerRelation,
+                                         data::Relation *outerRelation, data::Window *innerWindow,
+                                         data::Window *outerWindow, HistogramComputation *histograms,
+                                         core::ExecContext *ctx, const core::JoinPlan &plan)
+    : nodeId(nodeId), innerRelation(innerRelation), outerRelation(outerRelation), innerWindow(innerWindow),
+      outerWindow(outerWindow), histograms(histograms), ctx(ctx), plan(plan) {}
+
+NetworkPartitioning::~NetworkPartitioning() {}
+
+void NetworkPartitioning::execute() {
+  partition(innerRelation, innerWindow, histograms->innerLocal(), histograms->innerOffsetMap()->getExchangePlan());
+  partition(outerRelation, outerWindow, histograms->outerLocal(), histograms->outerOffsetMap()->getExchangePlan());
+}
+
+void NetworkPartitioning::partition(data::Relation *relation, data::Window *window,
+                                    histograms::LocalHistogram *local, const histograms::ExchangePlan &xp) {
+  const uint64_t n = relation->getLocalSize();
+  JOIN_ASSERT(xp.sendTotal == n, "NetworkPartitioning", "plan sends %lu of %lu tuples",
+              (unsigned long)xp.sendTotal, (unsigned long)n);
+  const uint32_t bits = plan.networkBits, F = 1u << bits;
+  const kernels::PartitionGeometry &g = local->geometry();
+  const uint32_t bpc = local->blocksPerChunk(), chunks = local->getChunkCount();
+  const bool single = xp.numberOfNodes == 1;
+  const uint32_t tb = window->tupleBytes();
+  void *send = single ? window->getData() : ctx->workspace().get(n * tb);
+  uint64_t *cursors = ctx->workspace().getArray<uint64_t>((uint64_t)F * g.blocks);
+  window->start();
+  if (ctx->onDevice()) {
+    uint64_t *base = ctx->workspace().getArray<uint64_t>((uint64_t)chunks * F);
+    ctx->copy(base, xp.digitBase.data(), xp.digitBase.size() * 8, true, false);
+    kernels::netCursors(local->blockHistogram(), F, g.blocks, bpc, base, cursors, ctx->stream());
+    for (uint32_t c = 0; c < chunks; ++c) {
+      const uint32_t b0 = c * bpc, b1 = std::min(g.blocks, b0 + bpc);
+      if (plan.wide)
+        kernels::netScatterWide(relation->getData(), n, bits, g, b0, b1, cursors, static_cast<data::Tuple *>(send),
+                                ctx->stream());
+      else
+        kernels::netScatter(relation->getData(), n, bits, plan.keyShift, g, b0, b1, cursors,
+                            static_cast<uint64_t *>(send), ctx->stream());
+      if (!single) window->exchange(send, c);
+    }
+  } else {
+    host::netCursors(local->blockHistogram(), F, g.blocks, bpc, xp.digitBase.data(), cursors);
+    for (uint32_t c = 0; c < chunks; ++c) {
+      const uint32_t b0 = c * bpc, b1 = std::min(g.blocks, b0 + bpc);
+      host::netScatter(relation->getData(), n, bits, plan.keyShift, g, b0, b1, cursors, send, plan.wide);
+      if (!single) window->exchange(send, c);
+    }
+  }
+}
+
+}  // namespace tasks
+}  // namespace hpcjoin

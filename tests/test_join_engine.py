@@ -1,0 +1,60 @@
+"""End-to-end HashJoin engine (single process) on host and device."""
+import pytest
+
+from conftest import devices
+
+
+def run_join(C, dev, G_R, G_S, outer_dist="UNIQUE", cfg=None, theta=0.75):
+    loc = "device" if dev == "cuda" else "host"
+    ctx = C.ExecContext(loc, 0 if loc == "device" else -1, C.LocalCommunicator())
+    inner = C.GenSpec(seed=1234)
+    outer = C.GenSpec(distribution=getattr(C.KeyDistribution, outer_dist), seed=4321,
+                      domain=0 if outer_dist == "UNIQUE" else G_R, zipf_theta=theta)
+    R = C.Relation(G_R, G_R, loc, 0)
+    S = C.Relation(G_S, G_S, loc, 0)
+    R.generate(inner, 0)
+    S.generate(outer, 0)
+    j = C.HashJoin(R, S, ctx, cfg or C.JoinConfig())
+    res = j.run()
+    return res, C.Relation.expected_matches(inner, G_R, outer, G_S), j
+
+
+@pytest.mark.parametrize("dev", devices())
+@pytest.mark.parametrize("dist", ["UNIQUE", "UNIFORM", "ZIPF", "MODULO"])
+def test_join_matches_oracle(C, dev, dist):
+    res, exp, _ = run_join(C, dev, 300_000, 500_000 if dist != "UNIQUE" else 300_000, dist)
+    assert res["global_matches"] == exp
+
+
+@pytest.mark.parametrize("dev", devices())
+def test_join_single_level(C, dev):
+    cfg = C.JoinConfig()
+    cfg.two_level = False
+    res, exp, j = run_join(C, dev, 200_000, 200_000, cfg=cfg)
+    assert not j.plan.two_level
+    assert res["global_matches"] == exp
+
+
+@pytest.mark.parametrize("dev", devices())
+def test_join_wide_and_materialize(C, dev):
+    cfg = C.JoinConfig()
+    cfg.format = C.TupleFormat.WIDE
+    cfg.materialize = True
+    res, exp, j = run_join(C, dev, 100_000, 100_000, cfg=cfg)
+    assert res["global_matches"] == exp == res["output_pairs"]
+    out = j.output()
+    assert out.shape == (exp, 2)
+
+
+@pytest.mark.parametrize("dev", devices())
+def test_join_repeatable(C, dev):
+    res, exp, j = run_join(C, dev, 200_000, 200_000)
+    for _ in range(3):
+        assert j.run()["global_matches"] == exp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G", [1 << 24, 128_000_000])
+def test_join_large_device(C, cuda, G):
+    res, exp, j = run_join(C, "cuda", G, G)
+    assert res["global_matches"] == exp
