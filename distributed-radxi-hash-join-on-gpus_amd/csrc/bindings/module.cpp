@@ -58,7 +58,7 @@ void setDevice(const at::Tensor &t) {
 
 // ---- single-relation network pass (one "rank", all partitions local) ------
 std::tuple<at::Tensor, at::Tensor> opNetPartition(const at::Tensor &tuples, int64_t bits, int64_t keyShift,
-                                                  bool wide, int64_t maxBlocks) {
+                                                  bool wide, int64_t maxBlocks, int64_t keyBits) {
   checkTuples(tuples, "tuples");
   setDevice(tuples);
   const uint64_t n = tuples.size(0);
@@ -78,17 +78,18 @@ std::tuple<at::Tensor, at::Tensor> opNetPartition(const at::Tensor &tuples, int6
     host::digitTotals(ptr<uint32_t>(blockHist), F, g.blocks, g.blocks, 1, ptr<uint64_t>(totals));
   }
   at::Tensor begin = at::zeros({(int64_t)F + 1}, at::kLong);
-  at::Tensor totalsH = totals.cpu();
-  for (uint32_t d = 0; d < F; ++d) begin[d + 1] = begin[d].item<int64_t>() + totalsH[d].item<int64_t>();
+  begin.slice(0, 1).copy_(at::cumsum(totals.cpu(), 0));
   at::Tensor base = begin.slice(0, 0, F).to(tuples.device()).contiguous();
   if (l == Location::Device) {
-    kernels::netCursors(ptr<uint32_t>(blockHist), F, g.blocks, g.blocks, ptr<uint64_t>(base), ptr<uint64_t>(cursors),
-                        nullptr);
+    const bool narrow = kernels::cursorsNarrow(n);
+    at::Tensor gcur = at::empty({(int64_t)kernels::CLAIM_GROUPS * F}, like(tuples));
+    kernels::netGroupCursors(ptr<uint32_t>(blockHist), F, g.blocks, g.blocks, ptr<uint64_t>(base), gcur.data_ptr(),
+                             narrow, nullptr);
     if (wide)
-      kernels::netScatterWide(in, n, bits, g, 0, g.blocks, ptr<uint64_t>(cursors), ptr<data::Tuple>(out), nullptr);
+      kernels::netScatterWide(in, n, bits, g, 0, g.blocks, gcur.data_ptr(), ptr<data::Tuple>(out), nullptr);
     else
-      kernels::netScatter(in, n, bits, (uint32_t)keyShift, g, 0, g.blocks, ptr<uint64_t>(cursors), ptr<uint64_t>(out),
-                          nullptr);
+      kernels::netScatter(in, n, bits, (uint32_t)keyShift, g, 0, g.blocks, gcur.data_ptr(), ptr<uint64_t>(out),
+                          nullptr, (uint32_t)keyBits);
   } else {
     host::netCursors(ptr<uint32_t>(blockHist), F, g.blocks, g.blocks, ptr<uint64_t>(base), ptr<uint64_t>(cursors));
     host::netScatter(in, n, bits, (uint32_t)keyShift, g, 0, g.blocks, ptr<uint64_t>(cursors), out.data_ptr(), wide);
@@ -135,7 +136,7 @@ std::tuple<at::Tensor, at::Tensor> opLocalPartition(const at::Tensor &values, co
     const uint64_t b = pbIn[lp].item<int64_t>(), e = pbIn[lp + 1].item<int64_t>();
     base[lp] = b;
     for (uint64_t o = b; o < e; o += kernels::LOCAL_ITEM_MAX)
-      items.push_back({o, (uint32_t)std::min<uint64_t>(kernels::LOCAL_ITEM_MAX, e - o), lp});
+      items.push_back({o, (uint32_t)std::min<uint64_t>(kernels::LOCAL_ITEM_MAX, e - o), lp, 0, 0});
   }
   lb[owned] = (uint32_t)items.size();
   base[owned] = owned ? (uint64_t)pbIn[owned].item<int64_t>() : 0;
@@ -145,7 +146,10 @@ std::tuple<at::Tensor, at::Tensor> opLocalPartition(const at::Tensor &values, co
   at::Tensor itemHist = at::empty({std::max<int64_t>(1, (int64_t)nItems * F)}, like(values, at::kInt));
   at::Tensor itemCursors = at::empty({std::max<int64_t>(1, (int64_t)nItems * F)}, like(values));
   if (values.is_cuda()) {
-    at::Tensor dItems = at::empty({std::max<int64_t>(1, (int64_t)nItems * 2)}, like(values));
+    const uint32_t streams = kernels::assignLocalStreams(items.data(), nItems);
+    const bool narrow = kernels::cursorsNarrow(values.size(0));
+    at::Tensor gcur = at::empty({std::max<int64_t>(1, (int64_t)streams * F)}, like(values));
+    at::Tensor dItems = at::empty({std::max<int64_t>(1, (int64_t)nItems * 3)}, like(values));
     at::Tensor dLb = at::empty({(int64_t)owned + 1}, like(values, at::kInt));
     at::Tensor dBase = at::empty({(int64_t)owned + 1}, like(values));
     HIP_CHECK(hipMemcpy(dItems.data_ptr(), items.data(), nItems * sizeof(kernels::LocalItem), hipMemcpyHostToDevice));
@@ -154,10 +158,10 @@ std::tuple<at::Tensor, at::Tensor> opLocalPartition(const at::Tensor &values, co
     const auto *di = ptr<const kernels::LocalItem>(dItems);
     kernels::localHistogram(values.data_ptr(), wide, di, nItems, (uint32_t)shift, (uint32_t)bits, ptr<uint32_t>(itemHist),
                             nullptr);
-    kernels::localCursors(ptr<uint32_t>(itemHist), ptr<uint32_t>(dLb), owned, (uint32_t)bits, ptr<uint64_t>(dBase),
-                          ptr<uint64_t>(itemCursors), ptr<uint64_t>(partBegin), nullptr);
-    kernels::localScatter(values.data_ptr(), wide, di, nItems, (uint32_t)shift, (uint32_t)bits,
-                          ptr<uint64_t>(itemCursors), out.data_ptr(), nullptr);
+    kernels::localCursors(ptr<uint32_t>(itemHist), ptr<uint32_t>(dLb), owned, (uint32_t)bits, ptr<uint64_t>(dBase), di,
+                          gcur.data_ptr(), narrow, ptr<uint64_t>(partBegin), nullptr);
+    kernels::localScatter(values.data_ptr(), wide, di, nItems, (uint32_t)shift, (uint32_t)bits, gcur.data_ptr(), narrow,
+                          out.data_ptr(), nullptr);
     HIP_CHECK(hipDeviceSynchronize());
   } else {
     host::localHistogram(values.data_ptr(), wide, items.data(), nItems, (uint32_t)shift, (uint32_t)bits,
@@ -313,6 +317,48 @@ double timeDevice(const std::function<void(hipStream_t)> &fn, int iters) {
   return ms[ms.size() / 2];
 }
 
+// Times the network scatter kernel alone (cursors precomputed) in one of the
+// ablation modes; returns ms per call.
+double benchScatter(const at::Tensor &tuples, int64_t bits, int64_t mode, int iters, int64_t maxBlocks,
+                    int64_t geometry) {
+  checkTuples(tuples, "tuples");
+  setDevice(tuples);
+  const uint64_t n = tuples.size(0);
+  const uint32_t F = 1u << bits;
+  const auto g = kernels::partitionGeometry(n, (uint32_t)maxBlocks);
+  at::Tensor blockHist = at::empty({(int64_t)F * g.blocks}, like(tuples, at::kInt));
+  at::Tensor totals = at::empty({(int64_t)F}, like(tuples));
+  at::Tensor cursors = at::empty({(int64_t)F * g.blocks}, like(tuples));
+  at::Tensor out = at::empty({(int64_t)n}, like(tuples));
+  kernels::netHistogram(ptr<data::Tuple>(tuples), n, bits, g, ptr<uint32_t>(blockHist), nullptr);
+  kernels::digitTotals(ptr<uint32_t>(blockHist), F, g.blocks, g.blocks, 1, ptr<uint64_t>(totals), nullptr);
+  at::Tensor base = (at::cumsum(totals, 0) - totals).contiguous();
+  kernels::netCursors(ptr<uint32_t>(blockHist), F, g.blocks, g.blocks, ptr<uint64_t>(base), ptr<uint64_t>(cursors),
+                      nullptr);
+  at::Tensor gcur32 = at::empty({8 * (int64_t)F}, like(tuples, at::kInt));
+  kernels::netGroupCursors(ptr<uint32_t>(blockHist), F, g.blocks, g.blocks, ptr<uint64_t>(base), gcur32.data_ptr(),
+                           true, nullptr);
+  at::Tensor work = gcur32.clone();
+  HIP_CHECK(hipDeviceSynchronize());
+  return timeDevice(
+      [&](hipStream_t s) {
+        HIP_CHECK(hipMemcpyAsync(work.data_ptr(), gcur32.data_ptr(), 8 * F * 4, hipMemcpyDeviceToDevice, s));
+        kernels::scatterAblation(ptr<data::Tuple>(tuples), n, bits, 32, g, ptr<uint64_t>(cursors), ptr<uint64_t>(out),
+                                 (int)mode, (int)geometry, s, work.data_ptr());
+      },
+      iters);
+}
+
+double benchHistogram(const at::Tensor &tuples, int64_t bits, int iters) {
+  setDevice(tuples);
+  const uint64_t n = tuples.size(0);
+  const auto g = kernels::partitionGeometry(n, 2048);
+  at::Tensor blockHist = at::empty({(int64_t)(1u << bits) * g.blocks}, like(tuples, at::kInt));
+  return timeDevice(
+      [&](hipStream_t s) { kernels::netHistogram(ptr<data::Tuple>(tuples), n, bits, g, ptr<uint32_t>(blockHist), s); },
+      iters);
+}
+
 double benchCopy(const at::Tensor &src, const at::Tensor &dst, int iters) {
   setDevice(src);
   const uint64_t n16 = src.numel() * src.element_size() / 16;
@@ -412,6 +458,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("local_bits", &core::JoinPlan::localBits)
       .def_readonly("key_shift", &core::JoinPlan::keyShift)
       .def_readonly("frag_shift", &core::JoinPlan::fragShift)
+      .def_readonly("key_bits", &core::JoinPlan::keyBits)
       .def_readonly("r_chunk", &core::JoinPlan::rChunk)
       .def_readonly("s_chunk", &core::JoinPlan::sChunk)
       .def_readonly("chunks", &core::JoinPlan::chunks)
@@ -611,7 +658,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   auto ops = m.def_submodule("ops", "kernel-level entry points on torch tensors (device or host)");
   ops.def("net_histogram", &opNetHistogram, py::arg("tuples"), py::arg("bits"), py::arg("max_blocks") = 2048);
   ops.def("net_partition", &opNetPartition, py::arg("tuples"), py::arg("bits"), py::arg("key_shift") = 32,
-          py::arg("wide") = false, py::arg("max_blocks") = 2048);
+          py::arg("wide") = false, py::arg("max_blocks") = 2048, py::arg("key_bits") = 64);
   ops.def("local_partition", &opLocalPartition, py::arg("values"), py::arg("part_begin"), py::arg("shift"),
           py::arg("bits"), py::arg("wide") = false);
   ops.def("build_probe", &opBuildProbe, py::arg("R"), py::arg("S"), py::arg("part_r"), py::arg("part_s"),
@@ -624,5 +671,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   ops.def("net_scatter_global_atomic", &opNetScatterGlobalAtomic);
   ops.def("bench_copy_ms", &benchCopy, py::arg("src"), py::arg("dst"), py::arg("iters") = 10);
   ops.def("bench_read_ms", &benchRead, py::arg("src"), py::arg("iters") = 10);
+  ops.def("bench_scatter_ms", &benchScatter, py::arg("tuples"), py::arg("bits"), py::arg("mode") = 0,
+          py::arg("iters") = 10, py::arg("max_blocks") = 2048, py::arg("geometry") = 0);
+  ops.def("bench_histogram_ms", &benchHistogram, py::arg("tuples"), py::arg("bits"), py::arg("iters") = 10);
   ops.def("partition_tile", []() { return kernels::PART_TILE; });
 }

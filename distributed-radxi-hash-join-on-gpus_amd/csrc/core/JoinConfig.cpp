@@ -59,8 +59,9 @@ JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t global
               "networkBits=%u out of range", p.networkBits);
   JOIN_ASSERT(p.localBits <= Configuration::GPU_MAX_FANOUT_BITS, "Plan", "localBits=%u out of range", p.localBits);
 
-  const uint32_t ridBits = ceilLog2(maxRid + 1);
-  const uint32_t keyBits = ceilLog2(maxKey + 1);
+  const uint32_t ridBits = maxRid == ~0ull ? 64 : ceilLog2(maxRid + 1);
+  const uint32_t keyBits = maxKey == ~0ull ? 64 : ceilLog2(maxKey + 1);
+  p.keyBits = keyBits;
   if (p.wide) {
     p.keyShift = 64;
     p.fragShift = 64;

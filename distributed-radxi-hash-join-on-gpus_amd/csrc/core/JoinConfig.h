@@ -48,6 +48,7 @@ struct JoinPlan {
   uint32_t localBits = 0;
   uint32_t keyShift = 32;
   uint32_t fragShift = 32;    // compressed: key fragment shift after both passes
+  uint32_t keyBits = 64;      // bits of the largest key over both relations
   uint32_t rChunk = 4096;
   uint32_t sChunk = 65536;
   uint32_t chunks = 1;

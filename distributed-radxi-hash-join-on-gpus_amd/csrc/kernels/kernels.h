@@ -39,7 +39,6 @@ struct PartitionGeometry {
 // contiguous run of tiles so its per-digit output runs stay contiguous.
 PartitionGeometry partitionGeometry(uint64_t n, uint32_t maxBlocks = 2048);
 
-size_t netScatterLdsBytes(uint32_t bits, bool wide);
 
 // ----------------------------------------------------------------- datagen
 enum class KeyDistribution : int { Unique = 0, Modulo = 1, Uniform = 2, Zipf = 3, Dense = 4 };
@@ -68,12 +67,36 @@ void digitTotals(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint32_
 void netCursors(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint32_t blocksPerChunk,
                 const uint64_t *base, uint64_t *cursors, hipStream_t s);
 // Compressed (8 B) and wide (16 B, full-range keys) scatter into the send buffer.
-// Scatters the tiles of workgroups [blockBegin, blockEnd) (one exchange chunk).
+// Group ("claim") cursors: workgroups are split into NGROUPS groups by
+// blockIdx % NGROUPS (the XCD round-robin: a speed assumption only); every
+// group owns a slice of every digit's region and claims runs from it with
+// one device atomic per digit per tile, so the workgroups of an XCD append to
+// ONE stream per digit and output lines fill inside that XCD's L2.
+constexpr uint32_t CLAIM_GROUPS = 8;
+// 32-bit cursors whenever every output position fits (half the atomics' bytes).
+inline bool cursorsNarrow(uint64_t outSize) { return outSize < (1ull << 32); }
+// gcur[c][g][d] (u32 if narrow else u64): start of group g's slice of digit d in chunk c.
+void netGroupCursors(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint32_t blocksPerChunk,
+                     const uint64_t *base, void *gcur, bool narrow, hipStream_t s);
+// Scatters the tiles of workgroups [blockBegin, blockEnd) (one exchange chunk)
+// claiming from that chunk's gcur[g][d] (narrow = cursorsNarrow(n)).
+// keyBits: bits of the largest key (lets the kernel carry the digit in the
+// packed word's spare top bits instead of a separate LDS array).
 void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift, const PartitionGeometry &g,
-                uint32_t blockBegin, uint32_t blockEnd, const uint64_t *cursors, uint64_t *out, hipStream_t s);
+                uint32_t blockBegin, uint32_t blockEnd, void *gcur, uint64_t *out, hipStream_t s,
+                uint32_t keyBits = 64);
 void netScatterWide(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
-                    uint32_t blockBegin, uint32_t blockEnd, const uint64_t *cursors, data::Tuple *out,
-                    hipStream_t s);
+                    uint32_t blockBegin, uint32_t blockEnd, void *gcur, data::Tuple *out, hipStream_t s);
+// Ablation entry (micro-benchmarks): mode 0 = real scatter, 1 = coalesced
+// write-out, 2 = no write-out; 32-bit cursors, compressed output.
+// geometry: 0 = 256x16 (default), 1 = 512x16, 2 = 1024x8, 3 = 1024x16,
+// 4 = 256x16 with a separate LDS digit array, 5 = 256x8.
+// geometries 6..9 = claim mode (256x16, 512x16, 1024x16, 1024x8) using gcur
+// (u32 group cursors [8][F], re-initialised by the caller before each call).
+void scatterAblation(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift, const PartitionGeometry &g,
+                     const uint64_t *cursors, uint64_t *out, int mode, int geometry, hipStream_t s,
+                     void *gcur = nullptr);
+
 // Ablation baseline: one global atomic per tuple, no LDS staging
 // (reference histogram_build_global / reorder_global, kernels.cu:256-298).
 void netScatterGlobalAtomic(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift,
@@ -86,7 +109,12 @@ struct LocalItem {
   uint64_t begin;
   uint32_t len;
   uint32_t lp;
+  uint32_t stream;  // claim stream (assignLocalStreams), device path only
+  uint32_t pad;
 };
+// Assigns claim streams (one per (lp, XCD group) run of the lp-sorted items);
+// returns the number of streams.
+uint32_t assignLocalStreams(LocalItem *items, uint32_t nItems);
 constexpr uint32_t LOCAL_ITEM_TILES = 16;
 constexpr uint32_t LOCAL_ITEM_MAX = LOCAL_ITEM_TILES * PART_TILE;  // 65536
 
@@ -94,10 +122,12 @@ constexpr uint32_t LOCAL_ITEM_MAX = LOCAL_ITEM_TILES * PART_TILE;  // 65536
 // shift = keyShift; for wide tuples word = key, shift = networkBits.
 void localHistogram(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift,
                     uint32_t bits, uint32_t *itemHist, hipStream_t s);
+// gcur[stream][F] (u32 if narrow else u64) claim slices + partBegin[owned*F+1].
 void localCursors(const uint32_t *itemHist, const uint32_t *lpItemBegin, uint32_t owned, uint32_t bits,
-                  const uint64_t *lpBase, uint64_t *itemCursors, uint64_t *partBegin, hipStream_t s);
+                  const uint64_t *lpBase, const LocalItem *items, void *gcur, bool narrow, uint64_t *partBegin,
+                  hipStream_t s);
 void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift,
-                  uint32_t bits, const uint64_t *itemCursors, void *out, hipStream_t s);
+                  uint32_t bits, void *gcur, bool narrow, void *out, hipStream_t s);
 
 // --------------------------------------------------------------- build/probe
 struct BPItem {

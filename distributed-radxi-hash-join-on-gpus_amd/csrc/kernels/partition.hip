@@ -28,6 +28,7 @@ namespace hpcjoin {
 namespace kernels {
 
 constexpr int NT = PART_THREADS;
+constexpr uint32_t NGROUPS = 8;  // XCDs on MI355X
 
 PartitionGeometry partitionGeometry(uint64_t n, uint32_t maxBlocks) {
   PartitionGeometry g;
@@ -42,22 +43,23 @@ PartitionGeometry partitionGeometry(uint64_t n, uint32_t maxBlocks) {
   return g;
 }
 
-static size_t scatterLds(uint32_t F, size_t outBytes) {
-  return size_t(F) * 16 + 64 + size_t(PART_TILE) * outBytes + size_t(PART_TILE) * 2;
-}
-
-size_t netScatterLdsBytes(uint32_t bits, bool wide) { return scatterLds(1u << bits, wide ? 16 : 8); }
 
 // ------------------------------------------------------------------ loads
+// Input streams are read exactly once: non-temporal loads keep them from
+// evicting the partially filled output lines the L2 is write-combining.
+using u64x2 = unsigned long long __attribute__((ext_vector_type(2)));
 template <typename InT>
 struct Loader;
 template <>
 struct Loader<ulonglong2> {
-  static __device__ __forceinline__ ulonglong2 load(const ulonglong2 *p) { return *p; }
+  static __device__ __forceinline__ ulonglong2 load(const ulonglong2 *p) {
+    const u64x2 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(p));
+    return make_ulonglong2(v.x, v.y);
+  }
 };
 template <>
 struct Loader<uint64_t> {
-  static __device__ __forceinline__ uint64_t load(const uint64_t *p) { return *p; }
+  static __device__ __forceinline__ uint64_t load(const uint64_t *p) { return __builtin_nontemporal_load(p); }
 };
 
 // ------------------------------------------------------- histogram (pass 1)
@@ -158,138 +160,436 @@ void netCursors(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint32_t
   HIP_CHECK_LAUNCH();
 }
 
+// Group cursors for claim-mode scatter: the workgroups of a chunk are split
+// into NGROUPS groups by (block - chunkBegin) % NGROUPS, which is the XCD
+// round-robin of the dispatcher (a speed assumption only).  Each group owns a
+// contiguous slice of every digit's region, sized by the group's histogram,
+// and its workgroups claim space from the slice with one device atomic per
+// digit per tile.  gcur[c][g][d] = base[c][d] + sum of the earlier groups.
+template <typename CurT>
+__global__ __launch_bounds__(NT) void netGroupCursorsKernel(const uint32_t *__restrict__ blockHist, uint32_t F,
+                                                            uint32_t blocks, uint32_t bpc, const uint64_t *base,
+                                                            CurT *gcur) {
+  __shared__ unsigned long long gs[NGROUPS];
+  const uint32_t d = blockIdx.x;
+  const uint32_t chunks = (blocks + bpc - 1) / bpc;
+  for (uint32_t c = 0; c < chunks; ++c) {
+    if (threadIdx.x < NGROUPS) gs[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t b0 = c * bpc, b1 = min(blocks, b0 + bpc);
+    unsigned long long mine = 0;  // NT % NGROUPS == 0: thread t only sees group t % NGROUPS
+    for (uint32_t b = b0 + threadIdx.x; b < b1; b += NT) mine += blockHist[(uint64_t)d * blocks + b];
+    atomicAdd(&gs[threadIdx.x % NGROUPS], mine);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long run = base[(uint64_t)c * F + d];
+      for (uint32_t g = 0; g < NGROUPS; ++g) {
+        gcur[((uint64_t)c * NGROUPS + g) * F + d] = (CurT)run;
+        run += gs[g];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+void netGroupCursors(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint32_t blocksPerChunk,
+                     const uint64_t *base, void *gcur, bool narrow, hipStream_t s) {
+  if (narrow)
+    hipLaunchKernelGGL(netGroupCursorsKernel<uint32_t>, dim3(F), dim3(NT), 0, s, blockHist, F, blocks, blocksPerChunk,
+                       base, reinterpret_cast<uint32_t *>(gcur));
+  else
+    hipLaunchKernelGGL(netGroupCursorsKernel<unsigned long long>, dim3(F), dim3(NT), 0, s, blockHist, F, blocks,
+                       blocksPerChunk, base, reinterpret_cast<unsigned long long *>(gcur));
+  HIP_CHECK_LAUNCH();
+}
+
 // -------------------------------------------------- LDS write-combining scatter
-struct ScatterLds {
-  uint64_t *cursor;  // [F]
-  uint32_t *cnt;     // [F]
-  uint32_t *off;     // [F]
-  uint32_t *wave;    // [16]
-  void *val;         // [TILE] of OutT
-  uint16_t *dig;     // [TILE]
+// A scatter policy says how a tuple is ranked (digit), what is staged in LDS
+// (the packed output word, possibly carrying its digit in spare top bits),
+// how the digit is recovered from the staged word and what is finally
+// written.  Only the compressed network pass may need a separate LDS digit
+// array: the local pass and wide tuples recompute the digit from the staged
+// word, and compressed words carry it in their top bits whenever the key
+// range leaves `bits` spare bits (JoinPlan knows; the 1B config does).
+struct NetCompressedPol {  // 16 B tuple -> 8 B CompressedTuple, digit in the top bits
+  using InT = ulonglong2;
+  using StageT = uint64_t;
+  using OutT = uint64_t;
+  static constexpr bool kDigArray = false;
+  uint64_t mask;
+  uint32_t bits, keyShift;
+  __device__ __forceinline__ uint32_t digit(const InT &x) const { return (uint32_t)(x.x & mask); }
+  __device__ __forceinline__ StageT stage(const InT &x, uint32_t d) const {
+    return x.y | ((x.x >> bits) << keyShift) | ((uint64_t)d << (64 - bits));
+  }
+  __device__ __forceinline__ uint32_t stagedDigit(const StageT &v) const { return (uint32_t)(v >> (64 - bits)); }
+  __device__ __forceinline__ OutT out(const StageT &v) const { return v & (~0ull >> bits); }
+};
+struct NetCompressedDigPol : NetCompressedPol {  // no spare bits: digits staged separately
+  static constexpr bool kDigArray = true;
+  __device__ __forceinline__ StageT stage(const InT &x, uint32_t) const { return x.y | ((x.x >> bits) << keyShift); }
+  __device__ __forceinline__ OutT out(const StageT &v) const { return v; }
+};
+struct NetWidePol {  // 16 B tuple -> 16 B tuple (full-range keys)
+  using InT = ulonglong2;
+  using StageT = ulonglong2;
+  using OutT = ulonglong2;
+  static constexpr bool kDigArray = false;
+  uint64_t mask;
+  __device__ __forceinline__ uint32_t digit(const InT &x) const { return (uint32_t)(x.x & mask); }
+  __device__ __forceinline__ StageT stage(const InT &x, uint32_t) const { return x; }
+  __device__ __forceinline__ uint32_t stagedDigit(const StageT &v) const { return (uint32_t)(v.x & mask); }
+  __device__ __forceinline__ OutT out(const StageT &v) const { return v; }
+};
+struct LocalCompressedPol {  // 8 B -> 8 B, digit = (value >> shift) & mask
+  using InT = uint64_t;
+  using StageT = uint64_t;
+  using OutT = uint64_t;
+  static constexpr bool kDigArray = false;
+  uint64_t mask;
+  uint32_t shift;
+  __device__ __forceinline__ uint32_t digit(const InT &x) const { return (uint32_t)((x >> shift) & mask); }
+  __device__ __forceinline__ StageT stage(const InT &x, uint32_t) const { return x; }
+  __device__ __forceinline__ uint32_t stagedDigit(const StageT &v) const { return digit(v); }
+  __device__ __forceinline__ OutT out(const StageT &v) const { return v; }
+};
+struct LocalWidePol {  // 16 B -> 16 B, digit = (key >> shift) & mask
+  using InT = ulonglong2;
+  using StageT = ulonglong2;
+  using OutT = ulonglong2;
+  static constexpr bool kDigArray = false;
+  uint64_t mask;
+  uint32_t shift;
+  __device__ __forceinline__ uint32_t digit(const InT &x) const { return (uint32_t)((x.x >> shift) & mask); }
+  __device__ __forceinline__ StageT stage(const InT &x, uint32_t) const { return x; }
+  __device__ __forceinline__ uint32_t stagedDigit(const StageT &v) const { return digit(v); }
+  __device__ __forceinline__ OutT out(const StageT &v) const { return v; }
 };
 
-template <typename OutT>
-__device__ __forceinline__ ScatterLds carveScatterLds(unsigned char *smem, uint32_t F) {
-  ScatterLds l;
-  l.cursor = reinterpret_cast<uint64_t *>(smem);
-  l.cnt = reinterpret_cast<uint32_t *>(l.cursor + F);
-  l.off = l.cnt + F;
-  l.wave = l.off + F;
-  l.val = reinterpret_cast<void *>(l.wave + 16);
-  l.dig = reinterpret_cast<uint16_t *>(reinterpret_cast<OutT *>(l.val) + PART_TILE);
-  return l;
+// LDS per workgroup: cursor and wbase (F x CurT), cnt and off (F x u32), scan
+// scratch, the reordered tile (TILE x StageT) and, only for
+// NetCompressedDigPol, the tile's digits (TILE x u16).  At F = 1024 with
+// 32-bit cursors and 8-byte words: 16 KiB + 32 KiB -> three 256-thread
+// workgroups (12 wave64s) per CU.
+template <class Pol, typename CurT, int TILE>
+struct ScatterLayout {
+  static __host__ __device__ constexpr size_t valOffset(uint32_t F) {
+    return ((size_t)F * (2 * sizeof(CurT) + 8) + 64 + 15) & ~size_t(15);
+  }
+  static __host__ __device__ constexpr size_t bytes(uint32_t F) {
+    return valOffset(F) + (size_t)TILE * sizeof(typename Pol::StageT) + (Pol::kDigArray ? (size_t)TILE * 2 : 0);
+  }
+};
+
+// Per-workgroup LDS carve of the scatter (see ScatterLayout).
+template <class Pol, typename CurT, int TILE>
+struct ScatterSmem {
+  CurT *cursor, *wbase;
+  uint32_t *cnt, *off, *wave;
+  typename Pol::StageT *val;
+  uint16_t *dig;
+  __device__ __forceinline__ ScatterSmem(unsigned char *smem, uint32_t F) {
+    cursor = reinterpret_cast<CurT *>(smem);
+    wbase = cursor + F;
+    cnt = reinterpret_cast<uint32_t *>(wbase + F);
+    off = cnt + F;
+    wave = off + F;
+    val = reinterpret_cast<typename Pol::StageT *>(smem + ScatterLayout<Pol, CurT, TILE>::valOffset(F));
+    dig = reinterpret_cast<uint16_t *>(val + TILE);
+  }
+};
+
+template <class Pol, int NTH, int IPT, bool FULL>
+__device__ __forceinline__ void loadTile(const typename Pol::InT *__restrict__ src, uint32_t count,
+                                         typename Pol::InT (&v)[IPT]) {
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    const uint32_t idx = i * NTH + threadIdx.x;
+    if (FULL || idx < count) v[i] = Loader<typename Pol::InT>::load(src + idx);
+  }
 }
 
-// Scatter [begin, end) of `in` into `out` at the cursors held in l.cursor
-// (initialised by the caller, advanced here).  DigitFn(InT) -> digit,
-// PackFn(InT) -> OutT.
-template <typename InT, typename OutT, typename DigitFn, typename PackFn>
-__device__ __forceinline__ void scatterRange(const InT *__restrict__ in, uint64_t begin, uint64_t end, uint32_t F,
-                                             const ScatterLds &l, OutT *__restrict__ out, DigitFn digitOf,
-                                             PackFn pack) {
-  OutT *sVal = reinterpret_cast<OutT *>(l.val);
+// One tile.  FULL tiles (every tile but a range's tail) are branch-free so
+// hipcc can keep all IPT LDS atomics, loads and stores in flight with counted
+// waits; the predicated tail path is only taken once per range.
+template <class Pol, typename CurT, int NTH, int IPT, int MODE, bool FULL, bool CLAIM>
+__device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict__ in, uint64_t base, uint64_t end,
+                                            uint32_t count, uint32_t F, const ScatterSmem<Pol, CurT, NTH * IPT> &l,
+                                            const Pol &pol, typename Pol::OutT *__restrict__ out,
+                                            typename Pol::InT (&v)[IPT], CurT *__restrict__ gcur) {
+  constexpr uint32_t TILE = NTH * IPT;
   const uint32_t t = threadIdx.x;
-  for (uint64_t base = begin; base < end; base += PART_TILE) {
-    const uint32_t cnt = (uint32_t)min((uint64_t)PART_TILE, end - base);
-    InT v[PART_ITEMS];
+  uint32_t dr[IPT];
 #pragma unroll
-    for (int i = 0; i < (int)PART_ITEMS; ++i) {
-      const uint32_t idx = i * NT + t;
-      if (idx < cnt) v[i] = Loader<InT>::load(in + base + idx);
+  for (int i = 0; i < IPT; ++i) {
+    const uint32_t idx = i * NTH + t;
+    if (FULL || idx < count) {
+      const uint32_t d = pol.digit(v[i]);
+      dr[i] = (d << 16) | atomicAdd(&l.cnt[d], 1u);
     }
-    uint32_t dr[PART_ITEMS];
+  }
+  __syncthreads();  // A: counts final; previous tile's write-out done
+  blockExclusiveScanLds<NTH, uint32_t, uint32_t>(l.cnt, l.off, (int)F, l.wave);
+  constexpr int MAXD = (1 << MAX_PART_BITS) / NTH > 0 ? (1 << MAX_PART_BITS) / NTH : 1;
+  CurT claim[MAXD];
+  if constexpr (CLAIM) {
+    // One device atomic per digit claims this tile's run in the group's slice.
 #pragma unroll
-    for (int i = 0; i < (int)PART_ITEMS; ++i) {
-      const uint32_t idx = i * NT + t;
-      if (idx < cnt) {
-        const uint32_t d = digitOf(v[i]);
-        const uint32_t r = atomicAdd(&l.cnt[d], 1u);
-        dr[i] = (d << 16) | r;
-      }
+    for (int k = 0; k < MAXD; ++k) {
+      const uint32_t d = t + k * NTH;
+      if (d < F) claim[k] = atomicAdd(&gcur[d], (CurT)l.cnt[d]);
     }
-    __syncthreads();
-    blockExclusiveScanLds<NT, uint32_t, uint32_t>(l.cnt, l.off, (int)F, l.wave);
-#pragma unroll
-    for (int i = 0; i < (int)PART_ITEMS; ++i) {
-      const uint32_t idx = i * NT + t;
-      if (idx < cnt) {
-        const uint32_t d = dr[i] >> 16;
-        const uint32_t pos = l.off[d] + (dr[i] & 0xFFFFu);
-        sVal[pos] = pack(v[i]);
-        l.dig[pos] = (uint16_t)d;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < (int)PART_ITEMS; ++i) {
-      const uint32_t idx = i * NT + t;
-      if (idx < cnt) {
-        const uint32_t d = l.dig[idx];
-        out[l.cursor[d] + (idx - l.off[d])] = sVal[idx];
-      }
-    }
-    __syncthreads();
-    for (uint32_t d = t; d < F; d += NT) {
-      l.cursor[d] += l.cnt[d];
+  } else {
+    for (uint32_t d = t; d < F; d += NTH) {
+      const CurT c = l.cursor[d];
+      l.wbase[d] = c - (CurT)l.off[d];  // wraps; wbase + idx lands back in range
+      l.cursor[d] = c + (CurT)l.cnt[d];
       l.cnt[d] = 0;
     }
-    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    const uint32_t idx = i * NTH + t;
+    if (FULL || idx < count) {
+      const uint32_t d = dr[i] >> 16;
+      const uint32_t pos = l.off[d] + (dr[i] & 0xFFFFu);
+      l.val[pos] = pol.stage(v[i], d);
+      if constexpr (Pol::kDigArray) l.dig[pos] = (uint16_t)d;
+    }
+  }
+  // Prefetch the next tile while this one is streamed out.
+  const uint64_t nbase = base + TILE;
+  if (nbase + TILE <= end)
+    loadTile<Pol, NTH, IPT, true>(in + nbase, TILE, v);
+  else if (nbase < end)
+    loadTile<Pol, NTH, IPT, false>(in + nbase, (uint32_t)(end - nbase), v);
+  if constexpr (CLAIM) {
+#pragma unroll
+    for (int k = 0; k < MAXD; ++k) {
+      const uint32_t d = t + k * NTH;
+      if (d < F) {
+        l.wbase[d] = claim[k] - (CurT)l.off[d];
+        l.cnt[d] = 0;
+      }
+    }
+  }
+  __syncthreads();  // B: staged tile and write bases visible
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    const uint32_t idx = i * NTH + t;
+    if (FULL || idx < count) {
+      const typename Pol::StageT x = l.val[idx];
+      uint32_t d;
+      if constexpr (Pol::kDigArray)
+        d = l.dig[idx];
+      else
+        d = pol.stagedDigit(x);
+      if constexpr (MODE == 0) {
+        out[(uint64_t)(CurT)(l.wbase[d] + (CurT)idx)] = pol.out(x);
+      } else if constexpr (MODE == 1) {
+        out[base + idx] = pol.out(x);
+        asm volatile("" ::"v"(l.wbase[d]));
+      } else {
+        const auto y = pol.out(x);
+        asm volatile("" ::"v"(y), "v"(l.wbase[d]));
+      }
+    }
   }
 }
 
-template <bool WIDE>
-__global__ __launch_bounds__(NT) void netScatterKernel(const ulonglong2 *__restrict__ in, uint64_t n, uint32_t tpb,
-                                                       uint32_t bits, uint32_t keyShift, uint32_t totalBlocks,
-                                                       uint32_t blockBegin, const uint64_t *__restrict__ cursors,
-                                                       void *out) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  using OutT = typename std::conditional<WIDE, ulonglong2, uint64_t>::type;
-  const uint32_t F = 1u << bits;
-  const uint64_t mask = F - 1;
-  const uint32_t blk = blockBegin + blockIdx.x;
-  ScatterLds l = carveScatterLds<OutT>(smem, F);
-  for (uint32_t d = threadIdx.x; d < F; d += NT) {
-    l.cursor[d] = cursors[(uint64_t)d * totalBlocks + blk];
-    l.cnt[d] = 0;
+// Scatter [begin, end) of `in` into `out` at the cursors held in LDS
+// (initialised by the caller, advanced here).  Per tile:
+//   rank (LDS atomics) | A | scan + per-digit write base | stage into LDS,
+//   prefetch next tile into registers | B | stream the reordered tile out.
+// MODE (ablation only): 0 = real scatter, 1 = coalesced write-out, 2 = none.
+template <class Pol, typename CurT, int NTH, int IPT, int MODE, bool CLAIM = false>
+__device__ __forceinline__ void scatterRange(const typename Pol::InT *__restrict__ in, uint64_t begin, uint64_t end,
+                                             uint32_t F, unsigned char *smem, const Pol &pol,
+                                             typename Pol::OutT *__restrict__ out, CurT *gcur = nullptr) {
+  constexpr uint32_t TILE = NTH * IPT;
+  const ScatterSmem<Pol, CurT, TILE> l(smem, F);
+  typename Pol::InT v[IPT];
+  if (begin + TILE <= end)
+    loadTile<Pol, NTH, IPT, true>(in + begin, TILE, v);
+  else if (begin < end)
+    loadTile<Pol, NTH, IPT, false>(in + begin, (uint32_t)(end - begin), v);
+  for (uint64_t base = begin; base < end; base += TILE) {
+    if (base + TILE <= end)
+      scatterTile<Pol, CurT, NTH, IPT, MODE, true, CLAIM>(in, base, end, TILE, F, l, pol, out, v, gcur);
+    else
+      scatterTile<Pol, CurT, NTH, IPT, MODE, false, CLAIM>(in, base, end, (uint32_t)(end - base), F, l, pol, out, v,
+                                                           gcur);
   }
+  __syncthreads();
+}
+
+// Occupancy target per geometry: 256-thread groups aim at 3 per CU (LDS-bound),
+// 512 at 2, 1024 at 1 (second launch-bounds argument = waves per SIMD).
+template <int NTH>
+struct ScatterOcc {
+  static constexpr int value = NTH == 256 ? 3 : (NTH == 512 ? 4 : 4);
+};
+
+template <class Pol, typename CurT, int NTH, int IPT, int MODE>
+__global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void netScatterKernel(
+    const typename Pol::InT *__restrict__ in, uint64_t n, uint32_t tpb, uint32_t F, Pol pol, uint32_t totalBlocks,
+    uint32_t blockBegin, const uint64_t *__restrict__ cursors, typename Pol::OutT *out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr uint32_t TILE = NTH * IPT;
+  const uint32_t blk = blockBegin + blockIdx.x;
+  CurT *cursor = reinterpret_cast<CurT *>(smem);
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(cursor + 2 * F);
+  for (uint32_t d = threadIdx.x; d < F; d += NTH) {
+    cursor[d] = (CurT)cursors[(uint64_t)d * totalBlocks + blk];
+    cnt[d] = 0;
+  }
+  __syncthreads();
+  const uint64_t begin = (uint64_t)blk * tpb * PART_TILE;  // geometry is in PART_TILE units
+  const uint64_t end = min(n, begin + (uint64_t)tpb * PART_TILE);
+  (void)TILE;
+  scatterRange<Pol, CurT, NTH, IPT, MODE>(in, begin, end, F, smem, pol, out);
+}
+
+// Claim-mode network scatter: cursors come from the group slices (gcur is
+// [NGROUPS][F] for this chunk), so no per-workgroup cursor array is loaded.
+template <class Pol, typename CurT, int NTH, int IPT, int MODE>
+__global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void netScatterClaimKernel(
+    const typename Pol::InT *__restrict__ in, uint64_t n, uint32_t tpb, uint32_t F, Pol pol, uint32_t blockBegin,
+    CurT *__restrict__ gcur, typename Pol::OutT *out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t blk = blockBegin + blockIdx.x;
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(reinterpret_cast<CurT *>(smem) + 2 * F);
+  for (uint32_t d = threadIdx.x; d < F; d += NTH) cnt[d] = 0;
   __syncthreads();
   const uint64_t begin = (uint64_t)blk * tpb * PART_TILE;
   const uint64_t end = min(n, begin + (uint64_t)tpb * PART_TILE);
-  auto digitOf = [mask](const ulonglong2 &x) -> uint32_t { return (uint32_t)(x.x & mask); };
-  if constexpr (WIDE) {
-    auto pack = [](const ulonglong2 &x) -> ulonglong2 { return x; };
-    scatterRange<ulonglong2, ulonglong2>(in, begin, end, F, l, reinterpret_cast<ulonglong2 *>(out), digitOf, pack);
+  scatterRange<Pol, CurT, NTH, IPT, MODE, true>(in, begin, end, F, smem, pol, out,
+                                                gcur + (size_t)(blockIdx.x % NGROUPS) * F);
+}
+
+// Default geometry (measured on MI355X, tools/microbench.py ablation).
+constexpr int SC_NTH = 256;
+constexpr int SC_IPT = 16;
+
+template <class Pol, typename CurT, int NTH = SC_NTH, int IPT = SC_IPT, int MODE = 0>
+static void launchNet(const Pol &pol, const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
+                      uint32_t blockBegin, uint32_t blockEnd, const uint64_t *cursors, void *out, hipStream_t s) {
+  const uint32_t F = 1u << bits;
+  const size_t lds = ScatterLayout<Pol, CurT, NTH * IPT>::bytes(F);
+  HJ_CHECK(lds <= 160 * 1024, "scatter LDS %zu too large", lds);
+  hipLaunchKernelGGL((netScatterKernel<Pol, CurT, NTH, IPT, MODE>), dim3(blockEnd - blockBegin), dim3(NTH), lds, s,
+                     reinterpret_cast<const typename Pol::InT *>(in), n, g.tilesPerBlock, F, pol, g.blocks,
+                     blockBegin, cursors, reinterpret_cast<typename Pol::OutT *>(out));
+  HIP_CHECK_LAUNCH();
+}
+
+// True when key >> bits, shifted to keyShift, leaves `bits` spare top bits.
+static bool digitFitsOnTop(uint32_t bits, uint32_t keyShift, uint32_t keyBits) {
+  const uint32_t high = keyBits > bits ? keyBits - bits : 0;
+  return keyShift + high + bits <= 64;
+}
+
+// Production geometry of the claim-mode scatter (tools/microbench.py
+// ablation on MI355X: 1024 threads x 8 tuples per LDS tile = 8192-tuple
+// tiles, one workgroup per CU).
+constexpr int CL_NTH = 1024;
+constexpr int CL_IPT = 8;
+
+template <class Pol>
+static void launchNetClaim(const Pol &pol, const data::Tuple *in, uint64_t n, uint32_t bits,
+                           const PartitionGeometry &g, uint32_t blockBegin, uint32_t blockEnd, void *gcur,
+                           void *out, hipStream_t s) {
+  const uint32_t F = 1u << bits;
+  const bool narrow = cursorsNarrow(n);
+  const auto *src = reinterpret_cast<const typename Pol::InT *>(in);
+  auto *dst = reinterpret_cast<typename Pol::OutT *>(out);
+  if (narrow) {
+    const size_t lds = ScatterLayout<Pol, uint32_t, CL_NTH * CL_IPT>::bytes(F);
+    HJ_CHECK(lds <= 160 * 1024, "scatter LDS %zu too large", lds);
+    hipLaunchKernelGGL((netScatterClaimKernel<Pol, uint32_t, CL_NTH, CL_IPT, 0>), dim3(blockEnd - blockBegin),
+                       dim3(CL_NTH), lds, s, src, n, g.tilesPerBlock, F, pol, blockBegin,
+                       reinterpret_cast<uint32_t *>(gcur), dst);
   } else {
-    auto pack = [bits, keyShift](const ulonglong2 &x) -> uint64_t { return x.y | ((x.x >> bits) << keyShift); };
-    scatterRange<ulonglong2, uint64_t>(in, begin, end, F, l, reinterpret_cast<uint64_t *>(out), digitOf, pack);
+    const size_t lds = ScatterLayout<Pol, unsigned long long, CL_NTH * CL_IPT>::bytes(F);
+    HJ_CHECK(lds <= 160 * 1024, "scatter LDS %zu too large", lds);
+    hipLaunchKernelGGL((netScatterClaimKernel<Pol, unsigned long long, CL_NTH, CL_IPT, 0>),
+                       dim3(blockEnd - blockBegin), dim3(CL_NTH), lds, s, src, n, g.tilesPerBlock, F, pol,
+                       blockBegin, reinterpret_cast<unsigned long long *>(gcur), dst);
   }
+  HIP_CHECK_LAUNCH();
 }
 
 void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift, const PartitionGeometry &g,
-                uint32_t blockBegin, uint32_t blockEnd, const uint64_t *cursors, uint64_t *out, hipStream_t s) {
+                uint32_t blockBegin, uint32_t blockEnd, void *gcur, uint64_t *out, hipStream_t s, uint32_t keyBits) {
   HJ_CHECK(bits >= 1 && bits <= MAX_PART_BITS, "netScatter: bits=%u out of range", bits);
   HJ_CHECK(blockBegin <= blockEnd && blockEnd <= g.blocks, "netScatter: block range [%u,%u) of %u", blockBegin,
            blockEnd, g.blocks);
   if (n == 0 || blockEnd == blockBegin) return;
-  const size_t lds = netScatterLdsBytes(bits, false);
-  hipLaunchKernelGGL(netScatterKernel<false>, dim3(blockEnd - blockBegin), dim3(NT), lds, s,
-                     reinterpret_cast<const ulonglong2 *>(in), n, g.tilesPerBlock, bits, keyShift, g.blocks,
-                     blockBegin, cursors, (void *)out);
-  HIP_CHECK_LAUNCH();
+  NetCompressedPol pol;
+  pol.mask = (1ull << bits) - 1;
+  pol.bits = bits;
+  pol.keyShift = keyShift;
+  if (digitFitsOnTop(bits, keyShift, keyBits)) {
+    launchNetClaim(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s);
+  } else {
+    NetCompressedDigPol dpol;
+    static_cast<NetCompressedPol &>(dpol) = pol;
+    launchNetClaim(dpol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s);
+  }
 }
 
 void netScatterWide(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
-                    uint32_t blockBegin, uint32_t blockEnd, const uint64_t *cursors, data::Tuple *out,
-                    hipStream_t s) {
+                    uint32_t blockBegin, uint32_t blockEnd, void *gcur, data::Tuple *out, hipStream_t s) {
   HJ_CHECK(bits >= 1 && bits <= MAX_PART_BITS, "netScatterWide: bits=%u out of range", bits);
   HJ_CHECK(blockBegin <= blockEnd && blockEnd <= g.blocks, "netScatterWide: block range [%u,%u) of %u",
            blockBegin, blockEnd, g.blocks);
   if (n == 0 || blockEnd == blockBegin) return;
-  const size_t lds = netScatterLdsBytes(bits, true);
-  hipLaunchKernelGGL(netScatterKernel<true>, dim3(blockEnd - blockBegin), dim3(NT), lds, s,
-                     reinterpret_cast<const ulonglong2 *>(in), n, g.tilesPerBlock, bits, 0u, g.blocks, blockBegin,
-                     cursors, (void *)out);
-  HIP_CHECK_LAUNCH();
+  NetWidePol pol;
+  pol.mask = (1ull << bits) - 1;
+  launchNetClaim(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s);
+}
+
+void scatterAblation(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift, const PartitionGeometry &g,
+                     const uint64_t *cursors, uint64_t *out, int mode, int geometry, hipStream_t s, void *gcur) {
+  NetCompressedPol pol;
+  pol.mask = (1ull << bits) - 1;
+  pol.bits = bits;
+  pol.keyShift = keyShift;
+  NetCompressedDigPol dpol;
+  static_cast<NetCompressedPol &>(dpol) = pol;
+#define HJ_CLAIM(NTH, IPT)                                                                                        \
+  do {                                                                                                            \
+    const size_t lds = ScatterLayout<NetCompressedPol, uint32_t, NTH * IPT>::bytes(1u << bits);                  \
+    auto *gc = reinterpret_cast<uint32_t *>(gcur);                                                                \
+    if (mode == 1)                                                                                                \
+      hipLaunchKernelGGL((netScatterClaimKernel<NetCompressedPol, uint32_t, NTH, IPT, 1>), dim3(g.blocks),        \
+                         dim3(NTH), lds, s, reinterpret_cast<const ulonglong2 *>(in), n, g.tilesPerBlock,         \
+                         1u << bits, pol, 0u, gc, out);                                                           \
+    else                                                                                                          \
+      hipLaunchKernelGGL((netScatterClaimKernel<NetCompressedPol, uint32_t, NTH, IPT, 0>), dim3(g.blocks),        \
+                         dim3(NTH), lds, s, reinterpret_cast<const ulonglong2 *>(in), n, g.tilesPerBlock,         \
+                         1u << bits, pol, 0u, gc, out);                                                           \
+  } while (0)
+#define HJ_ABL(P, p, NTH, IPT)                                                                                    \
+  do {                                                                                                            \
+    if (mode == 1) launchNet<P, uint32_t, NTH, IPT, 1>(p, in, n, bits, g, 0, g.blocks, cursors, out, s);          \
+    else if (mode == 2) launchNet<P, uint32_t, NTH, IPT, 2>(p, in, n, bits, g, 0, g.blocks, cursors, out, s);     \
+    else launchNet<P, uint32_t, NTH, IPT, 0>(p, in, n, bits, g, 0, g.blocks, cursors, out, s);                    \
+  } while (0)
+  switch (geometry) {
+    case 1: HJ_ABL(NetCompressedPol, pol, 512, 16); break;
+    case 2: HJ_ABL(NetCompressedPol, pol, 1024, 8); break;
+    case 3: HJ_ABL(NetCompressedPol, pol, 1024, 16); break;
+    case 4: HJ_ABL(NetCompressedDigPol, dpol, 256, 16); break;
+    case 5: HJ_ABL(NetCompressedPol, pol, 256, 8); break;
+    case 6: HJ_CLAIM(256, 16); break;
+    case 7: HJ_CLAIM(512, 16); break;
+    case 8: HJ_CLAIM(1024, 16); break;
+    case 9: HJ_CLAIM(1024, 8); break;
+    default: HJ_ABL(NetCompressedPol, pol, 256, 16); break;
+  }
+#undef HJ_ABL
+#undef HJ_CLAIM
 }
 
 // Ablation: per-tuple global atomics on a per-digit cursor (no LDS staging).
@@ -367,18 +667,37 @@ void localHistogram(const void *in, bool wide, const LocalItem *items, uint32_t 
   HIP_CHECK_LAUNCH();
 }
 
+uint32_t assignLocalStreams(LocalItem *items, uint32_t nItems) {
+  // Block b of the local scatter runs item (b % NGROUPS) * q + b / NGROUPS, so
+  // the items of group g = item / q are one contiguous run of the (lp-sorted)
+  // list and share an XCD; a stream = one (lp, group) run.
+  const uint32_t q = (nItems + NGROUPS - 1) / NGROUPS;
+  uint32_t streams = 0, prevLp = ~0u, prevG = ~0u;
+  for (uint32_t i = 0; i < nItems; ++i) {
+    const uint32_t g = i / (q ? q : 1);
+    if (items[i].lp != prevLp || g != prevG) {
+      ++streams;
+      prevLp = items[i].lp;
+      prevG = g;
+    }
+    items[i].stream = streams - 1;
+  }
+  return streams;
+}
+
 // One workgroup per owned partition lp: turns the [item][F] histograms of its
-// items into per-item cursors (sub-partition major) and the final partition
-// begin offsets partBegin[lp*F + q].
+// items into the start of every (stream, sub-partition) claim slice and the
+// final partition begin offsets partBegin[lp*F + q].
+template <typename CurT>
 __global__ __launch_bounds__(NT) void localCursorsKernel(const uint32_t *__restrict__ itemHist,
                                                          const uint32_t *__restrict__ lpItemBegin, uint32_t owned,
                                                          uint32_t bits, const uint64_t *__restrict__ lpBase,
-                                                         uint64_t *__restrict__ itemCursors,
+                                                         const LocalItem *__restrict__ items, CurT *__restrict__ gcur,
                                                          uint64_t *__restrict__ partBegin) {
   extern __shared__ __attribute__((aligned(16))) uint64_t csh[];
   const uint32_t F = 1u << bits;
-  uint64_t *tot = csh;           // [F]
-  uint64_t *wt = csh + F;        // [NT/64]
+  uint64_t *tot = csh;     // [F]
+  uint64_t *wt = csh + F;  // [NT/64]
   const uint32_t lp = blockIdx.x;
   const uint32_t ib = lpItemBegin[lp], ie = lpItemBegin[lp + 1];
   for (uint32_t q = threadIdx.x; q < F; q += NT) {
@@ -392,8 +711,13 @@ __global__ __launch_bounds__(NT) void localCursorsKernel(const uint32_t *__restr
   for (uint32_t q = threadIdx.x; q < F; q += NT) {
     uint64_t run = base + tot[q];
     partBegin[(uint64_t)lp * F + q] = run;
+    uint32_t prev = ~0u;
     for (uint32_t it = ib; it < ie; ++it) {
-      itemCursors[(uint64_t)it * F + q] = run;
+      const uint32_t st = items[it].stream;
+      if (st != prev) {
+        gcur[(uint64_t)st * F + q] = (CurT)run;
+        prev = st;
+      }
       run += itemHist[(uint64_t)it * F + q];
     }
   }
@@ -401,52 +725,57 @@ __global__ __launch_bounds__(NT) void localCursorsKernel(const uint32_t *__restr
 }
 
 void localCursors(const uint32_t *itemHist, const uint32_t *lpItemBegin, uint32_t owned, uint32_t bits,
-                  const uint64_t *lpBase, uint64_t *itemCursors, uint64_t *partBegin, hipStream_t s) {
+                  const uint64_t *lpBase, const LocalItem *items, void *gcur, bool narrow, uint64_t *partBegin,
+                  hipStream_t s) {
   if (owned == 0) return;
   const size_t lds = (size_t(1) << bits) * 8 + 64;
-  hipLaunchKernelGGL(localCursorsKernel, dim3(owned), dim3(NT), lds, s, itemHist, lpItemBegin, owned, bits, lpBase,
-                     itemCursors, partBegin);
+  if (narrow)
+    hipLaunchKernelGGL(localCursorsKernel<uint32_t>, dim3(owned), dim3(NT), lds, s, itemHist, lpItemBegin, owned, bits,
+                       lpBase, items, reinterpret_cast<uint32_t *>(gcur), partBegin);
+  else
+    hipLaunchKernelGGL(localCursorsKernel<unsigned long long>, dim3(owned), dim3(NT), lds, s, itemHist, lpItemBegin,
+                       owned, bits, lpBase, items, reinterpret_cast<unsigned long long *>(gcur), partBegin);
   HIP_CHECK_LAUNCH();
 }
 
-template <bool WIDE>
-__global__ __launch_bounds__(NT) void localScatterKernel(const void *__restrict__ in,
-                                                         const LocalItem *__restrict__ items, uint32_t shift,
-                                                         uint32_t bits, const uint64_t *__restrict__ itemCursors,
-                                                         void *out) {
+template <class Pol, typename CurT, int NTH, int IPT>
+__global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void localScatterClaimKernel(
+    const typename Pol::InT *__restrict__ in, const LocalItem *__restrict__ items, uint32_t nItems, uint32_t F,
+    Pol pol, CurT *__restrict__ gcur, typename Pol::OutT *out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  using T = typename std::conditional<WIDE, ulonglong2, uint64_t>::type;
-  const uint32_t F = 1u << bits;
-  const uint64_t mask = F - 1;
-  ScatterLds l = carveScatterLds<T>(smem, F);
-  for (uint32_t d = threadIdx.x; d < F; d += NT) {
-    l.cursor[d] = itemCursors[(uint64_t)blockIdx.x * F + d];
-    l.cnt[d] = 0;
-  }
+  const uint32_t q = (nItems + NGROUPS - 1) / NGROUPS;
+  const uint32_t item = (blockIdx.x % NGROUPS) * q + blockIdx.x / NGROUPS;  // XCD-contiguous items
+  if (item >= nItems) return;  // uniform per workgroup
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(reinterpret_cast<CurT *>(smem) + 2 * F);
+  for (uint32_t d = threadIdx.x; d < F; d += NTH) cnt[d] = 0;
   __syncthreads();
-  const LocalItem it = items[blockIdx.x];
-  const T *src = reinterpret_cast<const T *>(in);
-  auto pack = [](const T &x) -> T { return x; };
-  if constexpr (WIDE) {
-    auto digitOf = [shift, mask](const ulonglong2 &x) -> uint32_t { return (uint32_t)((x.x >> shift) & mask); };
-    scatterRange<T, T>(src, it.begin, it.begin + it.len, F, l, reinterpret_cast<T *>(out), digitOf, pack);
-  } else {
-    auto digitOf = [shift, mask](const uint64_t &x) -> uint32_t { return (uint32_t)((x >> shift) & mask); };
-    scatterRange<T, T>(src, it.begin, it.begin + it.len, F, l, reinterpret_cast<T *>(out), digitOf, pack);
-  }
+  const LocalItem it = items[item];
+  scatterRange<Pol, CurT, NTH, IPT, 0, true>(in, it.begin, it.begin + it.len, F, smem, pol, out,
+                                             gcur + (uint64_t)it.stream * F);
 }
 
 void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift, uint32_t bits,
-                  const uint64_t *itemCursors, void *out, hipStream_t s) {
+                  void *gcur, bool narrow, void *out, hipStream_t s) {
   HJ_CHECK(bits <= MAX_PART_BITS, "localScatter: bits=%u out of range", bits);
   if (nItems == 0) return;
-  const size_t lds = scatterLds(1u << bits, wide ? 16 : 8);
-  if (wide)
-    hipLaunchKernelGGL(localScatterKernel<true>, dim3(nItems), dim3(NT), lds, s, in, items, shift, bits,
-                       itemCursors, out);
-  else
-    hipLaunchKernelGGL(localScatterKernel<false>, dim3(nItems), dim3(NT), lds, s, in, items, shift, bits,
-                       itemCursors, out);
+  const uint32_t F = 1u << bits;
+  const uint64_t mask = F - 1;
+  const uint32_t grid = ((nItems + NGROUPS - 1) / NGROUPS) * NGROUPS;
+#define HJ_LOCAL(P, C)                                                                                        \
+  do {                                                                                                        \
+    P pol;                                                                                                    \
+    pol.mask = mask;                                                                                          \
+    pol.shift = shift;                                                                                        \
+    const size_t lds = ScatterLayout<P, C, CL_NTH * CL_IPT>::bytes(F);                                         \
+    hipLaunchKernelGGL((localScatterClaimKernel<P, C, CL_NTH, CL_IPT>), dim3(grid), dim3(CL_NTH), lds, s,      \
+                       reinterpret_cast<const typename P::InT *>(in), items, nItems, F, pol,                   \
+                       reinterpret_cast<C *>(gcur), reinterpret_cast<typename P::OutT *>(out));                \
+  } while (0)
+  if (wide && narrow) HJ_LOCAL(LocalWidePol, uint32_t);
+  else if (wide) HJ_LOCAL(LocalWidePol, unsigned long long);
+  else if (narrow) HJ_LOCAL(LocalCompressedPol, uint32_t);
+  else HJ_LOCAL(LocalCompressedPol, unsigned long long);
+#undef HJ_LOCAL
   HIP_CHECK_LAUNCH();
 }
 

@@ -46,7 +46,7 @@ void LocalPartitioning::partition(data::Window *w, int which) {
     for (; seg < xp.segments.size() && xp.segments[seg].lp == lp; ++seg)
       for (uint64_t off = 0; off < xp.segments[seg].len; off += kernels::LOCAL_ITEM_MAX) {
         const uint64_t len = std::min<uint64_t>(kernels::LOCAL_ITEM_MAX, xp.segments[seg].len - off);
-        it.push_back(kernels::LocalItem{xp.segments[seg].begin + off, (uint32_t)len, lp});
+        it.push_back(kernels::LocalItem{xp.segments[seg].begin + off, (uint32_t)len, lp, 0, 0});
       }
   }
   lb[owned] = (uint32_t)it.size();
@@ -55,10 +55,12 @@ void LocalPartitioning::partition(data::Window *w, int which) {
 
   void *out = ctx->workspace().get(std::max<uint64_t>(xp.recvTotal, 1) * tb);
   uint32_t *itemHist = ctx->workspace().getArray<uint32_t>(std::max<uint64_t>(1, (uint64_t)nItems * F));
-  uint64_t *itemCursors = ctx->workspace().getArray<uint64_t>(std::max<uint64_t>(1, (uint64_t)nItems * F));
   uint64_t *partBegin = ctx->workspace().getArray<uint64_t>((uint64_t)owned * F + 1);
 
   if (ctx->onDevice()) {
+    const uint32_t streams = kernels::assignLocalStreams(it.data(), nItems);
+    const bool narrow = kernels::cursorsNarrow(xp.recvTotal);
+    void *gcur = ctx->workspace().get(std::max<uint64_t>(1, (uint64_t)streams * F) * (narrow ? 4 : 8));
     kernels::LocalItem *dItems = ctx->workspace().getArray<kernels::LocalItem>(std::max<uint32_t>(nItems, 1));
     uint32_t *dLb = ctx->workspace().getArray<uint32_t>(owned + 1);
     uint64_t *dBase = ctx->workspace().getArray<uint64_t>(owned + 1);
@@ -70,9 +72,10 @@ void LocalPartitioning::partition(data::Window *w, int which) {
       ctx->copy(partBegin, zero.data(), 8, true, false);
     }
     kernels::localHistogram(w->getData(), wide, dItems, nItems, shift, bits, itemHist, ctx->stream());
-    kernels::localCursors(itemHist, dLb, owned, bits, dBase, itemCursors, partBegin, ctx->stream());
-    kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, itemCursors, out, ctx->stream());
+    kernels::localCursors(itemHist, dLb, owned, bits, dBase, dItems, gcur, narrow, partBegin, ctx->stream());
+    kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, gcur, narrow, out, ctx->stream());
   } else {
+    uint64_t *itemCursors = ctx->workspace().getArray<uint64_t>(std::max<uint64_t>(1, (uint64_t)nItems * F));
     if (owned == 0) partBegin[0] = 0;
     host::localHistogram(w->getData(), wide, it.data(), nItems, shift, bits, itemHist);
     host::localCursors(itemHist, lb.data(), owned, bits, xp.lpBase.data(), itemCursors, partBegin);

@@ -32,23 +32,28 @@ void NetworkPartitioning::partition(data::Relation *relation, data::Window *wind
   const bool single = xp.numberOfNodes == 1;
   const uint32_t tb = window->tupleBytes();
   void *send = single ? window->getData() : ctx->workspace().get(n * tb);
-  uint64_t *cursors = ctx->workspace().getArray<uint64_t>((uint64_t)F * g.blocks);
   window->start();
   if (ctx->onDevice()) {
+    // Claim-mode scatter: per-(chunk, XCD group, digit) slices, one device
+    // atomic per digit per 8192-tuple tile (kernels.h, CLAIM_GROUPS).
+    const bool narrow = kernels::cursorsNarrow(n);
+    const uint64_t cb = narrow ? 4 : 8, perChunk = (uint64_t)kernels::CLAIM_GROUPS * F * cb;
+    uint8_t *gcur = static_cast<uint8_t *>(ctx->workspace().get(chunks * perChunk));
     uint64_t *base = ctx->workspace().getArray<uint64_t>((uint64_t)chunks * F);
     ctx->copy(base, xp.digitBase.data(), xp.digitBase.size() * 8, true, false);
-    kernels::netCursors(local->blockHistogram(), F, g.blocks, bpc, base, cursors, ctx->stream());
+    kernels::netGroupCursors(local->blockHistogram(), F, g.blocks, bpc, base, gcur, narrow, ctx->stream());
     for (uint32_t c = 0; c < chunks; ++c) {
       const uint32_t b0 = c * bpc, b1 = std::min(g.blocks, b0 + bpc);
       if (plan.wide)
-        kernels::netScatterWide(relation->getData(), n, bits, g, b0, b1, cursors, static_cast<data::Tuple *>(send),
-                                ctx->stream());
+        kernels::netScatterWide(relation->getData(), n, bits, g, b0, b1, gcur + c * perChunk,
+                                static_cast<data::Tuple *>(send), ctx->stream());
       else
-        kernels::netScatter(relation->getData(), n, bits, plan.keyShift, g, b0, b1, cursors,
-                            static_cast<uint64_t *>(send), ctx->stream());
+        kernels::netScatter(relation->getData(), n, bits, plan.keyShift, g, b0, b1, gcur + c * perChunk,
+                            static_cast<uint64_t *>(send), ctx->stream(), plan.keyBits);
       if (!single) window->exchange(send, c);
     }
   } else {
+    uint64_t *cursors = ctx->workspace().getArray<uint64_t>((uint64_t)F * g.blocks);
     host::netCursors(local->blockHistogram(), F, g.blocks, bpc, xp.digitBase.data(), cursors);
     for (uint32_t c = 0; c < chunks; ++c) {
       const uint32_t b0 = c * bpc, b1 = std::min(g.blocks, b0 + bpc);

@@ -36,10 +36,11 @@ def test_net_histogram(C, dev, bits):
 
 @pytest.mark.parametrize("dev", devices())
 @pytest.mark.parametrize("bits,max_blocks", [(5, 2048), (9, 2048), (10, 7), (11, 64)])
-def test_net_partition_compressed(C, dev, bits, max_blocks):
+@pytest.mark.parametrize("key_bits", [30, 64])  # 30: digit carried in spare top bits; 64: LDS digit array
+def test_net_partition_compressed(C, dev, bits, max_blocks, key_bits):
     n = 250_000 + 17
     t = gen(C, n, device=dev, dist="UNIFORM", domain=1 << 30)
-    out, begin = C.ops.net_partition(t, bits, 32, False, max_blocks)
+    out, begin = C.ops.net_partition(t, bits, 32, False, max_blocks, key_bits)
     ref_sizes = torch.bincount((t[:, 0] & ((1 << bits) - 1)).cpu(), minlength=1 << bits)
     assert torch.equal(begin[1:] - begin[:-1], ref_sizes)
     k, r = unpack(out, bits, 32, begin)
