@@ -117,13 +117,29 @@ __device__ __forceinline__ void emitPair(const BPArgs &a, unsigned long long pos
   if (pos < a.outCapacity) a.outPairs[pos] = make_ulonglong2(ridR, ridS);
 }
 
+// Tuples per thread per batch: a whole 4096-tuple inner chunk is loaded with
+// one round of independent loads (16 per lane) before any LDS insert, instead
+// of one dependent HBM round trip per insert.
+constexpr int BP_K = 16;
+
+template <typename V, bool FULL>
+__device__ __forceinline__ void bpLoad(const V *__restrict__ src, uint32_t n, uint32_t b0, V (&v)[BP_K]) {
+#pragma unroll
+  for (int k = 0; k < BP_K; ++k) {
+    const uint32_t idx = b0 + k * BPT + threadIdx.x;
+    if (FULL || idx < n) v[k] = src[idx];
+  }
+}
+
 template <int MODE>
-__global__ __launch_bounds__(BPT) void buildProbeKernel(BPArgs a, const BPItem *__restrict__ items,
+__global__ __launch_bounds__(BPT, 4) void buildProbeKernel(BPArgs a, const BPItem *__restrict__ items,
                                                         const uint32_t *__restrict__ nItemsPtr, uint32_t capacity) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool WIDE = (MODE >= BP_WCOUNT);
   constexpr bool MAT = (MODE == BP_CMAT || MODE == BP_WMAT);
   using Entry = typename std::conditional<MODE == BP_CCOUNT, uint32_t, unsigned long long>::type;
+  using V = typename std::conditional<WIDE, ulonglong2, uint64_t>::type;
+  constexpr uint32_t BATCH = BPT * BP_K;
   const uint64_t maxSlots = uint64_t(1) << ceilLog2(2ull * a.rChunk);
   Entry *table = reinterpret_cast<Entry *>(smem);
   unsigned long long *ridTable = reinterpret_cast<unsigned long long *>(smem) + maxSlots;  // WMAT only
@@ -131,6 +147,8 @@ __global__ __launch_bounds__(BPT) void buildProbeKernel(BPArgs a, const BPItem *
   unsigned long long *wsum = reinterpret_cast<unsigned long long *>(smem + maxSlots * EB);
   const uint32_t t = threadIdx.x;
   const uint64_t ridMask = a.keyShift >= 64 ? ~0ull : ((1ull << a.keyShift) - 1);
+  const V *R = reinterpret_cast<const V *>(a.R);
+  const V *S = reinterpret_cast<const V *>(a.S);
   uint64_t matches = 0;
   const uint32_t nItems = min(*nItemsPtr, capacity);
 
@@ -145,85 +163,105 @@ __global__ __launch_bounds__(BPT) void buildProbeKernel(BPArgs a, const BPItem *
     if (tbits < 6) tbits = 6;
     const uint32_t slots = 1u << tbits, mask = slots - 1;
 
+    // First inner batch and first outer batch are in flight while the table is cleared.
+    V rv[BP_K], sv[BP_K];
+    if (nr >= BATCH) bpLoad<V, true>(R + rb, nr, 0, rv);
+    else bpLoad<V, false>(R + rb, nr, 0, rv);
+    if (ns >= BATCH) bpLoad<V, true>(S + sb, ns, 0, sv);
+    else bpLoad<V, false>(S + sb, ns, 0, sv);
     for (uint32_t i = t; i < slots; i += BPT) table[i] = (Entry)(MODE == BP_CCOUNT ? EMPTY32 : EMPTY64);
     __syncthreads();
 
     // ---- build
-    for (uint32_t i = t; i < nr; i += BPT) {
-      if constexpr (!WIDE) {
-        const uint64_t v = reinterpret_cast<const uint64_t *>(a.R)[rb + i];
-        const uint32_t frag = (uint32_t)(v >> a.fragShift);
-        uint32_t h = hash32(frag, tbits);
-        if constexpr (MODE == BP_CCOUNT) {
-          while (atomicCAS(&table[h], EMPTY32, frag) != EMPTY32) h = (h + 1) & mask;
-        } else {
-          while (atomicCAS(&table[h], EMPTY64, (unsigned long long)v) != EMPTY64) h = (h + 1) & mask;
+    for (uint32_t b0 = 0; b0 < nr; b0 += BATCH) {
+      if (b0) bpLoad<V, false>(R + rb, nr, b0, rv);
+#pragma unroll
+      for (int k = 0; k < BP_K; ++k) {
+        const uint32_t idx = b0 + k * BPT + t;
+        if (idx < nr) {
+          if constexpr (!WIDE) {
+            const uint64_t v = rv[k];
+            const uint32_t frag = (uint32_t)(v >> a.fragShift);
+            uint32_t h = hash32(frag, tbits);
+            if constexpr (MODE == BP_CCOUNT) {
+              while (atomicCAS(&table[h], EMPTY32, frag) != EMPTY32) h = (h + 1) & mask;
+            } else {
+              while (atomicCAS(&table[h], EMPTY64, (unsigned long long)v) != EMPTY64) h = (h + 1) & mask;
+            }
+          } else {
+            const ulonglong2 v = rv[k];
+            uint32_t h = hash64(v.x, tbits);
+            while (atomicCAS(&table[h], EMPTY64, (unsigned long long)v.x) != EMPTY64) h = (h + 1) & mask;
+            if constexpr (MAT) ridTable[h] = v.y;
+          }
         }
-      } else {
-        const ulonglong2 v = reinterpret_cast<const ulonglong2 *>(a.R)[rb + i];
-        uint32_t h = hash64(v.x, tbits);
-        while (atomicCAS(&table[h], EMPTY64, (unsigned long long)v.x) != EMPTY64) h = (h + 1) & mask;
-        if constexpr (MAT) ridTable[h] = v.y;
       }
     }
     __syncthreads();
 
     // ---- probe
-    for (uint32_t i0 = 0; i0 < ns; i0 += BPT) {
-      const uint32_t i = i0 + t;
-      const bool active = i < ns;
-      uint32_t found = 0;
-      uint64_t m0 = 0, m1 = 0, sRid = 0;
-      if (active) {
-        if constexpr (!WIDE) {
-          const uint64_t v = reinterpret_cast<const uint64_t *>(a.S)[sb + i];
-          const uint32_t frag = (uint32_t)(v >> a.fragShift);
-          uint32_t h = hash32(frag, tbits);
-          if constexpr (MODE == BP_CCOUNT) {
-            uint32_t e;
-            while ((e = table[h]) != EMPTY32) {
-              found += (e == frag);
-              h = (h + 1) & mask;
+    for (uint32_t b0 = 0; b0 < ns; b0 += BATCH) {
+      if (b0) {
+        if (b0 + BATCH <= ns) bpLoad<V, true>(S + sb, ns, b0, sv);
+        else bpLoad<V, false>(S + sb, ns, b0, sv);
+      }
+#pragma unroll
+      for (int k = 0; k < BP_K; ++k) {
+        const uint32_t idx = b0 + k * BPT + t;
+        const bool active = idx < ns;
+        uint32_t found = 0;
+        uint64_t m0 = 0, m1 = 0, sRid = 0;
+        if (active) {
+          if constexpr (!WIDE) {
+            const uint64_t v = sv[k];
+            const uint32_t frag = (uint32_t)(v >> a.fragShift);
+            uint32_t h = hash32(frag, tbits);
+            if constexpr (MODE == BP_CCOUNT) {
+              uint32_t e;
+              while ((e = table[h]) != EMPTY32) {
+                found += (e == frag);
+                h = (h + 1) & mask;
+              }
+            } else {
+              sRid = v & ridMask;
+              unsigned long long e;
+              while ((e = table[h]) != EMPTY64) {
+                if ((uint32_t)(e >> a.fragShift) == frag) {
+                  const uint64_t rr = e & ridMask;
+                  if (found == 0) m0 = rr;
+                  else if (found == 1) m1 = rr;
+                  else emitPair(a, atomicAdd(a.outCursor, 1ull), rr, sRid);  // overflow path
+                  ++found;
+                }
+                h = (h + 1) & mask;
+              }
             }
           } else {
-            sRid = v & ridMask;
+            const ulonglong2 v = sv[k];
+            uint32_t h = hash64(v.x, tbits);
+            sRid = v.y;
             unsigned long long e;
             while ((e = table[h]) != EMPTY64) {
-              if ((uint32_t)(e >> a.fragShift) == frag) {
-                const uint64_t rr = e & ridMask;
-                if (found == 0) m0 = rr;
-                else if (found == 1) m1 = rr;
-                else emitPair(a, atomicAdd(a.outCursor, 1ull), rr, sRid);  // overflow path
+              if (e == v.x) {
+                if constexpr (MAT) {
+                  const uint64_t rr = ridTable[h];
+                  if (found == 0) m0 = rr;
+                  else if (found == 1) m1 = rr;
+                  else emitPair(a, atomicAdd(a.outCursor, 1ull), rr, sRid);
+                }
                 ++found;
               }
               h = (h + 1) & mask;
             }
           }
-        } else {
-          const ulonglong2 v = reinterpret_cast<const ulonglong2 *>(a.S)[sb + i];
-          uint32_t h = hash64(v.x, tbits);
-          sRid = v.y;
-          unsigned long long e;
-          while ((e = table[h]) != EMPTY64) {
-            if (e == v.x) {
-              if constexpr (MAT) {
-                const uint64_t rr = ridTable[h];
-                if (found == 0) m0 = rr;
-                else if (found == 1) m1 = rr;
-                else emitPair(a, atomicAdd(a.outCursor, 1ull), rr, sRid);
-              }
-              ++found;
-            }
-            h = (h + 1) & mask;
-          }
         }
-      }
-      matches += found;
-      if constexpr (MAT) {
-        const uint32_t mine = found < MAT_SLOTS ? found : MAT_SLOTS;
-        const unsigned long long pos = reserveOutput(mine, a.outCursor);
-        if (mine > 0) emitPair(a, pos, m0, sRid);
-        if (mine > 1) emitPair(a, pos + 1, m1, sRid);
+        matches += found;
+        if constexpr (MAT) {
+          const uint32_t mine = found < MAT_SLOTS ? found : MAT_SLOTS;
+          const unsigned long long pos = reserveOutput(mine, a.outCursor);
+          if (mine > 0) emitPair(a, pos, m0, sRid);
+          if (mine > 1) emitPair(a, pos + 1, m1, sRid);
+        }
       }
     }
     __syncthreads();
