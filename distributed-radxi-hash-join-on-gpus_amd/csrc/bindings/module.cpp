@@ -8,6 +8,7 @@
 #include <memory>
 #include <vector>
 
+#include "../comm/InProcessCommunicator.h"
 #include "../comm/RcclCommunicator.h"
 #include "../comm/World.h"
 #include "../core/ExecContext.h"
@@ -501,6 +502,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              return std::make_shared<comm::RcclCommunicator>(v, rank, size, device);
            }),
            py::arg("unique_id"), py::arg("rank"), py::arg("size"), py::arg("device"));
+  py::class_<comm::InProcessGroup, std::shared_ptr<comm::InProcessGroup>>(m, "InProcessGroup")
+      .def(py::init<uint32_t>(), py::arg("size"))
+      .def("size", &comm::InProcessGroup::size)
+      .def("communicator", [](std::shared_ptr<comm::InProcessGroup> g, uint32_t rank) {
+        return std::static_pointer_cast<comm::Communicator>(std::make_shared<comm::InProcessCommunicator>(g, rank));
+      });
   m.def("rccl_unique_id", []() {
     auto v = comm::RcclCommunicator::uniqueId();
     return py::bytes(reinterpret_cast<const char *>(v.data()), v.size());

@@ -1,0 +1,70 @@
+#include "InProcessCommunicator.h"
+
+#include <cstring>
+
+#include "../utils/Hip.h"
+
+namespace hpcjoin {
+namespace comm {
+
+InProcessGroup::InProcessGroup(uint32_t size)
+    : slots(size, nullptr), counts(size, nullptr), displs(size, nullptr), size_(size) {}
+
+void InProcessGroup::barrier() {
+  std::unique_lock<std::mutex> lk(m_);
+  const uint64_t gen = generation_;
+  if (++waiting_ == size_) {
+    waiting_ = 0;
+    ++generation_;
+    cv_.notify_all();
+  } else {
+    cv_.wait(lk, [&] { return generation_ != gen; });
+  }
+}
+
+void InProcessCommunicator::allGatherHost(const uint64_t *send, uint64_t *recv, size_t count) {
+  InProcessGroup &g = *group_;
+  g.slots[rank_] = send;
+  g.barrier();
+  for (uint32_t r = 0; r < g.size(); ++r)
+    std::memcpy(recv + r * count, g.slots[r], count * sizeof(uint64_t));
+  g.barrier();
+}
+
+void InProcessCommunicator::allReduceSumHost(uint64_t *data, size_t count) {
+  std::vector<uint64_t> all(count * size());
+  allGatherHost(data, all.data(), count);
+  for (size_t i = 0; i < count; ++i) {
+    uint64_t s = 0;
+    for (uint32_t r = 0; r < size(); ++r) s += all[r * count + i];
+    data[i] = s;
+  }
+}
+
+void InProcessCommunicator::allToAllV(const uint64_t *send, const uint64_t *sendCounts, const uint64_t *sendDispls,
+                                      uint64_t *recv, const uint64_t *recvCounts, const uint64_t *recvDispls,
+                                      Location loc, hipStream_t stream) {
+  InProcessGroup &g = *group_;
+  const bool dev = loc == Location::Device;
+  if (dev) HIP_CHECK(hipStreamSynchronize(stream));  // my scatter output is complete
+  g.slots[rank_] = send;
+  g.counts[rank_] = sendCounts;
+  g.displs[rank_] = sendDispls;
+  g.barrier();
+  for (uint32_t src = 0; src < g.size(); ++src) {
+    const uint64_t n = recvCounts[src];
+    JOIN_ASSERT(g.counts[src][rank_] == n, "InProcess", "rank %u expects %lu words from %u, which sends %lu", rank_,
+                (unsigned long)n, src, (unsigned long)g.counts[src][rank_]);
+    if (!n) continue;
+    const uint64_t *from = static_cast<const uint64_t *>(g.slots[src]) + g.displs[src][rank_];
+    if (dev)
+      HIP_CHECK(hipMemcpyAsync(recv + recvDispls[src], from, n * 8, hipMemcpyDeviceToDevice, stream));
+    else
+      std::memcpy(recv + recvDispls[src], from, n * 8);
+  }
+  if (dev) HIP_CHECK(hipStreamSynchronize(stream));
+  g.barrier();  // nobody reuses a send buffer before every peer copied from it
+}
+
+}  // namespace comm
+}  // namespace hpcjoin

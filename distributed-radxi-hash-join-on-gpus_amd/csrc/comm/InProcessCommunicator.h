@@ -1,0 +1,58 @@
+// N ranks as threads of one process ("a fake communicator
+// (in-process threads exchanging buffers) lets the host-side offset and
+// assignment logic be tested without a cluster").  Works for host buffers and
+// for device buffers on one GPU (D2D copies), so the complete distributed
+// device path -- exchange plans, windows, chunked exchange, segments -- runs
+// under test on a single MI355X, where RCCL refuses two ranks per device.
+// Collectives are blocking; allToAllV synchronises the caller's stream first
+// so a sender's scatter kernel has finished before peers copy from it.
+#pragma once
+
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "Communicator.h"
+
+namespace hpcjoin {
+namespace comm {
+
+class InProcessGroup {
+ public:
+  explicit InProcessGroup(uint32_t size);
+  uint32_t size() const { return size_; }
+  void barrier();
+  // Shared slots: each rank publishes one pointer-sized value per phase.
+  std::vector<const void *> slots;
+  std::vector<const uint64_t *> counts, displs;
+  std::vector<uint64_t> scratch;  // all-gather staging
+
+ private:
+  uint32_t size_;
+  std::mutex m_;
+  std::condition_variable cv_;
+  uint32_t waiting_ = 0;
+  uint64_t generation_ = 0;
+};
+
+class InProcessCommunicator : public Communicator {
+ public:
+  InProcessCommunicator(std::shared_ptr<InProcessGroup> group, uint32_t rank) : group_(std::move(group)), rank_(rank) {}
+  uint32_t rank() const override { return rank_; }
+  uint32_t size() const override { return group_->size(); }
+  bool supports(Location) const override { return true; }
+  std::string name() const override { return "in_process"; }
+  void allGatherHost(const uint64_t *send, uint64_t *recv, size_t count) override;
+  void allReduceSumHost(uint64_t *data, size_t count) override;
+  void barrier() override { group_->barrier(); }
+  void allToAllV(const uint64_t *send, const uint64_t *sendCounts, const uint64_t *sendDispls, uint64_t *recv,
+                 const uint64_t *recvCounts, const uint64_t *recvDispls, Location loc, hipStream_t stream) override;
+
+ private:
+  std::shared_ptr<InProcessGroup> group_;
+  uint32_t rank_;
+};
+
+}  // namespace comm
+}  // namespace hpcjoin

@@ -17,8 +17,8 @@
 namespace hpcjoin {
 namespace operators {
 
-uint64_t HashJoin::RESULT_COUNTER = 0;
-std::queue<tasks::Task *> HashJoin::TASK_QUEUE;
+thread_local uint64_t HashJoin::RESULT_COUNTER = 0;
+thread_local std::queue<tasks::Task *> HashJoin::TASK_QUEUE;
 
 using performance::Measurements;
 using performance::nowUs;

@@ -62,8 +62,9 @@ class HashJoin {
   data::Relation *outerRelation;
 
  public:
-  static uint64_t RESULT_COUNTER;
-  static std::queue<tasks::Task *> TASK_QUEUE;
+  // thread_local: in-process ranks (InProcessCommunicator) each run on their own thread.
+  static thread_local uint64_t RESULT_COUNTER;
+  static thread_local std::queue<tasks::Task *> TASK_QUEUE;
 
  private:
   void makeJoinPlan();

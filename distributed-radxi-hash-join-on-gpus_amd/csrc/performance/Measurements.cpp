@@ -24,7 +24,7 @@ struct State {
   uint64_t tuples = 0;
 };
 State &st() {
-  static State s;
+  static thread_local State s;  // one per rank thread (in-process ranks)
   return s;
 }
 enum Phase { HIST = 0, WINALLOC, NET, NETWAIT, LOCPREP, LOCAL, NPHASE };

@@ -7,7 +7,7 @@
 namespace hpcjoin {
 namespace utils {
 
-static int g_rank = 0;
+static thread_local int g_rank = 0;
 int debugRank() { return g_rank; }
 void setDebugRank(int r) { g_rank = r; }
 

@@ -1,0 +1,124 @@
+"""Distributed join paths.
+
+* in-process ranks (threads sharing one process; host buffers here, device
+  buffers on the GPU box) exercise the full N-rank exchange logic;
+* a real multi-process run over torch.distributed (gloo) drives the
+  ProcessGroupCommunicator on the host path.
+"""
+import os
+import socket
+import subprocess
+import sys
+import threading
+
+import pytest
+
+from conftest import ROOT, devices
+
+
+def run_ranks(C, n_ranks, loc, G_R, G_S, cfg_fn=None, outer_dist="UNIQUE", theta=0.75):
+    group = C.InProcessGroup(n_ranks)
+    inner = C.GenSpec(seed=1234)
+    outer = C.GenSpec(distribution=getattr(C.KeyDistribution, outer_dist), seed=4321,
+                      domain=0 if outer_dist == "UNIQUE" else G_R, zipf_theta=theta)
+    results, errors = [None] * n_ranks, []
+
+    def rank_main(r):
+        try:
+            comm = group.communicator(r)
+            ctx = C.ExecContext(loc, 0 if loc == "device" else -1, comm)
+            R = C.Relation(C.Relation.local_size_for(G_R, r, n_ranks), G_R, loc, 0)
+            S = C.Relation(C.Relation.local_size_for(G_S, r, n_ranks), G_S, loc, 0)
+            R.generate(inner, C.Relation.local_offset_for(G_R, r, n_ranks))
+            S.generate(outer, C.Relation.local_offset_for(G_S, r, n_ranks))
+            cfg = C.JoinConfig()
+            if cfg_fn:
+                cfg_fn(cfg)
+            j = C.HashJoin(R, S, ctx, cfg)
+            res = j.run()
+            res2 = j.run()  # repeatable
+            assert res2["global_matches"] == res["global_matches"]
+            results[r] = (res, j.plan)
+        except Exception as e:  # surface in the main thread
+            errors.append((r, repr(e)))
+
+    threads = [threading.Thread(target=rank_main, args=(r,)) for r in range(n_ranks)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=600)
+    assert not errors, errors
+    return results, C.Relation.expected_matches(inner, G_R, outer, G_S)
+
+
+@pytest.mark.parametrize("dev", devices())
+@pytest.mark.parametrize("n_ranks", [2, 3, 4, 8])
+def test_in_process_ranks(C, dev, n_ranks):
+    loc = "device" if dev == "cuda" else "host"
+    results, exp = run_ranks(C, n_ranks, loc, 200_003, 300_007, outer_dist="UNIFORM")
+    assert all(r[0]["global_matches"] == exp for r in results)
+    assert sum(r[0]["local_matches"] for r in results) == exp
+    # every tuple ends up on exactly one owner
+    assert sum(r[0]["inner_received"] for r in results) == 200_003
+    assert sum(r[0]["outer_received"] for r in results) == 300_007
+
+
+@pytest.mark.parametrize("dev", devices())
+@pytest.mark.parametrize("chunks", [1, 3])
+@pytest.mark.parametrize("policy", ["ROUND_ROBIN", "LPT"])
+def test_in_process_chunked_exchange(C, dev, chunks, policy):
+    loc = "device" if dev == "cuda" else "host"
+
+    def cfg_fn(cfg):
+        cfg.chunks = chunks
+        cfg.assignment = getattr(C.AssignmentPolicy, policy)
+        cfg.max_partition_blocks = 16  # several blocks per chunk even at this size
+
+    results, exp = run_ranks(C, 4, loc, 500_000, 500_000, cfg_fn)
+    assert all(r[0]["global_matches"] == exp for r in results)
+
+
+@pytest.mark.parametrize("dev", devices())
+def test_in_process_skew_lpt_balances(C, dev):
+    loc = "device" if dev == "cuda" else "host"
+
+    def cfg_fn(cfg):
+        cfg.assignment = C.AssignmentPolicy.LPT
+
+    results, exp = run_ranks(C, 4, loc, 200_000, 800_000, cfg_fn, outer_dist="ZIPF", theta=0.9)
+    assert all(r[0]["global_matches"] == exp for r in results)
+    loads = [r[0]["inner_received"] + r[0]["outer_received"] for r in results]
+    assert max(loads) < 1.6 * (sum(loads) / len(loads)), loads
+
+
+@pytest.mark.parametrize("dev", devices())
+def test_in_process_wide_materialize(C, dev):
+    loc = "device" if dev == "cuda" else "host"
+
+    def cfg_fn(cfg):
+        cfg.format = C.TupleFormat.WIDE
+        cfg.materialize = True
+
+    results, exp = run_ranks(C, 2, loc, 100_000, 100_000, cfg_fn)
+    assert sum(r[0]["output_pairs"] for r in results) == exp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_multiprocess_host_join(world):
+    """torchrun-style launch: ProcessGroupCommunicator over gloo, host path."""
+    port = _free_port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+               HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    script = os.path.join(ROOT, "tests", "dist_worker.py")
+    procs = [subprocess.Popen([sys.executable, script], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(world)]
+    outs = [p.communicate(timeout=600)[0] for p in procs]
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o
+    assert "OK" in outs[0], outs[0]
