@@ -126,6 +126,14 @@ def main():
         if args.json_out:
             with open(args.json_out, "w") as f:
                 json.dump(line, f, indent=1)
+    # Deterministic teardown: engine objects (HIP streams, arenas, the RCCL
+    # communicator) go before torch.distributed and before interpreter exit.
+    del join, R, S, ctx
+    if on_gpu:
+        torch.cuda.synchronize()
+    if info.world > 1:
+        comm.barrier()
+    del comm
     if info.world > 1:
         dist.barrier()
         dist.destroy_process_group()

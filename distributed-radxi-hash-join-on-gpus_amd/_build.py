@@ -114,6 +114,11 @@ def build(jobs: int | None = None, verbose: bool = False, with_cli: bool = True)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = dict(ex.map(compile_one, jobs_list))
 
+    # drop objects of older source/header versions (keeps the gpurun snapshot small)
+    keep = {o.name for o in objs.values()}
+    for stale in (BUILD / "obj").glob("*.o"):
+        if stale.name not in keep and not stale.name.startswith("apps_"):
+            stale.unlink()
     core_objs = [str(objs[s]) for s in core + kernels]
     bind_objs = [str(objs[s]) for s in bindings]
     out = ext_path()

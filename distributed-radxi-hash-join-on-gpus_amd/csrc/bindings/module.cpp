@@ -483,6 +483,25 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         }
         return out;
       })
+      .def("all_to_all_v",
+           [](comm::Communicator &c, at::Tensor send, std::vector<uint64_t> sendCounts, at::Tensor recv,
+              std::vector<uint64_t> recvCounts) {
+             // Words (int64 elements); displacements are the running sums.
+             TORCH_CHECK(send.scalar_type() == at::kLong && recv.scalar_type() == at::kLong, "int64 tensors");
+             const uint32_t n = c.size();
+             TORCH_CHECK(sendCounts.size() == n && recvCounts.size() == n, "one count per rank");
+             std::vector<uint64_t> sd(n), rd(n);
+             for (uint32_t p = 1; p < n; ++p) {
+               sd[p] = sd[p - 1] + sendCounts[p - 1];
+               rd[p] = rd[p - 1] + recvCounts[p - 1];
+             }
+             const Location l = locOf(send);
+             if (l == Location::Device) HIP_CHECK(hipDeviceSynchronize());
+             py::gil_scoped_release nogil;
+             c.allToAllV(ptr<uint64_t>(send), sendCounts.data(), sd.data(), ptr<uint64_t>(recv), recvCounts.data(),
+                         rd.data(), l, nullptr);
+             if (l == Location::Device) HIP_CHECK(hipDeviceSynchronize());
+           })
       .def("all_reduce_sum", [](comm::Communicator &c, std::vector<uint64_t> v) {
         {
           py::gil_scoped_release nogil;
