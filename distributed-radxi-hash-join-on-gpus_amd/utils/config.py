@@ -1,0 +1,40 @@
+"""Runtime JoinConfig <-> dict / environment (the reference configures
+everything at compile time: core/Configuration.h + CMake -D macros)."""
+from __future__ import annotations
+
+import os
+
+from .._native import require_native
+
+_FIELDS = ["network_bits", "local_bits", "two_level", "key_shift", "materialize", "output_capacity", "build_target",
+           "r_chunk", "s_chunk", "chunks", "checks", "max_partition_blocks"]
+
+
+def config_to_dict(cfg) -> dict:
+    d = {f: getattr(cfg, f) for f in _FIELDS}
+    d["assignment"] = str(cfg.assignment).split(".")[-1]
+    d["format"] = str(cfg.format).split(".")[-1]
+    return d
+
+
+def config_from_dict(d: dict | None = None, env_prefix: str = "HPCJOIN_"):
+    """JoinConfig from a dict, overridden by HPCJOIN_<FIELD> environment variables."""
+    C = require_native()
+    cfg = C.JoinConfig()
+    merged = dict(d or {})
+    for f in _FIELDS + ["assignment", "format"]:
+        v = os.environ.get(env_prefix + f.upper())
+        if v is not None:
+            merged[f] = v
+    for k, v in merged.items():
+        if k == "assignment":
+            cfg.assignment = getattr(C.AssignmentPolicy, str(v).upper())
+        elif k == "format":
+            cfg.format = getattr(C.TupleFormat, str(v).upper())
+        elif k in ("two_level", "materialize", "checks"):
+            setattr(cfg, k, v if isinstance(v, bool) else str(v).lower() in ("1", "true", "yes"))
+        elif k in _FIELDS:
+            setattr(cfg, k, int(v))
+        else:
+            raise KeyError(f"unknown JoinConfig field {k}")
+    return cfg

@@ -1,0 +1,47 @@
+"""Standalone C++ driver (build/bin/hjoin_bench, no Python/torch) and bench.py."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+BIN = os.path.join(ROOT, "distributed-radxi-hash-join-on-gpus_amd", "build", "bin", "hjoin_bench")
+
+
+def _last_json(out):
+    return json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+
+
+def test_hjoin_bench_host(tmp_path):
+    assert os.path.exists(BIN), "run __graft_entry__.build() first"
+    r = subprocess.run([BIN, "--host", "--inner", "200000", "--outer", "300000", "--dist", "zipf", "--iters", "2",
+                        "--warmup", "0", "--perf-dir", str(tmp_path / "perf")],
+                       capture_output=True, text=True, timeout=300, env=dict(os.environ, HIP_VISIBLE_DEVICES=""))
+    assert r.returncode == 0, r.stdout + r.stderr
+    j = _last_json(r.stdout)
+    assert j["correct"] is True and j["matches"] == 300000
+    assert "[RESULTS] Tuples:" in r.stdout
+    assert (tmp_path / "perf" / "0.perf").exists()
+
+
+@pytest.mark.gpu
+def test_hjoin_bench_device():
+    r = subprocess.run([BIN, "--inner", "16000000", "--outer", "16000000", "--iters", "3"], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert _last_json(r.stdout)["correct"] is True
+
+
+def test_bench_py_cpu_contract():
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    j = _last_json(r.stdout)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in j, k
+    assert j["correct"] is True and j["n_gpus"] == 1 and j["steps"] == 2
