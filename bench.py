@@ -64,8 +64,12 @@ def main():
     S.generate(outer, C.Relation.local_offset_for(G_S, info.rank, info.world))
     expected = C.Relation.expected_matches(inner, G_R, outer, G_S)
 
-    cfg = C.JoinConfig()
-    cfg.chunks = args.chunks if args.chunks > 0 else (1 if info.world == 1 else 4)
+    from hpcjoin.utils import config_from_dict  # HPCJOIN_<FIELD> env overrides (sweeps)
+    cfg = config_from_dict({})
+    if args.chunks > 0:
+        cfg.chunks = args.chunks
+    elif "HPCJOIN_CHUNKS" not in os.environ:
+        cfg.chunks = 1 if info.world == 1 else 4
     join = C.HashJoin(R, S, ctx, cfg)
 
     def barrier():

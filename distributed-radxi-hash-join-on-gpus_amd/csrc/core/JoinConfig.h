@@ -31,7 +31,7 @@ struct JoinConfig {
   TupleFormat format = TupleFormat::Compressed;
   bool materialize = false;   // also write (rid_inner, rid_outer) pairs
   uint64_t outputCapacity = 0;  // materialize: pair capacity (0 = auto from oracle bound)
-  uint64_t buildTarget = 3072;  // target inner tuples per final partition
+  uint64_t buildTarget = 4096;  // target inner tuples per final partition (= one 256 x 16 LDS build batch)
   uint32_t rChunk = 0;          // max inner tuples per LDS table (0 = auto from LDS budget)
   uint32_t sChunk = 65536;      // max outer tuples per build/probe work item
   uint32_t chunks = 1;          // exchange pipeline slices per relation (>1: scatter(k+1) || all-to-all(k))

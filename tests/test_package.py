@@ -68,7 +68,7 @@ def test_radix_join_model_host(C):
 def test_plan_is_deterministic(C):
     cfg = C.JoinConfig()
     p = C.make_plan(cfg, 8, 1_000_000_000, 1_000_000_000, 999_999_999, 999_999_999)
-    assert (p.network_bits, p.local_bits, p.key_shift) == (10, 9, 32)
+    assert (p.network_bits, p.local_bits, p.key_shift) == (9, 9, 32)
     p16 = C.make_plan(cfg, 8, 1_000_000_000, 16_000_000_000, 999_999_999, 16_000_000_000 - 1)
     assert p16.key_shift == 34  # 16B rids need 34 bits
     with pytest.raises(RuntimeError):
