@@ -131,8 +131,11 @@ JoinResult HashJoin::run() {
   Measurements::storeNetworkDetails(innerRelation->getLocalSize(), outerRelation->getLocalSize(),
                                     hc.innerLocal()->getChunkCount());
   Measurements::startWaitingForNetworkCompletion();
+  // Only the inner window is awaited here (a stream wait, no host sync): the
+  // outer relation's all-to-all keeps running on the exchange stream while the
+  // inner relation's local radix pass runs; LocalPartitioning waits for the
+  // outer window right before its own pass.
   innerWindow.stop();
-  outerWindow.stop();
   if (config.checks) {
     innerWindow.assertAllTuplesWritten();
     outerWindow.assertAllTuplesWritten();
