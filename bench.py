@@ -124,6 +124,12 @@ def main():
             "expected_matches": expected,
             "correct": correct,
             "phases_ms": phases,
+            "engine": {"reruns": results[-1]["reruns"], "build_probe_items": results[-1]["build_probe_items"],
+                       "local_items": results[-1]["local_items"], "workspace_GB": round(ctx.workspace_capacity() / 1e9, 2),
+                       "workspace_peak_GB": round(ctx.workspace_peak() / 1e9, 2),
+                       "step_ms": [round(r["join_ms"], 2) for r in results],
+                       "setup_ms": [round(r["setup_ms"], 2) for r in results],
+                       "teardown_ms": [round(r["teardown_ms"], 2) for r in results]},
             "device": torch.cuda.get_device_name(0) if on_gpu else "cpu",
         }
         print(json.dumps(line), flush=True)

@@ -395,6 +395,8 @@ py::dict resultToDict(const operators::JoinResult &r) {
   d["dev_network_ms"] = r.devNetworkMs;
   d["dev_local_partition_ms"] = r.devLocalPartitionMs;
   d["dev_build_probe_ms"] = r.devBuildProbeMs;
+  d["setup_ms"] = r.setupMs;
+  d["teardown_ms"] = r.teardownMs;
   d["inner_received"] = r.innerReceived;
   d["outer_received"] = r.outerReceived;
   d["local_items"] = r.localItems;

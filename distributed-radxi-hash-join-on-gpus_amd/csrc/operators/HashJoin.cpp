@@ -93,7 +93,9 @@ JoinResult HashJoin::run() {
   result = JoinResult();
   result.innerLocal = innerRelation->getLocalSize();
   result.outerLocal = outerRelation->getLocalSize();
+  const uint64_t tSetup = nowUs();
   ctx->resetScratch();
+  result.setupMs = (nowUs() - tSetup) / 1000.0;
   const bool dev = ctx->onDevice();
   if (dev) HIP_CHECK(hipSetDevice(ctx->device()));
 
@@ -211,6 +213,7 @@ JoinResult HashJoin::run() {
   uint64_t g = result.localMatches;
   ctx->comm()->allReduceSumHost(&g, 1);
   result.globalMatches = g;
+  result.teardownMs = (nowUs() - t4) / 1000.0;
   RESULT_COUNTER = result.localMatches;
   return result;
 }

@@ -33,6 +33,7 @@ struct JoinResult {
   double joinMs = 0;               // host wall: histogram start -> local result available
   double histogramMs = 0, windowMs = 0, networkMs = 0, localMs = 0;  // host phases
   double devHistogramMs = 0, devNetworkMs = 0, devLocalPartitionMs = 0, devBuildProbeMs = 0;  // hipEvents
+  double setupMs = 0, teardownMs = 0;  // outside the join span: scratch reset / result reduction
   uint64_t innerReceived = 0, outerReceived = 0;
   uint64_t localItems = 0, buildProbeItems = 0;
   uint64_t innerLocal = 0, outerLocal = 0;
