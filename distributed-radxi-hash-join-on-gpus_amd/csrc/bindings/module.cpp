@@ -19,6 +19,7 @@
 #include "../memory/Arena.h"
 #include "../memory/Pool.h"
 #include "../operators/HashJoin.h"
+#include "../operators/LateMaterialization.h"
 #include "../performance/Measurements.h"
 #include "../utils/Hip.h"
 #include "ProcessGroupCommunicator.h"
@@ -248,6 +249,7 @@ at::Tensor opGenerate(int64_t n, int64_t globalOffset, int64_t globalSize, const
   p.seed = spec.seed;
   p.perm = kernels::FeistelPermutation::make(domain, spec.seed);
   if (spec.distribution == kernels::KeyDistribution::Zipf) p.zipf = host::makeZipf(domain, spec.zipfTheta);
+  p.tpchSparse = spec.tpchSparse;
   if (out.is_cuda()) {
     kernels::generate(ptr<data::Tuple>(out), n, p, nullptr);
     HIP_CHECK(hipDeviceSynchronize());
@@ -572,11 +574,25 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            }),
            py::arg("distribution") = kernels::KeyDistribution::Unique, py::arg("seed") = 1234, py::arg("domain") = 0,
            py::arg("key_offset") = 0, py::arg("zipf_theta") = 0.75)
+      .def(py::init([](kernels::KeyDistribution d, uint64_t seed, uint64_t domain, uint64_t keyOffset, double theta,
+                       bool sparse) {
+             data::GenSpec s;
+             s.distribution = d;
+             s.seed = seed;
+             s.domain = domain;
+             s.keyOffset = keyOffset;
+             s.zipfTheta = theta;
+             s.tpchSparse = sparse;
+             return s;
+           }),
+           py::arg("distribution"), py::arg("seed"), py::arg("domain"), py::arg("key_offset"), py::arg("zipf_theta"),
+           py::arg("tpch_sparse"))
       .def_readwrite("distribution", &data::GenSpec::distribution)
       .def_readwrite("seed", &data::GenSpec::seed)
       .def_readwrite("domain", &data::GenSpec::domain)
       .def_readwrite("key_offset", &data::GenSpec::keyOffset)
-      .def_readwrite("zipf_theta", &data::GenSpec::zipfTheta);
+      .def_readwrite("zipf_theta", &data::GenSpec::zipfTheta)
+      .def_readwrite("tpch_sparse", &data::GenSpec::tpchSparse);
 
   py::class_<PyRelation>(m, "Relation")
       .def(py::init([](uint64_t localSize, uint64_t globalSize, const std::string &loc, int device) {
@@ -652,6 +668,30 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         j.join();
       })
       .def_property_readonly("plan", &operators::HashJoin::getPlan)
+      .def(
+          "materialize_payloads",
+          [](operators::HashJoin &j, std::shared_ptr<core::ExecContext> ctx, at::Tensor innerRows, uint64_t innerOffset,
+             uint64_t innerGlobal, at::Tensor outerRows, uint64_t outerOffset, uint64_t outerGlobal) {
+            // Collective.  Returns [pairs, 10] int64: rid_inner, rid_outer, inner row (4), outer row (4).
+            TORCH_CHECK(j.getConfig().materialize, "join was not run with materialize=True");
+            TORCH_CHECK(innerRows.dim() == 2 && innerRows.size(1) == (int64_t)kernels::ROW_WORDS &&
+                            outerRows.dim() == 2 && outerRows.size(1) == (int64_t)kernels::ROW_WORDS,
+                        "payload rows must be [n, 4] int64 (32 bytes)");
+            operators::PayloadColumn a{ptr<uint64_t>(innerRows), (uint64_t)innerRows.size(0), innerOffset, innerGlobal};
+            operators::PayloadColumn b{ptr<uint64_t>(outerRows), (uint64_t)outerRows.size(0), outerOffset, outerGlobal};
+            const uint64_t n = j.lastResult().outputPairs;
+            at::Tensor out = at::empty({(int64_t)n, (int64_t)operators::LateMaterialization::OUT_WORDS},
+                                       at::TensorOptions().dtype(at::kLong).device(innerRows.device()));
+            if (innerRows.is_cuda()) HIP_CHECK(hipDeviceSynchronize());
+            {
+              py::gil_scoped_release nogil;
+              operators::LateMaterialization lm(ctx.get(), a, b);
+              lm.materialize(j.getOutput(), n, ptr<uint64_t>(out));
+            }
+            return out;
+          },
+          py::arg("context"), py::arg("inner_rows"), py::arg("inner_rid_offset"), py::arg("inner_global_rows"),
+          py::arg("outer_rows"), py::arg("outer_rid_offset"), py::arg("outer_global_rows"))
       .def("output", [](operators::HashJoin &j) {
         const auto &r = j.lastResult();
         const uint64_t n = std::min<uint64_t>(r.outputPairs, r.outputPairs);
@@ -695,6 +735,23 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   ops.def("generate", &opGenerate, py::arg("n"), py::arg("global_offset"), py::arg("global_size"), py::arg("spec"),
           py::arg("device") = "cpu");
   ops.def("scan_u32", &opScan);
+  ops.def(
+      "generate_payload",
+      [](int64_t n, uint64_t ridOffset, uint64_t seed, const std::string &device) {
+        at::Tensor out = at::empty({n, (int64_t)kernels::ROW_WORDS}, at::TensorOptions().dtype(at::kLong).device(device));
+        if (out.is_cuda()) {
+          setDevice(out);
+          kernels::generatePayload(ptr<uint64_t>(out), n, ridOffset, seed, nullptr);
+          HIP_CHECK(hipDeviceSynchronize());
+        } else {
+          uint64_t *o = ptr<uint64_t>(out);
+          for (int64_t i = 0; i < n; ++i)
+            for (uint32_t w = 0; w < kernels::ROW_WORDS; ++w)
+              o[i * kernels::ROW_WORDS + w] = kernels::payloadWord(seed, ridOffset + i, w);
+        }
+        return out;
+      },
+      py::arg("n"), py::arg("rid_offset"), py::arg("seed"), py::arg("device") = "cpu");
   ops.def("npj_count", &opNpjCount);
   ops.def("net_scatter_global_atomic", &opNetScatterGlobalAtomic);
   ops.def("bench_copy_ms", &benchCopy, py::arg("src"), py::arg("dst"), py::arg("iters") = 10);

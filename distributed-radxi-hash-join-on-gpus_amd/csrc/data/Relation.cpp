@@ -95,12 +95,15 @@ void Relation::generate(const GenSpec &spec, uint64_t globalOffset) {
   p.seed = spec.seed;
   p.perm = kernels::FeistelPermutation::make(p.domain, spec.seed);
   if (spec.distribution == KeyDistribution::Zipf) p.zipf = host::makeZipf(p.domain, spec.zipfTheta);
+  p.tpchSparse = spec.tpchSparse;
   runGenerate(data, localSize, p, loc_, device_);
   maxKey_ = spec.keyOffset + (spec.distribution == KeyDistribution::Dense ? globalSize : p.domain) - 1;
+  if (spec.tpchSparse) maxKey_ = kernels::tpchSparseKey(maxKey_);
 }
 
 uint64_t Relation::expectedMatches(const GenSpec &inner, uint64_t innerGlobal, const GenSpec &outer,
                                    uint64_t outerGlobal) {
+  if (inner.tpchSparse != outer.tpchSparse) return UINT64_MAX;  // the key transform must match
   const uint64_t innerDomain = inner.domain ? inner.domain : innerGlobal;
   const bool innerIsKeySet = (inner.distribution == KeyDistribution::Unique ||
                               inner.distribution == KeyDistribution::Dense) &&

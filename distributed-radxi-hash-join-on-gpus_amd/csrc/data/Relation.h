@@ -29,6 +29,7 @@ struct GenSpec {
   uint64_t domain = 0;       // key domain (0 = global size); FK relations use the inner size
   uint64_t keyOffset = 0;
   double zipfTheta = 0.75;
+  bool tpchSparse = false;   // TPC-H O_ORDERKEY layout applied to the generated key (both sides alike)
 };
 
 class Relation {

@@ -41,6 +41,7 @@ __global__ __launch_bounds__(256) void generateKernel(ulonglong2 *__restrict__ o
     const uint64_t gi = p.globalOffset + i;
     ulonglong2 t;
     t.x = genKey(p, gi);
+    if (p.tpchSparse) t.x = tpchSparseKey(t.x);
     t.y = p.ridOffset + i;
     out[i] = t;
   }

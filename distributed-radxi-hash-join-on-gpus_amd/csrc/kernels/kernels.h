@@ -53,7 +53,9 @@ struct GenParams {
   FeistelPermutation perm{};  // Unique/Modulo/Zipf rank -> key bijection
   uint64_t seed = 0;
   ZipfParams zipf{};
+  bool tpchSparse = false;    // TPC-H O_ORDERKEY layout: k -> (k / 8) * 32 + k % 8 + 1
 };
+HJ_HD uint64_t tpchSparseKey(uint64_t k) { return (k >> 3) * 32 + (k & 7) + 1; }
 void generate(data::Tuple *out, uint64_t n, const GenParams &p, hipStream_t s);
 
 // ------------------------------------------------- pass 1: network partition
@@ -184,5 +186,28 @@ namespace hpcjoin {
 namespace kernels {
 // out[0] = max key, out[1] = max rid over n tuples (device); out must be zeroed.
 void keyRidMax(const data::Tuple *in, uint64_t n, unsigned long long *out, hipStream_t s);
+}  // namespace kernels
+}  // namespace hpcjoin
+
+namespace hpcjoin {
+namespace kernels {
+// ------------------------------------------------ late materialization
+// Payload rows are ROW_WORDS x u64 (32 bytes), a pure function of (seed, rid).
+constexpr uint32_t ROW_WORDS = 4;
+HJ_HD uint64_t payloadWord(uint64_t seed, uint64_t rid, uint32_t w) {
+  return mix64(seed * 0x9E3779B97F4A7C15ULL + rid * ROW_WORDS + w);
+}
+void generatePayload(uint64_t *rows, uint64_t n, uint64_t ridOffset, uint64_t seed, hipStream_t s);
+// Requests for one side of the materialized pairs: x = owner | (pair index << 8), y = rid.
+void makeRequests(const ulonglong2 *pairs, uint64_t n, int side, uint64_t ridsPerRank, uint32_t nodes,
+                  ulonglong2 *req, hipStream_t s);
+// After partitioning requests by owner: rids[j] = req[j].y, idx[j] = req[j].x >> 8.
+void splitRequests(const ulonglong2 *req, uint64_t n, uint64_t *rids, uint64_t *idx, hipStream_t s);
+// rowsOut[j] = payload[rids[j] - ridOffset]
+void gatherRows(const uint64_t *rids, uint64_t n, uint64_t ridOffset, const uint64_t *payload, uint64_t *rowsOut,
+                hipStream_t s);
+// out[idx[j] * stride + col .. + ROW_WORDS) = rows[j]
+void placeRows(const uint64_t *rows, const uint64_t *idx, uint64_t n, uint64_t *out, uint32_t strideWords,
+               uint32_t colWord, hipStream_t s);
 }  // namespace kernels
 }  // namespace hpcjoin

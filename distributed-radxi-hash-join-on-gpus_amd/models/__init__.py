@@ -11,3 +11,4 @@
 from .radix_join import JoinRun, RadixHashJoin  # noqa: F401
 from .npj import NoPartitionJoin  # noqa: F401
 from . import workloads  # noqa: F401
+from .tpch import TpchJoin  # noqa: F401

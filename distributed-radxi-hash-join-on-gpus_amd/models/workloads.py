@@ -23,16 +23,17 @@ class Workload:
     wide: bool = False
     materialize: bool = False
     payload_bytes: int = 0               # late-materialized payload per side (TPC-H-like)
+    tpch_sparse: bool = False            # TPC-H O_ORDERKEY layout on both sides
     gpus: int = 1
     description: str = ""
 
     def specs(self):
         C = require_native()
-        inner = C.GenSpec(distribution=C.KeyDistribution.UNIQUE, seed=self.inner_seed)
+        inner = C.GenSpec(C.KeyDistribution.UNIQUE, self.inner_seed, 0, 0, 0.75, self.tpch_sparse)
         dist = getattr(C.KeyDistribution, self.outer_distribution)
-        outer = C.GenSpec(distribution=dist, seed=self.outer_seed,
-                          domain=0 if self.outer_distribution in ("UNIQUE", "DENSE") else self.inner_size,
-                          zipf_theta=self.zipf_theta)
+        outer = C.GenSpec(dist, self.outer_seed,
+                          0 if self.outer_distribution in ("UNIQUE", "DENSE") else self.inner_size, 0,
+                          self.zipf_theta, self.tpch_sparse)
         return inner, outer
 
     def expected_matches(self) -> int | None:
@@ -74,7 +75,7 @@ PRESETS = {
     "zipf_1b_16b": Workload("zipf_1b_16b", B, 16 * B, "ZIPF", 0.75, gpus=8,
                             description="config 4: 1B x 16B Zipf(0.75) foreign keys, LPT assignment"),
     "tpch_sf1000": Workload("tpch_sf1000", 1_500_000_000, 6_000_000_000, "MODULO", materialize=True,
-                            payload_bytes=32, gpus=8,
+                            payload_bytes=32, tpch_sparse=True, gpus=8,
                             description="config 5: orders x lineitem (4 lineitems per order), 32-byte payloads "
                                         "gathered by rid after the join (late materialization)"),
     # the reference's default workload: 20M x 20M per rank (main.cpp:70-71)

@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""TPC-H-like orders x lineitem join with late materialization of 32-byte
+payloads (BASELINE config 5; SF1000 = 1.5B orders x 6B lineitems on 8 GPUs).
+
+One step = join (sparse o_orderkey layout, 4 lineitems per order) + fetching
+both payload rows of every result pair from their owner ranks.  Default size
+is SF100 per GPU (150M x 600M), which fits one MI355X with room for the
+60 GB output.  Prints one JSON line (rank 0).
+
+    python tools/bench_tpch.py [--sf-per-gpu 100] [--steps 5] [--warmup 1]
+    python -m torch.distributed.run --nproc-per-node N ... tools/bench_tpch.py
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+import hpcjoin  # noqa: E402
+from hpcjoin.models import workloads as W  # noqa: E402
+from hpcjoin.models.tpch import TpchJoin, verify_sample  # noqa: E402
+from hpcjoin.parallel import init_distributed, shutdown  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sf-per-gpu", type=float, default=100.0)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    args = ap.parse_args()
+    hpcjoin.require_native()
+    info = init_distributed()
+    sf = args.sf_per_gpu * info.world
+    if not torch.cuda.is_available():
+        sf = min(sf, 0.01)
+    wl = W.get("tpch_sf1000").scaled(sf / 1000.0)
+    t = TpchJoin(wl, info=info)
+    for _ in range(args.warmup):
+        t.run()
+    join_ms, mat_ms, tot_ms, ok = [], [], [], True
+    for _ in range(args.steps):
+        t.comm.barrier()
+        res, out = t.run()
+        join_ms.append(res["join_ms"])
+        mat_ms.append(res["materialize_ms"])
+        tot_ms.append(res["total_ms"])
+        ok &= res["global_matches"] == wl.expected_matches()
+    ok &= verify_sample(out, 256)
+    tot = sorted(tot_ms)[len(tot_ms) // 2]
+    if info.world > 1:  # slowest rank defines the step
+        import torch.distributed as dist
+        v = torch.tensor([tot], device="cuda" if torch.cuda.is_available() else "cpu")
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        tot = float(v.item())
+    if info.rank == 0:
+        print(json.dumps({
+            "metric": "TPC-H-like join + 32 B payload late materialization",
+            "value": (wl.inner_size + wl.outer_size) / tot / 1e6, "unit": "G input tuples/s",
+            "n_gpus": info.world, "scale_factor": sf, "orders": wl.inner_size, "lineitem": wl.outer_size,
+            "output_rows_local": int(out.shape[0]), "output_bytes_per_row": int(out.shape[1]) * 8,
+            "median_total_ms": tot, "median_join_ms": sorted(join_ms)[len(join_ms) // 2],
+            "median_materialize_ms": sorted(mat_ms)[len(mat_ms) // 2],
+            "matches": int(res["global_matches"]), "correct": bool(ok)}), flush=True)
+    del out, t
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    shutdown()
+    sys.exit(0 if ok else 3)
+
+
+if __name__ == "__main__":
+    main()
