@@ -125,7 +125,7 @@ def build(jobs: int | None = None, verbose: bool = False, with_cli: bool = True)
     tmp_out = out.with_name(out.name + ".tmp")
     _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *core_objs, *bind_objs, "-o", str(tmp_out),
           f"-L{tlib}", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10", f"-Wl,-rpath,{tlib}",
-          f"-L{ROCM}/lib", "-lrccl", "-lamdhip64"], verbose)
+          f"-L{ROCM}/lib", "-lrccl", "-lrocprofiler-sdk-roctx", "-lamdhip64"], verbose)
     os.replace(tmp_out, out)
 
     if with_cli:
@@ -135,7 +135,7 @@ def build(jobs: int | None = None, verbose: bool = False, with_cli: bool = True)
         if not cli_obj.exists():
             _run([HIPCC, *f, "-c", str(cli_src), "-o", str(cli_obj)], verbose)
         _run([HIPCC, f"--offload-arch={ARCH}", str(cli_obj), *core_objs, "-o", str(BUILD / "bin" / "hjoin_bench"),
-              f"-L{ROCM}/lib", "-lrccl", "-lamdhip64", "-lpthread"], verbose)
+              f"-L{ROCM}/lib", "-lrccl", "-lrocprofiler-sdk-roctx", "-lamdhip64", "-lpthread"], verbose)
     return out
 
 

@@ -21,6 +21,7 @@
 #include "../operators/HashJoin.h"
 #include "../operators/LateMaterialization.h"
 #include "../performance/Measurements.h"
+#include "../utils/Fault.h"
 #include "../utils/Hip.h"
 #include "ProcessGroupCommunicator.h"
 
@@ -479,6 +480,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("size", &comm::Communicator::size)
       .def("name", &comm::Communicator::name)
       .def("barrier", &comm::Communicator::barrier, py::call_guard<py::gil_scoped_release>())
+      .def("check_health", &comm::Communicator::checkHealth)
+      .def("abort", &comm::Communicator::abort, py::arg("why"), py::call_guard<py::gil_scoped_release>())
       .def("all_gather", [](comm::Communicator &c, std::vector<uint64_t> v) {
         std::vector<uint64_t> out(v.size() * c.size());
         {
@@ -528,6 +531,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<comm::InProcessGroup, std::shared_ptr<comm::InProcessGroup>>(m, "InProcessGroup")
       .def(py::init<uint32_t>(), py::arg("size"))
       .def("size", &comm::InProcessGroup::size)
+      .def("abort", &comm::InProcessGroup::abort, py::arg("why"))
+      .def("aborted", &comm::InProcessGroup::aborted)
       .def("communicator", [](std::shared_ptr<comm::InProcessGroup> g, uint32_t rank) {
         return std::static_pointer_cast<comm::Communicator>(std::make_shared<comm::InProcessCommunicator>(g, rank));
       });
@@ -708,6 +713,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         return out;
       });
   m.def("result_counter", []() { return operators::HashJoin::RESULT_COUNTER; });
+
+  auto fault = m.def_submodule("fault", "failure detection and fault injection");
+  py::register_exception<utils::InjectedFault>(fault, "InjectedFault", PyExc_RuntimeError);
+  fault.def("arm", &utils::armFault, py::arg("phase"), py::arg("rank") = -1,
+            "Arm a one-shot fault for the calling thread at phase histogram|network|local|build_probe "
+            "(rank -1: any rank).  An empty phase disarms.");
+  fault.def("set_comm_timeout_ms", &utils::setCommTimeoutMs, py::arg("ms"));
+  fault.def("comm_timeout_ms", &utils::commTimeoutMs);
 
   auto meas = m.def_submodule("measurements");
   meas.def("init", &performance::Measurements::init, py::arg("node_id"), py::arg("number_of_nodes"),

@@ -29,6 +29,12 @@ class Communicator {
   // Where allToAllV buffers must live (Device for RCCL, Host for gloo).
   virtual bool supports(Location loc) const = 0;
   virtual std::string name() const = 0;
+  // Failure detection: throw if the communicator has seen an asynchronous
+  // error (RCCL) or a peer aborted (in-process).  Polled by blocking waits.
+  virtual void checkHealth() {}
+  // Tear the communicator down so that peers blocked in collectives fail
+  // instead of hanging (ncclCommAbort / group abort).  Idempotent.
+  virtual void abort(const std::string &why) { (void)why; }
 
   // recv[r * count + i] = rank r's send[i]   (host buffers, blocking)
   virtual void allGatherHost(const uint64_t *send, uint64_t *recv, size_t count) = 0;

@@ -1,7 +1,9 @@
 #include "InProcessCommunicator.h"
 
+#include <chrono>
 #include <cstring>
 
+#include "../utils/Fault.h"
 #include "../utils/Hip.h"
 
 namespace hpcjoin {
@@ -12,14 +14,43 @@ InProcessGroup::InProcessGroup(uint32_t size)
 
 void InProcessGroup::barrier() {
   std::unique_lock<std::mutex> lk(m_);
+  JOIN_ASSERT(!aborted_, "InProcess", "group aborted: %s", reason_.c_str());
   const uint64_t gen = generation_;
   if (++waiting_ == size_) {
     waiting_ = 0;
     ++generation_;
     cv_.notify_all();
-  } else {
-    cv_.wait(lk, [&] { return generation_ != gen; });
+    return;
   }
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(utils::commTimeoutMs());
+  if (!cv_.wait_until(lk, deadline, [&] { return generation_ != gen || aborted_; })) {
+    aborted_ = true;
+    reason_ = utils::format("barrier timed out after %lu ms with %u of %u ranks present",
+                            (unsigned long)utils::commTimeoutMs(), waiting_, size_);
+    cv_.notify_all();
+  }
+  if (generation_ == gen) {  // woken by an abort, not by the last arrival
+    --waiting_;
+    JOIN_ASSERT(false, "InProcess", "group aborted: %s", reason_.c_str());
+  }
+}
+
+void InProcessGroup::abort(const std::string &why) {
+  std::lock_guard<std::mutex> lk(m_);
+  if (!aborted_) {
+    aborted_ = true;
+    reason_ = why;
+  }
+  cv_.notify_all();
+}
+
+bool InProcessGroup::aborted() {
+  std::lock_guard<std::mutex> lk(m_);
+  return aborted_;
+}
+
+void InProcessCommunicator::checkHealth() {
+  JOIN_ASSERT(!group_->aborted(), "InProcess", "a peer rank aborted the group");
 }
 
 void InProcessCommunicator::allGatherHost(const uint64_t *send, uint64_t *recv, size_t count) {

@@ -11,6 +11,7 @@
 #include <condition_variable>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "Communicator.h"
@@ -22,7 +23,11 @@ class InProcessGroup {
  public:
   explicit InProcessGroup(uint32_t size);
   uint32_t size() const { return size_; }
+  // Blocks until all ranks arrive.  Throws if the group was aborted (a peer
+  // failed) or after utils::commTimeoutMs(), aborting the group itself then.
   void barrier();
+  void abort(const std::string &why);
+  bool aborted();
   // Shared slots: each rank publishes one pointer-sized value per phase.
   std::vector<const void *> slots;
   std::vector<const uint64_t *> counts, displs;
@@ -34,6 +39,8 @@ class InProcessGroup {
   std::condition_variable cv_;
   uint32_t waiting_ = 0;
   uint64_t generation_ = 0;
+  bool aborted_ = false;
+  std::string reason_;
 };
 
 class InProcessCommunicator : public Communicator {
@@ -46,6 +53,8 @@ class InProcessCommunicator : public Communicator {
   void allGatherHost(const uint64_t *send, uint64_t *recv, size_t count) override;
   void allReduceSumHost(uint64_t *data, size_t count) override;
   void barrier() override { group_->barrier(); }
+  void checkHealth() override;
+  void abort(const std::string &why) override { group_->abort(why); }
   void allToAllV(const uint64_t *send, const uint64_t *sendCounts, const uint64_t *sendDispls, uint64_t *recv,
                  const uint64_t *recvCounts, const uint64_t *recvDispls, Location loc, hipStream_t stream) override;
 

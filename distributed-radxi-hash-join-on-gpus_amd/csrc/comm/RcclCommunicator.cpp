@@ -4,6 +4,7 @@
 
 #include <cstring>
 
+#include "../utils/Fault.h"
 #include "../utils/Hip.h"
 
 #define RCCL_CHECK(expr)                                                                      \
@@ -40,6 +41,24 @@ RcclCommunicator::RcclCommunicator(const std::vector<uint8_t> &id, uint32_t rank
   comm_ = c;
 }
 
+void RcclCommunicator::checkHealth() {
+  JOIN_ASSERT(comm_ != nullptr, "RCCL", "communicator was aborted: %s", abortReason_.c_str());
+  ncclResult_t st = ncclSuccess;
+  RCCL_CHECK(ncclCommGetAsyncError(static_cast<ncclComm_t>(comm_), &st));
+  if (st != ncclSuccess && st != ncclInProgress) {
+    std::string why = utils::format("asynchronous RCCL error: %s", ncclGetErrorString(st));
+    abort(why);
+    utils::fail("RCCL", __FILE__, __LINE__, why);
+  }
+}
+
+void RcclCommunicator::abort(const std::string &why) {
+  if (!comm_) return;
+  abortReason_ = why;
+  (void)ncclCommAbort(static_cast<ncclComm_t>(comm_));
+  comm_ = nullptr;
+}
+
 RcclCommunicator::~RcclCommunicator() {
   if (comm_) ncclCommDestroy(static_cast<ncclComm_t>(comm_));
   if (scratch_) (void)hipFree(scratch_);
@@ -58,17 +77,19 @@ uint64_t *RcclCommunicator::scratch(size_t words) {
 void RcclCommunicator::allGatherHost(const uint64_t *send, uint64_t *recv, size_t count) {
   uint64_t *buf = scratch(count * size_);
   HIP_CHECK(hipMemcpyAsync(buf + count * rank_, send, count * 8, hipMemcpyHostToDevice, stream_));
+  checkHealth();
   RCCL_CHECK(ncclAllGather(buf + count * rank_, buf, count, ncclUint64, static_cast<ncclComm_t>(comm_), stream_));
   HIP_CHECK(hipMemcpyAsync(recv, buf, count * size_ * 8, hipMemcpyDeviceToHost, stream_));
-  HIP_CHECK(hipStreamSynchronize(stream_));
+  utils::waitStream(stream_, this, "ncclAllGather");
 }
 
 void RcclCommunicator::allReduceSumHost(uint64_t *data, size_t count) {
   uint64_t *buf = scratch(count);
   HIP_CHECK(hipMemcpyAsync(buf, data, count * 8, hipMemcpyHostToDevice, stream_));
+  checkHealth();
   RCCL_CHECK(ncclAllReduce(buf, buf, count, ncclUint64, ncclSum, static_cast<ncclComm_t>(comm_), stream_));
   HIP_CHECK(hipMemcpyAsync(data, buf, count * 8, hipMemcpyDeviceToHost, stream_));
-  HIP_CHECK(hipStreamSynchronize(stream_));
+  utils::waitStream(stream_, this, "ncclAllReduce");
 }
 
 void RcclCommunicator::barrier() {
@@ -80,6 +101,7 @@ void RcclCommunicator::allToAllV(const uint64_t *send, const uint64_t *sendCount
                                  uint64_t *recv, const uint64_t *recvCounts, const uint64_t *recvDispls,
                                  Location loc, hipStream_t stream) {
   JOIN_ASSERT(loc == Location::Device, "RCCL", "all-to-all buffers must be in HBM");
+  checkHealth();
   ncclComm_t c = static_cast<ncclComm_t>(comm_);
   // Own slice: plain D2D copy on the same stream (no RCCL channel needed).
   HJ_CHECK(sendCounts[rank_] == recvCounts[rank_], "self slice mismatch %lu != %lu",

@@ -6,6 +6,7 @@
 // collective would be per-link bound.
 #pragma once
 
+#include <string>
 #include <vector>
 
 #include "Communicator.h"
@@ -31,6 +32,8 @@ class RcclCommunicator : public Communicator {
   void allToAllV(const uint64_t *send, const uint64_t *sendCounts, const uint64_t *sendDispls, uint64_t *recv,
                  const uint64_t *recvCounts, const uint64_t *recvDispls, Location loc, hipStream_t stream) override;
   int device() const { return device_; }
+  void checkHealth() override;
+  void abort(const std::string &why) override;
 
  private:
   uint64_t *scratch(size_t words);
@@ -40,6 +43,7 @@ class RcclCommunicator : public Communicator {
   hipStream_t stream_ = nullptr;  // for the small blocking collectives
   uint64_t *scratch_ = nullptr;
   size_t scratchWords_ = 0;
+  std::string abortReason_;
 };
 
 }  // namespace comm

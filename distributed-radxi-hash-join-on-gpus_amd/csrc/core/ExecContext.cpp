@@ -4,6 +4,7 @@
 
 #include "../comm/Communicator.h"
 #include "../memory/Arena.h"
+#include "../utils/Fault.h"
 #include "../utils/Hip.h"
 
 namespace hpcjoin {
@@ -36,6 +37,11 @@ uint32_t ExecContext::numberOfNodes() const { return comm_->size(); }
 
 void ExecContext::synchronize() const {
   if (!onDevice()) return;
+  if (comm_->size() > 1) {  // a lost peer must not hang this rank forever
+    utils::waitStream(commStream_, comm_, "exchange stream");
+    utils::waitStream(stream_, comm_, "compute stream");
+    return;
+  }
   HIP_CHECK(hipStreamSynchronize(commStream_));
   HIP_CHECK(hipStreamSynchronize(stream_));
 }

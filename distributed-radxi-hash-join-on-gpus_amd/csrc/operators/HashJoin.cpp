@@ -8,10 +8,12 @@
 #include "../memory/Arena.h"
 #include "../performance/Clock.h"
 #include "../performance/Measurements.h"
+#include "../performance/Trace.h"
 #include "../tasks/BuildProbe.h"
 #include "../tasks/HistogramComputation.h"
 #include "../tasks/LocalPartitioning.h"
 #include "../tasks/NetworkPartitioning.h"
+#include "../utils/Fault.h"
 #include "../utils/Hip.h"
 
 namespace hpcjoin {
@@ -90,6 +92,20 @@ void HashJoin::join() {
 }
 
 JoinResult HashJoin::run() {
+  try {
+    return runImpl();
+  } catch (const std::exception &e) {
+    while (!TASK_QUEUE.empty()) {
+      delete TASK_QUEUE.front();
+      TASK_QUEUE.pop();
+    }
+    ctx->comm()->abort(e.what());
+    throw;
+  }
+}
+
+JoinResult HashJoin::runImpl() {
+  performance::TraceRange traceJoin("hpcjoin::join");
   result = JoinResult();
   result.innerLocal = innerRelation->getLocalSize();
   result.outerLocal = outerRelation->getLocalSize();
@@ -105,6 +121,8 @@ JoinResult HashJoin::run() {
 
   // ---------------------------------------------------------------- histogram
   Measurements::startHistogramComputation();
+  utils::faultPoint("histogram");
+  std::unique_ptr<performance::TraceRange> trace(new performance::TraceRange("histogram"));
   tasks::HistogramComputation hc(numberOfNodes, nodeId, innerRelation, outerRelation, ctx, plan,
                                  config.maxPartitionBlocks);
   hc.execute();
@@ -125,6 +143,9 @@ JoinResult HashJoin::run() {
 
   // ------------------------------------------------------------------ network
   Measurements::startNetworkPartitioning();
+  trace.reset();  // roctx ranges nest: pop before the next push
+  utils::faultPoint("network");
+  trace.reset(new performance::TraceRange("network_partitioning"));
   {
     tasks::NetworkPartitioning np(nodeId, innerRelation, outerRelation, &innerWindow, &outerWindow, &hc, ctx, plan);
     np.execute();
@@ -148,23 +169,32 @@ JoinResult HashJoin::run() {
 
   // -------------------------------------------------------------------- local
   Measurements::startLocalProcessingPreparations();
+  trace.reset();  // roctx ranges nest: pop before the next push
+  utils::faultPoint("local");
+  trace.reset(new performance::TraceRange("local_processing"));
   auto *lp = new tasks::LocalPartitioning(&innerWindow, &outerWindow, ctx, plan);
   TASK_QUEUE.push(lp);
   Measurements::stopLocalProcessingPreparations();
   Measurements::startLocalProcessing();
-  tasks::BuildProbe *bp = nullptr;
+  std::unique_ptr<tasks::BuildProbe> bp;
   while (!TASK_QUEUE.empty()) {
-    tasks::Task *t = TASK_QUEUE.front();
+    std::unique_ptr<tasks::Task> t(TASK_QUEUE.front());
     TASK_QUEUE.pop();
+    if (t->getType() == TASK_BUILD_PROBE) {
+      t.release();  // owned by bp
+      utils::faultPoint("build_probe");
+      bp->execute();
+      continue;
+    }
     t->execute();
     if (t->getType() == TASK_PARTITION) {
       if (dev) HIP_CHECK(hipEventRecord(ev[3], ctx->stream()));
       result.localItems = lp->workItems();
-      bp = new tasks::BuildProbe(&innerWindow, &outerWindow, ctx, plan, config.outputCapacity);
-      TASK_QUEUE.push(bp);
-      delete t;
+      bp.reset(new tasks::BuildProbe(&innerWindow, &outerWindow, ctx, plan, config.outputCapacity));
+      TASK_QUEUE.push(bp.get());
     }
   }
+  trace.reset();  // roctx ranges nest: pop before the next push
   if (dev) HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
   ctx->synchronize();
   while (bp->collect()) {  // rare: item list or output buffer overflowed -> exact re-run
@@ -181,7 +211,7 @@ JoinResult HashJoin::run() {
   result.outputOverflow = bp->outputOverflowed();
   result.buildProbeItems = bp->getWorkItems();
   output = bp->getOutput();
-  delete bp;
+  bp.reset();
   result.innerReceived = innerWindow.computeLocalWindowSize();
   result.outerReceived = outerWindow.computeLocalWindowSize();
   Measurements::storeLocalPartitioningDetails(result.innerReceived + result.outerReceived, result.localItems);

@@ -48,7 +48,10 @@ class HashJoin {
   ~HashJoin();
 
   void join();        // reference API: runs, updates RESULT_COUNTER (local matches)
-  JoinResult run();   // one full join
+  // One full join.  If any phase throws on this rank (HIP/RCCL error,
+  // failed invariant, injected fault, watchdog timeout), the pending tasks are
+  // dropped and the communicator is aborted so peers fail instead of hanging.
+  JoinResult run();
   const JoinResult &lastResult() const { return result; }
   const core::JoinPlan &getPlan() const { return plan; }
   const core::JoinConfig &getConfig() const { return config; }
@@ -69,6 +72,7 @@ class HashJoin {
 
  private:
   void makeJoinPlan();
+  JoinResult runImpl();
   core::ExecContext *ctx;
   std::unique_ptr<core::ExecContext> ownedCtx;
   core::JoinConfig config;

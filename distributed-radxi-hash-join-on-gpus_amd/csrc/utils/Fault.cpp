@@ -1,0 +1,78 @@
+#include "Fault.h"
+
+#include <atomic>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+
+#include "../comm/Communicator.h"
+#include "Hip.h"
+
+namespace hpcjoin {
+namespace utils {
+
+namespace {
+thread_local std::string t_phase;
+thread_local int t_rank = -1;
+thread_local bool t_armed = false;
+std::atomic<uint64_t> g_timeoutMs{0};
+
+bool envFault(const char *phase) {
+  const char *e = std::getenv("HPCJOIN_FAULT");
+  if (!e || !e[0]) return false;
+  const char *colon = std::strchr(e, ':');
+  const size_t n = colon ? (size_t)(colon - e) : std::strlen(e);
+  if (std::strlen(phase) != n || std::strncmp(e, phase, n) != 0) return false;
+  return !colon || std::atoi(colon + 1) == debugRank();
+}
+}  // namespace
+
+void armFault(const std::string &phase, int rank) {
+  t_phase = phase;
+  t_rank = rank;
+  t_armed = !phase.empty();
+}
+
+void faultPoint(const char *phase) {
+  const bool hit = (t_armed && t_phase == phase && (t_rank < 0 || t_rank == debugRank())) || envFault(phase);
+  if (hit) {
+    t_armed = false;  // one shot
+    throw InjectedFault(format("[FAULT][rank %d] injected fault at phase '%s'", debugRank(), phase));
+  }
+}
+
+uint64_t commTimeoutMs() {
+  uint64_t v = g_timeoutMs.load(std::memory_order_relaxed);
+  if (v) return v;
+  const char *e = std::getenv("HPCJOIN_COMM_TIMEOUT_S");
+  v = (e && e[0]) ? (uint64_t)(std::atof(e) * 1000.0) : 600000;
+  return v ? v : 1;
+}
+
+void setCommTimeoutMs(uint64_t ms) { g_timeoutMs.store(ms, std::memory_order_relaxed); }
+
+void waitStream(hipStream_t stream, comm::Communicator *comm, const char *what) {
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  const auto deadline = t0 + std::chrono::milliseconds(commTimeoutMs());
+  for (uint64_t spin = 0;; ++spin) {
+    hipError_t e = hipStreamQuery(stream);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) HIP_CHECK(e);
+    if (comm) comm->checkHealth();
+    const auto now = clk::now();
+    if (now > deadline) {
+      std::string why = format("%s did not complete within %lu ms", what, (unsigned long)commTimeoutMs());
+      if (comm) comm->abort(why);
+      fail("WATCHDOG", __FILE__, __LINE__, why);
+    }
+    // Short spin first (most waits end within microseconds of the last
+    // kernel), then back off so a stuck collective does not burn a core.
+    if (spin < 2000) std::this_thread::yield();
+    else std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
+}  // namespace utils
+}  // namespace hpcjoin

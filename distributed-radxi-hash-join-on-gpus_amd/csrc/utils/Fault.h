@@ -1,0 +1,43 @@
+// Failure detection and fault injection (the reference has none --
+// MPI errors are fatal and most CUDA errors unchecked).
+//
+// * faultPoint(phase): deterministic fault injection.  A fault is armed either
+//   programmatically per thread (in-process ranks are threads) or through
+//   HPCJOIN_FAULT="<phase>[:<rank>]" in the environment; the armed rank throws
+//   InjectedFault when it reaches that phase.  Tests use it to prove that a
+//   failing rank does not hang its peers.
+// * commTimeoutMs(): deadline for every blocking wait on communication
+//   (HPCJOIN_COMM_TIMEOUT_S, default 600 s).  Waits poll the communicator's
+//   health (RCCL async errors, aborted in-process groups) and give up with an
+//   exception instead of hanging forever.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+namespace hpcjoin {
+namespace comm {
+class Communicator;
+}
+namespace utils {
+
+struct InjectedFault : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+// Arm a fault for the calling thread (rank < 0: any rank). Empty phase disarms.
+void armFault(const std::string &phase, int rank = -1);
+void faultPoint(const char *phase);
+
+uint64_t commTimeoutMs();
+void setCommTimeoutMs(uint64_t ms);  // process-wide override (tests)
+
+// Wait until `stream` is idle.  Polls comm->checkHealth() and throws after
+// commTimeoutMs() (after aborting the communicator so peers fail fast, too).
+void waitStream(hipStream_t stream, comm::Communicator *comm, const char *what);
+
+}  // namespace utils
+}  // namespace hpcjoin
