@@ -73,6 +73,11 @@ def verify_sample(out: torch.Tensor, k: int = 64) -> bool:
     """Spot-check k output rows: payloads must be those of the rids they carry."""
     if out.shape[0] == 0:
         return True
-    sel = out[torch.linspace(0, out.shape[0] - 1, min(k, out.shape[0])).long()].cpu()
+    n = out.shape[0]
+    k = min(k, n)
+    # integer sample positions (a float linspace rounds past the last row at 6e8 rows)
+    pos = torch.arange(k, dtype=torch.int64) * (n - 1) // max(k - 1, 1)
+    assert int(pos.max()) < n
+    sel = out[pos.to(out.device)].cpu()
     return bool(torch.equal(sel[:, 2:6], payload_reference(sel[:, 0], ORDERS_SEED)) and
                 torch.equal(sel[:, 6:10], payload_reference(sel[:, 1], LINEITEM_SEED)))
