@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--dist", default="unique", choices=["unique", "uniform", "zipf", "modulo"])
     ap.add_argument("--theta", type=float, default=0.75)
     ap.add_argument("--chunks", type=int, default=0, help="exchange pipeline slices (0 = auto)")
+    ap.add_argument("--input", default="device", choices=["device", "pinned"],
+                    help="where the relations live: HBM, or pinned host memory read in place over the host link")
     ap.add_argument("--json-out", default="")
     args = ap.parse_args()
 
@@ -58,8 +60,9 @@ def main():
     outer = C.GenSpec(distribution=dmap[args.dist], seed=4321, domain=0 if args.dist == "unique" else G_R,
                       zipf_theta=args.theta)
     lr, ls = (C.Relation.local_size_for(G, info.rank, info.world) for G in (G_R, G_S))
-    R = C.Relation(lr, G_R, loc, info.local_rank)
-    S = C.Relation(ls, G_S, loc, info.local_rank)
+    rel_loc = "pinned" if on_gpu and args.input == "pinned" else loc
+    R = C.Relation(lr, G_R, rel_loc, info.local_rank)
+    S = C.Relation(ls, G_S, rel_loc, info.local_rank)
     R.generate(inner, C.Relation.local_offset_for(G_R, info.rank, info.world))
     S.generate(outer, C.Relation.local_offset_for(G_S, info.rank, info.world))
     expected = C.Relation.expected_matches(inner, G_R, outer, G_S)
@@ -119,6 +122,7 @@ def main():
                 else "single MI355X",
                 "plan": repr(join.plan),
                 "chunks": cfg.chunks,
+                "input": rel_loc,
             },
             "matches": results[-1]["global_matches"],
             "expected_matches": expected,

@@ -382,6 +382,39 @@ double benchRead(const at::Tensor &src, int iters) {
       iters);
 }
 
+// Host-link ceilings (the reference's dormant UVA_benchmark,
+// operators/gpu/small_data_optimized.cu): DMA copies both ways between pinned
+// host memory and HBM, and kernels reading pinned memory in place (the path
+// the engine uses for relations kept in pinned host memory).
+py::dict benchHostLink(uint64_t bytes, int device, int iters) {
+  HIP_CHECK(hipSetDevice(device));
+  bytes = std::max<uint64_t>(16, bytes / 16 * 16);
+  void *h = memory::Arena::rawAlloc(Location::Pinned, bytes, device);
+  void *d = memory::Arena::rawAlloc(Location::Device, bytes, device);
+  unsigned long long *sink = static_cast<unsigned long long *>(memory::Arena::rawAlloc(Location::Device, 8, device));
+  std::memset(h, 1, bytes);
+  py::dict out;
+  try {
+    const double h2d = timeDevice([&](hipStream_t s) { HIP_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s)); }, iters);
+    const double d2h = timeDevice([&](hipStream_t s) { HIP_CHECK(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s)); }, iters);
+    const double zc = timeDevice(
+        [&](hipStream_t s) { kernels::readKernel(static_cast<const ulonglong2 *>(h), bytes / 16, sink, s); }, iters);
+    out["bytes"] = bytes;
+    out["h2d_GBps"] = bytes / h2d / 1e6;
+    out["d2h_GBps"] = bytes / d2h / 1e6;
+    out["zero_copy_read_GBps"] = bytes / zc / 1e6;
+  } catch (...) {
+    memory::Arena::rawFree(Location::Pinned, h);
+    memory::Arena::rawFree(Location::Device, d);
+    memory::Arena::rawFree(Location::Device, sink);
+    throw;
+  }
+  memory::Arena::rawFree(Location::Pinned, h);
+  memory::Arena::rawFree(Location::Device, d);
+  memory::Arena::rawFree(Location::Device, sink);
+  return out;
+}
+
 py::dict resultToDict(const operators::JoinResult &r) {
   py::dict d;
   d["local_matches"] = r.localMatches;
@@ -551,6 +584,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   py::class_<core::ExecContext, std::shared_ptr<core::ExecContext>>(m, "ExecContext")
       .def(py::init([](const std::string &loc, int device, std::shared_ptr<comm::Communicator> c) {
+             TORCH_CHECK(loc == "device" || loc == "host", "engine location must be device|host");
              auto ctx = std::shared_ptr<core::ExecContext>(
                  new core::ExecContext(loc == "device" ? Location::Device : Location::Host, device, c.get()),
                  [c](core::ExecContext *p) { delete p; });
@@ -602,8 +636,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<PyRelation>(m, "Relation")
       .def(py::init([](uint64_t localSize, uint64_t globalSize, const std::string &loc, int device) {
              PyRelation r;
-             r.rel = std::make_shared<data::Relation>(localSize, globalSize,
-                                                      loc == "device" ? Location::Device : Location::Host, device);
+             TORCH_CHECK(loc == "device" || loc == "host" || loc == "pinned", "location must be device|host|pinned");
+             r.rel = std::make_shared<data::Relation>(
+                 localSize, globalSize,
+                 loc == "device" ? Location::Device : (loc == "pinned" ? Location::Pinned : Location::Host), device);
              return r;
            }),
            py::arg("local_size"), py::arg("global_size"), py::arg("location") = "device", py::arg("device") = 0)
@@ -769,6 +805,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   ops.def("net_scatter_global_atomic", &opNetScatterGlobalAtomic);
   ops.def("bench_copy_ms", &benchCopy, py::arg("src"), py::arg("dst"), py::arg("iters") = 10);
   ops.def("bench_read_ms", &benchRead, py::arg("src"), py::arg("iters") = 10);
+  ops.def("bench_host_link", &benchHostLink, py::arg("bytes") = (uint64_t)1 << 30, py::arg("device") = 0,
+          py::arg("iters") = 5);
   ops.def("bench_scatter_ms", &benchScatter, py::arg("tuples"), py::arg("bits"), py::arg("mode") = 0,
           py::arg("iters") = 10, py::arg("max_blocks") = 2048, py::arg("geometry") = 0);
   ops.def("bench_histogram_ms", &benchHistogram, py::arg("tuples"), py::arg("bits"), py::arg("iters") = 10);

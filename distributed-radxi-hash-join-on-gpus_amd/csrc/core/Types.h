@@ -16,9 +16,17 @@ namespace hpcjoin {
 // Where a buffer lives.  The engine has exactly two execution targets: the
 // MI355X (HBM, HIP kernels) and the single-thread host reference path that
 // mirrors the reference's CPU semantics (plumbing config 1 / test oracle).
-enum class Location : int { Host = 0, Device = 1 };
+// Host: pageable host memory (host engine).  Device: HBM.  Pinned: page-locked
+// host memory mapped into the GPU address space -- relations larger than HBM
+// stay there and the device kernels read them over the host link (the
+// reference's dormant UVA / out-of-GPU-memory path).
+enum class Location : int { Host = 0, Device = 1, Pinned = 2 };
 
-inline const char *locationName(Location l) { return l == Location::Device ? "device" : "host"; }
+inline const char *locationName(Location l) {
+  return l == Location::Device ? "device" : (l == Location::Pinned ? "pinned" : "host");
+}
+// Can device kernels dereference memory at this location?
+inline bool deviceAccessible(Location l) { return l != Location::Host; }
 
 HJ_HD uint32_t ceilLog2(uint64_t x) {
   uint32_t b = 0;

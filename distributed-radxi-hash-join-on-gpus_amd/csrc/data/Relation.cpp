@@ -50,7 +50,7 @@ uint64_t Relation::localOffsetFor(uint64_t globalSize, uint32_t nodeId, uint32_t
 }
 
 static void runGenerate(Tuple *out, uint64_t n, const kernels::GenParams &p, Location loc, int device) {
-  if (loc == Location::Device) {
+  if (deviceAccessible(loc)) {  // pinned: the GPU writes host memory over the host link
     HIP_CHECK(hipSetDevice(device));
     kernels::generate(out, n, p, nullptr);
     HIP_CHECK(hipDeviceSynchronize());
@@ -143,6 +143,7 @@ void Relation::distribute(uint32_t nodeId, uint32_t numberOfNodes, comm::Communi
   // Reference (Relation.cpp:99-141): pairwise swap of sections, then reshuffle.
   // Here: section k of every rank goes to rank k in one all-to-all.
   if (numberOfNodes <= 1) return;
+  JOIN_ASSERT(loc_ != Location::Pinned, "Relation", "distribute() of a pinned host relation is not supported");
   JOIN_ASSERT(comm && comm->size() == numberOfNodes && comm->rank() == nodeId, "Relation",
               "distribute needs the job communicator");
   std::vector<uint64_t> sendCounts(numberOfNodes), sendDispls(numberOfNodes), recvCounts(numberOfNodes),
@@ -178,8 +179,8 @@ void Relation::distribute(uint32_t nodeId, uint32_t numberOfNodes, comm::Communi
 void Relation::debugKeyPrint(uint64_t limit) {
   const uint64_t n = std::min(limit, localSize);
   std::vector<Tuple> h(n);
-  if (loc_ == Location::Device)
-    HIP_CHECK(hipMemcpy(h.data(), data, n * sizeof(Tuple), hipMemcpyDeviceToHost));
+  if (deviceAccessible(loc_))
+    HIP_CHECK(hipMemcpy(h.data(), data, n * sizeof(Tuple), hipMemcpyDefault));
   else
     std::memcpy(h.data(), data, n * sizeof(Tuple));
   for (uint64_t i = 0; i < n; ++i) std::fprintf(stdout, "%lu, ", (unsigned long)h[i].key);

@@ -15,6 +15,9 @@ void *Arena::rawAlloc(Location loc, uint64_t bytes, int device) {
   if (loc == Location::Device) {
     HIP_CHECK(hipSetDevice(device));
     HIP_CHECK(hipMalloc(&p, bytes));
+  } else if (loc == Location::Pinned) {
+    HIP_CHECK(hipSetDevice(device));
+    HIP_CHECK(hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable));
   } else {
     int r = posix_memalign(&p, ALIGNMENT, bytes);
     JOIN_ASSERT(r == 0 && p, "Arena", "posix_memalign(%lu) failed", (unsigned long)bytes);
@@ -26,6 +29,8 @@ void Arena::rawFree(Location loc, void *p) {
   if (!p) return;
   if (loc == Location::Device)
     (void)hipFree(p);  // never throw from a destructor path
+  else if (loc == Location::Pinned)
+    (void)hipHostFree(p);
   else
     std::free(p);
 }

@@ -50,8 +50,13 @@ HashJoin::~HashJoin() {
 }
 
 void HashJoin::makeJoinPlan() {
-  JOIN_ASSERT(innerRelation->location() == ctx->location() && outerRelation->location() == ctx->location(),
-              "HashJoin", "relations must live where the engine runs (%s)", locationName(ctx->location()));
+  // A device engine also reads pinned host relations in place (zero-copy over
+  // the host link: joins whose inputs exceed HBM).
+  auto usable = [&](data::Relation *r) {
+    return r->location() == ctx->location() || (ctx->onDevice() && r->location() == Location::Pinned);
+  };
+  JOIN_ASSERT(usable(innerRelation) && usable(outerRelation), "HashJoin",
+              "relations must live where the engine runs (%s) or in pinned host memory", locationName(ctx->location()));
   // Max key / rid over both relations and all ranks (the plan must be identical everywhere).
   uint64_t mx[2] = {0, 0};
   for (data::Relation *r : {innerRelation, outerRelation}) {

@@ -101,3 +101,9 @@ def scatter_ablation(n=1 << 28, bits_list=(4, 8, 10), iters=5, geometries=(0,)):
                 row["error"] = str(e).split("(")[0]
             out.append(row)
     return out
+
+
+def host_link(bytes_: int = 1 << 30, device: int = 0, iters: int = 5) -> dict:
+    """Host-link ceilings: DMA H2D / D2H and in-place kernel reads of pinned
+    host memory (the engine's path for relations kept in pinned memory)."""
+    return dict(require_native().ops.bench_host_link(bytes_, device, iters))

@@ -58,3 +58,20 @@ def test_join_repeatable(C, dev):
 def test_join_large_device(C, cuda, G):
     res, exp, j = run_join(C, "cuda", G, G)
     assert res["global_matches"] == exp
+
+
+@pytest.mark.gpu
+def test_pinned_host_relations(C, cuda):
+    """Relations in pinned host memory are joined in place by the device engine
+    (zero-copy reads over the host link: inputs larger than HBM)."""
+    n = 1 << 22
+    ctx = C.ExecContext("device", 0, C.LocalCommunicator())
+    R = C.Relation(n, n, "pinned", 0)
+    S = C.Relation(n, n, "pinned", 0)
+    assert R.location() == "pinned"
+    R.generate(C.GenSpec(seed=11), 0)
+    S.generate(C.GenSpec(seed=12), 0)
+    j = C.HashJoin(R, S, ctx, C.JoinConfig())
+    assert j.run()["global_matches"] == n
+    link = C.ops.bench_host_link(1 << 26, 0, 2)
+    assert link["h2d_GBps"] > 1 and link["zero_copy_read_GBps"] > 1

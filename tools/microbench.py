@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run the per-phase micro-benchmarks on cuda:0 and print one JSON line each.
 
-    python tools/microbench.py [copy|partition|local|bp|npj|all] [--n N] [--bits B]
+    python tools/microbench.py [copy|host_link|partition|local|bp|npj|ablation|all] [--n N] [--bits B]
 """
 import argparse
 import json
@@ -20,10 +20,12 @@ def main():
     ap.add_argument("--bits", type=int, default=10)
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()
-    todo = ["copy", "partition", "local", "bp", "npj"] if a.what == "all" else [a.what]
+    todo = ["copy", "host_link", "partition", "local", "bp", "npj"] if a.what == "all" else [a.what]
     for w in todo:
         if w == "copy":
             r = mb.copy_ceiling()
+        elif w == "host_link":
+            r = mb.host_link()
         elif w == "partition":
             r = mb.partition_phase(a.n, a.bits, iters=a.iters)
         elif w == "local":
