@@ -103,14 +103,23 @@ void bpEmit(const BPArgs &a, const uint32_t *counts, const uint32_t *offsets, BP
 }
 
 // Wave-aggregated output reservation: every lane of the (converged) wave calls
-// this with its number of register-held matches; returns the lane's base slot.
-__device__ __forceinline__ unsigned long long reserveOutput(uint32_t mine, unsigned long long *cursor) {
+// this with its number of register-held matches; returns the lane's slot.
+// With item offsets (two-pass materialization) the wave claims from the
+// item's LDS cursor; otherwise from the global cursor (single pass).
+__device__ __forceinline__ unsigned long long reserveOutput(uint32_t mine, unsigned long long *cursor,
+                                                            uint32_t *itemCursor, unsigned long long itemBase) {
   const uint32_t incl = waveInclusiveScan<uint32_t>(mine);
   const uint32_t total = __shfl(incl, WAVE - 1, WAVE);
   unsigned long long base = 0;
-  if ((threadIdx.x & (WAVE - 1)) == WAVE - 1 && total) base = atomicAdd(cursor, (unsigned long long)total);
+  if ((threadIdx.x & (WAVE - 1)) == WAVE - 1 && total)
+    base = itemCursor ? itemBase + atomicAdd(itemCursor, total) : atomicAdd(cursor, (unsigned long long)total);
   base = __shfl(base, WAVE - 1, WAVE);
   return base + (incl - mine);
+}
+
+__device__ __forceinline__ unsigned long long reserveOne(unsigned long long *cursor, uint32_t *itemCursor,
+                                                         unsigned long long itemBase) {
+  return itemCursor ? itemBase + atomicAdd(itemCursor, 1u) : atomicAdd(cursor, 1ull);
 }
 
 __device__ __forceinline__ void emitPair(const BPArgs &a, unsigned long long pos, uint64_t ridR, uint64_t ridS) {
@@ -151,6 +160,8 @@ __global__ __launch_bounds__(BPT, 4) void buildProbeKernel(BPArgs a, const BPIte
   const V *S = reinterpret_cast<const V *>(a.S);
   uint64_t matches = 0;
   const uint32_t nItems = min(*nItemsPtr, capacity);
+  __shared__ uint32_t itemCursorLds;
+  uint32_t *itemCursor = (MAT && a.itemOffsets) ? &itemCursorLds : nullptr;
 
   for (uint32_t w = blockIdx.x; w < nItems; w += gridDim.x) {
     const BPItem it = items[w];
@@ -162,6 +173,9 @@ __global__ __launch_bounds__(BPT, 4) void buildProbeKernel(BPArgs a, const BPIte
     uint32_t tbits = ceilLog2(2ull * nr);
     if (tbits < 6) tbits = 6;
     const uint32_t slots = 1u << tbits, mask = slots - 1;
+    const unsigned long long itemBase = itemCursor ? a.itemOffsets[w] : 0;
+    const uint64_t matchesBefore = matches;
+    if (itemCursor && t == 0) itemCursorLds = 0;
 
     // First inner batch and first outer batch are in flight while the table is cleared.
     V rv[BP_K], sv[BP_K];
@@ -230,7 +244,7 @@ __global__ __launch_bounds__(BPT, 4) void buildProbeKernel(BPArgs a, const BPIte
                   const uint64_t rr = e & ridMask;
                   if (found == 0) m0 = rr;
                   else if (found == 1) m1 = rr;
-                  else emitPair(a, atomicAdd(a.outCursor, 1ull), rr, sRid);  // overflow path
+                  else emitPair(a, reserveOne(a.outCursor, itemCursor, itemBase), rr, sRid);  // overflow path
                   ++found;
                 }
                 h = (h + 1) & mask;
@@ -247,7 +261,7 @@ __global__ __launch_bounds__(BPT, 4) void buildProbeKernel(BPArgs a, const BPIte
                   const uint64_t rr = ridTable[h];
                   if (found == 0) m0 = rr;
                   else if (found == 1) m1 = rr;
-                  else emitPair(a, atomicAdd(a.outCursor, 1ull), rr, sRid);
+                  else emitPair(a, reserveOne(a.outCursor, itemCursor, itemBase), rr, sRid);
                 }
                 ++found;
               }
@@ -258,11 +272,16 @@ __global__ __launch_bounds__(BPT, 4) void buildProbeKernel(BPArgs a, const BPIte
         matches += found;
         if constexpr (MAT) {
           const uint32_t mine = found < MAT_SLOTS ? found : MAT_SLOTS;
-          const unsigned long long pos = reserveOutput(mine, a.outCursor);
+          const unsigned long long pos = reserveOutput(mine, a.outCursor, itemCursor, itemBase);
           if (mine > 0) emitPair(a, pos, m0, sRid);
           if (mine > 1) emitPair(a, pos + 1, m1, sRid);
         }
       }
+    }
+    if (!MAT && a.itemCounts) {  // count pre-pass of a two-pass materialization
+      const unsigned long long im =
+          blockReduceSum<BPT, unsigned long long>((unsigned long long)(matches - matchesBefore), wsum);
+      if (t == 0) a.itemCounts[w] = (uint32_t)im;
     }
     __syncthreads();
   }

@@ -154,6 +154,13 @@ struct BPArgs {
   unsigned long long *outCursor = nullptr;  // materialize: pair cursor (device)
   ulonglong2 *outPairs = nullptr;           // materialize: (rid_inner, rid_outer)
   uint64_t outCapacity = 0;
+  // Exact materialization in two passes: a count pass writes the matches of
+  // every work item (itemCounts), an exclusive scan turns them into output
+  // offsets (itemOffsets), and the materialize pass places each item's pairs
+  // from its offset with LDS-atomic cursors -- no contended device-wide
+  // atomic per wave (measured 9.4M of them at 600M pairs).
+  uint32_t *itemCounts = nullptr;
+  const unsigned long long *itemOffsets = nullptr;
 };
 size_t bpLdsBytes(const BPArgs &a);
 void bpPlanCounts(const BPArgs &a, uint32_t *counts, hipStream_t s);
@@ -168,6 +175,9 @@ size_t scanWorkspaceBytes(uint64_t n);
 // out[i] = sum_{j<i} in[j]; *total = sum of all (device pointer, may be null).
 void scanExclusiveU32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *total, void *workspace,
                       hipStream_t s);
+// Same with 64-bit prefix sums (per-item match counts -> output offsets).
+void scanExclusiveU32to64(const uint32_t *in, unsigned long long *out, uint64_t n, unsigned long long *total,
+                          void *workspace, hipStream_t s);
 
 // --------------------------------------------------- no-partitioning join
 uint64_t npjTableSlots(uint64_t innerSize);

@@ -12,55 +12,68 @@ constexpr int SCAN_T = 256;
 constexpr int SCAN_PER = 8;
 constexpr uint32_t SCAN_TILE = SCAN_T * SCAN_PER;
 
-size_t scanWorkspaceBytes(uint64_t n) { return (ceilDiv(n, SCAN_TILE) + 16) * sizeof(uint32_t); }
+size_t scanWorkspaceBytes(uint64_t n) { return (ceilDiv(n, SCAN_TILE) + 16) * sizeof(uint64_t); }
 
+template <typename T>
 __global__ __launch_bounds__(SCAN_T) void scanReduceKernel(const uint32_t *__restrict__ in, uint64_t n,
-                                                           uint32_t *__restrict__ sums) {
-  __shared__ uint32_t wt[SCAN_T / WAVE];
+                                                           T *__restrict__ sums) {
+  __shared__ T wt[SCAN_T / WAVE];
   const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
-  uint32_t s = 0;
+  T s = 0;
 #pragma unroll
   for (int i = 0; i < SCAN_PER; ++i) {
     const uint64_t idx = base + (uint64_t)i * SCAN_T + threadIdx.x;
     if (idx < n) s += in[idx];
   }
-  s = blockReduceSum<SCAN_T, uint32_t>(s, wt);
+  s = blockReduceSum<SCAN_T, T>(s, wt);
   if (threadIdx.x == 0) sums[blockIdx.x] = s;
 }
 
-__global__ __launch_bounds__(SCAN_T) void scanSumsKernel(uint32_t *sums, uint32_t nb, uint32_t *total) {
-  __shared__ uint32_t wt[SCAN_T / WAVE];
-  const uint32_t t = blockExclusiveScanLds<SCAN_T, uint32_t, uint32_t>(sums, sums, (int)nb, wt);
+template <typename T>
+__global__ __launch_bounds__(SCAN_T) void scanSumsKernel(T *sums, uint32_t nb, T *total) {
+  __shared__ T wt[SCAN_T / WAVE];
+  const T t = blockExclusiveScanLds<SCAN_T, T, T>(sums, sums, (int)nb, wt);
   if (threadIdx.x == 0 && total) *total = t;
 }
 
+template <typename T>
 __global__ __launch_bounds__(SCAN_T) void scanDownKernel(const uint32_t *__restrict__ in, uint64_t n,
-                                                         const uint32_t *__restrict__ sums, uint32_t *__restrict__ out) {
-  __shared__ uint32_t tile[SCAN_TILE];
-  __shared__ uint32_t wt[SCAN_T / WAVE];
+                                                         const T *__restrict__ sums, T *__restrict__ out) {
+  __shared__ T tile[SCAN_TILE];
+  __shared__ T wt[SCAN_T / WAVE];
   const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
   const uint32_t cnt = (uint32_t)min((uint64_t)SCAN_TILE, n - base);
   for (uint32_t i = threadIdx.x; i < SCAN_TILE; i += SCAN_T) tile[i] = i < cnt ? in[base + i] : 0;
   __syncthreads();
-  blockExclusiveScanLds<SCAN_T, uint32_t, uint32_t>(tile, tile, (int)SCAN_TILE, wt);
-  const uint32_t off = sums[blockIdx.x];
+  blockExclusiveScanLds<SCAN_T, T, T>(tile, tile, (int)SCAN_TILE, wt);
+  const T off = sums[blockIdx.x];
   for (uint32_t i = threadIdx.x; i < cnt; i += SCAN_T) out[base + i] = tile[i] + off;
+}
+
+template <typename T>
+static void scanExclusive(const uint32_t *in, T *out, uint64_t n, T *total, void *workspace, hipStream_t s) {
+  if (n == 0) {
+    if (total) HIP_CHECK(hipMemsetAsync(total, 0, sizeof(T), s));
+    return;
+  }
+  const uint32_t nb = (uint32_t)ceilDiv(n, SCAN_TILE);
+  T *sums = reinterpret_cast<T *>(workspace);
+  hipLaunchKernelGGL(scanReduceKernel<T>, dim3(nb), dim3(SCAN_T), 0, s, in, n, sums);
+  HIP_CHECK_LAUNCH();
+  hipLaunchKernelGGL(scanSumsKernel<T>, dim3(1), dim3(SCAN_T), 0, s, sums, nb, total);
+  HIP_CHECK_LAUNCH();
+  hipLaunchKernelGGL(scanDownKernel<T>, dim3(nb), dim3(SCAN_T), 0, s, in, n, sums, out);
+  HIP_CHECK_LAUNCH();
 }
 
 void scanExclusiveU32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *total, void *workspace,
                       hipStream_t s) {
-  if (n == 0) {
-    if (total) HIP_CHECK(hipMemsetAsync(total, 0, sizeof(uint32_t), s));
-    return;
-  }
-  const uint32_t nb = (uint32_t)ceilDiv(n, SCAN_TILE);
-  uint32_t *sums = reinterpret_cast<uint32_t *>(workspace);
-  hipLaunchKernelGGL(scanReduceKernel, dim3(nb), dim3(SCAN_T), 0, s, in, n, sums);
-  HIP_CHECK_LAUNCH();
-  hipLaunchKernelGGL(scanSumsKernel, dim3(1), dim3(SCAN_T), 0, s, sums, nb, total);
-  HIP_CHECK_LAUNCH();
-  hipLaunchKernelGGL(scanDownKernel, dim3(nb), dim3(SCAN_T), 0, s, in, n, sums, out);
-  HIP_CHECK_LAUNCH();
+  scanExclusive<uint32_t>(in, out, n, total, workspace, s);
+}
+
+void scanExclusiveU32to64(const uint32_t *in, unsigned long long *out, uint64_t n, unsigned long long *total,
+                          void *workspace, hipStream_t s) {
+  scanExclusive<unsigned long long>(in, out, n, total, workspace, s);
 }
 
 }  // namespace kernels

@@ -91,6 +91,22 @@ void BuildProbe::execute() {
   kernels::bpPlanCounts(args, counts, ctx->stream());
   kernels::scanExclusiveU32(counts, offsets, args.P, nItems, scanWs, ctx->stream());
   kernels::bpEmit(args, counts, offsets, items, capacity, ctx->stream());
+  if (!plan.materialize) {
+    kernels::buildProbe(args, items, nItems, capacity, ctx->stream());
+    return;
+  }
+  // Two-pass exact materialization: count per item -> 64-bit offsets -> place.
+  uint32_t *itemCounts = ws.getArray<uint32_t>(capacity);
+  unsigned long long *itemOffsets = ws.getArray<unsigned long long>(capacity);
+  void *scanWs64 = ws.get(kernels::scanWorkspaceBytes(capacity));
+  HIP_CHECK(hipMemsetAsync(itemCounts, 0, (size_t)capacity * sizeof(uint32_t), ctx->stream()));
+  kernels::BPArgs countArgs = args;
+  countArgs.materialize = false;
+  countArgs.itemCounts = itemCounts;
+  kernels::buildProbe(countArgs, items, nItems, capacity, ctx->stream());  // -> counters[0] = matches
+  kernels::scanExclusiveU32to64(itemCounts, itemOffsets, capacity, args.outCursor, scanWs64, ctx->stream());
+  args.itemOffsets = itemOffsets;
+  args.result = counters + 3;  // the count pass already counted
   kernels::buildProbe(args, items, nItems, capacity, ctx->stream());
 }
 

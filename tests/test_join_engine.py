@@ -75,3 +75,40 @@ def test_pinned_host_relations(C, cuda):
     assert j.run()["global_matches"] == n
     link = C.ops.bench_host_link(1 << 26, 0, 2)
     assert link["h2d_GBps"] > 1 and link["zero_copy_read_GBps"] > 1
+
+
+@pytest.mark.parametrize("dev", devices())
+@pytest.mark.parametrize("fmt", ["COMPRESSED", "WIDE"])
+@pytest.mark.parametrize("inner_dist", ["UNIQUE", "UNIFORM"])
+def test_materialized_pairs_exact(C, dev, fmt, inner_dist):
+    """Every materialized (rid_inner, rid_outer) pair joins equal keys, and the
+    pair multiset is exactly the join (duplicate build keys exercise the
+    more-than-two-matches path of the probe)."""
+    import torch
+    G_R, G_S = 150_000, 400_000
+    loc = "device" if dev == "cuda" else "host"
+    ctx = C.ExecContext(loc, 0 if loc == "device" else -1, C.LocalCommunicator())
+    inner = C.GenSpec(distribution=getattr(C.KeyDistribution, inner_dist), seed=77,
+                      domain=0 if inner_dist == "UNIQUE" else G_R // 4)
+    outer = C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=78, domain=G_R, zipf_theta=0.9)
+    R = C.Relation(G_R, G_R, loc, 0)
+    S = C.Relation(G_S, G_S, loc, 0)
+    R.generate(inner, 0)
+    S.generate(outer, 0)
+    cfg = C.JoinConfig()
+    cfg.format = getattr(C.TupleFormat, fmt)
+    cfg.materialize = True
+    j = C.HashJoin(R, S, ctx, cfg)
+    res = j.run()
+    Rt, St = R.to_tensor().cpu(), S.to_tensor().cpu()
+    dom = int(max(Rt[:, 0].max(), St[:, 0].max())) + 1
+    exp = int((torch.bincount(Rt[:, 0], minlength=dom) * torch.bincount(St[:, 0], minlength=dom)).sum())
+    assert res["global_matches"] == exp == res["output_pairs"] and not res["output_overflow"]
+    pairs = j.output()
+    assert pairs.shape == (exp, 2)
+    keyR = torch.empty(G_R, dtype=torch.int64)
+    keyR[Rt[:, 1]] = Rt[:, 0]
+    keyS = torch.empty(G_S, dtype=torch.int64)
+    keyS[St[:, 1]] = St[:, 0]
+    assert torch.equal(keyR[pairs[:, 0]], keyS[pairs[:, 1]])
+    assert torch.unique(pairs[:, 0] * G_S + pairs[:, 1]).numel() == exp

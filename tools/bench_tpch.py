@@ -63,7 +63,12 @@ def main():
             "output_rows_local": int(out.shape[0]), "output_bytes_per_row": int(out.shape[1]) * 8,
             "median_total_ms": tot, "median_join_ms": sorted(join_ms)[len(join_ms) // 2],
             "median_materialize_ms": sorted(mat_ms)[len(mat_ms) // 2],
-            "matches": int(res["global_matches"]), "correct": bool(ok)}), flush=True)
+            "matches": int(res["global_matches"]), "correct": bool(ok),
+            "phases_ms": {k: round(res[k], 3) for k in ("histogram_ms", "network_ms", "local_ms", "dev_histogram_ms",
+                                                         "dev_network_ms", "dev_local_partition_ms",
+                                                         "dev_build_probe_ms", "setup_ms")},
+            "engine": {k: res[k] for k in ("reruns", "build_probe_items", "local_items", "output_overflow")},
+            "plan": repr(t.engine.plan)}), flush=True)
     del out, t
     if torch.cuda.is_available():
         torch.cuda.synchronize()
