@@ -217,6 +217,9 @@ void splitRequests(const ulonglong2 *req, uint64_t n, uint64_t *rids, uint64_t *
 void gatherRows(const uint64_t *rids, uint64_t n, uint64_t ridOffset, const uint64_t *payload, uint64_t *rowsOut,
                 hipStream_t s);
 // out[idx[j] * stride + col .. + ROW_WORDS) = rows[j]
+// Single rank: out[i] = {pair, rowsA[pair.x - offA], rowsB[pair.y - offB]} (10 words).
+void materializeLocal(const ulonglong2 *pairs, uint64_t n, const uint64_t *rowsA, uint64_t offA,
+                      const uint64_t *rowsB, uint64_t offB, uint64_t *out, hipStream_t s);
 void placeRows(const uint64_t *rows, const uint64_t *idx, uint64_t n, uint64_t *out, uint32_t strideWords,
                uint32_t colWord, hipStream_t s);
 }  // namespace kernels

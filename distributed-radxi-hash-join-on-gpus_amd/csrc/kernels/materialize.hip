@@ -119,5 +119,35 @@ void placeRows(const uint64_t *rows, const uint64_t *idx, uint64_t n, uint64_t *
   HIP_CHECK_LAUNCH();
 }
 
+// Single-rank fast path: both payload columns are local, so one pass per pair
+// reads the pair, gathers its two 32-byte rows and writes the whole 80-byte
+// output row (no request buckets, no intermediate row buffers).
+__global__ __launch_bounds__(MT) void materializeLocalKernel(const ulonglong2 *__restrict__ pairs, uint64_t n,
+                                                             const ulonglong2 *__restrict__ rowsA, uint64_t offA,
+                                                             const ulonglong2 *__restrict__ rowsB, uint64_t offB,
+                                                             ulonglong2 *__restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * MT;
+  for (uint64_t i = (uint64_t)blockIdx.x * MT + threadIdx.x; i < n; i += stride) {
+    const ulonglong2 p = pairs[i];
+    const uint64_t a = 2 * (p.x - offA), b = 2 * (p.y - offB);
+    const ulonglong2 a0 = rowsA[a], a1 = rowsA[a + 1], b0 = rowsB[b], b1 = rowsB[b + 1];
+    ulonglong2 *o = out + 5 * i;  // 80-byte row = 5 x 16 bytes
+    o[0] = p;
+    o[1] = a0;
+    o[2] = a1;
+    o[3] = b0;
+    o[4] = b1;
+  }
+}
+
+void materializeLocal(const ulonglong2 *pairs, uint64_t n, const uint64_t *rowsA, uint64_t offA,
+                      const uint64_t *rowsB, uint64_t offB, uint64_t *out, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(materializeLocalKernel, dim3(gridFor(n)), dim3(MT), 0, s, pairs, n,
+                     reinterpret_cast<const ulonglong2 *>(rowsA), offA, reinterpret_cast<const ulonglong2 *>(rowsB),
+                     offB, reinterpret_cast<ulonglong2 *>(out));
+  HIP_CHECK_LAUNCH();
+}
+
 }  // namespace kernels
 }  // namespace hpcjoin

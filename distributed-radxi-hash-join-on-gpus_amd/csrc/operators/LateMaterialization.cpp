@@ -27,6 +27,13 @@ static uint32_t ownerOf(uint64_t rid, uint64_t ridsPerRank, uint32_t nodes) {
 }
 
 void LateMaterialization::materialize(const ulonglong2 *pairs, uint64_t n, uint64_t *out) {
+  static_assert(OUT_WORDS == 2 + 2 * ROW_WORDS, "output row layout");
+  if (ctx->onDevice() && ctx->comm()->size() == 1) {
+    kernels::materializeLocal(pairs, n, cols[0].rows, cols[0].ridOffset, cols[1].rows, cols[1].ridOffset, out,
+                              ctx->stream());
+    HIP_CHECK(hipStreamSynchronize(ctx->stream()));
+    return;
+  }
   for (int side = 0; side < 2; ++side) {
     if (ctx->onDevice())
       fetchDevice(pairs, n, side, cols[side], out);

@@ -41,7 +41,9 @@ def main():
     for _ in range(args.warmup):
         t.run()
     join_ms, mat_ms, tot_ms, ok = [], [], [], True
+    out = None
     for _ in range(args.steps):
+        out = None  # release the previous output rows before the next step allocates
         t.comm.barrier()
         res, out = t.run()
         join_ms.append(res["join_ms"])
