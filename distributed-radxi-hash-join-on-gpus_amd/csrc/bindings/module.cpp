@@ -473,6 +473,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .value("COMPRESSED", core::TupleFormat::Compressed)
       .value("WIDE", core::TupleFormat::Wide);
 
+  py::enum_<core::KeyHashing>(m, "KeyHashing")
+      .value("AUTO", core::KeyHashing::Auto)
+      .value("OFF", core::KeyHashing::Off)
+      .value("ON", core::KeyHashing::On);
   py::class_<core::JoinConfig>(m, "JoinConfig")
       .def(py::init<>())
       .def_readwrite("network_bits", &core::JoinConfig::networkBits)
@@ -482,6 +486,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("assignment", &core::JoinConfig::assignment)
       .def_readwrite("format", &core::JoinConfig::format)
       .def_readwrite("materialize", &core::JoinConfig::materialize)
+      .def_readwrite("key_hashing", &core::JoinConfig::keyHashing)
       .def_readwrite("output_capacity", &core::JoinConfig::outputCapacity)
       .def_readwrite("build_target", &core::JoinConfig::buildTarget)
       .def_readwrite("r_chunk", &core::JoinConfig::rChunk)
@@ -494,6 +499,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<core::JoinPlan>(m, "JoinPlan")
       .def_readonly("number_of_nodes", &core::JoinPlan::numberOfNodes)
       .def_readonly("network_bits", &core::JoinPlan::networkBits)
+      .def_readonly("key_mix", &core::JoinPlan::keyMix)
       .def_readonly("local_bits", &core::JoinPlan::localBits)
       .def_readonly("key_shift", &core::JoinPlan::keyShift)
       .def_readonly("frag_shift", &core::JoinPlan::fragShift)

@@ -18,9 +18,9 @@ std::string JoinConfig::describe() const {
 
 std::string JoinPlan::describe() const {
   return utils::format("JoinPlan(nodes=%u networkBits=%u localBits=%u twoLevel=%d keyShift=%u fragShift=%u "
-                       "rChunk=%u sChunk=%u chunks=%u wide=%d materialize=%d assignment=%s)",
+                       "rChunk=%u sChunk=%u chunks=%u wide=%d materialize=%d keyMix=%d assignment=%s)",
                        numberOfNodes, networkBits, localBits, (int)twoLevel, keyShift, fragShift, rChunk, sChunk,
-                       chunks, (int)wide, (int)materialize,
+                       chunks, (int)wide, (int)materialize, (int)keyMix,
                        assignment == AssignmentPolicy::LPT ? "lpt" : "round_robin");
 }
 
@@ -62,6 +62,9 @@ JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t global
   const uint32_t ridBits = maxRid == ~0ull ? 64 : ceilLog2(maxRid + 1);
   const uint32_t keyBits = maxKey == ~0ull ? 64 : ceilLog2(maxKey + 1);
   p.keyBits = keyBits;
+  // Mixed keys stay below 2^keyBits; a full 64-bit domain could map a key onto
+  // the wide format's reserved empty marker, so mixing needs keyBits < 64.
+  p.keyMix = cfg.keyHashing == KeyHashing::On && keyBits < 64;
   if (p.wide) {
     p.keyShift = 64;
     p.fragShift = 64;

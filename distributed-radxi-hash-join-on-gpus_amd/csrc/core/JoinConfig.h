@@ -22,6 +22,14 @@ enum class TupleFormat : int {
   Wide = 1,        // 16-byte Tuple end to end: full 64-bit keys (the RCD / AoS path)
 };
 
+// Radix digits from the raw key (optimal for dense keys) or from a bijective
+// mix of it (keys with structured low bits: sparse TPC-H order keys, strides).
+enum class KeyHashing : int {
+  Auto = 0,  // decided at plan time from a histogram of the inner keys' low bits
+  Off = 1,
+  On = 2,
+};
+
 struct JoinConfig {
   uint32_t networkBits = 0;   // radix bits of the network pass (0 = auto)
   uint32_t localBits = 0;     // radix bits of the local pass (0 = auto; ignored if !twoLevel)
@@ -37,6 +45,7 @@ struct JoinConfig {
   uint32_t chunks = 1;          // exchange pipeline slices per relation (>1: scatter(k+1) || all-to-all(k))
   bool checks = true;           // cheap always-on invariants (all tuples written, sizes)
   uint32_t maxPartitionBlocks = 2048;  // network-pass grid cap (~8 WGs per CU)
+  KeyHashing keyHashing = KeyHashing::Auto;
 
   std::string describe() const;
 };
@@ -55,6 +64,7 @@ struct JoinPlan {
   bool twoLevel = true;
   bool wide = false;
   bool materialize = false;
+  bool keyMix = false;        // radix digits from kernels::KeyMix{keyBits} of the key
   AssignmentPolicy assignment = AssignmentPolicy::LPT;
   uint64_t networkPartitions() const { return uint64_t(1) << networkBits; }
   uint64_t localPartitions() const { return twoLevel ? (uint64_t(1) << localBits) : 1; }

@@ -21,8 +21,8 @@ LocalHistogram::LocalHistogram(data::Relation *relation)
 }
 
 LocalHistogram::LocalHistogram(data::Relation *relation, core::ExecContext *ctx, uint32_t bits, uint32_t chunks,
-                               uint32_t maxBlocks)
-    : relation(relation), ctx(ctx), bits(bits), chunks(std::max<uint32_t>(1, chunks)) {
+                               uint32_t maxBlocks, kernels::KeyMix mix)
+    : relation(relation), ctx(ctx), bits(bits), chunks(std::max<uint32_t>(1, chunks)), mix(mix) {
   geom = kernels::partitionGeometry(relation->getLocalSize(), std::max<uint32_t>(maxBlocks, this->chunks));
   if (this->chunks > geom.blocks) this->chunks = geom.blocks;
   bpc = (uint32_t)ceilDiv(geom.blocks, this->chunks);
@@ -39,11 +39,11 @@ void LocalHistogram::computeLocalHistogram() {
   blockHist = ctx->workspace().getArray<uint32_t>((uint64_t)F * geom.blocks);
   if (ctx->onDevice()) {
     totalsDev = ctx->workspace().getArray<uint64_t>((uint64_t)chunks * F);
-    kernels::netHistogram(relation->getData(), relation->getLocalSize(), bits, geom, blockHist, ctx->stream());
+    kernels::netHistogram(relation->getData(), relation->getLocalSize(), bits, geom, blockHist, ctx->stream(), mix);
     kernels::digitTotals(blockHist, F, geom.blocks, bpc, chunks, totalsDev, ctx->stream());
     ctx->copy(chunkValues.data(), totalsDev, chunkValues.size() * 8, false, true);
   } else {
-    host::netHistogram(relation->getData(), relation->getLocalSize(), bits, geom, blockHist);
+    host::netHistogram(relation->getData(), relation->getLocalSize(), bits, geom, blockHist, mix);
     host::digitTotals(blockHist, F, geom.blocks, bpc, chunks, chunkValues.data());
   }
 }

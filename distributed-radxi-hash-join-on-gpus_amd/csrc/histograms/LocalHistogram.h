@@ -20,7 +20,7 @@ class LocalHistogram {
  public:
   explicit LocalHistogram(data::Relation *relation);  // reference: host, Configuration fan-out, 1 chunk
   LocalHistogram(data::Relation *relation, core::ExecContext *ctx, uint32_t bits, uint32_t chunks,
-                 uint32_t maxBlocks = 2048);
+                 uint32_t maxBlocks = 2048, kernels::KeyMix mix = kernels::KeyMix());
   ~LocalHistogram();
 
   void computeLocalHistogram();  // device: enqueued; host values valid after ctx->synchronize()
@@ -48,6 +48,7 @@ class LocalHistogram {
   kernels::PartitionGeometry geom;
   uint32_t *blockHist = nullptr;
   uint64_t *totalsDev = nullptr;
+  kernels::KeyMix mix;
   bool summed = false;
 };
 

@@ -72,13 +72,13 @@ void generate(data::Tuple *out, uint64_t n, const kernels::GenParams &p) {
 
 // ------------------------------------------------------------ pass 1 (host)
 void netHistogram(const data::Tuple *in, uint64_t n, uint32_t bits, const kernels::PartitionGeometry &g,
-                  uint32_t *blockHist) {
+                  uint32_t *blockHist, kernels::KeyMix mix) {
   const uint32_t F = 1u << bits;
   const uint64_t mask = F - 1;
   std::memset(blockHist, 0, sizeof(uint32_t) * F * g.blocks);
   for (uint32_t b = 0; b < g.blocks; ++b) {
     const uint64_t begin = (uint64_t)b * g.tuplesPerBlock(), end = std::min(n, begin + g.tuplesPerBlock());
-    for (uint64_t i = begin; i < end; ++i) blockHist[(in[i].key & mask) * g.blocks + b]++;
+    for (uint64_t i = begin; i < end; ++i) blockHist[(mix.apply(in[i].key) & mask) * g.blocks + b]++;
   }
 }
 
@@ -107,7 +107,7 @@ void netCursors(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint32_t
 
 void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift,
                 const kernels::PartitionGeometry &g, uint32_t blockBegin, uint32_t blockEnd, const uint64_t *cursors,
-                void *out, bool wide) {
+                void *out, bool wide, kernels::KeyMix mix) {
   const uint32_t F = 1u << bits;
   const uint64_t mask = F - 1;
   std::vector<uint64_t> cur(F);
@@ -115,11 +115,12 @@ void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keySh
     for (uint32_t d = 0; d < F; ++d) cur[d] = cursors[(uint64_t)d * g.blocks + b];
     const uint64_t begin = (uint64_t)b * g.tuplesPerBlock(), end = std::min(n, begin + g.tuplesPerBlock());
     for (uint64_t i = begin; i < end; ++i) {
-      const uint64_t d = in[i].key & mask;
+      const uint64_t key = mix.apply(in[i].key);
+      const uint64_t d = key & mask;
       if (wide)
-        static_cast<data::Tuple *>(out)[cur[d]++] = in[i];
+        static_cast<data::Tuple *>(out)[cur[d]++] = data::Tuple{key, in[i].rid};
       else
-        static_cast<uint64_t *>(out)[cur[d]++] = in[i].rid | ((in[i].key >> bits) << keyShift);
+        static_cast<uint64_t *>(out)[cur[d]++] = in[i].rid | ((key >> bits) << keyShift);
     }
   }
 }

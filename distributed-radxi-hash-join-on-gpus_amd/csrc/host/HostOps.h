@@ -20,14 +20,14 @@ kernels::ZipfParams makeZipf(uint64_t n, double theta);
 void generate(data::Tuple *out, uint64_t n, const kernels::GenParams &p);
 
 void netHistogram(const data::Tuple *in, uint64_t n, uint32_t bits, const kernels::PartitionGeometry &g,
-                  uint32_t *blockHist);
+                  uint32_t *blockHist, kernels::KeyMix mix = kernels::KeyMix());
 void digitTotals(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint32_t blocksPerChunk, uint32_t chunks,
                  uint64_t *totals);
 void netCursors(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint32_t blocksPerChunk,
                 const uint64_t *base, uint64_t *cursors);
 void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift,
                 const kernels::PartitionGeometry &g, uint32_t blockBegin, uint32_t blockEnd, const uint64_t *cursors,
-                void *out, bool wide);
+                void *out, bool wide, kernels::KeyMix mix = kernels::KeyMix());
 
 void localHistogram(const void *in, bool wide, const kernels::LocalItem *items, uint32_t nItems, uint32_t shift,
                     uint32_t bits, uint32_t *itemHist);

@@ -59,9 +59,30 @@ HJ_HD uint64_t tpchSparseKey(uint64_t k) { return (k >> 3) * 32 + (k & 7) + 1; }
 void generate(data::Tuple *out, uint64_t n, const GenParams &p, hipStream_t s);
 
 // ------------------------------------------------- pass 1: network partition
+// Hash partitioning for keys whose low bits are structured (sparse TPC-H
+// order keys, multiples of a stride): radix digits are taken from a bijection
+// of the key on [0, 2^bits) instead of the raw key, and the mixed key is what
+// the network pass stores, so every later pass and the build/probe compare
+// mixed keys (equality is preserved by the bijection).  Off = identity, which
+// is optimal for dense keys (perfectly balanced partitions).
+struct KeyMix {
+  uint32_t on = 0;
+  uint32_t bits = 64;
+  HJ_HD uint64_t apply(uint64_t k) const {
+    if (!on) return k;
+    const uint64_t m = bits >= 64 ? ~0ull : ((1ull << bits) - 1);
+    const uint32_t h = (bits + 1) / 2;
+    k = (k * 0x9E3779B97F4A7C15ull) & m;  // odd multiplier: bijective mod 2^bits
+    k ^= k >> h;                           // xor-shift: bijective on [0, 2^bits)
+    k = (k * 0xC2B2AE3D27D4EB4Full) & m;
+    k ^= k >> h;
+    return k;
+  }
+};
+
 // blockHist is digit-major [F][blocks] (u32).
 void netHistogram(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
-                  uint32_t *blockHist, hipStream_t s);
+                  uint32_t *blockHist, hipStream_t s, KeyMix mix = KeyMix());
 // totals[c][F] = sum of blockHist over the blocks of chunk c (blocksPerChunk each).
 void digitTotals(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint32_t blocksPerChunk,
                  uint32_t chunks, uint64_t *totals, hipStream_t s);
@@ -86,9 +107,10 @@ void netGroupCursors(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uin
 // packed word's spare top bits instead of a separate LDS array).
 void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift, const PartitionGeometry &g,
                 uint32_t blockBegin, uint32_t blockEnd, void *gcur, uint64_t *out, hipStream_t s,
-                uint32_t keyBits = 64);
+                uint32_t keyBits = 64, KeyMix mix = KeyMix());
 void netScatterWide(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
-                    uint32_t blockBegin, uint32_t blockEnd, void *gcur, data::Tuple *out, hipStream_t s);
+                    uint32_t blockBegin, uint32_t blockEnd, void *gcur, data::Tuple *out, hipStream_t s,
+                    KeyMix mix = KeyMix());
 // Ablation entry (micro-benchmarks): mode 0 = real scatter, 1 = coalesced
 // write-out, 2 = no write-out; 32-bit cursors, compressed output.
 // geometry: 0 = 256x16 (default), 1 = 512x16, 2 = 1024x8, 3 = 1024x16,

@@ -65,7 +65,7 @@ struct Loader<uint64_t> {
 // ------------------------------------------------------- histogram (pass 1)
 __global__ __launch_bounds__(NT) void netHistogramKernel(const ulonglong2 *__restrict__ in, uint64_t n,
                                                          uint32_t tpb, uint32_t bits,
-                                                         uint32_t *__restrict__ blockHist) {
+                                                         uint32_t *__restrict__ blockHist, KeyMix mix) {
   extern __shared__ __attribute__((aligned(16))) uint32_t hsh[];
   const uint32_t F = 1u << bits, mask = F - 1;
   const int wid = threadIdx.x / WAVE;
@@ -79,7 +79,7 @@ __global__ __launch_bounds__(NT) void netHistogramKernel(const ulonglong2 *__res
 #pragma unroll
     for (int i = 0; i < (int)PART_ITEMS; ++i) {
       const uint64_t idx = base + (uint64_t)i * NT + threadIdx.x;
-      k[i] = idx < end ? in[idx].x : 0;
+      k[i] = idx < end ? mix.apply(in[idx].x) : 0;
     }
 #pragma unroll
     for (int i = 0; i < (int)PART_ITEMS; ++i) {
@@ -93,11 +93,11 @@ __global__ __launch_bounds__(NT) void netHistogramKernel(const ulonglong2 *__res
 }
 
 void netHistogram(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
-                  uint32_t *blockHist, hipStream_t s) {
+                  uint32_t *blockHist, hipStream_t s, KeyMix mix) {
   HJ_CHECK(bits >= 1 && bits <= MAX_PART_BITS, "netHistogram: bits=%u out of range", bits);
   const size_t lds = size_t(4) << bits << 2;
   hipLaunchKernelGGL(netHistogramKernel, dim3(g.blocks), dim3(NT), lds, s,
-                     reinterpret_cast<const ulonglong2 *>(in), n, g.tilesPerBlock, bits, blockHist);
+                     reinterpret_cast<const ulonglong2 *>(in), n, g.tilesPerBlock, bits, blockHist, mix);
   HIP_CHECK_LAUNCH();
 }
 
@@ -218,16 +218,19 @@ struct NetCompressedPol {  // 16 B tuple -> 8 B CompressedTuple, digit in the to
   static constexpr bool kDigArray = false;
   uint64_t mask;
   uint32_t bits, keyShift;
-  __device__ __forceinline__ uint32_t digit(const InT &x) const { return (uint32_t)(x.x & mask); }
+  KeyMix mix;
+  __device__ __forceinline__ uint32_t digit(const InT &x) const { return (uint32_t)(mix.apply(x.x) & mask); }
   __device__ __forceinline__ StageT stage(const InT &x, uint32_t d) const {
-    return x.y | ((x.x >> bits) << keyShift) | ((uint64_t)d << (64 - bits));
+    return x.y | ((mix.apply(x.x) >> bits) << keyShift) | ((uint64_t)d << (64 - bits));
   }
   __device__ __forceinline__ uint32_t stagedDigit(const StageT &v) const { return (uint32_t)(v >> (64 - bits)); }
   __device__ __forceinline__ OutT out(const StageT &v) const { return v & (~0ull >> bits); }
 };
 struct NetCompressedDigPol : NetCompressedPol {  // no spare bits: digits staged separately
   static constexpr bool kDigArray = true;
-  __device__ __forceinline__ StageT stage(const InT &x, uint32_t) const { return x.y | ((x.x >> bits) << keyShift); }
+  __device__ __forceinline__ StageT stage(const InT &x, uint32_t) const {
+    return x.y | ((mix.apply(x.x) >> bits) << keyShift);
+  }
   __device__ __forceinline__ OutT out(const StageT &v) const { return v; }
 };
 struct NetWidePol {  // 16 B tuple -> 16 B tuple (full-range keys)
@@ -236,8 +239,11 @@ struct NetWidePol {  // 16 B tuple -> 16 B tuple (full-range keys)
   using OutT = ulonglong2;
   static constexpr bool kDigArray = false;
   uint64_t mask;
-  __device__ __forceinline__ uint32_t digit(const InT &x) const { return (uint32_t)(x.x & mask); }
-  __device__ __forceinline__ StageT stage(const InT &x, uint32_t) const { return x; }
+  KeyMix mix;
+  __device__ __forceinline__ uint32_t digit(const InT &x) const { return (uint32_t)(mix.apply(x.x) & mask); }
+  __device__ __forceinline__ StageT stage(const InT &x, uint32_t) const {
+    return make_ulonglong2(mix.apply(x.x), x.y);
+  }
   __device__ __forceinline__ uint32_t stagedDigit(const StageT &v) const { return (uint32_t)(v.x & mask); }
   __device__ __forceinline__ OutT out(const StageT &v) const { return v; }
 };
@@ -520,7 +526,8 @@ static void launchNetClaim(const Pol &pol, const data::Tuple *in, uint64_t n, ui
 }
 
 void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift, const PartitionGeometry &g,
-                uint32_t blockBegin, uint32_t blockEnd, void *gcur, uint64_t *out, hipStream_t s, uint32_t keyBits) {
+                uint32_t blockBegin, uint32_t blockEnd, void *gcur, uint64_t *out, hipStream_t s, uint32_t keyBits,
+                KeyMix mix) {
   HJ_CHECK(bits >= 1 && bits <= MAX_PART_BITS, "netScatter: bits=%u out of range", bits);
   HJ_CHECK(blockBegin <= blockEnd && blockEnd <= g.blocks, "netScatter: block range [%u,%u) of %u", blockBegin,
            blockEnd, g.blocks);
@@ -529,7 +536,8 @@ void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keySh
   pol.mask = (1ull << bits) - 1;
   pol.bits = bits;
   pol.keyShift = keyShift;
-  if (digitFitsOnTop(bits, keyShift, keyBits)) {
+  pol.mix = mix;
+  if (digitFitsOnTop(bits, keyShift, mix.on ? std::max(keyBits, mix.bits) : keyBits)) {
     launchNetClaim(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s);
   } else {
     NetCompressedDigPol dpol;
@@ -539,13 +547,15 @@ void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keySh
 }
 
 void netScatterWide(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
-                    uint32_t blockBegin, uint32_t blockEnd, void *gcur, data::Tuple *out, hipStream_t s) {
+                    uint32_t blockBegin, uint32_t blockEnd, void *gcur, data::Tuple *out, hipStream_t s,
+                    KeyMix mix) {
   HJ_CHECK(bits >= 1 && bits <= MAX_PART_BITS, "netScatterWide: bits=%u out of range", bits);
   HJ_CHECK(blockBegin <= blockEnd && blockEnd <= g.blocks, "netScatterWide: block range [%u,%u) of %u",
            blockBegin, blockEnd, g.blocks);
   if (n == 0 || blockEnd == blockBegin) return;
   NetWidePol pol;
   pol.mask = (1ull << bits) - 1;
+  pol.mix = mix;
   launchNetClaim(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s);
 }
 

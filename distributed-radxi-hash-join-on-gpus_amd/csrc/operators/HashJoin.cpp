@@ -1,9 +1,12 @@
 #include "HashJoin.h"
 
 #include <algorithm>
+#include <cmath>
+#include <vector>
 
 #include "../comm/Communicator.h"
 #include "../comm/World.h"
+#include "../host/HostOps.h"
 #include "../data/Window.h"
 #include "../memory/Arena.h"
 #include "../performance/Clock.h"
@@ -86,9 +89,43 @@ void HashJoin::makeJoinPlan() {
   }
   plan = core::makePlan(config, numberOfNodes, innerRelation->getGlobalSize(), outerRelation->getGlobalSize(), mx[0],
                         mx[1]);
+  if (config.keyHashing == core::KeyHashing::Auto && plan.keyBits < 64) plan.keyMix = lowKeyBitsSkewed();
   JOIN_DEBUG("HashJoin", "%s", plan.describe().c_str());
   if (ctx->onDevice())
     for (auto &e : ev) HIP_CHECK(hipEventCreate(&e));
+}
+
+// KeyHashing::Auto: histogram the inner keys' low networkBits bits (all ranks)
+// once at plan time.  Dense keys give a flat histogram; keys with structured
+// low bits (sparse TPC-H order keys, strides) leave digits empty and overfill
+// others, which radix partitioning would carry into every later pass.
+bool HashJoin::lowKeyBitsSkewed() {
+  const uint32_t bits = std::min<uint32_t>(plan.networkBits, kernels::MAX_PART_BITS);
+  const uint32_t F = 1u << bits;
+  const uint64_t G = innerRelation->getGlobalSize();
+  if (G < 64ull * F) return false;  // too few keys to judge (and too small to matter)
+  const uint64_t n = innerRelation->getLocalSize();
+  const kernels::PartitionGeometry g = kernels::partitionGeometry(n);
+  std::vector<uint64_t> totals(F, 0);
+  uint32_t *blockHist = ctx->workspace().getArray<uint32_t>((uint64_t)F * g.blocks);
+  if (ctx->onDevice()) {
+    uint64_t *d = ctx->workspace().getArray<uint64_t>(F);
+    kernels::netHistogram(innerRelation->getData(), n, bits, g, blockHist, ctx->stream());
+    kernels::digitTotals(blockHist, F, g.blocks, g.blocks, 1, d, ctx->stream());
+    HIP_CHECK(hipMemcpyAsync(totals.data(), d, F * 8, hipMemcpyDeviceToHost, ctx->stream()));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream()));
+  } else {
+    host::netHistogram(innerRelation->getData(), n, bits, g, blockHist);
+    host::digitTotals(blockHist, F, g.blocks, g.blocks, 1, totals.data());
+  }
+  ctx->workspace().reset();
+  ctx->comm()->allReduceSumHost(totals.data(), F);
+  const double mean = (double)G / F;
+  const double mx = (double)*std::max_element(totals.begin(), totals.end());
+  const bool skewed = 2.0 * mx > 3.0 * mean + 16.0 * std::sqrt(mean) + 128.0;
+  JOIN_DEBUG("HashJoin", "inner low-bit histogram: max %.0f vs mean %.1f -> key mixing %s", mx, mean,
+             skewed ? "on" : "off");
+  return skewed;
 }
 
 void HashJoin::join() {

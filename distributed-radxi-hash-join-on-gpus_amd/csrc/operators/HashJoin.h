@@ -72,6 +72,7 @@ class HashJoin {
 
  private:
   void makeJoinPlan();
+  bool lowKeyBitsSkewed();
   JoinResult runImpl();
   core::ExecContext *ctx;
   std::unique_ptr<core::ExecContext> ownedCtx;

@@ -11,9 +11,11 @@ HistogramComputation::HistogramComputation(uint32_t numberOfNodes, uint32_t node
     : nodeId(nodeId), numberOfNodes(numberOfNodes), innerRelation(innerRelation), outerRelation(outerRelation),
       ctx(ctx) {
   innerRelationLocalHistogram.reset(
-      new histograms::LocalHistogram(innerRelation, ctx, plan.networkBits, plan.chunks, maxBlocks));
+      new histograms::LocalHistogram(innerRelation, ctx, plan.networkBits, plan.chunks, maxBlocks,
+                                     kernels::KeyMix{plan.keyMix ? 1u : 0u, plan.keyBits}));
   outerRelationLocalHistogram.reset(
-      new histograms::LocalHistogram(outerRelation, ctx, plan.networkBits, plan.chunks, maxBlocks));
+      new histograms::LocalHistogram(outerRelation, ctx, plan.networkBits, plan.chunks, maxBlocks,
+                                     kernels::KeyMix{plan.keyMix ? 1u : 0u, plan.keyBits}));
   innerRelationGlobalHistogram.reset(new histograms::GlobalHistogram(innerRelationLocalHistogram.get(), ctx->comm()));
   outerRelationGlobalHistogram.reset(new histograms::GlobalHistogram(outerRelationLocalHistogram.get(), ctx->comm()));
   assignment.reset(new histograms::AssignmentMap(numberOfNodes, innerRelationGlobalHistogram.get(),

@@ -33,6 +33,7 @@ void NetworkPartitioning::partition(data::Relation *relation, data::Window *wind
   const uint32_t tb = window->tupleBytes();
   void *send = single ? window->getData() : ctx->workspace().get(n * tb);
   window->start();
+  const kernels::KeyMix mix{plan.keyMix ? 1u : 0u, plan.keyBits};
   if (ctx->onDevice()) {
     // Claim-mode scatter: per-(chunk, XCD group, digit) slices, one device
     // atomic per digit per 8192-tuple tile (kernels.h, CLAIM_GROUPS).
@@ -46,10 +47,10 @@ void NetworkPartitioning::partition(data::Relation *relation, data::Window *wind
       const uint32_t b0 = c * bpc, b1 = std::min(g.blocks, b0 + bpc);
       if (plan.wide)
         kernels::netScatterWide(relation->getData(), n, bits, g, b0, b1, gcur + c * perChunk,
-                                static_cast<data::Tuple *>(send), ctx->stream());
+                                static_cast<data::Tuple *>(send), ctx->stream(), mix);
       else
         kernels::netScatter(relation->getData(), n, bits, plan.keyShift, g, b0, b1, gcur + c * perChunk,
-                            static_cast<uint64_t *>(send), ctx->stream(), plan.keyBits);
+                            static_cast<uint64_t *>(send), ctx->stream(), plan.keyBits, mix);
       if (!single) window->exchange(send, c);
     }
   } else {
@@ -57,7 +58,7 @@ void NetworkPartitioning::partition(data::Relation *relation, data::Window *wind
     host::netCursors(local->blockHistogram(), F, g.blocks, bpc, xp.digitBase.data(), cursors);
     for (uint32_t c = 0; c < chunks; ++c) {
       const uint32_t b0 = c * bpc, b1 = std::min(g.blocks, b0 + bpc);
-      host::netScatter(relation->getData(), n, bits, plan.keyShift, g, b0, b1, cursors, send, plan.wide);
+      host::netScatter(relation->getData(), n, bits, plan.keyShift, g, b0, b1, cursors, send, plan.wide, mix);
       if (!single) window->exchange(send, c);
     }
   }

@@ -14,6 +14,7 @@ def config_to_dict(cfg) -> dict:
     d = {f: getattr(cfg, f) for f in _FIELDS}
     d["assignment"] = str(cfg.assignment).split(".")[-1]
     d["format"] = str(cfg.format).split(".")[-1]
+    d["key_hashing"] = str(cfg.key_hashing).split(".")[-1]
     return d
 
 
@@ -22,7 +23,7 @@ def config_from_dict(d: dict | None = None, env_prefix: str = "HPCJOIN_"):
     C = require_native()
     cfg = C.JoinConfig()
     merged = dict(d or {})
-    for f in _FIELDS + ["assignment", "format"]:
+    for f in _FIELDS + ["assignment", "format", "key_hashing"]:
         v = os.environ.get(env_prefix + f.upper())
         if v is not None:
             merged[f] = v
@@ -31,6 +32,8 @@ def config_from_dict(d: dict | None = None, env_prefix: str = "HPCJOIN_"):
             cfg.assignment = getattr(C.AssignmentPolicy, str(v).upper())
         elif k == "format":
             cfg.format = getattr(C.TupleFormat, str(v).upper())
+        elif k == "key_hashing":
+            cfg.key_hashing = getattr(C.KeyHashing, str(v).upper())
         elif k in ("two_level", "materialize", "checks"):
             setattr(cfg, k, v if isinstance(v, bool) else str(v).lower() in ("1", "true", "yes"))
         elif k in _FIELDS:

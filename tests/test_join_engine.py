@@ -112,3 +112,46 @@ def test_materialized_pairs_exact(C, dev, fmt, inner_dist):
     keyS[St[:, 1]] = St[:, 0]
     assert torch.equal(keyR[pairs[:, 0]], keyS[pairs[:, 1]])
     assert torch.unique(pairs[:, 0] * G_S + pairs[:, 1]).numel() == exp
+
+
+@pytest.mark.parametrize("dev", devices())
+@pytest.mark.parametrize("fmt", ["COMPRESSED", "WIDE"])
+def test_key_hashing(C, dev, fmt):
+    """Structured low key bits (sparse TPC-H order keys use 8 of every 32
+    values) switch the radix digits to a bijective key mix: AUTO detects it,
+    results equal the raw-digit plan, and forcing ON keeps exact pairs."""
+    import torch
+    G_R, G_S = 1 << 17, 1 << 19
+    loc = "device" if dev == "cuda" else "host"
+    ctx = C.ExecContext(loc, 0 if loc == "device" else -1, C.LocalCommunicator())
+    inner = C.GenSpec(C.KeyDistribution.UNIQUE, 5, 0, 0, 0.75, True)
+    outer = C.GenSpec(C.KeyDistribution.MODULO, 6, G_R, 0, 0.75, True)
+    R = C.Relation(G_R, G_R, loc, 0)
+    S = C.Relation(G_S, G_S, loc, 0)
+    R.generate(inner, 0)
+    S.generate(outer, 0)
+    exp = C.Relation.expected_matches(inner, G_R, outer, G_S)
+    assert exp == G_S
+    runs = {}
+    for mode in ("AUTO", "OFF", "ON"):
+        cfg = C.JoinConfig()
+        cfg.format = getattr(C.TupleFormat, fmt)
+        cfg.key_hashing = getattr(C.KeyHashing, mode)
+        cfg.materialize = True
+        j = C.HashJoin(R, S, ctx, cfg)
+        runs[mode] = (j.plan.key_mix, j.run(), j.output())
+    assert runs["AUTO"][0] and runs["ON"][0] and not runs["OFF"][0]
+    for mode, (_, res, pairs) in runs.items():
+        assert res["global_matches"] == exp, mode
+        assert pairs.shape == (exp, 2)
+    Rt, St = R.to_tensor().cpu(), S.to_tensor().cpu()
+    keyR = torch.empty(G_R, dtype=torch.int64)
+    keyR[Rt[:, 1]] = Rt[:, 0]
+    keyS = torch.empty(G_S, dtype=torch.int64)
+    keyS[St[:, 1]] = St[:, 0]
+    pairs = runs["ON"][2]
+    assert torch.equal(keyR[pairs[:, 0]], keyS[pairs[:, 1]])
+    # dense keys keep raw digits
+    D = C.Relation(G_R, G_R, loc, 0)
+    D.generate(C.GenSpec(seed=9), 0)
+    assert not C.HashJoin(D, D, ctx, C.JoinConfig()).plan.key_mix
