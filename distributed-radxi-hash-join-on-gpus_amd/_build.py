@@ -139,6 +139,56 @@ def build(jobs: int | None = None, verbose: bool = False, with_cli: bool = True)
     return out
 
 
+SANITIZERS = {
+    # host code only: GPU sanitizers are not available on the MI355X pool
+    "address": ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined"],
+    "thread": ["-Xarch_host", "-fsanitize=thread"],
+}
+
+
+def build_sanitized(kind: str = "address", jobs: int | None = None, verbose: bool = False) -> Path:
+    """Host self-test (csrc/apps/host_selftest.cpp) with the runtime compiled
+    under ASan+UBSan ("address") or TSan ("thread").  Kernels are linked
+    unsanitized (they never run on this path)."""
+    jobs = jobs or min(16, os.cpu_count() or 4)
+    san = SANITIZERS[kind]
+    odir = BUILD / f"san-{kind}"
+    odir.mkdir(parents=True, exist_ok=True)
+    hdr = _header_digest()
+    core, kernels, _ = _sources()
+    flags = ["-O1", "-g", "-fno-omit-frame-pointer", "-std=c++17", "-fPIC", *san]
+    srcs = core + [CSRC / "apps" / "host_selftest.cpp"]
+
+    def compile_one(src):
+        h = hashlib.sha1(src.read_bytes() + hdr.encode() + " ".join(flags).encode()).hexdigest()[:16]
+        obj = odir / f"{str(src.relative_to(CSRC)).replace('/', '_')}.{h}.o"
+        if not obj.exists():
+            _run([HIPCC, *flags, "-c", str(src), "-o", str(obj) + ".tmp"], verbose)
+            os.replace(str(obj) + ".tmp", obj)
+        return obj
+
+    kflags = HIP_FLAGS + ["-D_GLIBCXX_USE_CXX11_ABI=1"]
+
+    def compile_kernel(src):
+        obj = odir / f"{str(src.relative_to(CSRC)).replace('/', '_')}.{hashlib.sha1(src.read_bytes() + hdr.encode()).hexdigest()[:16]}.k.o"
+        if not obj.exists():
+            _run([HIPCC, *kflags, "-c", str(src), "-o", str(obj) + ".tmp"], verbose)
+            os.replace(str(obj) + ".tmp", obj)
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(compile_one, srcs)) + list(ex.map(compile_kernel, kernels))
+    link_san = ["-fsanitize=address,undefined"] if kind == "address" else ["-fsanitize=thread"]
+    out = BUILD / "bin" / f"host_selftest_{kind}"
+    (BUILD / "bin").mkdir(parents=True, exist_ok=True)
+    _run([HIPCC, f"--offload-arch={ARCH}", "-fno-gpu-sanitize", *link_san, *map(str, objs), "-o", str(out),
+          f"-L{ROCM}/lib", "-lrccl", "-lrocprofiler-sdk-roctx", "-lamdhip64", "-lpthread"], verbose)
+    return out
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "sanitize":
+        print(build_sanitized(sys.argv[2], verbose="-v" in sys.argv))
+        sys.exit(0)
     p = build(verbose="-v" in sys.argv)
     print(p)

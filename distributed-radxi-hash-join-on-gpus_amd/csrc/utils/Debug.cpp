@@ -15,12 +15,13 @@ bool debugEnabled() {
 #ifdef JOIN_DEBUG_PRINT
   return true;
 #else
-  static int cached = -1;
-  if (cached < 0) {
+  // Magic static: initialised once, thread-safe (in-process ranks are threads;
+  // the earlier lazily written int was a data race found by the TSan build).
+  static const bool enabled = [] {
     const char *e = std::getenv("HPCJOIN_DEBUG");
-    cached = (e && e[0] && std::strcmp(e, "0") != 0) ? 1 : 0;
-  }
-  return cached == 1;
+    return e && e[0] && std::strcmp(e, "0") != 0;
+  }();
+  return enabled;
 #endif
 }
 
