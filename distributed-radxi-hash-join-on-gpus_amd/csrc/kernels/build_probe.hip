@@ -140,8 +140,17 @@ __device__ __forceinline__ void bpLoad(const V *__restrict__ src, uint32_t n, ui
   }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(BPT, 4) void buildProbeKernel(BPArgs a, const BPItem *__restrict__ items,
+// ITEMS: count pre-pass of a two-pass materialization (per-item match counts);
+// a separate instantiation so the count-only production kernel is unchanged.
+// Occupancy is LDS-bound: 4-byte count tables (32 KiB) fit 4 workgroups per
+// CU, 8-byte tables (64 KiB) only 2 -- so the 8-byte modes get the 256-VGPR
+// budget of 2 workgroups per CU instead of spilling to scratch at 128.
+// (The per-item count variant keeps 3: its extra reduction would spill at 128.)
+template <int MODE, bool ITEMS>
+constexpr int bpMinBlocks() { return MODE == 0 ? (ITEMS ? 3 : 4) : 2; }
+
+template <int MODE, bool ITEMS = false>
+__global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeKernel(BPArgs a, const BPItem *__restrict__ items,
                                                         const uint32_t *__restrict__ nItemsPtr, uint32_t capacity) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool WIDE = (MODE >= BP_WCOUNT);
@@ -161,7 +170,8 @@ __global__ __launch_bounds__(BPT, 4) void buildProbeKernel(BPArgs a, const BPIte
   uint64_t matches = 0;
   const uint32_t nItems = min(*nItemsPtr, capacity);
   __shared__ uint32_t itemCursorLds;
-  uint32_t *itemCursor = (MAT && a.itemOffsets) ? &itemCursorLds : nullptr;
+  uint32_t *itemCursor = nullptr;
+  if constexpr (MAT) itemCursor = a.itemOffsets ? &itemCursorLds : nullptr;
 
   for (uint32_t w = blockIdx.x; w < nItems; w += gridDim.x) {
     const BPItem it = items[w];
@@ -173,9 +183,14 @@ __global__ __launch_bounds__(BPT, 4) void buildProbeKernel(BPArgs a, const BPIte
     uint32_t tbits = ceilLog2(2ull * nr);
     if (tbits < 6) tbits = 6;
     const uint32_t slots = 1u << tbits, mask = slots - 1;
-    const unsigned long long itemBase = itemCursor ? a.itemOffsets[w] : 0;
+    unsigned long long itemBase = 0;
+    if constexpr (MAT) {
+      if (itemCursor) {
+        itemBase = a.itemOffsets[w];
+        if (t == 0) itemCursorLds = 0;
+      }
+    }
     const uint64_t matchesBefore = matches;
-    if (itemCursor && t == 0) itemCursorLds = 0;
 
     // First inner batch and first outer batch are in flight while the table is cleared.
     V rv[BP_K], sv[BP_K];
@@ -278,7 +293,7 @@ __global__ __launch_bounds__(BPT, 4) void buildProbeKernel(BPArgs a, const BPIte
         }
       }
     }
-    if (!MAT && a.itemCounts) {  // count pre-pass of a two-pass materialization
+    if constexpr (ITEMS) {
       const unsigned long long im =
           blockReduceSum<BPT, unsigned long long>((unsigned long long)(matches - matchesBefore), wsum);
       if (t == 0) a.itemCounts[w] = (uint32_t)im;
@@ -298,13 +313,21 @@ void buildProbe(const BPArgs &a, const BPItem *items, const uint32_t *nItems, ui
   const uint32_t blocks = capacity < maxBlocks ? capacity : maxBlocks;
   switch (bpMode(a)) {
     case BP_CCOUNT:
-      hipLaunchKernelGGL(buildProbeKernel<BP_CCOUNT>, dim3(blocks), dim3(BPT), lds, s, a, items, nItems, capacity);
+      if (a.itemCounts)
+        hipLaunchKernelGGL((buildProbeKernel<BP_CCOUNT, true>), dim3(blocks), dim3(BPT), lds, s, a, items, nItems,
+                           capacity);
+      else
+        hipLaunchKernelGGL(buildProbeKernel<BP_CCOUNT>, dim3(blocks), dim3(BPT), lds, s, a, items, nItems, capacity);
       break;
     case BP_CMAT:
       hipLaunchKernelGGL(buildProbeKernel<BP_CMAT>, dim3(blocks), dim3(BPT), lds, s, a, items, nItems, capacity);
       break;
     case BP_WCOUNT:
-      hipLaunchKernelGGL(buildProbeKernel<BP_WCOUNT>, dim3(blocks), dim3(BPT), lds, s, a, items, nItems, capacity);
+      if (a.itemCounts)
+        hipLaunchKernelGGL((buildProbeKernel<BP_WCOUNT, true>), dim3(blocks), dim3(BPT), lds, s, a, items, nItems,
+                           capacity);
+      else
+        hipLaunchKernelGGL(buildProbeKernel<BP_WCOUNT>, dim3(blocks), dim3(BPT), lds, s, a, items, nItems, capacity);
       break;
     default:
       hipLaunchKernelGGL(buildProbeKernel<BP_WMAT>, dim3(blocks), dim3(BPT), lds, s, a, items, nItems, capacity);
