@@ -21,6 +21,8 @@ namespace memory {
 class Arena {
  public:
   static constexpr uint64_t ALIGNMENT = 256;  // >= a 128-B L2 line, 16-B LDS-DMA friendly
+  static constexpr uint64_t BIG_BYTES = 4ull << 20;
+  static constexpr uint64_t BIG_ALIGNMENT = 2ull << 20;
 
   Arena(Location loc, int device = 0) : loc_(loc), device_(device) {}
   ~Arena();
