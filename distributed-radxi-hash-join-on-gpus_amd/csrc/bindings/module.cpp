@@ -422,6 +422,8 @@ py::dict resultToDict(const operators::JoinResult &r) {
   d["output_pairs"] = r.outputPairs;
   d["output_overflow"] = r.outputOverflow;
   d["reruns"] = r.reruns;
+  d["sampled_network"] = r.sampledNetwork;
+  d["network_fallbacks"] = r.networkFallbacks;
   d["join_ms"] = r.joinMs;
   d["histogram_ms"] = r.histogramMs;
   d["window_ms"] = r.windowMs;
@@ -477,6 +479,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .value("AUTO", core::KeyHashing::Auto)
       .value("OFF", core::KeyHashing::Off)
       .value("ON", core::KeyHashing::On);
+  py::enum_<core::NetworkHistogram>(m, "NetworkHistogram")
+      .value("AUTO", core::NetworkHistogram::Auto)
+      .value("EXACT", core::NetworkHistogram::Exact)
+      .value("SAMPLED", core::NetworkHistogram::Sampled);
   py::class_<core::JoinConfig>(m, "JoinConfig")
       .def(py::init<>())
       .def_readwrite("network_bits", &core::JoinConfig::networkBits)
@@ -487,6 +493,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("format", &core::JoinConfig::format)
       .def_readwrite("materialize", &core::JoinConfig::materialize)
       .def_readwrite("key_hashing", &core::JoinConfig::keyHashing)
+      .def_readwrite("network_histogram", &core::JoinConfig::networkHistogram)
+      .def_readwrite("sample_stride", &core::JoinConfig::sampleStride)
       .def_readwrite("output_capacity", &core::JoinConfig::outputCapacity)
       .def_readwrite("build_target", &core::JoinConfig::buildTarget)
       .def_readwrite("r_chunk", &core::JoinConfig::rChunk)
@@ -500,6 +508,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("number_of_nodes", &core::JoinPlan::numberOfNodes)
       .def_readonly("network_bits", &core::JoinPlan::networkBits)
       .def_readonly("key_mix", &core::JoinPlan::keyMix)
+      .def_readonly("sampled_network", &core::JoinPlan::sampledNetwork)
       .def_readonly("local_bits", &core::JoinPlan::localBits)
       .def_readonly("key_shift", &core::JoinPlan::keyShift)
       .def_readonly("frag_shift", &core::JoinPlan::fragShift)

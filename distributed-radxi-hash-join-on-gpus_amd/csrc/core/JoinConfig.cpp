@@ -18,9 +18,9 @@ std::string JoinConfig::describe() const {
 
 std::string JoinPlan::describe() const {
   return utils::format("JoinPlan(nodes=%u networkBits=%u localBits=%u twoLevel=%d keyShift=%u fragShift=%u "
-                       "rChunk=%u sChunk=%u chunks=%u wide=%d materialize=%d keyMix=%d assignment=%s)",
+                       "rChunk=%u sChunk=%u chunks=%u wide=%d materialize=%d keyMix=%d sampled=%d assignment=%s)",
                        numberOfNodes, networkBits, localBits, (int)twoLevel, keyShift, fragShift, rChunk, sChunk,
-                       chunks, (int)wide, (int)materialize, (int)keyMix,
+                       chunks, (int)wide, (int)materialize, (int)keyMix, (int)sampledNetwork,
                        assignment == AssignmentPolicy::LPT ? "lpt" : "round_robin");
 }
 

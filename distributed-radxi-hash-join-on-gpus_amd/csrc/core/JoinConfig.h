@@ -30,6 +30,13 @@ enum class KeyHashing : int {
   On = 2,
 };
 
+// How a single-rank device join sizes its network partitions.
+enum class NetworkHistogram : int {
+  Auto = 0,     // Sampled when N == 1 on a device, one chunk and >= 16M tuples per relation; else Exact
+  Exact = 1,    // full histogram pass (always the case for N > 1: the exchange needs exact counts)
+  Sampled = 2,  // tasks/SampledNetworkPartitioning (N == 1 device only; exact fallback on overflow)
+};
+
 struct JoinConfig {
   uint32_t networkBits = 0;   // radix bits of the network pass (0 = auto)
   uint32_t localBits = 0;     // radix bits of the local pass (0 = auto; ignored if !twoLevel)
@@ -46,6 +53,8 @@ struct JoinConfig {
   bool checks = true;           // cheap always-on invariants (all tuples written, sizes)
   uint32_t maxPartitionBlocks = 2048;  // network-pass grid cap (~8 WGs per CU)
   KeyHashing keyHashing = KeyHashing::Auto;
+  NetworkHistogram networkHistogram = NetworkHistogram::Auto;
+  uint32_t sampleStride = 16;   // sampled network pass: histogram 1 tile in sampleStride
 
   std::string describe() const;
 };
@@ -65,6 +74,7 @@ struct JoinPlan {
   bool wide = false;
   bool materialize = false;
   bool keyMix = false;        // radix digits from kernels::KeyMix{keyBits} of the key
+  bool sampledNetwork = false;  // single-rank network pass sized from a sampled histogram
   AssignmentPolicy assignment = AssignmentPolicy::LPT;
   uint64_t networkPartitions() const { return uint64_t(1) << networkBits; }
   uint64_t localPartitions() const { return twoLevel ? (uint64_t(1) << localBits) : 1; }

@@ -1,5 +1,7 @@
 #include "Window.h"
 
+#include <algorithm>
+
 #include "../comm/Communicator.h"
 #include "../memory/Arena.h"
 #include "../utils/Hip.h"
@@ -21,6 +23,13 @@ Window::Window(const histograms::ExchangePlan &plan, histograms::GlobalHistogram
       HIP_CHECK(hipEventCreateWithFlags(&done[c], hipEventDisableTiming));
     }
   }
+}
+
+Window::Window(const histograms::ExchangePlan &plan, uint64_t capacityTuples, core::ExecContext *ctx, bool wide)
+    : plan(plan), globalHistogram(nullptr), assignment(nullptr), ctx(ctx), wide(wide) {
+  localWindowSize = capacityTuples;
+  data = ctx->workspace().get(std::max<uint64_t>(capacityTuples, 1) * tupleBytes());
+  exchanged.assign(std::max<uint32_t>(plan.chunks, 1), false);
 }
 
 Window::~Window() {
@@ -94,9 +103,10 @@ Tuple *Window::getWidePartition(uint32_t partitionId) {
   return static_cast<Tuple *>(base) + plan.lpBase[lp];
 }
 
-uint64_t Window::computeLocalWindowSize() { return localWindowSize; }
+uint64_t Window::computeLocalWindowSize() { return plan.recvTotal; }
 
 uint64_t Window::computeWindowSize(uint32_t nodeId) {
+  if (!globalHistogram) return nodeId == plan.nodeId ? plan.recvTotal : 0;
   const uint32_t *owner = assignment->getPartitionAssignment();
   const uint64_t *g = globalHistogram->getGlobalHistogram();
   uint64_t s = 0;
@@ -110,8 +120,8 @@ void Window::assertAllTuplesWritten() {
   // global histogram mass of the partitions this node owns.
   for (uint32_t c = 0; c < plan.chunks; ++c)
     HJ_CHECK(exchanged[c] || plan.numberOfNodes == 1, "window chunk %u was never exchanged", c);
-  HJ_CHECK(computeWindowSize(plan.nodeId) == localWindowSize, "window holds %lu tuples, owners expect %lu",
-           (unsigned long)localWindowSize, (unsigned long)computeWindowSize(plan.nodeId));
+  HJ_CHECK(computeWindowSize(plan.nodeId) == plan.recvTotal, "window holds %lu tuples, owners expect %lu",
+           (unsigned long)plan.recvTotal, (unsigned long)computeWindowSize(plan.nodeId));
 }
 
 }  // namespace data

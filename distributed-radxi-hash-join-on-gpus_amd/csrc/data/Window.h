@@ -28,6 +28,9 @@ class Window {
  public:
   Window(const histograms::ExchangePlan &plan, histograms::GlobalHistogram *globalHistogram,
          histograms::AssignmentMap *assignment, core::ExecContext *ctx, bool wide);
+  // Single-rank window of `capacityTuples` whose plan is filled in after the
+  // scatter (sampled network pass: no histograms, no exchange).
+  Window(const histograms::ExchangePlan &plan, uint64_t capacityTuples, core::ExecContext *ctx, bool wide);
   ~Window();
   Window(const Window &) = delete;
   Window &operator=(const Window &) = delete;

@@ -36,8 +36,11 @@ struct ExchangePlan {
   std::vector<uint64_t> partSize;     // [owned]
   std::vector<uint64_t> lpBase;       // [owned + 1]
   std::vector<Segment> segments;      // by lp, then chunk, then source
+  // Sampled single-rank pass: partitions are runs of estimated slices with
+  // unused tail room between them (segments give the filled parts).
+  bool gapped = false;
   // True when the window is already partition-major (N == 1 and one chunk).
-  bool windowIsPartitionMajor() const { return numberOfNodes == 1 && chunks == 1; }
+  bool windowIsPartitionMajor() const { return numberOfNodes == 1 && chunks == 1 && !gapped; }
 };
 
 }  // namespace histograms

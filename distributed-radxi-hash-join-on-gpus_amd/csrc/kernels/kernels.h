@@ -82,7 +82,11 @@ struct KeyMix {
 
 // blockHist is digit-major [F][blocks] (u32).
 void netHistogram(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
-                  uint32_t *blockHist, hipStream_t s, KeyMix mix = KeyMix());
+                  uint32_t *blockHist, hipStream_t s, KeyMix mix = KeyMix(), uint32_t sampleStride = 1);
+// Sampled variant (sampleStride > 1): every workgroup counts only tiles 0, S,
+// 2S, ... of its own range (estimates for the single-rank sampled network pass).
+// totals[g][d] (u64): blockHist summed over the workgroups of XCD group g.
+void netGroupTotals(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint64_t *totals, hipStream_t s);
 // totals[c][F] = sum of blockHist over the blocks of chunk c (blocksPerChunk each).
 void digitTotals(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint32_t blocksPerChunk,
                  uint32_t chunks, uint64_t *totals, hipStream_t s);
@@ -107,10 +111,14 @@ void netGroupCursors(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uin
 // packed word's spare top bits instead of a separate LDS array).
 void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift, const PartitionGeometry &g,
                 uint32_t blockBegin, uint32_t blockEnd, void *gcur, uint64_t *out, hipStream_t s,
-                uint32_t keyBits = 64, KeyMix mix = KeyMix());
+                uint32_t keyBits = 64, KeyMix mix = KeyMix(), const void *gend = nullptr, int narrowMode = -1);
 void netScatterWide(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
                     uint32_t blockBegin, uint32_t blockEnd, void *gcur, data::Tuple *out, hipStream_t s,
-                    KeyMix mix = KeyMix());
+                    KeyMix mix = KeyMix(), const void *gend = nullptr, int narrowMode = -1);
+// gend (optional, same layout and width as gcur): end of every group slice.
+// Positions claimed past a slice end are not written; the final gcur values
+// tell the caller each slice's demand (the sampled pass re-runs exactly on
+// overflow).  narrowMode: 1/0 = 32/64-bit cursors, -1 = cursorsNarrow(n).
 // Ablation entry (micro-benchmarks): mode 0 = real scatter, 1 = coalesced
 // write-out, 2 = no write-out; 32-bit cursors, compressed output.
 // geometry: 0 = 256x16 (default), 1 = 512x16, 2 = 1024x8, 3 = 1024x16,

@@ -65,7 +65,8 @@ struct Loader<uint64_t> {
 // ------------------------------------------------------- histogram (pass 1)
 __global__ __launch_bounds__(NT) void netHistogramKernel(const ulonglong2 *__restrict__ in, uint64_t n,
                                                          uint32_t tpb, uint32_t bits,
-                                                         uint32_t *__restrict__ blockHist, KeyMix mix) {
+                                                         uint32_t *__restrict__ blockHist, KeyMix mix,
+                                                         uint32_t stride) {
   extern __shared__ __attribute__((aligned(16))) uint32_t hsh[];
   const uint32_t F = 1u << bits, mask = F - 1;
   const int wid = threadIdx.x / WAVE;
@@ -74,7 +75,7 @@ __global__ __launch_bounds__(NT) void netHistogramKernel(const ulonglong2 *__res
   uint32_t *wh = hsh + wid * F;
   const uint64_t begin = (uint64_t)blockIdx.x * tpb * PART_TILE;
   const uint64_t end = min(n, begin + (uint64_t)tpb * PART_TILE);
-  for (uint64_t base = begin; base < end; base += PART_TILE) {
+  for (uint64_t base = begin; base < end; base += (uint64_t)PART_TILE * stride) {
     uint64_t k[PART_ITEMS];
 #pragma unroll
     for (int i = 0; i < (int)PART_ITEMS; ++i) {
@@ -93,11 +94,12 @@ __global__ __launch_bounds__(NT) void netHistogramKernel(const ulonglong2 *__res
 }
 
 void netHistogram(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
-                  uint32_t *blockHist, hipStream_t s, KeyMix mix) {
+                  uint32_t *blockHist, hipStream_t s, KeyMix mix, uint32_t sampleStride) {
   HJ_CHECK(bits >= 1 && bits <= MAX_PART_BITS, "netHistogram: bits=%u out of range", bits);
+  HJ_CHECK(sampleStride >= 1, "netHistogram: sampleStride must be >= 1");
   const size_t lds = size_t(4) << bits << 2;
   hipLaunchKernelGGL(netHistogramKernel, dim3(g.blocks), dim3(NT), lds, s,
-                     reinterpret_cast<const ulonglong2 *>(in), n, g.tilesPerBlock, bits, blockHist, mix);
+                     reinterpret_cast<const ulonglong2 *>(in), n, g.tilesPerBlock, bits, blockHist, mix, sampleStride);
   HIP_CHECK_LAUNCH();
 }
 
@@ -200,6 +202,26 @@ void netGroupCursors(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uin
   else
     hipLaunchKernelGGL(netGroupCursorsKernel<unsigned long long>, dim3(F), dim3(NT), 0, s, blockHist, F, blocks,
                        blocksPerChunk, base, reinterpret_cast<unsigned long long *>(gcur));
+  HIP_CHECK_LAUNCH();
+}
+
+// totals[g][d] = sum of blockHist[d][b] over the blocks b of XCD group g (b % NGROUPS == g).
+__global__ __launch_bounds__(NT) void netGroupTotalsKernel(const uint32_t *__restrict__ blockHist, uint32_t F,
+                                                           uint32_t blocks, unsigned long long *totals) {
+  __shared__ unsigned long long gs[NGROUPS];
+  const uint32_t d = blockIdx.x;
+  if (threadIdx.x < NGROUPS) gs[threadIdx.x] = 0;
+  __syncthreads();
+  unsigned long long mine = 0;  // NT % NGROUPS == 0: thread t only sees group t % NGROUPS
+  for (uint32_t b = threadIdx.x; b < blocks; b += NT) mine += blockHist[(uint64_t)d * blocks + b];
+  atomicAdd(&gs[threadIdx.x % NGROUPS], mine);
+  __syncthreads();
+  if (threadIdx.x < NGROUPS) totals[(uint64_t)threadIdx.x * F + d] = gs[threadIdx.x];
+}
+
+void netGroupTotals(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint64_t *totals, hipStream_t s) {
+  hipLaunchKernelGGL(netGroupTotalsKernel, dim3(F), dim3(NT), 0, s, blockHist, F, blocks,
+                     reinterpret_cast<unsigned long long *>(totals));
   HIP_CHECK_LAUNCH();
 }
 
@@ -318,7 +340,10 @@ __device__ __forceinline__ void loadTile(const typename Pol::InT *__restrict__ s
 // One tile.  FULL tiles (every tile but a range's tail) are branch-free so
 // hipcc can keep all IPT LDS atomics, loads and stores in flight with counted
 // waits; the predicated tail path is only taken once per range.
-template <class Pol, typename CurT, int NTH, int IPT, int MODE, bool FULL, bool CLAIM>
+// BOUNDED (claim mode with estimated slices): l.cursor[d] holds the end of the
+// group's slice of digit d; claimed positions past it are not written (the
+// caller detects the overflow from the final claim cursors and re-runs).
+template <class Pol, typename CurT, int NTH, int IPT, int MODE, bool FULL, bool CLAIM, bool BOUNDED = false>
 __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict__ in, uint64_t base, uint64_t end,
                                             uint32_t count, uint32_t F, const ScatterSmem<Pol, CurT, NTH * IPT> &l,
                                             const Pol &pol, typename Pol::OutT *__restrict__ out,
@@ -391,7 +416,12 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
       else
         d = pol.stagedDigit(x);
       if constexpr (MODE == 0) {
-        out[(uint64_t)(CurT)(l.wbase[d] + (CurT)idx)] = pol.out(x);
+        const CurT pos = (CurT)(l.wbase[d] + (CurT)idx);
+        if constexpr (BOUNDED) {
+          if (pos < l.cursor[d]) out[(uint64_t)pos] = pol.out(x);
+        } else {
+          out[(uint64_t)pos] = pol.out(x);
+        }
       } else if constexpr (MODE == 1) {
         out[base + idx] = pol.out(x);
         asm volatile("" ::"v"(l.wbase[d]));
@@ -408,7 +438,7 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
 //   rank (LDS atomics) | A | scan + per-digit write base | stage into LDS,
 //   prefetch next tile into registers | B | stream the reordered tile out.
 // MODE (ablation only): 0 = real scatter, 1 = coalesced write-out, 2 = none.
-template <class Pol, typename CurT, int NTH, int IPT, int MODE, bool CLAIM = false>
+template <class Pol, typename CurT, int NTH, int IPT, int MODE, bool CLAIM = false, bool BOUNDED = false>
 __device__ __forceinline__ void scatterRange(const typename Pol::InT *__restrict__ in, uint64_t begin, uint64_t end,
                                              uint32_t F, unsigned char *smem, const Pol &pol,
                                              typename Pol::OutT *__restrict__ out, CurT *gcur = nullptr) {
@@ -421,10 +451,10 @@ __device__ __forceinline__ void scatterRange(const typename Pol::InT *__restrict
     loadTile<Pol, NTH, IPT, false>(in + begin, (uint32_t)(end - begin), v);
   for (uint64_t base = begin; base < end; base += TILE) {
     if (base + TILE <= end)
-      scatterTile<Pol, CurT, NTH, IPT, MODE, true, CLAIM>(in, base, end, TILE, F, l, pol, out, v, gcur);
+      scatterTile<Pol, CurT, NTH, IPT, MODE, true, CLAIM, BOUNDED>(in, base, end, TILE, F, l, pol, out, v, gcur);
     else
-      scatterTile<Pol, CurT, NTH, IPT, MODE, false, CLAIM>(in, base, end, (uint32_t)(end - base), F, l, pol, out, v,
-                                                           gcur);
+      scatterTile<Pol, CurT, NTH, IPT, MODE, false, CLAIM, BOUNDED>(in, base, end, (uint32_t)(end - base), F, l, pol,
+                                                                    out, v, gcur);
   }
   __syncthreads();
 }
@@ -458,19 +488,23 @@ __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void netScatterKernel(
 
 // Claim-mode network scatter: cursors come from the group slices (gcur is
 // [NGROUPS][F] for this chunk), so no per-workgroup cursor array is loaded.
-template <class Pol, typename CurT, int NTH, int IPT, int MODE>
+template <class Pol, typename CurT, int NTH, int IPT, int MODE, bool BOUNDED = false>
 __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void netScatterClaimKernel(
     const typename Pol::InT *__restrict__ in, uint64_t n, uint32_t tpb, uint32_t F, Pol pol, uint32_t blockBegin,
-    CurT *__restrict__ gcur, typename Pol::OutT *out) {
+    CurT *__restrict__ gcur, typename Pol::OutT *out, const CurT *__restrict__ gend = nullptr) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t blk = blockBegin + blockIdx.x;
+  CurT *sliceEnd = reinterpret_cast<CurT *>(smem);  // the per-workgroup cursor array is unused in claim mode
   uint32_t *cnt = reinterpret_cast<uint32_t *>(reinterpret_cast<CurT *>(smem) + 2 * F);
-  for (uint32_t d = threadIdx.x; d < F; d += NTH) cnt[d] = 0;
+  const size_t grp = (size_t)(blockIdx.x % NGROUPS) * F;
+  for (uint32_t d = threadIdx.x; d < F; d += NTH) {
+    cnt[d] = 0;
+    if constexpr (BOUNDED) sliceEnd[d] = gend[grp + d];
+  }
   __syncthreads();
   const uint64_t begin = (uint64_t)blk * tpb * PART_TILE;
   const uint64_t end = min(n, begin + (uint64_t)tpb * PART_TILE);
-  scatterRange<Pol, CurT, NTH, IPT, MODE, true>(in, begin, end, F, smem, pol, out,
-                                                gcur + (size_t)(blockIdx.x % NGROUPS) * F);
+  scatterRange<Pol, CurT, NTH, IPT, MODE, true, BOUNDED>(in, begin, end, F, smem, pol, out, gcur + grp);
 }
 
 // Default geometry (measured on MI355X, tools/microbench.py ablation).
@@ -504,30 +538,41 @@ constexpr int CL_IPT = 8;
 template <class Pol>
 static void launchNetClaim(const Pol &pol, const data::Tuple *in, uint64_t n, uint32_t bits,
                            const PartitionGeometry &g, uint32_t blockBegin, uint32_t blockEnd, void *gcur,
-                           void *out, hipStream_t s) {
+                           void *out, hipStream_t s, const void *gend, bool narrow) {
   const uint32_t F = 1u << bits;
-  const bool narrow = cursorsNarrow(n);
   const auto *src = reinterpret_cast<const typename Pol::InT *>(in);
   auto *dst = reinterpret_cast<typename Pol::OutT *>(out);
+  const dim3 grid(blockEnd - blockBegin);
   if (narrow) {
     const size_t lds = ScatterLayout<Pol, uint32_t, CL_NTH * CL_IPT>::bytes(F);
     HJ_CHECK(lds <= 160 * 1024, "scatter LDS %zu too large", lds);
-    hipLaunchKernelGGL((netScatterClaimKernel<Pol, uint32_t, CL_NTH, CL_IPT, 0>), dim3(blockEnd - blockBegin),
-                       dim3(CL_NTH), lds, s, src, n, g.tilesPerBlock, F, pol, blockBegin,
-                       reinterpret_cast<uint32_t *>(gcur), dst);
+    auto *gc = reinterpret_cast<uint32_t *>(gcur);
+    if (gend)
+      hipLaunchKernelGGL((netScatterClaimKernel<Pol, uint32_t, CL_NTH, CL_IPT, 0, true>), grid, dim3(CL_NTH), lds,
+                         s, src, n, g.tilesPerBlock, F, pol, blockBegin, gc, dst,
+                         reinterpret_cast<const uint32_t *>(gend));
+    else
+      hipLaunchKernelGGL((netScatterClaimKernel<Pol, uint32_t, CL_NTH, CL_IPT, 0>), grid, dim3(CL_NTH), lds, s, src,
+                         n, g.tilesPerBlock, F, pol, blockBegin, gc, dst, nullptr);
   } else {
     const size_t lds = ScatterLayout<Pol, unsigned long long, CL_NTH * CL_IPT>::bytes(F);
     HJ_CHECK(lds <= 160 * 1024, "scatter LDS %zu too large", lds);
-    hipLaunchKernelGGL((netScatterClaimKernel<Pol, unsigned long long, CL_NTH, CL_IPT, 0>),
-                       dim3(blockEnd - blockBegin), dim3(CL_NTH), lds, s, src, n, g.tilesPerBlock, F, pol,
-                       blockBegin, reinterpret_cast<unsigned long long *>(gcur), dst);
+    auto *gc = reinterpret_cast<unsigned long long *>(gcur);
+    if (gend)
+      hipLaunchKernelGGL((netScatterClaimKernel<Pol, unsigned long long, CL_NTH, CL_IPT, 0, true>), grid,
+                         dim3(CL_NTH), lds, s, src, n, g.tilesPerBlock, F, pol, blockBegin, gc, dst,
+                         reinterpret_cast<const unsigned long long *>(gend));
+    else
+      hipLaunchKernelGGL((netScatterClaimKernel<Pol, unsigned long long, CL_NTH, CL_IPT, 0>), grid, dim3(CL_NTH),
+                         lds, s, src, n, g.tilesPerBlock, F, pol, blockBegin, gc, dst, nullptr);
   }
   HIP_CHECK_LAUNCH();
 }
 
 void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift, const PartitionGeometry &g,
                 uint32_t blockBegin, uint32_t blockEnd, void *gcur, uint64_t *out, hipStream_t s, uint32_t keyBits,
-                KeyMix mix) {
+                KeyMix mix, const void *gend, int narrowMode) {
+  const bool narrow = narrowMode < 0 ? cursorsNarrow(n) : narrowMode != 0;
   HJ_CHECK(bits >= 1 && bits <= MAX_PART_BITS, "netScatter: bits=%u out of range", bits);
   HJ_CHECK(blockBegin <= blockEnd && blockEnd <= g.blocks, "netScatter: block range [%u,%u) of %u", blockBegin,
            blockEnd, g.blocks);
@@ -538,17 +583,18 @@ void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keySh
   pol.keyShift = keyShift;
   pol.mix = mix;
   if (digitFitsOnTop(bits, keyShift, mix.on ? std::max(keyBits, mix.bits) : keyBits)) {
-    launchNetClaim(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s);
+    launchNetClaim(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
   } else {
     NetCompressedDigPol dpol;
     static_cast<NetCompressedPol &>(dpol) = pol;
-    launchNetClaim(dpol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s);
+    launchNetClaim(dpol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
   }
 }
 
 void netScatterWide(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
                     uint32_t blockBegin, uint32_t blockEnd, void *gcur, data::Tuple *out, hipStream_t s,
-                    KeyMix mix) {
+                    KeyMix mix, const void *gend, int narrowMode) {
+  const bool narrow = narrowMode < 0 ? cursorsNarrow(n) : narrowMode != 0;
   HJ_CHECK(bits >= 1 && bits <= MAX_PART_BITS, "netScatterWide: bits=%u out of range", bits);
   HJ_CHECK(blockBegin <= blockEnd && blockEnd <= g.blocks, "netScatterWide: block range [%u,%u) of %u",
            blockBegin, blockEnd, g.blocks);
@@ -556,7 +602,7 @@ void netScatterWide(const data::Tuple *in, uint64_t n, uint32_t bits, const Part
   NetWidePol pol;
   pol.mask = (1ull << bits) - 1;
   pol.mix = mix;
-  launchNetClaim(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s);
+  launchNetClaim(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
 }
 
 void scatterAblation(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift, const PartitionGeometry &g,

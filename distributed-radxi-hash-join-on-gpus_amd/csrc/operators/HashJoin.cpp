@@ -16,6 +16,7 @@
 #include "../tasks/HistogramComputation.h"
 #include "../tasks/LocalPartitioning.h"
 #include "../tasks/NetworkPartitioning.h"
+#include "../tasks/SampledNetworkPartitioning.h"
 #include "../utils/Fault.h"
 #include "../utils/Hip.h"
 
@@ -90,6 +91,14 @@ void HashJoin::makeJoinPlan() {
   plan = core::makePlan(config, numberOfNodes, innerRelation->getGlobalSize(), outerRelation->getGlobalSize(), mx[0],
                         mx[1]);
   if (config.keyHashing == core::KeyHashing::Auto && plan.keyBits < 64) plan.keyMix = lowKeyBitsSkewed();
+  {
+    const bool eligible = numberOfNodes == 1 && ctx->onDevice() && plan.chunks == 1;
+    const uint64_t small = std::min(innerRelation->getGlobalSize(), outerRelation->getGlobalSize());
+    if (config.networkHistogram == core::NetworkHistogram::Sampled)
+      plan.sampledNetwork = eligible;
+    else if (config.networkHistogram == core::NetworkHistogram::Auto)
+      plan.sampledNetwork = eligible && small >= (16ull << 20);
+  }
   JOIN_DEBUG("HashJoin", "%s", plan.describe().c_str());
   if (ctx->onDevice())
     for (auto &e : ev) HIP_CHECK(hipEventCreate(&e));
@@ -165,45 +174,88 @@ JoinResult HashJoin::runImpl() {
   Measurements::startHistogramComputation();
   utils::faultPoint("histogram");
   std::unique_ptr<performance::TraceRange> trace(new performance::TraceRange("histogram"));
-  tasks::HistogramComputation hc(numberOfNodes, nodeId, innerRelation, outerRelation, ctx, plan,
-                                 config.maxPartitionBlocks);
-  hc.execute();
-  if (dev) HIP_CHECK(hipEventRecord(ev[1], ctx->stream()));
-  Measurements::stopHistogramComputation();
-  Measurements::storeHistogramDetails(hc.localUs, innerRelation->getLocalSize(), outerRelation->getLocalSize(),
-                                      hc.globalUs, hc.assignUs, hc.offsetUs);
-  const uint64_t t1 = nowUs();
-
-  // ------------------------------------------------------------------ windows
-  Measurements::startWindowAllocation();
-  data::Window innerWindow(hc.innerOffsetMap()->getExchangePlan(), hc.innerGlobal(), hc.assignmentMap(), ctx,
-                           plan.wide);
-  data::Window outerWindow(hc.outerOffsetMap()->getExchangePlan(), hc.outerGlobal(), hc.assignmentMap(), ctx,
-                           plan.wide);
-  Measurements::stopWindowAllocation();
-  const uint64_t t2 = nowUs();
-
-  // ------------------------------------------------------------------ network
-  Measurements::startNetworkPartitioning();
-  trace.reset();  // roctx ranges nest: pop before the next push
-  utils::faultPoint("network");
-  trace.reset(new performance::TraceRange("network_partitioning"));
-  {
-    tasks::NetworkPartitioning np(nodeId, innerRelation, outerRelation, &innerWindow, &outerWindow, &hc, ctx, plan);
+  std::unique_ptr<tasks::HistogramComputation> hc;
+  std::unique_ptr<tasks::SampledNetworkPartitioning> sp;
+  std::unique_ptr<data::Window> innerOwned, outerOwned;
+  data::Window *innerWindow = nullptr, *outerWindow = nullptr;
+  const bool sampled = plan.sampledNetwork && !sampledOverflowed;
+  uint64_t t1, t2;
+  if (sampled) {
+    // ---------------------------------------- single-rank sampled network pass
+    sp.reset(new tasks::SampledNetworkPartitioning(innerRelation, outerRelation, ctx, plan,
+                                                   config.maxPartitionBlocks, config.sampleStride));
+    const uint64_t h0 = nowUs();
+    sp->sample();
+    if (dev) HIP_CHECK(hipEventRecord(ev[1], ctx->stream()));
+    Measurements::stopHistogramComputation();
+    Measurements::storeHistogramDetails(nowUs() - h0, innerRelation->getLocalSize(), outerRelation->getLocalSize(),
+                                        0, 0, 0);
+    t1 = nowUs();
+    Measurements::startWindowAllocation();
+    sp->layout();
+    Measurements::stopWindowAllocation();
+    t2 = nowUs();
+    Measurements::startNetworkPartitioning();
+    trace.reset();  // roctx ranges nest: pop before the next push
+    utils::faultPoint("network");
+    trace.reset(new performance::TraceRange("network_partitioning"));
+    if (sp->scatter()) {
+      innerWindow = sp->innerWindow();
+      outerWindow = sp->outerWindow();
+    } else {
+      // A slice overflowed: the sample missed skew.  Redo this join (and all
+      // later ones) with the exact histogram path.
+      sampledOverflowed = true;
+      ++result.networkFallbacks;
+    }
+  }
+  if (!innerWindow) {
+    if (!sampled) {
+      hc.reset(new tasks::HistogramComputation(numberOfNodes, nodeId, innerRelation, outerRelation, ctx, plan,
+                                               config.maxPartitionBlocks));
+      hc->execute();
+      if (dev) HIP_CHECK(hipEventRecord(ev[1], ctx->stream()));
+      Measurements::stopHistogramComputation();
+      Measurements::storeHistogramDetails(hc->localUs, innerRelation->getLocalSize(), outerRelation->getLocalSize(),
+                                          hc->globalUs, hc->assignUs, hc->offsetUs);
+      t1 = nowUs();
+      Measurements::startWindowAllocation();
+    } else {
+      hc.reset(new tasks::HistogramComputation(numberOfNodes, nodeId, innerRelation, outerRelation, ctx, plan,
+                                               config.maxPartitionBlocks));
+      hc->execute();
+    }
+    innerOwned.reset(new data::Window(hc->innerOffsetMap()->getExchangePlan(), hc->innerGlobal(),
+                                      hc->assignmentMap(), ctx, plan.wide));
+    outerOwned.reset(new data::Window(hc->outerOffsetMap()->getExchangePlan(), hc->outerGlobal(),
+                                      hc->assignmentMap(), ctx, plan.wide));
+    innerWindow = innerOwned.get();
+    outerWindow = outerOwned.get();
+    if (!sampled) {
+      Measurements::stopWindowAllocation();
+      t2 = nowUs();
+      // ---------------------------------------------------------------- network
+      Measurements::startNetworkPartitioning();
+      trace.reset();  // roctx ranges nest: pop before the next push
+      utils::faultPoint("network");
+      trace.reset(new performance::TraceRange("network_partitioning"));
+    }
+    tasks::NetworkPartitioning np(nodeId, innerRelation, outerRelation, innerWindow, outerWindow, hc.get(), ctx,
+                                  plan);
     np.execute();
   }
   Measurements::stopNetworkPartitioning();
   Measurements::storeNetworkDetails(innerRelation->getLocalSize(), outerRelation->getLocalSize(),
-                                    hc.innerLocal()->getChunkCount());
+                                    hc ? hc->innerLocal()->getChunkCount() : 1);
   Measurements::startWaitingForNetworkCompletion();
   // Only the inner window is awaited here (a stream wait, no host sync): the
   // outer relation's all-to-all keeps running on the exchange stream while the
   // inner relation's local radix pass runs; LocalPartitioning waits for the
   // outer window right before its own pass.
-  innerWindow.stop();
-  if (config.checks) {
-    innerWindow.assertAllTuplesWritten();
-    outerWindow.assertAllTuplesWritten();
+  innerWindow->stop();
+  if (config.checks && hc) {
+    innerWindow->assertAllTuplesWritten();
+    outerWindow->assertAllTuplesWritten();
   }
   if (dev) HIP_CHECK(hipEventRecord(ev[2], ctx->stream()));
   Measurements::stopWaitingForNetworkCompletion();
@@ -214,7 +266,7 @@ JoinResult HashJoin::runImpl() {
   trace.reset();  // roctx ranges nest: pop before the next push
   utils::faultPoint("local");
   trace.reset(new performance::TraceRange("local_processing"));
-  auto *lp = new tasks::LocalPartitioning(&innerWindow, &outerWindow, ctx, plan);
+  auto *lp = new tasks::LocalPartitioning(innerWindow, outerWindow, ctx, plan);
   TASK_QUEUE.push(lp);
   Measurements::stopLocalProcessingPreparations();
   Measurements::startLocalProcessing();
@@ -232,7 +284,7 @@ JoinResult HashJoin::runImpl() {
     if (t->getType() == TASK_PARTITION) {
       if (dev) HIP_CHECK(hipEventRecord(ev[3], ctx->stream()));
       result.localItems = lp->workItems();
-      bp.reset(new tasks::BuildProbe(&innerWindow, &outerWindow, ctx, plan, config.outputCapacity));
+      bp.reset(new tasks::BuildProbe(innerWindow, outerWindow, ctx, plan, config.outputCapacity));
       TASK_QUEUE.push(bp.get());
     }
   }
@@ -254,8 +306,9 @@ JoinResult HashJoin::runImpl() {
   result.buildProbeItems = bp->getWorkItems();
   output = bp->getOutput();
   bp.reset();
-  result.innerReceived = innerWindow.computeLocalWindowSize();
-  result.outerReceived = outerWindow.computeLocalWindowSize();
+  result.innerReceived = innerWindow->computeLocalWindowSize();
+  result.outerReceived = outerWindow->computeLocalWindowSize();
+  result.sampledNetwork = sampled && !sampledOverflowed;
   Measurements::storeLocalPartitioningDetails(result.innerReceived + result.outerReceived, result.localItems);
   Measurements::storeBuildProbeDetails(result.innerReceived, result.outerReceived, result.buildProbeItems);
   Measurements::storeResultTuples(result.localMatches);

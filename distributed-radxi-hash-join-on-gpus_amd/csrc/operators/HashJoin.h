@@ -37,6 +37,8 @@ struct JoinResult {
   uint64_t innerReceived = 0, outerReceived = 0;
   uint64_t localItems = 0, buildProbeItems = 0;
   uint64_t innerLocal = 0, outerLocal = 0;
+  bool sampledNetwork = false;     // network pass sized from a sampled histogram (N == 1)
+  uint32_t networkFallbacks = 0;   // sampled pass overflowed -> exact re-run inside this join
 };
 
 class HashJoin {
@@ -79,6 +81,7 @@ class HashJoin {
   core::JoinConfig config;
   core::JoinPlan plan;
   JoinResult result;
+  bool sampledOverflowed = false;  // sticky: exact histograms after a sampled pass overflowed
   const ulonglong2 *output = nullptr;
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
 };

@@ -1,0 +1,184 @@
+#include "SampledNetworkPartitioning.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "../memory/Arena.h"
+#include "../utils/Hip.h"
+
+namespace hpcjoin {
+namespace tasks {
+
+using kernels::CLAIM_GROUPS;
+
+SampledNetworkPartitioning::SampledNetworkPartitioning(data::Relation *innerRelation, data::Relation *outerRelation,
+                                                       core::ExecContext *ctx, const core::JoinPlan &plan,
+                                                       uint32_t maxBlocks, uint32_t sampleStride)
+    : ctx(ctx), plan(plan), maxBlocks(maxBlocks), sampleStride(std::max<uint32_t>(1, sampleStride)) {
+  JOIN_ASSERT(ctx->onDevice() && ctx->numberOfNodes() == 1, "SampledNetwork", "single-rank device path only");
+  sides[0].relation = innerRelation;
+  sides[1].relation = outerRelation;
+}
+
+SampledNetworkPartitioning::~SampledNetworkPartitioning() {}
+
+void SampledNetworkPartitioning::sample() {
+  const uint32_t F = 1u << plan.networkBits;
+  const kernels::KeyMix mix{plan.keyMix ? 1u : 0u, plan.keyBits};
+  for (Side &s : sides) {
+    const uint64_t n = s.relation->getLocalSize();
+    s.geom = kernels::partitionGeometry(n, maxBlocks);
+    uint32_t *blockHist = ctx->workspace().getArray<uint32_t>((uint64_t)F * s.geom.blocks);
+    s.groupTotalsDev = ctx->workspace().getArray<uint64_t>((uint64_t)CLAIM_GROUPS * F);
+    kernels::netHistogram(s.relation->getData(), n, plan.networkBits, s.geom, blockHist, ctx->stream(), mix,
+                          sampleStride);
+    kernels::netGroupTotals(blockHist, F, s.geom.blocks, s.groupTotalsDev, ctx->stream());
+    s.sampled.assign((size_t)CLAIM_GROUPS * F, 0);
+    ctx->copy(s.sampled.data(), s.groupTotalsDev, s.sampled.size() * 8, false, true);
+  }
+  HIP_CHECK(hipStreamSynchronize(ctx->stream()));
+}
+
+void SampledNetworkPartitioning::layout() {
+  const uint32_t F = 1u << plan.networkBits, G = CLAIM_GROUPS;
+  for (Side &s : sides) {
+    const uint64_t n = s.relation->getLocalSize();
+    // Tuples each group scatters, and how many of them the sample read.
+    std::vector<double> total(G, 0.0), seen(G, 0.0);
+    const uint64_t span = (uint64_t)s.geom.tilesPerBlock * kernels::PART_TILE;
+    for (uint32_t b = 0; b < s.geom.blocks; ++b) {
+      const uint64_t begin = (uint64_t)b * span, end = std::min(n, begin + span);
+      if (begin >= end) continue;
+      total[b % G] += (double)(end - begin);
+      for (uint64_t t = begin; t < end; t += (uint64_t)kernels::PART_TILE * sampleStride)
+        seen[b % G] += (double)std::min<uint64_t>(kernels::PART_TILE, end - t);
+    }
+    s.start.assign((size_t)G * F, 0);
+    s.cap.assign((size_t)G * F, 0);
+    uint64_t cur = 0;
+    for (uint32_t d = 0; d < F; ++d)
+      for (uint32_t g = 0; g < G; ++g) {
+        const size_t i = (size_t)g * F + d;
+        double est = 0;
+        if (seen[g] > 0) est = (double)s.sampled[i] * total[g] / seen[g];
+        // Sampling error of a count scaled by total/seen is ~sqrt(est * total/seen);
+        // 6 sigma + 2% + a fixed floor keeps overflows (and their exact re-run) rare.
+        const double scale = seen[g] > 0 ? total[g] / seen[g] : 1.0;
+        const double margin = 6.0 * std::sqrt(std::max(est, 1.0) * scale) + 0.02 * est + 256.0;
+        const uint64_t cap = std::min<uint64_t>((uint64_t)std::ceil(est + margin), (uint64_t)total[g]);
+        s.start[i] = cur;
+        s.cap[i] = cap;
+        cur += cap;
+      }
+    s.capacityTotal = cur;
+    s.narrow = kernels::cursorsNarrow(cur);
+    // Plan skeleton (filled after the scatter); the window is sized by capacity.
+    histograms::ExchangePlan &x = s.xp;
+    x = histograms::ExchangePlan();
+    x.numberOfNodes = 1;
+    x.nodeId = 0;
+    x.partitions = F;
+    x.chunks = 1;
+    x.gapped = true;
+    x.owned.resize(F);
+    x.localIndex.resize(F);
+    for (uint32_t p = 0; p < F; ++p) {
+      x.owned[p] = p;
+      x.localIndex[p] = (int32_t)p;
+    }
+    x.sendTotal = n;
+    x.recvTotal = 0;
+    s.window.reset(new data::Window(x, cur, ctx, plan.wide));
+    // Claim cursors (slice starts) and slice ends, in the scatter's cursor width.
+    const size_t cb = s.narrow ? 4 : 8;
+    s.gcur = ctx->workspace().get((size_t)G * F * cb);
+    s.gend = ctx->workspace().get((size_t)G * F * cb);
+    if (s.narrow) {
+      std::vector<uint32_t> a((size_t)G * F), e((size_t)G * F);
+      for (size_t i = 0; i < a.size(); ++i) {
+        a[i] = (uint32_t)s.start[i];
+        e[i] = (uint32_t)(s.start[i] + s.cap[i]);
+      }
+      HIP_CHECK(hipMemcpyAsync(s.gcur, a.data(), a.size() * 4, hipMemcpyHostToDevice, ctx->stream()));
+      HIP_CHECK(hipMemcpyAsync(s.gend, e.data(), e.size() * 4, hipMemcpyHostToDevice, ctx->stream()));
+      HIP_CHECK(hipStreamSynchronize(ctx->stream()));  // host vectors go out of scope
+    } else {
+      std::vector<uint64_t> e((size_t)G * F);
+      for (size_t i = 0; i < e.size(); ++i) e[i] = s.start[i] + s.cap[i];
+      HIP_CHECK(hipMemcpyAsync(s.gcur, s.start.data(), e.size() * 8, hipMemcpyHostToDevice, ctx->stream()));
+      HIP_CHECK(hipMemcpyAsync(s.gend, e.data(), e.size() * 8, hipMemcpyHostToDevice, ctx->stream()));
+      HIP_CHECK(hipStreamSynchronize(ctx->stream()));
+    }
+  }
+}
+
+bool SampledNetworkPartitioning::scatter() {
+  const uint32_t F = 1u << plan.networkBits, G = CLAIM_GROUPS;
+  const kernels::KeyMix mix{plan.keyMix ? 1u : 0u, plan.keyBits};
+  std::vector<std::vector<uint32_t>> c32(2);
+  for (int k = 0; k < 2; ++k) {
+    Side &s = sides[k];
+    const uint64_t n = s.relation->getLocalSize();
+    s.window->start();
+    const int nm = s.narrow ? 1 : 0;
+    if (plan.wide)
+      kernels::netScatterWide(s.relation->getData(), n, plan.networkBits, s.geom, 0, s.geom.blocks, s.gcur,
+                              static_cast<data::Tuple *>(s.window->getData()), ctx->stream(), mix, s.gend, nm);
+    else
+      kernels::netScatter(s.relation->getData(), n, plan.networkBits, plan.keyShift, s.geom, 0, s.geom.blocks,
+                          s.gcur, static_cast<uint64_t *>(s.window->getData()), ctx->stream(), plan.keyBits, mix,
+                          s.gend, nm);
+  }
+  for (int k = 0; k < 2; ++k) {
+    Side &s = sides[k];
+    s.fill.assign((size_t)G * F, 0);
+    if (s.narrow) {
+      c32[k].assign((size_t)G * F, 0);
+      HIP_CHECK(hipMemcpyAsync(c32[k].data(), s.gcur, c32[k].size() * 4, hipMemcpyDeviceToHost, ctx->stream()));
+    } else {
+      HIP_CHECK(hipMemcpyAsync(s.fill.data(), s.gcur, s.fill.size() * 8, hipMemcpyDeviceToHost, ctx->stream()));
+    }
+  }
+  HIP_CHECK(hipStreamSynchronize(ctx->stream()));
+  bool ok = true;
+  for (int k = 0; k < 2; ++k) {
+    Side &s = sides[k];
+    uint64_t sum = 0;
+    for (size_t i = 0; i < s.fill.size(); ++i) {
+      const uint64_t end = s.narrow ? c32[k][i] : s.fill[i];  // final claim cursor
+      s.fill[i] = end - s.start[i];
+      sum += s.fill[i];
+      if (s.fill[i] > s.cap[i]) ok = false;
+    }
+    HJ_CHECK(sum == s.relation->getLocalSize(), "sampled network pass claimed %lu of %lu tuples", (unsigned long)sum,
+             (unsigned long)s.relation->getLocalSize());
+  }
+  if (!ok) return false;
+  for (Side &s : sides) finishPlan(s);
+  return true;
+}
+
+void SampledNetworkPartitioning::finishPlan(Side &s) {
+  const uint32_t F = 1u << plan.networkBits, G = CLAIM_GROUPS;
+  histograms::ExchangePlan &x = s.xp;
+  x.partSize.assign(F, 0);
+  x.lpBase.assign(F + 1, 0);
+  x.segments.clear();
+  for (uint32_t d = 0; d < F; ++d) {
+    for (uint32_t g = 0; g < G; ++g) {
+      const size_t i = (size_t)g * F + d;
+      if (s.fill[i]) x.segments.push_back(histograms::Segment{s.start[i], s.fill[i], d, 0, g});
+      x.partSize[d] += s.fill[i];
+    }
+    x.lpBase[d + 1] = x.lpBase[d] + x.partSize[d];
+  }
+  x.recvTotal = x.lpBase[F];
+  x.sendCounts.assign(1, x.recvTotal);
+  x.sendDispls.assign(1, 0);
+  x.recvCounts.assign(1, x.recvTotal);
+  x.recvDispls.assign(1, 0);
+}
+
+}  // namespace tasks
+}  // namespace hpcjoin

@@ -1,0 +1,69 @@
+// Single-rank network pass without the exact histogram read.
+//
+// With one rank nothing is exchanged, so the network histogram is only needed
+// to size the partition regions -- and reading both relations once just to
+// count costs a full pass over the input (16 B per tuple, ~20% of a 1B x 1B
+// join).  Here every workgroup histograms 1 tile in `sampleStride` of its own
+// range; each (XCD group, digit) claim slice gets the estimate plus a
+// statistical margin (6 sigma of the sampling error + 2%), and the bounded
+// claim-mode scatter (kernels::netScatter with gend) fills the slices.  The
+// final claim cursors give every slice's exact fill; the window's plan lists
+// the filled slices as segments, which is all the local pass needs.  If a
+// slice overflowed (skew the sample missed), the caller discards this pass and
+// runs the exact histogram path (HashJoin keeps using it afterwards).
+//
+// Replaces, for N == 1, HistogramComputation + NetworkPartitioning
+// (reference: histograms/LocalHistogram.cpp:35-53 + tasks/NetworkPartitioning.cpp:74-222).
+#pragma once
+
+#include <memory>
+#include <vector>
+
+#include "../core/ExecContext.h"
+#include "../core/JoinConfig.h"
+#include "../data/Relation.h"
+#include "../data/Window.h"
+#include "../histograms/ExchangePlan.h"
+#include "../kernels/kernels.h"
+
+namespace hpcjoin {
+namespace tasks {
+
+class SampledNetworkPartitioning {
+ public:
+  SampledNetworkPartitioning(data::Relation *innerRelation, data::Relation *outerRelation, core::ExecContext *ctx,
+                             const core::JoinPlan &plan, uint32_t maxBlocks, uint32_t sampleStride);
+  ~SampledNetworkPartitioning();
+
+  void sample();   // sampled histograms of both relations (one host sync)
+  void layout();   // slice layout + windows
+  bool scatter();  // bounded scatter of both relations, fill read back (one host sync); false = overflow
+
+  data::Window *innerWindow() { return sides[0].window.get(); }
+  data::Window *outerWindow() { return sides[1].window.get(); }
+  uint64_t capacity(int side) const { return sides[side].capacityTotal; }
+
+ private:
+  struct Side {
+    data::Relation *relation = nullptr;
+    kernels::PartitionGeometry geom;
+    histograms::ExchangePlan xp;
+    std::unique_ptr<data::Window> window;
+    uint64_t *groupTotalsDev = nullptr;
+    std::vector<uint64_t> sampled;     // [groups][F] sampled counts
+    std::vector<uint64_t> start, cap;  // [groups][F] slice start / capacity (tuples)
+    std::vector<uint64_t> fill;        // [groups][F] claimed after the scatter
+    void *gcur = nullptr, *gend = nullptr;
+    bool narrow = true;
+    uint64_t capacityTotal = 0;
+  };
+  void finishPlan(Side &s);
+
+  core::ExecContext *ctx;
+  const core::JoinPlan &plan;
+  uint32_t maxBlocks, sampleStride;
+  Side sides[2];
+};
+
+}  // namespace tasks
+}  // namespace hpcjoin

@@ -155,3 +155,62 @@ def test_key_hashing(C, dev, fmt):
     D = C.Relation(G_R, G_R, loc, 0)
     D.generate(C.GenSpec(seed=9), 0)
     assert not C.HashJoin(D, D, ctx, C.JoinConfig()).plan.key_mix
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dist,fmt,mat", [("UNIQUE", "COMPRESSED", False), ("ZIPF", "COMPRESSED", False),
+                                          ("MODULO", "WIDE", False), ("UNIFORM", "COMPRESSED", True)])
+def test_sampled_network_pass(C, cuda, dist, fmt, mat):
+    """Single-rank device joins size the network pass from a sampled histogram
+    (no full histogram read); results equal the exact path."""
+    G_R, G_S = 1 << 22, 3 << 21
+    out = {}
+    for mode in ("SAMPLED", "EXACT"):
+        cfg = C.JoinConfig()
+        cfg.network_histogram = getattr(C.NetworkHistogram, mode)
+        cfg.format = getattr(C.TupleFormat, fmt)
+        cfg.materialize = mat
+        res, exp, j = run_join(C, "cuda", G_R, G_S, dist, cfg=cfg)
+        assert j.plan.sampled_network == (mode == "SAMPLED")
+        assert res["sampled_network"] == (mode == "SAMPLED") and res["network_fallbacks"] == 0
+        assert res["global_matches"] == exp
+        for _ in range(2):
+            assert j.run()["global_matches"] == exp
+        out[mode] = j.output() if mat else None
+    if mat:
+        import torch
+        a, b = (torch.sort(out[m][:, 0] * G_S + out[m][:, 1]).values for m in ("SAMPLED", "EXACT"))
+        assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_sampled_network_overflow_falls_back(C, cuda):
+    """Adversarial layout for the sample: every 4096-tuple tile holds a single
+    network digit, so the sampled tiles (1 in 16 of each workgroup's range) miss
+    most digits.  Slices overflow, the join re-runs exactly, and later joins
+    stay on the exact path."""
+    import torch
+    n = 1 << 22
+    i = torch.arange(n, device="cuda")
+    keys = i * 512 + (i // 4096) % 512  # unique; low 9 bits = tile index mod 512
+    R = torch.stack([keys, i], 1).contiguous()
+    S = torch.stack([keys.flip(0), i], 1).contiguous()
+    ctx = C.ExecContext("device", 0, C.LocalCommunicator())
+    cfg = C.JoinConfig()
+    cfg.network_histogram = C.NetworkHistogram.SAMPLED
+    cfg.key_hashing = C.KeyHashing.OFF
+    cfg.network_bits = 9
+    cfg.max_partition_blocks = 16  # 64 tiles per workgroup, 4 of them sampled
+    j = C.HashJoin(C.Relation.from_tensor(R, n), C.Relation.from_tensor(S, n), ctx, cfg)
+    res = j.run()
+    assert res["network_fallbacks"] == 1 and not res["sampled_network"]
+    assert res["global_matches"] == n
+    res = j.run()
+    assert res["network_fallbacks"] == 0 and res["global_matches"] == n
+
+
+def test_sampled_network_host_is_exact(C):
+    cfg = C.JoinConfig()
+    cfg.network_histogram = C.NetworkHistogram.SAMPLED
+    res, exp, j = run_join(C, "cpu", 100_000, 100_000, cfg=cfg)
+    assert not j.plan.sampled_network and not res["sampled_network"] and res["global_matches"] == exp
