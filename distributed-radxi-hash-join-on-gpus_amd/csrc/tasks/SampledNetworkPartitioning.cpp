@@ -72,7 +72,9 @@ void SampledNetworkPartitioning::layout() {
         cur += cap;
       }
     s.capacityTotal = cur;
-    s.narrow = kernels::cursorsNarrow(cur);
+    // Claims may run past a slice end by up to n before the overflow is seen:
+    // 32-bit cursors only if even that cannot wrap.
+    s.narrow = kernels::cursorsNarrow(cur + n);
     // Plan skeleton (filled after the scatter); the window is sized by capacity.
     histograms::ExchangePlan &x = s.xp;
     x = histograms::ExchangePlan();
