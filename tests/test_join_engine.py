@@ -184,6 +184,15 @@ def test_sampled_network_pass(C, cuda, dist, fmt, mat):
 
 
 @pytest.mark.gpu
+def test_sampled_network_single_level(C, cuda):
+    cfg = C.JoinConfig()
+    cfg.network_histogram = C.NetworkHistogram.SAMPLED
+    cfg.two_level = False
+    res, exp, j = run_join(C, "cuda", 1 << 21, 1 << 21, cfg=cfg)
+    assert j.plan.sampled_network and res["sampled_network"] and res["global_matches"] == exp
+
+
+@pytest.mark.gpu
 def test_sampled_network_overflow_falls_back(C, cuda):
     """Adversarial layout for the sample: every 4096-tuple tile holds a single
     network digit, so the sampled tiles (1 in 16 of each workgroup's range) miss
