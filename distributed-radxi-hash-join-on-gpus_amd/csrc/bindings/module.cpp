@@ -424,6 +424,8 @@ py::dict resultToDict(const operators::JoinResult &r) {
   d["reruns"] = r.reruns;
   d["sampled_network"] = r.sampledNetwork;
   d["network_fallbacks"] = r.networkFallbacks;
+  d["sampled_local"] = r.sampledLocal;
+  d["local_fallbacks"] = r.localFallbacks;
   d["join_ms"] = r.joinMs;
   d["histogram_ms"] = r.histogramMs;
   d["window_ms"] = r.windowMs;
@@ -479,10 +481,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .value("AUTO", core::KeyHashing::Auto)
       .value("OFF", core::KeyHashing::Off)
       .value("ON", core::KeyHashing::On);
-  py::enum_<core::NetworkHistogram>(m, "NetworkHistogram")
-      .value("AUTO", core::NetworkHistogram::Auto)
-      .value("EXACT", core::NetworkHistogram::Exact)
-      .value("SAMPLED", core::NetworkHistogram::Sampled);
+  py::enum_<core::HistogramMode>(m, "HistogramMode")
+      .value("AUTO", core::HistogramMode::Auto)
+      .value("EXACT", core::HistogramMode::Exact)
+      .value("SAMPLED", core::HistogramMode::Sampled);
+  m.attr("NetworkHistogram") = m.attr("HistogramMode");
   py::class_<core::JoinConfig>(m, "JoinConfig")
       .def(py::init<>())
       .def_readwrite("network_bits", &core::JoinConfig::networkBits)
@@ -494,6 +497,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("materialize", &core::JoinConfig::materialize)
       .def_readwrite("key_hashing", &core::JoinConfig::keyHashing)
       .def_readwrite("network_histogram", &core::JoinConfig::networkHistogram)
+      .def_readwrite("local_histogram", &core::JoinConfig::localHistogram)
       .def_readwrite("sample_stride", &core::JoinConfig::sampleStride)
       .def_readwrite("output_capacity", &core::JoinConfig::outputCapacity)
       .def_readwrite("build_target", &core::JoinConfig::buildTarget)

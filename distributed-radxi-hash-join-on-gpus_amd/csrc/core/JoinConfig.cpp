@@ -33,6 +33,8 @@ JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t global
   p.materialize = cfg.materialize;
   p.assignment = cfg.assignment;
   p.chunks = std::max<uint32_t>(1, cfg.chunks);
+  p.localHistogram = cfg.localHistogram;
+  p.sampleStride = std::max<uint32_t>(1, cfg.sampleStride);
   p.sChunk = std::max<uint32_t>(1024, cfg.sChunk);
 
   const uint32_t maxBits = Configuration::GPU_MAX_FANOUT_BITS - 1;  // 1024-way per pass

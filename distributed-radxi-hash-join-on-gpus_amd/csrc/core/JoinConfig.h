@@ -30,11 +30,17 @@ enum class KeyHashing : int {
   On = 2,
 };
 
-// How a single-rank device join sizes its network partitions.
-enum class NetworkHistogram : int {
-  Auto = 0,     // Sampled when N == 1 on a device, one chunk and >= 16M tuples per relation; else Exact
-  Exact = 1,    // full histogram pass (always the case for N > 1: the exchange needs exact counts)
-  Sampled = 2,  // tasks/SampledNetworkPartitioning (N == 1 device only; exact fallback on overflow)
+// How a radix pass sizes its partitions: an exact histogram read of the input,
+// or a sampled one with statistical slack and an exact re-run on overflow.
+//   network pass: Sampled only for N == 1 on a device with one chunk (the
+//                 exchange needs exact counts); Auto = Sampled there when both
+//                 relations have >= 16M tuples (tasks/SampledNetworkPartitioning)
+//   local pass:   Sampled on a device (any N); Auto = Sampled when the window
+//                 holds >= 16M tuples (tasks/LocalPartitioning)
+enum class HistogramMode : int {
+  Auto = 0,
+  Exact = 1,
+  Sampled = 2,
 };
 
 struct JoinConfig {
@@ -53,8 +59,9 @@ struct JoinConfig {
   bool checks = true;           // cheap always-on invariants (all tuples written, sizes)
   uint32_t maxPartitionBlocks = 2048;  // network-pass grid cap (~8 WGs per CU)
   KeyHashing keyHashing = KeyHashing::Auto;
-  NetworkHistogram networkHistogram = NetworkHistogram::Auto;
-  uint32_t sampleStride = 16;   // sampled network pass: histogram 1 tile in sampleStride
+  HistogramMode networkHistogram = HistogramMode::Auto;
+  HistogramMode localHistogram = HistogramMode::Auto;
+  uint32_t sampleStride = 16;   // sampled passes: histogram 1 tile in sampleStride
 
   std::string describe() const;
 };
@@ -75,6 +82,8 @@ struct JoinPlan {
   bool materialize = false;
   bool keyMix = false;        // radix digits from kernels::KeyMix{keyBits} of the key
   bool sampledNetwork = false;  // single-rank network pass sized from a sampled histogram
+  HistogramMode localHistogram = HistogramMode::Exact;  // resolved per window size by LocalPartitioning
+  uint32_t sampleStride = 16;
   AssignmentPolicy assignment = AssignmentPolicy::LPT;
   uint64_t networkPartitions() const { return uint64_t(1) << networkBits; }
   uint64_t localPartitions() const { return twoLevel ? (uint64_t(1) << localBits) : 1; }

@@ -73,9 +73,10 @@ void Window::stop() {
 
 void Window::flush() { stop(); }
 
-void Window::setPartitioned(void *p, const uint64_t *pb, uint32_t bits) {
+void Window::setPartitioned(void *p, const uint64_t *pb, uint32_t bits, const uint64_t *pe) {
   partitioned = p;
   partBegin = pb;
+  partEnd = pe;
   localBits = bits;
 }
 
@@ -89,6 +90,7 @@ CompressedTuple *Window::getPartition(uint32_t partitionId) {
   JOIN_ASSERT(!wide, "Window", "wide window: use getWidePartition");
   const int32_t lp = plan.localIndex.at(partitionId);
   JOIN_ASSERT(lp >= 0, "Window", "partition %u is not owned by node %u", partitionId, plan.nodeId);
+  JOIN_ASSERT(!partEnd, "Window", "gapped local output: use getPartitionBegin/getPartitionEnd");
   void *base = partitioned ? partitioned : (plan.windowIsPartitionMajor() ? data : nullptr);
   JOIN_ASSERT(base, "Window", "partition-major view requires local partitioning first");
   return static_cast<CompressedTuple *>(base) + plan.lpBase[lp];
@@ -98,6 +100,7 @@ Tuple *Window::getWidePartition(uint32_t partitionId) {
   JOIN_ASSERT(wide, "Window", "compressed window: use getPartition");
   const int32_t lp = plan.localIndex.at(partitionId);
   JOIN_ASSERT(lp >= 0, "Window", "partition %u is not owned by node %u", partitionId, plan.nodeId);
+  JOIN_ASSERT(!partEnd, "Window", "gapped local output: use getPartitionBegin/getPartitionEnd");
   void *base = partitioned ? partitioned : (plan.windowIsPartitionMajor() ? data : nullptr);
   JOIN_ASSERT(base, "Window", "partition-major view requires local partitioning first");
   return static_cast<Tuple *>(base) + plan.lpBase[lp];

@@ -54,9 +54,12 @@ class Window {
   bool isWide() const { return wide; }
   const histograms::ExchangePlan &getPlan() const { return plan; }
   // Local partitioning hands back its partition-major output.
-  void setPartitioned(void *partitioned, const uint64_t *partBegin, uint32_t localBits);
+  // partEnd: null when partitions are contiguous (end of p = partBegin[p + 1]).
+  void setPartitioned(void *partitioned, const uint64_t *partBegin, uint32_t localBits,
+                      const uint64_t *partEnd = nullptr);
   void *getPartitionedData() const { return partitioned; }
   const uint64_t *getPartitionBegin() const { return partBegin; }  // [owned * 2^localBits + 1] (ctx location)
+  const uint64_t *getPartitionEnd() const { return partEnd; }      // null, or [owned * 2^localBits] (gapped)
   uint32_t getLocalBits() const { return localBits; }
 
  protected:
@@ -74,6 +77,7 @@ class Window {
   std::vector<bool> exchanged;
   void *partitioned = nullptr;
   const uint64_t *partBegin = nullptr;
+  const uint64_t *partEnd = nullptr;
   uint32_t localBits = 0;
 };
 

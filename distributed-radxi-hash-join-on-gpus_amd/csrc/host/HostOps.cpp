@@ -185,7 +185,8 @@ uint64_t buildProbe(const kernels::BPArgs &a) {
   const uint64_t ridMask = a.keyShift >= 64 ? ~0ull : ((1ull << a.keyShift) - 1);
   std::vector<uint64_t> bucket, next;
   for (uint32_t p = 0; p < a.P; ++p) {
-    const uint64_t rb = a.partR[p], re = a.partR[p + 1], sb = a.partS[p], se = a.partS[p + 1];
+    const uint64_t rb = a.partR[p], re = a.partREnd ? a.partREnd[p] : a.partR[p + 1], sb = a.partS[p],
+                   se = a.partSEnd ? a.partSEnd[p] : a.partS[p + 1];
     const uint64_t nr = re - rb;
     if (nr == 0 || se == sb) continue;
     const uint64_t N = nextPow2(nr);

@@ -59,22 +59,26 @@ __device__ __forceinline__ uint32_t hash64(uint64_t key, uint32_t tbits) {
 }
 
 __global__ __launch_bounds__(BPT) void bpPlanCountsKernel(const uint64_t *__restrict__ partR,
-                                                          const uint64_t *__restrict__ partS, uint32_t P, uint32_t rc,
+                                                          const uint64_t *__restrict__ partS,
+                                                          const uint64_t *__restrict__ partREnd,
+                                                          const uint64_t *__restrict__ partSEnd, uint32_t P, uint32_t rc,
                                                           uint32_t sc, uint32_t *counts) {
   const uint32_t p = blockIdx.x * BPT + threadIdx.x;
   if (p >= P) return;
-  const uint64_t nr = partR[p + 1] - partR[p], ns = partS[p + 1] - partS[p];
+  const uint64_t nr = partREnd[p] - partR[p], ns = partSEnd[p] - partS[p];
   counts[p] = (nr == 0 || ns == 0) ? 0u : (uint32_t)(ceilDiv(nr, rc) * ceilDiv(ns, sc));
 }
 
 void bpPlanCounts(const BPArgs &a, uint32_t *counts, hipStream_t s) {
   if (a.P == 0) return;
-  hipLaunchKernelGGL(bpPlanCountsKernel, dim3(ceilDiv(a.P, BPT)), dim3(BPT), 0, s, a.partR, a.partS, a.P, a.rChunk,
+  hipLaunchKernelGGL(bpPlanCountsKernel, dim3(ceilDiv(a.P, BPT)), dim3(BPT), 0, s, a.partR, a.partS,
+                     a.partREnd ? a.partREnd : a.partR + 1, a.partSEnd ? a.partSEnd : a.partS + 1, a.P, a.rChunk,
                      a.sChunk, counts);
   HIP_CHECK_LAUNCH();
 }
 
-__global__ __launch_bounds__(BPT) void bpEmitKernel(const uint64_t *__restrict__ partS, uint32_t P, uint32_t sc,
+__global__ __launch_bounds__(BPT) void bpEmitKernel(const uint64_t *__restrict__ partS,
+                                                    const uint64_t *__restrict__ partSEnd, uint32_t P, uint32_t sc,
                                                     const uint32_t *__restrict__ counts,
                                                     const uint32_t *__restrict__ offsets, BPItem *items,
                                                     uint32_t capacity) {
@@ -82,7 +86,7 @@ __global__ __launch_bounds__(BPT) void bpEmitKernel(const uint64_t *__restrict__
   if (p >= P) return;
   const uint32_t c = counts[p];
   if (c == 0) return;
-  const uint32_t nsChunks = (uint32_t)ceilDiv(partS[p + 1] - partS[p], sc);
+  const uint32_t nsChunks = (uint32_t)ceilDiv(partSEnd[p] - partS[p], sc);
   const uint32_t o = offsets[p];
   for (uint32_t i = 0; i < c && o + i < capacity; ++i) {
     BPItem it;
@@ -97,7 +101,8 @@ __global__ __launch_bounds__(BPT) void bpEmitKernel(const uint64_t *__restrict__
 void bpEmit(const BPArgs &a, const uint32_t *counts, const uint32_t *offsets, BPItem *items, uint32_t capacity,
             hipStream_t s) {
   if (a.P == 0) return;
-  hipLaunchKernelGGL(bpEmitKernel, dim3(ceilDiv(a.P, BPT)), dim3(BPT), 0, s, a.partS, a.P, a.sChunk, counts, offsets,
+  hipLaunchKernelGGL(bpEmitKernel, dim3(ceilDiv(a.P, BPT)), dim3(BPT), 0, s, a.partS,
+                     a.partSEnd ? a.partSEnd : a.partS + 1, a.P, a.sChunk, counts, offsets,
                      items, capacity);
   HIP_CHECK_LAUNCH();
 }
@@ -176,9 +181,9 @@ __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeK
   for (uint32_t w = blockIdx.x; w < nItems; w += gridDim.x) {
     const BPItem it = items[w];
     const uint64_t rb = a.partR[it.part] + (uint64_t)it.rChunk * a.rChunk;
-    const uint64_t re = min(a.partR[it.part + 1], rb + a.rChunk);
+    const uint64_t re = min(a.partREnd[it.part], rb + a.rChunk);
     const uint64_t sb = a.partS[it.part] + (uint64_t)it.sChunk * a.sChunk;
-    const uint64_t se = min(a.partS[it.part + 1], sb + a.sChunk);
+    const uint64_t se = min(a.partSEnd[it.part], sb + a.sChunk);
     const uint32_t nr = (uint32_t)(re - rb), ns = (uint32_t)(se - sb);
     uint32_t tbits = ceilLog2(2ull * nr);
     if (tbits < 6) tbits = 6;
@@ -304,8 +309,11 @@ __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeK
   if (t == 0 && total) atomicAdd(a.result, total);
 }
 
-void buildProbe(const BPArgs &a, const BPItem *items, const uint32_t *nItems, uint32_t capacity, hipStream_t s) {
+void buildProbe(const BPArgs &args, const BPItem *items, const uint32_t *nItems, uint32_t capacity, hipStream_t s) {
   if (capacity == 0) return;
+  BPArgs a = args;
+  if (!a.partREnd) a.partREnd = a.partR + 1;
+  if (!a.partSEnd) a.partSEnd = a.partS + 1;
   const size_t lds = bpLdsBytes(a);
   HJ_CHECK(lds <= 160 * 1024, "buildProbe: LDS request %zu exceeds 160 KiB (rChunk=%u)", lds, a.rChunk);
   const uint32_t perCu = (uint32_t)((160 * 1024) / lds);

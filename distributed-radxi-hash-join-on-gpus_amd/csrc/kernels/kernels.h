@@ -153,13 +153,27 @@ constexpr uint32_t LOCAL_ITEM_MAX = LOCAL_ITEM_TILES * PART_TILE;  // 65536
 // digit = (word >> shift) & (2^bits - 1).  For compressed tuples word = value,
 // shift = keyShift; for wide tuples word = key, shift = networkBits.
 void localHistogram(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift,
-                    uint32_t bits, uint32_t *itemHist, hipStream_t s);
+                    uint32_t bits, uint32_t *itemHist, hipStream_t s, uint32_t sampleStride = 1);
 // gcur[stream][F] (u32 if narrow else u64) claim slices + partBegin[owned*F+1].
 void localCursors(const uint32_t *itemHist, const uint32_t *lpItemBegin, uint32_t owned, uint32_t bits,
                   const uint64_t *lpBase, const LocalItem *items, void *gcur, bool narrow, uint64_t *partBegin,
                   hipStream_t s);
 void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift,
-                  uint32_t bits, void *gcur, bool narrow, void *out, hipStream_t s);
+                  uint32_t bits, void *gcur, bool narrow, void *out, hipStream_t s, const void *gend = nullptr);
+// Sampled local pass (no exact local histogram): itemHist from
+// localHistogram(sampleStride) -> per-final-partition capacities (estimate +
+// 6 sigma + 2% + 64) -> gapped partition-major layout: gcur = partBegin =
+// starts, gend = starts + caps (64-bit cursors; one claim stream per lp).
+// After the bounded localScatter the final gcur values are the partition ends.
+void localSampledLayout(const uint32_t *itemHist, const uint32_t *lpItemBegin, const LocalItem *items,
+                        uint32_t owned, uint32_t bits, uint32_t sampleStride, uint32_t *caps,
+                        unsigned long long *starts, void *scanWorkspace, unsigned long long *gcur,
+                        unsigned long long *gend, uint64_t *partBegin, hipStream_t s);
+// Upper bound of the layout's total capacity (host-side sizing of the output).
+uint64_t localSampledCapacityBound(uint64_t n, uint64_t partitions, uint32_t sampleStride);
+// *flag |= 1 if any gcur[i] > gend[i] (a bounded claim slice overflowed).
+void claimOverflow(const unsigned long long *gcur, const unsigned long long *gend, uint64_t P, unsigned int *flag,
+                   hipStream_t s);
 
 // --------------------------------------------------------------- build/probe
 struct BPItem {
@@ -173,6 +187,9 @@ struct BPArgs {
   const void *S = nullptr;        // partitioned outer
   const uint64_t *partR = nullptr;  // [P+1] partition begin offsets
   const uint64_t *partS = nullptr;
+  // Partition ends (gapped layouts of the sampled local pass); null = partR + 1 / partS + 1.
+  const uint64_t *partREnd = nullptr;
+  const uint64_t *partSEnd = nullptr;
   uint32_t P = 0;
   uint32_t rChunk = 4096;   // max inner tuples per LDS table
   uint32_t sChunk = 65536;  // max outer tuples per work item

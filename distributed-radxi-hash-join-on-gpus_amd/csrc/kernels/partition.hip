@@ -22,6 +22,8 @@
 #include "kernels.h"
 #include "device_common.h"
 
+#include <algorithm>
+#include <cmath>
 #include <type_traits>
 
 namespace hpcjoin {
@@ -684,7 +686,8 @@ __device__ __forceinline__ uint64_t localWord(const void *in, uint64_t i) {
 template <bool WIDE>
 __global__ __launch_bounds__(NT) void localHistogramKernel(const void *__restrict__ in,
                                                            const LocalItem *__restrict__ items, uint32_t shift,
-                                                           uint32_t bits, uint32_t *__restrict__ itemHist) {
+                                                           uint32_t bits, uint32_t *__restrict__ itemHist,
+                                                           uint32_t stride) {
   extern __shared__ __attribute__((aligned(16))) uint32_t hsh[];
   const uint32_t F = 1u << bits;
   const uint64_t mask = F - 1;
@@ -693,7 +696,7 @@ __global__ __launch_bounds__(NT) void localHistogramKernel(const void *__restric
   __syncthreads();
   const LocalItem it = items[blockIdx.x];
   uint32_t *wh = hsh + wid * F;
-  for (uint32_t base = 0; base < it.len; base += PART_TILE) {
+  for (uint32_t base = 0; base < it.len; base += PART_TILE * stride) {
     uint64_t w[PART_ITEMS];
 #pragma unroll
     for (int i = 0; i < (int)PART_ITEMS; ++i) {
@@ -712,14 +715,17 @@ __global__ __launch_bounds__(NT) void localHistogramKernel(const void *__restric
 }
 
 void localHistogram(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift,
-                    uint32_t bits, uint32_t *itemHist, hipStream_t s) {
+                    uint32_t bits, uint32_t *itemHist, hipStream_t s, uint32_t sampleStride) {
   HJ_CHECK(bits <= MAX_PART_BITS, "localHistogram: bits=%u out of range", bits);
+  HJ_CHECK(sampleStride >= 1, "localHistogram: sampleStride must be >= 1");
   if (nItems == 0) return;
   const size_t lds = size_t(4) << bits << 2;
   if (wide)
-    hipLaunchKernelGGL(localHistogramKernel<true>, dim3(nItems), dim3(NT), lds, s, in, items, shift, bits, itemHist);
+    hipLaunchKernelGGL(localHistogramKernel<true>, dim3(nItems), dim3(NT), lds, s, in, items, shift, bits, itemHist,
+                       sampleStride);
   else
-    hipLaunchKernelGGL(localHistogramKernel<false>, dim3(nItems), dim3(NT), lds, s, in, items, shift, bits, itemHist);
+    hipLaunchKernelGGL(localHistogramKernel<false>, dim3(nItems), dim3(NT), lds, s, in, items, shift, bits, itemHist,
+                       sampleStride);
   HIP_CHECK_LAUNCH();
 }
 
@@ -794,24 +800,118 @@ void localCursors(const uint32_t *itemHist, const uint32_t *lpItemBegin, uint32_
   HIP_CHECK_LAUNCH();
 }
 
-template <class Pol, typename CurT, int NTH, int IPT>
+// Sampled local pass: tuples of item it the histogram read (tiles 0, S, 2S...).
+__device__ __forceinline__ uint32_t sampledLen(uint32_t len, uint32_t stride) {
+  uint32_t seen = 0;
+  for (uint32_t b = 0; b < len; b += PART_TILE * stride) seen += min((uint32_t)PART_TILE, len - b);
+  return seen;
+}
+
+// One workgroup per owned partition lp: capacity of each final partition
+// (lp, q) = sampled estimate + 6 sigma of the sampling error + 2% + 64.
+__global__ __launch_bounds__(NT) void localCapacityKernel(const uint32_t *__restrict__ itemHist,
+                                                          const uint32_t *__restrict__ lpItemBegin,
+                                                          const LocalItem *__restrict__ items, uint32_t bits,
+                                                          uint32_t stride, uint32_t *__restrict__ caps) {
+  const uint32_t F = 1u << bits, lp = blockIdx.x;
+  const uint32_t ib = lpItemBegin[lp], ie = lpItemBegin[lp + 1];
+  double len = 0, seen = 0;
+  for (uint32_t it = ib; it < ie; ++it) {
+    len += items[it].len;
+    seen += sampledLen(items[it].len, stride);
+  }
+  const double scale = seen > 0 ? len / seen : 1.0;
+  for (uint32_t q = threadIdx.x; q < F; q += NT) {
+    double est = 0;
+    for (uint32_t it = ib; it < ie; ++it) {
+      const uint32_t s = sampledLen(items[it].len, stride);
+      if (s) est += (double)itemHist[(uint64_t)it * F + q] * ((double)items[it].len / s);
+    }
+    const double cap = est + 6.0 * sqrt(fmax(est, 1.0) * scale) + 0.02 * est + 64.0;
+    caps[(uint64_t)lp * F + q] = (uint32_t)min(ceil(cap), 4294967295.0);
+  }
+}
+
+// gcur = gstart = partBegin = exclusive prefix of caps; gend = start + cap.
+__global__ __launch_bounds__(NT) void localSampledCursorsKernel(const uint32_t *__restrict__ caps,
+                                                                const unsigned long long *__restrict__ starts,
+                                                                uint64_t P, unsigned long long *__restrict__ gcur,
+                                                                unsigned long long *__restrict__ gend,
+                                                                uint64_t *__restrict__ partBegin) {
+  const uint64_t stride = (uint64_t)gridDim.x * NT;
+  for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < P; i += stride) {
+    const unsigned long long s = starts[i];
+    gcur[i] = s;
+    gend[i] = s + caps[i];
+    partBegin[i] = s;
+  }
+}
+
+// flag |= some final claim cursor passed its slice end (the run is redone exactly).
+__global__ __launch_bounds__(NT) void claimOverflowKernel(const unsigned long long *__restrict__ gcur,
+                                                          const unsigned long long *__restrict__ gend, uint64_t P,
+                                                          unsigned int *flag) {
+  const uint64_t stride = (uint64_t)gridDim.x * NT;
+  bool over = false;
+  for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < P; i += stride) over |= gcur[i] > gend[i];
+  if (__any(over) && (threadIdx.x & (WAVE - 1)) == 0) atomicOr(flag, 1u);
+}
+
+void localSampledLayout(const uint32_t *itemHist, const uint32_t *lpItemBegin, const LocalItem *items,
+                        uint32_t owned, uint32_t bits, uint32_t sampleStride, uint32_t *caps,
+                        unsigned long long *starts, void *scanWorkspace, unsigned long long *gcur,
+                        unsigned long long *gend, uint64_t *partBegin, hipStream_t s) {
+  if (owned == 0) return;
+  const uint64_t P = (uint64_t)owned << bits;
+  hipLaunchKernelGGL(localCapacityKernel, dim3(owned), dim3(NT), 0, s, itemHist, lpItemBegin, items, bits,
+                     sampleStride, caps);
+  HIP_CHECK_LAUNCH();
+  scanExclusiveU32to64(caps, starts, P, nullptr, scanWorkspace, s);
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(ceilDiv(P, NT), 4096);
+  hipLaunchKernelGGL(localSampledCursorsKernel, dim3(grid), dim3(NT), 0, s, caps, starts, P, gcur, gend, partBegin);
+  HIP_CHECK_LAUNCH();
+}
+
+uint64_t localSampledCapacityBound(uint64_t n, uint64_t partitions, uint32_t sampleStride) {
+  // Sum of the per-partition capacities: estimates sum to n; by Cauchy-Schwarz
+  // the 6-sigma terms sum to at most 6 sqrt(n * S * P); +66 per partition for
+  // the constant, the ceil and float rounding.
+  const double bound = 1.02 * (double)n +
+                       6.0 * std::sqrt(((double)n + (double)partitions) * sampleStride * (double)partitions) +
+                       66.0 * (double)partitions;
+  return (uint64_t)(bound * 1.001) + 1024;
+}
+
+void claimOverflow(const unsigned long long *gcur, const unsigned long long *gend, uint64_t P, unsigned int *flag,
+                   hipStream_t s) {
+  if (P == 0) return;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(ceilDiv(P, NT), 4096);
+  hipLaunchKernelGGL(claimOverflowKernel, dim3(grid), dim3(NT), 0, s, gcur, gend, P, flag);
+  HIP_CHECK_LAUNCH();
+}
+
+template <class Pol, typename CurT, int NTH, int IPT, bool BOUNDED = false>
 __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void localScatterClaimKernel(
     const typename Pol::InT *__restrict__ in, const LocalItem *__restrict__ items, uint32_t nItems, uint32_t F,
-    Pol pol, CurT *__restrict__ gcur, typename Pol::OutT *out) {
+    Pol pol, CurT *__restrict__ gcur, typename Pol::OutT *out, const CurT *__restrict__ gend) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t q = (nItems + NGROUPS - 1) / NGROUPS;
   const uint32_t item = (blockIdx.x % NGROUPS) * q + blockIdx.x / NGROUPS;  // XCD-contiguous items
   if (item >= nItems) return;  // uniform per workgroup
+  CurT *sliceEnd = reinterpret_cast<CurT *>(smem);
   uint32_t *cnt = reinterpret_cast<uint32_t *>(reinterpret_cast<CurT *>(smem) + 2 * F);
-  for (uint32_t d = threadIdx.x; d < F; d += NTH) cnt[d] = 0;
-  __syncthreads();
   const LocalItem it = items[item];
-  scatterRange<Pol, CurT, NTH, IPT, 0, true>(in, it.begin, it.begin + it.len, F, smem, pol, out,
-                                             gcur + (uint64_t)it.stream * F);
+  for (uint32_t d = threadIdx.x; d < F; d += NTH) {
+    cnt[d] = 0;
+    if constexpr (BOUNDED) sliceEnd[d] = gend[(uint64_t)it.stream * F + d];
+  }
+  __syncthreads();
+  scatterRange<Pol, CurT, NTH, IPT, 0, true, BOUNDED>(in, it.begin, it.begin + it.len, F, smem, pol, out,
+                                                      gcur + (uint64_t)it.stream * F);
 }
 
 void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift, uint32_t bits,
-                  void *gcur, bool narrow, void *out, hipStream_t s) {
+                  void *gcur, bool narrow, void *out, hipStream_t s, const void *gend) {
   HJ_CHECK(bits <= MAX_PART_BITS, "localScatter: bits=%u out of range", bits);
   if (nItems == 0) return;
   const uint32_t F = 1u << bits;
@@ -823,9 +923,15 @@ void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nI
     pol.mask = mask;                                                                                          \
     pol.shift = shift;                                                                                        \
     const size_t lds = ScatterLayout<P, C, CL_NTH * CL_IPT>::bytes(F);                                         \
-    hipLaunchKernelGGL((localScatterClaimKernel<P, C, CL_NTH, CL_IPT>), dim3(grid), dim3(CL_NTH), lds, s,      \
-                       reinterpret_cast<const typename P::InT *>(in), items, nItems, F, pol,                   \
-                       reinterpret_cast<C *>(gcur), reinterpret_cast<typename P::OutT *>(out));                \
+    if (gend)                                                                                                 \
+      hipLaunchKernelGGL((localScatterClaimKernel<P, C, CL_NTH, CL_IPT, true>), dim3(grid), dim3(CL_NTH), lds, \
+                         s, reinterpret_cast<const typename P::InT *>(in), items, nItems, F, pol,              \
+                         reinterpret_cast<C *>(gcur), reinterpret_cast<typename P::OutT *>(out),               \
+                         reinterpret_cast<const C *>(gend));                                                   \
+    else                                                                                                      \
+      hipLaunchKernelGGL((localScatterClaimKernel<P, C, CL_NTH, CL_IPT>), dim3(grid), dim3(CL_NTH), lds, s,    \
+                         reinterpret_cast<const typename P::InT *>(in), items, nItems, F, pol,                 \
+                         reinterpret_cast<C *>(gcur), reinterpret_cast<typename P::OutT *>(out), nullptr);     \
   } while (0)
   if (wide && narrow) HJ_LOCAL(LocalWidePol, uint32_t);
   else if (wide) HJ_LOCAL(LocalWidePol, unsigned long long);

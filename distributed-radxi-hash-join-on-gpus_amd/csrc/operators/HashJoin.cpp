@@ -91,12 +91,13 @@ void HashJoin::makeJoinPlan() {
   plan = core::makePlan(config, numberOfNodes, innerRelation->getGlobalSize(), outerRelation->getGlobalSize(), mx[0],
                         mx[1]);
   if (config.keyHashing == core::KeyHashing::Auto && plan.keyBits < 64) plan.keyMix = lowKeyBitsSkewed();
+  if (!ctx->onDevice()) plan.localHistogram = core::HistogramMode::Exact;  // sampling pays on HBM only
   {
     const bool eligible = numberOfNodes == 1 && ctx->onDevice() && plan.chunks == 1;
     const uint64_t small = std::min(innerRelation->getGlobalSize(), outerRelation->getGlobalSize());
-    if (config.networkHistogram == core::NetworkHistogram::Sampled)
+    if (config.networkHistogram == core::HistogramMode::Sampled)
       plan.sampledNetwork = eligible;
-    else if (config.networkHistogram == core::NetworkHistogram::Auto)
+    else if (config.networkHistogram == core::HistogramMode::Auto)
       plan.sampledNetwork = eligible && small >= (16ull << 20);
   }
   JOIN_DEBUG("HashJoin", "%s", plan.describe().c_str());
@@ -146,10 +147,7 @@ JoinResult HashJoin::run() {
   try {
     return runImpl();
   } catch (const std::exception &e) {
-    while (!TASK_QUEUE.empty()) {
-      delete TASK_QUEUE.front();
-      TASK_QUEUE.pop();
-    }
+    while (!TASK_QUEUE.empty()) TASK_QUEUE.pop();  // tasks are owned (and freed) by runImpl
     ctx->comm()->abort(e.what());
     throw;
   }
@@ -266,16 +264,17 @@ JoinResult HashJoin::runImpl() {
   trace.reset();  // roctx ranges nest: pop before the next push
   utils::faultPoint("local");
   trace.reset(new performance::TraceRange("local_processing"));
-  auto *lp = new tasks::LocalPartitioning(innerWindow, outerWindow, ctx, plan);
-  TASK_QUEUE.push(lp);
+  std::unique_ptr<tasks::LocalPartitioning> lp(
+      new tasks::LocalPartitioning(innerWindow, outerWindow, ctx, plan, localOverflowed));
+  TASK_QUEUE.push(lp.get());
   Measurements::stopLocalProcessingPreparations();
   Measurements::startLocalProcessing();
   std::unique_ptr<tasks::BuildProbe> bp;
+  // Both tasks are owned here (lp is re-created if its sampled layout overflows).
   while (!TASK_QUEUE.empty()) {
-    std::unique_ptr<tasks::Task> t(TASK_QUEUE.front());
+    tasks::Task *t = TASK_QUEUE.front();
     TASK_QUEUE.pop();
     if (t->getType() == TASK_BUILD_PROBE) {
-      t.release();  // owned by bp
       utils::faultPoint("build_probe");
       bp->execute();
       continue;
@@ -291,6 +290,23 @@ JoinResult HashJoin::runImpl() {
   trace.reset();  // roctx ranges nest: pop before the next push
   if (dev) HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
   ctx->synchronize();
+  result.sampledLocal = lp->sampled();
+  if (lp->sampled() && lp->overflowed()) {
+    // A sampled slot overflowed (skew the sample missed): the build/probe ran
+    // on incomplete partitions.  Redo the local pass exactly, then the
+    // build/probe; later joins stay exact.
+    localOverflowed = true;
+    ++result.localFallbacks;
+    result.sampledLocal = false;
+    bp.reset();
+    lp.reset(new tasks::LocalPartitioning(innerWindow, outerWindow, ctx, plan, true));
+    lp->execute();
+    result.localItems = lp->workItems();
+    bp.reset(new tasks::BuildProbe(innerWindow, outerWindow, ctx, plan, config.outputCapacity));
+    bp->execute();
+    if (dev) HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
+    ctx->synchronize();
+  }
   while (bp->collect()) {  // rare: item list or output buffer overflowed -> exact re-run
     ++result.reruns;
     bp->execute();

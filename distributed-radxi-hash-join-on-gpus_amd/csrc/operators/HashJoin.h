@@ -39,6 +39,8 @@ struct JoinResult {
   uint64_t innerLocal = 0, outerLocal = 0;
   bool sampledNetwork = false;     // network pass sized from a sampled histogram (N == 1)
   uint32_t networkFallbacks = 0;   // sampled pass overflowed -> exact re-run inside this join
+  bool sampledLocal = false;       // local pass sized from a sampled histogram
+  uint32_t localFallbacks = 0;     // sampled local pass overflowed -> exact re-run
 };
 
 class HashJoin {
@@ -82,6 +84,7 @@ class HashJoin {
   core::JoinPlan plan;
   JoinResult result;
   bool sampledOverflowed = false;  // sticky: exact histograms after a sampled pass overflowed
+  bool localOverflowed = false;    // sticky: exact local pass after a sampled one overflowed
   const ulonglong2 *output = nullptr;
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
 };

@@ -43,6 +43,8 @@ void BuildProbe::configure() {
   args.S = wo->getPartitionedData();
   args.partR = wi->getPartitionBegin();
   args.partS = wo->getPartitionBegin();
+  args.partREnd = wi->getPartitionEnd();
+  args.partSEnd = wo->getPartitionEnd();
   args.P = owned << wi->getLocalBits();
   args.rChunk = plan.rChunk;
   args.sChunk = plan.sChunk;

@@ -8,8 +8,8 @@ namespace hpcjoin {
 namespace tasks {
 
 LocalPartitioning::LocalPartitioning(data::Window *innerWindow, data::Window *outerWindow, core::ExecContext *ctx,
-                                     const core::JoinPlan &plan)
-    : ctx(ctx), plan(plan) {
+                                     const core::JoinPlan &plan, bool forceExact)
+    : ctx(ctx), plan(plan), forceExact(forceExact) {
   windows[0] = innerWindow;
   windows[1] = outerWindow;
 }
@@ -19,6 +19,13 @@ LocalPartitioning::~LocalPartitioning() {}
 void LocalPartitioning::execute() {
   partition(windows[0], 0);
   partition(windows[1], 1);
+}
+
+bool LocalPartitioning::overflowed() const {
+  if (!overflowFlag) return false;
+  unsigned int f = 0;
+  HIP_CHECK(hipMemcpy(&f, overflowFlag, sizeof(f), hipMemcpyDeviceToHost));
+  return f != 0;
 }
 
 void LocalPartitioning::partition(data::Window *w, int which) {
@@ -53,10 +60,46 @@ void LocalPartitioning::partition(data::Window *w, int which) {
   const uint32_t nItems = (uint32_t)it.size();
   const uint32_t shift = wide ? plan.networkBits : plan.keyShift;
 
-  void *out = ctx->workspace().get(std::max<uint64_t>(xp.recvTotal, 1) * tb);
   uint32_t *itemHist = ctx->workspace().getArray<uint32_t>(std::max<uint64_t>(1, (uint64_t)nItems * F));
-  uint64_t *partBegin = ctx->workspace().getArray<uint64_t>((uint64_t)owned * F + 1);
 
+  const bool sampledMode =
+      ctx->onDevice() && !forceExact && plan.twoLevel && bits > 0 &&
+      (plan.localHistogram == core::HistogramMode::Sampled ||
+       (plan.localHistogram == core::HistogramMode::Auto && xp.recvTotal >= (16ull << 20)));
+  if (sampledMode) {
+    sampledSide[which] = true;
+    // One claim stream per network partition (its items are XCD-contiguous
+    // except at group boundaries), so every final partition is one slot.
+    for (auto &x : it) x.stream = x.lp;
+    const uint64_t P = (uint64_t)owned * F;
+    const uint32_t S = plan.sampleStride;
+    const uint64_t cap = kernels::localSampledCapacityBound(xp.recvTotal, P, S);
+    void *sout = ctx->workspace().get(std::max<uint64_t>(cap, 1) * tb);
+    uint32_t *caps = ctx->workspace().getArray<uint32_t>(std::max<uint64_t>(P, 1));
+    auto *starts = ctx->workspace().getArray<unsigned long long>(std::max<uint64_t>(P, 1));
+    void *scanWs = ctx->workspace().get(kernels::scanWorkspaceBytes(std::max<uint64_t>(P, 1)));
+    auto *gcur = ctx->workspace().getArray<unsigned long long>(std::max<uint64_t>(P, 1));
+    auto *gend = ctx->workspace().getArray<unsigned long long>(std::max<uint64_t>(P, 1));
+    uint64_t *pbeg = ctx->workspace().getArray<uint64_t>(std::max<uint64_t>(P, 1));
+    kernels::LocalItem *dItems = ctx->workspace().getArray<kernels::LocalItem>(std::max<uint32_t>(nItems, 1));
+    uint32_t *dLb = ctx->workspace().getArray<uint32_t>(owned + 1);
+    ctx->copy(dItems, it.data(), (uint64_t)nItems * sizeof(kernels::LocalItem), true, false);
+    ctx->copy(dLb, lb.data(), (owned + 1) * 4ull, true, false);
+    if (!overflowFlag) {
+      overflowFlag = ctx->workspace().getArray<unsigned int>(1);
+      HIP_CHECK(hipMemsetAsync(overflowFlag, 0, sizeof(unsigned int), ctx->stream()));
+    }
+    kernels::localHistogram(w->getData(), wide, dItems, nItems, shift, bits, itemHist, ctx->stream(), S);
+    kernels::localSampledLayout(itemHist, dLb, dItems, owned, bits, S, caps, starts, scanWs, gcur, gend, pbeg,
+                                ctx->stream());
+    kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, gcur, false, sout, ctx->stream(), gend);
+    kernels::claimOverflow(gcur, gend, P, overflowFlag, ctx->stream());
+    // Final claim cursors are the partition ends (valid when no slot overflowed).
+    w->setPartitioned(sout, pbeg, bits, reinterpret_cast<const uint64_t *>(gcur));
+    return;
+  }
+  void *out = ctx->workspace().get(std::max<uint64_t>(xp.recvTotal, 1) * tb);
+  uint64_t *partBegin = ctx->workspace().getArray<uint64_t>((uint64_t)owned * F + 1);
   if (ctx->onDevice()) {
     const uint32_t streams = kernels::assignLocalStreams(it.data(), nItems);
     const bool narrow = kernels::cursorsNarrow(xp.recvTotal);

@@ -7,6 +7,15 @@
 // write-combining scatter.  Work items never cross a (chunk, source,
 // partition) segment of the window, so the source-major RCCL layout needs
 // no compaction pass.
+//
+// Sampled mode (device, JoinPlan::localHistogram): the per-item histograms
+// read 1 tile in sampleStride, each final partition gets a slot sized from
+// the estimate plus 6 sigma of the sampling error, and the bounded scatter
+// fills them (one claim stream per network partition).  Partitions then have
+// tail gaps, so the window gets explicit partition ends (the final claim
+// cursors) for the build/probe.  An overflowing slot raises a device flag
+// that HashJoin reads after the build/probe; it then redoes the local pass
+// exactly (forceExact) and the build/probe.
 #pragma once
 
 #include <vector>
@@ -23,7 +32,7 @@ namespace tasks {
 class LocalPartitioning : public Task {
  public:
   LocalPartitioning(data::Window *innerWindow, data::Window *outerWindow, core::ExecContext *ctx,
-                    const core::JoinPlan &plan);
+                    const core::JoinPlan &plan, bool forceExact = false);
   ~LocalPartitioning();
 
   void execute();
@@ -31,6 +40,9 @@ class LocalPartitioning : public Task {
 
   uint64_t partitionedElements() const { return elements; }
   uint64_t workItems() const { return items[0].size() + items[1].size(); }
+  bool sampled() const { return sampledSide[0] || sampledSide[1]; }
+  // After the stream is synchronised: did a sampled slot overflow?
+  bool overflowed() const;
 
  protected:
   void partition(data::Window *window, int which);
@@ -43,6 +55,9 @@ class LocalPartitioning : public Task {
   std::vector<uint32_t> lpItemBegin[2];
   std::vector<uint64_t> zero;
   uint64_t elements = 0;
+  bool forceExact;
+  bool sampledSide[2] = {false, false};
+  unsigned int *overflowFlag = nullptr;  // device
 };
 
 }  // namespace tasks

@@ -16,6 +16,7 @@ def config_to_dict(cfg) -> dict:
     d["format"] = str(cfg.format).split(".")[-1]
     d["key_hashing"] = str(cfg.key_hashing).split(".")[-1]
     d["network_histogram"] = str(cfg.network_histogram).split(".")[-1]
+    d["local_histogram"] = str(cfg.local_histogram).split(".")[-1]
     return d
 
 
@@ -24,7 +25,7 @@ def config_from_dict(d: dict | None = None, env_prefix: str = "HPCJOIN_"):
     C = require_native()
     cfg = C.JoinConfig()
     merged = dict(d or {})
-    for f in _FIELDS + ["assignment", "format", "key_hashing", "network_histogram"]:
+    for f in _FIELDS + ["assignment", "format", "key_hashing", "network_histogram", "local_histogram"]:
         v = os.environ.get(env_prefix + f.upper())
         if v is not None:
             merged[f] = v
@@ -35,8 +36,8 @@ def config_from_dict(d: dict | None = None, env_prefix: str = "HPCJOIN_"):
             cfg.format = getattr(C.TupleFormat, str(v).upper())
         elif k == "key_hashing":
             cfg.key_hashing = getattr(C.KeyHashing, str(v).upper())
-        elif k == "network_histogram":
-            cfg.network_histogram = getattr(C.NetworkHistogram, str(v).upper())
+        elif k in ("network_histogram", "local_histogram"):
+            setattr(cfg, k, getattr(C.HistogramMode, str(v).upper()))
         elif k in ("two_level", "materialize", "checks"):
             setattr(cfg, k, v if isinstance(v, bool) else str(v).lower() in ("1", "true", "yes"))
         elif k in _FIELDS:

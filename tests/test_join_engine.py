@@ -167,12 +167,14 @@ def test_sampled_network_pass(C, cuda, dist, fmt, mat):
     out = {}
     for mode in ("SAMPLED", "EXACT"):
         cfg = C.JoinConfig()
-        cfg.network_histogram = getattr(C.NetworkHistogram, mode)
+        cfg.network_histogram = getattr(C.HistogramMode, mode)
+        cfg.local_histogram = getattr(C.HistogramMode, mode)
         cfg.format = getattr(C.TupleFormat, fmt)
         cfg.materialize = mat
         res, exp, j = run_join(C, "cuda", G_R, G_S, dist, cfg=cfg)
         assert j.plan.sampled_network == (mode == "SAMPLED")
         assert res["sampled_network"] == (mode == "SAMPLED") and res["network_fallbacks"] == 0
+        assert res["sampled_local"] == (mode == "SAMPLED") and res["local_fallbacks"] == 0
         assert res["global_matches"] == exp
         for _ in range(2):
             assert j.run()["global_matches"] == exp
@@ -186,7 +188,7 @@ def test_sampled_network_pass(C, cuda, dist, fmt, mat):
 @pytest.mark.gpu
 def test_sampled_network_single_level(C, cuda):
     cfg = C.JoinConfig()
-    cfg.network_histogram = C.NetworkHistogram.SAMPLED
+    cfg.network_histogram = C.HistogramMode.SAMPLED
     cfg.two_level = False
     res, exp, j = run_join(C, "cuda", 1 << 21, 1 << 21, cfg=cfg)
     assert j.plan.sampled_network and res["sampled_network"] and res["global_matches"] == exp
@@ -206,7 +208,7 @@ def test_sampled_network_overflow_falls_back(C, cuda):
     S = torch.stack([keys.flip(0), i], 1).contiguous()
     ctx = C.ExecContext("device", 0, C.LocalCommunicator())
     cfg = C.JoinConfig()
-    cfg.network_histogram = C.NetworkHistogram.SAMPLED
+    cfg.network_histogram = C.HistogramMode.SAMPLED
     cfg.key_hashing = C.KeyHashing.OFF
     cfg.network_bits = 9
     cfg.max_partition_blocks = 16  # 64 tiles per workgroup, 4 of them sampled
@@ -220,6 +222,33 @@ def test_sampled_network_overflow_falls_back(C, cuda):
 
 def test_sampled_network_host_is_exact(C):
     cfg = C.JoinConfig()
-    cfg.network_histogram = C.NetworkHistogram.SAMPLED
+    cfg.network_histogram = C.HistogramMode.SAMPLED
     res, exp, j = run_join(C, "cpu", 100_000, 100_000, cfg=cfg)
     assert not j.plan.sampled_network and not res["sampled_network"] and res["global_matches"] == exp
+
+
+@pytest.mark.gpu
+def test_sampled_local_overflow_falls_back(C, cuda):
+    """Inside every network partition the local digits rise with input order,
+    so the sampled first tile of each local work item sees only low digits:
+    slots overflow, the local pass and build/probe are redone exactly, and
+    later joins use the exact local pass."""
+    import torch
+    n = 1 << 26
+    i = torch.arange(n, device="cuda")
+    net, j = i % 512, i // 512
+    keys = ((j % 256) << 18) | ((j // 256) << 9) | net  # unique; local digit = j // 256 rises with i
+    R = torch.stack([keys, i], 1).contiguous()
+    S = torch.stack([keys.flip(0), i], 1).contiguous()
+    ctx = C.ExecContext("device", 0, C.LocalCommunicator())
+    cfg = C.JoinConfig()
+    cfg.network_histogram = C.HistogramMode.EXACT
+    cfg.local_histogram = C.HistogramMode.SAMPLED
+    cfg.key_hashing = C.KeyHashing.OFF
+    cfg.network_bits, cfg.local_bits = 9, 9
+    j = C.HashJoin(C.Relation.from_tensor(R, n), C.Relation.from_tensor(S, n), ctx, cfg)
+    res = j.run()
+    assert res["local_fallbacks"] == 1 and not res["sampled_local"]
+    assert res["global_matches"] == n
+    res = j.run()
+    assert res["local_fallbacks"] == 0 and not res["sampled_local"] and res["global_matches"] == n
