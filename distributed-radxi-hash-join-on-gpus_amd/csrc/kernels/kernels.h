@@ -168,11 +168,12 @@ void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nI
 void localSampledLayout(const uint32_t *itemHist, const uint32_t *lpItemBegin, const LocalItem *items,
                         uint32_t owned, uint32_t bits, uint32_t sampleStride, uint32_t *caps,
                         unsigned long long *starts, void *scanWorkspace, unsigned long long *gcur,
-                        unsigned long long *gend, uint64_t *partBegin, hipStream_t s);
+                        unsigned long long *gend, uint64_t *partBegin, uint64_t capacity, hipStream_t s);
 // Upper bound of the layout's total capacity (host-side sizing of the output).
 uint64_t localSampledCapacityBound(uint64_t n, uint64_t partitions, uint32_t sampleStride);
-// *flag |= 1 if any gcur[i] > gend[i] (a bounded claim slice overflowed).
-void claimOverflow(const unsigned long long *gcur, const unsigned long long *gend, uint64_t P, unsigned int *flag,
+// *flag |= 1 if any gcur[i] > gend[i] (a bounded claim slice overflowed);
+// gcur is clamped to gend, so it is always safe to use as partition ends.
+void claimOverflow(unsigned long long *gcur, const unsigned long long *gend, uint64_t P, unsigned int *flag,
                    hipStream_t s);
 
 // --------------------------------------------------------------- build/probe

@@ -832,35 +832,47 @@ __global__ __launch_bounds__(NT) void localCapacityKernel(const uint32_t *__rest
   }
 }
 
-// gcur = gstart = partBegin = exclusive prefix of caps; gend = start + cap.
+// gcur = partBegin = exclusive prefix of caps; gend = start + cap.  Both are
+// clamped to the allocated capacity, so no write or later read can leave the
+// buffer even if the host-side bound were ever too small (the slot would
+// just overflow and trigger the exact re-run).
 __global__ __launch_bounds__(NT) void localSampledCursorsKernel(const uint32_t *__restrict__ caps,
                                                                 const unsigned long long *__restrict__ starts,
-                                                                uint64_t P, unsigned long long *__restrict__ gcur,
+                                                                uint64_t P, unsigned long long capacity,
+                                                                unsigned long long *__restrict__ gcur,
                                                                 unsigned long long *__restrict__ gend,
                                                                 uint64_t *__restrict__ partBegin) {
   const uint64_t stride = (uint64_t)gridDim.x * NT;
   for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < P; i += stride) {
-    const unsigned long long s = starts[i];
+    const unsigned long long s = min(starts[i], capacity);
     gcur[i] = s;
-    gend[i] = s + caps[i];
+    gend[i] = min(s + (unsigned long long)caps[i], capacity);
     partBegin[i] = s;
   }
 }
 
-// flag |= some final claim cursor passed its slice end (the run is redone exactly).
-__global__ __launch_bounds__(NT) void claimOverflowKernel(const unsigned long long *__restrict__ gcur,
+// flag |= some final claim cursor passed its slice end (the run is redone
+// exactly); gcur is clamped to the slice end so that, used as partition ends,
+// it never points past what was written.
+__global__ __launch_bounds__(NT) void claimOverflowKernel(unsigned long long *__restrict__ gcur,
                                                           const unsigned long long *__restrict__ gend, uint64_t P,
                                                           unsigned int *flag) {
   const uint64_t stride = (uint64_t)gridDim.x * NT;
   bool over = false;
-  for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < P; i += stride) over |= gcur[i] > gend[i];
+  for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < P; i += stride) {
+    const unsigned long long g = gcur[i], e = gend[i];
+    if (g > e) {
+      over = true;
+      gcur[i] = e;
+    }
+  }
   if (__any(over) && (threadIdx.x & (WAVE - 1)) == 0) atomicOr(flag, 1u);
 }
 
 void localSampledLayout(const uint32_t *itemHist, const uint32_t *lpItemBegin, const LocalItem *items,
                         uint32_t owned, uint32_t bits, uint32_t sampleStride, uint32_t *caps,
                         unsigned long long *starts, void *scanWorkspace, unsigned long long *gcur,
-                        unsigned long long *gend, uint64_t *partBegin, hipStream_t s) {
+                        unsigned long long *gend, uint64_t *partBegin, uint64_t capacity, hipStream_t s) {
   if (owned == 0) return;
   const uint64_t P = (uint64_t)owned << bits;
   hipLaunchKernelGGL(localCapacityKernel, dim3(owned), dim3(NT), 0, s, itemHist, lpItemBegin, items, bits,
@@ -868,7 +880,8 @@ void localSampledLayout(const uint32_t *itemHist, const uint32_t *lpItemBegin, c
   HIP_CHECK_LAUNCH();
   scanExclusiveU32to64(caps, starts, P, nullptr, scanWorkspace, s);
   const uint32_t grid = (uint32_t)std::min<uint64_t>(ceilDiv(P, NT), 4096);
-  hipLaunchKernelGGL(localSampledCursorsKernel, dim3(grid), dim3(NT), 0, s, caps, starts, P, gcur, gend, partBegin);
+  hipLaunchKernelGGL(localSampledCursorsKernel, dim3(grid), dim3(NT), 0, s, caps, starts, P,
+                     (unsigned long long)capacity, gcur, gend, partBegin);
   HIP_CHECK_LAUNCH();
 }
 
@@ -876,13 +889,14 @@ uint64_t localSampledCapacityBound(uint64_t n, uint64_t partitions, uint32_t sam
   // Sum of the per-partition capacities: estimates sum to n; by Cauchy-Schwarz
   // the 6-sigma terms sum to at most 6 sqrt(n * S * P); +66 per partition for
   // the constant, the ceil and float rounding.
+  // (an item's len/seen ratio is at most ~sampleStride; +1 covers the rounding)
   const double bound = 1.02 * (double)n +
-                       6.0 * std::sqrt(((double)n + (double)partitions) * sampleStride * (double)partitions) +
+                       6.0 * std::sqrt(((double)n + (double)partitions) * (sampleStride + 1.0) * (double)partitions) +
                        66.0 * (double)partitions;
   return (uint64_t)(bound * 1.001) + 1024;
 }
 
-void claimOverflow(const unsigned long long *gcur, const unsigned long long *gend, uint64_t P, unsigned int *flag,
+void claimOverflow(unsigned long long *gcur, const unsigned long long *gend, uint64_t P, unsigned int *flag,
                    hipStream_t s) {
   if (P == 0) return;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(ceilDiv(P, NT), 4096);

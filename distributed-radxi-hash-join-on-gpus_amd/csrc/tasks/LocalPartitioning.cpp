@@ -90,7 +90,7 @@ void LocalPartitioning::partition(data::Window *w, int which) {
       HIP_CHECK(hipMemsetAsync(overflowFlag, 0, sizeof(unsigned int), ctx->stream()));
     }
     kernels::localHistogram(w->getData(), wide, dItems, nItems, shift, bits, itemHist, ctx->stream(), S);
-    kernels::localSampledLayout(itemHist, dLb, dItems, owned, bits, S, caps, starts, scanWs, gcur, gend, pbeg,
+    kernels::localSampledLayout(itemHist, dLb, dItems, owned, bits, S, caps, starts, scanWs, gcur, gend, pbeg, cap,
                                 ctx->stream());
     kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, gcur, false, sout, ctx->stream(), gend);
     kernels::claimOverflow(gcur, gend, P, overflowFlag, ctx->stream());
