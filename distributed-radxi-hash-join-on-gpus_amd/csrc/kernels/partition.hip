@@ -828,7 +828,11 @@ __global__ __launch_bounds__(NT) void localCapacityKernel(const uint32_t *__rest
       if (s) est += (double)itemHist[(uint64_t)it * F + q] * ((double)items[it].len / s);
     }
     const double cap = est + 6.0 * sqrt(fmax(est, 1.0) * scale) + 0.02 * est + 64.0;
-    caps[(uint64_t)lp * F + q] = (uint32_t)min(ceil(cap), 4294967295.0);
+    // Whole 128-byte lines per slot: partitions never share a cache line, so
+    // the scatter's partial lines at slot edges are not split across XCDs and
+    // every build/probe read starts line-aligned.
+    const uint32_t c = (uint32_t)min(ceil(cap), 4294967040.0);
+    caps[(uint64_t)lp * F + q] = (c + 15u) & ~15u;
   }
 }
 
@@ -887,12 +891,12 @@ void localSampledLayout(const uint32_t *itemHist, const uint32_t *lpItemBegin, c
 
 uint64_t localSampledCapacityBound(uint64_t n, uint64_t partitions, uint32_t sampleStride) {
   // Sum of the per-partition capacities: estimates sum to n; by Cauchy-Schwarz
-  // the 6-sigma terms sum to at most 6 sqrt(n * S * P); +66 per partition for
+  // the 6-sigma terms sum to at most 6 sqrt(n * S * P); +81 per partition for
   // the constant, the ceil and float rounding.
   // (an item's len/seen ratio is at most ~sampleStride; +1 covers the rounding)
   const double bound = 1.02 * (double)n +
                        6.0 * std::sqrt(((double)n + (double)partitions) * (sampleStride + 1.0) * (double)partitions) +
-                       66.0 * (double)partitions;
+                       81.0 * (double)partitions;  // 64 + ceil + 15 of line rounding + float slack
   return (uint64_t)(bound * 1.001) + 1024;
 }
 

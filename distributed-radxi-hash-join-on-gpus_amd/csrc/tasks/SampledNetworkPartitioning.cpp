@@ -66,7 +66,8 @@ void SampledNetworkPartitioning::layout() {
         // 6 sigma + 2% + a fixed floor keeps overflows (and their exact re-run) rare.
         const double scale = seen[g] > 0 ? total[g] / seen[g] : 1.0;
         const double margin = 6.0 * std::sqrt(std::max(est, 1.0) * scale) + 0.02 * est + 256.0;
-        const uint64_t cap = std::min<uint64_t>((uint64_t)std::ceil(est + margin), (uint64_t)total[g]);
+        // whole 128-byte lines per slice (16 tuples): slices never share a line
+        const uint64_t cap = (std::min<uint64_t>((uint64_t)std::ceil(est + margin), (uint64_t)total[g]) + 15) & ~15ull;
         s.start[i] = cur;
         s.cap[i] = cap;
         cur += cap;
