@@ -616,6 +616,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("number_of_nodes", &core::ExecContext::numberOfNodes)
       .def("workspace_capacity", [](core::ExecContext &c) { return c.workspace().capacity(); })
       .def("workspace_peak", [](core::ExecContext &c) { return c.workspace().peak(); })
+      .def("reset_scratch", &core::ExecContext::resetScratch, py::call_guard<py::gil_scoped_release>(),
+           "Rewind the arenas; if the last join spilled into fallback allocations, re-reserve one block of "
+           "the observed peak now (so the next join does not pay for it)")
       .def("reserve_workspace", [](core::ExecContext &c, uint64_t b) { c.workspace().reserve(b); })
       .def("synchronize", &core::ExecContext::synchronize);
 

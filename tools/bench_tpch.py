@@ -40,6 +40,7 @@ def main():
     t = TpchJoin(wl, info=info)
     for _ in range(args.warmup):
         t.run()
+    t.ctx.reset_scratch()  # arena grown to the warmup peak before timing
     join_ms, mat_ms, tot_ms, ok = [], [], [], True
     out = None
     for _ in range(args.steps):
@@ -69,7 +70,10 @@ def main():
             "phases_ms": {k: round(res[k], 3) for k in ("histogram_ms", "network_ms", "local_ms", "dev_histogram_ms",
                                                          "dev_network_ms", "dev_local_partition_ms",
                                                          "dev_build_probe_ms", "setup_ms")},
-            "engine": {k: res[k] for k in ("reruns", "build_probe_items", "local_items", "output_overflow")},
+            "engine": {k: res[k] for k in ("reruns", "build_probe_items", "local_items", "output_overflow",
+                                           "sampled_network", "sampled_local", "network_fallbacks",
+                                           "local_fallbacks")},
+            "step_join_ms": [round(x, 3) for x in join_ms],
             "plan": repr(t.engine.plan)}), flush=True)
     del out, t
     if torch.cuda.is_available():
