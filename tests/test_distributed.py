@@ -78,6 +78,25 @@ def test_in_process_chunked_exchange(C, dev, chunks, policy):
     assert all(r[0]["global_matches"] == exp for r in results)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_ranks,chunks,fmt", [(2, 1, "COMPRESSED"), (4, 3, "COMPRESSED"), (3, 2, "WIDE")])
+def test_in_process_sampled_local_pass(C, cuda, n_ranks, chunks, fmt):
+    """The sampled local pass on multi-rank windows (segments per chunk and
+    source; the network pass stays exact for N > 1)."""
+
+    def cfg_fn(cfg):
+        cfg.local_histogram = C.HistogramMode.SAMPLED
+        cfg.network_histogram = C.HistogramMode.SAMPLED  # ignored for N > 1
+        cfg.chunks = chunks
+        cfg.format = getattr(C.TupleFormat, fmt)
+
+    results, exp = run_ranks(C, n_ranks, "device", 3_000_017, 4_000_037, cfg_fn, outer_dist="ZIPF", theta=0.8)
+    for res, plan in results:
+        assert res["global_matches"] == exp
+        assert res["sampled_local"] and not res["sampled_network"] and not plan.sampled_network
+        assert res["local_fallbacks"] == 0
+
+
 @pytest.mark.parametrize("dev", devices())
 def test_in_process_skew_lpt_balances(C, dev):
     loc = "device" if dev == "cuda" else "host"
