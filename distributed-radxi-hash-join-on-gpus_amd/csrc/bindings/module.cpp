@@ -827,6 +827,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   ops.def("net_scatter_global_atomic", &opNetScatterGlobalAtomic);
   ops.def("bench_copy_ms", &benchCopy, py::arg("src"), py::arg("dst"), py::arg("iters") = 10);
   ops.def("bench_read_ms", &benchRead, py::arg("src"), py::arg("iters") = 10);
+  // Single un-timed launches on the null stream (MALL probe, tools/mall_probe.py).
+  ops.def("copy_into", [](const at::Tensor &src, const at::Tensor &dst) {
+    setDevice(src);
+    HJ_CHECK(dst.numel() * dst.element_size() >= src.numel() * src.element_size(), "copy_into: dst too small");
+    kernels::copyKernel(ptr<const ulonglong2>(src), ptr<ulonglong2>(dst), src.numel() * src.element_size() / 16, nullptr);
+  });
+  ops.def("read_sink", [](const at::Tensor &src, const at::Tensor &sink) {
+    setDevice(src);
+    kernels::readKernel(ptr<const ulonglong2>(src), src.numel() * src.element_size() / 16,
+                        ptr<unsigned long long>(sink), nullptr);
+  });
   ops.def("bench_host_link", &benchHostLink, py::arg("bytes") = (uint64_t)1 << 30, py::arg("device") = 0,
           py::arg("iters") = 5);
   ops.def("bench_scatter_ms", &benchScatter, py::arg("tuples"), py::arg("bits"), py::arg("mode") = 0,

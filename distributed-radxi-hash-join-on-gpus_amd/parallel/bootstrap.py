@@ -25,6 +25,17 @@ def init_distributed(backend: str | None = None, device: bool | None = None) -> 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if os.environ.get("HPCJOIN_SHARE_GPU") == "1" and world > 1:
+        # Rehearsal of the multi-GPU path on a box with fewer GPUs than ranks:
+        # ranks share devices round-robin, and each rank claims its own RCCL
+        # host id so RCCL's duplicate-GPU check passes and it falls back to its
+        # socket transport.  Every engine code path (RCCL all-gather,
+        # all-to-allv, all-reduce, torch.distributed bootstrap) still runs.
+        # Must happen before anything initialises RCCL.
+        os.environ["NCCL_HOSTID"] = f"hpcjoin-rehearsal-{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
+        local_rank = local_rank % max(1, torch.cuda.device_count())
     if device is None:
         device = torch.cuda.is_available()
     if device:

@@ -177,3 +177,29 @@ def test_tpch_late_materialization(C, dev, n_ranks):
     # each order appears exactly 4 times
     counts = torch.bincount(allrows[:, 0], minlength=wl.inner_size)
     assert int(counts.min()) == 4 and int(counts.max()) == 4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_rccl_multiprocess_shared_gpu(world):
+    """One process per rank over the real RCCL library, as torchrun launches
+    bench.py on an 8-GPU node.  The GPU box has one MI355X, so the ranks share
+    it (HPCJOIN_SHARE_GPU=1: each rank claims its own RCCL host id and RCCL
+    runs its socket transport instead of xGMI); every engine call -- bootstrap,
+    histogram all-gather, chunked all-to-allv, result all-reduce -- is the one
+    the multi-GPU run makes."""
+    port = _free_port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+               LOCAL_WORLD_SIZE=str(world), HPCJOIN_SHARE_GPU="1")
+    script = os.path.join(ROOT, "tests", "rccl_worker.py")
+    procs = [subprocess.Popen([sys.executable, "-u", script], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(world)]
+    try:
+        outs = [p.communicate(timeout=100)[0] for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o[-4000:]
+    assert "OK" in outs[0], outs[0][-4000:]
