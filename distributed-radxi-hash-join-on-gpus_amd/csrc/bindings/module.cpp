@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <memory>
+#include <tuple>
 #include <vector>
 
 #include "../comm/InProcessCommunicator.h"
@@ -363,6 +364,99 @@ double benchHistogram(const at::Tensor &tuples, int64_t bits, int iters) {
       iters);
 }
 
+// Wire codec on explicit segments [(raw offset, n, rid base)] (tests and the
+// wire micro-benchmark).  Segments are packed back to back.
+std::vector<kernels::WireSeg> wireSegs(const std::vector<std::tuple<uint64_t, uint64_t, uint64_t>> &segs,
+                                       const kernels::WireCodec &c, uint64_t *words, uint64_t *groups) {
+  std::vector<kernels::WireSeg> out;
+  uint64_t off = 0, g = 0;
+  for (const auto &t : segs) {
+    const uint64_t n = std::get<1>(t);
+    if (n) out.push_back({std::get<0>(t), off, n, std::get<2>(t), g});
+    off += c.words(n);
+    g += ceilDiv(n, 64);
+  }
+  *words = off;
+  *groups = g;
+  return out;
+}
+
+kernels::WireCodec makeCodec(uint32_t w, uint32_t ridBits, uint32_t keyShift) {
+  TORCH_CHECK(w >= 1 && w <= 64 && ridBits <= w && keyShift >= ridBits && keyShift < 64, "bad wire codec");
+  kernels::WireCodec c;
+  c.w = w;
+  c.ridBits = ridBits;
+  c.keyShift = keyShift;
+  return c;
+}
+
+at::Tensor opWirePack(const at::Tensor &raw, uint32_t w, uint32_t ridBits, uint32_t keyShift,
+                      const std::vector<std::tuple<uint64_t, uint64_t, uint64_t>> &segs) {
+  checkWords(raw, "raw");
+  setDevice(raw);
+  const kernels::WireCodec c = makeCodec(w, ridBits, keyShift);
+  uint64_t words, groups;
+  std::vector<kernels::WireSeg> sg = wireSegs(segs, c, &words, &groups);
+  for (const auto &x : sg) TORCH_CHECK(x.raw + x.n <= (uint64_t)raw.numel(), "segment out of range");
+  at::Tensor wire = at::zeros({(int64_t)std::max<uint64_t>(words, 1)}, like(raw));
+  if (raw.is_cuda()) {
+    at::Tensor d = at::empty({(int64_t)(std::max<size_t>(sg.size(), 1) * sizeof(kernels::WireSeg))},
+                             like(raw, at::kByte));
+    HIP_CHECK(hipMemcpy(d.data_ptr(), sg.data(), sg.size() * sizeof(kernels::WireSeg), hipMemcpyHostToDevice));
+    kernels::wirePack(ptr<uint64_t>(raw), ptr<uint64_t>(wire), ptr<kernels::WireSeg>(d), (uint32_t)sg.size(), groups,
+                      c, nullptr);
+    HIP_CHECK(hipDeviceSynchronize());
+  } else {
+    host::wirePack(ptr<uint64_t>(raw), ptr<uint64_t>(wire), sg.data(), (uint32_t)sg.size(), c);
+  }
+  return wire;
+}
+
+void opWireUnpack(const at::Tensor &wire, const at::Tensor &raw, uint32_t w, uint32_t ridBits, uint32_t keyShift,
+                  const std::vector<std::tuple<uint64_t, uint64_t, uint64_t>> &segs) {
+  checkWords(wire, "wire");
+  checkWords(raw, "raw");
+  setDevice(raw);
+  const kernels::WireCodec c = makeCodec(w, ridBits, keyShift);
+  uint64_t words, groups;
+  std::vector<kernels::WireSeg> sg = wireSegs(segs, c, &words, &groups);
+  TORCH_CHECK(words <= (uint64_t)wire.numel(), "wire buffer too small");
+  for (const auto &x : sg) TORCH_CHECK(x.raw + x.n <= (uint64_t)raw.numel(), "segment out of range");
+  if (raw.is_cuda()) {
+    at::Tensor d = at::empty({(int64_t)(std::max<size_t>(sg.size(), 1) * sizeof(kernels::WireSeg))},
+                             like(raw, at::kByte));
+    HIP_CHECK(hipMemcpy(d.data_ptr(), sg.data(), sg.size() * sizeof(kernels::WireSeg), hipMemcpyHostToDevice));
+    kernels::wireUnpack(ptr<uint64_t>(wire), ptr<uint64_t>(raw), ptr<kernels::WireSeg>(d), (uint32_t)sg.size(),
+                        groups, c, nullptr);
+    HIP_CHECK(hipDeviceSynchronize());
+  } else {
+    host::wireUnpack(ptr<uint64_t>(wire), ptr<uint64_t>(raw), sg.data(), (uint32_t)sg.size(), c);
+  }
+}
+
+// Pack + unpack of one n-tuple segment, device ms each (median).
+py::dict benchWire(const at::Tensor &raw, uint32_t w, uint32_t ridBits, uint32_t keyShift, int iters) {
+  checkWords(raw, "raw");
+  TORCH_CHECK(raw.is_cuda(), "bench_wire needs a HIP tensor");
+  setDevice(raw);
+  const kernels::WireCodec c = makeCodec(w, ridBits, keyShift);
+  uint64_t words, groups;
+  std::vector<kernels::WireSeg> sg = wireSegs({{0, (uint64_t)raw.numel(), 0}}, c, &words, &groups);
+  at::Tensor wire = at::empty({(int64_t)words}, like(raw));
+  at::Tensor back = at::empty_like(raw);
+  at::Tensor d = at::empty({(int64_t)sizeof(kernels::WireSeg)}, like(raw, at::kByte));
+  HIP_CHECK(hipMemcpy(d.data_ptr(), sg.data(), sizeof(kernels::WireSeg), hipMemcpyHostToDevice));
+  const auto *ds = ptr<kernels::WireSeg>(d);
+  py::dict out;
+  out["pack_ms"] = timeDevice(
+      [&](hipStream_t s) { kernels::wirePack(ptr<uint64_t>(raw), ptr<uint64_t>(wire), ds, 1, groups, c, s); }, iters);
+  out["unpack_ms"] = timeDevice(
+      [&](hipStream_t s) { kernels::wireUnpack(ptr<uint64_t>(wire), ptr<uint64_t>(back), ds, 1, groups, c, s); },
+      iters);
+  out["wire_bytes"] = words * 8;
+  return out;
+}
+
 double benchCopy(const at::Tensor &src, const at::Tensor &dst, int iters) {
   setDevice(src);
   const uint64_t n16 = src.numel() * src.element_size() / 16;
@@ -438,6 +532,7 @@ py::dict resultToDict(const operators::JoinResult &r) {
   d["setup_ms"] = r.setupMs;
   d["teardown_ms"] = r.teardownMs;
   d["inner_received"] = r.innerReceived;
+  d["wire_bytes"] = r.wireBytes;
   d["outer_received"] = r.outerReceived;
   d["local_items"] = r.localItems;
   d["build_probe_items"] = r.buildProbeItems;
@@ -486,6 +581,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .value("EXACT", core::HistogramMode::Exact)
       .value("SAMPLED", core::HistogramMode::Sampled);
   m.attr("NetworkHistogram") = m.attr("HistogramMode");
+  py::enum_<core::WireCodecMode>(m, "WireCodecMode")
+      .value("AUTO", core::WireCodecMode::Auto)
+      .value("OFF", core::WireCodecMode::Off)
+      .value("ON", core::WireCodecMode::On);
   py::class_<core::JoinConfig>(m, "JoinConfig")
       .def(py::init<>())
       .def_readwrite("network_bits", &core::JoinConfig::networkBits)
@@ -499,6 +598,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("network_histogram", &core::JoinConfig::networkHistogram)
       .def_readwrite("local_histogram", &core::JoinConfig::localHistogram)
       .def_readwrite("sample_stride", &core::JoinConfig::sampleStride)
+      .def_readwrite("wire_codec", &core::JoinConfig::wireCodec)
       .def_readwrite("output_capacity", &core::JoinConfig::outputCapacity)
       .def_readwrite("build_target", &core::JoinConfig::buildTarget)
       .def_readwrite("r_chunk", &core::JoinConfig::rChunk)
@@ -517,6 +617,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("key_shift", &core::JoinPlan::keyShift)
       .def_readonly("frag_shift", &core::JoinPlan::fragShift)
       .def_readonly("key_bits", &core::JoinPlan::keyBits)
+      .def_property_readonly("wire_bits", [](const core::JoinPlan &p) {
+        return std::vector<uint32_t>{p.wireBits[0], p.wireBits[1]};
+      })
       .def_readonly("r_chunk", &core::JoinPlan::rChunk)
       .def_readonly("s_chunk", &core::JoinPlan::sChunk)
       .def_readonly("chunks", &core::JoinPlan::chunks)
@@ -824,6 +927,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       },
       py::arg("n"), py::arg("rid_offset"), py::arg("seed"), py::arg("device") = "cpu");
   ops.def("npj_count", &opNpjCount);
+  ops.def("wire_pack", &opWirePack, py::arg("raw"), py::arg("w"), py::arg("rid_bits"), py::arg("key_shift"),
+          py::arg("segments"));
+  ops.def("wire_unpack", &opWireUnpack, py::arg("wire"), py::arg("raw"), py::arg("w"), py::arg("rid_bits"),
+          py::arg("key_shift"), py::arg("segments"));
+  ops.def("bench_wire", &benchWire, py::arg("raw"), py::arg("w"), py::arg("rid_bits"), py::arg("key_shift"),
+          py::arg("iters") = 10);
   ops.def("net_scatter_global_atomic", &opNetScatterGlobalAtomic);
   ops.def("bench_copy_ms", &benchCopy, py::arg("src"), py::arg("dst"), py::arg("iters") = 10);
   ops.def("bench_read_ms", &benchRead, py::arg("src"), py::arg("iters") = 10);

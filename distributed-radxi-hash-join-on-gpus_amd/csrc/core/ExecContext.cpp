@@ -22,6 +22,7 @@ ExecContext::ExecContext(Location loc, int device, comm::Communicator *comm)
     HIP_CHECK(hipSetDevice(device_));
     HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     HIP_CHECK(hipStreamCreateWithFlags(&commStream_, hipStreamNonBlocking));
+    HIP_CHECK(hipStreamCreateWithFlags(&decodeStream_, hipStreamNonBlocking));
   }
 }
 
@@ -30,6 +31,7 @@ ExecContext::~ExecContext() {
   staging_.reset();
   if (stream_) (void)hipStreamDestroy(stream_);
   if (commStream_) (void)hipStreamDestroy(commStream_);
+  if (decodeStream_) (void)hipStreamDestroy(decodeStream_);
 }
 
 uint32_t ExecContext::nodeId() const { return comm_->rank(); }
@@ -39,10 +41,12 @@ void ExecContext::synchronize() const {
   if (!onDevice()) return;
   if (comm_->size() > 1) {  // a lost peer must not hang this rank forever
     utils::waitStream(commStream_, comm_, "exchange stream");
+    utils::waitStream(decodeStream_, comm_, "decode stream");
     utils::waitStream(stream_, comm_, "compute stream");
     return;
   }
   HIP_CHECK(hipStreamSynchronize(commStream_));
+  HIP_CHECK(hipStreamSynchronize(decodeStream_));
   HIP_CHECK(hipStreamSynchronize(stream_));
 }
 

@@ -33,6 +33,7 @@ class ExecContext {
   int device() const { return device_; }
   hipStream_t stream() const { return stream_; }          // compute stream
   hipStream_t commStream() const { return commStream_; }  // exchange stream (overlaps compute)
+  hipStream_t decodeStream() const { return decodeStream_; }  // wire unpack (overlaps the next exchange)
   comm::Communicator *comm() const { return comm_; }
   uint32_t nodeId() const;
   uint32_t numberOfNodes() const;
@@ -49,6 +50,7 @@ class ExecContext {
   comm::Communicator *comm_;
   hipStream_t stream_ = nullptr;
   hipStream_t commStream_ = nullptr;
+  hipStream_t decodeStream_ = nullptr;
   std::unique_ptr<memory::Arena> workspace_;
   std::unique_ptr<memory::Arena> staging_;
 };

@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "Configuration.h"
 #include "Types.h"
@@ -43,6 +44,14 @@ enum class HistogramMode : int {
   Sampled = 2,
 };
 
+// Exchange wire format (kernels.h, WireCodec): bit-packed frame-of-reference
+// tuples on the xGMI links instead of full 8-byte CompressedTuples.
+enum class WireCodecMode : int {
+  Auto = 0,  // device engine, N > 1, when it saves >= 1/8 of the bytes
+  Off = 1,
+  On = 2,    // whenever the tuple fits < 64 bits (also the host path: tests)
+};
+
 struct JoinConfig {
   uint32_t networkBits = 0;   // radix bits of the network pass (0 = auto)
   uint32_t localBits = 0;     // radix bits of the local pass (0 = auto; ignored if !twoLevel)
@@ -62,6 +71,7 @@ struct JoinConfig {
   HistogramMode networkHistogram = HistogramMode::Auto;
   HistogramMode localHistogram = HistogramMode::Auto;
   uint32_t sampleStride = 16;   // sampled passes: histogram 1 tile in sampleStride
+  WireCodecMode wireCodec = WireCodecMode::Auto;
 
   std::string describe() const;
 };
@@ -85,6 +95,11 @@ struct JoinPlan {
   HistogramMode localHistogram = HistogramMode::Exact;  // resolved per window size by LocalPartitioning
   uint32_t sampleStride = 16;
   AssignmentPolicy assignment = AssignmentPolicy::LPT;
+  // Wire codec per relation (0 = inner, 1 = outer): bits per tuple (0 = off),
+  // rid bits, and every rank's rid base.  Set by HashJoin::planWireCodec.
+  uint32_t wireBits[2] = {0, 0};
+  uint32_t wireRidBits[2] = {0, 0};
+  std::vector<uint64_t> ridBase[2];
   uint64_t networkPartitions() const { return uint64_t(1) << networkBits; }
   uint64_t localPartitions() const { return twoLevel ? (uint64_t(1) << localBits) : 1; }
   std::string describe() const;

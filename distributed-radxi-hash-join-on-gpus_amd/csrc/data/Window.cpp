@@ -1,8 +1,10 @@
 #include "Window.h"
 
 #include <algorithm>
+#include <cstring>
 
 #include "../comm/Communicator.h"
+#include "../host/HostOps.h"
 #include "../memory/Arena.h"
 #include "../utils/Hip.h"
 
@@ -35,12 +37,90 @@ Window::Window(const histograms::ExchangePlan &plan, uint64_t capacityTuples, co
 Window::~Window() {
   for (auto e : ready) (void)hipEventDestroy(e);
   for (auto e : done) (void)hipEventDestroy(e);
+  for (auto e : wired) (void)hipEventDestroy(e);
+}
+
+void Window::setWireCodec(const kernels::WireCodec &c, const std::vector<uint64_t> &bases) {
+  JOIN_ASSERT(!wide || c.w == 0, "Window", "the wire codec packs 8-byte CompressedTuples only");
+  JOIN_ASSERT(c.w == 0 || bases.size() == plan.numberOfNodes, "Window", "need one rid base per rank");
+  codec = c;
+  ridBase = bases;
+  if (codec.w && ctx->onDevice() && plan.numberOfNodes > 1 && wired.empty()) {
+    wired.resize(plan.chunks);
+    for (auto &e : wired) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+}
+
+// Packed exchange of one chunk: pack (compute stream) -> own slice copied raw
+// + all-to-allv of the wire words (exchange stream) -> unpack into the window
+// (decode stream, so the next chunk's all-to-allv starts right away).
+void Window::exchangePacked(const uint64_t *send, uint32_t chunk) {
+  const uint32_t N = plan.numberOfNodes, me = plan.nodeId;
+  if (sendSegs.empty()) {
+    sendSegs.resize(plan.chunks);
+    recvSegs.resize(plan.chunks);
+  }
+  std::vector<kernels::WireSeg> &ss = sendSegs[chunk], &rs = recvSegs[chunk];
+  ss.clear();
+  rs.clear();
+  std::vector<uint64_t> sc(N, 0), sd(N, 0), rc(N, 0), rd(N, 0);
+  uint64_t sOff = 0, rOff = 0, sGroups = 0, rGroups = 0;
+  for (uint32_t p = 0; p < N; ++p) {
+    if (p == me) continue;
+    const uint64_t n = plan.sendCounts[(size_t)chunk * N + p], m = plan.recvCounts[(size_t)chunk * N + p];
+    if (n) ss.push_back({plan.sendDispls[(size_t)chunk * N + p], sOff, n, ridBase[me], sGroups});
+    sc[p] = codec.words(n);
+    sd[p] = sOff;
+    sOff += sc[p];
+    sGroups += ceilDiv(n, 64);
+    if (m) rs.push_back({plan.recvDispls[(size_t)chunk * N + p], rOff, m, ridBase[p], rGroups});
+    rc[p] = codec.words(m);
+    rd[p] = rOff;
+    rOff += rc[p];
+    rGroups += ceilDiv(m, 64);
+  }
+  wireSent += sOff;
+  const uint64_t selfN = plan.sendCounts[(size_t)chunk * N + me];
+  const uint64_t selfSrc = plan.sendDispls[(size_t)chunk * N + me], selfDst = plan.recvDispls[(size_t)chunk * N + me];
+  JOIN_ASSERT(selfN == plan.recvCounts[(size_t)chunk * N + me], "Window", "own slice mismatch");
+  uint64_t *wsend = ctx->workspace().getArray<uint64_t>(std::max<uint64_t>(sOff, 1));
+  uint64_t *wrecv = ctx->workspace().getArray<uint64_t>(std::max<uint64_t>(rOff, 1));
+  uint64_t *dst = static_cast<uint64_t *>(data);
+  if (ctx->onDevice() && N > 1) {
+    kernels::WireSeg *dS = ctx->workspace().getArray<kernels::WireSeg>(std::max<size_t>(ss.size(), 1));
+    kernels::WireSeg *dR = ctx->workspace().getArray<kernels::WireSeg>(std::max<size_t>(rs.size(), 1));
+    ctx->copy(dS, ss.data(), ss.size() * sizeof(kernels::WireSeg), true, false);
+    ctx->copy(dR, rs.data(), rs.size() * sizeof(kernels::WireSeg), true, false);
+    kernels::wirePack(send, wsend, dS, (uint32_t)ss.size(), sGroups, codec, ctx->stream());
+    HIP_CHECK(hipEventRecord(ready[chunk], ctx->stream()));
+    HIP_CHECK(hipStreamWaitEvent(ctx->commStream(), ready[chunk], 0));
+    if (selfN)
+      HIP_CHECK(hipMemcpyAsync(dst + selfDst, send + selfSrc, selfN * 8, hipMemcpyDeviceToDevice,
+                               ctx->commStream()));
+    ctx->comm()->allToAllV(wsend, sc.data(), sd.data(), wrecv, rc.data(), rd.data(), Location::Device,
+                           ctx->commStream());
+    HIP_CHECK(hipEventRecord(wired[chunk], ctx->commStream()));
+    HIP_CHECK(hipStreamWaitEvent(ctx->decodeStream(), wired[chunk], 0));
+    kernels::wireUnpack(wrecv, dst, dR, (uint32_t)rs.size(), rGroups, codec, ctx->decodeStream());
+    HIP_CHECK(hipEventRecord(done[chunk], ctx->decodeStream()));
+  } else {
+    host::wirePack(send, wsend, ss.data(), (uint32_t)ss.size(), codec);
+    if (selfN) std::memcpy(dst + selfDst, send + selfSrc, selfN * 8);
+    ctx->comm()->allToAllV(wsend, sc.data(), sd.data(), wrecv, rc.data(), rd.data(), ctx->location(),
+                           ctx->stream());
+    host::wireUnpack(wrecv, dst, rs.data(), (uint32_t)rs.size(), codec);
+  }
 }
 
 void Window::start() { open = true; }
 
 void Window::exchange(const void *sendBuffer, uint32_t chunk) {
   JOIN_ASSERT(chunk < plan.chunks, "Window", "chunk %u out of range", chunk);
+  if (codec.w && plan.numberOfNodes > 1) {
+    exchangePacked(static_cast<const uint64_t *>(sendBuffer), chunk);
+    exchanged[chunk] = true;
+    return;
+  }
   const uint32_t N = plan.numberOfNodes;
   const uint64_t w = tupleBytes() / 8;  // 8-byte words per tuple
   std::vector<uint64_t> sc(N), sd(N), rc(N), rd(N);
@@ -50,6 +130,8 @@ void Window::exchange(const void *sendBuffer, uint32_t chunk) {
     rc[p] = plan.recvCounts[(size_t)chunk * N + p] * w;
     rd[p] = plan.recvDispls[(size_t)chunk * N + p] * w;
   }
+  for (uint32_t p = 0; p < N; ++p)
+    if (p != plan.nodeId) wireSent += sc[p];
   const uint64_t *src = static_cast<const uint64_t *>(sendBuffer);
   uint64_t *dst = static_cast<uint64_t *>(data);
   if (ctx->onDevice() && N > 1) {

@@ -18,6 +18,7 @@
 #include "../histograms/AssignmentMap.h"
 #include "../histograms/ExchangePlan.h"
 #include "../histograms/GlobalHistogram.h"
+#include "../kernels/kernels.h"
 #include "CompressedTuple.h"
 #include "Tuple.h"
 
@@ -41,6 +42,11 @@ class Window {
   // Enqueue the all-to-allv of one chunk once the compute stream reaches this
   // point (the chunk's scatter kernel is already enqueued on it).
   void exchange(const void *sendBuffer, uint32_t chunk);
+  // Bit-pack tuples on the wire (kernels.h, WireCodec); ridBase[rank] is each
+  // sender's rid base.  Call before the first exchange.
+  void setWireCodec(const kernels::WireCodec &codec, const std::vector<uint64_t> &ridBase);
+  const kernels::WireCodec &wireCodec() const { return codec; }
+  uint64_t wireBytesSent() const { return wireSent * 8; }  // bytes this rank put on the links (all chunks)
 
   CompressedTuple *getPartition(uint32_t partitionId);  // partition-major (after local partitioning)
   Tuple *getWidePartition(uint32_t partitionId);
@@ -75,6 +81,13 @@ class Window {
   bool open = false;
   std::vector<hipEvent_t> ready, done;
   std::vector<bool> exchanged;
+  void exchangePacked(const uint64_t *send, uint32_t chunk);
+  kernels::WireCodec codec;
+  std::vector<uint64_t> ridBase;
+  // Per-chunk segment lists: kept alive until the join ends (async H2D source).
+  std::vector<std::vector<kernels::WireSeg>> sendSegs, recvSegs;
+  std::vector<hipEvent_t> wired;  // chunk's all-to-allv done (exchange stream -> decode stream)
+  uint64_t wireSent = 0;
   void *partitioned = nullptr;
   const uint64_t *partBegin = nullptr;
   const uint64_t *partEnd = nullptr;

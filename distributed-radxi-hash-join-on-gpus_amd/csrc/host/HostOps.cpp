@@ -250,5 +250,40 @@ uint64_t npjJoin(const data::Tuple *R, uint64_t nR, const data::Tuple *S, uint64
   return m;
 }
 
+// Wire codec twins: a plain bit-stream writer/reader over each segment's
+// groups of 64 (independent of the device's per-lane word assembly).
+void wirePack(const uint64_t *raw, uint64_t *wire, const kernels::WireSeg *segs, uint32_t nSegs,
+              const kernels::WireCodec &c) {
+  const uint64_t wmask = c.w >= 64 ? ~0ull : ((1ull << c.w) - 1);
+  for (uint32_t s = 0; s < nSegs; ++s) {
+    const kernels::WireSeg &sg = segs[s];
+    uint64_t *out = wire + sg.wire;
+    std::fill(out, out + c.words(sg.n), 0ull);
+    for (uint64_t t = 0; t < sg.n; ++t) {
+      const uint64_t e = c.encode(raw[sg.raw + t], sg.base) & wmask;
+      const uint64_t bit = (t / 64) * 64 * c.w + (t % 64) * c.w;
+      const uint64_t j = bit / 64, o = bit % 64;
+      out[j] |= e << o;
+      if (o + c.w > 64) out[j + 1] |= e >> (64 - o);
+    }
+  }
+}
+
+void wireUnpack(const uint64_t *wire, uint64_t *raw, const kernels::WireSeg *segs, uint32_t nSegs,
+                const kernels::WireCodec &c) {
+  const uint64_t wmask = c.w >= 64 ? ~0ull : ((1ull << c.w) - 1);
+  for (uint32_t s = 0; s < nSegs; ++s) {
+    const kernels::WireSeg &sg = segs[s];
+    const uint64_t *in = wire + sg.wire;
+    for (uint64_t t = 0; t < sg.n; ++t) {
+      const uint64_t bit = (t / 64) * 64 * c.w + (t % 64) * c.w;
+      const uint64_t j = bit / 64, o = bit % 64;
+      uint64_t e = in[j] >> o;
+      if (o + c.w > 64) e |= in[j + 1] << (64 - o);
+      raw[sg.raw + t] = c.decode(e & wmask, sg.base);
+    }
+  }
+}
+
 }  // namespace host
 }  // namespace hpcjoin

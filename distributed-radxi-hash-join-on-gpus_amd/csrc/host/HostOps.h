@@ -40,6 +40,12 @@ void localScatter(const void *in, bool wide, const kernels::LocalItem *items, ui
 // a.materialize) writes pairs through a.outPairs / a.outCursor (host memory).
 uint64_t buildProbe(const kernels::BPArgs &a);
 
+// Wire codec (kernels.h, WireCodec) over host segment lists.
+void wirePack(const uint64_t *raw, uint64_t *wire, const kernels::WireSeg *segs, uint32_t nSegs,
+              const kernels::WireCodec &c);
+void wireUnpack(const uint64_t *wire, uint64_t *raw, const kernels::WireSeg *segs, uint32_t nSegs,
+                const kernels::WireCodec &c);
+
 uint64_t npjJoin(const data::Tuple *R, uint64_t nR, const data::Tuple *S, uint64_t nS);
 
 }  // namespace host

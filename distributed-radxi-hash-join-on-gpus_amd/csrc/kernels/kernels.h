@@ -218,6 +218,43 @@ void bpEmit(const BPArgs &a, const uint32_t *counts, const uint32_t *offsets, BP
 // written by the scan, so no host round trip sits between plan and probe.
 void buildProbe(const BPArgs &a, const BPItem *items, const uint32_t *nItems, uint32_t capacity, hipStream_t s);
 
+// ------------------------------------------------------------ wire codec
+// Exchange wire format for 8-byte CompressedTuples (N > 1).  On the wire a
+// tuple needs only its key fragment above the network digit (the receiver
+// knows the partition) and its rid relative to the sending rank's smallest
+// rid (frame of reference): w = ridBits + keyFragmentBits bits, e.g. 48 for
+// 1B unique keys on 8 ranks (21 + 27) instead of 64.  Tuples are bit-packed
+// in groups of 64: a group of a segment occupies w u64 words, lane j of a
+// wave64 writing word j.  The xGMI links are the bottleneck of the
+// distributed join, so this cuts the exchange time by (64 - w) / 64.
+struct WireCodec {
+  uint32_t w = 0;         // bits per tuple on the wire (0 = codec off)
+  uint32_t ridBits = 0;   // low bits of a wire value: rid - base
+  uint32_t keyShift = 32; // CompressedTuple: value = rid | fragment << keyShift
+  HJ_HD uint64_t encode(uint64_t v, uint64_t base) const {
+    const uint64_t rid = v & ((1ull << keyShift) - 1);
+    return (rid - base) | ((v >> keyShift) << ridBits);
+  }
+  HJ_HD uint64_t decode(uint64_t e, uint64_t base) const {
+    const uint64_t rid = (e & ((1ull << ridBits) - 1)) + base;
+    return rid | ((e >> ridBits) << keyShift);
+  }
+  HJ_HD uint64_t words(uint64_t n) const { return (n + 63) / 64 * w; }
+};
+// One contiguous run of tuples <-> one packed run of words.
+struct WireSeg {
+  uint64_t raw;     // tuple offset in the raw (8-byte) buffer
+  uint64_t wire;    // word offset in the wire buffer
+  uint64_t n;       // tuples
+  uint64_t base;    // rid base of the sending rank
+  uint64_t group0;  // first global group index of this segment (prefix of ceil(n/64))
+};
+// segs is a device array (nSegs entries, ascending group0); totalGroups = sum ceil(n/64).
+void wirePack(const uint64_t *raw, uint64_t *wire, const WireSeg *segs, uint32_t nSegs, uint64_t totalGroups,
+              const WireCodec &c, hipStream_t s);
+void wireUnpack(const uint64_t *wire, uint64_t *raw, const WireSeg *segs, uint32_t nSegs, uint64_t totalGroups,
+                const WireCodec &c, hipStream_t s);
+
 // ------------------------------------------------------------------- scans
 size_t scanWorkspaceBytes(uint64_t n);
 // out[i] = sum_{j<i} in[j]; *total = sum of all (device pointer, may be null).
@@ -242,7 +279,8 @@ void readKernel(const ulonglong2 *in, uint64_t n16, unsigned long long *sink, hi
 
 namespace hpcjoin {
 namespace kernels {
-// out[0] = max key, out[1] = max rid over n tuples (device); out must be zeroed.
+// out[0] = max key, out[1] = max rid, out[2] = min rid over n tuples (device);
+// out[0..1] must be zeroed and out[2] set to ~0.
 void keyRidMax(const data::Tuple *in, uint64_t n, unsigned long long *out, hipStream_t s);
 }  // namespace kernels
 }  // namespace hpcjoin

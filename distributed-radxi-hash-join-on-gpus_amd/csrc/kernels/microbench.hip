@@ -29,21 +29,25 @@ __global__ __launch_bounds__(256) void readKernelImpl(const ulonglong2 *__restri
 __global__ __launch_bounds__(256) void keyRidMaxKernel(const ulonglong2 *__restrict__ in, uint64_t n,
                                                        unsigned long long *out) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;
-  unsigned long long k = 0, r = 0;
+  unsigned long long k = 0, r = 0, rmin = ~0ull;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
     const ulonglong2 v = in[i];
     k = v.x > k ? v.x : k;
     r = v.y > r ? v.y : r;
+    rmin = v.y < rmin ? v.y : rmin;
   }
 #pragma unroll
   for (int o = WAVE / 2; o > 0; o >>= 1) {
-    const unsigned long long k2 = __shfl_xor(k, o, WAVE), r2 = __shfl_xor(r, o, WAVE);
+    const unsigned long long k2 = __shfl_xor(k, o, WAVE), r2 = __shfl_xor(r, o, WAVE),
+                             m2 = __shfl_xor(rmin, o, WAVE);
     k = k2 > k ? k2 : k;
     r = r2 > r ? r2 : r;
+    rmin = m2 < rmin ? m2 : rmin;
   }
   if ((threadIdx.x & (WAVE - 1)) == 0) {
     atomicMax(&out[0], k);
     atomicMax(&out[1], r);
+    atomicMin(&out[2], rmin);
   }
 }
 

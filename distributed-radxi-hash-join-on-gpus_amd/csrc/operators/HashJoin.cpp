@@ -61,35 +61,45 @@ void HashJoin::makeJoinPlan() {
   };
   JOIN_ASSERT(usable(innerRelation) && usable(outerRelation), "HashJoin",
               "relations must live where the engine runs (%s) or in pinned host memory", locationName(ctx->location()));
-  // Max key / rid over both relations and all ranks (the plan must be identical everywhere).
-  uint64_t mx[2] = {0, 0};
+  // Max key / rid over both relations and all ranks (the plan must be identical
+  // everywhere), plus each rank's rid range per relation (wire codec bases).
+  // Per rank: {max key, max rid, min rid inner, max rid inner, min rid outer, max rid outer}.
+  constexpr size_t STATS = 6;
+  uint64_t st[STATS] = {0, 0, ~0ull, 0, ~0ull, 0};
+  int which = 0;
   for (data::Relation *r : {innerRelation, outerRelation}) {
+    uint64_t h[3] = {0, 0, ~0ull};
     if (ctx->onDevice()) {
-      unsigned long long *d = ctx->workspace().getArray<unsigned long long>(2);
-      HIP_CHECK(hipMemsetAsync(d, 0, 16, ctx->stream()));
+      unsigned long long *d = ctx->workspace().getArray<unsigned long long>(3);
+      HIP_CHECK(hipMemcpyAsync(d, h, 24, hipMemcpyHostToDevice, ctx->stream()));
       kernels::keyRidMax(r->getData(), r->getLocalSize(), d, ctx->stream());
-      unsigned long long h[2];
-      HIP_CHECK(hipMemcpyAsync(h, d, 16, hipMemcpyDeviceToHost, ctx->stream()));
+      HIP_CHECK(hipMemcpyAsync(h, d, 24, hipMemcpyDeviceToHost, ctx->stream()));
       HIP_CHECK(hipStreamSynchronize(ctx->stream()));
-      mx[0] = std::max<uint64_t>(mx[0], h[0]);
-      mx[1] = std::max<uint64_t>(mx[1], h[1]);
     } else {
       const data::Tuple *t = r->getData();
       for (uint64_t i = 0; i < r->getLocalSize(); ++i) {
-        mx[0] = std::max(mx[0], t[i].key);
-        mx[1] = std::max(mx[1], t[i].rid);
+        h[0] = std::max<uint64_t>(h[0], t[i].key);
+        h[1] = std::max<uint64_t>(h[1], t[i].rid);
+        h[2] = std::min<uint64_t>(h[2], t[i].rid);
       }
     }
+    st[0] = std::max(st[0], h[0]);
+    st[1] = std::max(st[1], h[1]);
+    st[2 + 2 * which] = h[2];
+    st[3 + 2 * which] = h[1];
+    ++which;
   }
   ctx->workspace().reset();
-  std::vector<uint64_t> all(2 * numberOfNodes);
-  ctx->comm()->allGatherHost(mx, all.data(), 2);
+  std::vector<uint64_t> all(STATS * numberOfNodes);
+  ctx->comm()->allGatherHost(st, all.data(), STATS);
+  uint64_t mx[2] = {0, 0};
   for (uint32_t r = 0; r < numberOfNodes; ++r) {
-    mx[0] = std::max(mx[0], all[2 * r]);
-    mx[1] = std::max(mx[1], all[2 * r + 1]);
+    mx[0] = std::max(mx[0], all[STATS * r]);
+    mx[1] = std::max(mx[1], all[STATS * r + 1]);
   }
   plan = core::makePlan(config, numberOfNodes, innerRelation->getGlobalSize(), outerRelation->getGlobalSize(), mx[0],
                         mx[1]);
+  planWireCodec(all, STATS);
   if (config.keyHashing == core::KeyHashing::Auto && plan.keyBits < 64) plan.keyMix = lowKeyBitsSkewed();
   if (!ctx->onDevice()) plan.localHistogram = core::HistogramMode::Exact;  // sampling pays on HBM only
   {
@@ -103,6 +113,37 @@ void HashJoin::makeJoinPlan() {
   JOIN_DEBUG("HashJoin", "%s", plan.describe().c_str());
   if (ctx->onDevice())
     for (auto &e : ev) HIP_CHECK(hipEventCreate(&e));
+}
+
+// Wire codec per relation (kernels.h, WireCodec): frame-of-reference rids
+// (base = the sending rank's smallest rid) plus the key fragment above the
+// network digit.  Auto packs on a device engine with N > 1 when it saves at
+// least 1/8 of the wire bytes (w <= 56); On forces it (also on the host path).
+void HashJoin::planWireCodec(const std::vector<uint64_t> &all, size_t stride) {
+  for (int r = 0; r < 2; ++r) {
+    plan.wireBits[r] = 0;
+    plan.wireRidBits[r] = 0;
+    plan.ridBase[r].assign(numberOfNodes, 0);
+  }
+  if (plan.wide || numberOfNodes == 1 || config.wireCodec == core::WireCodecMode::Off) return;
+  const uint32_t keyW = plan.keyBits > plan.networkBits ? plan.keyBits - plan.networkBits : 0;
+  for (int r = 0; r < 2; ++r) {
+    uint64_t span = 1;
+    for (uint32_t n = 0; n < numberOfNodes; ++n) {
+      const uint64_t lo = all[stride * n + 2 + 2 * r], hi = all[stride * n + 3 + 2 * r];
+      if (lo > hi) continue;  // empty slice
+      plan.ridBase[r][n] = lo;
+      span = std::max<uint64_t>(span, hi - lo + 1);
+    }
+    const uint32_t ridBits = std::max<uint32_t>(1, ceilLog2(span));
+    const uint32_t w = ridBits + keyW;
+    const bool on = config.wireCodec == core::WireCodecMode::On ? w < 64 : (ctx->onDevice() && w <= 56);
+    if (on && ridBits <= plan.keyShift) {
+      plan.wireBits[r] = w;
+      plan.wireRidBits[r] = ridBits;
+    }
+  }
+  JOIN_DEBUG("HashJoin", "wire codec: inner %u bits, outer %u bits per tuple", plan.wireBits[0], plan.wireBits[1]);
 }
 
 // KeyHashing::Auto: histogram the inner keys' low networkBits bits (all ranks)
@@ -229,6 +270,14 @@ JoinResult HashJoin::runImpl() {
                                       hc->assignmentMap(), ctx, plan.wide));
     innerWindow = innerOwned.get();
     outerWindow = outerOwned.get();
+    for (int r = 0; r < 2; ++r)
+      if (plan.wireBits[r]) {
+        kernels::WireCodec c;
+        c.w = plan.wireBits[r];
+        c.ridBits = plan.wireRidBits[r];
+        c.keyShift = plan.keyShift;
+        (r == 0 ? innerWindow : outerWindow)->setWireCodec(c, plan.ridBase[r]);
+      }
     if (!sampled) {
       Measurements::stopWindowAllocation();
       t2 = nowUs();
@@ -322,6 +371,7 @@ JoinResult HashJoin::runImpl() {
   result.buildProbeItems = bp->getWorkItems();
   output = bp->getOutput();
   bp.reset();
+  result.wireBytes = innerWindow->wireBytesSent() + outerWindow->wireBytesSent();
   result.innerReceived = innerWindow->computeLocalWindowSize();
   result.outerReceived = outerWindow->computeLocalWindowSize();
   result.sampledNetwork = sampled && !sampledOverflowed;

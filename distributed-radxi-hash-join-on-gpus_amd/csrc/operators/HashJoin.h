@@ -35,6 +35,7 @@ struct JoinResult {
   double devHistogramMs = 0, devNetworkMs = 0, devLocalPartitionMs = 0, devBuildProbeMs = 0;  // hipEvents
   double setupMs = 0, teardownMs = 0;  // outside the join span: scratch reset / result reduction
   uint64_t innerReceived = 0, outerReceived = 0;
+  uint64_t wireBytes = 0;          // bytes this rank sent to peers (after the wire codec)
   uint64_t localItems = 0, buildProbeItems = 0;
   uint64_t innerLocal = 0, outerLocal = 0;
   bool sampledNetwork = false;     // network pass sized from a sampled histogram (N == 1)
@@ -77,6 +78,7 @@ class HashJoin {
  private:
   void makeJoinPlan();
   bool lowKeyBitsSkewed();
+  void planWireCodec(const std::vector<uint64_t> &rankStats, size_t stride);
   JoinResult runImpl();
   core::ExecContext *ctx;
   std::unique_ptr<core::ExecContext> ownedCtx;

@@ -107,3 +107,18 @@ def host_link(bytes_: int = 1 << 30, device: int = 0, iters: int = 5) -> dict:
     """Host-link ceilings: DMA H2D / D2H and in-place kernel reads of pinned
     host memory (the engine's path for relations kept in pinned memory)."""
     return dict(require_native().ops.bench_host_link(bytes_, device, iters))
+
+
+def wire_phase(n=1 << 28, w=48, rid_bits=27, iters=5):
+    """Wire codec (exchange bit-packing): pack and unpack of n CompressedTuples
+    into w-bit wire values; HBM streaming, 8 + w/8 bytes per tuple each."""
+    C = require_native()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    rid = torch.randint(0, 1 << rid_bits, (n,), device="cuda", dtype=torch.int64, generator=g)
+    frag = torch.randint(0, 1 << (w - rid_bits), (n,), device="cuda", dtype=torch.int64, generator=g)
+    raw = rid | (frag << 32)
+    r = C.ops.bench_wire(raw, w, rid_bits, 32, iters)
+    moved = n * 8 + r["wire_bytes"]
+    return {"n": n, "w": w, "pack_ms": r["pack_ms"], "unpack_ms": r["unpack_ms"],
+            "pack_TBps": moved / r["pack_ms"] / 1e9, "unpack_TBps": moved / r["unpack_ms"] / 1e9,
+            "wire_ratio": r["wire_bytes"] / (n * 8)}

@@ -16,7 +16,7 @@ import pytest
 from conftest import ROOT, devices
 
 
-def run_ranks(C, n_ranks, loc, G_R, G_S, cfg_fn=None, outer_dist="UNIQUE", theta=0.75):
+def run_ranks(C, n_ranks, loc, G_R, G_S, cfg_fn=None, outer_dist="UNIQUE", theta=0.75, outputs=None):
     group = C.InProcessGroup(n_ranks)
     inner = C.GenSpec(seed=1234)
     outer = C.GenSpec(distribution=getattr(C.KeyDistribution, outer_dist), seed=4321,
@@ -39,6 +39,8 @@ def run_ranks(C, n_ranks, loc, G_R, G_S, cfg_fn=None, outer_dist="UNIQUE", theta
             res2 = j.run()  # repeatable
             assert res2["global_matches"] == res["global_matches"]
             results[r] = (res, j.plan)
+            if outputs is not None:
+                outputs[r] = j.output()
         except Exception as e:  # surface in the main thread
             errors.append((r, repr(e)))
 
@@ -120,6 +122,39 @@ def test_in_process_wide_materialize(C, dev):
 
     results, exp = run_ranks(C, 2, loc, 100_000, 100_000, cfg_fn)
     assert sum(r[0]["output_pairs"] for r in results) == exp
+
+
+@pytest.mark.parametrize("dev", devices())
+@pytest.mark.parametrize("n_ranks,chunks", [(2, 1), (3, 2), (8, 1)])
+def test_wire_codec_exchange(C, dev, n_ranks, chunks):
+    """Bit-packed exchange (frame-of-reference rids + key fragment): exact
+    counts, fewer bytes on the links, and every materialized (rid, rid) pair
+    still joins equal keys -- so rids and key fragments decode exactly."""
+    import torch
+    loc = "device" if dev == "cuda" else "host"
+    G_R, G_S = 150_001, 250_003
+
+    def cfg_fn(cfg, mode):
+        cfg.wire_codec = mode
+        cfg.chunks = chunks
+        cfg.materialize = True
+
+    outs = [None] * n_ranks
+    results, exp = run_ranks(C, n_ranks, loc, G_R, G_S, lambda c: cfg_fn(c, C.WireCodecMode.ON),
+                             outer_dist="UNIFORM", outputs=outs)
+    plain, _ = run_ranks(C, n_ranks, loc, G_R, G_S, lambda c: cfg_fn(c, C.WireCodecMode.OFF), outer_dist="UNIFORM")
+    for (res, plan), (res0, plan0) in zip(results, plain):
+        assert res["global_matches"] == exp
+        assert 0 < plan.wire_bits[0] < 64 and 0 < plan.wire_bits[1] < 64
+        assert plan0.wire_bits == [0, 0]
+        pad = 2 * chunks * n_ranks * 64 * 8  # one partial group per segment
+        assert res["wire_bytes"] <= res0["wire_bytes"] * max(plan.wire_bits) / 64 + pad
+    pairs = torch.cat(outs)
+    assert pairs.shape[0] == exp
+    R = C.ops.generate(G_R, 0, G_R, C.GenSpec(seed=1234), "cpu")
+    S = C.ops.generate(G_S, 0, G_S, C.GenSpec(distribution=C.KeyDistribution.UNIFORM, seed=4321, domain=G_R), "cpu")
+    assert torch.equal(R[pairs[:, 0], 0], S[pairs[:, 1], 0])
+    assert pairs[:, 1].unique().numel() == exp  # every outer row matched once (unique inner keys)
 
 
 def _free_port():

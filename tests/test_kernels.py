@@ -167,3 +167,37 @@ def test_global_atomic_scatter_ablation(C, cuda):
     v, b = C.ops.net_partition(t, 6, 32)
     v2 = C.ops.net_scatter_global_atomic(t, 6, 32, b)
     assert torch.equal(torch.sort(v2.cpu()).values, torch.sort(v.cpu()).values)
+
+
+@pytest.mark.parametrize("dev", devices())
+@pytest.mark.parametrize("w,rid_bits", [(48, 27), (33, 20), (64, 32), (7, 3), (50, 29)])
+def test_wire_codec_roundtrip(C, dev, w, rid_bits):
+    """Bit-packed exchange format: segments of odd lengths with their own rid
+    bases round-trip exactly, and the device packing equals the host's
+    (independent bit-stream implementation) word for word."""
+    import torch
+    g = torch.Generator().manual_seed(w)
+    key_shift = 32
+    key_bits = w - rid_bits
+    segs = [(0, 1, 5), (1, 64, 1000), (65, 130, 0), (300, 0, 7), (300, 1000, 1 << 20)]
+    n = 1300
+    rid = torch.zeros(n, dtype=torch.int64)
+    frag = torch.randint(0, 1 << key_bits, (n,), generator=g, dtype=torch.int64)
+    for off, cnt, base in segs:  # rids must stay below 2^key_shift
+        base = base if rid_bits < 32 else 0
+        rid[off:off + cnt] = base + torch.randint(0, 1 << rid_bits, (cnt,), generator=g, dtype=torch.int64)
+    segs = [(off, cnt, base if rid_bits < 32 else 0) for off, cnt, base in segs]
+    raw = rid | (frag << key_shift)
+    host_wire = C.ops.wire_pack(raw, w, rid_bits, key_shift, segs)
+    assert host_wire.numel() == sum((c + 63) // 64 * w for _, c, _ in segs)
+    back = torch.full_like(raw, -1)
+    C.ops.wire_unpack(host_wire, back, w, rid_bits, key_shift, segs)
+    mask = back != -1
+    assert mask.sum() == sum(c for _, c, _ in segs)
+    assert torch.equal(back[mask], raw[mask])
+    if dev == "cuda":
+        dwire = C.ops.wire_pack(raw.cuda(), w, rid_bits, key_shift, segs)
+        assert torch.equal(dwire.cpu(), host_wire)
+        dback = torch.full_like(raw, -1).cuda()
+        C.ops.wire_unpack(dwire, dback, w, rid_bits, key_shift, segs)
+        assert torch.equal(dback.cpu(), back)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run the per-phase micro-benchmarks on cuda:0 and print one JSON line each.
 
-    python tools/microbench.py [copy|host_link|partition|local|bp|npj|ablation|all] [--n N] [--bits B]
+    python tools/microbench.py [copy|host_link|partition|local|bp|npj|wire|ablation|all] [--n N] [--bits B]
 """
 import argparse
 import json
@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--bits", type=int, default=10)
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()
-    todo = ["copy", "host_link", "partition", "local", "bp", "npj"] if a.what == "all" else [a.what]
+    todo = ["copy", "host_link", "partition", "local", "bp", "npj", "wire"] if a.what == "all" else [a.what]
     for w in todo:
         if w == "copy":
             r = mb.copy_ceiling()
@@ -36,6 +36,8 @@ def main():
             for r in mb.scatter_ablation(a.n, (8, 9, 10, 11), a.iters, geometries=(0, 3, 6, 7, 8, 9)):
                 print(json.dumps({"bench": "scatter_ablation", **r}), flush=True)
             continue
+        elif w == "wire":
+            r = mb.wire_phase(a.n, iters=a.iters)
         elif w == "npj":
             r = mb.npj_phase(min(a.n, 1 << 26), iters=a.iters)
         else:
