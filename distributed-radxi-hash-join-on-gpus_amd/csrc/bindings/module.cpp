@@ -599,6 +599,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("local_histogram", &core::JoinConfig::localHistogram)
       .def_readwrite("sample_stride", &core::JoinConfig::sampleStride)
       .def_readwrite("wire_codec", &core::JoinConfig::wireCodec)
+      .def_readwrite("split_local", &core::JoinConfig::splitLocal)
+      .def_readwrite("direct_count", &core::JoinConfig::directCount)
       .def_readwrite("output_capacity", &core::JoinConfig::outputCapacity)
       .def_readwrite("build_target", &core::JoinConfig::buildTarget)
       .def_readwrite("r_chunk", &core::JoinConfig::rChunk)
@@ -617,6 +619,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("key_shift", &core::JoinPlan::keyShift)
       .def_readonly("frag_shift", &core::JoinPlan::fragShift)
       .def_readonly("key_bits", &core::JoinPlan::keyBits)
+      .def_readonly("split_local", &core::JoinPlan::splitLocal)
       .def_property_readonly("wire_bits", [](const core::JoinPlan &p) {
         return std::vector<uint32_t>{p.wireBits[0], p.wireBits[1]};
       })

@@ -18,10 +18,12 @@ std::string JoinConfig::describe() const {
 
 std::string JoinPlan::describe() const {
   return utils::format("JoinPlan(nodes=%u networkBits=%u localBits=%u twoLevel=%d keyShift=%u fragShift=%u "
-                       "rChunk=%u sChunk=%u chunks=%u wide=%d materialize=%d keyMix=%d sampled=%d assignment=%s wire=%u/%u)",
+                       "rChunk=%u sChunk=%u chunks=%u wide=%d materialize=%d keyMix=%d sampled=%d assignment=%s wire=%u/%u "
+                       "split=%d)",
                        numberOfNodes, networkBits, localBits, (int)twoLevel, keyShift, fragShift, rChunk, sChunk,
                        chunks, (int)wide, (int)materialize, (int)keyMix, (int)sampledNetwork,
-                       assignment == AssignmentPolicy::LPT ? "lpt" : "round_robin", wireBits[0], wireBits[1]);
+                       assignment == AssignmentPolicy::LPT ? "lpt" : "round_robin", wireBits[0], wireBits[1],
+                       (int)splitLocal);
 }
 
 JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t globalInner, uint64_t globalOuter,
@@ -31,6 +33,7 @@ JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t global
   p.twoLevel = cfg.twoLevel;
   p.wide = cfg.format == TupleFormat::Wide;
   p.materialize = cfg.materialize;
+  p.directCount = cfg.directCount;
   p.assignment = cfg.assignment;
   p.chunks = std::max<uint32_t>(1, cfg.chunks);
   p.localHistogram = cfg.localHistogram;
@@ -74,6 +77,8 @@ JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t global
   } else {
     p.keyShift = cfg.keyShift ? cfg.keyShift : std::max<uint32_t>(32, ridBits);
     JOIN_ASSERT(ridBits <= p.keyShift, "Plan", "rids need %u bits but keyShift=%u", ridBits, p.keyShift);
+    JOIN_ASSERT(p.keyShift >= 32, "Plan", "keyShift=%u: the rid field of a CompressedTuple is at least 32 bits",
+                p.keyShift);
     const uint32_t keyHighBits = keyBits > p.networkBits ? keyBits - p.networkBits : 0;
     JOIN_ASSERT(keyHighBits <= 64 - p.keyShift, "Plan",
                 "keys need %u bits: %u above the %u network bits do not fit the %u bits of a CompressedTuple above "
@@ -83,6 +88,12 @@ JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t global
     // The LDS table uses 0xFFFFFFFF as its empty marker: fragments must stay below it.
     JOIN_ASSERT(keyHighBits <= 31 + (p.twoLevel ? p.localBits : 0), "Plan",
                 "key fragment (%u bits) would reach the LDS empty marker 0xFFFFFFFF", keyHighBits);
+  }
+
+  if (!p.wide && p.twoLevel) {
+    const uint32_t passBits = p.networkBits + p.localBits;
+    const uint32_t fragBits = p.keyBits > passBits ? p.keyBits - passBits : 0;
+    p.splitLocal = cfg.splitLocal && ridBits <= 32 && fragBits <= 16;
   }
 
   // LDS budget: a 32 KiB table (counting, 4-byte fragments) lets 5 workgroups

@@ -72,6 +72,8 @@ struct JoinConfig {
   HistogramMode localHistogram = HistogramMode::Auto;
   uint32_t sampleStride = 16;   // sampled passes: histogram 1 tile in sampleStride
   WireCodecMode wireCodec = WireCodecMode::Auto;
+  bool splitLocal = true;       // device: split local pass output (u32 rid + u16 fragment columns) when they fit
+  bool directCount = true;      // count-only build/probe: direct-addressed LDS counts when fragments are <= 13 bits
 
   std::string describe() const;
 };
@@ -97,6 +99,8 @@ struct JoinPlan {
   AssignmentPolicy assignment = AssignmentPolicy::LPT;
   // Wire codec per relation (0 = inner, 1 = outer): bits per tuple (0 = off),
   // rid bits, and every rank's rid base.  Set by HashJoin::planWireCodec.
+  bool splitLocal = false;    // local pass writes split columns (kernels.h, SplitLayout)
+  bool directCount = true;    // build/probe may use direct-addressed count tables
   uint32_t wireBits[2] = {0, 0};
   uint32_t wireRidBits[2] = {0, 0};
   std::vector<uint64_t> ridBase[2];

@@ -155,7 +155,8 @@ void Window::stop() {
 
 void Window::flush() { stop(); }
 
-void Window::setPartitioned(void *p, const uint64_t *pb, uint32_t bits, const uint64_t *pe) {
+void Window::setPartitioned(void *p, const uint64_t *pb, uint32_t bits, const uint64_t *pe, uint16_t *hi) {
+  partitionedHi = hi;
   partitioned = p;
   partBegin = pb;
   partEnd = pe;
@@ -173,6 +174,7 @@ CompressedTuple *Window::getPartition(uint32_t partitionId) {
   const int32_t lp = plan.localIndex.at(partitionId);
   JOIN_ASSERT(lp >= 0, "Window", "partition %u is not owned by node %u", partitionId, plan.nodeId);
   JOIN_ASSERT(!partEnd, "Window", "gapped local output: use getPartitionBegin/getPartitionEnd");
+  JOIN_ASSERT(!partitionedHi, "Window", "split local output: use getPartitionedData / getPartitionedHi");
   void *base = partitioned ? partitioned : (plan.windowIsPartitionMajor() ? data : nullptr);
   JOIN_ASSERT(base, "Window", "partition-major view requires local partitioning first");
   return static_cast<CompressedTuple *>(base) + plan.lpBase[lp];

@@ -61,8 +61,11 @@ class Window {
   const histograms::ExchangePlan &getPlan() const { return plan; }
   // Local partitioning hands back its partition-major output.
   // partEnd: null when partitions are contiguous (end of p = partBegin[p + 1]).
+  // hi: the fragment column of the split layout (kernels.h, SplitLayout);
+  // partitioned is then the u32 rid column.
   void setPartitioned(void *partitioned, const uint64_t *partBegin, uint32_t localBits,
-                      const uint64_t *partEnd = nullptr);
+                      const uint64_t *partEnd = nullptr, uint16_t *hi = nullptr);
+  const uint16_t *getPartitionedHi() const { return partitionedHi; }  // null unless split
   void *getPartitionedData() const { return partitioned; }
   const uint64_t *getPartitionBegin() const { return partBegin; }  // [owned * 2^localBits + 1] (ctx location)
   const uint64_t *getPartitionEnd() const { return partEnd; }      // null, or [owned * 2^localBits] (gapped)
@@ -92,6 +95,7 @@ class Window {
   const uint64_t *partBegin = nullptr;
   const uint64_t *partEnd = nullptr;
   uint32_t localBits = 0;
+  uint16_t *partitionedHi = nullptr;
 };
 
 }  // namespace data

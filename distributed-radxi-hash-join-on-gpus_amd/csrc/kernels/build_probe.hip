@@ -46,7 +46,19 @@ static size_t bpEntryBytes(int mode) {
   }
 }
 
+// Direct-addressed counting: a final partition's fragments span at most
+// 2^fragBits values, so with fragBits <= 13 (8192 x 4 B = 32 KiB, the hash
+// table's own budget) counts[fragment] replaces hashing: one LDS atomic add
+// per inner tuple, one LDS read per outer tuple, no probe chains, duplicates
+// on either side counted exactly.  1B unique keys after 9 + 9 radix bits
+// leave 12 fragment bits.
+constexpr uint32_t BP_DIRECT_MAX_BITS = 13;
+static bool bpDirect(const BPArgs &a) {
+  return bpMode(a) == BP_CCOUNT && a.fragBits > 0 && a.fragBits <= BP_DIRECT_MAX_BITS;
+}
+
 size_t bpLdsBytes(const BPArgs &a) {
+  if (bpDirect(a)) return (size_t(4) << a.fragBits) + 64;
   const uint64_t slots = uint64_t(1) << ceilLog2(2ull * a.rChunk);
   return slots * bpEntryBytes(bpMode(a)) + 64;
 }
@@ -145,6 +157,33 @@ __device__ __forceinline__ void bpLoad(const V *__restrict__ src, uint32_t n, ui
   }
 }
 
+// One batch of an item's side into registers.  Counting keeps only the 32-bit
+// key fragment per tuple (half the registers of the 8-byte value, so 16
+// loads per lane stay in flight without scratch spills); materializing keeps
+// the whole tuple.  Sources: 8-byte / 16-byte tuples, or the local pass's
+// split columns (kernels.h, SplitLayout), where counting reads only the
+// 2-byte fragment column.
+template <int MODE, bool SPLIT, typename L, bool FULL>
+__device__ __forceinline__ void bpLoadSide(const void *__restrict__ src, const uint16_t *__restrict__ hi,
+                                           uint64_t off, uint32_t n, uint32_t b0, const BPArgs &a, L (&v)[BP_K]) {
+#pragma unroll
+  for (int k = 0; k < BP_K; ++k) {
+    const uint32_t idx = b0 + k * BPT + threadIdx.x;
+    if (FULL || idx < n) {
+      if constexpr (MODE == BP_CCOUNT) {
+        if constexpr (SPLIT)
+          v[k] = hi[off + idx];
+        else  // fragShift >= keyShift >= 32: the fragment lies in the tuple's high dword
+          v[k] = reinterpret_cast<const uint32_t *>(src)[2 * (off + idx) + 1] >> (a.fragShift - 32);
+      } else if constexpr (SPLIT) {
+        v[k] = (uint64_t)reinterpret_cast<const uint32_t *>(src)[off + idx] | ((uint64_t)hi[off + idx] << a.fragShift);
+      } else {
+        v[k] = reinterpret_cast<const L *>(src)[off + idx];
+      }
+    }
+  }
+}
+
 // ITEMS: count pre-pass of a two-pass materialization (per-item match counts);
 // a separate instantiation so the count-only production kernel is unchanged.
 // Occupancy is LDS-bound: 4-byte count tables (32 KiB) fit 4 workgroups per
@@ -154,7 +193,7 @@ __device__ __forceinline__ void bpLoad(const V *__restrict__ src, uint32_t n, ui
 template <int MODE, bool ITEMS>
 constexpr int bpMinBlocks() { return MODE == 0 ? (ITEMS ? 3 : 4) : 2; }
 
-template <int MODE, bool ITEMS = false>
+template <int MODE, bool ITEMS = false, bool SPLIT = false, bool DIRECT = false>
 __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeKernel(BPArgs a, const BPItem *__restrict__ items,
                                                         const uint32_t *__restrict__ nItemsPtr, uint32_t capacity) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -163,15 +202,16 @@ __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeK
   using Entry = typename std::conditional<MODE == BP_CCOUNT, uint32_t, unsigned long long>::type;
   using V = typename std::conditional<WIDE, ulonglong2, uint64_t>::type;
   constexpr uint32_t BATCH = BPT * BP_K;
-  const uint64_t maxSlots = uint64_t(1) << ceilLog2(2ull * a.rChunk);
+  const uint64_t maxSlots = DIRECT ? (uint64_t(1) << a.fragBits) : (uint64_t(1) << ceilLog2(2ull * a.rChunk));
   Entry *table = reinterpret_cast<Entry *>(smem);
   unsigned long long *ridTable = reinterpret_cast<unsigned long long *>(smem) + maxSlots;  // WMAT only
   constexpr size_t EB = MODE == BP_CCOUNT ? 4 : (MODE == BP_WMAT ? 16 : 8);
   unsigned long long *wsum = reinterpret_cast<unsigned long long *>(smem + maxSlots * EB);
   const uint32_t t = threadIdx.x;
   const uint64_t ridMask = a.keyShift >= 64 ? ~0ull : ((1ull << a.keyShift) - 1);
-  const V *R = reinterpret_cast<const V *>(a.R);
-  const V *S = reinterpret_cast<const V *>(a.S);
+  static_assert(!(SPLIT && WIDE), "the split layout holds compressed tuples");
+  static_assert(!DIRECT || MODE == BP_CCOUNT, "direct-addressed tables count only");
+  using L = typename std::conditional<MODE == BP_CCOUNT, uint32_t, V>::type;  // register-held element
   uint64_t matches = 0;
   const uint32_t nItems = min(*nItemsPtr, capacity);
   __shared__ uint32_t itemCursorLds;
@@ -185,8 +225,8 @@ __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeK
     const uint64_t sb = a.partS[it.part] + (uint64_t)it.sChunk * a.sChunk;
     const uint64_t se = min(a.partSEnd[it.part], sb + a.sChunk);
     const uint32_t nr = (uint32_t)(re - rb), ns = (uint32_t)(se - sb);
-    uint32_t tbits = ceilLog2(2ull * nr);
-    if (tbits < 6) tbits = 6;
+    uint32_t tbits = DIRECT ? a.fragBits : ceilLog2(2ull * nr);
+    if (!DIRECT && tbits < 6) tbits = 6;
     const uint32_t slots = 1u << tbits, mask = slots - 1;
     unsigned long long itemBase = 0;
     if constexpr (MAT) {
@@ -198,30 +238,32 @@ __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeK
     const uint64_t matchesBefore = matches;
 
     // First inner batch and first outer batch are in flight while the table is cleared.
-    V rv[BP_K], sv[BP_K];
-    if (nr >= BATCH) bpLoad<V, true>(R + rb, nr, 0, rv);
-    else bpLoad<V, false>(R + rb, nr, 0, rv);
-    if (ns >= BATCH) bpLoad<V, true>(S + sb, ns, 0, sv);
-    else bpLoad<V, false>(S + sb, ns, 0, sv);
-    for (uint32_t i = t; i < slots; i += BPT) table[i] = (Entry)(MODE == BP_CCOUNT ? EMPTY32 : EMPTY64);
+    L rv[BP_K], sv[BP_K];
+    if (nr >= BATCH) bpLoadSide<MODE, SPLIT, L, true>(a.R, a.Rhi, rb, nr, 0, a, rv);
+    else bpLoadSide<MODE, SPLIT, L, false>(a.R, a.Rhi, rb, nr, 0, a, rv);
+    if (ns >= BATCH) bpLoadSide<MODE, SPLIT, L, true>(a.S, a.Shi, sb, ns, 0, a, sv);
+    else bpLoadSide<MODE, SPLIT, L, false>(a.S, a.Shi, sb, ns, 0, a, sv);
+    for (uint32_t i = t; i < slots; i += BPT) table[i] = DIRECT ? (Entry)0 : (Entry)(MODE == BP_CCOUNT ? EMPTY32 : EMPTY64);
     __syncthreads();
 
     // ---- build
     for (uint32_t b0 = 0; b0 < nr; b0 += BATCH) {
-      if (b0) bpLoad<V, false>(R + rb, nr, b0, rv);
+      if (b0) bpLoadSide<MODE, SPLIT, L, false>(a.R, a.Rhi, rb, nr, b0, a, rv);
 #pragma unroll
       for (int k = 0; k < BP_K; ++k) {
         const uint32_t idx = b0 + k * BPT + t;
         if (idx < nr) {
-          if constexpr (!WIDE) {
+          if constexpr (DIRECT) {
+            atomicAdd(&table[rv[k]], 1u);
+          } else if constexpr (MODE == BP_CCOUNT) {
+            const uint32_t frag = rv[k];
+            uint32_t h = hash32(frag, tbits);
+            while (atomicCAS(&table[h], EMPTY32, frag) != EMPTY32) h = (h + 1) & mask;
+          } else if constexpr (!WIDE) {
             const uint64_t v = rv[k];
             const uint32_t frag = (uint32_t)(v >> a.fragShift);
             uint32_t h = hash32(frag, tbits);
-            if constexpr (MODE == BP_CCOUNT) {
-              while (atomicCAS(&table[h], EMPTY32, frag) != EMPTY32) h = (h + 1) & mask;
-            } else {
-              while (atomicCAS(&table[h], EMPTY64, (unsigned long long)v) != EMPTY64) h = (h + 1) & mask;
-            }
+            while (atomicCAS(&table[h], EMPTY64, (unsigned long long)v) != EMPTY64) h = (h + 1) & mask;
           } else {
             const ulonglong2 v = rv[k];
             uint32_t h = hash64(v.x, tbits);
@@ -236,8 +278,8 @@ __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeK
     // ---- probe
     for (uint32_t b0 = 0; b0 < ns; b0 += BATCH) {
       if (b0) {
-        if (b0 + BATCH <= ns) bpLoad<V, true>(S + sb, ns, b0, sv);
-        else bpLoad<V, false>(S + sb, ns, b0, sv);
+        if (b0 + BATCH <= ns) bpLoadSide<MODE, SPLIT, L, true>(a.S, a.Shi, sb, ns, b0, a, sv);
+        else bpLoadSide<MODE, SPLIT, L, false>(a.S, a.Shi, sb, ns, b0, a, sv);
       }
 #pragma unroll
       for (int k = 0; k < BP_K; ++k) {
@@ -246,17 +288,21 @@ __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeK
         uint32_t found = 0;
         uint64_t m0 = 0, m1 = 0, sRid = 0;
         if (active) {
-          if constexpr (!WIDE) {
+          if constexpr (DIRECT) {
+            found = table[sv[k]];
+          } else if constexpr (MODE == BP_CCOUNT) {
+            const uint32_t frag = sv[k];
+            uint32_t h = hash32(frag, tbits);
+            uint32_t e;
+            while ((e = table[h]) != EMPTY32) {
+              found += (e == frag);
+              h = (h + 1) & mask;
+            }
+          } else if constexpr (!WIDE) {
             const uint64_t v = sv[k];
             const uint32_t frag = (uint32_t)(v >> a.fragShift);
             uint32_t h = hash32(frag, tbits);
-            if constexpr (MODE == BP_CCOUNT) {
-              uint32_t e;
-              while ((e = table[h]) != EMPTY32) {
-                found += (e == frag);
-                h = (h + 1) & mask;
-              }
-            } else {
+            {
               sRid = v & ridMask;
               unsigned long long e;
               while ((e = table[h]) != EMPTY64) {
@@ -319,14 +365,35 @@ void buildProbe(const BPArgs &args, const BPItem *items, const uint32_t *nItems,
   const uint32_t perCu = (uint32_t)((160 * 1024) / lds);
   const uint32_t maxBlocks = 256 * (perCu < 8 ? (perCu ? perCu : 1) : 8);
   const uint32_t blocks = capacity < maxBlocks ? capacity : maxBlocks;
+  HJ_CHECK(!(a.split && a.wide), "buildProbe: the split layout holds compressed tuples");
+  HJ_CHECK(!a.split || (a.Rhi && a.Shi), "buildProbe: split layout without fragment columns");
+  HJ_CHECK(a.wide || a.fragShift >= 32, "buildProbe: fragShift=%u < 32 (the rid field of a CompressedTuple is >= 32 bits)",
+           a.fragShift);
+  if (bpMode(a) == BP_CCOUNT) {
+    // Count-only instantiations: per-item counts (two-pass materialization's
+    // count pass) x split columns x direct-addressed table.
+#define HJ_BP_COUNT(ITEMS, SPLIT, DIRECT)                                                                         \
+  hipLaunchKernelGGL((buildProbeKernel<BP_CCOUNT, ITEMS, SPLIT, DIRECT>), dim3(blocks), dim3(BPT), lds, s, a, items, \
+                     nItems, capacity)
+    const bool direct = bpDirect(a), it = a.itemCounts != nullptr, sp = a.split != 0;
+    if (it) {
+      if (sp) { if (direct) HJ_BP_COUNT(true, true, true); else HJ_BP_COUNT(true, true, false); }
+      else { if (direct) HJ_BP_COUNT(true, false, true); else HJ_BP_COUNT(true, false, false); }
+    } else {
+      if (sp) { if (direct) HJ_BP_COUNT(false, true, true); else HJ_BP_COUNT(false, true, false); }
+      else { if (direct) HJ_BP_COUNT(false, false, true); else HJ_BP_COUNT(false, false, false); }
+    }
+#undef HJ_BP_COUNT
+    HIP_CHECK_LAUNCH();
+    return;
+  }
+  if (a.split) {  // materialize
+    hipLaunchKernelGGL((buildProbeKernel<BP_CMAT, false, true>), dim3(blocks), dim3(BPT), lds, s, a, items, nItems,
+                       capacity);
+    HIP_CHECK_LAUNCH();
+    return;
+  }
   switch (bpMode(a)) {
-    case BP_CCOUNT:
-      if (a.itemCounts)
-        hipLaunchKernelGGL((buildProbeKernel<BP_CCOUNT, true>), dim3(blocks), dim3(BPT), lds, s, a, items, nItems,
-                           capacity);
-      else
-        hipLaunchKernelGGL(buildProbeKernel<BP_CCOUNT>, dim3(blocks), dim3(BPT), lds, s, a, items, nItems, capacity);
-      break;
     case BP_CMAT:
       hipLaunchKernelGGL(buildProbeKernel<BP_CMAT>, dim3(blocks), dim3(BPT), lds, s, a, items, nItems, capacity);
       break;

@@ -158,8 +158,27 @@ void localHistogram(const void *in, bool wide, const LocalItem *items, uint32_t 
 void localCursors(const uint32_t *itemHist, const uint32_t *lpItemBegin, uint32_t owned, uint32_t bits,
                   const uint64_t *lpBase, const LocalItem *items, void *gcur, bool narrow, uint64_t *partBegin,
                   hipStream_t s);
+// Split (SoA) tuples of the local pass output (device, compressed format),
+// the columnar layout of the reference's dormant GPU library (relation_t
+// {key*, id*}, /root/reference/data/data.hpp:57-62): after both radix passes
+// a final partition implies networkBits + localBits key bits, so a tuple is
+// its rid (u32 column) plus the key fragment above fragShift (u16 column) --
+// 6 bytes instead of 8, and a count-only build/probe reads just the 2-byte
+// fragment column.  Both columns are unit-stride in every scatter run and
+// every build/probe batch.
+struct SplitLayout {
+  uint32_t on = 0;
+  uint32_t fragShift = 32;   // CompressedTuple fragment position (value >> fragShift)
+  uint16_t *hi = nullptr;    // fragment column (element i <-> lo[i])
+  HJ_HD uint64_t value(uint32_t rid, uint16_t frag) const { return (uint64_t)rid | ((uint64_t)frag << fragShift); }
+};
+constexpr uint32_t SPLIT_BYTES = 6;
+
+// split.on (compressed input only): out is the u32 rid column, split.hi the
+// u16 fragment column (kernels.h, SplitLayout).
 void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift,
-                  uint32_t bits, void *gcur, bool narrow, void *out, hipStream_t s, const void *gend = nullptr);
+                  uint32_t bits, void *gcur, bool narrow, void *out, hipStream_t s, const void *gend = nullptr,
+                  SplitLayout split = SplitLayout());
 // Sampled local pass (no exact local histogram): itemHist from
 // localHistogram(sampleStride) -> per-final-partition capacities (estimate +
 // 6 sigma + 2% + 64) -> gapped partition-major layout: gcur = partBegin =
@@ -168,9 +187,12 @@ void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nI
 void localSampledLayout(const uint32_t *itemHist, const uint32_t *lpItemBegin, const LocalItem *items,
                         uint32_t owned, uint32_t bits, uint32_t sampleStride, uint32_t *caps,
                         unsigned long long *starts, void *scanWorkspace, unsigned long long *gcur,
-                        unsigned long long *gend, uint64_t *partBegin, uint64_t capacity, hipStream_t s);
+                        unsigned long long *gend, uint64_t *partBegin, uint64_t capacity, hipStream_t s,
+                        uint32_t align = 16);
 // Upper bound of the layout's total capacity (host-side sizing of the output).
-uint64_t localSampledCapacityBound(uint64_t n, uint64_t partitions, uint32_t sampleStride);
+// align: slot granularity in tuples (16 = 128-byte lines of 8-byte tuples,
+// 64 = whole lines of both split columns).
+uint64_t localSampledCapacityBound(uint64_t n, uint64_t partitions, uint32_t sampleStride, uint32_t align = 16);
 // *flag |= 1 if any gcur[i] > gend[i] (a bounded claim slice overflowed);
 // gcur is clamped to gend, so it is always safe to use as partition ends.
 void claimOverflow(unsigned long long *gcur, const unsigned long long *gend, uint64_t P, unsigned int *flag,
@@ -196,8 +218,17 @@ struct BPArgs {
   uint32_t sChunk = 65536;  // max outer tuples per work item
   uint32_t fragShift = 0;   // compressed: key fragment = value >> fragShift
   uint32_t keyShift = 32;   // compressed: rid = value & (2^keyShift - 1)
+  // Compressed: fragments are < 2^fragBits (0 = unknown).  Counting with
+  // fragBits <= BP_DIRECT_MAX_BITS uses a direct-addressed LDS count array
+  // (counts[fragment]) instead of a hash table.
+  uint32_t fragBits = 0;
   bool wide = false;
   bool materialize = false;
+  // Split layout (on = 1): R and S are u32 rid columns, Rhi / Shi the u16
+  // fragment columns (kernels.h, SplitLayout).
+  uint32_t split = 0;
+  const uint16_t *Rhi = nullptr;
+  const uint16_t *Shi = nullptr;
   unsigned long long *result = nullptr;     // match counter (device)
   unsigned long long *outCursor = nullptr;  // materialize: pair cursor (device)
   ulonglong2 *outPairs = nullptr;           // materialize: (rid_inner, rid_outer)

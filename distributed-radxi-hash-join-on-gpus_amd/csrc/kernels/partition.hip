@@ -249,6 +249,7 @@ struct NetCompressedPol {  // 16 B tuple -> 8 B CompressedTuple, digit in the to
   }
   __device__ __forceinline__ uint32_t stagedDigit(const StageT &v) const { return (uint32_t)(v >> (64 - bits)); }
   __device__ __forceinline__ OutT out(const StageT &v) const { return v & (~0ull >> bits); }
+  __device__ __forceinline__ void store(OutT *o, uint64_t pos, const StageT &v) const { o[pos] = out(v); }
 };
 struct NetCompressedDigPol : NetCompressedPol {  // no spare bits: digits staged separately
   static constexpr bool kDigArray = true;
@@ -256,6 +257,7 @@ struct NetCompressedDigPol : NetCompressedPol {  // no spare bits: digits staged
     return x.y | ((mix.apply(x.x) >> bits) << keyShift);
   }
   __device__ __forceinline__ OutT out(const StageT &v) const { return v; }
+  __device__ __forceinline__ void store(OutT *o, uint64_t pos, const StageT &v) const { o[pos] = out(v); }
 };
 struct NetWidePol {  // 16 B tuple -> 16 B tuple (full-range keys)
   using InT = ulonglong2;
@@ -270,6 +272,7 @@ struct NetWidePol {  // 16 B tuple -> 16 B tuple (full-range keys)
   }
   __device__ __forceinline__ uint32_t stagedDigit(const StageT &v) const { return (uint32_t)(v.x & mask); }
   __device__ __forceinline__ OutT out(const StageT &v) const { return v; }
+  __device__ __forceinline__ void store(OutT *o, uint64_t pos, const StageT &v) const { o[pos] = out(v); }
 };
 struct LocalCompressedPol {  // 8 B -> 8 B, digit = (value >> shift) & mask
   using InT = uint64_t;
@@ -282,6 +285,7 @@ struct LocalCompressedPol {  // 8 B -> 8 B, digit = (value >> shift) & mask
   __device__ __forceinline__ StageT stage(const InT &x, uint32_t) const { return x; }
   __device__ __forceinline__ uint32_t stagedDigit(const StageT &v) const { return digit(v); }
   __device__ __forceinline__ OutT out(const StageT &v) const { return v; }
+  __device__ __forceinline__ void store(OutT *o, uint64_t pos, const StageT &v) const { o[pos] = out(v); }
 };
 struct LocalWidePol {  // 16 B -> 16 B, digit = (key >> shift) & mask
   using InT = ulonglong2;
@@ -294,6 +298,16 @@ struct LocalWidePol {  // 16 B -> 16 B, digit = (key >> shift) & mask
   __device__ __forceinline__ StageT stage(const InT &x, uint32_t) const { return x; }
   __device__ __forceinline__ uint32_t stagedDigit(const StageT &v) const { return digit(v); }
   __device__ __forceinline__ OutT out(const StageT &v) const { return v; }
+  __device__ __forceinline__ void store(OutT *o, uint64_t pos, const StageT &v) const { o[pos] = out(v); }
+};
+struct LocalSplitPol : LocalCompressedPol {  // 8 B -> u32 rid + u16 fragment (kernels.h, SplitLayout)
+  using OutT = uint32_t;
+  uint16_t *hi;
+  uint32_t fragShift;
+  __device__ __forceinline__ void store(OutT *o, uint64_t pos, const StageT &v) const {
+    o[pos] = (uint32_t)v;
+    hi[pos] = (uint16_t)(v >> fragShift);
+  }
 };
 
 // LDS per workgroup: cursor and wbase (F x CurT), cnt and off (F x u32), scan
@@ -420,9 +434,9 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
       if constexpr (MODE == 0) {
         const CurT pos = (CurT)(l.wbase[d] + (CurT)idx);
         if constexpr (BOUNDED) {
-          if (pos < l.cursor[d]) out[(uint64_t)pos] = pol.out(x);
+          if (pos < l.cursor[d]) pol.store(out, (uint64_t)pos, x);
         } else {
-          out[(uint64_t)pos] = pol.out(x);
+          pol.store(out, (uint64_t)pos, x);
         }
       } else if constexpr (MODE == 1) {
         out[base + idx] = pol.out(x);
@@ -812,7 +826,7 @@ __device__ __forceinline__ uint32_t sampledLen(uint32_t len, uint32_t stride) {
 __global__ __launch_bounds__(NT) void localCapacityKernel(const uint32_t *__restrict__ itemHist,
                                                           const uint32_t *__restrict__ lpItemBegin,
                                                           const LocalItem *__restrict__ items, uint32_t bits,
-                                                          uint32_t stride, uint32_t *__restrict__ caps) {
+                                                          uint32_t stride, uint32_t align, uint32_t *__restrict__ caps) {
   const uint32_t F = 1u << bits, lp = blockIdx.x;
   const uint32_t ib = lpItemBegin[lp], ie = lpItemBegin[lp + 1];
   double len = 0, seen = 0;
@@ -828,11 +842,12 @@ __global__ __launch_bounds__(NT) void localCapacityKernel(const uint32_t *__rest
       if (s) est += (double)itemHist[(uint64_t)it * F + q] * ((double)items[it].len / s);
     }
     const double cap = est + 6.0 * sqrt(fmax(est, 1.0) * scale) + 0.02 * est + 64.0;
-    // Whole 128-byte lines per slot: partitions never share a cache line, so
-    // the scatter's partial lines at slot edges are not split across XCDs and
-    // every build/probe read starts line-aligned.
+    // Whole 128-byte lines per slot (align = 16 tuples of 8 bytes, or 64 of
+    // 6 bytes): partitions never share a cache line, so the scatter's partial
+    // lines at slot edges are not split across XCDs and every build/probe read
+    // starts line-aligned.
     const uint32_t c = (uint32_t)min(ceil(cap), 4294967040.0);
-    caps[(uint64_t)lp * F + q] = (c + 15u) & ~15u;
+    caps[(uint64_t)lp * F + q] = (c + align - 1) / align * align;
   }
 }
 
@@ -876,11 +891,13 @@ __global__ __launch_bounds__(NT) void claimOverflowKernel(unsigned long long *__
 void localSampledLayout(const uint32_t *itemHist, const uint32_t *lpItemBegin, const LocalItem *items,
                         uint32_t owned, uint32_t bits, uint32_t sampleStride, uint32_t *caps,
                         unsigned long long *starts, void *scanWorkspace, unsigned long long *gcur,
-                        unsigned long long *gend, uint64_t *partBegin, uint64_t capacity, hipStream_t s) {
+                        unsigned long long *gend, uint64_t *partBegin, uint64_t capacity, hipStream_t s,
+                        uint32_t align) {
   if (owned == 0) return;
+  HJ_CHECK(align >= 1 && align <= 256, "localSampledLayout: align=%u", align);
   const uint64_t P = (uint64_t)owned << bits;
   hipLaunchKernelGGL(localCapacityKernel, dim3(owned), dim3(NT), 0, s, itemHist, lpItemBegin, items, bits,
-                     sampleStride, caps);
+                     sampleStride, align, caps);
   HIP_CHECK_LAUNCH();
   scanExclusiveU32to64(caps, starts, P, nullptr, scanWorkspace, s);
   const uint32_t grid = (uint32_t)std::min<uint64_t>(ceilDiv(P, NT), 4096);
@@ -889,14 +906,14 @@ void localSampledLayout(const uint32_t *itemHist, const uint32_t *lpItemBegin, c
   HIP_CHECK_LAUNCH();
 }
 
-uint64_t localSampledCapacityBound(uint64_t n, uint64_t partitions, uint32_t sampleStride) {
+uint64_t localSampledCapacityBound(uint64_t n, uint64_t partitions, uint32_t sampleStride, uint32_t align) {
   // Sum of the per-partition capacities: estimates sum to n; by Cauchy-Schwarz
   // the 6-sigma terms sum to at most 6 sqrt(n * S * P); +81 per partition for
   // the constant, the ceil and float rounding.
   // (an item's len/seen ratio is at most ~sampleStride; +1 covers the rounding)
   const double bound = 1.02 * (double)n +
                        6.0 * std::sqrt(((double)n + (double)partitions) * (sampleStride + 1.0) * (double)partitions) +
-                       81.0 * (double)partitions;  // 64 + ceil + 15 of line rounding + float slack
+                       (66.0 + align) * (double)partitions;  // 64 + ceil + line rounding + float slack
   return (uint64_t)(bound * 1.001) + 1024;
 }
 
@@ -928,8 +945,17 @@ __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void localScatterClaim
                                                       gcur + (uint64_t)it.stream * F);
 }
 
+template <class P>
+static void setSplit(P &, const SplitLayout &) {}
+static void setSplit(LocalSplitPol &p, const SplitLayout &sl) {
+  p.hi = sl.hi;
+  p.fragShift = sl.fragShift;
+}
+
 void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift, uint32_t bits,
-                  void *gcur, bool narrow, void *out, hipStream_t s, const void *gend) {
+                  void *gcur, bool narrow, void *out, hipStream_t s, const void *gend, SplitLayout split) {
+  HJ_CHECK(!(wide && split.on), "localScatter: the split layout needs compressed input");
+  HJ_CHECK(!split.on || split.hi, "localScatter: split layout without a fragment column");
   HJ_CHECK(bits <= MAX_PART_BITS, "localScatter: bits=%u out of range", bits);
   if (nItems == 0) return;
   const uint32_t F = 1u << bits;
@@ -940,6 +966,7 @@ void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nI
     P pol;                                                                                                    \
     pol.mask = mask;                                                                                          \
     pol.shift = shift;                                                                                        \
+    setSplit(pol, split);                                                                                     \
     const size_t lds = ScatterLayout<P, C, CL_NTH * CL_IPT>::bytes(F);                                         \
     if (gend)                                                                                                 \
       hipLaunchKernelGGL((localScatterClaimKernel<P, C, CL_NTH, CL_IPT, true>), dim3(grid), dim3(CL_NTH), lds, \
@@ -953,6 +980,8 @@ void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nI
   } while (0)
   if (wide && narrow) HJ_LOCAL(LocalWidePol, uint32_t);
   else if (wide) HJ_LOCAL(LocalWidePol, unsigned long long);
+  else if (split.on && narrow) HJ_LOCAL(LocalSplitPol, uint32_t);
+  else if (split.on) HJ_LOCAL(LocalSplitPol, unsigned long long);
   else if (narrow) HJ_LOCAL(LocalCompressedPol, uint32_t);
   else HJ_LOCAL(LocalCompressedPol, unsigned long long);
 #undef HJ_LOCAL

@@ -101,7 +101,10 @@ void HashJoin::makeJoinPlan() {
                         mx[1]);
   planWireCodec(all, STATS);
   if (config.keyHashing == core::KeyHashing::Auto && plan.keyBits < 64) plan.keyMix = lowKeyBitsSkewed();
-  if (!ctx->onDevice()) plan.localHistogram = core::HistogramMode::Exact;  // sampling pays on HBM only
+  if (!ctx->onDevice()) {
+    plan.localHistogram = core::HistogramMode::Exact;  // sampling pays on HBM only
+    plan.splitLocal = false;                           // split columns are a device layout
+  }
   {
     const bool eligible = numberOfNodes == 1 && ctx->onDevice() && plan.chunks == 1;
     const uint64_t small = std::min(innerRelation->getGlobalSize(), outerRelation->getGlobalSize());

@@ -1,5 +1,6 @@
 #include "BuildProbe.h"
 
+#include <algorithm>
 #include <cstring>
 
 #include "../host/HostOps.h"
@@ -50,8 +51,18 @@ void BuildProbe::configure() {
   args.sChunk = plan.sChunk;
   args.fragShift = plan.wide ? 64 : plan.keyShift + wi->getLocalBits();
   args.keyShift = plan.keyShift;
+  if (!plan.wide && plan.directCount) {  // fragments are < 2^fragBits (direct-addressed counting when small)
+    const uint32_t passBits = plan.networkBits + wi->getLocalBits();
+    args.fragBits = plan.keyBits > passBits ? std::min<uint32_t>(32, plan.keyBits - passBits) : 1;
+  }
   args.wide = plan.wide;
   args.materialize = plan.materialize;
+  if (wi->getPartitionedHi()) {
+    JOIN_ASSERT(wo->getPartitionedHi(), "BuildProbe", "one side split, the other not");
+    args.split = 1;
+    args.Rhi = wi->getPartitionedHi();
+    args.Shi = wo->getPartitionedHi();
+  }
   if (capacity == 0)
     capacity = (uint32_t)std::min<uint64_t>(
         0xFFFFFFF0ull, 2ull * args.P + outerPartitionSize / args.sChunk + innerPartitionSize / args.rChunk + 1024);

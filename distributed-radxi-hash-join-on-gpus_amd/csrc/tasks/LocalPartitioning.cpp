@@ -59,6 +59,12 @@ void LocalPartitioning::partition(data::Window *w, int which) {
   lb[owned] = (uint32_t)it.size();
   const uint32_t nItems = (uint32_t)it.size();
   const uint32_t shift = wide ? plan.networkBits : plan.keyShift;
+  // Split output columns (kernels.h, SplitLayout): device, compressed, planned to fit.
+  kernels::SplitLayout split;
+  split.on = ctx->onDevice() && !wide && plan.splitLocal ? 1u : 0u;
+  split.fragShift = plan.fragShift;
+  const uint32_t ob = split.on ? 4 : tb;       // bytes per tuple of the main output column
+  const uint32_t align = split.on ? 64 : 16;   // slot granularity: whole 128-byte lines of every column
 
   uint32_t *itemHist = ctx->workspace().getArray<uint32_t>(std::max<uint64_t>(1, (uint64_t)nItems * F));
 
@@ -73,8 +79,9 @@ void LocalPartitioning::partition(data::Window *w, int which) {
     for (auto &x : it) x.stream = x.lp;
     const uint64_t P = (uint64_t)owned * F;
     const uint32_t S = plan.sampleStride;
-    const uint64_t cap = kernels::localSampledCapacityBound(xp.recvTotal, P, S);
-    void *sout = ctx->workspace().get(std::max<uint64_t>(cap, 1) * tb);
+    const uint64_t cap = kernels::localSampledCapacityBound(xp.recvTotal, P, S, align);
+    void *sout = ctx->workspace().get(std::max<uint64_t>(cap, 1) * ob);
+    if (split.on) split.hi = ctx->workspace().getArray<uint16_t>(std::max<uint64_t>(cap, 1));
     uint32_t *caps = ctx->workspace().getArray<uint32_t>(std::max<uint64_t>(P, 1));
     auto *starts = ctx->workspace().getArray<unsigned long long>(std::max<uint64_t>(P, 1));
     void *scanWs = ctx->workspace().get(kernels::scanWorkspaceBytes(std::max<uint64_t>(P, 1)));
@@ -91,14 +98,16 @@ void LocalPartitioning::partition(data::Window *w, int which) {
     }
     kernels::localHistogram(w->getData(), wide, dItems, nItems, shift, bits, itemHist, ctx->stream(), S);
     kernels::localSampledLayout(itemHist, dLb, dItems, owned, bits, S, caps, starts, scanWs, gcur, gend, pbeg, cap,
-                                ctx->stream());
-    kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, gcur, false, sout, ctx->stream(), gend);
+                                ctx->stream(), align);
+    kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, gcur, false, sout, ctx->stream(), gend,
+                          split);
     kernels::claimOverflow(gcur, gend, P, overflowFlag, ctx->stream());
     // Final claim cursors are the partition ends (valid when no slot overflowed).
-    w->setPartitioned(sout, pbeg, bits, reinterpret_cast<const uint64_t *>(gcur));
+    w->setPartitioned(sout, pbeg, bits, reinterpret_cast<const uint64_t *>(gcur), split.hi);
     return;
   }
-  void *out = ctx->workspace().get(std::max<uint64_t>(xp.recvTotal, 1) * tb);
+  void *out = ctx->workspace().get(std::max<uint64_t>(xp.recvTotal, 1) * ob);
+  if (split.on) split.hi = ctx->workspace().getArray<uint16_t>(std::max<uint64_t>(xp.recvTotal, 1));
   uint64_t *partBegin = ctx->workspace().getArray<uint64_t>((uint64_t)owned * F + 1);
   if (ctx->onDevice()) {
     const uint32_t streams = kernels::assignLocalStreams(it.data(), nItems);
@@ -116,7 +125,8 @@ void LocalPartitioning::partition(data::Window *w, int which) {
     }
     kernels::localHistogram(w->getData(), wide, dItems, nItems, shift, bits, itemHist, ctx->stream());
     kernels::localCursors(itemHist, dLb, owned, bits, dBase, dItems, gcur, narrow, partBegin, ctx->stream());
-    kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, gcur, narrow, out, ctx->stream());
+    kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, gcur, narrow, out, ctx->stream(), nullptr,
+                          split);
   } else {
     uint64_t *itemCursors = ctx->workspace().getArray<uint64_t>(std::max<uint64_t>(1, (uint64_t)nItems * F));
     if (owned == 0) partBegin[0] = 0;
@@ -124,7 +134,7 @@ void LocalPartitioning::partition(data::Window *w, int which) {
     host::localCursors(itemHist, lb.data(), owned, bits, xp.lpBase.data(), itemCursors, partBegin);
     host::localScatter(w->getData(), wide, it.data(), nItems, shift, bits, itemCursors, out);
   }
-  w->setPartitioned(out, partBegin, bits);
+  w->setPartitioned(out, partBegin, bits, nullptr, split.hi);
 }
 
 }  // namespace tasks

@@ -252,3 +252,44 @@ def test_sampled_local_overflow_falls_back(C, cuda):
     assert res["global_matches"] == n
     res = j.run()
     assert res["local_fallbacks"] == 0 and not res["sampled_local"] and res["global_matches"] == n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sampled", [True, False])
+@pytest.mark.parametrize("G", [1 << 22, 20_000_003])
+def test_split_local_output(C, cuda, sampled, G):
+    """Split local pass output (u32 rid + u16 fragment columns): same counts
+    and the same materialized pairs as the 8-byte layout, exact and sampled
+    local passes, skewed outer side."""
+    import torch
+    out = {}
+    for narrow in (True, False):
+        cfg = C.JoinConfig()
+        cfg.split_local = narrow
+        cfg.materialize = True
+        cfg.local_histogram = C.HistogramMode.SAMPLED if sampled else C.HistogramMode.EXACT
+        res, exp, j = run_join(C, "cuda", G, G + 12345, "ZIPF", cfg=cfg, theta=0.6)
+        assert j.plan.split_local == narrow
+        assert res["global_matches"] == exp and res["local_fallbacks"] == 0
+        p = j.output()
+        out[narrow] = p[torch.argsort(p[:, 1] * (1 << 32) + p[:, 0])]
+    assert torch.equal(out[True], out[False])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dist", ["UNIQUE", "ZIPF", "MODULO"])
+@pytest.mark.parametrize("split", [True, False])
+def test_direct_count_table(C, cuda, dist, split):
+    """Count-only build/probe with direct-addressed LDS counts (fragments of at
+    most 13 bits) equals the hash-table path, duplicates on both sides included."""
+    counts = {}
+    for direct in (True, False):
+        cfg = C.JoinConfig()
+        cfg.direct_count = direct
+        cfg.split_local = split
+        G = 6_000_011
+        res, exp, j = run_join(C, "cuda", G, G + 777, dist, cfg=cfg, theta=0.9)
+        assert j.plan.key_bits - j.plan.network_bits - j.plan.local_bits <= 13
+        assert res["global_matches"] == exp
+        counts[direct] = res["global_matches"]
+    assert counts[True] == counts[False]
