@@ -601,6 +601,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("wire_codec", &core::JoinConfig::wireCodec)
       .def_readwrite("split_local", &core::JoinConfig::splitLocal)
       .def_readwrite("direct_count", &core::JoinConfig::directCount)
+      .def_readwrite("local_item_tiles", &core::JoinConfig::localItemTiles)
+      .def_readwrite("local_geometry", &core::JoinConfig::localGeometry)
+      .def_readwrite("local_sample_stride", &core::JoinConfig::localSampleStride)
       .def_readwrite("output_capacity", &core::JoinConfig::outputCapacity)
       .def_readwrite("build_target", &core::JoinConfig::buildTarget)
       .def_readwrite("r_chunk", &core::JoinConfig::rChunk)

@@ -34,10 +34,13 @@ JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t global
   p.wide = cfg.format == TupleFormat::Wide;
   p.materialize = cfg.materialize;
   p.directCount = cfg.directCount;
+  p.localItemTiles = std::max<uint32_t>(1, std::min<uint32_t>(cfg.localItemTiles, 1024));
+  p.localGeometry = cfg.localGeometry;
   p.assignment = cfg.assignment;
   p.chunks = std::max<uint32_t>(1, cfg.chunks);
   p.localHistogram = cfg.localHistogram;
   p.sampleStride = std::max<uint32_t>(1, cfg.sampleStride);
+  p.localSampleStride = std::max<uint32_t>(1, cfg.localSampleStride);
   p.sChunk = std::max<uint32_t>(1024, cfg.sChunk);
 
   const uint32_t maxBits = Configuration::GPU_MAX_FANOUT_BITS - 1;  // 1024-way per pass

@@ -70,10 +70,13 @@ struct JoinConfig {
   KeyHashing keyHashing = KeyHashing::Auto;
   HistogramMode networkHistogram = HistogramMode::Auto;
   HistogramMode localHistogram = HistogramMode::Auto;
-  uint32_t sampleStride = 16;   // sampled passes: histogram 1 tile in sampleStride
+  uint32_t sampleStride = 64;   // sampled network pass: histogram 1 tile in sampleStride (per-slot counts ~1e5+)
+  uint32_t localSampleStride = 16;  // sampled local pass: 1 tile in localSampleStride of every work item
   WireCodecMode wireCodec = WireCodecMode::Auto;
   bool splitLocal = true;       // device: split local pass output (u32 rid + u16 fragment columns) when they fit
   bool directCount = true;      // count-only build/probe: direct-addressed LDS counts when fragments are <= 13 bits
+  uint32_t localItemTiles = 64; // local pass work item: up to this many 4096-tuple tiles of one segment
+  uint32_t localGeometry = 0;   // local scatter workgroup geometry (0 = 1024 x 8; 1-4: sweep alternatives)
 
   std::string describe() const;
 };
@@ -95,12 +98,15 @@ struct JoinPlan {
   bool keyMix = false;        // radix digits from kernels::KeyMix{keyBits} of the key
   bool sampledNetwork = false;  // single-rank network pass sized from a sampled histogram
   HistogramMode localHistogram = HistogramMode::Exact;  // resolved per window size by LocalPartitioning
-  uint32_t sampleStride = 16;
+  uint32_t sampleStride = 64;
+  uint32_t localSampleStride = 16;
   AssignmentPolicy assignment = AssignmentPolicy::LPT;
   // Wire codec per relation (0 = inner, 1 = outer): bits per tuple (0 = off),
   // rid bits, and every rank's rid base.  Set by HashJoin::planWireCodec.
   bool splitLocal = false;    // local pass writes split columns (kernels.h, SplitLayout)
   bool directCount = true;    // build/probe may use direct-addressed count tables
+  uint32_t localItemTiles = 64;
+  uint32_t localGeometry = 0;
   uint32_t wireBits[2] = {0, 0};
   uint32_t wireRidBits[2] = {0, 0};
   std::vector<uint64_t> ridBase[2];

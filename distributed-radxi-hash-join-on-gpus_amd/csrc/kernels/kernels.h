@@ -178,7 +178,7 @@ constexpr uint32_t SPLIT_BYTES = 6;
 // u16 fragment column (kernels.h, SplitLayout).
 void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift,
                   uint32_t bits, void *gcur, bool narrow, void *out, hipStream_t s, const void *gend = nullptr,
-                  SplitLayout split = SplitLayout());
+                  SplitLayout split = SplitLayout(), uint32_t geometry = 0);
 // Sampled local pass (no exact local histogram): itemHist from
 // localHistogram(sampleStride) -> per-final-partition capacities (estimate +
 // 6 sigma + 2% + 64) -> gapped partition-major layout: gcur = partBegin =

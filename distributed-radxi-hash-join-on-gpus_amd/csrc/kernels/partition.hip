@@ -952,8 +952,23 @@ static void setSplit(LocalSplitPol &p, const SplitLayout &sl) {
   p.fragShift = sl.fragShift;
 }
 
+// Alternative workgroup geometries of the production local scatter (split
+// output, 64-bit cursors, bounded slots) for the geometry sweep.
+template <int NTH, int IPT>
+static void launchLocalSplitGeom(const void *in, const LocalItem *items, uint32_t nItems, uint32_t F,
+                                 const LocalSplitPol &pol, void *gcur, void *out, const void *gend, hipStream_t s) {
+  const size_t lds = ScatterLayout<LocalSplitPol, unsigned long long, NTH * IPT>::bytes(F);
+  HJ_CHECK(lds <= 160 * 1024, "local scatter LDS %zu too large", lds);
+  const uint32_t grid = ((nItems + NGROUPS - 1) / NGROUPS) * NGROUPS;
+  hipLaunchKernelGGL((localScatterClaimKernel<LocalSplitPol, unsigned long long, NTH, IPT, true>), dim3(grid),
+                     dim3(NTH), lds, s, reinterpret_cast<const uint64_t *>(in), items, nItems, F, pol,
+                     reinterpret_cast<unsigned long long *>(gcur), reinterpret_cast<uint32_t *>(out),
+                     reinterpret_cast<const unsigned long long *>(gend));
+}
+
 void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift, uint32_t bits,
-                  void *gcur, bool narrow, void *out, hipStream_t s, const void *gend, SplitLayout split) {
+                  void *gcur, bool narrow, void *out, hipStream_t s, const void *gend, SplitLayout split,
+                  uint32_t geometry) {
   HJ_CHECK(!(wide && split.on), "localScatter: the split layout needs compressed input");
   HJ_CHECK(!split.on || split.hi, "localScatter: split layout without a fragment column");
   HJ_CHECK(bits <= MAX_PART_BITS, "localScatter: bits=%u out of range", bits);
@@ -961,6 +976,20 @@ void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nI
   const uint32_t F = 1u << bits;
   const uint64_t mask = F - 1;
   const uint32_t grid = ((nItems + NGROUPS - 1) / NGROUPS) * NGROUPS;
+  if (geometry != 0 && split.on && !wide && !narrow && gend) {
+    LocalSplitPol pol;
+    pol.mask = mask;
+    pol.shift = shift;
+    setSplit(pol, split);
+    switch (geometry) {
+      case 1: launchLocalSplitGeom<512, 8>(in, items, nItems, F, pol, gcur, out, gend, s); break;
+      case 2: launchLocalSplitGeom<512, 16>(in, items, nItems, F, pol, gcur, out, gend, s); break;
+      case 3: launchLocalSplitGeom<256, 16>(in, items, nItems, F, pol, gcur, out, gend, s); break;
+      default: launchLocalSplitGeom<1024, 16>(in, items, nItems, F, pol, gcur, out, gend, s); break;
+    }
+    HIP_CHECK_LAUNCH();
+    return;
+  }
 #define HJ_LOCAL(P, C)                                                                                        \
   do {                                                                                                        \
     P pol;                                                                                                    \

@@ -48,11 +48,12 @@ void LocalPartitioning::partition(data::Window *w, int which) {
   it.clear();
   lb.assign(owned + 1, 0);
   size_t seg = 0;
+  const uint64_t itemMax = (uint64_t)plan.localItemTiles * kernels::PART_TILE;
   for (uint32_t lp = 0; lp < owned; ++lp) {
     lb[lp] = (uint32_t)it.size();
     for (; seg < xp.segments.size() && xp.segments[seg].lp == lp; ++seg)
-      for (uint64_t off = 0; off < xp.segments[seg].len; off += kernels::LOCAL_ITEM_MAX) {
-        const uint64_t len = std::min<uint64_t>(kernels::LOCAL_ITEM_MAX, xp.segments[seg].len - off);
+      for (uint64_t off = 0; off < xp.segments[seg].len; off += itemMax) {
+        const uint64_t len = std::min<uint64_t>(itemMax, xp.segments[seg].len - off);
         it.push_back(kernels::LocalItem{xp.segments[seg].begin + off, (uint32_t)len, lp, 0, 0});
       }
   }
@@ -78,7 +79,7 @@ void LocalPartitioning::partition(data::Window *w, int which) {
     // except at group boundaries), so every final partition is one slot.
     for (auto &x : it) x.stream = x.lp;
     const uint64_t P = (uint64_t)owned * F;
-    const uint32_t S = plan.sampleStride;
+    const uint32_t S = plan.localSampleStride;
     const uint64_t cap = kernels::localSampledCapacityBound(xp.recvTotal, P, S, align);
     void *sout = ctx->workspace().get(std::max<uint64_t>(cap, 1) * ob);
     if (split.on) split.hi = ctx->workspace().getArray<uint16_t>(std::max<uint64_t>(cap, 1));
@@ -100,7 +101,7 @@ void LocalPartitioning::partition(data::Window *w, int which) {
     kernels::localSampledLayout(itemHist, dLb, dItems, owned, bits, S, caps, starts, scanWs, gcur, gend, pbeg, cap,
                                 ctx->stream(), align);
     kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, gcur, false, sout, ctx->stream(), gend,
-                          split);
+                          split, plan.localGeometry);
     kernels::claimOverflow(gcur, gend, P, overflowFlag, ctx->stream());
     // Final claim cursors are the partition ends (valid when no slot overflowed).
     w->setPartitioned(sout, pbeg, bits, reinterpret_cast<const uint64_t *>(gcur), split.hi);

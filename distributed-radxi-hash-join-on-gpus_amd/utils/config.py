@@ -7,7 +7,9 @@ import os
 from .._native import require_native
 
 _FIELDS = ["network_bits", "local_bits", "two_level", "key_shift", "materialize", "output_capacity", "build_target",
-           "r_chunk", "s_chunk", "chunks", "checks", "max_partition_blocks", "sample_stride"]
+           "r_chunk", "s_chunk", "chunks", "checks", "max_partition_blocks", "sample_stride", "local_sample_stride", "local_item_tiles", "local_geometry",
+           "split_local", "direct_count"]
+_BOOLS = ("two_level", "materialize", "checks", "split_local", "direct_count")
 
 
 def config_to_dict(cfg) -> dict:
@@ -17,6 +19,7 @@ def config_to_dict(cfg) -> dict:
     d["key_hashing"] = str(cfg.key_hashing).split(".")[-1]
     d["network_histogram"] = str(cfg.network_histogram).split(".")[-1]
     d["local_histogram"] = str(cfg.local_histogram).split(".")[-1]
+    d["wire_codec"] = str(cfg.wire_codec).split(".")[-1]
     return d
 
 
@@ -25,7 +28,7 @@ def config_from_dict(d: dict | None = None, env_prefix: str = "HPCJOIN_"):
     C = require_native()
     cfg = C.JoinConfig()
     merged = dict(d or {})
-    for f in _FIELDS + ["assignment", "format", "key_hashing", "network_histogram", "local_histogram"]:
+    for f in _FIELDS + ["assignment", "format", "key_hashing", "network_histogram", "local_histogram", "wire_codec"]:
         v = os.environ.get(env_prefix + f.upper())
         if v is not None:
             merged[f] = v
@@ -38,8 +41,10 @@ def config_from_dict(d: dict | None = None, env_prefix: str = "HPCJOIN_"):
             cfg.key_hashing = getattr(C.KeyHashing, str(v).upper())
         elif k in ("network_histogram", "local_histogram"):
             setattr(cfg, k, getattr(C.HistogramMode, str(v).upper()))
-        elif k in ("two_level", "materialize", "checks"):
+        elif k in _BOOLS:
             setattr(cfg, k, v if isinstance(v, bool) else str(v).lower() in ("1", "true", "yes"))
+        elif k == "wire_codec":
+            cfg.wire_codec = getattr(C.WireCodecMode, str(v).upper())
         elif k in _FIELDS:
             setattr(cfg, k, int(v))
         else:
