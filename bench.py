@@ -132,6 +132,9 @@ def main():
             "correct": correct,
             "phases_ms": phases,
             "engine": {"reruns": results[-1]["reruns"], "build_probe_items": results[-1]["build_probe_items"],
+                       "network_fallbacks": sum(r["network_fallbacks"] for r in results),
+                       "local_fallbacks": sum(r["local_fallbacks"] for r in results),
+                       "wire_bytes": results[-1]["wire_bytes"],
                        "local_items": results[-1]["local_items"], "workspace_GB": round(ctx.workspace_capacity() / 1e9, 2),
                        "workspace_peak_GB": round(ctx.workspace_peak() / 1e9, 2),
                        "step_ms": [round(r["join_ms"], 2) for r in results],

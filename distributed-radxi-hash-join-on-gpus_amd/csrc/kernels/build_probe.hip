@@ -184,6 +184,91 @@ __device__ __forceinline__ void bpLoadSide(const void *__restrict__ src, const u
   }
 }
 
+// Production count kernel of the split layout with direct-addressed tables:
+// the fragment column is read as aligned 8-byte words (4 fragments each, one
+// 512-byte request per wave instruction instead of 128 bytes), elements
+// outside [begin, end) of a word are masked, and only a 32-bit fragment
+// array lives in registers: 5 workgroups (20 wave64s) per CU at 81 VGPRs,
+// no scratch (8 per CU would cap VGPRs at 64 and spill).
+constexpr int BPD_T = 256;
+constexpr int BPD_K = 8;  // words per lane per batch: 8192 fragments per workgroup batch
+
+template <bool FULL>
+__device__ __forceinline__ void bpdLoad(const uint64_t *__restrict__ w, uint32_t nw, uint32_t b0,
+                                        uint64_t (&v)[BPD_K]) {
+#pragma unroll
+  for (int k = 0; k < BPD_K; ++k) {
+    const uint32_t idx = b0 + k * BPD_T + threadIdx.x;
+    if (FULL || idx < nw) v[k] = w[idx];
+  }
+}
+
+__global__ __launch_bounds__(BPD_T, 5) void bpDirectSplitKernel(BPArgs a, const BPItem *__restrict__ items,
+                                                                 const uint32_t *__restrict__ nItemsPtr,
+                                                                 uint32_t capacity) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(smem);
+  const uint32_t slots = 1u << a.fragBits;
+  unsigned long long *wsum = reinterpret_cast<unsigned long long *>(smem + ((size_t)slots * 4 + 15) / 16 * 16);
+  const uint64_t *R64 = reinterpret_cast<const uint64_t *>(a.Rhi);
+  const uint64_t *S64 = reinterpret_cast<const uint64_t *>(a.Shi);
+  constexpr uint32_t WB = BPD_T * BPD_K;  // words per batch
+  const uint32_t t = threadIdx.x;
+  const uint32_t nItems = min(*nItemsPtr, capacity);
+  uint64_t matches = 0;
+  for (uint32_t w = blockIdx.x; w < nItems; w += gridDim.x) {
+    const BPItem it = items[w];
+    const uint64_t rb = a.partR[it.part] + (uint64_t)it.rChunk * a.rChunk;
+    const uint64_t re = min(a.partREnd[it.part], rb + a.rChunk);
+    const uint64_t sb = a.partS[it.part] + (uint64_t)it.sChunk * a.sChunk;
+    const uint64_t se = min(a.partSEnd[it.part], sb + a.sChunk);
+    // Aligned word ranges covering [rb, re) and [sb, se).
+    const uint64_t rw0 = rb >> 2, sw0 = sb >> 2;
+    const uint32_t rnw = re > rb ? (uint32_t)(((re + 3) >> 2) - rw0) : 0;
+    const uint32_t snw = se > sb ? (uint32_t)(((se + 3) >> 2) - sw0) : 0;
+    uint64_t rv[BPD_K], sv[BPD_K];
+    if (rnw >= WB) bpdLoad<true>(R64 + rw0, rnw, 0, rv);
+    else bpdLoad<false>(R64 + rw0, rnw, 0, rv);
+    if (snw >= WB) bpdLoad<true>(S64 + sw0, snw, 0, sv);
+    else bpdLoad<false>(S64 + sw0, snw, 0, sv);
+    for (uint32_t i = t; i < slots; i += BPD_T) cnt[i] = 0;
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < rnw; b0 += WB) {
+      if (b0) bpdLoad<false>(R64 + rw0, rnw, b0, rv);
+#pragma unroll
+      for (int k = 0; k < BPD_K; ++k) {
+        const uint32_t idx = b0 + k * BPD_T + t;
+        if (idx < rnw) {
+          const uint64_t e0 = (rw0 + idx) << 2;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (e0 + j >= rb && e0 + j < re) atomicAdd(&cnt[(uint32_t)(rv[k] >> (16 * j)) & 0xFFFFu], 1u);
+        }
+      }
+    }
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < snw; b0 += WB) {
+      if (b0) {
+        if (b0 + WB <= snw) bpdLoad<true>(S64 + sw0, snw, b0, sv);
+        else bpdLoad<false>(S64 + sw0, snw, b0, sv);
+      }
+#pragma unroll
+      for (int k = 0; k < BPD_K; ++k) {
+        const uint32_t idx = b0 + k * BPD_T + t;
+        if (idx < snw) {
+          const uint64_t e0 = (sw0 + idx) << 2;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (e0 + j >= sb && e0 + j < se) matches += cnt[(uint32_t)(sv[k] >> (16 * j)) & 0xFFFFu];
+        }
+      }
+    }
+    __syncthreads();  // the next item clears the table
+  }
+  const unsigned long long total = blockReduceSum<BPD_T, unsigned long long>((unsigned long long)matches, wsum);
+  if (t == 0 && total) atomicAdd(a.result, total);
+}
+
 // ITEMS: count pre-pass of a two-pass materialization (per-item match counts);
 // a separate instantiation so the count-only production kernel is unchanged.
 // Occupancy is LDS-bound: 4-byte count tables (32 KiB) fit 4 workgroups per
@@ -369,6 +454,14 @@ void buildProbe(const BPArgs &args, const BPItem *items, const uint32_t *nItems,
   HJ_CHECK(!a.split || (a.Rhi && a.Shi), "buildProbe: split layout without fragment columns");
   HJ_CHECK(a.wide || a.fragShift >= 32, "buildProbe: fragShift=%u < 32 (the rid field of a CompressedTuple is >= 32 bits)",
            a.fragShift);
+  if (bpMode(a) == BP_CCOUNT && a.split && bpDirect(a) && !a.itemCounts) {
+    const size_t ldsD = ((size_t(4) << a.fragBits) + 15) / 16 * 16 + 64;
+    const uint32_t perCuD = (uint32_t)std::min<size_t>(5, (160 * 1024) / ldsD);  // the kernel's occupancy target
+    const uint32_t blocksD = std::min<uint32_t>(capacity, 256 * std::max<uint32_t>(perCuD, 1));
+    hipLaunchKernelGGL(bpDirectSplitKernel, dim3(blocksD), dim3(BPD_T), ldsD, s, a, items, nItems, capacity);
+    HIP_CHECK_LAUNCH();
+    return;
+  }
   if (bpMode(a) == BP_CCOUNT) {
     // Count-only instantiations: per-item counts (two-pass materialization's
     // count pass) x split columns x direct-addressed table.
