@@ -32,6 +32,7 @@ struct Case {
   kernels::KeyDistribution outer;
   bool wide, materialize, tpch;
   core::KeyHashing hashing;
+  bool wire = false;  // bit-packed exchange (host twin of kernels/wire.hip)
 };
 
 bool runCase(const Case &c, uint32_t ranks, uint64_t G) {
@@ -59,6 +60,7 @@ bool runCase(const Case &c, uint32_t ranks, uint64_t G) {
       cfg.materialize = c.materialize;
       cfg.keyHashing = c.hashing;
       cfg.chunks = 2;
+      cfg.wireCodec = c.wire ? core::WireCodecMode::On : core::WireCodecMode::Off;
       operators::HashJoin j(&R, &S, &ctx, cfg);
       operators::JoinResult res = j.run();
       matches[r] = res.globalMatches;
@@ -157,6 +159,8 @@ int main(int argc, char **argv) {
       {"wide_materialize", kernels::KeyDistribution::Uniform, true, true, false, core::KeyHashing::Auto},
       {"tpch_materialize", kernels::KeyDistribution::Modulo, false, true, true, core::KeyHashing::Auto},
       {"mix_on_wide", kernels::KeyDistribution::Modulo, true, false, false, core::KeyHashing::On},
+      {"wire_zipf", kernels::KeyDistribution::Zipf, false, false, false, core::KeyHashing::Auto, true},
+      {"wire_tpch_materialize", kernels::KeyDistribution::Modulo, false, true, true, core::KeyHashing::Auto, true},
   };
   bool ok = true;
   for (const Case &c : cases) ok = runCase(c, ranks, G) && ok;
