@@ -102,7 +102,8 @@ struct JoinPlan {
   uint32_t localSampleStride = 16;
   AssignmentPolicy assignment = AssignmentPolicy::LPT;
   // Wire codec per relation (0 = inner, 1 = outer): bits per tuple (0 = off),
-  // rid bits, and every rank's rid base.  Set by HashJoin::planWireCodec.
+  // rid bits, and the rid base of every (rank, exchange chunk), rank-major.
+  // Set by HashJoin::planWireCodec.
   bool splitLocal = false;    // local pass writes split columns (kernels.h, SplitLayout)
   bool directCount = true;    // build/probe may use direct-addressed count tables
   uint32_t localItemTiles = 64;

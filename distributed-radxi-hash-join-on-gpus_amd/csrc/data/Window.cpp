@@ -42,9 +42,12 @@ Window::~Window() {
 
 void Window::setWireCodec(const kernels::WireCodec &c, const std::vector<uint64_t> &bases) {
   JOIN_ASSERT(!wide || c.w == 0, "Window", "the wire codec packs 8-byte CompressedTuples only");
-  JOIN_ASSERT(c.w == 0 || bases.size() == plan.numberOfNodes, "Window", "need one rid base per rank");
+  JOIN_ASSERT(c.w == 0 || (bases.size() >= plan.numberOfNodes && bases.size() % plan.numberOfNodes == 0 &&
+                            bases.size() / plan.numberOfNodes >= plan.chunks),
+              "Window", "need one rid base per (rank, chunk)");
   codec = c;
   ridBase = bases;
+  ridBaseChunks = c.w ? (uint32_t)(bases.size() / plan.numberOfNodes) : 1;
   if (codec.w && ctx->onDevice() && plan.numberOfNodes > 1 && wired.empty()) {
     wired.resize(plan.chunks);
     for (auto &e : wired) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -68,12 +71,14 @@ void Window::exchangePacked(const uint64_t *send, uint32_t chunk) {
   for (uint32_t p = 0; p < N; ++p) {
     if (p == me) continue;
     const uint64_t n = plan.sendCounts[(size_t)chunk * N + p], m = plan.recvCounts[(size_t)chunk * N + p];
-    if (n) ss.push_back({plan.sendDispls[(size_t)chunk * N + p], sOff, n, ridBase[me], sGroups});
+    if (n) ss.push_back({plan.sendDispls[(size_t)chunk * N + p], sOff, n, ridBase[(size_t)me * ridBaseChunks + chunk],
+                         sGroups});
     sc[p] = codec.words(n);
     sd[p] = sOff;
     sOff += sc[p];
     sGroups += ceilDiv(n, 64);
-    if (m) rs.push_back({plan.recvDispls[(size_t)chunk * N + p], rOff, m, ridBase[p], rGroups});
+    if (m) rs.push_back({plan.recvDispls[(size_t)chunk * N + p], rOff, m, ridBase[(size_t)p * ridBaseChunks + chunk],
+                         rGroups});
     rc[p] = codec.words(m);
     rd[p] = rOff;
     rOff += rc[p];

@@ -42,8 +42,9 @@ class Window {
   // Enqueue the all-to-allv of one chunk once the compute stream reaches this
   // point (the chunk's scatter kernel is already enqueued on it).
   void exchange(const void *sendBuffer, uint32_t chunk);
-  // Bit-pack tuples on the wire (kernels.h, WireCodec); ridBase[rank] is each
-  // sender's rid base.  Call before the first exchange.
+  // Bit-pack tuples on the wire (kernels.h, WireCodec); ridBase[rank * C + c]
+  // is the rid base of sender `rank`'s chunk c (C = ridBase.size() / ranks).
+  // Call before the first exchange.
   void setWireCodec(const kernels::WireCodec &codec, const std::vector<uint64_t> &ridBase);
   const kernels::WireCodec &wireCodec() const { return codec; }
   uint64_t wireBytesSent() const { return wireSent * 8; }  // bytes this rank put on the links (all chunks)
@@ -87,6 +88,7 @@ class Window {
   void exchangePacked(const uint64_t *send, uint32_t chunk);
   kernels::WireCodec codec;
   std::vector<uint64_t> ridBase;
+  uint32_t ridBaseChunks = 1;
   // Per-chunk segment lists: kept alive until the join ends (async H2D source).
   std::vector<std::vector<kernels::WireSeg>> sendSegs, recvSegs;
   std::vector<hipEvent_t> wired;  // chunk's all-to-allv done (exchange stream -> decode stream)

@@ -31,6 +31,17 @@ LocalHistogram::LocalHistogram(data::Relation *relation, core::ExecContext *ctx,
 
 LocalHistogram::~LocalHistogram() {}
 
+void LocalHistogram::chunkRange(uint64_t n, uint32_t chunks, uint32_t maxBlocks, uint32_t c, uint64_t *begin,
+                                uint64_t *end) {
+  chunks = std::max<uint32_t>(1, chunks);
+  const kernels::PartitionGeometry g = kernels::partitionGeometry(n, std::max<uint32_t>(maxBlocks, chunks));
+  if (chunks > g.blocks) chunks = g.blocks;
+  const uint64_t bpc = ceilDiv(g.blocks, chunks);
+  const uint64_t per = bpc * g.tuplesPerBlock();
+  *begin = std::min<uint64_t>(n, (uint64_t)c * per);
+  *end = std::min<uint64_t>(n, *begin + per);
+}
+
 void LocalHistogram::computeLocalHistogram() {
   const uint32_t F = 1u << bits;
   values.assign(F, 0);

@@ -27,6 +27,11 @@ class LocalHistogram {
   uint64_t *getLocalHistogram();  // [F], summed over chunks
   uint64_t *getChunkHistograms();  // [chunks][F]
 
+  // Tuple range [begin, end) of exchange chunk c for a relation of n tuples:
+  // the same block split as the constructor's (chunks may shrink for tiny n).
+  static void chunkRange(uint64_t n, uint32_t chunks, uint32_t maxBlocks, uint32_t c, uint64_t *begin,
+                         uint64_t *end);
+
   uint32_t getPartitionBits() const { return bits; }
   uint32_t getPartitionCount() const { return 1u << bits; }
   uint32_t getChunkCount() const { return chunks; }

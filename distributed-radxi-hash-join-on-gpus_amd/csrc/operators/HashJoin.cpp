@@ -62,36 +62,42 @@ void HashJoin::makeJoinPlan() {
   JOIN_ASSERT(usable(innerRelation) && usable(outerRelation), "HashJoin",
               "relations must live where the engine runs (%s) or in pinned host memory", locationName(ctx->location()));
   // Max key / rid over both relations and all ranks (the plan must be identical
-  // everywhere), plus each rank's rid range per relation (wire codec bases).
-  // Per rank: {max key, max rid, min rid inner, max rid inner, min rid outer, max rid outer}.
-  constexpr size_t STATS = 6;
-  uint64_t st[STATS] = {0, 0, ~0ull, 0, ~0ull, 0};
+  // everywhere), plus each rank's rid range per relation and exchange chunk
+  // (wire codec bases).  Per rank: {max key, max rid, then for inner and outer
+  // and every chunk c: min rid, max rid}.
+  const uint32_t C = std::max<uint32_t>(1, config.chunks);
+  const size_t STATS = 2 + 4 * (size_t)C;
+  std::vector<uint64_t> st(STATS, 0);
   int which = 0;
   for (data::Relation *r : {innerRelation, outerRelation}) {
-    uint64_t h[3] = {0, 0, ~0ull};
-    if (ctx->onDevice()) {
-      unsigned long long *d = ctx->workspace().getArray<unsigned long long>(3);
-      HIP_CHECK(hipMemcpyAsync(d, h, 24, hipMemcpyHostToDevice, ctx->stream()));
-      kernels::keyRidMax(r->getData(), r->getLocalSize(), d, ctx->stream());
-      HIP_CHECK(hipMemcpyAsync(h, d, 24, hipMemcpyDeviceToHost, ctx->stream()));
-      HIP_CHECK(hipStreamSynchronize(ctx->stream()));
-    } else {
-      const data::Tuple *t = r->getData();
-      for (uint64_t i = 0; i < r->getLocalSize(); ++i) {
-        h[0] = std::max<uint64_t>(h[0], t[i].key);
-        h[1] = std::max<uint64_t>(h[1], t[i].rid);
-        h[2] = std::min<uint64_t>(h[2], t[i].rid);
+    for (uint32_t c = 0; c < C; ++c) {
+      uint64_t b, e;
+      histograms::LocalHistogram::chunkRange(r->getLocalSize(), C, config.maxPartitionBlocks, c, &b, &e);
+      uint64_t h[3] = {0, 0, ~0ull};
+      if (ctx->onDevice() && e > b) {
+        unsigned long long *d = ctx->workspace().getArray<unsigned long long>(3);
+        HIP_CHECK(hipMemcpyAsync(d, h, 24, hipMemcpyHostToDevice, ctx->stream()));
+        kernels::keyRidMax(r->getData() + b, e - b, d, ctx->stream());
+        HIP_CHECK(hipMemcpyAsync(h, d, 24, hipMemcpyDeviceToHost, ctx->stream()));
+        HIP_CHECK(hipStreamSynchronize(ctx->stream()));
+      } else if (!ctx->onDevice()) {
+        const data::Tuple *t = r->getData();
+        for (uint64_t i = b; i < e; ++i) {
+          h[0] = std::max<uint64_t>(h[0], t[i].key);
+          h[1] = std::max<uint64_t>(h[1], t[i].rid);
+          h[2] = std::min<uint64_t>(h[2], t[i].rid);
+        }
       }
+      st[0] = std::max(st[0], h[0]);
+      st[1] = std::max(st[1], h[1]);
+      st[2 + ((size_t)which * C + c) * 2] = h[2];
+      st[3 + ((size_t)which * C + c) * 2] = h[1];
     }
-    st[0] = std::max(st[0], h[0]);
-    st[1] = std::max(st[1], h[1]);
-    st[2 + 2 * which] = h[2];
-    st[3 + 2 * which] = h[1];
     ++which;
   }
   ctx->workspace().reset();
   std::vector<uint64_t> all(STATS * numberOfNodes);
-  ctx->comm()->allGatherHost(st, all.data(), STATS);
+  ctx->comm()->allGatherHost(st.data(), all.data(), STATS);
   uint64_t mx[2] = {0, 0};
   for (uint32_t r = 0; r < numberOfNodes; ++r) {
     mx[0] = std::max(mx[0], all[STATS * r]);
@@ -99,7 +105,7 @@ void HashJoin::makeJoinPlan() {
   }
   plan = core::makePlan(config, numberOfNodes, innerRelation->getGlobalSize(), outerRelation->getGlobalSize(), mx[0],
                         mx[1]);
-  planWireCodec(all, STATS);
+  planWireCodec(all, STATS, C);
   if (config.keyHashing == core::KeyHashing::Auto && plan.keyBits < 64) plan.keyMix = lowKeyBitsSkewed();
   if (!ctx->onDevice()) {
     plan.localHistogram = core::HistogramMode::Exact;  // sampling pays on HBM only
@@ -119,25 +125,29 @@ void HashJoin::makeJoinPlan() {
 }
 
 // Wire codec per relation (kernels.h, WireCodec): frame-of-reference rids
-// (base = the sending rank's smallest rid) plus the key fragment above the
-// network digit.  Auto packs on a device engine with N > 1 when it saves at
-// least 1/8 of the wire bytes (w <= 56); On forces it (also on the host path).
-void HashJoin::planWireCodec(const std::vector<uint64_t> &all, size_t stride) {
+// (base = the smallest rid of the sending rank's exchange chunk: a chunk is a
+// contiguous quarter of the rank's input, so positional rids need 2 bits less
+// than with one base per rank) plus the key fragment above the network digit.
+// Auto packs on a device engine with N > 1 when it saves at least 1/8 of the
+// wire bytes (w <= 56); On forces it (also on the host path).
+void HashJoin::planWireCodec(const std::vector<uint64_t> &all, size_t stride, uint32_t chunks) {
   for (int r = 0; r < 2; ++r) {
     plan.wireBits[r] = 0;
     plan.wireRidBits[r] = 0;
-    plan.ridBase[r].assign(numberOfNodes, 0);
+    plan.ridBase[r].assign((size_t)numberOfNodes * chunks, 0);
   }
   if (plan.wide || numberOfNodes == 1 || config.wireCodec == core::WireCodecMode::Off) return;
   const uint32_t keyW = plan.keyBits > plan.networkBits ? plan.keyBits - plan.networkBits : 0;
   for (int r = 0; r < 2; ++r) {
     uint64_t span = 1;
-    for (uint32_t n = 0; n < numberOfNodes; ++n) {
-      const uint64_t lo = all[stride * n + 2 + 2 * r], hi = all[stride * n + 3 + 2 * r];
-      if (lo > hi) continue;  // empty slice
-      plan.ridBase[r][n] = lo;
-      span = std::max<uint64_t>(span, hi - lo + 1);
-    }
+    for (uint32_t n = 0; n < numberOfNodes; ++n)
+      for (uint32_t c = 0; c < chunks; ++c) {
+        const size_t at = stride * n + 2 + ((size_t)r * chunks + c) * 2;
+        const uint64_t lo = all[at], hi = all[at + 1];
+        if (lo > hi) continue;  // empty chunk
+        plan.ridBase[r][(size_t)n * chunks + c] = lo;
+        span = std::max<uint64_t>(span, hi - lo + 1);
+      }
     const uint32_t ridBits = std::max<uint32_t>(1, ceilLog2(span));
     const uint32_t w = ridBits + keyW;
     const bool on = config.wireCodec == core::WireCodecMode::On ? w < 64 : (ctx->onDevice() && w <= 56);

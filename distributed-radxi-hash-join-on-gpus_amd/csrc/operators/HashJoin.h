@@ -78,7 +78,7 @@ class HashJoin {
  private:
   void makeJoinPlan();
   bool lowKeyBitsSkewed();
-  void planWireCodec(const std::vector<uint64_t> &rankStats, size_t stride);
+  void planWireCodec(const std::vector<uint64_t> &rankStats, size_t stride, uint32_t chunks);
   JoinResult runImpl();
   core::ExecContext *ctx;
   std::unique_ptr<core::ExecContext> ownedCtx;
