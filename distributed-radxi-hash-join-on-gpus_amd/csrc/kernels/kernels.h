@@ -254,7 +254,8 @@ void buildProbe(const BPArgs &a, const BPItem *items, const uint32_t *nItems, ui
 // tuple needs only its key fragment above the network digit (the receiver
 // knows the partition) and its rid relative to the sending rank's smallest
 // rid (frame of reference): w = ridBits + keyFragmentBits bits, e.g. 48 for
-// 1B unique keys on 8 ranks (21 + 27) instead of 64.  Tuples are bit-packed
+// 1B unique keys on 8 ranks (21 + 25 with one rid base per rank and
+// exchange chunk) instead of 64.  Tuples are bit-packed
 // in groups of 64: a group of a segment occupies w u64 words, lane j of a
 // wave64 writing word j.  The xGMI links are the bottleneck of the
 // distributed join, so this cuts the exchange time by (64 - w) / 64.
