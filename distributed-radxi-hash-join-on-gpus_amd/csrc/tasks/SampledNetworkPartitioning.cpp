@@ -97,21 +97,21 @@ void SampledNetworkPartitioning::layout() {
     const size_t cb = s.narrow ? 4 : 8;
     s.gcur = ctx->workspace().get((size_t)G * F * cb);
     s.gend = ctx->workspace().get((size_t)G * F * cb);
+    // Asynchronous uploads from member vectors (no host round trip before the scatter).
     if (s.narrow) {
-      std::vector<uint32_t> a((size_t)G * F), e((size_t)G * F);
-      for (size_t i = 0; i < a.size(); ++i) {
-        a[i] = (uint32_t)s.start[i];
-        e[i] = (uint32_t)(s.start[i] + s.cap[i]);
+      s.cur32.resize((size_t)G * F);
+      s.end32.resize((size_t)G * F);
+      for (size_t i = 0; i < s.cur32.size(); ++i) {
+        s.cur32[i] = (uint32_t)s.start[i];
+        s.end32[i] = (uint32_t)(s.start[i] + s.cap[i]);
       }
-      HIP_CHECK(hipMemcpyAsync(s.gcur, a.data(), a.size() * 4, hipMemcpyHostToDevice, ctx->stream()));
-      HIP_CHECK(hipMemcpyAsync(s.gend, e.data(), e.size() * 4, hipMemcpyHostToDevice, ctx->stream()));
-      HIP_CHECK(hipStreamSynchronize(ctx->stream()));  // host vectors go out of scope
+      HIP_CHECK(hipMemcpyAsync(s.gcur, s.cur32.data(), s.cur32.size() * 4, hipMemcpyHostToDevice, ctx->stream()));
+      HIP_CHECK(hipMemcpyAsync(s.gend, s.end32.data(), s.end32.size() * 4, hipMemcpyHostToDevice, ctx->stream()));
     } else {
-      std::vector<uint64_t> e((size_t)G * F);
-      for (size_t i = 0; i < e.size(); ++i) e[i] = s.start[i] + s.cap[i];
-      HIP_CHECK(hipMemcpyAsync(s.gcur, s.start.data(), e.size() * 8, hipMemcpyHostToDevice, ctx->stream()));
-      HIP_CHECK(hipMemcpyAsync(s.gend, e.data(), e.size() * 8, hipMemcpyHostToDevice, ctx->stream()));
-      HIP_CHECK(hipStreamSynchronize(ctx->stream()));
+      s.end64.resize((size_t)G * F);
+      for (size_t i = 0; i < s.end64.size(); ++i) s.end64[i] = s.start[i] + s.cap[i];
+      HIP_CHECK(hipMemcpyAsync(s.gcur, s.start.data(), s.end64.size() * 8, hipMemcpyHostToDevice, ctx->stream()));
+      HIP_CHECK(hipMemcpyAsync(s.gend, s.end64.data(), s.end64.size() * 8, hipMemcpyHostToDevice, ctx->stream()));
     }
   }
 }

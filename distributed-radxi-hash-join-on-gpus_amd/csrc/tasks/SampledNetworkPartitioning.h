@@ -53,6 +53,9 @@ class SampledNetworkPartitioning {
     std::vector<uint64_t> sampled;     // [groups][F] sampled counts
     std::vector<uint64_t> start, cap;  // [groups][F] slice start / capacity (tuples)
     std::vector<uint64_t> fill;        // [groups][F] claimed after the scatter
+    // Host sources of the asynchronous cursor uploads (alive until the join ends).
+    std::vector<uint32_t> cur32, end32;
+    std::vector<uint64_t> end64;
     void *gcur = nullptr, *gend = nullptr;
     bool narrow = true;
     uint64_t capacityTotal = 0;
