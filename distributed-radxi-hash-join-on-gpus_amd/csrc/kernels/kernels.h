@@ -181,7 +181,7 @@ void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nI
                   SplitLayout split = SplitLayout(), uint32_t geometry = 0);
 // Sampled local pass (no exact local histogram): itemHist from
 // localHistogram(sampleStride) -> per-final-partition capacities (estimate +
-// 6 sigma + 2% + 64) -> gapped partition-major layout: gcur = partBegin =
+// 8 sigma + 2% + 64) -> gapped partition-major layout: gcur = partBegin =
 // starts, gend = starts + caps (64-bit cursors; one claim stream per lp).
 // After the bounded localScatter the final gcur values are the partition ends.
 void localSampledLayout(const uint32_t *itemHist, const uint32_t *lpItemBegin, const LocalItem *items,

@@ -822,7 +822,13 @@ __device__ __forceinline__ uint32_t sampledLen(uint32_t len, uint32_t stride) {
 }
 
 // One workgroup per owned partition lp: capacity of each final partition
-// (lp, q) = sampled estimate + 6 sigma of the sampling error + 2% + 64.
+// (lp, q) = sampled estimate + LOCAL_SIGMAS sigma of the sampling error + 2% + 64.
+// With ~240 sampled tuples per final partition (1 tile in 16), a low sample
+// shrinks both the estimate and its margin: at 6 sigma a slot overflows with
+// probability ~1e-7 (Poisson lower tail), i.e. a few percent of 1B x 1B joins
+// (2^19 slots) would take the exact re-run; at 8 sigma ~1e-11.  The price is
+// memory only (gaps are never read): ~+15% of the local output allocation.
+constexpr double LOCAL_SIGMAS = 8.0;
 __global__ __launch_bounds__(NT) void localCapacityKernel(const uint32_t *__restrict__ itemHist,
                                                           const uint32_t *__restrict__ lpItemBegin,
                                                           const LocalItem *__restrict__ items, uint32_t bits,
@@ -841,7 +847,7 @@ __global__ __launch_bounds__(NT) void localCapacityKernel(const uint32_t *__rest
       const uint32_t s = sampledLen(items[it].len, stride);
       if (s) est += (double)itemHist[(uint64_t)it * F + q] * ((double)items[it].len / s);
     }
-    const double cap = est + 6.0 * sqrt(fmax(est, 1.0) * scale) + 0.02 * est + 64.0;
+    const double cap = est + LOCAL_SIGMAS * sqrt(fmax(est, 1.0) * scale) + 0.02 * est + 64.0;
     // Whole 128-byte lines per slot (align = 16 tuples of 8 bytes, or 64 of
     // 6 bytes): partitions never share a cache line, so the scatter's partial
     // lines at slot edges are not split across XCDs and every build/probe read
@@ -908,11 +914,11 @@ void localSampledLayout(const uint32_t *itemHist, const uint32_t *lpItemBegin, c
 
 uint64_t localSampledCapacityBound(uint64_t n, uint64_t partitions, uint32_t sampleStride, uint32_t align) {
   // Sum of the per-partition capacities: estimates sum to n; by Cauchy-Schwarz
-  // the 6-sigma terms sum to at most 6 sqrt(n * S * P); +81 per partition for
+  // the sigma terms sum to at most LOCAL_SIGMAS sqrt(n * S * P); + per partition for
   // the constant, the ceil and float rounding.
   // (an item's len/seen ratio is at most ~sampleStride; +1 covers the rounding)
   const double bound = 1.02 * (double)n +
-                       6.0 * std::sqrt(((double)n + (double)partitions) * (sampleStride + 1.0) * (double)partitions) +
+                       LOCAL_SIGMAS * std::sqrt(((double)n + (double)partitions) * (sampleStride + 1.0) * (double)partitions) +
                        (66.0 + align) * (double)partitions;  // 64 + ceil + line rounding + float slack
   return (uint64_t)(bound * 1.001) + 1024;
 }
