@@ -44,7 +44,10 @@ JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t global
   p.sChunk = std::max<uint32_t>(1024, cfg.sChunk);
 
   const uint32_t maxBits = Configuration::GPU_MAX_FANOUT_BITS - 1;  // 1024-way per pass
-  const uint64_t target = std::max<uint64_t>(256, cfg.buildTarget);
+  // Materializing compressed tuples: final partitions of <= 2048 inner tuples
+  // fit one 32 KiB (fragment, rid) table of the split materializing kernel.
+  const bool matNarrow = p.materialize && !p.wide && !cfg.rChunk;
+  const uint64_t target = std::max<uint64_t>(256, matNarrow ? std::min<uint64_t>(cfg.buildTarget, 2048) : cfg.buildTarget);
   const uint32_t totalBits = ceilLog2(ceilDiv(std::max<uint64_t>(globalInner, 1), target));
   // >= 8 network partitions per node so LPT has room to balance.
   const uint32_t minNet = std::max<uint32_t>(4, ceilLog2(numberOfNodes) + 3);
@@ -100,12 +103,13 @@ JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t global
   }
 
   // LDS budget: a 32 KiB table (counting, 4-byte fragments) lets 5 workgroups
-  // (20 wave64s) share a CU; 8- and 16-byte entries get 64 KiB (2 per CU).
+  // (20 wave64s) share a CU; materializing compressed tuples also uses 32 KiB
+  // (4 per CU); wide entries get 64 KiB (2 per CU).
   if (cfg.rChunk) {
     p.rChunk = cfg.rChunk;
   } else {
     const uint32_t entry = p.wide ? (p.materialize ? 16 : 8) : (p.materialize ? 8 : 4);
-    const uint32_t budget = entry == 4 ? 32 * 1024 : 64 * 1024;
+    const uint32_t budget = (entry == 4 || matNarrow) ? 32 * 1024 : 64 * 1024;
     p.rChunk = (budget / entry) / 2;
   }
   return p;

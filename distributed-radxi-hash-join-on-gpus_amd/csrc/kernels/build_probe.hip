@@ -269,6 +269,145 @@ __global__ __launch_bounds__(BPD_T, 5) void bpDirectSplitKernel(BPArgs a, const 
   if (t == 0 && total) atomicAdd(a.result, total);
 }
 
+// Materializing build/probe of the split layout (u32 rid column + u16
+// fragment column).  The LDS table is two u32 arrays (fragment, rid) of
+// nextpow2(2 * rChunk) slots; with the planner's 2048-tuple inner chunks that
+// is 32 KiB, and at 117 VGPRs (no scratch; a 5-per-CU budget spilled 68 B per
+// lane) 4 workgroups share a CU (the generic 8-byte-entry kernel held 176
+// VGPRs and 64 KiB: 2 per CU).  Per outer batch
+// every lane first probes all its tuples (first match + match count per
+// tuple), then the wave reserves its output once: per-batch wave scans give
+// each (tuple, lane) a slot, one LDS atomic per wave claims the range, and
+// every store instruction writes lane-consecutive pairs.  Tuples with more
+// than one match walk their chain again to emit the rest.
+constexpr int BPM_T = 256;
+constexpr int BPM_K = 8;
+
+template <bool FULL>
+__device__ __forceinline__ void bpmLoad(const uint32_t *__restrict__ rid, const uint16_t *__restrict__ hi, uint64_t off,
+                                        uint32_t n, uint32_t b0, uint32_t (&r)[BPM_K], uint32_t (&f)[BPM_K]) {
+#pragma unroll
+  for (int k = 0; k < BPM_K; ++k) {
+    const uint32_t idx = b0 + k * BPM_T + threadIdx.x;
+    if (FULL || idx < n) {
+      r[k] = rid[off + idx];
+      f[k] = hi[off + idx];
+    }
+  }
+}
+
+__global__ __launch_bounds__(BPM_T, 4) void bpMatSplitKernel(BPArgs a, const BPItem *__restrict__ items,
+                                                              const uint32_t *__restrict__ nItemsPtr,
+                                                              uint32_t capacity) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t maxSlots = 1u << ceilLog2(2ull * a.rChunk);
+  uint32_t *fragT = reinterpret_cast<uint32_t *>(smem);
+  uint32_t *ridT = fragT + maxSlots;
+  unsigned long long *wsum = reinterpret_cast<unsigned long long *>(ridT + maxSlots);
+  __shared__ uint32_t itemCursor;
+  const uint32_t *Rr = reinterpret_cast<const uint32_t *>(a.R);
+  const uint32_t *Sr = reinterpret_cast<const uint32_t *>(a.S);
+  constexpr uint32_t BATCH = BPM_T * BPM_K;
+  const uint32_t t = threadIdx.x, lane = t & (WAVE - 1);
+  const bool perItem = a.itemOffsets != nullptr;
+  const uint32_t nItems = min(*nItemsPtr, capacity);
+  uint64_t matches = 0;
+  for (uint32_t w = blockIdx.x; w < nItems; w += gridDim.x) {
+    const BPItem it = items[w];
+    const uint64_t rb = a.partR[it.part] + (uint64_t)it.rChunk * a.rChunk;
+    const uint64_t re = min(a.partREnd[it.part], rb + a.rChunk);
+    const uint64_t sb = a.partS[it.part] + (uint64_t)it.sChunk * a.sChunk;
+    const uint64_t se = min(a.partSEnd[it.part], sb + a.sChunk);
+    const uint32_t nr = (uint32_t)(re - rb), ns = (uint32_t)(se - sb);
+    uint32_t tbits = ceilLog2(2ull * nr);
+    if (tbits < 6) tbits = 6;
+    const uint32_t slots = 1u << tbits, mask = slots - 1;
+    const unsigned long long itemBase = perItem ? a.itemOffsets[w] : 0ull;
+    uint32_t rr[BPM_K], rf[BPM_K], sr[BPM_K], sf[BPM_K];
+    if (nr >= BATCH) bpmLoad<true>(Rr, a.Rhi, rb, nr, 0, rr, rf);
+    else bpmLoad<false>(Rr, a.Rhi, rb, nr, 0, rr, rf);
+    if (ns >= BATCH) bpmLoad<true>(Sr, a.Shi, sb, ns, 0, sr, sf);
+    else bpmLoad<false>(Sr, a.Shi, sb, ns, 0, sr, sf);
+    for (uint32_t i = t; i < slots; i += BPM_T) fragT[i] = EMPTY32;
+    if (t == 0) itemCursor = 0;
+    __syncthreads();
+
+    // ---- build
+    for (uint32_t b0 = 0; b0 < nr; b0 += BATCH) {
+      if (b0) bpmLoad<false>(Rr, a.Rhi, rb, nr, b0, rr, rf);
+#pragma unroll
+      for (int k = 0; k < BPM_K; ++k) {
+        if (b0 + k * BPM_T + t < nr) {
+          uint32_t h = hash32(rf[k], tbits);
+          while (atomicCAS(&fragT[h], EMPTY32, rf[k]) != EMPTY32) h = (h + 1) & mask;
+          ridT[h] = rr[k];
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- probe
+    for (uint32_t b0 = 0; b0 < ns; b0 += BATCH) {
+      if (b0) {
+        if (b0 + BATCH <= ns) bpmLoad<true>(Sr, a.Shi, sb, ns, b0, sr, sf);
+        else bpmLoad<false>(Sr, a.Shi, sb, ns, b0, sr, sf);
+      }
+      const uint32_t kmax = min((uint32_t)BPM_K, (uint32_t)ceilDiv(ns - b0, BPM_T));  // block-uniform
+      uint32_t found[BPM_K], first[BPM_K], incl[BPM_K];
+      uint32_t waveTotal = 0;
+#pragma unroll
+      for (int k = 0; k < BPM_K; ++k) {
+        found[k] = 0;
+        first[k] = 0;
+        incl[k] = 0;
+        if ((uint32_t)k >= kmax) continue;
+        if (b0 + k * BPM_T + t < ns) {
+          const uint32_t frag = sf[k];
+          uint32_t h = hash32(frag, tbits), e;
+          while ((e = fragT[h]) != EMPTY32) {
+            if (e == frag) {
+              if (found[k] == 0) first[k] = ridT[h];
+              ++found[k];
+            }
+            h = (h + 1) & mask;
+          }
+        }
+        incl[k] = waveInclusiveScan<uint32_t>(found[k]);
+        waveTotal += __shfl(incl[k], WAVE - 1, WAVE);
+        matches += found[k];
+      }
+      unsigned long long base = 0;
+      if (lane == WAVE - 1 && waveTotal)
+        base = perItem ? itemBase + atomicAdd(&itemCursor, waveTotal)
+                       : atomicAdd(a.outCursor, (unsigned long long)waveTotal);
+      base = __shfl(base, WAVE - 1, WAVE);
+#pragma unroll
+      for (int k = 0; k < BPM_K; ++k) {
+        if ((uint32_t)k >= kmax) break;
+        const unsigned long long pos = base + incl[k] - found[k];
+        if (found[k]) emitPair(a, pos, first[k], sr[k]);
+        if (found[k] > 1) {  // duplicate inner keys: emit the chain's other matches
+          const uint32_t frag = sf[k];
+          uint32_t h = hash32(frag, tbits), e, j = 0;
+          while ((e = fragT[h]) != EMPTY32) {
+            if (e == frag) {
+              if (j) emitPair(a, pos + j, ridT[h], sr[k]);
+              ++j;
+            }
+            h = (h + 1) & mask;
+          }
+        }
+        base += __shfl(incl[k], WAVE - 1, WAVE);
+      }
+    }
+    __syncthreads();  // the next item clears the table and the cursor
+  }
+  const unsigned long long total = blockReduceSum<BPM_T, unsigned long long>((unsigned long long)matches, wsum);
+  if (t == 0 && total) atomicAdd(a.result, total);
+}
+
+static size_t bpMatSplitLds(const BPArgs &a) { return (size_t(8) << ceilLog2(2ull * a.rChunk)) + 64; }
+
 // ITEMS: count pre-pass of a two-pass materialization (per-item match counts);
 // a separate instantiation so the count-only production kernel is unchanged.
 // Occupancy is LDS-bound: 4-byte count tables (32 KiB) fit 4 workgroups per
@@ -481,8 +620,11 @@ void buildProbe(const BPArgs &args, const BPItem *items, const uint32_t *nItems,
     return;
   }
   if (a.split) {  // materialize
-    hipLaunchKernelGGL((buildProbeKernel<BP_CMAT, false, true>), dim3(blocks), dim3(BPT), lds, s, a, items, nItems,
-                       capacity);
+    const size_t ldsM = bpMatSplitLds(a);
+    HJ_CHECK(ldsM <= 160 * 1024, "buildProbe: LDS request %zu exceeds 160 KiB (rChunk=%u)", ldsM, a.rChunk);
+    const uint32_t perCuM = (uint32_t)std::min<size_t>(4, (160 * 1024) / ldsM);
+    const uint32_t blocksM = std::min<uint32_t>(capacity, 256 * std::max<uint32_t>(perCuM, 1));
+    hipLaunchKernelGGL(bpMatSplitKernel, dim3(blocksM), dim3(BPM_T), ldsM, s, a, items, nItems, capacity);
     HIP_CHECK_LAUNCH();
     return;
   }

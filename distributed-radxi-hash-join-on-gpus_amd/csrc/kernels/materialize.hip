@@ -122,28 +122,91 @@ void placeRows(const uint64_t *rows, const uint64_t *idx, uint64_t n, uint64_t *
 // Single-rank fast path: both payload columns are local, so one pass per pair
 // reads the pair, gathers its two 32-byte rows and writes the whole 80-byte
 // output row (no request buckets, no intermediate row buffers).
+//
+// A wave owns 64 consecutive pairs per step.  Gathers go by lane pairs: lanes
+// 2j and 2j+1 read the two 16-byte halves of one row, so each load instruction
+// touches 32 whole rows instead of 64 half rows.  The 64 output rows (5 KiB,
+// contiguous in the output) are assembled in a wave-private LDS buffer and
+// written by 5 instructions of 64 consecutive 16-byte pieces.  The direct form
+// (5 stores per lane at an 80-byte lane stride) cost 43.9 ms for the SF100
+// 600M pairs (profiles/r1_tpch_sf100_kernel_stats.md).
+constexpr int MAT_WAVES = MT / 64;
+using u64x2 = unsigned long long __attribute__((ext_vector_type(2)));
+
+// NT: non-temporal output stores.  XCD: the grid's 8 XCD groups (blockIdx % 8)
+// each walk one contiguous eighth of the pairs, so the ~4 pairs that share an
+// inner row (one build/probe item) are served from one XCD's L2.  Measured on
+// SF100: direct stores 42.3 ms, LDS-staged 39.3, + XCD walk 38.6 (variants
+// without NT within 1%); the rest is the random 32-byte row gathers, fetched
+// as 64-byte requests (FETCH_SIZE 89 GB for 600M pairs).
+template <bool NT, bool XCD>
 __global__ __launch_bounds__(MT) void materializeLocalKernel(const ulonglong2 *__restrict__ pairs, uint64_t n,
                                                              const ulonglong2 *__restrict__ rowsA, uint64_t offA,
                                                              const ulonglong2 *__restrict__ rowsB, uint64_t offB,
                                                              ulonglong2 *__restrict__ out) {
-  const uint64_t stride = (uint64_t)gridDim.x * MT;
-  for (uint64_t i = (uint64_t)blockIdx.x * MT + threadIdx.x; i < n; i += stride) {
-    const ulonglong2 p = pairs[i];
-    const uint64_t a = 2 * (p.x - offA), b = 2 * (p.y - offB);
-    const ulonglong2 a0 = rowsA[a], a1 = rowsA[a + 1], b0 = rowsB[b], b1 = rowsB[b + 1];
-    ulonglong2 *o = out + 5 * i;  // 80-byte row = 5 x 16 bytes
-    o[0] = p;
-    o[1] = a0;
-    o[2] = a1;
-    o[3] = b0;
-    o[4] = b1;
+  __shared__ ulonglong2 stage[MAT_WAVES][5 * 64];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  ulonglong2 *w = stage[wave];
+  const uint64_t steps = ceilDiv(n, 64);
+  uint64_t first = (uint64_t)blockIdx.x * MAT_WAVES + wave, last = steps, waveStride = (uint64_t)gridDim.x * MAT_WAVES;
+  if (XCD) {  // gridDim.x % 8 == 0: XCD x = blockIdx % 8 walks the x-th eighth of the steps
+    const uint32_t x = blockIdx.x & 7;
+    const uint64_t seg0 = steps * x / 8;
+    last = steps * (x + 1) / 8;
+    first = seg0 + (uint64_t)(blockIdx.x >> 3) * MAT_WAVES + wave;
+    waveStride = (uint64_t)(gridDim.x >> 3) * MAT_WAVES;
+  }
+  for (uint64_t st = first; st < last; st += waveStride) {
+    const uint64_t base = st * 64;
+    const uint32_t m = (uint32_t)(n - base < 64 ? n - base : 64);
+    const ulonglong2 p = lane < m ? pairs[base + lane] : make_ulonglong2(offA, offB);
+    const uint32_t half = lane & 1;
+    ulonglong2 ra[2], rb[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const uint32_t j = (lane >> 1) + 32 * k;  // pair whose row half this lane moves
+      const uint64_t x = __shfl(p.x, j, 64), y = __shfl(p.y, j, 64);
+      if (j < m) {
+        ra[k] = rowsA[2 * (x - offA) + half];
+        rb[k] = rowsB[2 * (y - offB) + half];
+      }
+    }
+    w[5 * lane] = p;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const uint32_t j = (lane >> 1) + 32 * k;
+      w[5 * j + 1 + half] = ra[k];
+      w[5 * j + 3 + half] = rb[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    ulonglong2 *o = out + 5 * base;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const uint32_t q = 64 * k + lane;
+      if (q < 5 * m) {
+        const ulonglong2 v = w[q];
+        if (NT) {
+          const u64x2 vv = {v.x, v.y};
+          __builtin_nontemporal_store(vv, reinterpret_cast<u64x2 *>(o + q));
+        } else {
+          o[q] = v;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
 void materializeLocal(const ulonglong2 *pairs, uint64_t n, const uint64_t *rowsA, uint64_t offA,
                       const uint64_t *rowsB, uint64_t offB, uint64_t *out, hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(materializeLocalKernel, dim3(gridFor(n)), dim3(MT), 0, s, pairs, n,
+  const uint64_t blocks = ceilDiv(ceilDiv(n, 64), MAT_WAVES);
+  const uint32_t grid = (uint32_t)(blocks < 8192 ? (blocks + 7) / 8 * 8 : 8192);
+  hipLaunchKernelGGL((materializeLocalKernel<true, true>), dim3(grid), dim3(MT), 0, s, pairs, n,
                      reinterpret_cast<const ulonglong2 *>(rowsA), offA, reinterpret_cast<const ulonglong2 *>(rowsB),
                      offB, reinterpret_cast<ulonglong2 *>(out));
   HIP_CHECK_LAUNCH();
