@@ -293,3 +293,37 @@ def test_direct_count_table(C, cuda, dist, split):
         assert res["global_matches"] == exp
         counts[direct] = res["global_matches"]
     assert counts[True] == counts[False]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("r_chunk", [0, 512])
+def test_materialize_split_duplicates(C, cuda, r_chunk):
+    """Materializing build/probe of the split layout (bpMatSplitKernel): 16
+    duplicates of every inner key (chain re-walk for the extra matches) and,
+    with r_chunk=512, inner partitions split over several LDS tables."""
+    import torch
+    G_R, G_S = 160_000, 300_000
+    ctx = C.ExecContext("device", 0, C.LocalCommunicator())
+    inner = C.GenSpec(distribution=C.KeyDistribution.MODULO, seed=91, domain=G_R // 16)
+    outer = C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=92, domain=G_R // 8, zipf_theta=0.5)
+    R = C.Relation(G_R, G_R, "device", 0)
+    S = C.Relation(G_S, G_S, "device", 0)
+    R.generate(inner, 0)
+    S.generate(outer, 0)
+    cfg = C.JoinConfig()
+    cfg.materialize = True
+    cfg.r_chunk = r_chunk
+    j = C.HashJoin(R, S, ctx, cfg)
+    assert j.plan.split_local
+    res = j.run()
+    Rt, St = R.to_tensor().cpu(), S.to_tensor().cpu()
+    dom = int(max(Rt[:, 0].max(), St[:, 0].max())) + 1
+    exp = int((torch.bincount(Rt[:, 0], minlength=dom) * torch.bincount(St[:, 0], minlength=dom)).sum())
+    assert res["global_matches"] == exp == res["output_pairs"] and not res["output_overflow"]
+    pairs = j.output().cpu()
+    keyR = torch.empty(G_R, dtype=torch.int64)
+    keyR[Rt[:, 1]] = Rt[:, 0]
+    keyS = torch.empty(G_S, dtype=torch.int64)
+    keyS[St[:, 1]] = St[:, 0]
+    assert torch.equal(keyR[pairs[:, 0]], keyS[pairs[:, 1]])
+    assert torch.unique(pairs[:, 0] * G_S + pairs[:, 1]).numel() == exp
