@@ -601,6 +601,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("wire_codec", &core::JoinConfig::wireCodec)
       .def_readwrite("split_local", &core::JoinConfig::splitLocal)
       .def_readwrite("direct_count", &core::JoinConfig::directCount)
+      .def_readwrite("split_histogram", &core::JoinConfig::splitHistogram)
       .def_readwrite("local_item_tiles", &core::JoinConfig::localItemTiles)
       .def_readwrite("local_geometry", &core::JoinConfig::localGeometry)
       .def_readwrite("local_sample_stride", &core::JoinConfig::localSampleStride)
@@ -618,6 +619,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("network_bits", &core::JoinPlan::networkBits)
       .def_readonly("key_mix", &core::JoinPlan::keyMix)
       .def_readonly("sampled_network", &core::JoinPlan::sampledNetwork)
+      .def_readonly("split_histogram", &core::JoinPlan::splitHistogram)
       .def_readonly("local_bits", &core::JoinPlan::localBits)
       .def_readonly("key_shift", &core::JoinPlan::keyShift)
       .def_readonly("frag_shift", &core::JoinPlan::fragShift)

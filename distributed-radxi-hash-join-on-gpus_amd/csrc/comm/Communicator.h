@@ -38,6 +38,10 @@ class Communicator {
 
   // recv[r * count + i] = rank r's send[i]   (host buffers, blocking)
   virtual void allGatherHost(const uint64_t *send, uint64_t *recv, size_t count) = 0;
+  // Same on device buffers, enqueued on `stream` in issue order with the
+  // stream's other collectives (RCCL: no host sync).  The default stages
+  // through the host and completes before returning.
+  virtual void allGatherDevice(const uint64_t *send, uint64_t *recv, size_t count, hipStream_t stream);
   // data[i] = sum over ranks (host buffer, blocking)
   virtual void allReduceSumHost(uint64_t *data, size_t count) = 0;
   virtual void barrier() = 0;

@@ -1,10 +1,19 @@
 #include <cstring>
+#include <vector>
 
 #include "../utils/Hip.h"
 #include "Communicator.h"
 
 namespace hpcjoin {
 namespace comm {
+
+void Communicator::allGatherDevice(const uint64_t *send, uint64_t *recv, size_t count, hipStream_t stream) {
+  std::vector<uint64_t> mine(count), all(count * size());
+  HIP_CHECK(hipStreamSynchronize(stream));
+  if (count) HIP_CHECK(hipMemcpy(mine.data(), send, count * 8, hipMemcpyDeviceToHost));
+  allGatherHost(mine.data(), all.data(), count);
+  if (count) HIP_CHECK(hipMemcpy(recv, all.data(), all.size() * 8, hipMemcpyHostToDevice));
+}
 
 void LocalCommunicator::allGatherHost(const uint64_t *send, uint64_t *recv, size_t count) {
   if (send != recv) std::memmove(recv, send, count * sizeof(uint64_t));

@@ -83,6 +83,11 @@ void RcclCommunicator::allGatherHost(const uint64_t *send, uint64_t *recv, size_
   utils::waitStream(stream_, this, "ncclAllGather");
 }
 
+void RcclCommunicator::allGatherDevice(const uint64_t *send, uint64_t *recv, size_t count, hipStream_t stream) {
+  checkHealth();
+  RCCL_CHECK(ncclAllGather(send, recv, count, ncclUint64, static_cast<ncclComm_t>(comm_), stream));
+}
+
 void RcclCommunicator::allReduceSumHost(uint64_t *data, size_t count) {
   uint64_t *buf = scratch(count);
   HIP_CHECK(hipMemcpyAsync(buf, data, count * 8, hipMemcpyHostToDevice, stream_));

@@ -27,6 +27,7 @@ class RcclCommunicator : public Communicator {
   bool supports(Location loc) const override { return loc == Location::Device; }
   std::string name() const override { return "rccl"; }
   void allGatherHost(const uint64_t *send, uint64_t *recv, size_t count) override;
+  void allGatherDevice(const uint64_t *send, uint64_t *recv, size_t count, hipStream_t stream) override;
   void allReduceSumHost(uint64_t *data, size_t count) override;
   void barrier() override;
   void allToAllV(const uint64_t *send, const uint64_t *sendCounts, const uint64_t *sendDispls, uint64_t *recv,

@@ -49,6 +49,11 @@ void GlobalHistogram::computeGlobalHistograms(GlobalHistogram &inner, GlobalHist
   outer.absorb(all.data(), a + b, a);
 }
 
+void GlobalHistogram::setGathered(const uint64_t *gathered) {
+  const size_t per = (size_t)localHistogram->getChunkCount() * localHistogram->getPartitionCount();
+  absorb(gathered, per, 0);
+}
+
 uint64_t *GlobalHistogram::getGlobalHistogram() { return values.data(); }
 
 }  // namespace histograms

@@ -28,6 +28,10 @@ class GlobalHistogram {
   // One collective for both relations (what HistogramComputation uses).
   static void computeGlobalHistograms(GlobalHistogram &inner, GlobalHistogram &outer);
 
+  // Take the [rank][chunk][partition] table of this relation alone from an
+  // all-gather done elsewhere (e.g. on device, overlapped with an exchange).
+  void setGathered(const uint64_t *gathered);
+
   uint64_t *getGlobalHistogram();  // [F]
   // count of partition p in chunk c on rank r
   uint64_t rankCount(uint32_t r, uint32_t c, uint32_t p) const {

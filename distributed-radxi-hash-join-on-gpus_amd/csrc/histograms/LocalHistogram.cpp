@@ -6,6 +6,7 @@
 #include "../core/Configuration.h"
 #include "../host/HostOps.h"
 #include "../memory/Arena.h"
+#include "../utils/Debug.h"
 #include "../utils/Hip.h"
 
 namespace hpcjoin {
@@ -57,6 +58,54 @@ void LocalHistogram::computeLocalHistogram() {
     host::netHistogram(relation->getData(), relation->getLocalSize(), bits, geom, blockHist, mix);
     host::digitTotals(blockHist, F, geom.blocks, bpc, chunks, chunkValues.data());
   }
+}
+
+void LocalHistogram::computeLocalHistogramDevice() {
+  const uint32_t F = 1u << bits;
+  JOIN_ASSERT(ctx->onDevice(), "LocalHistogram", "device histogram on a host context");
+  summed = false;
+  blockHist = ctx->workspace().getArray<uint32_t>((uint64_t)F * geom.blocks);
+  totalsDev = ctx->workspace().getArray<uint64_t>((uint64_t)chunks * F);
+  kernels::netHistogram(relation->getData(), relation->getLocalSize(), bits, geom, blockHist, ctx->stream(), mix);
+  kernels::digitTotals(blockHist, F, geom.blocks, bpc, chunks, totalsDev, ctx->stream());
+}
+
+void LocalHistogram::computeSampledEstimate(uint32_t stride) {
+  const uint32_t F = 1u << bits;
+  values.assign(F, 0);
+  chunkValues.assign((size_t)chunks * F, 0);
+  summed = false;
+  uint32_t *sampleHist = ctx->workspace().getArray<uint32_t>((uint64_t)F * geom.blocks);
+  if (ctx->onDevice()) {
+    uint64_t *t = ctx->workspace().getArray<uint64_t>((uint64_t)chunks * F);
+    kernels::netHistogram(relation->getData(), relation->getLocalSize(), bits, geom, sampleHist, ctx->stream(), mix,
+                          std::max<uint32_t>(1, stride));
+    kernels::digitTotals(sampleHist, F, geom.blocks, bpc, chunks, t, ctx->stream());
+    ctx->copy(chunkValues.data(), t, chunkValues.size() * 8, false, true);
+  } else {
+    host::netHistogram(relation->getData(), relation->getLocalSize(), bits, geom, sampleHist, mix);
+    host::digitTotals(sampleHist, F, geom.blocks, bpc, chunks, chunkValues.data());
+  }
+}
+
+void LocalHistogram::scaleEstimate() {
+  const uint32_t F = 1u << bits;
+  const uint64_t n = relation->getLocalSize(), per = (uint64_t)bpc * geom.tuplesPerBlock();
+  for (uint32_t c = 0; c < chunks; ++c) {
+    const uint64_t b = std::min<uint64_t>(n, (uint64_t)c * per), e = std::min<uint64_t>(n, b + per);
+    uint64_t *v = &chunkValues[(size_t)c * F];
+    uint64_t sampledTuples = 0;
+    for (uint32_t d = 0; d < F; ++d) sampledTuples += v[d];
+    if (!sampledTuples) continue;
+    const double scale = (double)(e - b) / (double)sampledTuples;
+    for (uint32_t d = 0; d < F; ++d) v[d] = (uint64_t)(v[d] * scale + 0.5);
+  }
+  summed = false;
+}
+
+void LocalHistogram::setChunkHistograms(const uint64_t *v) {
+  chunkValues.assign(v, v + (size_t)chunks * (1u << bits));
+  summed = false;
 }
 
 uint64_t *LocalHistogram::getChunkHistograms() { return chunkValues.data(); }

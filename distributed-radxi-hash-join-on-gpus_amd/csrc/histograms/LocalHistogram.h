@@ -24,6 +24,16 @@ class LocalHistogram {
   ~LocalHistogram();
 
   void computeLocalHistogram();  // device: enqueued; host values valid after ctx->synchronize()
+  // Device only: per-workgroup histogram and per-chunk totals stay in HBM
+  // (chunkTotalsDevice()); no copy to the host.
+  void computeLocalHistogramDevice();
+  const uint64_t *chunkTotalsDevice() const { return totalsDev; }
+  // Estimate from 1 tile in `stride` per workgroup (device: enqueued; call
+  // scaleEstimate() after ctx->synchronize()).  Per-chunk counts are scaled to
+  // the chunk's tuple count.  Used for the partition assignment only.
+  void computeSampledEstimate(uint32_t stride);
+  void scaleEstimate();
+  void setChunkHistograms(const uint64_t *v);  // [chunks][F] (e.g. this rank's row of a gather)
   uint64_t *getLocalHistogram();  // [F], summed over chunks
   uint64_t *getChunkHistograms();  // [chunks][F]
 

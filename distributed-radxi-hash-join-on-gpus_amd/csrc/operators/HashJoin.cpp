@@ -119,6 +119,7 @@ void HashJoin::makeJoinPlan() {
     else if (config.networkHistogram == core::HistogramMode::Auto)
       plan.sampledNetwork = eligible && small >= (16ull << 20);
   }
+  plan.splitHistogram = config.splitHistogram && numberOfNodes > 1 && ctx->onDevice();
   JOIN_DEBUG("HashJoin", "%s", plan.describe().c_str());
   if (ctx->onDevice())
     for (auto &e : ev) HIP_CHECK(hipEventCreate(&e));
@@ -260,6 +261,47 @@ JoinResult HashJoin::runImpl() {
       sampledOverflowed = true;
       ++result.networkFallbacks;
     }
+  }
+  if (!innerWindow && plan.splitHistogram && !sampled) {
+    // ------------------------ N > 1: outer histogram overlaps the inner exchange
+    hc.reset(new tasks::HistogramComputation(numberOfNodes, nodeId, innerRelation, outerRelation, ctx, plan,
+                                             config.maxPartitionBlocks));
+    hc->executeInner(config.sampleStride);
+    if (dev) HIP_CHECK(hipEventRecord(ev[1], ctx->stream()));
+    Measurements::stopHistogramComputation();
+    Measurements::storeHistogramDetails(hc->localUs, innerRelation->getLocalSize(), outerRelation->getLocalSize(),
+                                        hc->globalUs, hc->assignUs, hc->offsetUs);
+    t1 = nowUs();
+    Measurements::startWindowAllocation();
+    auto makeWindow = [&](int r) {
+      std::unique_ptr<data::Window> w(new data::Window(
+          (r == 0 ? hc->innerOffsetMap() : hc->outerOffsetMap())->getExchangePlan(),
+          r == 0 ? hc->innerGlobal() : hc->outerGlobal(), hc->assignmentMap(), ctx, plan.wide));
+      if (plan.wireBits[r]) {
+        kernels::WireCodec c;
+        c.w = plan.wireBits[r];
+        c.ridBits = plan.wireRidBits[r];
+        c.keyShift = plan.keyShift;
+        w->setWireCodec(c, plan.ridBase[r]);
+      }
+      return w;
+    };
+    innerOwned = makeWindow(0);
+    innerWindow = innerOwned.get();
+    Measurements::stopWindowAllocation();
+    t2 = nowUs();
+    Measurements::startNetworkPartitioning();
+    trace.reset();  // roctx ranges nest: pop before the next push
+    utils::faultPoint("network");
+    trace.reset(new performance::TraceRange("network_partitioning"));
+    tasks::NetworkPartitioning np(nodeId, innerRelation, outerRelation, innerWindow, nullptr, hc.get(), ctx, plan);
+    np.partitionInner([&](uint32_t c) {
+      if (c == 0) hc->launchOuter(ctx->commStream());
+    });
+    hc->finishOuter();
+    outerOwned = makeWindow(1);
+    outerWindow = outerOwned.get();
+    np.partitionOuter(outerWindow);
   }
   if (!innerWindow) {
     if (!sampled) {

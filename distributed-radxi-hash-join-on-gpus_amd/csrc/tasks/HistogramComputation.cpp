@@ -1,6 +1,11 @@
 #include "HistogramComputation.h"
 
+#include "../comm/Communicator.h"
+#include "../memory/Arena.h"
 #include "../performance/Clock.h"
+#include "../utils/Debug.h"
+#include "../utils/Fault.h"
+#include "../utils/Hip.h"
 
 namespace hpcjoin {
 namespace tasks {
@@ -26,7 +31,57 @@ HistogramComputation::HistogramComputation(uint32_t numberOfNodes, uint32_t node
                                                outerRelationGlobalHistogram.get(), assignment.get()));
 }
 
-HistogramComputation::~HistogramComputation() {}
+HistogramComputation::~HistogramComputation() {
+  if (outerHistDone) (void)hipEventDestroy(outerHistDone);
+  if (outerGatherDone) (void)hipEventDestroy(outerGatherDone);
+}
+
+void HistogramComputation::executeInner(uint32_t sampleStride) {
+  uint64_t t0 = performance::nowUs();
+  innerRelationLocalHistogram->computeLocalHistogram();
+  outerRelationLocalHistogram->computeSampledEstimate(sampleStride);
+  ctx->synchronize();
+  outerRelationLocalHistogram->scaleEstimate();
+  localUs = performance::nowUs() - t0;
+  t0 = performance::nowUs();
+  histograms::GlobalHistogram::computeGlobalHistograms(*innerRelationGlobalHistogram, *outerRelationGlobalHistogram);
+  globalUs = performance::nowUs() - t0;
+  t0 = performance::nowUs();
+  assignment->computePartitionAssignment();  // outer side: the estimate
+  assignUs = performance::nowUs() - t0;
+  t0 = performance::nowUs();
+  innerOffsets->computeOffsets();
+  offsetUs = performance::nowUs() - t0;
+}
+
+void HistogramComputation::launchOuter(hipStream_t exchangeStream) {
+  JOIN_ASSERT(ctx->onDevice(), "HistogramComputation", "split histograms run on the device path");
+  histograms::LocalHistogram *h = outerRelationLocalHistogram.get();
+  const size_t per = (size_t)h->getChunkCount() * h->getPartitionCount();
+  if (!outerHistDone) HIP_CHECK(hipEventCreateWithFlags(&outerHistDone, hipEventDisableTiming));
+  if (!outerGatherDone) HIP_CHECK(hipEventCreateWithFlags(&outerGatherDone, hipEventDisableTiming));
+  h->computeLocalHistogramDevice();
+  HIP_CHECK(hipEventRecord(outerHistDone, ctx->stream()));
+  uint64_t *gatherDev = ctx->workspace().getArray<uint64_t>(per * numberOfNodes);
+  outerGatherHost = ctx->staging().getArray<uint64_t>(per * numberOfNodes);
+  HIP_CHECK(hipStreamWaitEvent(exchangeStream, outerHistDone, 0));
+  ctx->comm()->allGatherDevice(h->chunkTotalsDevice(), gatherDev, per, exchangeStream);
+  HIP_CHECK(hipMemcpyAsync(outerGatherHost, gatherDev, per * numberOfNodes * 8, hipMemcpyDeviceToHost,
+                           exchangeStream));
+  HIP_CHECK(hipEventRecord(outerGatherDone, exchangeStream));
+  outerLaunched = true;
+}
+
+void HistogramComputation::finishOuter() {
+  JOIN_ASSERT(outerLaunched, "HistogramComputation", "finishOuter() before launchOuter()");
+  utils::waitEvent(outerGatherDone, ctx->comm(), "outer histogram all-gather");
+  histograms::LocalHistogram *h = outerRelationLocalHistogram.get();
+  const size_t per = (size_t)h->getChunkCount() * h->getPartitionCount();
+  h->setChunkHistograms(outerGatherHost + per * nodeId);
+  outerRelationGlobalHistogram->setGathered(outerGatherHost);
+  outerOffsets->computeOffsets();
+  outerLaunched = false;
+}
 
 void HistogramComputation::execute() {
   computeLocalHistograms();

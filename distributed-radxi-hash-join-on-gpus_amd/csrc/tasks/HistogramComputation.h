@@ -26,6 +26,18 @@ class HistogramComputation : public Task {
   void execute();
   task_type_t getType() { return TASK_HISTOGRAM; }
 
+  // Split pipeline (JoinPlan::splitHistogram, device, N > 1): the outer
+  // relation's exact histogram leaves the head of the join.
+  //  executeInner(): inner exact + outer sampled estimate, one all-gather,
+  //    assignment (LPT on the estimate), inner offsets.
+  //  launchOuter(s): outer exact histogram on the compute stream and its
+  //    all-gather enqueued on `s` (the exchange stream, after the inner
+  //    chunks already issued there), then a copy to pinned host memory.
+  //  finishOuter(): waits for that copy only, then outer offsets.
+  void executeInner(uint32_t sampleStride);
+  void launchOuter(hipStream_t exchangeStream);
+  void finishOuter();
+
   uint32_t *getAssignment();
   uint64_t *getInnerRelationLocalHistogram();
   uint64_t *getOuterRelationLocalHistogram();
@@ -66,6 +78,9 @@ class HistogramComputation : public Task {
 
  private:
   core::ExecContext *ctx;
+  hipEvent_t outerHistDone = nullptr, outerGatherDone = nullptr;
+  uint64_t *outerGatherHost = nullptr;  // pinned (staging arena)
+  bool outerLaunched = false;
 };
 
 }  // namespace tasks

@@ -21,8 +21,19 @@ void NetworkPartitioning::execute() {
   partition(outerRelation, outerWindow, histograms->outerLocal(), histograms->outerOffsetMap()->getExchangePlan());
 }
 
+void NetworkPartitioning::partitionInner(const std::function<void(uint32_t)> &afterChunk) {
+  partition(innerRelation, innerWindow, histograms->innerLocal(), histograms->innerOffsetMap()->getExchangePlan(),
+            afterChunk);
+}
+
+void NetworkPartitioning::partitionOuter(data::Window *window) {
+  outerWindow = window;
+  partition(outerRelation, outerWindow, histograms->outerLocal(), histograms->outerOffsetMap()->getExchangePlan());
+}
+
 void NetworkPartitioning::partition(data::Relation *relation, data::Window *window,
-                                    histograms::LocalHistogram *local, const histograms::ExchangePlan &xp) {
+                                    histograms::LocalHistogram *local, const histograms::ExchangePlan &xp,
+                                    const std::function<void(uint32_t)> &afterChunk) {
   const uint64_t n = relation->getLocalSize();
   JOIN_ASSERT(xp.sendTotal == n, "NetworkPartitioning", "plan sends %lu of %lu tuples",
               (unsigned long)xp.sendTotal, (unsigned long)n);
@@ -52,6 +63,7 @@ void NetworkPartitioning::partition(data::Relation *relation, data::Window *wind
         kernels::netScatter(relation->getData(), n, bits, plan.keyShift, g, b0, b1, gcur + c * perChunk,
                             static_cast<uint64_t *>(send), ctx->stream(), plan.keyBits, mix);
       if (!single) window->exchange(send, c);
+      if (afterChunk) afterChunk(c);
     }
   } else {
     uint64_t *cursors = ctx->workspace().getArray<uint64_t>((uint64_t)F * g.blocks);
@@ -60,6 +72,7 @@ void NetworkPartitioning::partition(data::Relation *relation, data::Window *wind
       const uint32_t b0 = c * bpc, b1 = std::min(g.blocks, b0 + bpc);
       host::netScatter(relation->getData(), n, bits, plan.keyShift, g, b0, b1, cursors, send, plan.wide, mix);
       if (!single) window->exchange(send, c);
+      if (afterChunk) afterChunk(c);
     }
   }
 }

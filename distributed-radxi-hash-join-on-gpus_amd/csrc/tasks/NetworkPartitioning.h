@@ -8,6 +8,8 @@
 // write-combining + double-buffered MPI_Put).
 #pragma once
 
+#include <functional>
+
 #include "../core/ExecContext.h"
 #include "../data/Relation.h"
 #include "../data/Window.h"
@@ -27,9 +29,15 @@ class NetworkPartitioning : public Task {
   void execute();
   task_type_t getType() { return TASK_NET_PARTITION; }
 
+  // Split histogram pipeline (HistogramComputation::launchOuter): the inner
+  // relation first, with a hook after each chunk has been handed to the
+  // exchange; the outer relation once its window exists.
+  void partitionInner(const std::function<void(uint32_t)> &afterChunk);
+  void partitionOuter(data::Window *window);
+
  protected:
   void partition(data::Relation *relation, data::Window *window, histograms::LocalHistogram *local,
-                 const histograms::ExchangePlan &xp);
+                 const histograms::ExchangePlan &xp, const std::function<void(uint32_t)> &afterChunk = {});
 
  protected:
   uint32_t nodeId;

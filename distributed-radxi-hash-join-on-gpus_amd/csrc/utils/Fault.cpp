@@ -52,12 +52,13 @@ uint64_t commTimeoutMs() {
 
 void setCommTimeoutMs(uint64_t ms) { g_timeoutMs.store(ms, std::memory_order_relaxed); }
 
-void waitStream(hipStream_t stream, comm::Communicator *comm, const char *what) {
+template <typename Query>
+static void waitUntil(Query query, comm::Communicator *comm, const char *what) {
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
   const auto deadline = t0 + std::chrono::milliseconds(commTimeoutMs());
   for (uint64_t spin = 0;; ++spin) {
-    hipError_t e = hipStreamQuery(stream);
+    hipError_t e = query();
     if (e == hipSuccess) return;
     if (e != hipErrorNotReady) HIP_CHECK(e);
     if (comm) comm->checkHealth();
@@ -72,6 +73,14 @@ void waitStream(hipStream_t stream, comm::Communicator *comm, const char *what) 
     if (spin < 2000) std::this_thread::yield();
     else std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
+}
+
+void waitStream(hipStream_t stream, comm::Communicator *comm, const char *what) {
+  waitUntil([stream] { return hipStreamQuery(stream); }, comm, what);
+}
+
+void waitEvent(hipEvent_t event, comm::Communicator *comm, const char *what) {
+  waitUntil([event] { return hipEventQuery(event); }, comm, what);
 }
 
 }  // namespace utils

@@ -38,6 +38,8 @@ void setCommTimeoutMs(uint64_t ms);  // process-wide override (tests)
 // Wait until `stream` is idle.  Polls comm->checkHealth() and throws after
 // commTimeoutMs() (after aborting the communicator so peers fail fast, too).
 void waitStream(hipStream_t stream, comm::Communicator *comm, const char *what);
+// Same for one event (work queued behind it on its stream is not waited for).
+void waitEvent(hipEvent_t event, comm::Communicator *comm, const char *what);
 
 }  // namespace utils
 }  // namespace hpcjoin

@@ -157,6 +157,36 @@ def test_wire_codec_exchange(C, dev, n_ranks, chunks):
     assert pairs[:, 1].unique().numel() == exp  # every outer row matched once (unique inner keys)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_ranks,chunks,mat", [(2, 1, False), (3, 4, True), (8, 2, False)])
+def test_split_histogram_pipeline(C, cuda, n_ranks, chunks, mat):
+    """N > 1 device joins take the assignment from an outer-side estimate and
+    run the outer exact histogram + its all-gather behind the inner exchange
+    (JoinPlan.split_histogram).  Skewed outer side, LPT: counts and
+    materialized pairs equal the fused-histogram path."""
+    import torch
+    out = {}
+    for split in (True, False):
+        pairs = [None] * n_ranks
+
+        def cfg_fn(c, split=split):
+            c.split_histogram = split
+            c.chunks = chunks
+            c.materialize = mat
+            c.assignment = C.AssignmentPolicy.LPT
+
+        results, exp = run_ranks(C, n_ranks, "device", 300_007, 700_001, cfg_fn=cfg_fn, outer_dist="ZIPF",
+                                 theta=0.9, outputs=pairs if mat else None)
+        for res, plan in results:
+            assert plan.split_histogram == split
+            assert res["global_matches"] == exp
+        if mat:
+            p = torch.cat([x.cpu() for x in pairs])
+            out[split] = p[torch.argsort(p[:, 1] * (1 << 32) + p[:, 0])]
+    if mat:
+        assert torch.equal(out[True], out[False])
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
