@@ -602,6 +602,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("split_local", &core::JoinConfig::splitLocal)
       .def_readwrite("direct_count", &core::JoinConfig::directCount)
       .def_readwrite("split_histogram", &core::JoinConfig::splitHistogram)
+      .def_readwrite("pipeline_outer", &core::JoinConfig::pipelineOuter)
       .def_readwrite("local_item_tiles", &core::JoinConfig::localItemTiles)
       .def_readwrite("local_geometry", &core::JoinConfig::localGeometry)
       .def_readwrite("local_sample_stride", &core::JoinConfig::localSampleStride)
@@ -620,6 +621,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("key_mix", &core::JoinPlan::keyMix)
       .def_readonly("sampled_network", &core::JoinPlan::sampledNetwork)
       .def_readonly("split_histogram", &core::JoinPlan::splitHistogram)
+      .def_readonly("pipeline_outer", &core::JoinPlan::pipelineOuter)
       .def_readonly("local_bits", &core::JoinPlan::localBits)
       .def_readonly("key_shift", &core::JoinPlan::keyShift)
       .def_readonly("frag_shift", &core::JoinPlan::fragShift)

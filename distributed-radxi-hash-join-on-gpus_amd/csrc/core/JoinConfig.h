@@ -76,6 +76,7 @@ struct JoinConfig {
   bool splitLocal = true;       // device: split local pass output (u32 rid + u16 fragment columns) when they fit
   bool directCount = true;      // count-only build/probe: direct-addressed LDS counts when fragments are <= 13 bits
   bool splitHistogram = true;   // N > 1 on device: outer exact histogram overlaps the inner exchange
+  bool pipelineOuter = true;    // N > 1 on device, counting: outer local pass + build/probe per received chunk
   uint32_t localItemTiles = 64; // local pass work item: up to this many 4096-tuple tiles of one segment
   uint32_t localGeometry = 0;   // local scatter workgroup geometry (0 = 1024 x 8; 1-4: sweep alternatives)
 
@@ -99,6 +100,7 @@ struct JoinPlan {
   bool keyMix = false;        // radix digits from kernels::KeyMix{keyBits} of the key
   bool sampledNetwork = false;  // single-rank network pass sized from a sampled histogram
   bool splitHistogram = false;  // N > 1: assignment from an outer estimate, outer exact histogram off the head
+  bool pipelineOuter = false;   // N > 1 counting: outer local pass + build/probe per exchange chunk
   HistogramMode localHistogram = HistogramMode::Exact;  // resolved per window size by LocalPartitioning
   uint32_t sampleStride = 64;
   uint32_t localSampleStride = 16;

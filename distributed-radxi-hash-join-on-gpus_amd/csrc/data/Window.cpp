@@ -34,6 +34,33 @@ Window::Window(const histograms::ExchangePlan &plan, uint64_t capacityTuples, co
   exchanged.assign(std::max<uint32_t>(plan.chunks, 1), false);
 }
 
+Window::Window(std::unique_ptr<histograms::ExchangePlan> ownPlan, void *data, core::ExecContext *ctx, bool wide,
+               hipEvent_t arrived)
+    : ownedPlan(std::move(ownPlan)), plan(*ownedPlan), globalHistogram(nullptr), assignment(nullptr), ctx(ctx),
+      wide(wide), viewArrived(arrived) {
+  localWindowSize = plan.recvTotal;
+  this->data = data;
+  exchanged.assign(std::max<uint32_t>(plan.chunks, 1), true);
+}
+
+std::unique_ptr<Window> Window::chunkView(uint32_t chunk) const {
+  JOIN_ASSERT(chunk < plan.chunks, "Window", "chunk view %u of %u chunks", chunk, plan.chunks);
+  std::unique_ptr<histograms::ExchangePlan> v(new histograms::ExchangePlan(plan));
+  const uint32_t owned = (uint32_t)plan.owned.size();
+  v->segments.clear();
+  v->partSize.assign(owned, 0);
+  for (const histograms::Segment &s : plan.segments)
+    if (s.chunk == chunk) {
+      v->segments.push_back(s);
+      v->partSize[s.lp] += s.len;
+    }
+  v->lpBase.assign(owned + 1, 0);
+  for (uint32_t lp = 0; lp < owned; ++lp) v->lpBase[lp + 1] = v->lpBase[lp] + v->partSize[lp];
+  v->recvTotal = v->lpBase[owned];
+  hipEvent_t arrived = chunk < done.size() ? done[chunk] : nullptr;
+  return std::unique_ptr<Window>(new Window(std::move(v), data, ctx, wide, arrived));
+}
+
 Window::~Window() {
   for (auto e : ready) (void)hipEventDestroy(e);
   for (auto e : done) (void)hipEventDestroy(e);
@@ -152,6 +179,11 @@ void Window::exchange(const void *sendBuffer, uint32_t chunk) {
 }
 
 void Window::stop() {
+  if (ownedPlan) {  // chunk view
+    if (viewArrived) HIP_CHECK(hipStreamWaitEvent(ctx->stream(), viewArrived, 0));
+    open = false;
+    return;
+  }
   if (ctx->onDevice() && plan.numberOfNodes > 1)
     for (uint32_t c = 0; c < plan.chunks; ++c)
       if (exchanged[c]) HIP_CHECK(hipStreamWaitEvent(ctx->stream(), done[c], 0));

@@ -9,6 +9,8 @@
 // without a host round trip.
 #pragma once
 
+#include <memory>
+
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -33,6 +35,10 @@ class Window {
   // scatter (sampled network pass: no histograms, no exchange).
   Window(const histograms::ExchangePlan &plan, uint64_t capacityTuples, core::ExecContext *ctx, bool wide);
   ~Window();
+  // View of exchange chunk c alone (its segments; the data is shared): stop()
+  // waits for that chunk only, so the local pass and build/probe can run on a
+  // chunk while later chunks are still on the links.
+  std::unique_ptr<Window> chunkView(uint32_t chunk) const;
   Window(const Window &) = delete;
   Window &operator=(const Window &) = delete;
 
@@ -77,7 +83,11 @@ class Window {
   void *data;
 
  private:
+  Window(std::unique_ptr<histograms::ExchangePlan> ownPlan, void *data, core::ExecContext *ctx, bool wide,
+         hipEvent_t arrived);
+  std::unique_ptr<histograms::ExchangePlan> ownedPlan;  // chunk views only
   const histograms::ExchangePlan &plan;
+  hipEvent_t viewArrived = nullptr;  // chunk views: the parent's event for that chunk
   histograms::GlobalHistogram *globalHistogram;
   histograms::AssignmentMap *assignment;
   core::ExecContext *ctx;

@@ -120,6 +120,8 @@ void HashJoin::makeJoinPlan() {
       plan.sampledNetwork = eligible && small >= (16ull << 20);
   }
   plan.splitHistogram = config.splitHistogram && numberOfNodes > 1 && ctx->onDevice();
+  plan.pipelineOuter = config.pipelineOuter && numberOfNodes > 1 && ctx->onDevice() && !plan.materialize &&
+                       plan.twoLevel;
   JOIN_DEBUG("HashJoin", "%s", plan.describe().c_str());
   if (ctx->onDevice())
     for (auto &e : ev) HIP_CHECK(hipEventCreate(&e));
@@ -370,25 +372,46 @@ JoinResult HashJoin::runImpl() {
   trace.reset(new performance::TraceRange("local_processing"));
   std::unique_ptr<tasks::LocalPartitioning> lp(
       new tasks::LocalPartitioning(innerWindow, outerWindow, ctx, plan, localOverflowed));
-  TASK_QUEUE.push(lp.get());
   Measurements::stopLocalProcessingPreparations();
   Measurements::startLocalProcessing();
-  std::unique_ptr<tasks::BuildProbe> bp;
-  // Both tasks are owned here (lp is re-created if its sampled layout overflows).
-  while (!TASK_QUEUE.empty()) {
-    tasks::Task *t = TASK_QUEUE.front();
-    TASK_QUEUE.pop();
-    if (t->getType() == TASK_BUILD_PROBE) {
-      utils::faultPoint("build_probe");
-      bp->execute();
-      continue;
+  // Every build/probe of this join (one, or one per outer chunk when pipelined).
+  std::vector<std::unique_ptr<tasks::BuildProbe>> bps;
+  std::vector<std::unique_ptr<data::Window>> outerViews;
+  const uint32_t outerChunks = outerWindow->getPlan().chunks;
+  if (plan.pipelineOuter && !localOverflowed && outerChunks > 1) {
+    // ---- N > 1, counting: the outer relation is local-partitioned and probed
+    // chunk by chunk as its exchange chunks land (chunk views of the window),
+    // so after the last chunk arrives only its own share is left to do.  The
+    // inner tables are rebuilt per chunk (2-byte fragments, off the critical
+    // path while later chunks are on the links).
+    lp->partitionSide(innerWindow, 0);
+    for (uint32_t c = 0; c < outerChunks; ++c) {
+      outerViews.push_back(outerWindow->chunkView(c));
+      lp->partitionSide(outerViews.back().get(), 1 + (int)c);
+      if (c + 1 == outerChunks && dev) HIP_CHECK(hipEventRecord(ev[3], ctx->stream()));
+      if (c == 0) utils::faultPoint("build_probe");
+      bps.emplace_back(new tasks::BuildProbe(innerWindow, outerViews.back().get(), ctx, plan, config.outputCapacity));
+      bps.back()->execute();
     }
-    t->execute();
-    if (t->getType() == TASK_PARTITION) {
-      if (dev) HIP_CHECK(hipEventRecord(ev[3], ctx->stream()));
-      result.localItems = lp->workItems();
-      bp.reset(new tasks::BuildProbe(innerWindow, outerWindow, ctx, plan, config.outputCapacity));
-      TASK_QUEUE.push(bp.get());
+    result.localItems = lp->workItems();
+  } else {
+    TASK_QUEUE.push(lp.get());
+    // Both tasks are owned here (lp is re-created if its sampled layout overflows).
+    while (!TASK_QUEUE.empty()) {
+      tasks::Task *t = TASK_QUEUE.front();
+      TASK_QUEUE.pop();
+      if (t->getType() == TASK_BUILD_PROBE) {
+        utils::faultPoint("build_probe");
+        t->execute();
+        continue;
+      }
+      t->execute();
+      if (t->getType() == TASK_PARTITION) {
+        if (dev) HIP_CHECK(hipEventRecord(ev[3], ctx->stream()));
+        result.localItems = lp->workItems();
+        bps.emplace_back(new tasks::BuildProbe(innerWindow, outerWindow, ctx, plan, config.outputCapacity));
+        TASK_QUEUE.push(bps.back().get());
+      }
     }
   }
   trace.reset();  // roctx ranges nest: pop before the next push
@@ -397,35 +420,43 @@ JoinResult HashJoin::runImpl() {
   result.sampledLocal = lp->sampled();
   if (lp->sampled() && lp->overflowed()) {
     // A sampled slot overflowed (skew the sample missed): the build/probe ran
-    // on incomplete partitions.  Redo the local pass exactly, then the
-    // build/probe; later joins stay exact.
+    // on incomplete partitions.  Redo the local pass exactly over the whole
+    // windows, then the build/probe; later joins stay exact.
     localOverflowed = true;
     ++result.localFallbacks;
     result.sampledLocal = false;
-    bp.reset();
+    bps.clear();
+    outerViews.clear();
     lp.reset(new tasks::LocalPartitioning(innerWindow, outerWindow, ctx, plan, true));
     lp->execute();
     result.localItems = lp->workItems();
-    bp.reset(new tasks::BuildProbe(innerWindow, outerWindow, ctx, plan, config.outputCapacity));
-    bp->execute();
+    bps.emplace_back(new tasks::BuildProbe(innerWindow, outerWindow, ctx, plan, config.outputCapacity));
+    bps.back()->execute();
     if (dev) HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
     ctx->synchronize();
   }
-  while (bp->collect()) {  // rare: item list or output buffer overflowed -> exact re-run
-    ++result.reruns;
-    bp->execute();
-    if (dev) HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
-    ctx->synchronize();
-  }
+  for (auto &bp : bps)
+    while (bp->collect()) {  // rare: item list or output buffer overflowed -> exact re-run
+      ++result.reruns;
+      bp->execute();
+      if (dev) HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
+      ctx->synchronize();
+    }
   Measurements::stopLocalProcessing();
   const uint64_t t4 = nowUs();
 
-  result.localMatches = bp->getMatches();
-  result.outputPairs = plan.materialize ? std::min<uint64_t>(bp->getOutputCount(), UINT64_MAX) : 0;
-  result.outputOverflow = bp->outputOverflowed();
-  result.buildProbeItems = bp->getWorkItems();
-  output = bp->getOutput();
-  bp.reset();
+  result.localMatches = 0;
+  result.buildProbeItems = 0;
+  for (auto &bp : bps) {
+    result.localMatches += bp->getMatches();
+    result.buildProbeItems += bp->getWorkItems();
+  }
+  // Materializing joins have exactly one build/probe (never pipelined).
+  result.outputPairs = plan.materialize ? std::min<uint64_t>(bps.front()->getOutputCount(), UINT64_MAX) : 0;
+  result.outputOverflow = bps.front()->outputOverflowed();
+  output = bps.front()->getOutput();
+  bps.clear();
+  outerViews.clear();
   result.wireBytes = innerWindow->wireBytesSent() + outerWindow->wireBytesSent();
   result.innerReceived = innerWindow->computeLocalWindowSize();
   result.outerReceived = outerWindow->computeLocalWindowSize();

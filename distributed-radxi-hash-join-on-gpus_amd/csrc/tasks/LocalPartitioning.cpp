@@ -43,6 +43,10 @@ void LocalPartitioning::partition(data::Window *w, int which) {
     return;
   }
   const uint32_t bits = plan.twoLevel ? plan.localBits : 0, F = 1u << bits;
+  if ((size_t)which >= items.size()) {
+    items.resize(which + 1);
+    lpItemBegin.resize(which + 1);
+  }
   std::vector<kernels::LocalItem> &it = items[which];
   std::vector<uint32_t> &lb = lpItemBegin[which];
   it.clear();
@@ -59,6 +63,7 @@ void LocalPartitioning::partition(data::Window *w, int which) {
   }
   lb[owned] = (uint32_t)it.size();
   const uint32_t nItems = (uint32_t)it.size();
+  itemTotal += nItems;
   const uint32_t shift = wide ? plan.networkBits : plan.keyShift;
   // Split output columns (kernels.h, SplitLayout): device, compressed, planned to fit.
   kernels::SplitLayout split;
@@ -74,7 +79,7 @@ void LocalPartitioning::partition(data::Window *w, int which) {
       (plan.localHistogram == core::HistogramMode::Sampled ||
        (plan.localHistogram == core::HistogramMode::Auto && xp.recvTotal >= (16ull << 20)));
   if (sampledMode) {
-    sampledSide[which] = true;
+    anySampled = true;
     // One claim stream per network partition (its items are XCD-contiguous
     // except at group boundaries), so every final partition is one slot.
     for (auto &x : it) x.stream = x.lp;

@@ -38,9 +38,13 @@ class LocalPartitioning : public Task {
   void execute();
   task_type_t getType() { return TASK_PARTITION; }
 
+  // One side at a time (pipelined outer relation: one call per chunk view of
+  // the outer window, slot >= 1 distinct per call).
+  void partitionSide(data::Window *window, int slot) { partition(window, slot); }
+
   uint64_t partitionedElements() const { return elements; }
-  uint64_t workItems() const { return items[0].size() + items[1].size(); }
-  bool sampled() const { return sampledSide[0] || sampledSide[1]; }
+  uint64_t workItems() const { return itemTotal; }
+  bool sampled() const { return anySampled; }
   // After the stream is synchronised: did a sampled slot overflow?
   bool overflowed() const;
 
@@ -51,12 +55,14 @@ class LocalPartitioning : public Task {
   data::Window *windows[2];
   core::ExecContext *ctx;
   core::JoinPlan plan;
-  std::vector<kernels::LocalItem> items[2];
-  std::vector<uint32_t> lpItemBegin[2];
+  // Per side (slot): host item lists stay alive until the join ends (async H2D sources).
+  std::vector<std::vector<kernels::LocalItem>> items;
+  std::vector<std::vector<uint32_t>> lpItemBegin;
+  uint64_t itemTotal = 0;
   std::vector<uint64_t> zero;
   uint64_t elements = 0;
   bool forceExact;
-  bool sampledSide[2] = {false, false};
+  bool anySampled = false;
   unsigned int *overflowFlag = nullptr;  // device
 };
 
