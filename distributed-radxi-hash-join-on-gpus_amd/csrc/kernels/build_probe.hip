@@ -188,22 +188,25 @@ __device__ __forceinline__ void bpLoadSide(const void *__restrict__ src, const u
 // the fragment column is read as aligned 8-byte words (4 fragments each, one
 // 512-byte request per wave instruction instead of 128 bytes), elements
 // outside [begin, end) of a word are masked, and only a 32-bit fragment
-// array lives in registers: 5 workgroups (20 wave64s) per CU at 81 VGPRs,
-// no scratch (8 per CU would cap VGPRs at 64 and spill).
+// array lives in registers.  4 words per lane per batch (4096 fragments per
+// workgroup, one final partition's side) keep it at 50 VGPRs, so 8
+// workgroups (32 wave64s, 8 x 16 KiB of LDS) share a CU: 0.81 ms per 1B x 1B
+// join against 1.04 ms with 8 words per lane at 5 per CU (81 VGPRs).
 constexpr int BPD_T = 256;
-constexpr int BPD_K = 8;  // words per lane per batch: 8192 fragments per workgroup batch
+constexpr int BPD_K = 4;     // words per lane per batch: 4096 fragments per workgroup batch
+constexpr int BPD_MINB = 8;  // workgroups per CU
 
-template <bool FULL>
-__device__ __forceinline__ void bpdLoad(const uint64_t *__restrict__ w, uint32_t nw, uint32_t b0,
-                                        uint64_t (&v)[BPD_K]) {
+template <int K, bool FULL>
+__device__ __forceinline__ void bpdLoad(const uint64_t *__restrict__ w, uint32_t nw, uint32_t b0, uint64_t (&v)[K]) {
 #pragma unroll
-  for (int k = 0; k < BPD_K; ++k) {
+  for (int k = 0; k < K; ++k) {
     const uint32_t idx = b0 + k * BPD_T + threadIdx.x;
     if (FULL || idx < nw) v[k] = w[idx];
   }
 }
 
-__global__ __launch_bounds__(BPD_T, 5) void bpDirectSplitKernel(BPArgs a, const BPItem *__restrict__ items,
+template <int K, int MINB>
+__global__ __launch_bounds__(BPD_T, MINB) void bpDirectSplitKernel(BPArgs a, const BPItem *__restrict__ items,
                                                                  const uint32_t *__restrict__ nItemsPtr,
                                                                  uint32_t capacity) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -212,7 +215,7 @@ __global__ __launch_bounds__(BPD_T, 5) void bpDirectSplitKernel(BPArgs a, const 
   unsigned long long *wsum = reinterpret_cast<unsigned long long *>(smem + ((size_t)slots * 4 + 15) / 16 * 16);
   const uint64_t *R64 = reinterpret_cast<const uint64_t *>(a.Rhi);
   const uint64_t *S64 = reinterpret_cast<const uint64_t *>(a.Shi);
-  constexpr uint32_t WB = BPD_T * BPD_K;  // words per batch
+  constexpr uint32_t WB = BPD_T * K;  // words per batch
   const uint32_t t = threadIdx.x;
   const uint32_t nItems = min(*nItemsPtr, capacity);
   uint64_t matches = 0;
@@ -226,17 +229,17 @@ __global__ __launch_bounds__(BPD_T, 5) void bpDirectSplitKernel(BPArgs a, const 
     const uint64_t rw0 = rb >> 2, sw0 = sb >> 2;
     const uint32_t rnw = re > rb ? (uint32_t)(((re + 3) >> 2) - rw0) : 0;
     const uint32_t snw = se > sb ? (uint32_t)(((se + 3) >> 2) - sw0) : 0;
-    uint64_t rv[BPD_K], sv[BPD_K];
-    if (rnw >= WB) bpdLoad<true>(R64 + rw0, rnw, 0, rv);
-    else bpdLoad<false>(R64 + rw0, rnw, 0, rv);
-    if (snw >= WB) bpdLoad<true>(S64 + sw0, snw, 0, sv);
-    else bpdLoad<false>(S64 + sw0, snw, 0, sv);
+    uint64_t rv[K], sv[K];
+    if (rnw >= WB) bpdLoad<K, true>(R64 + rw0, rnw, 0, rv);
+    else bpdLoad<K, false>(R64 + rw0, rnw, 0, rv);
+    if (snw >= WB) bpdLoad<K, true>(S64 + sw0, snw, 0, sv);
+    else bpdLoad<K, false>(S64 + sw0, snw, 0, sv);
     for (uint32_t i = t; i < slots; i += BPD_T) cnt[i] = 0;
     __syncthreads();
     for (uint32_t b0 = 0; b0 < rnw; b0 += WB) {
-      if (b0) bpdLoad<false>(R64 + rw0, rnw, b0, rv);
+      if (b0) bpdLoad<K, false>(R64 + rw0, rnw, b0, rv);
 #pragma unroll
-      for (int k = 0; k < BPD_K; ++k) {
+      for (int k = 0; k < K; ++k) {
         const uint32_t idx = b0 + k * BPD_T + t;
         if (idx < rnw) {
           const uint64_t e0 = (rw0 + idx) << 2;
@@ -249,11 +252,11 @@ __global__ __launch_bounds__(BPD_T, 5) void bpDirectSplitKernel(BPArgs a, const 
     __syncthreads();
     for (uint32_t b0 = 0; b0 < snw; b0 += WB) {
       if (b0) {
-        if (b0 + WB <= snw) bpdLoad<true>(S64 + sw0, snw, b0, sv);
-        else bpdLoad<false>(S64 + sw0, snw, b0, sv);
+        if (b0 + WB <= snw) bpdLoad<K, true>(S64 + sw0, snw, b0, sv);
+        else bpdLoad<K, false>(S64 + sw0, snw, b0, sv);
       }
 #pragma unroll
-      for (int k = 0; k < BPD_K; ++k) {
+      for (int k = 0; k < K; ++k) {
         const uint32_t idx = b0 + k * BPD_T + t;
         if (idx < snw) {
           const uint64_t e0 = (sw0 + idx) << 2;
@@ -595,9 +598,10 @@ void buildProbe(const BPArgs &args, const BPItem *items, const uint32_t *nItems,
            a.fragShift);
   if (bpMode(a) == BP_CCOUNT && a.split && bpDirect(a) && !a.itemCounts) {
     const size_t ldsD = ((size_t(4) << a.fragBits) + 15) / 16 * 16 + 64;
-    const uint32_t perCuD = (uint32_t)std::min<size_t>(5, (160 * 1024) / ldsD);  // the kernel's occupancy target
+    const uint32_t perCuD = (uint32_t)std::min<size_t>(BPD_MINB, (160 * 1024) / ldsD);  // occupancy target
     const uint32_t blocksD = std::min<uint32_t>(capacity, 256 * std::max<uint32_t>(perCuD, 1));
-    hipLaunchKernelGGL(bpDirectSplitKernel, dim3(blocksD), dim3(BPD_T), ldsD, s, a, items, nItems, capacity);
+    hipLaunchKernelGGL((bpDirectSplitKernel<BPD_K, BPD_MINB>), dim3(blocksD), dim3(BPD_T), ldsD, s, a, items, nItems,
+                       capacity);
     HIP_CHECK_LAUNCH();
     return;
   }
