@@ -119,9 +119,10 @@ void HashJoin::makeJoinPlan() {
     else if (config.networkHistogram == core::HistogramMode::Auto)
       plan.sampledNetwork = eligible && small >= (16ull << 20);
   }
-  plan.splitHistogram = config.splitHistogram && numberOfNodes > 1 && ctx->onDevice();
-  plan.pipelineOuter = config.pipelineOuter && numberOfNodes > 1 && ctx->onDevice() && !plan.materialize &&
-                       plan.twoLevel;
+  // N > 1 pipelines (also on the host path, where they run in place: same
+  // logic, covered by the CPU tests).
+  plan.splitHistogram = config.splitHistogram && numberOfNodes > 1;
+  plan.pipelineOuter = config.pipelineOuter && numberOfNodes > 1 && !plan.materialize && plan.twoLevel;
   JOIN_DEBUG("HashJoin", "%s", plan.describe().c_str());
   if (ctx->onDevice())
     for (auto &e : ev) HIP_CHECK(hipEventCreate(&e));

@@ -55,9 +55,16 @@ void HistogramComputation::executeInner(uint32_t sampleStride) {
 }
 
 void HistogramComputation::launchOuter(hipStream_t exchangeStream) {
-  JOIN_ASSERT(ctx->onDevice(), "HistogramComputation", "split histograms run on the device path");
   histograms::LocalHistogram *h = outerRelationLocalHistogram.get();
   const size_t per = (size_t)h->getChunkCount() * h->getPartitionCount();
+  if (!ctx->onDevice()) {  // host path: the same sequence, completed in place
+    h->computeLocalHistogram();
+    outerGatherHostVec.resize(per * numberOfNodes);
+    ctx->comm()->allGatherHost(h->getChunkHistograms(), outerGatherHostVec.data(), per);
+    outerGatherHost = outerGatherHostVec.data();
+    outerLaunched = true;
+    return;
+  }
   if (!outerHistDone) HIP_CHECK(hipEventCreateWithFlags(&outerHistDone, hipEventDisableTiming));
   if (!outerGatherDone) HIP_CHECK(hipEventCreateWithFlags(&outerGatherDone, hipEventDisableTiming));
   h->computeLocalHistogramDevice();
@@ -74,7 +81,7 @@ void HistogramComputation::launchOuter(hipStream_t exchangeStream) {
 
 void HistogramComputation::finishOuter() {
   JOIN_ASSERT(outerLaunched, "HistogramComputation", "finishOuter() before launchOuter()");
-  utils::waitEvent(outerGatherDone, ctx->comm(), "outer histogram all-gather");
+  if (ctx->onDevice()) utils::waitEvent(outerGatherDone, ctx->comm(), "outer histogram all-gather");
   histograms::LocalHistogram *h = outerRelationLocalHistogram.get();
   const size_t per = (size_t)h->getChunkCount() * h->getPartitionCount();
   h->setChunkHistograms(outerGatherHost + per * nodeId);

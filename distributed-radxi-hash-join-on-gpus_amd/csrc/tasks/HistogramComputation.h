@@ -4,6 +4,7 @@
 #pragma once
 
 #include <memory>
+#include <vector>
 
 #include "../core/ExecContext.h"
 #include "../data/Relation.h"
@@ -79,7 +80,8 @@ class HistogramComputation : public Task {
  private:
   core::ExecContext *ctx;
   hipEvent_t outerHistDone = nullptr, outerGatherDone = nullptr;
-  uint64_t *outerGatherHost = nullptr;  // pinned (staging arena)
+  uint64_t *outerGatherHost = nullptr;  // pinned (staging arena); host path: outerGatherHostVec
+  std::vector<uint64_t> outerGatherHostVec;
   bool outerLaunched = false;
 };
 

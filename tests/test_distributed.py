@@ -157,9 +157,9 @@ def test_wire_codec_exchange(C, dev, n_ranks, chunks):
     assert pairs[:, 1].unique().numel() == exp  # every outer row matched once (unique inner keys)
 
 
-@pytest.mark.gpu
+@pytest.mark.parametrize("dev", devices())
 @pytest.mark.parametrize("n_ranks,chunks,mat", [(2, 1, False), (3, 4, True), (8, 2, False)])
-def test_split_histogram_pipeline(C, cuda, n_ranks, chunks, mat):
+def test_split_histogram_pipeline(C, dev, n_ranks, chunks, mat):
     """N > 1 device joins take the assignment from an outer-side estimate and
     run the outer exact histogram + its all-gather behind the inner exchange
     (JoinPlan.split_histogram).  Skewed outer side, LPT: counts and
@@ -175,8 +175,8 @@ def test_split_histogram_pipeline(C, cuda, n_ranks, chunks, mat):
             c.materialize = mat
             c.assignment = C.AssignmentPolicy.LPT
 
-        results, exp = run_ranks(C, n_ranks, "device", 300_007, 700_001, cfg_fn=cfg_fn, outer_dist="ZIPF",
-                                 theta=0.9, outputs=pairs if mat else None)
+        results, exp = run_ranks(C, n_ranks, "device" if dev == "cuda" else "host", 300_007, 700_001, cfg_fn=cfg_fn,
+                                 outer_dist="ZIPF", theta=0.9, outputs=pairs if mat else None)
         for res, plan in results:
             assert plan.split_histogram == split
             assert res["global_matches"] == exp
@@ -187,9 +187,9 @@ def test_split_histogram_pipeline(C, cuda, n_ranks, chunks, mat):
         assert torch.equal(out[True], out[False])
 
 
-@pytest.mark.gpu
+@pytest.mark.parametrize("dev", devices())
 @pytest.mark.parametrize("n_ranks,chunks,local", [(2, 2, "EXACT"), (3, 4, "SAMPLED"), (4, 3, "AUTO")])
-def test_pipelined_outer_chunks(C, cuda, n_ranks, chunks, local):
+def test_pipelined_outer_chunks(C, dev, n_ranks, chunks, local):
     """N > 1 counting joins local-partition and probe the outer relation one
     exchange chunk at a time (Window.chunkView); results equal the
     whole-window path, exact and sampled local passes, skewed outer side."""
@@ -199,7 +199,8 @@ def test_pipelined_outer_chunks(C, cuda, n_ranks, chunks, local):
             c.pipeline_outer = pipe
             c.chunks = chunks
             c.local_histogram = getattr(C.HistogramMode, local)
-        results, exp = run_ranks(C, n_ranks, "device", 400_009, 900_007, cfg_fn=cfg_fn, outer_dist="ZIPF", theta=0.8)
+        results, exp = run_ranks(C, n_ranks, "device" if dev == "cuda" else "host", 400_009, 900_007, cfg_fn=cfg_fn,
+                                 outer_dist="ZIPF", theta=0.8)
         for res, plan in results:
             assert plan.pipeline_outer == pipe
             assert res["global_matches"] == exp and res["local_fallbacks"] == 0
