@@ -105,13 +105,13 @@ void SampledNetworkPartitioning::layout() {
         s.cur32[i] = (uint32_t)s.start[i];
         s.end32[i] = (uint32_t)(s.start[i] + s.cap[i]);
       }
-      HIP_CHECK(hipMemcpyAsync(s.gcur, s.cur32.data(), s.cur32.size() * 4, hipMemcpyHostToDevice, ctx->stream()));
-      HIP_CHECK(hipMemcpyAsync(s.gend, s.end32.data(), s.end32.size() * 4, hipMemcpyHostToDevice, ctx->stream()));
+      ctx->copy(s.gcur, s.cur32.data(), s.cur32.size() * 4, true, false);
+      ctx->copy(s.gend, s.end32.data(), s.end32.size() * 4, true, false);
     } else {
       s.end64.resize((size_t)G * F);
       for (size_t i = 0; i < s.end64.size(); ++i) s.end64[i] = s.start[i] + s.cap[i];
-      HIP_CHECK(hipMemcpyAsync(s.gcur, s.start.data(), s.end64.size() * 8, hipMemcpyHostToDevice, ctx->stream()));
-      HIP_CHECK(hipMemcpyAsync(s.gend, s.end64.data(), s.end64.size() * 8, hipMemcpyHostToDevice, ctx->stream()));
+      ctx->copy(s.gcur, s.start.data(), s.end64.size() * 8, true, false);
+      ctx->copy(s.gend, s.end64.data(), s.end64.size() * 8, true, false);
     }
   }
 }
