@@ -236,6 +236,10 @@ JoinResult HashJoin::runImpl() {
   data::Window *innerWindow = nullptr, *outerWindow = nullptr;
   const bool sampled = plan.sampledNetwork && !sampledOverflowed;
   uint64_t t1, t2;
+  // Local pass (created early on the single-rank sampled path, which starts
+  // the inner relation's local pass while the outer scatter still runs).
+  std::unique_ptr<tasks::LocalPartitioning> lp;
+  bool networkEventRecorded = false;
   if (sampled) {
     // ---------------------------------------- single-rank sampled network pass
     sp.reset(new tasks::SampledNetworkPartitioning(innerRelation, outerRelation, ctx, plan,
@@ -248,17 +252,34 @@ JoinResult HashJoin::runImpl() {
                                         0, 0, 0);
     t1 = nowUs();
     Measurements::startWindowAllocation();
-    sp->layout();
+    sp->layoutSide(0);
     Measurements::stopWindowAllocation();
     t2 = nowUs();
     Measurements::startNetworkPartitioning();
     trace.reset();  // roctx ranges nest: pop before the next push
     utils::faultPoint("network");
     trace.reset(new performance::TraceRange("network_partitioning"));
-    if (sp->scatter()) {
+    // Host work of each side runs while the GPU works on the other: the
+    // outer layout during the inner scatter, the inner plan and local-pass
+    // setup during the outer scatter, the outer plan during the inner local
+    // pass.
+    sp->scatterSide(0);
+    sp->layoutSide(1);
+    sp->scatterSide(1);
+    if (dev) HIP_CHECK(hipEventRecord(ev[2], ctx->stream()));
+    networkEventRecorded = true;
+    bool ok = sp->finishSide(0);
+    if (ok) {
+      lp.reset(new tasks::LocalPartitioning(sp->innerWindow(), sp->outerWindow(), ctx, plan, localOverflowed));
+      lp->partitionSide(sp->innerWindow(), 0);
+      ok = sp->finishSide(1);
+    }
+    if (ok) {
       innerWindow = sp->innerWindow();
       outerWindow = sp->outerWindow();
     } else {
+      lp.reset();  // an inner local pass may be queued: harmless, its output is dropped
+      networkEventRecorded = false;
       // A slice overflowed: the sample missed skew.  Redo this join (and all
       // later ones) with the exact histogram path.
       sampledOverflowed = true;
@@ -362,7 +383,7 @@ JoinResult HashJoin::runImpl() {
     innerWindow->assertAllTuplesWritten();
     outerWindow->assertAllTuplesWritten();
   }
-  if (dev) HIP_CHECK(hipEventRecord(ev[2], ctx->stream()));
+  if (dev && !networkEventRecorded) HIP_CHECK(hipEventRecord(ev[2], ctx->stream()));
   Measurements::stopWaitingForNetworkCompletion();
   const uint64_t t3 = nowUs();
 
@@ -371,8 +392,7 @@ JoinResult HashJoin::runImpl() {
   trace.reset();  // roctx ranges nest: pop before the next push
   utils::faultPoint("local");
   trace.reset(new performance::TraceRange("local_processing"));
-  std::unique_ptr<tasks::LocalPartitioning> lp(
-      new tasks::LocalPartitioning(innerWindow, outerWindow, ctx, plan, localOverflowed));
+  if (!lp) lp.reset(new tasks::LocalPartitioning(innerWindow, outerWindow, ctx, plan, localOverflowed));
   Measurements::stopLocalProcessingPreparations();
   Measurements::startLocalProcessing();
   // Every build/probe of this join (one, or one per outer chunk when pipelined).

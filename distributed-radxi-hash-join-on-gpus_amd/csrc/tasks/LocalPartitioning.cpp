@@ -17,7 +17,8 @@ LocalPartitioning::LocalPartitioning(data::Window *innerWindow, data::Window *ou
 LocalPartitioning::~LocalPartitioning() {}
 
 void LocalPartitioning::execute() {
-  partition(windows[0], 0);
+  if (!innerDone) partition(windows[0], 0);
+  innerDone = true;
   partition(windows[1], 1);
 }
 

@@ -40,7 +40,10 @@ class LocalPartitioning : public Task {
 
   // One side at a time (pipelined outer relation: one call per chunk view of
   // the outer window, slot >= 1 distinct per call).
-  void partitionSide(data::Window *window, int slot) { partition(window, slot); }
+  void partitionSide(data::Window *window, int slot) {
+    partition(window, slot);
+    if (slot == 0) innerDone = true;
+  }
 
   uint64_t partitionedElements() const { return elements; }
   uint64_t workItems() const { return itemTotal; }
@@ -63,6 +66,7 @@ class LocalPartitioning : public Task {
   uint64_t elements = 0;
   bool forceExact;
   bool anySampled = false;
+  bool innerDone = false;  // partitionSide(inner, 0) ran already: execute() does the outer side only
   unsigned int *overflowFlag = nullptr;  // device
 };
 

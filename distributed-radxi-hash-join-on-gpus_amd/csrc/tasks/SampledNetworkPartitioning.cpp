@@ -21,7 +21,12 @@ SampledNetworkPartitioning::SampledNetworkPartitioning(data::Relation *innerRela
   sides[1].relation = outerRelation;
 }
 
-SampledNetworkPartitioning::~SampledNetworkPartitioning() {}
+SampledNetworkPartitioning::~SampledNetworkPartitioning() {
+  for (Side &s : sides) {
+    if (s.sampledReady) (void)hipEventDestroy(s.sampledReady);
+    if (s.cursorsReady) (void)hipEventDestroy(s.cursorsReady);
+  }
+}
 
 void SampledNetworkPartitioning::sample() {
   const uint32_t F = 1u << plan.networkBits;
@@ -34,15 +39,24 @@ void SampledNetworkPartitioning::sample() {
     kernels::netHistogram(s.relation->getData(), n, plan.networkBits, s.geom, blockHist, ctx->stream(), mix,
                           sampleStride);
     kernels::netGroupTotals(blockHist, F, s.geom.blocks, s.groupTotalsDev, ctx->stream());
-    s.sampled.assign((size_t)CLAIM_GROUPS * F, 0);
-    ctx->copy(s.sampled.data(), s.groupTotalsDev, s.sampled.size() * 8, false, true);
+    s.sampled = ctx->staging().getArray<uint64_t>((uint64_t)CLAIM_GROUPS * F);
+    HIP_CHECK(hipMemcpyAsync(s.sampled, s.groupTotalsDev, (size_t)CLAIM_GROUPS * F * 8, hipMemcpyDeviceToHost,
+                             ctx->stream()));
+    if (!s.sampledReady) HIP_CHECK(hipEventCreateWithFlags(&s.sampledReady, hipEventDisableTiming));
+    HIP_CHECK(hipEventRecord(s.sampledReady, ctx->stream()));
   }
-  HIP_CHECK(hipStreamSynchronize(ctx->stream()));
 }
 
 void SampledNetworkPartitioning::layout() {
+  layoutSide(0);
+  layoutSide(1);
+}
+
+void SampledNetworkPartitioning::layoutSide(int k) {
   const uint32_t F = 1u << plan.networkBits, G = CLAIM_GROUPS;
-  for (Side &s : sides) {
+  {
+    Side &s = sides[k];
+    HIP_CHECK(hipEventSynchronize(s.sampledReady));
     const uint64_t n = s.relation->getLocalSize();
     // Tuples each group scatters, and how many of them the sample read.
     std::vector<double> total(G, 0.0), seen(G, 0.0);
@@ -117,48 +131,52 @@ void SampledNetworkPartitioning::layout() {
 }
 
 bool SampledNetworkPartitioning::scatter() {
+  scatterSide(0);
+  scatterSide(1);
+  const bool ok0 = finishSide(0);
+  const bool ok1 = finishSide(1);
+  return ok0 && ok1;
+}
+
+void SampledNetworkPartitioning::scatterSide(int k) {
   const uint32_t F = 1u << plan.networkBits, G = CLAIM_GROUPS;
   const kernels::KeyMix mix{plan.keyMix ? 1u : 0u, plan.keyBits};
-  std::vector<std::vector<uint32_t>> c32(2);
-  for (int k = 0; k < 2; ++k) {
-    Side &s = sides[k];
-    const uint64_t n = s.relation->getLocalSize();
-    s.window->start();
-    const int nm = s.narrow ? 1 : 0;
-    if (plan.wide)
-      kernels::netScatterWide(s.relation->getData(), n, plan.networkBits, s.geom, 0, s.geom.blocks, s.gcur,
-                              static_cast<data::Tuple *>(s.window->getData()), ctx->stream(), mix, s.gend, nm);
-    else
-      kernels::netScatter(s.relation->getData(), n, plan.networkBits, plan.keyShift, s.geom, 0, s.geom.blocks,
-                          s.gcur, static_cast<uint64_t *>(s.window->getData()), ctx->stream(), plan.keyBits, mix,
-                          s.gend, nm);
-  }
-  for (int k = 0; k < 2; ++k) {
-    Side &s = sides[k];
-    s.fill.assign((size_t)G * F, 0);
-    if (s.narrow) {
-      c32[k].assign((size_t)G * F, 0);
-      HIP_CHECK(hipMemcpyAsync(c32[k].data(), s.gcur, c32[k].size() * 4, hipMemcpyDeviceToHost, ctx->stream()));
-    } else {
-      HIP_CHECK(hipMemcpyAsync(s.fill.data(), s.gcur, s.fill.size() * 8, hipMemcpyDeviceToHost, ctx->stream()));
-    }
-  }
-  HIP_CHECK(hipStreamSynchronize(ctx->stream()));
+  Side &s = sides[k];
+  const uint64_t n = s.relation->getLocalSize();
+  s.window->start();
+  const int nm = s.narrow ? 1 : 0;
+  if (plan.wide)
+    kernels::netScatterWide(s.relation->getData(), n, plan.networkBits, s.geom, 0, s.geom.blocks, s.gcur,
+                            static_cast<data::Tuple *>(s.window->getData()), ctx->stream(), mix, s.gend, nm);
+  else
+    kernels::netScatter(s.relation->getData(), n, plan.networkBits, plan.keyShift, s.geom, 0, s.geom.blocks, s.gcur,
+                        static_cast<uint64_t *>(s.window->getData()), ctx->stream(), plan.keyBits, mix, s.gend, nm);
+  const size_t bytes = (size_t)G * F * (s.narrow ? 4 : 8);
+  s.cursorsBack = ctx->staging().get(bytes);
+  HIP_CHECK(hipMemcpyAsync(s.cursorsBack, s.gcur, bytes, hipMemcpyDeviceToHost, ctx->stream()));
+  if (!s.cursorsReady) HIP_CHECK(hipEventCreateWithFlags(&s.cursorsReady, hipEventDisableTiming));
+  HIP_CHECK(hipEventRecord(s.cursorsReady, ctx->stream()));
+}
+
+bool SampledNetworkPartitioning::finishSide(int k) {
+  const uint32_t F = 1u << plan.networkBits, G = CLAIM_GROUPS;
+  Side &s = sides[k];
+  HIP_CHECK(hipEventSynchronize(s.cursorsReady));
+  s.fill.assign((size_t)G * F, 0);
+  const uint32_t *c32 = static_cast<const uint32_t *>(s.cursorsBack);
+  const uint64_t *c64 = static_cast<const uint64_t *>(s.cursorsBack);
   bool ok = true;
-  for (int k = 0; k < 2; ++k) {
-    Side &s = sides[k];
-    uint64_t sum = 0;
-    for (size_t i = 0; i < s.fill.size(); ++i) {
-      const uint64_t end = s.narrow ? c32[k][i] : s.fill[i];  // final claim cursor
-      s.fill[i] = end - s.start[i];
-      sum += s.fill[i];
-      if (s.fill[i] > s.cap[i]) ok = false;
-    }
-    HJ_CHECK(sum == s.relation->getLocalSize(), "sampled network pass claimed %lu of %lu tuples", (unsigned long)sum,
-             (unsigned long)s.relation->getLocalSize());
+  uint64_t sum = 0;
+  for (size_t i = 0; i < s.fill.size(); ++i) {
+    const uint64_t end = s.narrow ? c32[i] : c64[i];  // final claim cursor
+    s.fill[i] = end - s.start[i];
+    sum += s.fill[i];
+    if (s.fill[i] > s.cap[i]) ok = false;
   }
+  HJ_CHECK(sum == s.relation->getLocalSize(), "sampled network pass claimed %lu of %lu tuples", (unsigned long)sum,
+           (unsigned long)s.relation->getLocalSize());
   if (!ok) return false;
-  for (Side &s : sides) finishPlan(s);
+  finishPlan(s);
   return true;
 }
 

@@ -34,10 +34,22 @@ class SampledNetworkPartitioning {
   SampledNetworkPartitioning(data::Relation *innerRelation, data::Relation *outerRelation, core::ExecContext *ctx,
                              const core::JoinPlan &plan, uint32_t maxBlocks, uint32_t sampleStride);
   ~SampledNetworkPartitioning();
+  SampledNetworkPartitioning(const SampledNetworkPartitioning &) = delete;
+  SampledNetworkPartitioning &operator=(const SampledNetworkPartitioning &) = delete;
 
-  void sample();   // sampled histograms of both relations (one host sync)
-  void layout();   // slice layout + windows
-  bool scatter();  // bounded scatter of both relations, fill read back (one host sync); false = overflow
+  // Per side k (0 = inner, 1 = outer), so the host work of one side overlaps
+  // the other side's kernels: sample() enqueues both sampled histograms;
+  // layoutSide(k) waits for side k's counts only and uploads its slices;
+  // scatterSide(k) enqueues the bounded scatter and the read-back of its
+  // final cursors; finishSide(k) waits for those and builds the window plan
+  // (false = a slice overflowed).
+  void sample();
+  void layoutSide(int k);
+  void scatterSide(int k);
+  bool finishSide(int k);
+  // Both sides in order (one wait per side).
+  void layout();
+  bool scatter();
 
   data::Window *innerWindow() { return sides[0].window.get(); }
   data::Window *outerWindow() { return sides[1].window.get(); }
@@ -50,7 +62,9 @@ class SampledNetworkPartitioning {
     histograms::ExchangePlan xp;
     std::unique_ptr<data::Window> window;
     uint64_t *groupTotalsDev = nullptr;
-    std::vector<uint64_t> sampled;     // [groups][F] sampled counts
+    uint64_t *sampled = nullptr;       // [groups][F] sampled counts (pinned staging)
+    void *cursorsBack = nullptr;       // [groups][F] final claim cursors (pinned staging)
+    hipEvent_t sampledReady = nullptr, cursorsReady = nullptr;
     std::vector<uint64_t> start, cap;  // [groups][F] slice start / capacity (tuples)
     std::vector<uint64_t> fill;        // [groups][F] claimed after the scatter
     // Host sources of the asynchronous cursor uploads (alive until the join ends).
