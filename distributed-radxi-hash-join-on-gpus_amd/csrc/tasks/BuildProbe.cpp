@@ -106,6 +106,7 @@ void BuildProbe::execute() {
   kernels::bpEmit(args, counts, offsets, items, capacity, ctx->stream());
   if (!plan.materialize) {
     kernels::buildProbe(args, items, nItems, capacity, ctx->stream());
+    readBackCounters();
     return;
   }
   // Two-pass exact materialization: count per item -> 64-bit offsets -> place.
@@ -121,6 +122,15 @@ void BuildProbe::execute() {
   args.itemOffsets = itemOffsets;
   args.result = counters + 3;  // the count pass already counted
   kernels::buildProbe(args, items, nItems, capacity, ctx->stream());
+  readBackCounters();
+}
+
+// Enqueued behind the build/probe, so the join's final synchronisation also
+// completes the read-back (no separate blocking copy afterwards).
+void BuildProbe::readBackCounters() {
+  countersBack = ctx->staging().getArray<unsigned long long>(4);
+  HIP_CHECK(hipMemcpyAsync(countersBack, counters, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                           ctx->stream()));
 }
 
 bool BuildProbe::collect() {
@@ -129,7 +139,8 @@ bool BuildProbe::collect() {
     return false;
   }
   unsigned long long h[4];
-  HIP_CHECK(hipMemcpy(h, counters, sizeof(h), hipMemcpyDeviceToHost));
+  HIP_CHECK(hipStreamSynchronize(ctx->stream()));  // no-op after the caller's sync
+  std::memcpy(h, countersBack, sizeof(h));
   matches = h[0];
   outputCount = h[1];
   uint32_t items;

@@ -35,6 +35,11 @@ class BuildProbe : public Task {
   // true if the work-item list or the output buffer overflowed and
   // execute() must run again (it then sizes both exactly).
   bool collect();
+
+ private:
+  void readBackCounters();
+
+ public:
   uint64_t getMatches() const { return matches; }
   uint64_t getOutputCount() const { return outputCount; }
   uint32_t getWorkItems() const { return workItems; }
@@ -56,6 +61,7 @@ class BuildProbe : public Task {
   uint32_t capacity = 0;
   uint64_t outputCapacity = 0;
   unsigned long long *counters = nullptr;  // [0] matches [1] out cursor [2] item count (u32)
+  unsigned long long *countersBack = nullptr;  // pinned copy, enqueued at the end of execute()
   ulonglong2 *outPairs = nullptr;
   std::vector<uint64_t> refBounds;  // reference ctor: partition begin arrays
   uint64_t matches = 0, outputCount = 0;

@@ -24,9 +24,8 @@ void LocalPartitioning::execute() {
 
 bool LocalPartitioning::overflowed() const {
   if (!overflowFlag) return false;
-  unsigned int f = 0;
-  HIP_CHECK(hipMemcpy(&f, overflowFlag, sizeof(f), hipMemcpyDeviceToHost));
-  return f != 0;
+  HIP_CHECK(hipStreamSynchronize(ctx->stream()));  // no-op after the caller's sync
+  return *overflowBack != 0;
 }
 
 void LocalPartitioning::partition(data::Window *w, int which) {
@@ -109,6 +108,10 @@ void LocalPartitioning::partition(data::Window *w, int which) {
     kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, gcur, false, sout, ctx->stream(), gend,
                           split, plan.localGeometry);
     kernels::claimOverflow(gcur, gend, P, overflowFlag, ctx->stream());
+    // Read back with the join's final synchronisation (the flag accumulates
+    // over sides; the last copy enqueued sees them all).
+    if (!overflowBack) overflowBack = ctx->staging().getArray<unsigned int>(1);
+    HIP_CHECK(hipMemcpyAsync(overflowBack, overflowFlag, sizeof(unsigned int), hipMemcpyDeviceToHost, ctx->stream()));
     // Final claim cursors are the partition ends (valid when no slot overflowed).
     w->setPartitioned(sout, pbeg, bits, reinterpret_cast<const uint64_t *>(gcur), split.hi);
     return;

@@ -68,6 +68,7 @@ class LocalPartitioning : public Task {
   bool anySampled = false;
   bool innerDone = false;  // partitionSide(inner, 0) ran already: execute() does the outer side only
   unsigned int *overflowFlag = nullptr;  // device
+  unsigned int *overflowBack = nullptr;  // pinned copy, refreshed after every sampled side
 };
 
 }  // namespace tasks
