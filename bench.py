@@ -81,10 +81,13 @@ def main():
         if on_gpu:
             torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
+    # Grow the engine arena to the first warmup's peak right after it, so the
+    # remaining warmups (not the first timed join) are the first to run on the
+    # freshly reserved workspace; the first join pays a one-time hipMalloc.
+    for i in range(args.warmup):
         join.run()
-    # Grow the engine arena to the warmup's peak now: the first timed join must
-    # not pay for a one-time hipMalloc of the workspace (seconds at 100 GB).
+        if i == 0:
+            ctx.reset_scratch()
     ctx.reset_scratch()
     barrier()
     results = []
