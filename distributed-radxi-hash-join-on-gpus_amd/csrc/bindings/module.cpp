@@ -519,6 +519,7 @@ py::dict resultToDict(const operators::JoinResult &r) {
   d["sampled_network"] = r.sampledNetwork;
   d["network_fallbacks"] = r.networkFallbacks;
   d["sampled_local"] = r.sampledLocal;
+  d["bitmap_join"] = r.bitmapJoin;
   d["local_fallbacks"] = r.localFallbacks;
   d["join_ms"] = r.joinMs;
   d["histogram_ms"] = r.histogramMs;
@@ -601,6 +602,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("wire_codec", &core::JoinConfig::wireCodec)
       .def_readwrite("split_local", &core::JoinConfig::splitLocal)
       .def_readwrite("direct_count", &core::JoinConfig::directCount)
+      .def_readwrite("bitmap_join", &core::JoinConfig::bitmapJoin)
       .def_readwrite("split_histogram", &core::JoinConfig::splitHistogram)
       .def_readwrite("pipeline_outer", &core::JoinConfig::pipelineOuter)
       .def_readwrite("local_item_tiles", &core::JoinConfig::localItemTiles)
@@ -620,6 +622,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("network_bits", &core::JoinPlan::networkBits)
       .def_readonly("key_mix", &core::JoinPlan::keyMix)
       .def_readonly("sampled_network", &core::JoinPlan::sampledNetwork)
+      .def_readonly("bitmap_join", &core::JoinPlan::bitmapJoin)
+      .def_readonly("bitmap_bits", &core::JoinPlan::bitmapBits)
       .def_readonly("split_histogram", &core::JoinPlan::splitHistogram)
       .def_readonly("pipeline_outer", &core::JoinPlan::pipelineOuter)
       .def_readonly("local_bits", &core::JoinPlan::localBits)

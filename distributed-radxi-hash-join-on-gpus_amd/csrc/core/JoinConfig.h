@@ -77,6 +77,9 @@ struct JoinConfig {
   bool directCount = true;      // count-only build/probe: direct-addressed LDS counts when fragments are <= 13 bits
   bool splitHistogram = true;   // N > 1 on device: outer exact histogram overlaps the inner exchange
   bool pipelineOuter = true;    // N > 1 on device, counting: outer local pass + build/probe per received chunk
+  bool bitmapJoin = true;       // N == 1 on device, counting, sampled network pass: one LDS bitmap per network
+                                // partition instead of the local pass when the fragment range fits (unique inner
+                                // keys; a duplicate falls back to the two-level pass)
   uint32_t localItemTiles = 64; // local pass work item: up to this many 4096-tuple tiles of one segment
   uint32_t localGeometry = 0;   // local scatter workgroup geometry (0 = 1024 x 8; 1-4: sweep alternatives)
 
@@ -101,6 +104,8 @@ struct JoinPlan {
   bool sampledNetwork = false;  // single-rank network pass sized from a sampled histogram
   bool splitHistogram = false;  // N > 1: assignment from an outer estimate, outer exact histogram off the head
   bool pipelineOuter = false;   // N > 1 counting: outer local pass + build/probe per exchange chunk
+  bool bitmapJoin = false;      // single-level bitmap join (kernels::bitmapJoin) after the sampled network pass
+  uint32_t bitmapBits = 0;      // fragment bits per network partition (bitmap size 2^bitmapBits)
   HistogramMode localHistogram = HistogramMode::Exact;  // resolved per window size by LocalPartitioning
   uint32_t sampleStride = 64;
   uint32_t localSampleStride = 16;

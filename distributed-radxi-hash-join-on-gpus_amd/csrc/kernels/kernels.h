@@ -249,6 +249,17 @@ void bpEmit(const BPArgs &a, const uint32_t *counts, const uint32_t *offsets, BP
 // written by the scan, so no host round trip sits between plan and probe.
 void buildProbe(const BPArgs &a, const BPItem *items, const uint32_t *nItems, uint32_t capacity, hipStream_t s);
 
+// Single-level counting join of unique inner keys (bitmap_join.hip): one
+// workgroup per network partition sets a 2^bits LDS bitmap from the inner
+// fragments (value >> keyShift) and tests the outer ones.  Partition d is the
+// `groups` segments [start[d * groups + g], + len[...]) of each window.
+// *matches += matches; *dup |= 1 if an inner fragment repeats (or is out of
+// range): the count is then invalid and the caller falls back.
+constexpr uint32_t BITMAP_MAX_BITS = 20;  // 128 KiB of LDS
+void bitmapJoin(const uint64_t *r, const uint64_t *s, const uint64_t *rStart, const uint32_t *rLen,
+                const uint64_t *sStart, const uint32_t *sLen, uint32_t partitions, uint32_t groups,
+                uint32_t keyShift, uint32_t bits, unsigned long long *matches, uint32_t *dup, hipStream_t st);
+
 // ------------------------------------------------------------ wire codec
 // Exchange wire format for 8-byte CompressedTuples (N > 1).  On the wire a
 // tuple needs only its key fragment above the network digit (the receiver

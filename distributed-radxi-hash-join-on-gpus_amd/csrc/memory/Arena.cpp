@@ -2,6 +2,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 
 #include "../utils/Hip.h"
@@ -9,9 +11,31 @@
 namespace hpcjoin {
 namespace memory {
 
+// HPCJOIN_TRACE_ALLOC=1: one stderr line per raw allocation (arena growth or
+// fallback) with its duration -- steady-state joins should print none.
+static bool traceAlloc() {
+  static const bool on = [] {
+    const char *e = std::getenv("HPCJOIN_TRACE_ALLOC");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 void *Arena::rawAlloc(Location loc, uint64_t bytes, int device) {
   if (bytes == 0) bytes = ALIGNMENT;
   void *p = nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
+  struct Trace {
+    Location loc;
+    uint64_t bytes;
+    std::chrono::steady_clock::time_point t0;
+    ~Trace() {
+      if (traceAlloc())
+        std::fprintf(stderr, "[arena] alloc %s %.3f MB in %.3f ms\n",
+                     loc == Location::Device ? "device" : (loc == Location::Pinned ? "pinned" : "host"), bytes / 1e6,
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+  } trace{loc, bytes, t0};
   if (loc == Location::Device) {
     HIP_CHECK(hipSetDevice(device));
     HIP_CHECK(hipMalloc(&p, bytes));

@@ -119,6 +119,32 @@ void HashJoin::makeJoinPlan() {
     else if (config.networkHistogram == core::HistogramMode::Auto)
       plan.sampledNetwork = eligible && small >= (16ull << 20);
   }
+  // N == 1 counting joins: the single-level bitmap join replaces the local
+  // pass when the key fragment above the network digit fits an LDS bitmap.
+  // The network pass then runs at MAX_PART_BITS (2048 partitions: enough
+  // workgroups, and 2^19-bit = 64 KiB bitmaps for 1B dense keys).  The plan
+  // keeps a two-level split of the same total for the duplicate-key fallback.
+  if (config.bitmapJoin && plan.sampledNetwork && !plan.materialize && !plan.wide && !plan.keyMix) {
+    const uint32_t nb = config.networkBits ? config.networkBits : kernels::MAX_PART_BITS;
+    const uint32_t bits = plan.keyBits > nb ? plan.keyBits - nb : 0;
+    if (plan.keyBits < 64 && bits <= kernels::BITMAP_MAX_BITS && plan.keyShift + bits <= 64) {
+      if (nb != plan.networkBits) {
+        core::JoinConfig c2 = config;
+        const uint32_t total = plan.networkBits + plan.localBits;
+        c2.networkBits = nb;
+        c2.localBits = total > nb ? std::min<uint32_t>(total - nb, kernels::MAX_PART_BITS) : 1;
+        core::JoinPlan p2 = core::makePlan(c2, numberOfNodes, innerRelation->getGlobalSize(),
+                                           outerRelation->getGlobalSize(), mx[0], mx[1]);
+        p2.keyMix = plan.keyMix;
+        p2.sampledNetwork = plan.sampledNetwork;
+        p2.localHistogram = plan.localHistogram;
+        plan = p2;
+        planWireCodec(all, STATS, C);
+      }
+      plan.bitmapJoin = true;
+      plan.bitmapBits = bits;
+    }
+  }
   // N > 1 pipelines (also on the host path, where they run in place: same
   // logic, covered by the CPU tests).
   plan.splitHistogram = config.splitHistogram && numberOfNodes > 1;
@@ -196,6 +222,39 @@ bool HashJoin::lowKeyBitsSkewed() {
   return skewed;
 }
 
+void HashJoin::launchBitmapJoin(data::Window *inner, data::Window *outer) {
+  const uint32_t F = 1u << plan.networkBits, G = kernels::CLAIM_GROUPS;
+  uint64_t *dStart[2];
+  uint32_t *dLen[2];
+  data::Window *w[2] = {inner, outer};
+  for (int k = 0; k < 2; ++k) {
+    bmStart[k].assign((size_t)F * G, 0);
+    bmLen[k].assign((size_t)F * G, 0);
+    for (const histograms::Segment &sg : w[k]->getPlan().segments) {
+      HJ_CHECK(sg.lp < F && sg.source < G && sg.len < (1ull << 32), "bitmap join: segment (%u, %u) of %lu tuples",
+               sg.lp, sg.source, (unsigned long)sg.len);
+      const size_t i = (size_t)sg.lp * G + sg.source;
+      HJ_CHECK(bmLen[k][i] == 0, "bitmap join: two segments for partition %u, group %u", sg.lp, sg.source);
+      bmStart[k][i] = sg.begin;
+      bmLen[k][i] = (uint32_t)sg.len;
+    }
+    dStart[k] = ctx->workspace().getArray<uint64_t>((uint64_t)F * G);
+    dLen[k] = ctx->workspace().getArray<uint32_t>((uint64_t)F * G);
+    ctx->copy(dStart[k], bmStart[k].data(), bmStart[k].size() * 8, true, false);
+    ctx->copy(dLen[k], bmLen[k].data(), bmLen[k].size() * 4, true, false);
+  }
+  unsigned long long *dOut = ctx->workspace().getArray<unsigned long long>(2);
+  HIP_CHECK(hipMemsetAsync(dOut, 0, 16, ctx->stream()));
+  HIP_CHECK(hipEventRecord(ev[3], ctx->stream()));
+  utils::faultPoint("build_probe");
+  kernels::bitmapJoin(static_cast<const uint64_t *>(inner->getData()), static_cast<const uint64_t *>(outer->getData()),
+                      dStart[0], dLen[0], dStart[1], dLen[1], F, G, plan.keyShift, plan.bitmapBits, dOut,
+                      reinterpret_cast<uint32_t *>(dOut + 1), ctx->stream());
+  HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
+  bmBack = ctx->staging().getArray<unsigned long long>(2);
+  HIP_CHECK(hipMemcpyAsync(bmBack, dOut, 16, hipMemcpyDeviceToHost, ctx->stream()));
+}
+
 void HashJoin::join() {
   run();
   RESULT_COUNTER = result.localMatches;
@@ -240,6 +299,7 @@ JoinResult HashJoin::runImpl() {
   // the inner relation's local pass while the outer scatter still runs).
   std::unique_ptr<tasks::LocalPartitioning> lp;
   bool networkEventRecorded = false;
+  bool bitmapLaunched = false, bitmapDone = false;
   if (sampled) {
     // ---------------------------------------- single-rank sampled network pass
     sp.reset(new tasks::SampledNetworkPartitioning(innerRelation, outerRelation, ctx, plan,
@@ -269,7 +329,13 @@ JoinResult HashJoin::runImpl() {
     if (dev) HIP_CHECK(hipEventRecord(ev[2], ctx->stream()));
     networkEventRecorded = true;
     bool ok = sp->finishSide(0);
-    if (ok) {
+    if (ok && plan.bitmapJoin) {
+      ok = sp->finishSide(1);
+      if (ok) {
+        launchBitmapJoin(sp->innerWindow(), sp->outerWindow());
+        bitmapLaunched = true;
+      }
+    } else if (ok) {
       lp.reset(new tasks::LocalPartitioning(sp->innerWindow(), sp->outerWindow(), ctx, plan, localOverflowed));
       lp->partitionSide(sp->innerWindow(), 0);
       ok = sp->finishSide(1);
@@ -392,12 +458,31 @@ JoinResult HashJoin::runImpl() {
   trace.reset();  // roctx ranges nest: pop before the next push
   utils::faultPoint("local");
   trace.reset(new performance::TraceRange("local_processing"));
-  if (!lp) lp.reset(new tasks::LocalPartitioning(innerWindow, outerWindow, ctx, plan, localOverflowed));
-  Measurements::stopLocalProcessingPreparations();
-  Measurements::startLocalProcessing();
   // Every build/probe of this join (one, or one per outer chunk when pipelined).
   std::vector<std::unique_ptr<tasks::BuildProbe>> bps;
   std::vector<std::unique_ptr<data::Window>> outerViews;
+  uint64_t bitmapMatches = 0;
+  if (bitmapLaunched) {
+    Measurements::stopLocalProcessingPreparations();
+    Measurements::startLocalProcessing();
+    ctx->synchronize();
+    if (bmBack[1] == 0) {
+      bitmapMatches = bmBack[0];
+      bitmapDone = true;
+    } else {
+      // A repeated (or out-of-range) inner key fragment: the bitmap cannot
+      // count it.  Run the two-level pass on the same windows; later joins
+      // skip the bitmap.
+      plan.bitmapJoin = false;
+      ++result.localFallbacks;
+    }
+  }
+  if (!bitmapDone) {
+  if (!lp) lp.reset(new tasks::LocalPartitioning(innerWindow, outerWindow, ctx, plan, localOverflowed));
+  if (!bitmapLaunched) {
+    Measurements::stopLocalProcessingPreparations();
+    Measurements::startLocalProcessing();
+  }
   const uint32_t outerChunks = outerWindow->getPlan().chunks;
   if (plan.pipelineOuter && !localOverflowed && outerChunks > 1) {
     // ---- N > 1, counting: the outer relation is local-partitioned and probed
@@ -463,19 +548,22 @@ JoinResult HashJoin::runImpl() {
       if (dev) HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
       ctx->synchronize();
     }
+  }  // !bitmapDone
   Measurements::stopLocalProcessing();
   const uint64_t t4 = nowUs();
 
-  result.localMatches = 0;
-  result.buildProbeItems = 0;
+  result.localMatches = bitmapMatches;
+  result.buildProbeItems = bitmapDone ? (1ull << plan.networkBits) : 0;
+  result.bitmapJoin = bitmapDone;
   for (auto &bp : bps) {
     result.localMatches += bp->getMatches();
     result.buildProbeItems += bp->getWorkItems();
   }
   // Materializing joins have exactly one build/probe (never pipelined).
-  result.outputPairs = plan.materialize ? std::min<uint64_t>(bps.front()->getOutputCount(), UINT64_MAX) : 0;
-  result.outputOverflow = bps.front()->outputOverflowed();
-  output = bps.front()->getOutput();
+  result.outputPairs =
+      plan.materialize && !bps.empty() ? std::min<uint64_t>(bps.front()->getOutputCount(), UINT64_MAX) : 0;
+  result.outputOverflow = !bps.empty() && bps.front()->outputOverflowed();
+  output = bps.empty() ? nullptr : bps.front()->getOutput();
   bps.clear();
   outerViews.clear();
   result.wireBytes = innerWindow->wireBytesSent() + outerWindow->wireBytesSent();

@@ -15,6 +15,7 @@
 #include <cstdint>
 #include <memory>
 #include <queue>
+#include <vector>
 
 #include "../core/ExecContext.h"
 #include "../core/JoinConfig.h"
@@ -22,6 +23,9 @@
 #include "../tasks/Task.h"
 
 namespace hpcjoin {
+namespace data {
+class Window;
+}
 namespace operators {
 
 struct JoinResult {
@@ -41,6 +45,7 @@ struct JoinResult {
   bool sampledNetwork = false;     // network pass sized from a sampled histogram (N == 1)
   uint32_t networkFallbacks = 0;   // sampled pass overflowed -> exact re-run inside this join
   bool sampledLocal = false;       // local pass sized from a sampled histogram
+  bool bitmapJoin = false;         // single-level bitmap join counted the matches (no local pass)
   uint32_t localFallbacks = 0;     // sampled local pass overflowed -> exact re-run
 };
 
@@ -87,6 +92,12 @@ class HashJoin {
   JoinResult result;
   bool sampledOverflowed = false;  // sticky: exact histograms after a sampled pass overflowed
   bool localOverflowed = false;    // sticky: exact local pass after a sampled one overflowed
+  // Single-level bitmap join (plan.bitmapJoin): enqueue kernels::bitmapJoin over
+  // the two sampled-pass windows and the read-back of {matches, dup}.
+  void launchBitmapJoin(data::Window *inner, data::Window *outer);
+  std::vector<uint64_t> bmStart[2];
+  std::vector<uint32_t> bmLen[2];
+  unsigned long long *bmBack = nullptr;  // pinned: {matches, dup}
   const ulonglong2 *output = nullptr;
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
 };

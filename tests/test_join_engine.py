@@ -171,6 +171,7 @@ def test_sampled_network_pass(C, cuda, dist, fmt, mat):
         cfg.local_histogram = getattr(C.HistogramMode, mode)
         cfg.format = getattr(C.TupleFormat, fmt)
         cfg.materialize = mat
+        cfg.bitmap_join = False  # the two-level pass is under test here
         res, exp, j = run_join(C, "cuda", G_R, G_S, dist, cfg=cfg)
         assert j.plan.sampled_network == (mode == "SAMPLED")
         assert res["sampled_network"] == (mode == "SAMPLED") and res["network_fallbacks"] == 0
@@ -327,3 +328,51 @@ def test_materialize_split_duplicates(C, cuda, r_chunk):
     keyS[St[:, 1]] = St[:, 0]
     assert torch.equal(keyR[pairs[:, 0]], keyS[pairs[:, 1]])
     assert torch.unique(pairs[:, 0] * G_S + pairs[:, 1]).numel() == exp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dist", ["UNIQUE", "UNIFORM", "ZIPF"])
+def test_bitmap_join(C, cuda, dist):
+    """Single-level bitmap join (N == 1, counting, sampled network pass): one
+    LDS bitmap per 2048-way network partition, no local pass; counts equal
+    the oracle and the two-level path, foreign-key outer sides included."""
+    G_R, G_S = 1 << 24, (1 << 24) + 4321
+    counts = {}
+    for bitmap in (True, False):
+        cfg = C.JoinConfig()
+        cfg.network_histogram = C.HistogramMode.SAMPLED
+        cfg.bitmap_join = bitmap
+        res, exp, j = run_join(C, "cuda", G_R, G_S, dist, cfg=cfg, theta=0.9)
+        assert j.plan.bitmap_join == bitmap and res["bitmap_join"] == bitmap
+        if bitmap:
+            assert j.plan.network_bits == 11 and j.plan.bitmap_bits == j.plan.key_bits - 11
+            assert res["local_fallbacks"] == 0 and res["local_items"] == 0
+        assert res["global_matches"] == exp
+        for _ in range(2):
+            assert j.run()["global_matches"] == exp
+        counts[bitmap] = res["global_matches"]
+    assert counts[True] == counts[False]
+
+
+@pytest.mark.gpu
+def test_bitmap_join_duplicate_inner_falls_back(C, cuda):
+    """A repeated inner key cannot be counted by a bitmap: the kernel flags it,
+    the same join finishes on the two-level pass (exact count), and later
+    joins skip the bitmap."""
+    import torch
+    n = 1 << 24
+    i = torch.arange(n, device="cuda")
+    keys = i.clone()
+    keys[n // 2] = keys[n // 3]  # one duplicate inner key
+    R = torch.stack([keys, i], 1).contiguous()
+    S = torch.stack([i.flip(0), i], 1).contiguous()
+    ctx = C.ExecContext("device", 0, C.LocalCommunicator())
+    cfg = C.JoinConfig()
+    cfg.network_histogram = C.HistogramMode.SAMPLED
+    j = C.HashJoin(C.Relation.from_tensor(R, n), C.Relation.from_tensor(S, n), ctx, cfg)
+    assert j.plan.bitmap_join
+    exp = n  # key n//2 lost its inner row, key n//3 matches twice
+    res = j.run()
+    assert res["local_fallbacks"] == 1 and not res["bitmap_join"] and res["global_matches"] == exp
+    res = j.run()
+    assert res["local_fallbacks"] == 0 and not res["bitmap_join"] and res["global_matches"] == exp
