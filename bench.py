@@ -141,7 +141,10 @@ def main():
                        "local_items": results[-1]["local_items"], "workspace_GB": round(ctx.workspace_capacity() / 1e9, 2),
                        "workspace_peak_GB": round(ctx.workspace_peak() / 1e9, 2),
                        "step_ms": [round(r["join_ms"], 2) for r in results],
-                       "step_dev_network_ms": [round(r["dev_network_ms"], 2) for r in results],
+                       "step_phases_ms": [[round(r[k], 2) for k in ("histogram_ms", "network_ms", "local_ms",
+                                                                      "dev_histogram_ms", "dev_network_ms",
+                                                                      "dev_local_partition_ms", "dev_build_probe_ms")]
+                                          for r in results],
                        "setup_ms": [round(r["setup_ms"], 2) for r in results],
                        "teardown_ms": [round(r["teardown_ms"], 2) for r in results]},
             "device": torch.cuda.get_device_name(0) if on_gpu else "cpu",

@@ -23,6 +23,7 @@
 #include "device_common.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <type_traits>
 
@@ -549,12 +550,13 @@ static bool digitFitsOnTop(uint32_t bits, uint32_t keyShift, uint32_t keyBits) {
 // ablation on MI355X: 1024 threads x 8 tuples per LDS tile = 8192-tuple
 // tiles, one workgroup per CU).
 constexpr int CL_NTH = 1024;
-constexpr int CL_IPT = 8;
+constexpr int CL_IPT_DEFAULT = 8;
+constexpr int CL_IPT = CL_IPT_DEFAULT;
 
-template <class Pol>
-static void launchNetClaim(const Pol &pol, const data::Tuple *in, uint64_t n, uint32_t bits,
-                           const PartitionGeometry &g, uint32_t blockBegin, uint32_t blockEnd, void *gcur,
-                           void *out, hipStream_t s, const void *gend, bool narrow) {
+template <class Pol, int CL_IPT>
+static void launchNetClaimIpt(const Pol &pol, const data::Tuple *in, uint64_t n, uint32_t bits,
+                              const PartitionGeometry &g, uint32_t blockBegin, uint32_t blockEnd, void *gcur,
+                              void *out, hipStream_t s, const void *gend, bool narrow) {
   const uint32_t F = 1u << bits;
   const auto *src = reinterpret_cast<const typename Pol::InT *>(in);
   auto *dst = reinterpret_cast<typename Pol::OutT *>(out);
@@ -583,6 +585,26 @@ static void launchNetClaim(const Pol &pol, const data::Tuple *in, uint64_t n, ui
                          lds, s, src, n, g.tilesPerBlock, F, pol, blockBegin, gc, dst, nullptr);
   }
   HIP_CHECK_LAUNCH();
+}
+
+// Tile of the claim scatter: 8192 tuples, or 15360 when the fan-out is 2048
+// (HPCJOIN_NET_IPT=15): longer runs per partition and tile, one workgroup per CU.
+static int netIpt() {
+  static const int v = [] {
+    const char *e = std::getenv("HPCJOIN_NET_IPT");
+    return e ? std::atoi(e) : CL_IPT_DEFAULT;
+  }();
+  return v;
+}
+
+template <class Pol>
+static void launchNetClaim(const Pol &pol, const data::Tuple *in, uint64_t n, uint32_t bits,
+                           const PartitionGeometry &g, uint32_t blockBegin, uint32_t blockEnd, void *gcur,
+                           void *out, hipStream_t s, const void *gend, bool narrow) {
+  if (netIpt() == 15 && narrow && bits == MAX_PART_BITS)
+    launchNetClaimIpt<Pol, 15>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
+  else
+    launchNetClaimIpt<Pol, CL_IPT_DEFAULT>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
 }
 
 void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift, const PartitionGeometry &g,

@@ -334,7 +334,7 @@ def test_materialize_split_duplicates(C, cuda, r_chunk):
 @pytest.mark.parametrize("dist", ["UNIQUE", "UNIFORM", "ZIPF"])
 def test_bitmap_join(C, cuda, dist):
     """Single-level bitmap join (N == 1, counting, sampled network pass): one
-    LDS bitmap per 2048-way network partition, no local pass; counts equal
+    LDS bitmap per 1024-way network partition, no local pass; counts equal
     the oracle and the two-level path, foreign-key outer sides included."""
     G_R, G_S = 1 << 24, (1 << 24) + 4321
     counts = {}
@@ -345,7 +345,7 @@ def test_bitmap_join(C, cuda, dist):
         res, exp, j = run_join(C, "cuda", G_R, G_S, dist, cfg=cfg, theta=0.9)
         assert j.plan.bitmap_join == bitmap and res["bitmap_join"] == bitmap
         if bitmap:
-            assert j.plan.network_bits == 11 and j.plan.bitmap_bits == j.plan.key_bits - 11
+            assert j.plan.network_bits == 10 and j.plan.bitmap_bits == j.plan.key_bits - 10
             assert res["local_fallbacks"] == 0 and res["local_items"] == 0
         assert res["global_matches"] == exp
         for _ in range(2):
