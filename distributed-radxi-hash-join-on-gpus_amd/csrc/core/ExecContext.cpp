@@ -29,6 +29,7 @@ ExecContext::ExecContext(Location loc, int device, comm::Communicator *comm)
 }
 
 ExecContext::~ExecContext() {
+  for (hipEvent_t e : events_) (void)hipEventDestroy(e);
   workspace_.reset();
   staging_.reset();
   if (stream_) (void)hipStreamDestroy(stream_);
@@ -76,6 +77,16 @@ void ExecContext::copy(void *dst, const void *src, uint64_t bytes, bool toDevice
 void ExecContext::resetScratch() {
   workspace_->reset();
   staging_->reset();
+  eventsUsed_ = 0;
+}
+
+hipEvent_t ExecContext::acquireEvent() {
+  if (eventsUsed_ == events_.size()) {
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    events_.push_back(e);
+  }
+  return events_[eventsUsed_++];
 }
 
 }  // namespace core

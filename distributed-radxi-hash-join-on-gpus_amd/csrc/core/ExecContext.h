@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <memory>
+#include <vector>
 
 #include "JoinConfig.h"
 #include "Types.h"
@@ -43,9 +44,15 @@ class ExecContext {
   void synchronize() const;                 // compute + comm streams
   void copy(void *dst, const void *src, uint64_t bytes, bool toDevice, bool fromDevice) const;  // async on stream()
   void resetScratch();
+  // Synchronisation event (timing disabled) from a per-context pool, valid
+  // until the next resetScratch(): joins reuse the same events instead of
+  // creating and destroying several per join.
+  hipEvent_t acquireEvent();
 
  private:
   Location loc_;
+  std::vector<hipEvent_t> events_;
+  size_t eventsUsed_ = 0;
   int device_;
   comm::Communicator *comm_;
   hipStream_t stream_ = nullptr;

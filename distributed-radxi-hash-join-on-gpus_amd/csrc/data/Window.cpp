@@ -21,8 +21,8 @@ Window::Window(const histograms::ExchangePlan &plan, histograms::GlobalHistogram
     ready.resize(plan.chunks);
     done.resize(plan.chunks);
     for (uint32_t c = 0; c < plan.chunks; ++c) {
-      HIP_CHECK(hipEventCreateWithFlags(&ready[c], hipEventDisableTiming));
-      HIP_CHECK(hipEventCreateWithFlags(&done[c], hipEventDisableTiming));
+      ready[c] = ctx->acquireEvent();
+      done[c] = ctx->acquireEvent();
     }
   }
 }
@@ -61,11 +61,7 @@ std::unique_ptr<Window> Window::chunkView(uint32_t chunk) const {
   return std::unique_ptr<Window>(new Window(std::move(v), data, ctx, wide, arrived));
 }
 
-Window::~Window() {
-  for (auto e : ready) (void)hipEventDestroy(e);
-  for (auto e : done) (void)hipEventDestroy(e);
-  for (auto e : wired) (void)hipEventDestroy(e);
-}
+Window::~Window() = default;  // events belong to the context pool
 
 void Window::setWireCodec(const kernels::WireCodec &c, const std::vector<uint64_t> &bases) {
   JOIN_ASSERT(!wide || c.w == 0, "Window", "the wire codec packs 8-byte CompressedTuples only");
@@ -77,7 +73,7 @@ void Window::setWireCodec(const kernels::WireCodec &c, const std::vector<uint64_
   ridBaseChunks = c.w ? (uint32_t)(bases.size() / plan.numberOfNodes) : 1;
   if (codec.w && ctx->onDevice() && plan.numberOfNodes > 1 && wired.empty()) {
     wired.resize(plan.chunks);
-    for (auto &e : wired) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto &e : wired) e = ctx->acquireEvent();
   }
 }
 

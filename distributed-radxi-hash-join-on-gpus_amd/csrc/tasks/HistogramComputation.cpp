@@ -31,10 +31,7 @@ HistogramComputation::HistogramComputation(uint32_t numberOfNodes, uint32_t node
                                                outerRelationGlobalHistogram.get(), assignment.get()));
 }
 
-HistogramComputation::~HistogramComputation() {
-  if (outerHistDone) (void)hipEventDestroy(outerHistDone);
-  if (outerGatherDone) (void)hipEventDestroy(outerGatherDone);
-}
+HistogramComputation::~HistogramComputation() = default;  // events belong to the context pool
 
 void HistogramComputation::executeInner(uint32_t sampleStride) {
   uint64_t t0 = performance::nowUs();
@@ -65,8 +62,8 @@ void HistogramComputation::launchOuter(hipStream_t exchangeStream) {
     outerLaunched = true;
     return;
   }
-  if (!outerHistDone) HIP_CHECK(hipEventCreateWithFlags(&outerHistDone, hipEventDisableTiming));
-  if (!outerGatherDone) HIP_CHECK(hipEventCreateWithFlags(&outerGatherDone, hipEventDisableTiming));
+  if (!outerHistDone) outerHistDone = ctx->acquireEvent();
+  if (!outerGatherDone) outerGatherDone = ctx->acquireEvent();
   h->computeLocalHistogramDevice();
   HIP_CHECK(hipEventRecord(outerHistDone, ctx->stream()));
   uint64_t *gatherDev = ctx->workspace().getArray<uint64_t>(per * numberOfNodes);

@@ -21,12 +21,7 @@ SampledNetworkPartitioning::SampledNetworkPartitioning(data::Relation *innerRela
   sides[1].relation = outerRelation;
 }
 
-SampledNetworkPartitioning::~SampledNetworkPartitioning() {
-  for (Side &s : sides) {
-    if (s.sampledReady) (void)hipEventDestroy(s.sampledReady);
-    if (s.cursorsReady) (void)hipEventDestroy(s.cursorsReady);
-  }
-}
+SampledNetworkPartitioning::~SampledNetworkPartitioning() = default;  // events belong to the context pool
 
 void SampledNetworkPartitioning::sample() {
   const uint32_t F = 1u << plan.networkBits;
@@ -42,7 +37,7 @@ void SampledNetworkPartitioning::sample() {
     s.sampled = ctx->staging().getArray<uint64_t>((uint64_t)CLAIM_GROUPS * F);
     HIP_CHECK(hipMemcpyAsync(s.sampled, s.groupTotalsDev, (size_t)CLAIM_GROUPS * F * 8, hipMemcpyDeviceToHost,
                              ctx->stream()));
-    if (!s.sampledReady) HIP_CHECK(hipEventCreateWithFlags(&s.sampledReady, hipEventDisableTiming));
+    if (!s.sampledReady) s.sampledReady = ctx->acquireEvent();
     HIP_CHECK(hipEventRecord(s.sampledReady, ctx->stream()));
   }
 }
@@ -154,7 +149,7 @@ void SampledNetworkPartitioning::scatterSide(int k) {
   const size_t bytes = (size_t)G * F * (s.narrow ? 4 : 8);
   s.cursorsBack = ctx->staging().get(bytes);
   HIP_CHECK(hipMemcpyAsync(s.cursorsBack, s.gcur, bytes, hipMemcpyDeviceToHost, ctx->stream()));
-  if (!s.cursorsReady) HIP_CHECK(hipEventCreateWithFlags(&s.cursorsReady, hipEventDisableTiming));
+  if (!s.cursorsReady) s.cursorsReady = ctx->acquireEvent();
   HIP_CHECK(hipEventRecord(s.cursorsReady, ctx->stream()));
 }
 
