@@ -20,6 +20,12 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# Host<->device copies of a join are small (plan uploads, cursor and counter
+# read-backs): run them as blit kernels on the compute queue, not on the SDMA
+# engines.  With SDMA on, about every second process stalled one join (the
+# 4th) by 17-45 ms inside the first small copy; with it off 5/5 runs were
+# clean (profiles/r1_sdma_outlier.md).  Must be set before HIP initialises.
+os.environ.setdefault("HSA_ENABLE_SDMA", "0")
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
