@@ -228,31 +228,31 @@ bool HashJoin::lowKeyBitsSkewed() {
 
 void HashJoin::launchBitmapJoin(data::Window *inner, data::Window *outer) {
   const uint32_t F = 1u << plan.networkBits, G = kernels::CLAIM_GROUPS;
-  uint64_t *dStart[2];
-  uint32_t *dLen[2];
+  const size_t n = (size_t)F * G;
+  // One upload: [inner starts | outer starts] (u64), [inner lens | outer lens]
+  // (u32), then the zeroed {matches, dup} words.
+  const size_t words = 2 * n + n + 2;  // u64 words: 2n starts, 2n u32 lens = n words, 2 counters
+  bmUpload.assign(words, 0);
+  uint64_t *starts = bmUpload.data();
+  uint32_t *lens = reinterpret_cast<uint32_t *>(bmUpload.data() + 2 * n);
   data::Window *w[2] = {inner, outer};
-  for (int k = 0; k < 2; ++k) {
-    bmStart[k].assign((size_t)F * G, 0);
-    bmLen[k].assign((size_t)F * G, 0);
+  for (int k = 0; k < 2; ++k)
     for (const histograms::Segment &sg : w[k]->getPlan().segments) {
       HJ_CHECK(sg.lp < F && sg.source < G && sg.len < (1ull << 32), "bitmap join: segment (%u, %u) of %lu tuples",
                sg.lp, sg.source, (unsigned long)sg.len);
-      const size_t i = (size_t)sg.lp * G + sg.source;
-      HJ_CHECK(bmLen[k][i] == 0, "bitmap join: two segments for partition %u, group %u", sg.lp, sg.source);
-      bmStart[k][i] = sg.begin;
-      bmLen[k][i] = (uint32_t)sg.len;
+      const size_t i = k * n + (size_t)sg.lp * G + sg.source;
+      HJ_CHECK(lens[i] == 0, "bitmap join: two segments for partition %u, group %u", sg.lp, sg.source);
+      starts[i] = sg.begin;
+      lens[i] = (uint32_t)sg.len;
     }
-    dStart[k] = ctx->workspace().getArray<uint64_t>((uint64_t)F * G);
-    dLen[k] = ctx->workspace().getArray<uint32_t>((uint64_t)F * G);
-    ctx->copy(dStart[k], bmStart[k].data(), bmStart[k].size() * 8, true, false);
-    ctx->copy(dLen[k], bmLen[k].data(), bmLen[k].size() * 4, true, false);
-  }
-  unsigned long long *dOut = ctx->workspace().getArray<unsigned long long>(2);
-  HIP_CHECK(hipMemsetAsync(dOut, 0, 16, ctx->stream()));
+  uint64_t *dev = ctx->workspace().getArray<uint64_t>(words);
+  ctx->copy(dev, bmUpload.data(), words * 8, true, false);
+  const uint32_t *dLens = reinterpret_cast<const uint32_t *>(dev + 2 * n);
+  unsigned long long *dOut = reinterpret_cast<unsigned long long *>(dev + 3 * n);
   HIP_CHECK(hipEventRecord(ev[3], ctx->stream()));
   utils::faultPoint("build_probe");
   kernels::bitmapJoin(static_cast<const uint64_t *>(inner->getData()), static_cast<const uint64_t *>(outer->getData()),
-                      dStart[0], dLen[0], dStart[1], dLen[1], F, G, plan.keyShift, plan.bitmapBits, dOut,
+                      dev, dLens, dev + n, dLens + n, F, G, plan.keyShift, plan.bitmapBits, dOut,
                       reinterpret_cast<uint32_t *>(dOut + 1), ctx->stream());
   HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
   bmBack = ctx->staging().getArray<unsigned long long>(2);

@@ -95,8 +95,7 @@ class HashJoin {
   // Single-level bitmap join (plan.bitmapJoin): enqueue kernels::bitmapJoin over
   // the two sampled-pass windows and the read-back of {matches, dup}.
   void launchBitmapJoin(data::Window *inner, data::Window *outer);
-  std::vector<uint64_t> bmStart[2];
-  std::vector<uint32_t> bmLen[2];
+  std::vector<uint64_t> bmUpload;  // host source of the segment table upload (alive until the join ends)
   unsigned long long *bmBack = nullptr;  // pinned: {matches, dup}
   const ulonglong2 *output = nullptr;
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
