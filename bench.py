@@ -25,7 +25,10 @@ sys.path.insert(0, ROOT)
 # engines.  With SDMA on, about every second process stalled one join (the
 # 4th) by 17-45 ms inside the first small copy; with it off 5/5 runs were
 # clean (profiles/r1_sdma_outlier.md).  Must be set before HIP initialises.
-os.environ.setdefault("HSA_ENABLE_SDMA", "0")
+# Single-process runs only: multi-rank runs keep the runtime default (their
+# RCCL rehearsals over the socket transport were measured with SDMA on).
+if int(os.environ.get("WORLD_SIZE", "1")) == 1:
+    os.environ.setdefault("HSA_ENABLE_SDMA", "0")
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
