@@ -61,6 +61,7 @@ int main(int argc, char **argv) {
     else if (a == "--materialize") cfg.materialize = true;
     else if (a == "--wide") cfg.format = core::TupleFormat::Wide;
     else if (a == "--round-robin") cfg.assignment = core::AssignmentPolicy::RoundRobin;
+    else if (a == "--two-level-only") cfg.bitmapJoin = false;  // no single-level bitmap join (N == 1)
     else if (a == "--perf-dir") perfDir = next();
     else {
       std::fprintf(stderr, "unknown argument %s\n", a.c_str());

@@ -28,9 +28,10 @@ def test_hjoin_bench_host(tmp_path):
 
 
 @pytest.mark.gpu
-def test_hjoin_bench_device():
-    r = subprocess.run([BIN, "--inner", "16000000", "--outer", "16000000", "--iters", "3"], capture_output=True,
-                       text=True, timeout=300)
+@pytest.mark.parametrize("extra", [[], ["--two-level-only"]])
+def test_hjoin_bench_device(extra):
+    r = subprocess.run([BIN, "--inner", "16777216", "--outer", "16777216", "--iters", "3", *extra],
+                       capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert _last_json(r.stdout)["correct"] is True
 

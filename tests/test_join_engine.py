@@ -376,3 +376,19 @@ def test_bitmap_join_duplicate_inner_falls_back(C, cuda):
     assert res["local_fallbacks"] == 1 and not res["bitmap_join"] and res["global_matches"] == exp
     res = j.run()
     assert res["local_fallbacks"] == 0 and not res["bitmap_join"] and res["global_matches"] == exp
+
+
+def test_bitmap_join_config_and_host_plan(C, monkeypatch):
+    """The bitmap join is a device single-rank plan: on by default in the
+    config, switchable through HPCJOIN_BITMAP_JOIN, never chosen on the host
+    path (which runs the two-level pass)."""
+    from hpcjoin.utils import config_from_dict, config_to_dict
+    assert C.JoinConfig().bitmap_join is True
+    monkeypatch.setenv("HPCJOIN_BITMAP_JOIN", "0")
+    cfg = config_from_dict({})
+    assert cfg.bitmap_join is False and config_to_dict(cfg)["bitmap_join"] is False
+    cfg = C.JoinConfig()
+    cfg.network_histogram = C.HistogramMode.SAMPLED
+    res, exp, j = run_join(C, "cpu", 100_000, 100_000, cfg=cfg)
+    assert not j.plan.bitmap_join and not res["bitmap_join"] and res["global_matches"] == exp
+    assert "bitmap=0/0" in repr(j.plan)
