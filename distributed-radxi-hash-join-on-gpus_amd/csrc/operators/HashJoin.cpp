@@ -482,76 +482,76 @@ JoinResult HashJoin::runImpl() {
     }
   }
   if (!bitmapDone) {
-  if (!lp) lp.reset(new tasks::LocalPartitioning(innerWindow, outerWindow, ctx, plan, localOverflowed));
-  if (!bitmapLaunched) {
-    Measurements::stopLocalProcessingPreparations();
-    Measurements::startLocalProcessing();
-  }
-  const uint32_t outerChunks = outerWindow->getPlan().chunks;
-  if (plan.pipelineOuter && !localOverflowed && outerChunks > 1) {
-    // ---- N > 1, counting: the outer relation is local-partitioned and probed
-    // chunk by chunk as its exchange chunks land (chunk views of the window),
-    // so after the last chunk arrives only its own share is left to do.  The
-    // inner tables are rebuilt per chunk (2-byte fragments, off the critical
-    // path while later chunks are on the links).
-    lp->partitionSide(innerWindow, 0);
-    for (uint32_t c = 0; c < outerChunks; ++c) {
-      outerViews.push_back(outerWindow->chunkView(c));
-      lp->partitionSide(outerViews.back().get(), 1 + (int)c);
-      if (c + 1 == outerChunks && dev) HIP_CHECK(hipEventRecord(ev[3], ctx->stream()));
-      if (c == 0) utils::faultPoint("build_probe");
-      bps.emplace_back(new tasks::BuildProbe(innerWindow, outerViews.back().get(), ctx, plan, config.outputCapacity));
-      bps.back()->execute();
+    if (!lp) lp.reset(new tasks::LocalPartitioning(innerWindow, outerWindow, ctx, plan, localOverflowed));
+    if (!bitmapLaunched) {
+      Measurements::stopLocalProcessingPreparations();
+      Measurements::startLocalProcessing();
     }
-    result.localItems = lp->workItems();
-  } else {
-    TASK_QUEUE.push(lp.get());
-    // Both tasks are owned here (lp is re-created if its sampled layout overflows).
-    while (!TASK_QUEUE.empty()) {
-      tasks::Task *t = TASK_QUEUE.front();
-      TASK_QUEUE.pop();
-      if (t->getType() == TASK_BUILD_PROBE) {
-        utils::faultPoint("build_probe");
+    const uint32_t outerChunks = outerWindow->getPlan().chunks;
+    if (plan.pipelineOuter && !localOverflowed && outerChunks > 1) {
+      // ---- N > 1, counting: the outer relation is local-partitioned and probed
+      // chunk by chunk as its exchange chunks land (chunk views of the window),
+      // so after the last chunk arrives only its own share is left to do.  The
+      // inner tables are rebuilt per chunk (2-byte fragments, off the critical
+      // path while later chunks are on the links).
+      lp->partitionSide(innerWindow, 0);
+      for (uint32_t c = 0; c < outerChunks; ++c) {
+        outerViews.push_back(outerWindow->chunkView(c));
+        lp->partitionSide(outerViews.back().get(), 1 + (int)c);
+        if (c + 1 == outerChunks && dev) HIP_CHECK(hipEventRecord(ev[3], ctx->stream()));
+        if (c == 0) utils::faultPoint("build_probe");
+        bps.emplace_back(new tasks::BuildProbe(innerWindow, outerViews.back().get(), ctx, plan, config.outputCapacity));
+        bps.back()->execute();
+      }
+      result.localItems = lp->workItems();
+    } else {
+      TASK_QUEUE.push(lp.get());
+      // Both tasks are owned here (lp is re-created if its sampled layout overflows).
+      while (!TASK_QUEUE.empty()) {
+        tasks::Task *t = TASK_QUEUE.front();
+        TASK_QUEUE.pop();
+        if (t->getType() == TASK_BUILD_PROBE) {
+          utils::faultPoint("build_probe");
+          t->execute();
+          continue;
+        }
         t->execute();
-        continue;
-      }
-      t->execute();
-      if (t->getType() == TASK_PARTITION) {
-        if (dev) HIP_CHECK(hipEventRecord(ev[3], ctx->stream()));
-        result.localItems = lp->workItems();
-        bps.emplace_back(new tasks::BuildProbe(innerWindow, outerWindow, ctx, plan, config.outputCapacity));
-        TASK_QUEUE.push(bps.back().get());
+        if (t->getType() == TASK_PARTITION) {
+          if (dev) HIP_CHECK(hipEventRecord(ev[3], ctx->stream()));
+          result.localItems = lp->workItems();
+          bps.emplace_back(new tasks::BuildProbe(innerWindow, outerWindow, ctx, plan, config.outputCapacity));
+          TASK_QUEUE.push(bps.back().get());
+        }
       }
     }
-  }
-  trace.reset();  // roctx ranges nest: pop before the next push
-  if (dev) HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
-  ctx->synchronize();
-  result.sampledLocal = lp->sampled();
-  if (lp->sampled() && lp->overflowed()) {
-    // A sampled slot overflowed (skew the sample missed): the build/probe ran
-    // on incomplete partitions.  Redo the local pass exactly over the whole
-    // windows, then the build/probe; later joins stay exact.
-    localOverflowed = true;
-    ++result.localFallbacks;
-    result.sampledLocal = false;
-    bps.clear();
-    outerViews.clear();
-    lp.reset(new tasks::LocalPartitioning(innerWindow, outerWindow, ctx, plan, true));
-    lp->execute();
-    result.localItems = lp->workItems();
-    bps.emplace_back(new tasks::BuildProbe(innerWindow, outerWindow, ctx, plan, config.outputCapacity));
-    bps.back()->execute();
+    trace.reset();  // roctx ranges nest: pop before the next push
     if (dev) HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
     ctx->synchronize();
-  }
-  for (auto &bp : bps)
-    while (bp->collect()) {  // rare: item list or output buffer overflowed -> exact re-run
-      ++result.reruns;
-      bp->execute();
+    result.sampledLocal = lp->sampled();
+    if (lp->sampled() && lp->overflowed()) {
+      // A sampled slot overflowed (skew the sample missed): the build/probe ran
+      // on incomplete partitions.  Redo the local pass exactly over the whole
+      // windows, then the build/probe; later joins stay exact.
+      localOverflowed = true;
+      ++result.localFallbacks;
+      result.sampledLocal = false;
+      bps.clear();
+      outerViews.clear();
+      lp.reset(new tasks::LocalPartitioning(innerWindow, outerWindow, ctx, plan, true));
+      lp->execute();
+      result.localItems = lp->workItems();
+      bps.emplace_back(new tasks::BuildProbe(innerWindow, outerWindow, ctx, plan, config.outputCapacity));
+      bps.back()->execute();
       if (dev) HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
       ctx->synchronize();
     }
+    for (auto &bp : bps)
+      while (bp->collect()) {  // rare: item list or output buffer overflowed -> exact re-run
+        ++result.reruns;
+        bp->execute();
+        if (dev) HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
+        ctx->synchronize();
+      }
   }  // !bitmapDone
   Measurements::stopLocalProcessing();
   const uint64_t t4 = nowUs();
