@@ -20,7 +20,7 @@ namespace hpcjoin {
 namespace kernels {
 
 constexpr int BM_NTH = 1024;
-constexpr int BM_U = 4;  // loads in flight per lane
+constexpr int BM_U = 8;  // loads in flight per lane
 
 __device__ __forceinline__ uint64_t bmLoad(const uint64_t *p) { return __builtin_nontemporal_load(p); }
 
