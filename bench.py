@@ -15,11 +15,73 @@ checked against the exact oracle (|R| for unique keys).
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+
+def _spawn_ranks_if_needed():
+    """``python bench.py --gpus N`` without a launcher: start N fresh rank
+    processes (one per GPU, torchrun-style env) and exit with their status.
+
+    Runs before torch/HIP are imported, so this process never touches the GPU
+    (no exec of a GPU-initialised process).  Rank 0's JSON line reaches
+    stdout unchanged (children inherit it); a failing rank makes the whole job
+    fail and the other ranks are killed, so nothing hangs in a collective.
+    """
+    if "WORLD_SIZE" in os.environ:
+        return
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    known, _ = ap.parse_known_args()
+    n = known.gpus
+    if n <= 1:
+        return
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n), HPCJOIN_SPAWNED="1")
+    procs = []
+    for r in range(n):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r), GROUP_RANK="0")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                                      start_new_session=True))
+    def signal_all(sig):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, sig)
+                except ProcessLookupError:
+                    pass
+
+    rc, killed_at = 0, None
+    pending = set(range(n))
+    while pending:
+        for r in list(pending):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            pending.discard(r)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench.py: rank {r} exited with {code}; stopping the other ranks", file=sys.stderr, flush=True)
+                signal_all(signal.SIGTERM)
+                killed_at = time.time()
+        if killed_at is not None and time.time() - killed_at > 15:
+            signal_all(signal.SIGKILL)
+            killed_at = time.time()
+        time.sleep(0.05)
+    sys.exit(rc)
+
+
+if __name__ == "__main__":
+    _spawn_ranks_if_needed()
 # Host<->device copies of a join are small (plan uploads, cursor and counter
 # read-backs): run them as blit kernels on the compute queue, not on the SDMA
 # engines.  With SDMA on, about every second process stalled one join (the
@@ -37,52 +99,21 @@ import hpcjoin  # noqa: E402
 from hpcjoin.parallel import init_distributed, make_context  # noqa: E402
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--inner", type=float, default=1e9)
-    ap.add_argument("--outer", type=float, default=1e9)
-    ap.add_argument("--dist", default="unique", choices=["unique", "uniform", "zipf", "modulo"])
-    ap.add_argument("--theta", type=float, default=0.75)
-    ap.add_argument("--chunks", type=int, default=0, help="exchange pipeline slices (0 = auto)")
-    ap.add_argument("--input", default="device", choices=["device", "pinned"],
-                    help="where the relations live: HBM, or pinned host memory read in place over the host link")
-    ap.add_argument("--json-out", default="")
-    args = ap.parse_args()
+DIST = {"unique": "UNIQUE", "uniform": "UNIFORM", "zipf": "ZIPF", "modulo": "MODULO"}
+PHASES = ("histogram_ms", "network_ms", "local_ms", "dev_histogram_ms", "dev_network_ms", "dev_local_partition_ms",
+          "dev_build_probe_ms")
 
-    C = hpcjoin.require_native()
-    info = init_distributed()
-    assert info.world == args.gpus or args.gpus == 1 and info.world == 1, \
-        f"--gpus {args.gpus} but WORLD_SIZE={info.world}"
-    on_gpu = torch.cuda.is_available()
-    loc = "device" if on_gpu else "host"
-    ctx, comm = make_context(info, loc)
 
-    G_R, G_S = int(args.inner), int(args.outer)
-    if not on_gpu:  # CPU fallback for plumbing only: keep it small
-        G_R, G_S = min(G_R, 1 << 20), min(G_S, 1 << 20)
-    inner = C.GenSpec(distribution=C.KeyDistribution.UNIQUE, seed=1234)
-    dmap = {"unique": C.KeyDistribution.UNIQUE, "uniform": C.KeyDistribution.UNIFORM,
-            "zipf": C.KeyDistribution.ZIPF, "modulo": C.KeyDistribution.MODULO}
-    outer = C.GenSpec(distribution=dmap[args.dist], seed=4321, domain=0 if args.dist == "unique" else G_R,
-                      zipf_theta=args.theta)
+def measure(C, info, ctx, comm, on_gpu, G_R, G_S, inner, outer, cfg, rel_loc, steps, warmup):
+    """Generate this rank's slices, build the join (timed with its first run:
+    the cold-join cost incl. planning), warm up, then time `steps` joins
+    between barriers; the max over ranks is the step time."""
     lr, ls = (C.Relation.local_size_for(G, info.rank, info.world) for G in (G_R, G_S))
-    rel_loc = "pinned" if on_gpu and args.input == "pinned" else loc
     R = C.Relation(lr, G_R, rel_loc, info.local_rank)
     S = C.Relation(ls, G_S, rel_loc, info.local_rank)
     R.generate(inner, C.Relation.local_offset_for(G_R, info.rank, info.world))
     S.generate(outer, C.Relation.local_offset_for(G_S, info.rank, info.world))
     expected = C.Relation.expected_matches(inner, G_R, outer, G_S)
-
-    from hpcjoin.utils import config_from_dict  # HPCJOIN_<FIELD> env overrides (sweeps)
-    cfg = config_from_dict({})
-    if args.chunks > 0:
-        cfg.chunks = args.chunks
-    elif "HPCJOIN_CHUNKS" not in os.environ:
-        cfg.chunks = 1 if info.world == 1 else 4
-    join = C.HashJoin(R, S, ctx, cfg)
 
     def barrier():
         if info.world > 1:
@@ -90,72 +121,162 @@ def main():
         if on_gpu:
             torch.cuda.synchronize()
 
-    # Grow the engine arena to the first warmup's peak right after it, so the
+    barrier()
+    t0 = time.perf_counter()
+    join = C.HashJoin(R, S, ctx, cfg)
+    first = join.run()
+    barrier()
+    first_ms = (time.perf_counter() - t0) * 1e3
+    # Grow the engine arena to the first join's peak right after it, so the
     # remaining warmups (not the first timed join) are the first to run on the
     # freshly reserved workspace; the first join pays a one-time hipMalloc.
-    for i in range(args.warmup):
+    ctx.reset_scratch()
+    for _ in range(max(0, warmup - 1)):
         join.run()
-        if i == 0:
-            ctx.reset_scratch()
     ctx.reset_scratch()
     barrier()
     results = []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         results.append(join.run())
     barrier()
     elapsed = time.perf_counter() - t0
-    # max over ranks
-    mine = [int(elapsed * 1e9)]
-    elapsed_ns = max(comm.all_gather(mine)) if info.world > 1 else mine[0]
-    elapsed = elapsed_ns / 1e9
-    ms_per_step = elapsed * 1e3 / args.steps
-    value = (G_R + G_S) * args.steps / elapsed / 1e9
-    correct = all(r["global_matches"] == expected for r in results) if expected is not None else None
-    phases = {k: round(sum(r[k] for r in results) / len(results), 3)
-              for k in ("histogram_ms", "network_ms", "local_ms", "dev_histogram_ms", "dev_network_ms",
-                        "dev_local_partition_ms", "dev_build_probe_ms")}
+    mine = [int(elapsed * 1e9), int(first_ms * 1e6)]
+    if info.world > 1:
+        allv = comm.all_gather(mine)
+        elapsed, first_ms = max(allv[0::2]) / 1e9, max(allv[1::2]) / 1e6
+    ms = elapsed * 1e3 / steps
+    out = {
+        "ms_per_step": round(ms, 3),
+        "value": round((G_R + G_S) * steps / elapsed / 1e9, 4),
+        "first_join_ms": round(first_ms, 3),
+        "matches": results[-1]["global_matches"],
+        "expected_matches": expected,
+        "correct": all(r["global_matches"] == expected for r in [first] + results) if expected is not None else None,
+        "plan": repr(join.plan),
+        "phases_ms": {k: round(sum(r[k] for r in results) / len(results), 3) for k in PHASES},
+        "results": results,
+        "join": join,
+    }
+    del R, S
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--inner", type=float, default=1e9)
+    ap.add_argument("--outer", type=float, default=1e9)
+    ap.add_argument("--dist", default="unique", choices=list(DIST))
+    ap.add_argument("--theta", type=float, default=0.75)
+    ap.add_argument("--chunks", type=int, default=0, help="exchange pipeline slices (0 = auto)")
+    ap.add_argument("--input", default="device", choices=["device", "pinned"],
+                    help="where the relations live: HBM, or pinned host memory read in place over the host link")
+    ap.add_argument("--general", default="on", choices=["on", "off"],
+                    help="also time the general path: the same join on sparse random 63-bit keys")
+    ap.add_argument("--json-out", default="")
+    args = ap.parse_args()
+
+    C = hpcjoin.require_native()
+    info = init_distributed()
+    if info.world != args.gpus and not (args.gpus == 1 and info.world == 1):
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={info.world}")
+    on_gpu = torch.cuda.is_available()
+    loc = "device" if on_gpu else "host"
+    ctx, comm = make_context(info, loc)
+
+    G_R, G_S = int(args.inner), int(args.outer)
+    if not on_gpu:  # CPU fallback for plumbing only: keep it small
+        G_R, G_S = min(G_R, 1 << 20), min(G_S, 1 << 20)
+    rel_loc = "pinned" if on_gpu and args.input == "pinned" else loc
+
+    from hpcjoin.utils import config_from_dict  # HPCJOIN_<FIELD> env overrides (sweeps)
+    cfg = config_from_dict({})
+    if args.chunks > 0:
+        cfg.chunks = args.chunks
+    elif "HPCJOIN_CHUNKS" not in os.environ:
+        cfg.chunks = 1 if info.world == 1 else 4
+
+    def specs(sparse):
+        inner = C.GenSpec(distribution=C.KeyDistribution.UNIQUE, seed=1234)
+        outer = C.GenSpec(distribution=getattr(C.KeyDistribution, DIST[args.dist]), seed=4321,
+                          domain=0 if args.dist == "unique" else G_R, zipf_theta=args.theta)
+        inner.sparse64 = outer.sparse64 = sparse
+        return inner, outer
+
+    head = measure(C, info, ctx, comm, on_gpu, G_R, G_S, *specs(False), cfg, rel_loc, args.steps, args.warmup)
+    join, results = head.pop("join"), head.pop("results")
+    plan = join.plan
+    engine = {"reruns": results[-1]["reruns"], "build_probe_items": results[-1]["build_probe_items"],
+              "network_fallbacks": sum(r["network_fallbacks"] for r in results),
+              "local_fallbacks": sum(r["local_fallbacks"] for r in results),
+              "wire_bytes": results[-1]["wire_bytes"],
+              "local_items": results[-1]["local_items"], "workspace_GB": round(ctx.workspace_capacity() / 1e9, 2),
+              "workspace_peak_GB": round(ctx.workspace_peak() / 1e9, 2),
+              "step_ms": [round(r["join_ms"], 2) for r in results],
+              "step_phases_ms": [[round(r[k], 2) for k in PHASES] for r in results]}
+    # The plan's own link-traffic prediction (both N > 1 alternatives), so a
+    # measured multi-GPU step can be checked against what the links allow.
+    links = None
+    if info.world > 1:
+        gbps = plan.link_gbps
+        links = {"chosen": "replicated_bitmap" if plan.bitmap_replicated else "shuffle",
+                 "replicated_bytes_per_rank": int(plan.replicated_link_bytes),
+                 "shuffle_bytes_per_rank": int(plan.shuffle_link_bytes),
+                 "link_GBps_per_rank": gbps,
+                 "predicted_replicated_ms": round(plan.replicated_link_bytes / gbps / 1e6, 3) if gbps else None,
+                 "predicted_shuffle_ms": round(plan.shuffle_link_bytes / gbps / 1e6, 3) if gbps else None,
+                 "measured_wire_bytes_rank0": results[-1]["wire_bytes"]}
+    del join
+    ctx.reset_scratch()
+
+    general = None
+    if args.general == "on" and args.dist in ("unique", "uniform", "zipf"):
+        g = measure(C, info, ctx, comm, on_gpu, G_R, G_S, *specs(True), cfg, rel_loc,
+                    max(2, args.steps // 2), max(1, args.warmup))
+        g.pop("join")
+        g.pop("results")
+        general = {"data": "synthetic: unique random 63-bit keys (a fixed bijection of 0..G-1 over [0, 2^63)), "
+                           "same join, generated on device",
+                   **g}
+        ctx.reset_scratch()
+
+    correct = head["correct"] is not False and (general is None or general["correct"] is not False)
     if info.rank == 0:
         line = {
-            "metric": "billion tuples/sec (whole node), 1B x 1B uniform int64 keys",
-            "value": round(value, 4),
+            "metric": "billion tuples/sec (whole node), 1B x 1B uniform int64 keys, 1/2/4/8 MI355X",
+            "value": head["value"],
             "unit": "billion tuples/s",
             "n_gpus": info.world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 3),
+            "ms_per_step": head["ms_per_step"],
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "int64 keys (8-byte CompressedTuple after the network pass)",
-            "data": "synthetic: unique int64 keys 0..G-1 under a keyed Feistel permutation, generated on device",
+            "dtype": "int64 keys (u32 key fragments / 8-byte CompressedTuples after the network pass)",
+            "data": "synthetic: unique int64 keys 0..G-1 in a keyed pseudo-random order (the reference generator, "
+                    "Relation.cpp:63-97), generated on device",
             "config": {
                 "model": f"distributed radix hash join, {args.dist} keys, |R|={G_R}, |S|={G_S}",
                 "global_batch": G_R + G_S,
                 "seq_len": 1,
-                "parallelism": f"hash-partition x{info.world} (RCCL all-to-allv over xGMI)" if info.world > 1
-                else "single MI355X",
-                "plan": repr(join.plan),
+                "parallelism": (f"{'replicated bitmap' if plan.bitmap_replicated else 'hash-partition shuffle'} "
+                                f"x{info.world} (RCCL over xGMI)") if info.world > 1 else "single MI355X",
+                "plan": head["plan"],
                 "chunks": cfg.chunks,
                 "input": rel_loc,
             },
-            "matches": results[-1]["global_matches"],
-            "expected_matches": expected,
-            "correct": correct,
-            "phases_ms": phases,
-            "engine": {"reruns": results[-1]["reruns"], "build_probe_items": results[-1]["build_probe_items"],
-                       "network_fallbacks": sum(r["network_fallbacks"] for r in results),
-                       "local_fallbacks": sum(r["local_fallbacks"] for r in results),
-                       "wire_bytes": results[-1]["wire_bytes"],
-                       "local_items": results[-1]["local_items"], "workspace_GB": round(ctx.workspace_capacity() / 1e9, 2),
-                       "workspace_peak_GB": round(ctx.workspace_peak() / 1e9, 2),
-                       "step_ms": [round(r["join_ms"], 2) for r in results],
-                       "step_phases_ms": [[round(r[k], 2) for k in ("histogram_ms", "network_ms", "local_ms",
-                                                                      "dev_histogram_ms", "dev_network_ms",
-                                                                      "dev_local_partition_ms", "dev_build_probe_ms")]
-                                          for r in results],
-                       "setup_ms": [round(r["setup_ms"], 2) for r in results],
-                       "teardown_ms": [round(r["teardown_ms"], 2) for r in results]},
+            "first_join_ms": head["first_join_ms"],
+            "matches": head["matches"],
+            "expected_matches": head["expected_matches"],
+            "correct": head["correct"],
+            "phases_ms": head["phases_ms"],
+            "links": links,
+            "general_path": general,
+            "engine": engine,
             "device": torch.cuda.get_device_name(0) if on_gpu else "cpu",
         }
         print(json.dumps(line), flush=True)
@@ -164,7 +285,7 @@ def main():
                 json.dump(line, f, indent=1)
     # Deterministic teardown: engine objects (HIP streams, arenas, the RCCL
     # communicator) go before torch.distributed and before interpreter exit.
-    del join, R, S, ctx
+    del ctx
     if on_gpu:
         torch.cuda.synchronize()
     if info.world > 1:
@@ -173,7 +294,7 @@ def main():
     if info.world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    if correct is False:
+    if not correct:
         sys.exit(3)
 
 

@@ -252,6 +252,7 @@ at::Tensor opGenerate(int64_t n, int64_t globalOffset, int64_t globalSize, const
   p.perm = kernels::FeistelPermutation::make(domain, spec.seed);
   if (spec.distribution == kernels::KeyDistribution::Zipf) p.zipf = host::makeZipf(domain, spec.zipfTheta);
   p.tpchSparse = spec.tpchSparse;
+  p.sparse64 = spec.sparse64;
   if (out.is_cuda()) {
     kernels::generate(ptr<data::Tuple>(out), n, p, nullptr);
     HIP_CHECK(hipDeviceSynchronize());
@@ -586,6 +587,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .value("AUTO", core::WireCodecMode::Auto)
       .value("OFF", core::WireCodecMode::Off)
       .value("ON", core::WireCodecMode::On);
+  py::enum_<core::PlanChoice>(m, "PlanChoice")
+      .value("AUTO", core::PlanChoice::Auto)
+      .value("OFF", core::PlanChoice::Off)
+      .value("ON", core::PlanChoice::On);
   py::class_<core::JoinConfig>(m, "JoinConfig")
       .def(py::init<>())
       .def_readwrite("network_bits", &core::JoinConfig::networkBits)
@@ -603,6 +608,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("split_local", &core::JoinConfig::splitLocal)
       .def_readwrite("direct_count", &core::JoinConfig::directCount)
       .def_readwrite("bitmap_join", &core::JoinConfig::bitmapJoin)
+      .def_readwrite("replicate_bitmap", &core::JoinConfig::replicateBitmap)
       .def_readwrite("split_histogram", &core::JoinConfig::splitHistogram)
       .def_readwrite("pipeline_outer", &core::JoinConfig::pipelineOuter)
       .def_readwrite("local_item_tiles", &core::JoinConfig::localItemTiles)
@@ -624,6 +630,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("sampled_network", &core::JoinPlan::sampledNetwork)
       .def_readonly("bitmap_join", &core::JoinPlan::bitmapJoin)
       .def_readonly("bitmap_bits", &core::JoinPlan::bitmapBits)
+      .def_readonly("bitmap_replicated", &core::JoinPlan::bitmapReplicated)
+      .def_readonly("replicated_link_bytes", &core::JoinPlan::replicatedLinkBytes)
+      .def_readonly("shuffle_link_bytes", &core::JoinPlan::shuffleLinkBytes)
+      .def_readonly("link_gbps", &core::JoinPlan::linkGBps)
       .def_readonly("split_histogram", &core::JoinPlan::splitHistogram)
       .def_readonly("pipeline_outer", &core::JoinPlan::pipelineOuter)
       .def_readonly("local_bits", &core::JoinPlan::localBits)
@@ -770,7 +780,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("domain", &data::GenSpec::domain)
       .def_readwrite("key_offset", &data::GenSpec::keyOffset)
       .def_readwrite("zipf_theta", &data::GenSpec::zipfTheta)
-      .def_readwrite("tpch_sparse", &data::GenSpec::tpchSparse);
+      .def_readwrite("tpch_sparse", &data::GenSpec::tpchSparse)
+      .def_readwrite("sparse64", &data::GenSpec::sparse64);
 
   py::class_<PyRelation>(m, "Relation")
       .def(py::init([](uint64_t localSize, uint64_t globalSize, const std::string &loc, int device) {

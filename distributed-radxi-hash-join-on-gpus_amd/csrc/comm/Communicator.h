@@ -44,6 +44,10 @@ class Communicator {
   virtual void allGatherDevice(const uint64_t *send, uint64_t *recv, size_t count, hipStream_t stream);
   // data[i] = sum over ranks (host buffer, blocking)
   virtual void allReduceSumHost(uint64_t *data, size_t count) = 0;
+  // Same on a device buffer, in place, enqueued on `stream` (RCCL: ncclAllReduce,
+  // no host sync).  The default stages through the host and completes before
+  // returning.  Used for the replicated bitmaps (disjoint bits: sum == OR).
+  virtual void allReduceSumDevice(uint64_t *data, size_t count, hipStream_t stream);
   virtual void barrier() = 0;
   // Variable all-to-all of 8-byte words.  Counts / displacements are per peer
   // and in words.  Device communicators enqueue on `stream` and return;

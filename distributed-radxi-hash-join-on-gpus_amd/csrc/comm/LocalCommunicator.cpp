@@ -15,6 +15,15 @@ void Communicator::allGatherDevice(const uint64_t *send, uint64_t *recv, size_t 
   if (count) HIP_CHECK(hipMemcpy(recv, all.data(), all.size() * 8, hipMemcpyHostToDevice));
 }
 
+void Communicator::allReduceSumDevice(uint64_t *data, size_t count, hipStream_t stream) {
+  if (size() == 1 || count == 0) return;
+  std::vector<uint64_t> h(count);
+  HIP_CHECK(hipStreamSynchronize(stream));
+  HIP_CHECK(hipMemcpy(h.data(), data, count * 8, hipMemcpyDeviceToHost));
+  allReduceSumHost(h.data(), count);
+  HIP_CHECK(hipMemcpy(data, h.data(), count * 8, hipMemcpyHostToDevice));
+}
+
 void LocalCommunicator::allGatherHost(const uint64_t *send, uint64_t *recv, size_t count) {
   if (send != recv) std::memmove(recv, send, count * sizeof(uint64_t));
 }

@@ -97,6 +97,12 @@ void RcclCommunicator::allReduceSumHost(uint64_t *data, size_t count) {
   utils::waitStream(stream_, this, "ncclAllReduce");
 }
 
+void RcclCommunicator::allReduceSumDevice(uint64_t *data, size_t count, hipStream_t stream) {
+  if (count == 0) return;
+  checkHealth();
+  RCCL_CHECK(ncclAllReduce(data, data, count, ncclUint64, ncclSum, static_cast<ncclComm_t>(comm_), stream));
+}
+
 void RcclCommunicator::barrier() {
   uint64_t one = 1;
   allReduceSumHost(&one, 1);

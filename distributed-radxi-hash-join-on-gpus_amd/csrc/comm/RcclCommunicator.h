@@ -29,6 +29,7 @@ class RcclCommunicator : public Communicator {
   void allGatherHost(const uint64_t *send, uint64_t *recv, size_t count) override;
   void allGatherDevice(const uint64_t *send, uint64_t *recv, size_t count, hipStream_t stream) override;
   void allReduceSumHost(uint64_t *data, size_t count) override;
+  void allReduceSumDevice(uint64_t *data, size_t count, hipStream_t stream) override;
   void barrier() override;
   void allToAllV(const uint64_t *send, const uint64_t *sendCounts, const uint64_t *sendDispls, uint64_t *recv,
                  const uint64_t *recvCounts, const uint64_t *recvDispls, Location loc, hipStream_t stream) override;

@@ -19,11 +19,12 @@ std::string JoinConfig::describe() const {
 std::string JoinPlan::describe() const {
   return utils::format("JoinPlan(nodes=%u networkBits=%u localBits=%u twoLevel=%d keyShift=%u fragShift=%u "
                        "rChunk=%u sChunk=%u chunks=%u wide=%d materialize=%d keyMix=%d sampled=%d assignment=%s wire=%u/%u "
-                       "split=%d splitHist=%d pipeOuter=%d bitmap=%d/%u)",
+                       "split=%d splitHist=%d pipeOuter=%d bitmap=%d/%u%s)",
                        numberOfNodes, networkBits, localBits, (int)twoLevel, keyShift, fragShift, rChunk, sChunk,
                        chunks, (int)wide, (int)materialize, (int)keyMix, (int)sampledNetwork,
                        assignment == AssignmentPolicy::LPT ? "lpt" : "round_robin", wireBits[0], wireBits[1],
-                       (int)splitLocal, (int)splitHistogram, (int)pipelineOuter, (int)bitmapJoin, bitmapBits);
+                       (int)splitLocal, (int)splitHistogram, (int)pipelineOuter, (int)bitmapJoin, bitmapBits,
+                       bitmapReplicated ? " replicated" : "");
 }
 
 JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t globalInner, uint64_t globalOuter,
@@ -76,6 +77,14 @@ JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t global
   // Mixed keys stay below 2^keyBits; a full 64-bit domain could map a key onto
   // the wide format's reserved empty marker, so mixing needs keyBits < 64.
   p.keyMix = cfg.keyHashing == KeyHashing::On && keyBits < 64;
+  if (!p.wide) {
+    // Keys too wide for a CompressedTuple (sparse 63-bit keys, rids beyond
+    // 2^32 next to them): run the 16-byte Tuple format end to end instead.
+    const uint32_t ks = cfg.keyShift ? cfg.keyShift : std::max<uint32_t>(32, ridBits);
+    const uint32_t high = keyBits > p.networkBits ? keyBits - p.networkBits : 0;
+    const uint32_t local = p.twoLevel ? p.localBits : 0;
+    if (ks >= 64 || high > 64 - ks || high > 31 + local) p.wide = true;
+  }
   if (p.wide) {
     p.keyShift = 64;
     p.fragShift = 64;

@@ -52,6 +52,13 @@ enum class WireCodecMode : int {
   On = 2,    // whenever the tuple fits < 64 bits (also the host path: tests)
 };
 
+// Tri-state switch of an optional plan (Auto = the planner's cost model decides).
+enum class PlanChoice : int {
+  Auto = 0,
+  Off = 1,
+  On = 2,
+};
+
 struct JoinConfig {
   uint32_t networkBits = 0;   // radix bits of the network pass (0 = auto)
   uint32_t localBits = 0;     // radix bits of the local pass (0 = auto; ignored if !twoLevel)
@@ -80,6 +87,13 @@ struct JoinConfig {
   bool bitmapJoin = true;       // N == 1 on device, counting, sampled network pass: one LDS bitmap per network
                                 // partition instead of the local pass when the fragment range fits (unique inner
                                 // keys; a duplicate falls back to the two-level pass)
+  // N > 1 counting joins of unique inner keys whose key range fits bitmaps
+  // (tasks/BitmapJoin): every rank builds the bitmaps of its own inner keys,
+  // one RCCL all-reduce ORs them, and every rank probes its own outer tuples
+  // -- no tuple crosses a link.  Auto: on a device engine when its link bytes
+  // (2 (N-1)/N * 2^keyBits / 8) undercut the shuffle's; On: whenever the key
+  // range fits (host path and N == 1 included); Off: never.
+  PlanChoice replicateBitmap = PlanChoice::Auto;
   uint32_t localItemTiles = 64; // local pass work item: up to this many 4096-tuple tiles of one segment
   uint32_t localGeometry = 0;   // local scatter workgroup geometry (0 = 1024 x 8; 1-4: sweep alternatives)
 
@@ -106,6 +120,12 @@ struct JoinPlan {
   bool pipelineOuter = false;   // N > 1 counting: outer local pass + build/probe per exchange chunk
   bool bitmapJoin = false;      // single-level bitmap join (kernels::bitmapJoin) after the sampled network pass
   uint32_t bitmapBits = 0;      // fragment bits per network partition (bitmap size 2^bitmapBits)
+  bool bitmapReplicated = false;  // bitmaps all-reduced over ranks, outer probed in place (tasks/BitmapJoin)
+  // Cost model of the N > 1 plan choice: bytes one rank puts on its links per
+  // join for the replicated bitmaps and for the tuple shuffle, and the
+  // predicted link time of each at linkGBps per rank (7 xGMI peers).
+  double replicatedLinkBytes = 0, shuffleLinkBytes = 0;
+  double linkGBps = 0;
   HistogramMode localHistogram = HistogramMode::Exact;  // resolved per window size by LocalPartitioning
   uint32_t sampleStride = 64;
   uint32_t localSampleStride = 16;

@@ -69,6 +69,7 @@ void Relation::fillUniqueValues(uint64_t startKeyValue, uint64_t startRidValue) 
   p.perm = kernels::FeistelPermutation::make(localSize, 1234 + startKeyValue * 7 + startRidValue);
   runGenerate(data, localSize, p, loc_, device_);
   maxKey_ = startKeyValue + (localSize ? localSize - 1 : 0);
+  setGenerated(startRidValue, true);
 }
 
 void Relation::fillModuloValues(uint64_t startKeyValue, uint64_t startRidValue, uint64_t innerRelationSize) {
@@ -82,6 +83,7 @@ void Relation::fillModuloValues(uint64_t startKeyValue, uint64_t startRidValue, 
   p.perm = kernels::FeistelPermutation::make(innerRelationSize, 4321 + startKeyValue);
   runGenerate(data, localSize, p, loc_, device_);
   maxKey_ = startKeyValue + innerRelationSize - 1;
+  setGenerated(startRidValue, true);
 }
 
 void Relation::generate(const GenSpec &spec, uint64_t globalOffset) {
@@ -96,14 +98,27 @@ void Relation::generate(const GenSpec &spec, uint64_t globalOffset) {
   p.perm = kernels::FeistelPermutation::make(p.domain, spec.seed);
   if (spec.distribution == KeyDistribution::Zipf) p.zipf = host::makeZipf(p.domain, spec.zipfTheta);
   p.tpchSparse = spec.tpchSparse;
+  p.sparse64 = spec.sparse64;
   runGenerate(data, localSize, p, loc_, device_);
   maxKey_ = spec.keyOffset + (spec.distribution == KeyDistribution::Dense ? globalSize : p.domain) - 1;
   if (spec.tpchSparse) maxKey_ = kernels::tpchSparseKey(maxKey_);
+  if (spec.sparse64) maxKey_ = kernels::SPARSE_KEY_MAX;
+  // Keys are permutations / draws over a dense domain (or a bijective mix of
+  // one): uniform low bits.  The TPC-H layout leaves digits empty.
+  setGenerated(globalOffset, !spec.tpchSparse);
+}
+
+void Relation::setGenerated(uint64_t ridBase, bool lowBitsUniform) {
+  keyBoundKnown_ = true;
+  ridsPositional_ = true;
+  ridBase_ = ridBase;
+  lowBitsUniform_ = lowBitsUniform;
 }
 
 uint64_t Relation::expectedMatches(const GenSpec &inner, uint64_t innerGlobal, const GenSpec &outer,
                                    uint64_t outerGlobal) {
-  if (inner.tpchSparse != outer.tpchSparse) return UINT64_MAX;  // the key transform must match
+  if (inner.tpchSparse != outer.tpchSparse || inner.sparse64 != outer.sparse64)
+    return UINT64_MAX;  // the key transforms must match
   const uint64_t innerDomain = inner.domain ? inner.domain : innerGlobal;
   const bool innerIsKeySet = (inner.distribution == KeyDistribution::Unique ||
                               inner.distribution == KeyDistribution::Dense) &&
@@ -174,6 +189,7 @@ void Relation::distribute(uint32_t nodeId, uint32_t numberOfNodes, comm::Communi
     randomOrder();
   }
   memory::Arena::rawFree(loc_, incoming);
+  ridsPositional_ = false;  // rids moved with their tuples; keys keep their bound
 }
 
 void Relation::debugKeyPrint(uint64_t limit) {

@@ -30,6 +30,7 @@ struct GenSpec {
   uint64_t keyOffset = 0;
   double zipfTheta = 0.75;
   bool tpchSparse = false;   // TPC-H O_ORDERKEY layout applied to the generated key (both sides alike)
+  bool sparse64 = false;     // sparse random 63-bit keys (kernels::sparseKey), both sides alike
 };
 
 class Relation {
@@ -68,10 +69,19 @@ class Relation {
   static uint64_t expectedMatches(const GenSpec &inner, uint64_t innerGlobal, const GenSpec &outer,
                                   uint64_t outerGlobal);
   uint64_t maxKey() const { return maxKey_; }
+  // Bounds the planner can use without reading the tuples (set by the
+  // generators, cleared by distribute()/external data): every key <= maxKey(),
+  // the rid of local tuple i is ridBase() + i, and the low key bits are
+  // uniform (no key mixing needed).
+  bool keyBoundKnown() const { return keyBoundKnown_; }
+  bool ridsPositional() const { return ridsPositional_; }
+  uint64_t ridBase() const { return ridBase_; }
+  bool lowBitsUniform() const { return lowBitsUniform_; }
 
  protected:
   void randomOrder();
   void ensureHostMirror();
+  void setGenerated(uint64_t ridBase, bool lowBitsUniform);
 
  protected:
   uint64_t localSize;
@@ -84,6 +94,10 @@ class Relation {
   bool owns_;
   bool fromPool_;
   uint64_t maxKey_ = 0;
+  bool keyBoundKnown_ = false;
+  bool ridsPositional_ = false;
+  uint64_t ridBase_ = 0;
+  bool lowBitsUniform_ = false;
 };
 
 }  // namespace data

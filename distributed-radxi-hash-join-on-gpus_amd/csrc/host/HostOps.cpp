@@ -65,7 +65,8 @@ void generate(data::Tuple *out, uint64_t n, const kernels::GenParams &p) {
         break;
       default: k = p.keyOffset + p.perm(zipfRank(p.zipf, kernels::uniform01(p.seed, gi))); break;
     }
-    out[i].key = p.tpchSparse ? kernels::tpchSparseKey(k) : k;
+    if (p.tpchSparse) k = kernels::tpchSparseKey(k);
+    out[i].key = p.sparse64 ? kernels::sparseKey(k) : k;
     out[i].rid = p.ridOffset + i;
   }
 }

@@ -2,17 +2,26 @@
 // partition.
 //
 // After the network pass every partition holds the key fragments above the
-// network digit (CompressedTuple: value >> keyShift).  With dense keys the
-// fragment range of one partition is 2^(keyBits - networkBits); when that fits
-// an LDS bitmap (<= 2^20 bits = 128 KiB) the partition is joined in place, as
-// the reference's default single-level plan does
-// (core/Configuration.h:28 ENABLE_TWO_LEVEL_PARTITIONING=false; build/probe per
-// network partition, tasks/BuildProbe.cpp:47-121), without the second radix
-// pass.  Build: atomicOr of the fragment's bit; a bit that was already set is
-// a duplicate inner key, which the bitmap cannot count -- the kernel raises
-// `dup` and the caller redoes the join with the two-level pass.  Probe: one
-// LDS bit test per outer tuple.  Partitions arrive as the sampled network
-// pass's claim slices (up to `groups` segments per partition, gaps between).
+// network digit.  With dense keys the fragment range of one partition is
+// 2^(keyBits - networkBits); when that fits an LDS bitmap (<= 2^20 bits =
+// 128 KiB) the partition is joined in place, as the reference's default
+// single-level plan does (core/Configuration.h:28 ENABLE_TWO_LEVEL_PARTITIONING
+// = false; build/probe per network partition, tasks/BuildProbe.cpp:47-121),
+// without the second radix pass.  Build: atomicOr of the fragment's bit; a bit
+// that was already set is a duplicate inner key, which a bitmap cannot count
+// -- the kernel raises BM_FLAG_DUP and the caller redoes the join on the
+// two-level pass.  Probe: one LDS bit test per outer tuple.
+//
+// Three launch shapes (kernels.h):
+//   bitmapJoin   build + probe of partition d in one workgroup (one rank)
+//   bitmapBuild  the partition's bitmap is written to HBM (replicated plan:
+//                every rank's bitmaps are summed by an RCCL all-reduce)
+//   bitmapProbe  the (all-reduced) bitmap is loaded into LDS, its bits are
+//                counted (cross-rank duplicate check), the outer side probed
+// Elements are u32 key fragments of the count-only network pass (claim
+// slices of a sampled pass, read as 16-byte vectors: slices start on 16-
+// element boundaries) or 8-byte CompressedTuples (value >> keyShift) of an
+// exchanged window (host-built segment table).
 #include "kernels.h"
 #include "device_common.h"
 
@@ -20,81 +29,268 @@ namespace hpcjoin {
 namespace kernels {
 
 constexpr int BM_NTH = 1024;
-constexpr int BM_U = 8;  // loads in flight per lane
+constexpr int BM_U = 4;  // 16-byte loads in flight per lane (64 B, as 8 x 8-byte loads before)
 
-__device__ __forceinline__ uint64_t bmLoad(const uint64_t *p) { return __builtin_nontemporal_load(p); }
+using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(BM_NTH) void bitmapJoinKernel(
-    const uint64_t *__restrict__ r, const uint64_t *__restrict__ s, const uint64_t *__restrict__ rStart,
-    const uint32_t *__restrict__ rLen, const uint64_t *__restrict__ sStart, const uint32_t *__restrict__ sLen,
-    uint32_t groups, uint32_t keyShift, uint32_t words, unsigned long long *__restrict__ matches,
-    uint32_t *__restrict__ dup) {
+// Claim slices [CLAIM_GROUPS][F] of a sampled network pass: slice (g, d) is
+// [start, min(cur, end)); cur > end means it overflowed (flagged, the caller
+// redoes the join with exact slices).
+template <typename CurT>
+struct ClaimSrc {
+  const CurT *start, *cur, *end;
+  uint32_t F;
+  __device__ __forceinline__ uint32_t groups() const { return CLAIM_GROUPS; }
+  __device__ __forceinline__ void get(uint32_t d, uint32_t g, uint64_t &b, uint64_t &len, uint32_t &flags) const {
+    const size_t i = (size_t)g * F + d;
+    const uint64_t s0 = start[i], c = cur[i], e = end[i];
+    if (c > e) flags |= BM_FLAG_OVERFLOW;
+    b = s0;
+    len = (c < e ? c : e) - s0;
+  }
+};
+
+// Host-built segment table [F][groups] (exchanged windows: one segment per
+// (source rank, exchange chunk) of every owned partition).
+struct TableSrc {
+  const uint64_t *start;
+  const uint64_t *len;
+  uint32_t G;
+  __device__ __forceinline__ uint32_t groups() const { return G; }
+  __device__ __forceinline__ void get(uint32_t d, uint32_t g, uint64_t &b, uint64_t &n, uint32_t &) const {
+    const size_t i = (size_t)d * G + g;
+    b = start[i];
+    n = len[i];
+  }
+};
+
+// fn(fragment) for every element of src[0, len).
+template <typename E, typename Fn>
+__device__ __forceinline__ void visitSlice(const E *__restrict__ src, uint64_t len, uint32_t shift, Fn &&fn) {
+  const uint32_t t = threadIdx.x;
+  if constexpr (sizeof(E) == 4) {
+    const u32x4 *v = reinterpret_cast<const u32x4 *>(src);
+    const uint64_t nv = len >> 2;
+    for (uint64_t i0 = 0; i0 < nv; i0 += (uint64_t)BM_NTH * BM_U) {
+      u32x4 x[BM_U];
+#pragma unroll
+      for (int k = 0; k < BM_U; ++k) {
+        const uint64_t i = i0 + (uint64_t)k * BM_NTH + t;
+        if (i < nv) x[k] = __builtin_nontemporal_load(v + i);
+      }
+#pragma unroll
+      for (int k = 0; k < BM_U; ++k) {
+        const uint64_t i = i0 + (uint64_t)k * BM_NTH + t;
+        if (i < nv) {
+          fn((uint64_t)x[k].x);
+          fn((uint64_t)x[k].y);
+          fn((uint64_t)x[k].z);
+          fn((uint64_t)x[k].w);
+        }
+      }
+    }
+    const uint32_t rem = (uint32_t)(len & 3);
+    if (t < rem) fn((uint64_t)src[(nv << 2) + t]);
+  } else {
+    constexpr int U8 = 2 * BM_U;
+    for (uint64_t i0 = 0; i0 < len; i0 += (uint64_t)BM_NTH * U8) {
+      uint64_t x[U8];
+#pragma unroll
+      for (int k = 0; k < U8; ++k) {
+        const uint64_t i = i0 + (uint64_t)k * BM_NTH + t;
+        if (i < len) x[k] = __builtin_nontemporal_load(src + i);
+      }
+#pragma unroll
+      for (int k = 0; k < U8; ++k) {
+        const uint64_t i = i0 + (uint64_t)k * BM_NTH + t;
+        if (i < len) fn(x[k] >> shift);  // only lanes holding an element (no padding values)
+      }
+    }
+  }
+}
+
+template <typename E, class Src>
+__device__ __forceinline__ void bmBuild(uint32_t *bm, const E *__restrict__ r, const Src &rs, uint32_t shift,
+                                        uint64_t limit, uint32_t &flags) {
+  const uint32_t d = blockIdx.x;
+  for (uint32_t g = 0; g < rs.groups(); ++g) {
+    uint64_t b, len;
+    rs.get(d, g, b, len, flags);
+    visitSlice<E>(r + b, len, shift, [&](uint64_t f) {
+      if (f >= limit) {  // outside the planned fragment range: the caller falls back
+        flags |= BM_FLAG_DUP;
+        return;
+      }
+      const uint32_t bit = 1u << (f & 31);
+      if (atomicOr(&bm[f >> 5], bit) & bit) flags |= BM_FLAG_DUP;
+    });
+  }
+}
+
+template <typename E, class Src>
+__device__ __forceinline__ uint64_t bmProbe(const uint32_t *bm, const E *__restrict__ s, const Src &ss, uint32_t shift,
+                                            uint64_t limit, uint32_t &flags) {
+  const uint32_t d = blockIdx.x;
+  uint32_t cnt = 0;
+  for (uint32_t g = 0; g < ss.groups(); ++g) {
+    uint64_t b, len;
+    ss.get(d, g, b, len, flags);
+    visitSlice<E>(s + b, len, shift, [&](uint64_t f) {
+      if (f < limit) cnt += (bm[f >> 5] >> (f & 31)) & 1u;
+    });
+  }
+  return cnt;
+}
+
+__device__ __forceinline__ void bmFinish(BitmapCounters *out, uint64_t matches, uint64_t bits, uint32_t flags) {
+#pragma unroll
+  for (int o = WAVE / 2; o > 0; o >>= 1) {
+    matches += __shfl_xor(matches, o);
+    bits += __shfl_xor(bits, o);
+  }
+  if ((threadIdx.x & (WAVE - 1)) == 0) {
+    if (matches) atomicAdd(&out->matches, (unsigned long long)matches);
+    if (bits) atomicAdd(&out->popcount, (unsigned long long)bits);
+  }
+  if (flags) atomicOr(&out->flags, flags);
+}
+
+template <typename E, class Src>
+__global__ __launch_bounds__(BM_NTH) void bitmapJoinKernel(const E *__restrict__ r, const E *__restrict__ s, Src rs,
+                                                           Src ss, uint32_t shift, uint32_t words,
+                                                           BitmapCounters *__restrict__ out) {
   extern __shared__ uint32_t bm[];
-  const uint32_t d = blockIdx.x, t = threadIdx.x;
-  for (uint32_t w = t; w < words; w += BM_NTH) bm[w] = 0;
+  for (uint32_t w = threadIdx.x; w < words; w += BM_NTH) bm[w] = 0;
   __syncthreads();
   const uint64_t limit = (uint64_t)words * 32;
-  uint32_t dupv = 0;
-  for (uint32_t g = 0; g < groups; ++g) {
-    const uint64_t *src = r + rStart[(size_t)d * groups + g];
-    const uint32_t n = rLen[(size_t)d * groups + g];
-    for (uint32_t i0 = 0; i0 < n; i0 += BM_NTH * BM_U) {
-      uint64_t v[BM_U];
-#pragma unroll
-      for (int k = 0; k < BM_U; ++k) {
-        const uint32_t i = i0 + k * BM_NTH + t;
-        v[k] = i < n ? bmLoad(src + i) : ~0ull;
-      }
-#pragma unroll
-      for (int k = 0; k < BM_U; ++k) {
-        if (i0 + k * BM_NTH + t >= n) continue;
-        const uint64_t f = v[k] >> keyShift;
-        if (f >= limit) {  // outside the planned range: let the caller fall back
-          dupv = 1;
-          continue;
-        }
-        const uint32_t bit = 1u << (f & 31);
-        dupv |= (atomicOr(&bm[f >> 5], bit) & bit) ? 1u : 0u;
-      }
-    }
-  }
+  uint32_t flags = 0;
+  bmBuild<E>(bm, r, rs, shift, limit, flags);
   __syncthreads();
-  uint32_t cnt = 0;
-  for (uint32_t g = 0; g < groups; ++g) {
-    const uint64_t *src = s + sStart[(size_t)d * groups + g];
-    const uint32_t n = sLen[(size_t)d * groups + g];
-    for (uint32_t i0 = 0; i0 < n; i0 += BM_NTH * BM_U) {
-      uint64_t v[BM_U];
-#pragma unroll
-      for (int k = 0; k < BM_U; ++k) {
-        const uint32_t i = i0 + k * BM_NTH + t;
-        v[k] = i < n ? bmLoad(src + i) : ~0ull;
-      }
-#pragma unroll
-      for (int k = 0; k < BM_U; ++k) {
-        const uint64_t f = v[k] >> keyShift;  // padding lanes carry ~0 >> keyShift >= limit
-        if (f < limit) cnt += (bm[f >> 5] >> (f & 31)) & 1u;
-      }
-    }
-  }
-#pragma unroll
-  for (int o = WAVE / 2; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-  if ((t & (WAVE - 1)) == 0 && cnt) atomicAdd(matches, (unsigned long long)cnt);
-  if (dupv) atomicOr(dup, 1u);
+  const uint64_t cnt = bmProbe<E>(bm, s, ss, shift, limit, flags);
+  bmFinish(out, cnt, 0, flags);
 }
 
-void bitmapJoin(const uint64_t *r, const uint64_t *s, const uint64_t *rStart, const uint32_t *rLen,
-                const uint64_t *sStart, const uint32_t *sLen, uint32_t partitions, uint32_t groups,
-                uint32_t keyShift, uint32_t bits, unsigned long long *matches, uint32_t *dup, hipStream_t st) {
-  HJ_CHECK(bits <= BITMAP_MAX_BITS, "bitmapJoin: %u fragment bits exceed the %u-bit LDS bitmap", bits,
+template <typename E, class Src>
+__global__ __launch_bounds__(BM_NTH) void bitmapBuildKernel(const E *__restrict__ r, Src rs, uint32_t shift,
+                                                            uint32_t words, uint32_t *__restrict__ bitmaps,
+                                                            BitmapCounters *__restrict__ out) {
+  extern __shared__ uint32_t bm[];
+  for (uint32_t w = threadIdx.x; w < words; w += BM_NTH) bm[w] = 0;
+  __syncthreads();
+  uint32_t flags = 0;
+  bmBuild<E>(bm, r, rs, shift, (uint64_t)words * 32, flags);
+  __syncthreads();
+  uint32_t *dst = bitmaps + (size_t)blockIdx.x * words;
+  for (uint32_t w = threadIdx.x; w < words; w += BM_NTH) dst[w] = bm[w];
+  bmFinish(out, 0, 0, flags);
+}
+
+template <typename E, class Src>
+__global__ __launch_bounds__(BM_NTH) void bitmapProbeKernel(const E *__restrict__ s, Src ss, uint32_t shift,
+                                                            uint32_t words, const uint32_t *__restrict__ bitmaps,
+                                                            BitmapCounters *__restrict__ out) {
+  extern __shared__ uint32_t bm[];
+  const u32x4 *src = reinterpret_cast<const u32x4 *>(bitmaps + (size_t)blockIdx.x * words);
+  uint64_t bits = 0;
+  for (uint32_t w = threadIdx.x; w < words / 4; w += BM_NTH) {  // words is a power of two >= 32
+    const u32x4 x = __builtin_nontemporal_load(src + w);
+    bm[4 * w] = x.x;
+    bm[4 * w + 1] = x.y;
+    bm[4 * w + 2] = x.z;
+    bm[4 * w + 3] = x.w;
+    bits += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
+  }
+  __syncthreads();
+  uint32_t flags = 0;
+  const uint64_t cnt = bmProbe<E>(bm, s, ss, shift, (uint64_t)words * 32, flags);
+  bmFinish(out, cnt, bits, flags);
+}
+
+uint32_t bitmapWords(uint32_t bits) { return bits > 7 ? 1u << (bits - 5) : 4u; }
+
+static void checkBits(uint32_t bits, uint32_t keyShift, uint32_t elemBytes) {
+  HJ_CHECK(bits <= BITMAP_MAX_BITS, "bitmap join: %u fragment bits exceed the %u-bit LDS bitmap", bits,
            BITMAP_MAX_BITS);
-  HJ_CHECK(keyShift < 64, "bitmapJoin: keyShift=%u", keyShift);
+  HJ_CHECK(elemBytes == 4 || elemBytes == 8, "bitmap join: %u-byte elements", elemBytes);
+  HJ_CHECK(elemBytes == 8 ? keyShift < 64 : keyShift == 0, "bitmap join: keyShift=%u for %u-byte elements", keyShift,
+           elemBytes);
+}
+
+// Dispatch on (element, slice source): u32 fragments come with claim slices,
+// 8-byte CompressedTuples with a segment table.
+#define HJ_BM_DISPATCH(LAUNCH)                                                                                   \
+  do {                                                                                                           \
+    if (elemBytes == 4) {                                                                                        \
+      HJ_CHECK(src.kind == BitmapSlices::Claim, "bitmap join: u32 fragments need claim slices");                \
+      using E = uint32_t;                                                                                        \
+      if (src.narrow) {                                                                                          \
+        using S = ClaimSrc<uint32_t>;                                                                            \
+        LAUNCH;                                                                                                  \
+      } else {                                                                                                   \
+        using S = ClaimSrc<unsigned long long>;                                                                  \
+        LAUNCH;                                                                                                  \
+      }                                                                                                          \
+    } else {                                                                                                     \
+      HJ_CHECK(src.kind == BitmapSlices::Table, "bitmap join: 8-byte tuples need a segment table");             \
+      using E = uint64_t;                                                                                        \
+      using S = TableSrc;                                                                                        \
+      LAUNCH;                                                                                                    \
+    }                                                                                                            \
+  } while (0)
+
+template <class S>
+static S makeSrc(const BitmapSlices &b, uint32_t F);
+template <>
+ClaimSrc<uint32_t> makeSrc(const BitmapSlices &b, uint32_t F) {
+  return ClaimSrc<uint32_t>{static_cast<const uint32_t *>(b.start), static_cast<const uint32_t *>(b.cur),
+                            static_cast<const uint32_t *>(b.end), F};
+}
+template <>
+ClaimSrc<unsigned long long> makeSrc(const BitmapSlices &b, uint32_t F) {
+  return ClaimSrc<unsigned long long>{static_cast<const unsigned long long *>(b.start),
+                                      static_cast<const unsigned long long *>(b.cur),
+                                      static_cast<const unsigned long long *>(b.end), F};
+}
+template <>
+TableSrc makeSrc(const BitmapSlices &b, uint32_t) {
+  return TableSrc{b.segStart, b.segLen, b.groups};
+}
+
+void bitmapJoin(uint32_t elemBytes, const void *r, const void *s, const BitmapSlices &rsl, const BitmapSlices &ssl,
+                uint32_t partitions, uint32_t keyShift, uint32_t bits, BitmapCounters *out, hipStream_t st) {
+  checkBits(bits, keyShift, elemBytes);
+  HJ_CHECK(rsl.kind == ssl.kind && rsl.narrow == ssl.narrow, "bitmap join: inner and outer slices differ in kind");
   if (partitions == 0) return;
-  const uint32_t words = bits > 5 ? 1u << (bits - 5) : 1u;
-  hipLaunchKernelGGL(bitmapJoinKernel, dim3(partitions), dim3(BM_NTH), (size_t)words * 4, st, r, s, rStart, rLen,
-                     sStart, sLen, groups, keyShift, words, matches, dup);
+  const uint32_t words = bitmapWords(bits);
+  const BitmapSlices &src = rsl;
+  HJ_BM_DISPATCH(hipLaunchKernelGGL((bitmapJoinKernel<E, S>), dim3(partitions), dim3(BM_NTH), (size_t)words * 4, st,
+                                    static_cast<const E *>(r), static_cast<const E *>(s), makeSrc<S>(rsl, partitions),
+                                    makeSrc<S>(ssl, partitions), keyShift, words, out));
   HIP_CHECK_LAUNCH();
 }
+
+void bitmapBuild(uint32_t elemBytes, const void *r, const BitmapSlices &src, uint32_t partitions, uint32_t keyShift,
+                 uint32_t bits, uint32_t *bitmaps, BitmapCounters *out, hipStream_t st) {
+  checkBits(bits, keyShift, elemBytes);
+  if (partitions == 0) return;
+  const uint32_t words = bitmapWords(bits);
+  HJ_BM_DISPATCH(hipLaunchKernelGGL((bitmapBuildKernel<E, S>), dim3(partitions), dim3(BM_NTH), (size_t)words * 4, st,
+                                    static_cast<const E *>(r), makeSrc<S>(src, partitions), keyShift, words, bitmaps,
+                                    out));
+  HIP_CHECK_LAUNCH();
+}
+
+void bitmapProbe(uint32_t elemBytes, const void *s, const BitmapSlices &src, uint32_t partitions, uint32_t keyShift,
+                 uint32_t bits, const uint32_t *bitmaps, BitmapCounters *out, hipStream_t st) {
+  checkBits(bits, keyShift, elemBytes);
+  if (partitions == 0) return;
+  const uint32_t words = bitmapWords(bits);
+  HJ_BM_DISPATCH(hipLaunchKernelGGL((bitmapProbeKernel<E, S>), dim3(partitions), dim3(BM_NTH), (size_t)words * 4, st,
+                                    static_cast<const E *>(s), makeSrc<S>(src, partitions), keyShift, words, bitmaps,
+                                    out));
+  HIP_CHECK_LAUNCH();
+}
+#undef HJ_BM_DISPATCH
 
 }  // namespace kernels
 }  // namespace hpcjoin

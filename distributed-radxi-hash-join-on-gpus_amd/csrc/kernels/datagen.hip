@@ -42,6 +42,7 @@ __global__ __launch_bounds__(256) void generateKernel(ulonglong2 *__restrict__ o
     ulonglong2 t;
     t.x = genKey(p, gi);
     if (p.tpchSparse) t.x = tpchSparseKey(t.x);
+    if (p.sparse64) t.x = sparseKey(t.x);
     t.y = p.ridOffset + i;
     out[i] = t;
   }

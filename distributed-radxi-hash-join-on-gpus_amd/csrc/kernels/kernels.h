@@ -54,6 +54,7 @@ struct GenParams {
   uint64_t seed = 0;
   ZipfParams zipf{};
   bool tpchSparse = false;    // TPC-H O_ORDERKEY layout: k -> (k / 8) * 32 + k % 8 + 1
+  bool sparse64 = false;      // sparse random 63-bit keys: k -> sparseKey(k) (after tpchSparse)
 };
 HJ_HD uint64_t tpchSparseKey(uint64_t k) { return (k >> 3) * 32 + (k & 7) + 1; }
 void generate(data::Tuple *out, uint64_t n, const GenParams &p, hipStream_t s);
@@ -79,6 +80,17 @@ struct KeyMix {
     return k;
   }
 };
+
+// Sparse random int64 keys (BASELINE: "random int64 keys"): a fixed bijection
+// of [0, 2^63) applied to the generated dense key, so unique / foreign-key
+// structure (and the exact oracle) is preserved while the keys spread over
+// the whole non-negative int64 range -- a 1B-key relation then needs all 63
+// key bits, so only the wide / key-only paths can join it.
+constexpr uint64_t SPARSE_KEY_MAX = (1ull << 63) - 1;
+HJ_HD uint64_t sparseKey(uint64_t k) {
+  const KeyMix m{1u, 63u};
+  return m.apply((k ^ 0x2545F4914F6CDD1DULL) & SPARSE_KEY_MAX);
+}
 
 // blockHist is digit-major [F][blocks] (u32).
 void netHistogram(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
@@ -115,6 +127,27 @@ void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keySh
 void netScatterWide(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
                     uint32_t blockBegin, uint32_t blockEnd, void *gcur, data::Tuple *out, hipStream_t s,
                     KeyMix mix = KeyMix(), const void *gend = nullptr, int narrowMode = -1);
+// Count-only projection (JoinPlan::fragments): the scatter writes only the
+// u32 key fragment (mixed key >> bits) -- 4 bytes per tuple instead of 8.
+// Needs fragment bits + bits <= 32 (fragWordFits).
+HJ_HD bool fragWordFits(uint32_t keyBits, uint32_t bits) { return keyBits <= 32 || keyBits <= bits; }
+void netScatterFrag(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g, uint32_t blockBegin,
+                    uint32_t blockEnd, void *gcur, uint32_t *out, hipStream_t s, uint32_t keyBits,
+                    KeyMix mix = KeyMix(), const void *gend = nullptr, int narrowMode = -1);
+// Sampled network pass sized on the device (no host round trip): from the
+// sampled [G][F] group totals (netGroupTotals) to bounded claim slices
+// gstart/gcur/gend ([G][F], u32 if narrow else u64) and *capacityUsed = the
+// sum of the slice capacities.  The host sizes the output buffer with
+// sampledLayoutCapacityBound() beforehand.
+struct SampleScale {
+  double total[CLAIM_GROUPS];  // tuples each XCD group scatters
+  double seen[CLAIM_GROUPS];   // of those, read by the sampled histogram
+  double sigmas, frac, floor;  // margin = sigmas * sigma + frac * est + floor (0, 0, 0 = exact histogram)
+};
+SampleScale sampleScale(const PartitionGeometry &g, uint64_t n, uint32_t sampleStride, bool exact);
+uint64_t sampledLayoutCapacityBound(const SampleScale &sc, uint32_t F);
+void netSampledLayout(const uint64_t *sampled, uint32_t F, const SampleScale &sc, void *gstart, void *gcur, void *gend,
+                      bool narrow, unsigned long long *capacityUsed, hipStream_t s);
 // gend (optional, same layout and width as gcur): end of every group slice.
 // Positions claimed past a slice end are not written; the final gcur values
 // tell the caller each slice's demand (the sampled pass re-runs exactly on
@@ -251,14 +284,40 @@ void buildProbe(const BPArgs &a, const BPItem *items, const uint32_t *nItems, ui
 
 // Single-level counting join of unique inner keys (bitmap_join.hip): one
 // workgroup per network partition sets a 2^bits LDS bitmap from the inner
-// fragments (value >> keyShift) and tests the outer ones.  Partition d is the
-// `groups` segments [start[d * groups + g], + len[...]) of each window.
-// *matches += matches; *dup |= 1 if an inner fragment repeats (or is out of
-// range): the count is then invalid and the caller falls back.
+// fragments and tests the outer ones.
+//   elemBytes 4: u32 key fragments (count-only network pass), keyShift 0,
+//                partitions given as the claim slices of a sampled pass
+//   elemBytes 8: CompressedTuples (fragment = value >> keyShift), partitions
+//                given as a segment table [F][groups] (exchanged windows)
 constexpr uint32_t BITMAP_MAX_BITS = 20;  // 128 KiB of LDS
-void bitmapJoin(const uint64_t *r, const uint64_t *s, const uint64_t *rStart, const uint32_t *rLen,
-                const uint64_t *sStart, const uint32_t *sLen, uint32_t partitions, uint32_t groups,
-                uint32_t keyShift, uint32_t bits, unsigned long long *matches, uint32_t *dup, hipStream_t st);
+constexpr uint32_t BM_FLAG_DUP = 1;       // an inner fragment repeats or leaves the range: fall back
+constexpr uint32_t BM_FLAG_OVERFLOW = 2;  // a sampled claim slice overflowed: redo with exact slices
+struct BitmapCounters {
+  unsigned long long matches;
+  unsigned long long popcount;  // bitmapProbe: set bits of the probed bitmaps
+  unsigned int flags;
+  unsigned int pad;
+};
+struct BitmapSlices {
+  enum Kind : int { Claim = 0, Table = 1 };
+  int kind = Claim;
+  // Claim: [CLAIM_GROUPS][F] slice starts, final claim cursors, slice ends (u32 if narrow).
+  const void *start = nullptr, *cur = nullptr, *end = nullptr;
+  bool narrow = true;
+  // Table: [F][groups] segment starts and lengths (device arrays).
+  const uint64_t *segStart = nullptr, *segLen = nullptr;
+  uint32_t groups = 0;
+};
+// u32 words of one partition's bitmap (a power of two >= 4).
+uint32_t bitmapWords(uint32_t bits);
+void bitmapJoin(uint32_t elemBytes, const void *r, const void *s, const BitmapSlices &rs, const BitmapSlices &ss,
+                uint32_t partitions, uint32_t keyShift, uint32_t bits, BitmapCounters *out, hipStream_t st);
+// bitmaps[d * bitmapWords(bits) ...] = partition d's bitmap of r.
+void bitmapBuild(uint32_t elemBytes, const void *r, const BitmapSlices &rs, uint32_t partitions, uint32_t keyShift,
+                 uint32_t bits, uint32_t *bitmaps, BitmapCounters *out, hipStream_t st);
+// Probes s against bitmaps (e.g. all-reduced over ranks); out->popcount += set bits.
+void bitmapProbe(uint32_t elemBytes, const void *s, const BitmapSlices &ss, uint32_t partitions, uint32_t keyShift,
+                 uint32_t bits, const uint32_t *bitmaps, BitmapCounters *out, hipStream_t st);
 
 // ------------------------------------------------------------ wire codec
 // Exchange wire format for 8-byte CompressedTuples (N > 1).  On the wire a
@@ -274,9 +333,11 @@ struct WireCodec {
   uint32_t w = 0;         // bits per tuple on the wire (0 = codec off)
   uint32_t ridBits = 0;   // low bits of a wire value: rid - base
   uint32_t keyShift = 32; // CompressedTuple: value = rid | fragment << keyShift
+  // ridBits == 0 (count-only joins: no rid is ever read): only the key
+  // fragment travels; decoded tuples carry the sender's base as their rid.
   HJ_HD uint64_t encode(uint64_t v, uint64_t base) const {
     const uint64_t rid = v & ((1ull << keyShift) - 1);
-    return (rid - base) | ((v >> keyShift) << ridBits);
+    return ((rid - base) & ((1ull << ridBits) - 1)) | ((v >> keyShift) << ridBits);
   }
   HJ_HD uint64_t decode(uint64_t e, uint64_t base) const {
     const uint64_t rid = (e & ((1ull << ridBits) - 1)) + base;

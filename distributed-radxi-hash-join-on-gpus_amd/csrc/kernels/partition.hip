@@ -260,6 +260,28 @@ struct NetCompressedDigPol : NetCompressedPol {  // no spare bits: digits staged
   __device__ __forceinline__ OutT out(const StageT &v) const { return v; }
   __device__ __forceinline__ void store(OutT *o, uint64_t pos, const StageT &v) const { o[pos] = out(v); }
 };
+// Count-only projection: a counting join never reads a rid, so the network
+// pass keeps only the key fragment above the network digit (4 bytes instead
+// of the 8-byte CompressedTuple; the reference compares key bits only,
+// tasks/BuildProbe.cpp:101-102, and reports only the count, :115).  The
+// digit rides in the staged word's top bits (fragBits + bits <= 32, checked
+// by the launcher).
+struct NetFragPol {
+  using InT = ulonglong2;
+  using StageT = uint32_t;
+  using OutT = uint32_t;
+  static constexpr bool kDigArray = false;
+  uint64_t mask;
+  uint32_t bits;
+  KeyMix mix;
+  __device__ __forceinline__ uint32_t digit(const InT &x) const { return (uint32_t)(mix.apply(x.x) & mask); }
+  __device__ __forceinline__ StageT stage(const InT &x, uint32_t d) const {
+    return (uint32_t)(mix.apply(x.x) >> bits) | (d << (32 - bits));
+  }
+  __device__ __forceinline__ uint32_t stagedDigit(const StageT &v) const { return v >> (32 - bits); }
+  __device__ __forceinline__ OutT out(const StageT &v) const { return v & (0xFFFFFFFFu >> bits); }
+  __device__ __forceinline__ void store(OutT *o, uint64_t pos, const StageT &v) const { o[pos] = out(v); }
+};
 struct NetWidePol {  // 16 B tuple -> 16 B tuple (full-range keys)
   using InT = ulonglong2;
   using StageT = ulonglong2;
@@ -641,6 +663,135 @@ void netScatterWide(const data::Tuple *in, uint64_t n, uint32_t bits, const Part
   pol.mask = (1ull << bits) - 1;
   pol.mix = mix;
   launchNetClaim(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
+}
+
+void netScatterFrag(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g, uint32_t blockBegin,
+                    uint32_t blockEnd, void *gcur, uint32_t *out, hipStream_t s, uint32_t keyBits, KeyMix mix,
+                    const void *gend, int narrowMode) {
+  const bool narrow = narrowMode < 0 ? cursorsNarrow(n) : narrowMode != 0;
+  HJ_CHECK(bits >= 1 && bits <= MAX_PART_BITS, "netScatterFrag: bits=%u out of range", bits);
+  const uint32_t kb = mix.on ? std::max(keyBits, mix.bits) : keyBits;
+  HJ_CHECK(fragWordFits(kb, bits), "netScatterFrag: %u-bit keys leave a fragment wider than %u bits above %u radix bits",
+           kb, 32 - bits, bits);
+  HJ_CHECK(blockBegin <= blockEnd && blockEnd <= g.blocks, "netScatterFrag: block range [%u,%u) of %u", blockBegin,
+           blockEnd, g.blocks);
+  if (n == 0 || blockEnd == blockBegin) return;
+  NetFragPol pol;
+  pol.mask = (1ull << bits) - 1;
+  pol.bits = bits;
+  pol.mix = mix;
+  launchNetClaim(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
+}
+
+// ------------------------------------------------ device-side sampled layout
+// Turns the sampled per-(XCD group, digit) counts into bounded claim slices
+// on the device, so a sampled network pass needs no host round trip between
+// its histogram and its scatter (the whole count-only join is then one
+// stream of kernels with a single synchronisation at the end).  Entry
+// j = d * G + g (partition-major, groups inside) is stored at i = g * F + d,
+// the claim-cursor layout.  cap = roundup16(min(est + margin, total_g)),
+// est = sampled * total_g / seen_g, margin = sigmas * sqrt(max(est, 1) *
+// total_g / seen_g) + frac * est + floor (sigmas = frac = floor = 0 with an
+// exact histogram: the slices are then exactly the counts, rounded to lines).
+constexpr int LAY_NT = 1024;
+template <typename CurT>
+__global__ __launch_bounds__(LAY_NT) void netSampledLayoutKernel(const unsigned long long *__restrict__ sampled,
+                                                                  uint32_t F, SampleScale sc, CurT *__restrict__ gstart,
+                                                                  CurT *__restrict__ gcur, CurT *__restrict__ gend,
+                                                                  unsigned long long *__restrict__ capacityUsed) {
+  __shared__ unsigned long long wt[LAY_NT / WAVE];
+  constexpr uint32_t G = NGROUPS;
+  const uint32_t n = F * G;
+  const uint32_t per = (n + LAY_NT - 1) / LAY_NT, t = threadIdx.x;
+  const uint32_t j0 = t * per;
+  constexpr int MAXPER = ((1u << MAX_PART_BITS) * NGROUPS + LAY_NT - 1) / LAY_NT;
+  unsigned long long cap[MAXPER];
+  unsigned long long local = 0;
+#pragma unroll
+  for (int k = 0; k < MAXPER; ++k) {
+    cap[k] = 0;
+    const uint32_t j = j0 + k;
+    if (k < (int)per && j < n) {
+      const uint32_t d = j / G, g = j % G;
+      const double seen = sc.seen[g], total = sc.total[g];
+      double c = 0;
+      if (seen > 0) {
+        const double scale = total / seen;
+        const double est = (double)sampled[(size_t)g * F + d] * scale;
+        const double margin = sc.sigmas * sqrt(fmax(est, 1.0) * scale) + sc.frac * est + sc.floor;
+        c = fmin(ceil(est + margin), total);
+      }
+      cap[k] = ((unsigned long long)c + 15ull) & ~15ull;
+      local += cap[k];
+    }
+  }
+  const unsigned long long incl = waveInclusiveScan<unsigned long long>(local);
+  const int lane = t & (WAVE - 1), wid = t / WAVE;
+  if (lane == WAVE - 1) wt[wid] = incl;
+  __syncthreads();
+  unsigned long long run = incl - local;
+  for (int w = 0; w < wid; ++w) run += wt[w];
+#pragma unroll
+  for (int k = 0; k < MAXPER; ++k) {
+    const uint32_t j = j0 + k;
+    if (k < (int)per && j < n) {
+      const uint32_t i = (j % G) * F + j / G;
+      gstart[i] = (CurT)run;
+      gcur[i] = (CurT)run;
+      gend[i] = (CurT)(run + cap[k]);
+      run += cap[k];
+    }
+  }
+  if (t == LAY_NT - 1) *capacityUsed = run;
+}
+
+void netSampledLayout(const uint64_t *sampled, uint32_t F, const SampleScale &sc, void *gstart, void *gcur, void *gend,
+                      bool narrow, unsigned long long *capacityUsed, hipStream_t s) {
+  HJ_CHECK(F >= 1 && F <= (1u << MAX_PART_BITS), "netSampledLayout: F=%u", F);
+  const auto *src = reinterpret_cast<const unsigned long long *>(sampled);
+  if (narrow)
+    hipLaunchKernelGGL(netSampledLayoutKernel<uint32_t>, dim3(1), dim3(LAY_NT), 0, s, src, F, sc,
+                       static_cast<uint32_t *>(gstart), static_cast<uint32_t *>(gcur), static_cast<uint32_t *>(gend),
+                       capacityUsed);
+  else
+    hipLaunchKernelGGL(netSampledLayoutKernel<unsigned long long>, dim3(1), dim3(LAY_NT), 0, s, src, F, sc,
+                       static_cast<unsigned long long *>(gstart), static_cast<unsigned long long *>(gcur),
+                       static_cast<unsigned long long *>(gend), capacityUsed);
+  HIP_CHECK_LAUNCH();
+}
+
+SampleScale sampleScale(const PartitionGeometry &g, uint64_t n, uint32_t sampleStride, bool exact) {
+  SampleScale sc{};
+  const uint64_t span = (uint64_t)g.tilesPerBlock * PART_TILE;
+  for (uint32_t b = 0; b < g.blocks; ++b) {
+    const uint64_t begin = (uint64_t)b * span, end = std::min(n, begin + span);
+    if (begin >= end) continue;
+    sc.total[b % NGROUPS] += (double)(end - begin);
+    for (uint64_t t = begin; t < end; t += (uint64_t)PART_TILE * sampleStride)
+      sc.seen[b % NGROUPS] += (double)std::min<uint64_t>(PART_TILE, end - t);
+  }
+  if (exact) {
+    sc.sigmas = sc.frac = sc.floor = 0;
+  } else {  // 6 sigma + 2% + 256 (tasks/SampledNetworkPartitioning.cpp, same statistics)
+    sc.sigmas = 6.0;
+    sc.frac = 0.02;
+    sc.floor = 256.0;
+  }
+  return sc;
+}
+
+uint64_t sampledLayoutCapacityBound(const SampleScale &sc, uint32_t F) {
+  // Per group: sum_d est_d = total_g; sum_d sqrt(max(est_d,1) * scale) <=
+  // sqrt(F * scale * (total_g + F)) (Cauchy-Schwarz); + ceil and the 16-tuple
+  // line rounding per slice.
+  double b = 0;
+  for (uint32_t g = 0; g < NGROUPS; ++g) {
+    if (sc.total[g] <= 0) continue;
+    const double scale = sc.seen[g] > 0 ? sc.total[g] / sc.seen[g] : 1.0;
+    b += (1.0 + sc.frac) * sc.total[g] + sc.sigmas * std::sqrt((double)F * scale * (sc.total[g] + F)) +
+         (sc.floor + 17.0) * F;
+  }
+  return (uint64_t)(b * 1.0001) + 4096;
 }
 
 void scatterAblation(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift, const PartitionGeometry &g,

@@ -12,6 +12,7 @@
 #include "../performance/Clock.h"
 #include "../performance/Measurements.h"
 #include "../performance/Trace.h"
+#include "../tasks/BitmapJoin.h"
 #include "../tasks/BuildProbe.h"
 #include "../tasks/HistogramComputation.h"
 #include "../tasks/LocalPartitioning.h"
@@ -64,17 +65,27 @@ void HashJoin::makeJoinPlan() {
   // Max key / rid over both relations and all ranks (the plan must be identical
   // everywhere), plus each rank's rid range per relation and exchange chunk
   // (wire codec bases).  Per rank: {max key, max rid, then for inner and outer
-  // and every chunk c: min rid, max rid}.
+  // and every chunk c: min rid, max rid, and last whether the inner keys' low
+  // bits are known to be uniform}.  Generated relations know these bounds
+  // (Relation::keyBoundKnown / ridsPositional): no pass over the data; others
+  // are scanned once here (kernels::keyRidMax).
   const uint32_t C = std::max<uint32_t>(1, config.chunks);
-  const size_t STATS = 2 + 4 * (size_t)C;
+  const size_t STATS = 3 + 4 * (size_t)C;
   std::vector<uint64_t> st(STATS, 0);
   int which = 0;
   for (data::Relation *r : {innerRelation, outerRelation}) {
+    const bool known = r->keyBoundKnown() && r->ridsPositional();
     for (uint32_t c = 0; c < C; ++c) {
       uint64_t b, e;
       histograms::LocalHistogram::chunkRange(r->getLocalSize(), C, config.maxPartitionBlocks, c, &b, &e);
       uint64_t h[3] = {0, 0, ~0ull};
-      if (ctx->onDevice() && e > b) {
+      if (known) {
+        h[0] = r->maxKey();
+        if (e > b) {
+          h[1] = r->ridBase() + e - 1;
+          h[2] = r->ridBase() + b;
+        }
+      } else if (ctx->onDevice() && e > b) {
         unsigned long long *d = ctx->workspace().getArray<unsigned long long>(3);
         HIP_CHECK(hipMemcpyAsync(d, h, 24, hipMemcpyHostToDevice, ctx->stream()));
         kernels::keyRidMax(r->getData() + b, e - b, d, ctx->stream());
@@ -95,67 +106,95 @@ void HashJoin::makeJoinPlan() {
     }
     ++which;
   }
+  st[STATS - 1] = innerRelation->lowBitsUniform() ? 1 : 0;
   ctx->workspace().reset();
   std::vector<uint64_t> all(STATS * numberOfNodes);
   ctx->comm()->allGatherHost(st.data(), all.data(), STATS);
   uint64_t mx[2] = {0, 0};
+  bool lowBitsUniform = true;
   for (uint32_t r = 0; r < numberOfNodes; ++r) {
     mx[0] = std::max(mx[0], all[STATS * r]);
     mx[1] = std::max(mx[1], all[STATS * r + 1]);
+    lowBitsUniform = lowBitsUniform && all[STATS * r + STATS - 1] == 1;
   }
   plan = core::makePlan(config, numberOfNodes, innerRelation->getGlobalSize(), outerRelation->getGlobalSize(), mx[0],
                         mx[1]);
   planWireCodec(all, STATS, C);
-  if (config.keyHashing == core::KeyHashing::Auto && plan.keyBits < 64) plan.keyMix = lowKeyBitsSkewed();
+  // Key mixing only when the inner keys' low bits are not known to be uniform
+  // and a histogram of them says they are skewed (a collective: every rank
+  // takes the same branch, lowBitsUniform is all-gathered).
+  if (config.keyHashing == core::KeyHashing::Auto && plan.keyBits < 64)
+    plan.keyMix = lowBitsUniform ? false : lowKeyBitsSkewed();
   if (!ctx->onDevice()) {
     plan.localHistogram = core::HistogramMode::Exact;  // sampling pays on HBM only
     plan.splitLocal = false;                           // split columns are a device layout
   }
-  {
-    const bool eligible = numberOfNodes == 1 && ctx->onDevice() && plan.chunks == 1;
-    const uint64_t small = std::min(innerRelation->getGlobalSize(), outerRelation->getGlobalSize());
-    if (config.networkHistogram == core::HistogramMode::Sampled)
-      plan.sampledNetwork = eligible;
-    else if (config.networkHistogram == core::HistogramMode::Auto)
-      plan.sampledNetwork = eligible && small >= (16ull << 20);
-  }
-  // N == 1 counting joins: the single-level bitmap join replaces the local
-  // pass when the key fragment above the network digit fits an LDS bitmap.
-  // The network pass then runs at 10 bits (1024 partitions, 128 KiB bitmaps
-  // for 1B dense keys: measured 13.5 ms per 1B x 1B join vs 14.1 ms at 11 bits
-  // with 64 KiB bitmaps -- the 2048-way scatter writes shorter runs), or 11
-  // bits when the key range needs it.  The plan keeps a two-level split of the
-  // same total for the duplicate-key fallback.
-  if (config.bitmapJoin && plan.sampledNetwork && !plan.materialize && !plan.wide && !plan.keyMix) {
-    const uint32_t want = plan.keyBits > kernels::BITMAP_MAX_BITS ? plan.keyBits - kernels::BITMAP_MAX_BITS : 0;
-    const uint32_t nb = config.networkBits ? config.networkBits
-                                           : std::min<uint32_t>(kernels::MAX_PART_BITS, std::max<uint32_t>(10, want));
-    const uint32_t bits = plan.keyBits > nb ? plan.keyBits - nb : 0;
-    if (plan.keyBits < 64 && bits <= kernels::BITMAP_MAX_BITS && plan.keyShift + bits <= 64) {
-      if (nb != plan.networkBits) {
-        core::JoinConfig c2 = config;
-        const uint32_t total = plan.networkBits + plan.localBits;
-        c2.networkBits = nb;
-        c2.localBits = total > nb ? std::min<uint32_t>(total - nb, kernels::MAX_PART_BITS) : 1;
-        core::JoinPlan p2 = core::makePlan(c2, numberOfNodes, innerRelation->getGlobalSize(),
-                                           outerRelation->getGlobalSize(), mx[0], mx[1]);
-        p2.keyMix = plan.keyMix;
-        p2.sampledNetwork = plan.sampledNetwork;
-        p2.localHistogram = plan.localHistogram;
-        plan = p2;
-        planWireCodec(all, STATS, C);
-      }
-      plan.bitmapJoin = true;
-      plan.bitmapBits = bits;
-    }
-  }
+  const uint64_t small = std::min(innerRelation->getGlobalSize(), outerRelation->getGlobalSize());
+  const bool sampleable =
+      config.networkHistogram == core::HistogramMode::Sampled ||
+      (config.networkHistogram == core::HistogramMode::Auto && small >= (16ull << 20));
+  plan.sampledNetwork = numberOfNodes == 1 && ctx->onDevice() && plan.chunks == 1 && sampleable;
   // N > 1 pipelines (also on the host path, where they run in place: same
   // logic, covered by the CPU tests).
   plan.splitHistogram = config.splitHistogram && numberOfNodes > 1;
   plan.pipelineOuter = config.pipelineOuter && numberOfNodes > 1 && !plan.materialize && plan.twoLevel;
+  basePlan = plan;  // the two-level plan: what a bitmap plan falls back to
+  bitmapExact = !(ctx->onDevice() && sampleable);
+  planBitmap();
   JOIN_DEBUG("HashJoin", "%s", plan.describe().c_str());
   if (ctx->onDevice())
-    for (auto &e : ev) HIP_CHECK(hipEventCreate(&e));
+    for (auto &e : ev)
+      if (!e) HIP_CHECK(hipEventCreate(&e));
+}
+
+// Count-only single-level bitmap plans (tasks/BitmapJoin) and the N > 1 cost
+// model.  The network pass runs at 10 bits (1024 partitions, 128 KiB bitmaps
+// for 1B dense keys: measured 13.5 ms per 1B x 1B join vs 14.1 ms at 11 bits
+// with 64 KiB bitmaps -- the 2048-way scatter writes shorter runs), or 11 when
+// the key range needs it.
+//   N == 1: on a device engine whenever the fragments fit (host path: only
+//           when replicateBitmap = On; it is the reference CPU path there).
+//   N > 1:  replicated bitmaps (no tuple shuffle) when they put fewer bytes on
+//           the links than the shuffle would (Auto, device), or when forced.
+// Link bytes per rank and join:
+//   replicated  2 (N-1)/N * 2^(networkBits + bitmapBits) / 8   (ring all-reduce)
+//   shuffle     (N-1)/N * (|R| w_R + |S| w_S) / 8 / N          (w = wire bits per tuple)
+void HashJoin::planBitmap() {
+  const uint32_t N = numberOfNodes;
+  plan.bitmapJoin = false;
+  plan.bitmapReplicated = false;
+  plan.linkGBps = N > 1 ? kLinkGBpsPerPeer * (double)std::min<uint32_t>(N - 1, 7) : 0.0;
+  {
+    const double share = N > 1 ? (double)(N - 1) / N : 0.0;
+    const double wR = plan.wide ? 128 : (plan.wireBits[0] ? plan.wireBits[0] : 64);
+    const double wS = plan.wide ? 128 : (plan.wireBits[1] ? plan.wireBits[1] : 64);
+    plan.shuffleLinkBytes = share *
+                            ((double)innerRelation->getGlobalSize() * wR + (double)outerRelation->getGlobalSize() * wS) /
+                            8.0 / std::max<uint32_t>(N, 1);
+  }
+  if (!config.bitmapJoin || plan.materialize || plan.wide || plan.keyBits >= 64) return;
+  const uint32_t want = plan.keyBits > kernels::BITMAP_MAX_BITS ? plan.keyBits - kernels::BITMAP_MAX_BITS : 0;
+  const uint32_t nb =
+      config.networkBits ? config.networkBits : std::min<uint32_t>(kernels::MAX_PART_BITS, std::max<uint32_t>(10, want));
+  const uint32_t bits = plan.keyBits > nb ? plan.keyBits - nb : 0;
+  if (bits > kernels::BITMAP_MAX_BITS || !kernels::fragWordFits(plan.keyBits, nb)) return;
+  const double bitmapBytes = (double)(1ull << nb) * kernels::bitmapWords(bits) * 4;
+  plan.replicatedLinkBytes = N > 1 ? 2.0 * (N - 1) / N * bitmapBytes : 0.0;
+  bool use;
+  if (N == 1)
+    use = ctx->onDevice() || config.replicateBitmap == core::PlanChoice::On;
+  else if (config.replicateBitmap == core::PlanChoice::On)
+    use = true;
+  else if (config.replicateBitmap == core::PlanChoice::Off)
+    use = false;
+  else
+    use = ctx->onDevice() && plan.replicatedLinkBytes <= plan.shuffleLinkBytes;
+  if (!use) return;
+  plan.networkBits = nb;
+  plan.bitmapJoin = true;
+  plan.bitmapBits = bits;
+  plan.bitmapReplicated = N > 1;
+  plan.sampledNetwork = !bitmapExact;
 }
 
 // Wire codec per relation (kernels.h, WireCodec): frame-of-reference rids
@@ -182,10 +221,12 @@ void HashJoin::planWireCodec(const std::vector<uint64_t> &all, size_t stride, ui
         plan.ridBase[r][(size_t)n * chunks + c] = lo;
         span = std::max<uint64_t>(span, hi - lo + 1);
       }
-    const uint32_t ridBits = std::max<uint32_t>(1, ceilLog2(span));
+    // Counting joins never read a rid after the network pass (every count
+    // kernel compares key fragments only): the wire carries the fragment alone.
+    const uint32_t ridBits = plan.materialize ? std::max<uint32_t>(1, ceilLog2(span)) : 0;
     const uint32_t w = ridBits + keyW;
     const bool on = config.wireCodec == core::WireCodecMode::On ? w < 64 : (ctx->onDevice() && w <= 56);
-    if (on && ridBits <= plan.keyShift) {
+    if (on && w >= 1 && ridBits <= plan.keyShift) {
       plan.wireBits[r] = w;
       plan.wireRidBits[r] = ridBits;
     }
@@ -226,39 +267,6 @@ bool HashJoin::lowKeyBitsSkewed() {
   return skewed;
 }
 
-void HashJoin::launchBitmapJoin(data::Window *inner, data::Window *outer) {
-  const uint32_t F = 1u << plan.networkBits, G = kernels::CLAIM_GROUPS;
-  const size_t n = (size_t)F * G;
-  // One upload: [inner starts | outer starts] (u64), [inner lens | outer lens]
-  // (u32), then the zeroed {matches, dup} words.
-  const size_t words = 2 * n + n + 2;  // u64 words: 2n starts, 2n u32 lens = n words, 2 counters
-  bmUpload.assign(words, 0);
-  uint64_t *starts = bmUpload.data();
-  uint32_t *lens = reinterpret_cast<uint32_t *>(bmUpload.data() + 2 * n);
-  data::Window *w[2] = {inner, outer};
-  for (int k = 0; k < 2; ++k)
-    for (const histograms::Segment &sg : w[k]->getPlan().segments) {
-      HJ_CHECK(sg.lp < F && sg.source < G && sg.len < (1ull << 32), "bitmap join: segment (%u, %u) of %lu tuples",
-               sg.lp, sg.source, (unsigned long)sg.len);
-      const size_t i = k * n + (size_t)sg.lp * G + sg.source;
-      HJ_CHECK(lens[i] == 0, "bitmap join: two segments for partition %u, group %u", sg.lp, sg.source);
-      starts[i] = sg.begin;
-      lens[i] = (uint32_t)sg.len;
-    }
-  uint64_t *dev = ctx->workspace().getArray<uint64_t>(words);
-  ctx->copy(dev, bmUpload.data(), words * 8, true, false);
-  const uint32_t *dLens = reinterpret_cast<const uint32_t *>(dev + 2 * n);
-  unsigned long long *dOut = reinterpret_cast<unsigned long long *>(dev + 3 * n);
-  HIP_CHECK(hipEventRecord(ev[3], ctx->stream()));
-  utils::faultPoint("build_probe");
-  kernels::bitmapJoin(static_cast<const uint64_t *>(inner->getData()), static_cast<const uint64_t *>(outer->getData()),
-                      dev, dLens, dev + n, dLens + n, F, G, plan.keyShift, plan.bitmapBits, dOut,
-                      reinterpret_cast<uint32_t *>(dOut + 1), ctx->stream());
-  HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
-  bmBack = ctx->staging().getArray<unsigned long long>(2);
-  HIP_CHECK(hipMemcpyAsync(bmBack, dOut, 16, hipMemcpyDeviceToHost, ctx->stream()));
-}
-
 void HashJoin::join() {
   run();
   RESULT_COUNTER = result.localMatches;
@@ -272,6 +280,59 @@ JoinResult HashJoin::run() {
     ctx->comm()->abort(e.what());
     throw;
   }
+}
+
+// The count-only bitmap plan (tasks/BitmapJoin).  false: the inner relation
+// has a repeated key (on some rank) -- the plan falls back to the two-level
+// one for this and every later join, and runImpl continues with it.
+bool HashJoin::runBitmap(uint64_t t0) {
+  std::unique_ptr<performance::TraceRange> trace(new performance::TraceRange("bitmap_join"));
+  Measurements::startHistogramComputation();
+  utils::faultPoint("histogram");
+  Measurements::stopHistogramComputation();
+  Measurements::startNetworkPartitioning();
+  tasks::BitmapJoin bj(innerRelation, outerRelation, ctx, plan, config.maxPartitionBlocks, config.sampleStride, ev);
+  tasks::BitmapJoin::Outcome o = bj.run(bitmapExact);
+  if (o.overflow) {
+    // A sampled slice overflowed on some rank (skew the sample missed): every
+    // rank redoes the join with exact histograms, as do later joins.
+    bitmapExact = true;
+    plan.sampledNetwork = false;
+    ++result.networkFallbacks;
+    if (ctx->onDevice()) HIP_CHECK(hipEventRecord(ev[0], ctx->stream()));
+    o = bj.run(true);
+    JOIN_ASSERT(!o.overflow, "HashJoin", "exact bitmap pass overflowed");
+  }
+  Measurements::stopNetworkPartitioning();
+  if (o.dup) {
+    plan = basePlan;
+    ++result.localFallbacks;
+    JOIN_DEBUG("HashJoin", "bitmap join: repeated inner key -> %s", plan.describe().c_str());
+    return false;
+  }
+  Measurements::startLocalProcessing();
+  Measurements::stopLocalProcessing();
+  const uint64_t t4 = nowUs();
+  result.bitmapJoin = true;
+  result.sampledNetwork = !bitmapExact;
+  result.localMatches = o.localMatches;
+  result.globalMatches = o.globalMatches;
+  result.buildProbeItems = 1ull << plan.networkBits;
+  result.innerReceived = innerRelation->getLocalSize();
+  result.outerReceived = outerRelation->getLocalSize();
+  result.wireBytes = o.linkBytes;
+  result.joinMs = (t4 - t0) / 1000.0;
+  result.networkMs = result.joinMs;
+  result.devNetworkMs = o.devSampleMs + o.devScatterMs;
+  result.devBuildProbeMs = o.devJoinMs;
+  Measurements::storeNetworkDetails(innerRelation->getLocalSize(), outerRelation->getLocalSize(), 1);
+  Measurements::storeBuildProbeDetails(result.innerReceived, result.outerReceived, result.buildProbeItems);
+  Measurements::storeResultTuples(result.localMatches);
+  Measurements::storeDevicePhase("DNET", result.devNetworkMs);
+  Measurements::storeDevicePhase("DBP", result.devBuildProbeMs);
+  Measurements::stopJoin();
+  RESULT_COUNTER = result.localMatches;
+  return true;
 }
 
 JoinResult HashJoin::runImpl() {
@@ -288,6 +349,7 @@ JoinResult HashJoin::runImpl() {
   Measurements::startJoin();
   const uint64_t t0 = nowUs();
   if (dev) HIP_CHECK(hipEventRecord(ev[0], ctx->stream()));
+  if (plan.bitmapJoin && runBitmap(t0)) return result;
 
   // ---------------------------------------------------------------- histogram
   Measurements::startHistogramComputation();
@@ -303,7 +365,6 @@ JoinResult HashJoin::runImpl() {
   // the inner relation's local pass while the outer scatter still runs).
   std::unique_ptr<tasks::LocalPartitioning> lp;
   bool networkEventRecorded = false;
-  bool bitmapLaunched = false, bitmapDone = false;
   if (sampled) {
     // ---------------------------------------- single-rank sampled network pass
     sp.reset(new tasks::SampledNetworkPartitioning(innerRelation, outerRelation, ctx, plan,
@@ -333,13 +394,7 @@ JoinResult HashJoin::runImpl() {
     if (dev) HIP_CHECK(hipEventRecord(ev[2], ctx->stream()));
     networkEventRecorded = true;
     bool ok = sp->finishSide(0);
-    if (ok && plan.bitmapJoin) {
-      ok = sp->finishSide(1);
-      if (ok) {
-        launchBitmapJoin(sp->innerWindow(), sp->outerWindow());
-        bitmapLaunched = true;
-      }
-    } else if (ok) {
+    if (ok) {
       lp.reset(new tasks::LocalPartitioning(sp->innerWindow(), sp->outerWindow(), ctx, plan, localOverflowed));
       lp->partitionSide(sp->innerWindow(), 0);
       ok = sp->finishSide(1);
@@ -465,28 +520,10 @@ JoinResult HashJoin::runImpl() {
   // Every build/probe of this join (one, or one per outer chunk when pipelined).
   std::vector<std::unique_ptr<tasks::BuildProbe>> bps;
   std::vector<std::unique_ptr<data::Window>> outerViews;
-  uint64_t bitmapMatches = 0;
-  if (bitmapLaunched) {
+  {
+    if (!lp) lp.reset(new tasks::LocalPartitioning(innerWindow, outerWindow, ctx, plan, localOverflowed));
     Measurements::stopLocalProcessingPreparations();
     Measurements::startLocalProcessing();
-    ctx->synchronize();
-    if (bmBack[1] == 0) {
-      bitmapMatches = bmBack[0];
-      bitmapDone = true;
-    } else {
-      // A repeated (or out-of-range) inner key fragment: the bitmap cannot
-      // count it.  Run the two-level pass on the same windows; later joins
-      // skip the bitmap.
-      plan.bitmapJoin = false;
-      ++result.localFallbacks;
-    }
-  }
-  if (!bitmapDone) {
-    if (!lp) lp.reset(new tasks::LocalPartitioning(innerWindow, outerWindow, ctx, plan, localOverflowed));
-    if (!bitmapLaunched) {
-      Measurements::stopLocalProcessingPreparations();
-      Measurements::startLocalProcessing();
-    }
     const uint32_t outerChunks = outerWindow->getPlan().chunks;
     if (plan.pipelineOuter && !localOverflowed && outerChunks > 1) {
       // ---- N > 1, counting: the outer relation is local-partitioned and probed
@@ -552,13 +589,12 @@ JoinResult HashJoin::runImpl() {
         if (dev) HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
         ctx->synchronize();
       }
-  }  // !bitmapDone
+  }
   Measurements::stopLocalProcessing();
   const uint64_t t4 = nowUs();
 
-  result.localMatches = bitmapMatches;
-  result.buildProbeItems = bitmapDone ? (1ull << plan.networkBits) : 0;
-  result.bitmapJoin = bitmapDone;
+  result.localMatches = 0;
+  result.buildProbeItems = 0;
   for (auto &bp : bps) {
     result.localMatches += bp->getMatches();
     result.buildProbeItems += bp->getWorkItems();

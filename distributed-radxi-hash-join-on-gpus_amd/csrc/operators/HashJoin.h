@@ -49,6 +49,11 @@ struct JoinResult {
   uint32_t localFallbacks = 0;     // sampled local pass overflowed -> exact re-run
 };
 
+// Achievable one-way bandwidth of one xGMI peer link (MI355X: 7 links of
+// ~153 GB/s bidirectional, ~77 GB/s each way; ~64 GB/s is what a grouped
+// RCCL send/recv reaches per peer).  Only the planner's cost model uses it.
+constexpr double kLinkGBpsPerPeer = 64.0;
+
 class HashJoin {
  public:
   // Reference constructor: world communicator, default JoinConfig, relation location.
@@ -82,6 +87,8 @@ class HashJoin {
 
  private:
   void makeJoinPlan();
+  void planBitmap();
+  bool runBitmap(uint64_t t0);
   bool lowKeyBitsSkewed();
   void planWireCodec(const std::vector<uint64_t> &rankStats, size_t stride, uint32_t chunks);
   JoinResult runImpl();
@@ -92,11 +99,8 @@ class HashJoin {
   JoinResult result;
   bool sampledOverflowed = false;  // sticky: exact histograms after a sampled pass overflowed
   bool localOverflowed = false;    // sticky: exact local pass after a sampled one overflowed
-  // Single-level bitmap join (plan.bitmapJoin): enqueue kernels::bitmapJoin over
-  // the two sampled-pass windows and the read-back of {matches, dup}.
-  void launchBitmapJoin(data::Window *inner, data::Window *outer);
-  std::vector<uint64_t> bmUpload;  // host source of the segment table upload (alive until the join ends)
-  unsigned long long *bmBack = nullptr;  // pinned: {matches, dup}
+  core::JoinPlan basePlan;         // two-level plan (what a bitmap plan falls back to)
+  bool bitmapExact = false;        // bitmap plan: exact histograms (small inputs, or after an overflow)
   const ulonglong2 *output = nullptr;
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
 };

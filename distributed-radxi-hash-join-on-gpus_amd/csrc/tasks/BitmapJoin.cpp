@@ -1,0 +1,191 @@
+#include "BitmapJoin.h"
+
+#include <algorithm>
+#include <vector>
+
+#include "../comm/Communicator.h"
+#include "../memory/Arena.h"
+#include "../performance/Trace.h"
+#include "../utils/Fault.h"
+#include "../utils/Hip.h"
+
+namespace hpcjoin {
+namespace tasks {
+
+using kernels::BitmapCounters;
+using kernels::BitmapSlices;
+using kernels::CLAIM_GROUPS;
+
+BitmapJoin::BitmapJoin(data::Relation *innerRelation, data::Relation *outerRelation, core::ExecContext *ctx,
+                       const core::JoinPlan &plan, uint32_t maxBlocks, uint32_t sampleStride, hipEvent_t *ev)
+    : inner(innerRelation), outer(outerRelation), ctx(ctx), plan(plan), maxBlocks(maxBlocks),
+      sampleStride(std::max<uint32_t>(1, sampleStride)), ev(ev) {
+  JOIN_ASSERT(plan.bitmapJoin && !plan.materialize && !plan.wide, "BitmapJoin", "needs a counting bitmap plan");
+  JOIN_ASSERT(plan.bitmapBits <= kernels::BITMAP_MAX_BITS, "BitmapJoin", "%u fragment bits do not fit a bitmap",
+              plan.bitmapBits);
+  JOIN_ASSERT(kernels::fragWordFits(plan.keyBits, plan.networkBits), "BitmapJoin",
+              "%u-bit keys do not leave a u32 fragment above %u radix bits", plan.keyBits, plan.networkBits);
+}
+
+BitmapJoin::Outcome BitmapJoin::run(bool exact) { return ctx->onDevice() ? runDevice(exact) : runHost(); }
+
+// Sampled (or exact) histogram -> device layout of bounded claim slices ->
+// bounded claim scatter of u32 fragments.  Nothing here waits for the device.
+void BitmapJoin::partitionSide(Side &s, bool exact) {
+  const uint32_t bits = plan.networkBits, F = 1u << bits, G = CLAIM_GROUPS;
+  const uint64_t n = s.relation->getLocalSize();
+  const uint32_t stride = exact ? 1 : sampleStride;
+  memory::Arena &ws = ctx->workspace();
+  const hipStream_t st = ctx->stream();
+  const kernels::KeyMix mix{plan.keyMix ? 1u : 0u, plan.keyBits};
+  s.geom = kernels::partitionGeometry(n, maxBlocks);
+  uint32_t *blockHist = ws.getArray<uint32_t>((uint64_t)F * s.geom.blocks);
+  uint64_t *totals = ws.getArray<uint64_t>((uint64_t)G * F);
+  kernels::netHistogram(s.relation->getData(), n, bits, s.geom, blockHist, st, mix, stride);
+  kernels::netGroupTotals(blockHist, F, s.geom.blocks, totals, st);
+  const kernels::SampleScale sc = kernels::sampleScale(s.geom, n, stride, exact);
+  const uint64_t cap = kernels::sampledLayoutCapacityBound(sc, F);
+  // Claims may run past a slice end by up to n before the overflow is seen.
+  const bool narrow = kernels::cursorsNarrow(cap + n);
+  const size_t cb = narrow ? 4 : 8;
+  void *gstart = ws.get((size_t)G * F * cb), *gcur = ws.get((size_t)G * F * cb), *gend = ws.get((size_t)G * F * cb);
+  unsigned long long *used = ws.getArray<unsigned long long>(1);
+  kernels::netSampledLayout(totals, F, sc, gstart, gcur, gend, narrow, used, st);
+  s.frags = ws.getArray<uint32_t>(std::max<uint64_t>(cap, 16));
+  kernels::netScatterFrag(s.relation->getData(), n, bits, s.geom, 0, s.geom.blocks, gcur, s.frags, st, plan.keyBits,
+                          mix, gend, narrow ? 1 : 0);
+  s.slices = BitmapSlices();
+  s.slices.kind = BitmapSlices::Claim;
+  s.slices.start = gstart;
+  s.slices.cur = gcur;
+  s.slices.end = gend;
+  s.slices.narrow = narrow;
+}
+
+BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
+  const uint32_t F = 1u << plan.networkBits, N = ctx->numberOfNodes(), bits = plan.bitmapBits;
+  const hipStream_t st = ctx->stream();
+  memory::Arena &ws = ctx->workspace();
+  BitmapCounters *cnt = ws.getArray<BitmapCounters>(1);
+  HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(BitmapCounters), st));
+  Side si{inner, {}, nullptr, {}}, so{outer, {}, nullptr, {}};
+  Outcome o;
+  {
+    performance::TraceRange tr("bitmap_network_inner");
+    utils::faultPoint("network");
+    partitionSide(si, exact);
+  }
+  HIP_CHECK(hipEventRecord(ev[1], st));
+  if (N == 1) {
+    partitionSide(so, exact);
+    HIP_CHECK(hipEventRecord(ev[2], st));
+    HIP_CHECK(hipEventRecord(ev[3], st));
+    utils::faultPoint("build_probe");
+    kernels::bitmapJoin(4, si.frags, so.frags, si.slices, so.slices, F, 0, bits, cnt, st);
+  } else {
+    const uint32_t words = kernels::bitmapWords(bits);
+    uint32_t *bm = ws.getArray<uint32_t>((size_t)F * words);
+    kernels::bitmapBuild(4, si.frags, si.slices, F, 0, bits, bm, cnt, st);
+    hipEvent_t built = ctx->acquireEvent(), reduced = ctx->acquireEvent();
+    HIP_CHECK(hipEventRecord(built, st));
+    HIP_CHECK(hipStreamWaitEvent(ctx->commStream(), built, 0));
+    // The all-reduce (exchange stream) overlaps the outer side's network pass.
+    ctx->comm()->allReduceSumDevice(reinterpret_cast<uint64_t *>(bm), (size_t)F * words / 2, ctx->commStream());
+    HIP_CHECK(hipEventRecord(reduced, ctx->commStream()));
+    o.linkBytes = (uint64_t)(2.0 * (N - 1) / N * (double)F * words * 4);
+    partitionSide(so, exact);
+    HIP_CHECK(hipEventRecord(ev[2], st));
+    HIP_CHECK(hipStreamWaitEvent(st, reduced, 0));
+    HIP_CHECK(hipEventRecord(ev[3], st));
+    utils::faultPoint("build_probe");
+    kernels::bitmapProbe(4, so.frags, so.slices, F, 0, bits, bm, cnt, st);
+  }
+  HIP_CHECK(hipEventRecord(ev[4], st));
+  BitmapCounters *back = ctx->staging().getArray<BitmapCounters>(1);
+  HIP_CHECK(hipMemcpyAsync(back, cnt, sizeof(BitmapCounters), hipMemcpyDeviceToHost, st));
+  ctx->synchronize();
+  float ms = 0;
+  HIP_CHECK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+  o.devSampleMs = ms;
+  HIP_CHECK(hipEventElapsedTime(&ms, ev[1], ev[2]));
+  o.devScatterMs = ms;
+  HIP_CHECK(hipEventElapsedTime(&ms, ev[3], ev[4]));
+  o.devJoinMs = ms;
+  o.localMatches = back->matches;
+  o.popcount = back->popcount;
+  agree(o, back->flags);
+  return o;
+}
+
+// Host reference of the same plan (CPU tests of the N-rank logic): exact
+// partitioning into u32 fragments, bitmaps as u64 words so the all-reduce
+// runs on the host communicator.
+BitmapJoin::Outcome BitmapJoin::runHost() {
+  const uint32_t nb = plan.networkBits, F = 1u << nb, N = ctx->numberOfNodes();
+  const uint32_t words = kernels::bitmapWords(plan.bitmapBits);
+  const uint64_t limit = (uint64_t)words * 32;
+  const kernels::KeyMix mix{plan.keyMix ? 1u : 0u, plan.keyBits};
+  auto partition = [&](data::Relation *r, std::vector<uint32_t> &frags, std::vector<uint64_t> &begin) {
+    const data::Tuple *t = r->getData();
+    const uint64_t n = r->getLocalSize();
+    begin.assign(F + 1, 0);
+    for (uint64_t i = 0; i < n; ++i) ++begin[(mix.apply(t[i].key) & (F - 1)) + 1];
+    for (uint32_t p = 0; p < F; ++p) begin[p + 1] += begin[p];
+    std::vector<uint64_t> cur(begin.begin(), begin.end() - 1);
+    frags.resize(n);
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint64_t k = mix.apply(t[i].key);
+      frags[cur[k & (F - 1)]++] = (uint32_t)(k >> nb);
+    }
+  };
+  std::vector<uint32_t> rf, sf;
+  std::vector<uint64_t> rb, sb;
+  utils::faultPoint("network");
+  partition(inner, rf, rb);
+  partition(outer, sf, sb);
+  std::vector<uint64_t> bm64((size_t)F * words / 2, 0);
+  uint32_t *bm = reinterpret_cast<uint32_t *>(bm64.data());
+  uint32_t flags = 0;
+  for (uint32_t p = 0; p < F; ++p)
+    for (uint64_t i = rb[p]; i < rb[p + 1]; ++i) {
+      const uint64_t f = rf[i];
+      if (f >= limit) {
+        flags |= kernels::BM_FLAG_DUP;
+        continue;
+      }
+      uint32_t &w = bm[(size_t)p * words + (f >> 5)];
+      const uint32_t bit = 1u << (f & 31);
+      if (w & bit) flags |= kernels::BM_FLAG_DUP;
+      w |= bit;
+    }
+  Outcome o;
+  if (N > 1) {
+    ctx->comm()->allReduceSumHost(bm64.data(), bm64.size());
+    o.linkBytes = (uint64_t)(2.0 * (N - 1) / N * (double)bm64.size() * 8);
+    for (uint64_t w : bm64) o.popcount += (uint64_t)__builtin_popcountll(w);
+  }
+  utils::faultPoint("build_probe");
+  for (uint32_t p = 0; p < F; ++p)
+    for (uint64_t i = sb[p]; i < sb[p + 1]; ++i) {
+      const uint64_t f = sf[i];
+      if (f < limit) o.localMatches += (bm[(size_t)p * words + (f >> 5)] >> (f & 31)) & 1u;
+    }
+  agree(o, flags);
+  return o;
+}
+
+// One all-reduce decides for every rank: matches, and whether any rank saw a
+// duplicate or an overflowed slice.  Replicated plans also compare the set
+// bits of the combined bitmaps (identical on every rank) with |R|.
+void BitmapJoin::agree(Outcome &o, uint64_t localFlags) {
+  uint64_t v[3] = {o.localMatches, (localFlags & kernels::BM_FLAG_DUP) ? 1ull : 0ull,
+                   (localFlags & kernels::BM_FLAG_OVERFLOW) ? 1ull : 0ull};
+  ctx->comm()->allReduceSumHost(v, 3);
+  o.globalMatches = v[0];
+  o.dup = v[1] > 0;
+  o.overflow = v[2] > 0;
+  if (ctx->numberOfNodes() > 1 && !o.overflow && o.popcount != inner->getGlobalSize()) o.dup = true;
+}
+
+}  // namespace tasks
+}  // namespace hpcjoin

@@ -1,0 +1,85 @@
+// Count-only single-level bitmap join (JoinPlan::bitmapJoin).
+//
+// The reference's default plan joins every network partition directly, with
+// no second radix pass (core/Configuration.h:28, operators/HashJoin.cpp:138-166,
+// tasks/BuildProbe.cpp:47-121), and a counting join only ever compares key
+// bits and reports a count (tasks/BuildProbe.cpp:101-102,115).  For unique
+// inner keys whose range fits 2^20 bits per network partition that join is a
+// bitmap: this task runs it end to end as one stream of kernels with a single
+// synchronisation at the end.
+//
+// Per relation side (local to the rank, no exchange):
+//   sampled LDS histogram (1 tile in sampleStride) -> per-(XCD group, digit)
+//   claim slices laid out ON THE DEVICE (kernels::netSampledLayout) ->
+//   bounded claim scatter writing u32 key fragments (kernels::netScatterFrag,
+//   4 bytes per tuple: the count-only projection).
+// Then
+//   N == 1  kernels::bitmapJoin: one workgroup per partition builds a 128 KiB
+//           LDS bitmap from the inner fragments and probes the outer ones.
+//   N > 1   replicated plan: kernels::bitmapBuild writes every partition's
+//           bitmap of this rank's inner keys to HBM; ONE RCCL all-reduce (sum)
+//           over the exchange stream combines them (unique keys set disjoint
+//           bits, so the sum is the OR) while the outer side is partitioned on
+//           the compute stream; kernels::bitmapProbe loads each combined
+//           bitmap into LDS and probes this rank's own outer tuples.  No tuple
+//           crosses a link: the links carry 2 (N-1)/N * 2^keyBits / 8 bytes
+//           per rank instead of (N-1)/N of every tuple (HashJoin's cost model
+//           picks the cheaper).  A key held by two ranks turns into a carry of
+//           the sum; every rank counts the set bits of the whole combined
+//           bitmap while probing, and popcount != |R| (global) flags it.
+// Outcomes (agreed by all ranks through the result all-reduce):
+//   overflow  a sampled slice overflowed: rerun with exact histograms
+//   dup       a repeated inner key (or a fragment out of range): the caller
+//             redoes the join on the two-level pass
+// The host path (CPU, tests) runs the same plan with exact partitioning.
+#pragma once
+
+#include <cstdint>
+
+#include "../core/ExecContext.h"
+#include "../core/JoinConfig.h"
+#include "../data/Relation.h"
+#include "../kernels/kernels.h"
+
+namespace hpcjoin {
+namespace tasks {
+
+class BitmapJoin {
+ public:
+  struct Outcome {
+    uint64_t localMatches = 0;
+    uint64_t globalMatches = 0;
+    uint64_t popcount = 0;     // replicated: set bits of the combined bitmaps
+    bool dup = false;          // some rank saw a repeated/out-of-range inner fragment, or a cross-rank carry
+    bool overflow = false;     // some rank's sampled slice overflowed
+    uint64_t linkBytes = 0;    // this rank's share of the all-reduce traffic (ring estimate)
+    double devSampleMs = 0, devScatterMs = 0, devJoinMs = 0;  // hipEvents (device engine)
+  };
+
+  // ev: 5 timing events of the caller (ev[0] already recorded at join start).
+  BitmapJoin(data::Relation *innerRelation, data::Relation *outerRelation, core::ExecContext *ctx,
+             const core::JoinPlan &plan, uint32_t maxBlocks, uint32_t sampleStride, hipEvent_t *ev);
+  // exact: full histograms (no overflow possible).  Collective for N > 1.
+  Outcome run(bool exact);
+
+ private:
+  struct Side {
+    data::Relation *relation;
+    kernels::PartitionGeometry geom;
+    uint32_t *frags = nullptr;
+    kernels::BitmapSlices slices;
+  };
+  void partitionSide(Side &s, bool exact);
+  Outcome runDevice(bool exact);
+  Outcome runHost();
+  void agree(Outcome &o, uint64_t localFlags);
+
+  data::Relation *inner, *outer;
+  core::ExecContext *ctx;
+  const core::JoinPlan &plan;
+  uint32_t maxBlocks, sampleStride;
+  hipEvent_t *ev;
+};
+
+}  // namespace tasks
+}  // namespace hpcjoin

@@ -30,6 +30,9 @@ def main():
          {"chunks": 4}),
         ("materialize", C.GenSpec(seed=99), G_R, {"materialize": True}),
         ("wide", C.GenSpec(seed=99), G_R, {"format": C.TupleFormat.WIDE}),
+        ("unique-shuffle", C.GenSpec(seed=99), G_R, {"bitmap_join": False}),
+        ("zipf-shuffle-chunks3", C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=78, domain=G_R, zipf_theta=0.9),
+         G_S, {"bitmap_join": False, "chunks": 3}),
     ]
     R = C.Relation(C.Relation.local_size_for(G_R, info.rank, info.world), G_R, "device", info.local_rank)
     R.generate(inner, C.Relation.local_offset_for(G_R, info.rank, info.world))
@@ -41,6 +44,10 @@ def main():
             setattr(cfg, k, v)
         j = C.HashJoin(R, S, ctx, cfg)
         exp = C.Relation.expected_matches(inner, G_R, spec, G)
+        # counting joins of these unique inner keys take the replicated bitmaps
+        # (one ncclAllReduce) unless the shuffle is forced
+        want_bitmap = not opts.get("materialize") and "format" not in opts and opts.get("bitmap_join", True)
+        assert j.plan.bitmap_join == want_bitmap and j.plan.bitmap_replicated == want_bitmap, (name, j.plan)
         for _ in range(2):
             res = j.run()
             assert res["global_matches"] == exp, (name, res["global_matches"], exp)

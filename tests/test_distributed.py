@@ -72,6 +72,7 @@ def test_in_process_chunked_exchange(C, dev, chunks, policy):
     loc = "device" if dev == "cuda" else "host"
 
     def cfg_fn(cfg):
+        cfg.bitmap_join = False  # the tuple exchange is under test
         cfg.chunks = chunks
         cfg.assignment = getattr(C.AssignmentPolicy, policy)
         cfg.max_partition_blocks = 16  # several blocks per chunk even at this size
@@ -87,6 +88,7 @@ def test_in_process_sampled_local_pass(C, cuda, n_ranks, chunks, fmt):
     source; the network pass stays exact for N > 1)."""
 
     def cfg_fn(cfg):
+        cfg.bitmap_join = False
         cfg.local_histogram = C.HistogramMode.SAMPLED
         cfg.network_histogram = C.HistogramMode.SAMPLED  # ignored for N > 1
         cfg.chunks = chunks
@@ -105,6 +107,7 @@ def test_in_process_skew_lpt_balances(C, dev):
 
     def cfg_fn(cfg):
         cfg.assignment = C.AssignmentPolicy.LPT
+        cfg.bitmap_join = False
 
     results, exp = run_ranks(C, 4, loc, 200_000, 800_000, cfg_fn, outer_dist="ZIPF", theta=0.9)
     assert all(r[0]["global_matches"] == exp for r in results)
@@ -170,6 +173,7 @@ def test_split_histogram_pipeline(C, dev, n_ranks, chunks, mat):
         pairs = [None] * n_ranks
 
         def cfg_fn(c, split=split):
+            c.bitmap_join = False
             c.split_histogram = split
             c.chunks = chunks
             c.materialize = mat
@@ -196,6 +200,7 @@ def test_pipelined_outer_chunks(C, dev, n_ranks, chunks, local):
     got = {}
     for pipe in (True, False):
         def cfg_fn(c, pipe=pipe):
+            c.bitmap_join = False
             c.pipeline_outer = pipe
             c.chunks = chunks
             c.local_histogram = getattr(C.HistogramMode, local)
@@ -266,7 +271,7 @@ def test_tpch_late_materialization(C, dev, n_ranks):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_rccl_multiprocess_shared_gpu(world):
     """One process per rank over the real RCCL library, as torchrun launches
     bench.py on an 8-GPU node.  The GPU box has one MI355X, so the ranks share
@@ -281,7 +286,7 @@ def test_rccl_multiprocess_shared_gpu(world):
     procs = [subprocess.Popen([sys.executable, "-u", script], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(world)]
     try:
-        outs = [p.communicate(timeout=100)[0] for p in procs]
+        outs = [p.communicate(timeout=110)[0] for p in procs]
     finally:
         for p in procs:
             if p.poll() is None:

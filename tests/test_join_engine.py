@@ -21,15 +21,22 @@ def run_join(C, dev, G_R, G_S, outer_dist="UNIQUE", cfg=None, theta=0.75):
 
 @pytest.mark.parametrize("dev", devices())
 @pytest.mark.parametrize("dist", ["UNIQUE", "UNIFORM", "ZIPF", "MODULO"])
-def test_join_matches_oracle(C, dev, dist):
-    res, exp, _ = run_join(C, dev, 300_000, 500_000 if dist != "UNIQUE" else 300_000, dist)
+@pytest.mark.parametrize("bitmap", [True, False])
+def test_join_matches_oracle(C, dev, dist, bitmap):
+    cfg = C.JoinConfig()
+    cfg.bitmap_join = bitmap
+    if bitmap:
+        cfg.replicate_bitmap = C.PlanChoice.ON  # the host path takes it only when forced
+    res, exp, j = run_join(C, dev, 300_000, 500_000 if dist != "UNIQUE" else 300_000, dist, cfg=cfg)
     assert res["global_matches"] == exp
+    assert j.plan.bitmap_join == bitmap == res["bitmap_join"]
 
 
 @pytest.mark.parametrize("dev", devices())
 def test_join_single_level(C, dev):
     cfg = C.JoinConfig()
     cfg.two_level = False
+    cfg.bitmap_join = False
     res, exp, j = run_join(C, dev, 200_000, 200_000, cfg=cfg)
     assert not j.plan.two_level
     assert res["global_matches"] == exp
@@ -191,6 +198,7 @@ def test_sampled_network_single_level(C, cuda):
     cfg = C.JoinConfig()
     cfg.network_histogram = C.HistogramMode.SAMPLED
     cfg.two_level = False
+    cfg.bitmap_join = False
     res, exp, j = run_join(C, "cuda", 1 << 21, 1 << 21, cfg=cfg)
     assert j.plan.sampled_network and res["sampled_network"] and res["global_matches"] == exp
 
@@ -247,6 +255,7 @@ def test_sampled_local_overflow_falls_back(C, cuda):
     cfg.local_histogram = C.HistogramMode.SAMPLED
     cfg.key_hashing = C.KeyHashing.OFF
     cfg.network_bits, cfg.local_bits = 9, 9
+    cfg.bitmap_join = False
     j = C.HashJoin(C.Relation.from_tensor(R, n), C.Relation.from_tensor(S, n), ctx, cfg)
     res = j.run()
     assert res["local_fallbacks"] == 1 and not res["sampled_local"]
@@ -286,6 +295,7 @@ def test_direct_count_table(C, cuda, dist, split):
     counts = {}
     for direct in (True, False):
         cfg = C.JoinConfig()
+        cfg.bitmap_join = False
         cfg.direct_count = direct
         cfg.split_local = split
         G = 6_000_011
