@@ -631,6 +631,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("bitmap_join", &core::JoinPlan::bitmapJoin)
       .def_readonly("bitmap_bits", &core::JoinPlan::bitmapBits)
       .def_readonly("bitmap_replicated", &core::JoinPlan::bitmapReplicated)
+      .def_readonly("key_only", &core::JoinPlan::keyOnly)
       .def_readonly("replicated_link_bytes", &core::JoinPlan::replicatedLinkBytes)
       .def_readonly("shuffle_link_bytes", &core::JoinPlan::shuffleLinkBytes)
       .def_readonly("link_gbps", &core::JoinPlan::linkGBps)

@@ -19,12 +19,12 @@ std::string JoinConfig::describe() const {
 std::string JoinPlan::describe() const {
   return utils::format("JoinPlan(nodes=%u networkBits=%u localBits=%u twoLevel=%d keyShift=%u fragShift=%u "
                        "rChunk=%u sChunk=%u chunks=%u wide=%d materialize=%d keyMix=%d sampled=%d assignment=%s wire=%u/%u "
-                       "split=%d splitHist=%d pipeOuter=%d bitmap=%d/%u%s)",
+                       "split=%d splitHist=%d pipeOuter=%d bitmap=%d/%u%s%s)",
                        numberOfNodes, networkBits, localBits, (int)twoLevel, keyShift, fragShift, rChunk, sChunk,
                        chunks, (int)wide, (int)materialize, (int)keyMix, (int)sampledNetwork,
                        assignment == AssignmentPolicy::LPT ? "lpt" : "round_robin", wireBits[0], wireBits[1],
                        (int)splitLocal, (int)splitHistogram, (int)pipelineOuter, (int)bitmapJoin, bitmapBits,
-                       bitmapReplicated ? " replicated" : "");
+                       bitmapReplicated ? " replicated" : "", keyOnly ? " keyOnly" : "");
 }
 
 JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t globalInner, uint64_t globalOuter,
@@ -79,13 +79,22 @@ JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t global
   p.keyMix = cfg.keyHashing == KeyHashing::On && keyBits < 64;
   if (!p.wide) {
     // Keys too wide for a CompressedTuple (sparse 63-bit keys, rids beyond
-    // 2^32 next to them): run the 16-byte Tuple format end to end instead.
+    // 2^32 next to them): counting joins carry 8-byte key-only words, and
+    // materializing ones the 16-byte Tuple format end to end.
     const uint32_t ks = cfg.keyShift ? cfg.keyShift : std::max<uint32_t>(32, ridBits);
     const uint32_t high = keyBits > p.networkBits ? keyBits - p.networkBits : 0;
     const uint32_t local = p.twoLevel ? p.localBits : 0;
-    if (ks >= 64 || high > 64 - ks || high > 31 + local) p.wide = true;
+    if (ks >= 64 || high > 64 - ks || high > 31 + local) {
+      if (p.materialize)
+        p.wide = true;
+      else
+        p.keyOnly = true;
+    }
   }
-  if (p.wide) {
+  if (p.keyOnly) {
+    p.keyShift = 0;
+    p.fragShift = p.twoLevel ? p.localBits : 0;
+  } else if (p.wide) {
     p.keyShift = 64;
     p.fragShift = 64;
     JOIN_ASSERT(maxKey != ~0ull, "Plan", "wide format reserves key 0xFFFFFFFFFFFFFFFF as the empty slot");
@@ -105,7 +114,7 @@ JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t global
                 "key fragment (%u bits) would reach the LDS empty marker 0xFFFFFFFF", keyHighBits);
   }
 
-  if (!p.wide && p.twoLevel) {
+  if (!p.wide && !p.keyOnly && p.twoLevel) {
     const uint32_t passBits = p.networkBits + p.localBits;
     const uint32_t fragBits = p.keyBits > passBits ? p.keyBits - passBits : 0;
     p.splitLocal = cfg.splitLocal && ridBits <= 32 && fragBits <= 16;
@@ -117,7 +126,7 @@ JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t global
   if (cfg.rChunk) {
     p.rChunk = cfg.rChunk;
   } else {
-    const uint32_t entry = p.wide ? (p.materialize ? 16 : 8) : (p.materialize ? 8 : 4);
+    const uint32_t entry = p.wide ? (p.materialize ? 16 : 8) : (p.materialize || p.keyOnly ? 8 : 4);
     const uint32_t budget = (entry == 4 || matNarrow) ? 32 * 1024 : 64 * 1024;
     p.rChunk = (budget / entry) / 2;
   }

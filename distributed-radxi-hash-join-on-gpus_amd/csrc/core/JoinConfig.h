@@ -115,6 +115,11 @@ struct JoinPlan {
   bool wide = false;
   bool materialize = false;
   bool keyMix = false;        // radix digits from kernels::KeyMix{keyBits} of the key
+  // Counting join whose keys do not fit a CompressedTuple (sparse 63-bit keys):
+  // after the network pass a tuple is the 8-byte word key >> networkBits (no
+  // rid: a count never reads one), keyShift = 0.  The wide format's 16 bytes
+  // are kept only for materializing joins and when TupleFormat::Wide is asked.
+  bool keyOnly = false;
   bool sampledNetwork = false;  // single-rank network pass sized from a sampled histogram
   bool splitHistogram = false;  // N > 1: assignment from an outer estimate, outer exact histogram off the head
   bool pipelineOuter = false;   // N > 1 counting: outer local pass + build/probe per exchange chunk

@@ -108,8 +108,9 @@ void netCursors(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint32_t
 
 void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift,
                 const kernels::PartitionGeometry &g, uint32_t blockBegin, uint32_t blockEnd, const uint64_t *cursors,
-                void *out, bool wide, kernels::KeyMix mix) {
+                void *out, bool wide, kernels::KeyMix mix, bool withRids) {
   const uint32_t F = 1u << bits;
+  const uint64_t ridMask = withRids ? ~0ull : 0ull;
   const uint64_t mask = F - 1;
   std::vector<uint64_t> cur(F);
   for (uint32_t b = blockBegin; b < blockEnd; ++b) {
@@ -121,7 +122,7 @@ void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keySh
       if (wide)
         static_cast<data::Tuple *>(out)[cur[d]++] = data::Tuple{key, in[i].rid};
       else
-        static_cast<uint64_t *>(out)[cur[d]++] = in[i].rid | ((key >> bits) << keyShift);
+        static_cast<uint64_t *>(out)[cur[d]++] = (in[i].rid & ridMask) | ((key >> bits) << keyShift);
     }
   }
 }

@@ -27,7 +27,7 @@ void netCursors(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint32_t
                 const uint64_t *base, uint64_t *cursors);
 void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift,
                 const kernels::PartitionGeometry &g, uint32_t blockBegin, uint32_t blockEnd, const uint64_t *cursors,
-                void *out, bool wide, kernels::KeyMix mix = kernels::KeyMix());
+                void *out, bool wide, kernels::KeyMix mix = kernels::KeyMix(), bool withRids = true);
 
 void localHistogram(const void *in, bool wide, const kernels::LocalItem *items, uint32_t nItems, uint32_t shift,
                     uint32_t bits, uint32_t *itemHist);

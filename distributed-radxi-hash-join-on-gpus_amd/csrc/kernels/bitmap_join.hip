@@ -25,11 +25,22 @@
 #include "kernels.h"
 #include "device_common.h"
 
+#include <cstdlib>
+
 namespace hpcjoin {
 namespace kernels {
 
 constexpr int BM_NTH = 1024;
-constexpr int BM_U = 4;  // 16-byte loads in flight per lane (64 B, as 8 x 8-byte loads before)
+constexpr int BM_U = 4;  // default 16-byte loads in flight per lane (64 B, as 8 x 8-byte loads before)
+
+// Loads in flight per lane: 4 (default) or 8 (HPCJOIN_BM_U=8, sweep).
+static int bmUnroll() {
+  static const int v = [] {
+    const char *e = std::getenv("HPCJOIN_BM_U");
+    return e && std::atoi(e) == 8 ? 8 : BM_U;
+  }();
+  return v;
+}
 
 using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
 
@@ -65,21 +76,21 @@ struct TableSrc {
 };
 
 // fn(fragment) for every element of src[0, len).
-template <typename E, typename Fn>
+template <typename E, int U, typename Fn>
 __device__ __forceinline__ void visitSlice(const E *__restrict__ src, uint64_t len, uint32_t shift, Fn &&fn) {
   const uint32_t t = threadIdx.x;
   if constexpr (sizeof(E) == 4) {
     const u32x4 *v = reinterpret_cast<const u32x4 *>(src);
     const uint64_t nv = len >> 2;
-    for (uint64_t i0 = 0; i0 < nv; i0 += (uint64_t)BM_NTH * BM_U) {
-      u32x4 x[BM_U];
+    for (uint64_t i0 = 0; i0 < nv; i0 += (uint64_t)BM_NTH * U) {
+      u32x4 x[U];
 #pragma unroll
-      for (int k = 0; k < BM_U; ++k) {
+      for (int k = 0; k < U; ++k) {
         const uint64_t i = i0 + (uint64_t)k * BM_NTH + t;
         if (i < nv) x[k] = __builtin_nontemporal_load(v + i);
       }
 #pragma unroll
-      for (int k = 0; k < BM_U; ++k) {
+      for (int k = 0; k < U; ++k) {
         const uint64_t i = i0 + (uint64_t)k * BM_NTH + t;
         if (i < nv) {
           fn((uint64_t)x[k].x);
@@ -92,7 +103,7 @@ __device__ __forceinline__ void visitSlice(const E *__restrict__ src, uint64_t l
     const uint32_t rem = (uint32_t)(len & 3);
     if (t < rem) fn((uint64_t)src[(nv << 2) + t]);
   } else {
-    constexpr int U8 = 2 * BM_U;
+    constexpr int U8 = 2 * U;
     for (uint64_t i0 = 0; i0 < len; i0 += (uint64_t)BM_NTH * U8) {
       uint64_t x[U8];
 #pragma unroll
@@ -109,14 +120,14 @@ __device__ __forceinline__ void visitSlice(const E *__restrict__ src, uint64_t l
   }
 }
 
-template <typename E, class Src>
+template <typename E, int U, class Src>
 __device__ __forceinline__ void bmBuild(uint32_t *bm, const E *__restrict__ r, const Src &rs, uint32_t shift,
                                         uint64_t limit, uint32_t &flags) {
   const uint32_t d = blockIdx.x;
   for (uint32_t g = 0; g < rs.groups(); ++g) {
     uint64_t b, len;
     rs.get(d, g, b, len, flags);
-    visitSlice<E>(r + b, len, shift, [&](uint64_t f) {
+    visitSlice<E, U>(r + b, len, shift, [&](uint64_t f) {
       if (f >= limit) {  // outside the planned fragment range: the caller falls back
         flags |= BM_FLAG_DUP;
         return;
@@ -127,7 +138,7 @@ __device__ __forceinline__ void bmBuild(uint32_t *bm, const E *__restrict__ r, c
   }
 }
 
-template <typename E, class Src>
+template <typename E, int U, class Src>
 __device__ __forceinline__ uint64_t bmProbe(const uint32_t *bm, const E *__restrict__ s, const Src &ss, uint32_t shift,
                                             uint64_t limit, uint32_t &flags) {
   const uint32_t d = blockIdx.x;
@@ -135,7 +146,7 @@ __device__ __forceinline__ uint64_t bmProbe(const uint32_t *bm, const E *__restr
   for (uint32_t g = 0; g < ss.groups(); ++g) {
     uint64_t b, len;
     ss.get(d, g, b, len, flags);
-    visitSlice<E>(s + b, len, shift, [&](uint64_t f) {
+    visitSlice<E, U>(s + b, len, shift, [&](uint64_t f) {
       if (f < limit) cnt += (bm[f >> 5] >> (f & 31)) & 1u;
     });
   }
@@ -155,7 +166,7 @@ __device__ __forceinline__ void bmFinish(BitmapCounters *out, uint64_t matches, 
   if (flags) atomicOr(&out->flags, flags);
 }
 
-template <typename E, class Src>
+template <typename E, int U, class Src>
 __global__ __launch_bounds__(BM_NTH) void bitmapJoinKernel(const E *__restrict__ r, const E *__restrict__ s, Src rs,
                                                            Src ss, uint32_t shift, uint32_t words,
                                                            BitmapCounters *__restrict__ out) {
@@ -164,13 +175,13 @@ __global__ __launch_bounds__(BM_NTH) void bitmapJoinKernel(const E *__restrict__
   __syncthreads();
   const uint64_t limit = (uint64_t)words * 32;
   uint32_t flags = 0;
-  bmBuild<E>(bm, r, rs, shift, limit, flags);
+  bmBuild<E, U>(bm, r, rs, shift, limit, flags);
   __syncthreads();
-  const uint64_t cnt = bmProbe<E>(bm, s, ss, shift, limit, flags);
+  const uint64_t cnt = bmProbe<E, U>(bm, s, ss, shift, limit, flags);
   bmFinish(out, cnt, 0, flags);
 }
 
-template <typename E, class Src>
+template <typename E, int U, class Src>
 __global__ __launch_bounds__(BM_NTH) void bitmapBuildKernel(const E *__restrict__ r, Src rs, uint32_t shift,
                                                             uint32_t words, uint32_t *__restrict__ bitmaps,
                                                             BitmapCounters *__restrict__ out) {
@@ -178,14 +189,14 @@ __global__ __launch_bounds__(BM_NTH) void bitmapBuildKernel(const E *__restrict_
   for (uint32_t w = threadIdx.x; w < words; w += BM_NTH) bm[w] = 0;
   __syncthreads();
   uint32_t flags = 0;
-  bmBuild<E>(bm, r, rs, shift, (uint64_t)words * 32, flags);
+  bmBuild<E, U>(bm, r, rs, shift, (uint64_t)words * 32, flags);
   __syncthreads();
   uint32_t *dst = bitmaps + (size_t)blockIdx.x * words;
   for (uint32_t w = threadIdx.x; w < words; w += BM_NTH) dst[w] = bm[w];
   bmFinish(out, 0, 0, flags);
 }
 
-template <typename E, class Src>
+template <typename E, int U, class Src>
 __global__ __launch_bounds__(BM_NTH) void bitmapProbeKernel(const E *__restrict__ s, Src ss, uint32_t shift,
                                                             uint32_t words, const uint32_t *__restrict__ bitmaps,
                                                             BitmapCounters *__restrict__ out) {
@@ -202,7 +213,7 @@ __global__ __launch_bounds__(BM_NTH) void bitmapProbeKernel(const E *__restrict_
   }
   __syncthreads();
   uint32_t flags = 0;
-  const uint64_t cnt = bmProbe<E>(bm, s, ss, shift, (uint64_t)words * 32, flags);
+  const uint64_t cnt = bmProbe<E, U>(bm, s, ss, shift, (uint64_t)words * 32, flags);
   bmFinish(out, cnt, bits, flags);
 }
 
@@ -225,15 +236,23 @@ static void checkBits(uint32_t bits, uint32_t keyShift, uint32_t elemBytes) {
       using E = uint32_t;                                                                                        \
       if (src.narrow) {                                                                                          \
         using S = ClaimSrc<uint32_t>;                                                                            \
-        LAUNCH;                                                                                                  \
+        if (bmUnroll() == 8) {                                                                                   \
+          constexpr int U = 8;                                                                                   \
+          LAUNCH;                                                                                                \
+        } else {                                                                                                 \
+          constexpr int U = BM_U;                                                                                \
+          LAUNCH;                                                                                                \
+        }                                                                                                        \
       } else {                                                                                                   \
         using S = ClaimSrc<unsigned long long>;                                                                  \
+        constexpr int U = BM_U;                                                                                  \
         LAUNCH;                                                                                                  \
       }                                                                                                          \
     } else {                                                                                                     \
       HJ_CHECK(src.kind == BitmapSlices::Table, "bitmap join: 8-byte tuples need a segment table");             \
       using E = uint64_t;                                                                                        \
       using S = TableSrc;                                                                                        \
+      constexpr int U = BM_U;                                                                                    \
       LAUNCH;                                                                                                    \
     }                                                                                                            \
   } while (0)
@@ -263,7 +282,7 @@ void bitmapJoin(uint32_t elemBytes, const void *r, const void *s, const BitmapSl
   if (partitions == 0) return;
   const uint32_t words = bitmapWords(bits);
   const BitmapSlices &src = rsl;
-  HJ_BM_DISPATCH(hipLaunchKernelGGL((bitmapJoinKernel<E, S>), dim3(partitions), dim3(BM_NTH), (size_t)words * 4, st,
+  HJ_BM_DISPATCH(hipLaunchKernelGGL((bitmapJoinKernel<E, U, S>), dim3(partitions), dim3(BM_NTH), (size_t)words * 4, st,
                                     static_cast<const E *>(r), static_cast<const E *>(s), makeSrc<S>(rsl, partitions),
                                     makeSrc<S>(ssl, partitions), keyShift, words, out));
   HIP_CHECK_LAUNCH();
@@ -274,7 +293,7 @@ void bitmapBuild(uint32_t elemBytes, const void *r, const BitmapSlices &src, uin
   checkBits(bits, keyShift, elemBytes);
   if (partitions == 0) return;
   const uint32_t words = bitmapWords(bits);
-  HJ_BM_DISPATCH(hipLaunchKernelGGL((bitmapBuildKernel<E, S>), dim3(partitions), dim3(BM_NTH), (size_t)words * 4, st,
+  HJ_BM_DISPATCH(hipLaunchKernelGGL((bitmapBuildKernel<E, U, S>), dim3(partitions), dim3(BM_NTH), (size_t)words * 4, st,
                                     static_cast<const E *>(r), makeSrc<S>(src, partitions), keyShift, words, bitmaps,
                                     out));
   HIP_CHECK_LAUNCH();
@@ -285,7 +304,7 @@ void bitmapProbe(uint32_t elemBytes, const void *s, const BitmapSlices &src, uin
   checkBits(bits, keyShift, elemBytes);
   if (partitions == 0) return;
   const uint32_t words = bitmapWords(bits);
-  HJ_BM_DISPATCH(hipLaunchKernelGGL((bitmapProbeKernel<E, S>), dim3(partitions), dim3(BM_NTH), (size_t)words * 4, st,
+  HJ_BM_DISPATCH(hipLaunchKernelGGL((bitmapProbeKernel<E, U, S>), dim3(partitions), dim3(BM_NTH), (size_t)words * 4, st,
                                     static_cast<const E *>(s), makeSrc<S>(src, partitions), keyShift, words, bitmaps,
                                     out));
   HIP_CHECK_LAUNCH();

@@ -33,15 +33,20 @@ constexpr uint32_t EMPTY32 = 0xFFFFFFFFu;
 constexpr unsigned long long EMPTY64 = ~0ull;
 constexpr int MAT_SLOTS = 2;  // register-held matches per probe before the overflow path
 
-enum BPMode : int { BP_CCOUNT = 0, BP_CMAT = 1, BP_WCOUNT = 2, BP_WMAT = 3 };
+// BP_KCOUNT: counting over key-only 8-byte words (whole-value compare).
+enum BPMode : int { BP_CCOUNT = 0, BP_CMAT = 1, BP_WCOUNT = 2, BP_WMAT = 3, BP_KCOUNT = 4 };
 
-static int bpMode(const BPArgs &a) { return (a.wide ? 2 : 0) + (a.materialize ? 1 : 0); }
+static int bpMode(const BPArgs &a) {
+  if (a.keyOnly) return BP_KCOUNT;
+  return (a.wide ? 2 : 0) + (a.materialize ? 1 : 0);
+}
 
 static size_t bpEntryBytes(int mode) {
   switch (mode) {
     case BP_CCOUNT: return 4;
     case BP_CMAT: return 8;
     case BP_WCOUNT: return 8;
+    case BP_KCOUNT: return 8;
     default: return 16;
   }
 }
@@ -424,7 +429,7 @@ template <int MODE, bool ITEMS = false, bool SPLIT = false, bool DIRECT = false>
 __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeKernel(BPArgs a, const BPItem *__restrict__ items,
                                                         const uint32_t *__restrict__ nItemsPtr, uint32_t capacity) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr bool WIDE = (MODE >= BP_WCOUNT);
+  constexpr bool WIDE = (MODE == BP_WCOUNT || MODE == BP_WMAT);
   constexpr bool MAT = (MODE == BP_CMAT || MODE == BP_WMAT);
   using Entry = typename std::conditional<MODE == BP_CCOUNT, uint32_t, unsigned long long>::type;
   using V = typename std::conditional<WIDE, ulonglong2, uint64_t>::type;
@@ -486,6 +491,10 @@ __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeK
             const uint32_t frag = rv[k];
             uint32_t h = hash32(frag, tbits);
             while (atomicCAS(&table[h], EMPTY32, frag) != EMPTY32) h = (h + 1) & mask;
+          } else if constexpr (MODE == BP_KCOUNT) {
+            const uint64_t v = rv[k];
+            uint32_t h = hash64(v, tbits);
+            while (atomicCAS(&table[h], EMPTY64, (unsigned long long)v) != EMPTY64) h = (h + 1) & mask;
           } else if constexpr (!WIDE) {
             const uint64_t v = rv[k];
             const uint32_t frag = (uint32_t)(v >> a.fragShift);
@@ -523,6 +532,14 @@ __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeK
             uint32_t e;
             while ((e = table[h]) != EMPTY32) {
               found += (e == frag);
+              h = (h + 1) & mask;
+            }
+          } else if constexpr (MODE == BP_KCOUNT) {
+            const uint64_t v = sv[k];
+            uint32_t h = hash64(v, tbits);
+            unsigned long long e;
+            while ((e = table[h]) != EMPTY64) {
+              found += (e == v);
               h = (h + 1) & mask;
             }
           } else if constexpr (!WIDE) {
@@ -594,8 +611,14 @@ void buildProbe(const BPArgs &args, const BPItem *items, const uint32_t *nItems,
   const uint32_t blocks = capacity < maxBlocks ? capacity : maxBlocks;
   HJ_CHECK(!(a.split && a.wide), "buildProbe: the split layout holds compressed tuples");
   HJ_CHECK(!a.split || (a.Rhi && a.Shi), "buildProbe: split layout without fragment columns");
-  HJ_CHECK(a.wide || a.fragShift >= 32, "buildProbe: fragShift=%u < 32 (the rid field of a CompressedTuple is >= 32 bits)",
-           a.fragShift);
+  HJ_CHECK(a.wide || a.keyOnly || a.fragShift >= 32,
+           "buildProbe: fragShift=%u < 32 (the rid field of a CompressedTuple is >= 32 bits)", a.fragShift);
+  HJ_CHECK(!(a.keyOnly && (a.materialize || a.wide || a.split)), "buildProbe: key-only words count only, unsplit");
+  if (bpMode(a) == BP_KCOUNT) {
+    hipLaunchKernelGGL(buildProbeKernel<BP_KCOUNT>, dim3(blocks), dim3(BPT), lds, s, a, items, nItems, capacity);
+    HIP_CHECK_LAUNCH();
+    return;
+  }
   if (bpMode(a) == BP_CCOUNT && a.split && bpDirect(a) && !a.itemCounts) {
     const size_t ldsD = ((size_t(4) << a.fragBits) + 15) / 16 * 16 + 64;
     const uint32_t perCuD = (uint32_t)std::min<size_t>(BPD_MINB, (160 * 1024) / ldsD);  // occupancy target

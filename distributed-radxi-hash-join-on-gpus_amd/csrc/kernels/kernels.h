@@ -121,9 +121,12 @@ void netGroupCursors(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uin
 // claiming from that chunk's gcur[g][d] (narrow = cursorsNarrow(n)).
 // keyBits: bits of the largest key (lets the kernel carry the digit in the
 // packed word's spare top bits instead of a separate LDS array).
+// withRids = false: key-only words (value = mixed key >> bits, keyShift 0) for
+// counting joins whose keys do not fit a CompressedTuple (JoinPlan::keyOnly).
 void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift, const PartitionGeometry &g,
                 uint32_t blockBegin, uint32_t blockEnd, void *gcur, uint64_t *out, hipStream_t s,
-                uint32_t keyBits = 64, KeyMix mix = KeyMix(), const void *gend = nullptr, int narrowMode = -1);
+                uint32_t keyBits = 64, KeyMix mix = KeyMix(), const void *gend = nullptr, int narrowMode = -1,
+                bool withRids = true);
 void netScatterWide(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
                     uint32_t blockBegin, uint32_t blockEnd, void *gcur, data::Tuple *out, hipStream_t s,
                     KeyMix mix = KeyMix(), const void *gend = nullptr, int narrowMode = -1);
@@ -257,6 +260,9 @@ struct BPArgs {
   uint32_t fragBits = 0;
   bool wide = false;
   bool materialize = false;
+  // Key-only words (JoinPlan::keyOnly, counting): R and S hold 8-byte
+  // key >> networkBits values; the table compares whole values.
+  bool keyOnly = false;
   // Split layout (on = 1): R and S are u32 rid columns, Rhi / Shi the u16
   // fragment columns (kernels.h, SplitLayout).
   uint32_t split = 0;

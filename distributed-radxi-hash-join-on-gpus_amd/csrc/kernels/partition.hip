@@ -244,9 +244,12 @@ struct NetCompressedPol {  // 16 B tuple -> 8 B CompressedTuple, digit in the to
   uint64_t mask;
   uint32_t bits, keyShift;
   KeyMix mix;
+  // ~0 = keep the rid below keyShift; 0 = key-only words (count-only joins of
+  // keys too wide for a CompressedTuple: value = key >> bits, keyShift = 0).
+  uint64_t ridMask = ~0ull;
   __device__ __forceinline__ uint32_t digit(const InT &x) const { return (uint32_t)(mix.apply(x.x) & mask); }
   __device__ __forceinline__ StageT stage(const InT &x, uint32_t d) const {
-    return x.y | ((mix.apply(x.x) >> bits) << keyShift) | ((uint64_t)d << (64 - bits));
+    return (x.y & ridMask) | ((mix.apply(x.x) >> bits) << keyShift) | ((uint64_t)d << (64 - bits));
   }
   __device__ __forceinline__ uint32_t stagedDigit(const StageT &v) const { return (uint32_t)(v >> (64 - bits)); }
   __device__ __forceinline__ OutT out(const StageT &v) const { return v & (~0ull >> bits); }
@@ -255,7 +258,7 @@ struct NetCompressedPol {  // 16 B tuple -> 8 B CompressedTuple, digit in the to
 struct NetCompressedDigPol : NetCompressedPol {  // no spare bits: digits staged separately
   static constexpr bool kDigArray = true;
   __device__ __forceinline__ StageT stage(const InT &x, uint32_t) const {
-    return x.y | ((mix.apply(x.x) >> bits) << keyShift);
+    return (x.y & ridMask) | ((mix.apply(x.x) >> bits) << keyShift);
   }
   __device__ __forceinline__ OutT out(const StageT &v) const { return v; }
   __device__ __forceinline__ void store(OutT *o, uint64_t pos, const StageT &v) const { o[pos] = out(v); }
@@ -623,6 +626,14 @@ template <class Pol>
 static void launchNetClaim(const Pol &pol, const data::Tuple *in, uint64_t n, uint32_t bits,
                            const PartitionGeometry &g, uint32_t blockBegin, uint32_t blockEnd, void *gcur,
                            void *out, hipStream_t s, const void *gend, bool narrow) {
+  // 4-byte staged words (count-only fragments) leave LDS room for 16384-tuple
+  // tiles: twice the run length per partition and tile (HPCJOIN_NET_IPT=16).
+  if constexpr (sizeof(typename Pol::StageT) == 4) {
+    if (netIpt() == 16) {
+      launchNetClaimIpt<Pol, 16>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
+      return;
+    }
+  }
   if (netIpt() == 15 && narrow && bits == MAX_PART_BITS)
     launchNetClaimIpt<Pol, 15>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
   else
@@ -631,7 +642,7 @@ static void launchNetClaim(const Pol &pol, const data::Tuple *in, uint64_t n, ui
 
 void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift, const PartitionGeometry &g,
                 uint32_t blockBegin, uint32_t blockEnd, void *gcur, uint64_t *out, hipStream_t s, uint32_t keyBits,
-                KeyMix mix, const void *gend, int narrowMode) {
+                KeyMix mix, const void *gend, int narrowMode, bool withRids) {
   const bool narrow = narrowMode < 0 ? cursorsNarrow(n) : narrowMode != 0;
   HJ_CHECK(bits >= 1 && bits <= MAX_PART_BITS, "netScatter: bits=%u out of range", bits);
   HJ_CHECK(blockBegin <= blockEnd && blockEnd <= g.blocks, "netScatter: block range [%u,%u) of %u", blockBegin,
@@ -642,6 +653,8 @@ void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keySh
   pol.bits = bits;
   pol.keyShift = keyShift;
   pol.mix = mix;
+  pol.ridMask = withRids ? ~0ull : 0ull;
+  HJ_CHECK(withRids || keyShift == 0, "netScatter: key-only words need keyShift 0 (got %u)", keyShift);
   if (digitFitsOnTop(bits, keyShift, mix.on ? std::max(keyBits, mix.bits) : keyBits)) {
     launchNetClaim(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
   } else {

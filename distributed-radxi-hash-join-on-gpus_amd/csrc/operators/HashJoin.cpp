@@ -172,7 +172,7 @@ void HashJoin::planBitmap() {
                             ((double)innerRelation->getGlobalSize() * wR + (double)outerRelation->getGlobalSize() * wS) /
                             8.0 / std::max<uint32_t>(N, 1);
   }
-  if (!config.bitmapJoin || plan.materialize || plan.wide || plan.keyBits >= 64) return;
+  if (!config.bitmapJoin || plan.materialize || plan.wide || plan.keyOnly || plan.keyBits >= 64) return;
   const uint32_t want = plan.keyBits > kernels::BITMAP_MAX_BITS ? plan.keyBits - kernels::BITMAP_MAX_BITS : 0;
   const uint32_t nb =
       config.networkBits ? config.networkBits : std::min<uint32_t>(kernels::MAX_PART_BITS, std::max<uint32_t>(10, want));
@@ -209,7 +209,7 @@ void HashJoin::planWireCodec(const std::vector<uint64_t> &all, size_t stride, ui
     plan.wireRidBits[r] = 0;
     plan.ridBase[r].assign((size_t)numberOfNodes * chunks, 0);
   }
-  if (plan.wide || numberOfNodes == 1 || config.wireCodec == core::WireCodecMode::Off) return;
+  if (plan.wide || plan.keyOnly || numberOfNodes == 1 || config.wireCodec == core::WireCodecMode::Off) return;
   const uint32_t keyW = plan.keyBits > plan.networkBits ? plan.keyBits - plan.networkBits : 0;
   for (int r = 0; r < 2; ++r) {
     uint64_t span = 1;

@@ -51,11 +51,12 @@ void BuildProbe::configure() {
   args.sChunk = plan.sChunk;
   args.fragShift = plan.wide ? 64 : plan.keyShift + wi->getLocalBits();
   args.keyShift = plan.keyShift;
-  if (!plan.wide && plan.directCount) {  // fragments are < 2^fragBits (direct-addressed counting when small)
+  if (!plan.wide && !plan.keyOnly && plan.directCount) {  // fragments are < 2^fragBits (direct-addressed counting when small)
     const uint32_t passBits = plan.networkBits + wi->getLocalBits();
     args.fragBits = plan.keyBits > passBits ? std::min<uint32_t>(32, plan.keyBits - passBits) : 1;
   }
   args.wide = plan.wide;
+  args.keyOnly = plan.keyOnly;
   args.materialize = plan.materialize;
   if (wi->getPartitionedHi()) {
     JOIN_ASSERT(wo->getPartitionedHi(), "BuildProbe", "one side split, the other not");

@@ -61,7 +61,8 @@ void NetworkPartitioning::partition(data::Relation *relation, data::Window *wind
                                 static_cast<data::Tuple *>(send), ctx->stream(), mix);
       else
         kernels::netScatter(relation->getData(), n, bits, plan.keyShift, g, b0, b1, gcur + c * perChunk,
-                            static_cast<uint64_t *>(send), ctx->stream(), plan.keyBits, mix);
+                            static_cast<uint64_t *>(send), ctx->stream(), plan.keyBits, mix, nullptr, -1,
+                            !plan.keyOnly);
       if (!single) window->exchange(send, c);
       if (afterChunk) afterChunk(c);
     }
@@ -70,7 +71,8 @@ void NetworkPartitioning::partition(data::Relation *relation, data::Window *wind
     host::netCursors(local->blockHistogram(), F, g.blocks, bpc, xp.digitBase.data(), cursors);
     for (uint32_t c = 0; c < chunks; ++c) {
       const uint32_t b0 = c * bpc, b1 = std::min(g.blocks, b0 + bpc);
-      host::netScatter(relation->getData(), n, bits, plan.keyShift, g, b0, b1, cursors, send, plan.wide, mix);
+      host::netScatter(relation->getData(), n, bits, plan.keyShift, g, b0, b1, cursors, send, plan.wide, mix,
+                       !plan.keyOnly);
       if (!single) window->exchange(send, c);
       if (afterChunk) afterChunk(c);
     }

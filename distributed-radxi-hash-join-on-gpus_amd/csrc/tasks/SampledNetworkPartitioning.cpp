@@ -145,7 +145,7 @@ void SampledNetworkPartitioning::scatterSide(int k) {
                             static_cast<data::Tuple *>(s.window->getData()), ctx->stream(), mix, s.gend, nm);
   else
     kernels::netScatter(s.relation->getData(), n, plan.networkBits, plan.keyShift, s.geom, 0, s.geom.blocks, s.gcur,
-                        static_cast<uint64_t *>(s.window->getData()), ctx->stream(), plan.keyBits, mix, s.gend, nm);
+                        static_cast<uint64_t *>(s.window->getData()), ctx->stream(), plan.keyBits, mix, s.gend, nm, !plan.keyOnly);
   const size_t bytes = (size_t)G * F * (s.narrow ? 4 : 8);
   s.cursorsBack = ctx->staging().get(bytes);
   HIP_CHECK(hipMemcpyAsync(s.cursorsBack, s.gcur, bytes, hipMemcpyDeviceToHost, ctx->stream()));

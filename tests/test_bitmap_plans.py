@@ -174,8 +174,9 @@ def test_sparse64_generator(C):
 
 @pytest.mark.parametrize("dev", devices())
 def test_sparse64_join_auto_wide(C, dev):
-    """63-bit keys do not fit a CompressedTuple: the planner switches to the
-    wide format by itself (no assertion) and the join is exact."""
+    """63-bit keys do not fit a CompressedTuple: the planner switches by itself
+    (no assertion) to 8-byte key-only words for a count and to the wide
+    format when materializing; both joins are exact."""
     loc = "device" if dev == "cuda" else "host"
     ctx = C.ExecContext(loc, 0 if loc == "device" else -1, C.LocalCommunicator())
     G_R, G_S = 150_000, 400_000
@@ -188,8 +189,42 @@ def test_sparse64_join_auto_wide(C, dev):
     R.generate(inner, 0)
     S.generate(outer, 0)
     j = C.HashJoin(R, S, ctx, C.JoinConfig())
-    assert j.plan.wide and not j.plan.bitmap_join and j.plan.key_bits == 63
-    assert j.run()["global_matches"] == C.Relation.expected_matches(inner, G_R, outer, G_S) == G_S
+    assert j.plan.key_only and not j.plan.wide and not j.plan.bitmap_join and j.plan.key_bits == 63
+    exp = C.Relation.expected_matches(inner, G_R, outer, G_S)
+    assert exp == G_S
+    for _ in range(2):
+        assert j.run()["global_matches"] == exp
+    cfg = C.JoinConfig()
+    cfg.materialize = True
+    j = C.HashJoin(R, S, ctx, cfg)
+    assert j.plan.wide and not j.plan.key_only
+    res = j.run()
+    assert res["global_matches"] == exp == res["output_pairs"]
+    pairs = j.output()
+    Rt, St = R.to_tensor().cpu(), S.to_tensor().cpu()
+    assert torch.equal(Rt[pairs[:, 0], 0], St[pairs[:, 1], 0])
+
+
+@pytest.mark.parametrize("dev", devices())
+@pytest.mark.parametrize("n_ranks", [2, 4])
+def test_sparse64_key_only_ranks(C, dev, n_ranks):
+    """Key-only words through the N-rank shuffle (exchange, local pass, KCOUNT
+    build/probe), chunked exchange included."""
+    loc = "device" if dev == "cuda" else "host"
+    G_R, G_S = 120_011, 300_007
+    inner = C.GenSpec(seed=31)
+    inner.sparse64 = True
+    outer = C.GenSpec(distribution=C.KeyDistribution.UNIFORM, seed=32, domain=G_R)
+    outer.sparse64 = True
+
+    def cfg_fn(c):
+        c.chunks = 2
+    out = run_ranks(C, n_ranks, loc, generated(C, loc, inner, G_R, n_ranks), generated(C, loc, outer, G_S, n_ranks),
+                    G_R, G_S, cfg_fn)
+    for res_list, plan in out:
+        assert plan.key_only and not plan.bitmap_join
+        for res in res_list:
+            assert res["global_matches"] == G_S
 
 
 def test_generated_relations_skip_planning_scans(C):

@@ -71,8 +71,11 @@ def test_plan_is_deterministic(C):
     assert (p.network_bits, p.local_bits, p.key_shift) == (9, 9, 32)
     p16 = C.make_plan(cfg, 8, 1_000_000_000, 16_000_000_000, 999_999_999, 16_000_000_000 - 1)
     assert p16.key_shift == 34  # 16B rids need 34 bits
-    wide = C.make_plan(cfg, 1, 1000, 1000, (1 << 62), 1000)  # keys too wide for a CompressedTuple
-    assert wide.wide and wide.key_shift == 64  # -> the 16-byte Tuple format, chosen by the planner
+    ko = C.make_plan(cfg, 1, 1000, 1000, (1 << 62), 1000)  # keys too wide for a CompressedTuple
+    assert ko.key_only and not ko.wide and ko.key_shift == 0  # counting: 8-byte key-only words
+    cfg.materialize = True
+    wide = C.make_plan(cfg, 1, 1000, 1000, (1 << 62), 1000)
+    assert wide.wide and wide.key_shift == 64  # materializing: the 16-byte Tuple format
     cfg.format = C.TupleFormat.WIDE
     with pytest.raises(RuntimeError):
         C.make_plan(cfg, 1, 1000, 1000, (1 << 64) - 1, 1000)  # the wide format reserves key 2^64-1
