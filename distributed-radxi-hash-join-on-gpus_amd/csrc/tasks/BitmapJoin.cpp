@@ -80,11 +80,13 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
     partitionSide(so, exact);
     HIP_CHECK(hipEventRecord(ev[2], st));
     HIP_CHECK(hipEventRecord(ev[3], st));
+    utils::faultPoint("local");
     utils::faultPoint("build_probe");
     kernels::bitmapJoin(4, si.frags, so.frags, si.slices, so.slices, F, 0, bits, cnt, st);
   } else {
     const uint32_t words = kernels::bitmapWords(bits);
     uint32_t *bm = ws.getArray<uint32_t>((size_t)F * words);
+    utils::faultPoint("local");
     kernels::bitmapBuild(4, si.frags, si.slices, F, 0, bits, bm, cnt, st);
     hipEvent_t built = ctx->acquireEvent(), reduced = ctx->acquireEvent();
     HIP_CHECK(hipEventRecord(built, st));
@@ -143,6 +145,7 @@ BitmapJoin::Outcome BitmapJoin::runHost() {
   utils::faultPoint("network");
   partition(inner, rf, rb);
   partition(outer, sf, sb);
+  utils::faultPoint("local");
   std::vector<uint64_t> bm64((size_t)F * words / 2, 0);
   uint32_t *bm = reinterpret_cast<uint32_t *>(bm64.data());
   uint32_t flags = 0;
