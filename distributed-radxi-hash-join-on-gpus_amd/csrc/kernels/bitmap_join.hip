@@ -75,30 +75,40 @@ struct TableSrc {
   }
 };
 
-// fn(fragment) for every element of src[0, len).
+// fn(fragment) for every element of src[0, len).  u32 fragments: 16-byte
+// vector loads, software-pipelined -- batch k+1 is in flight while batch k is
+// consumed, so a workgroup (one per CU: its 128 KiB bitmap fills the LDS) does
+// not sit out one HBM latency per batch.
 template <typename E, int U, typename Fn>
 __device__ __forceinline__ void visitSlice(const E *__restrict__ src, uint64_t len, uint32_t shift, Fn &&fn) {
   const uint32_t t = threadIdx.x;
   if constexpr (sizeof(E) == 4) {
     const u32x4 *v = reinterpret_cast<const u32x4 *>(src);
     const uint64_t nv = len >> 2;
-    for (uint64_t i0 = 0; i0 < nv; i0 += (uint64_t)BM_NTH * U) {
-      u32x4 x[U];
+    constexpr uint64_t STEP = (uint64_t)BM_NTH * U;
+    u32x4 cur[U], nxt[U];
+    auto load = [&](u32x4(&x)[U], uint64_t i0) {
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         const uint64_t i = i0 + (uint64_t)k * BM_NTH + t;
         if (i < nv) x[k] = __builtin_nontemporal_load(v + i);
       }
+    };
+    if (nv) load(cur, 0);
+    for (uint64_t i0 = 0; i0 < nv; i0 += STEP) {
+      if (i0 + STEP < nv) load(nxt, i0 + STEP);
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         const uint64_t i = i0 + (uint64_t)k * BM_NTH + t;
         if (i < nv) {
-          fn((uint64_t)x[k].x);
-          fn((uint64_t)x[k].y);
-          fn((uint64_t)x[k].z);
-          fn((uint64_t)x[k].w);
+          fn((uint64_t)cur[k].x);
+          fn((uint64_t)cur[k].y);
+          fn((uint64_t)cur[k].z);
+          fn((uint64_t)cur[k].w);
         }
       }
+#pragma unroll
+      for (int k = 0; k < U; ++k) cur[k] = nxt[k];
     }
     const uint32_t rem = (uint32_t)(len & 3);
     if (t < rem) fn((uint64_t)src[(nv << 2) + t]);
@@ -120,10 +130,14 @@ __device__ __forceinline__ void visitSlice(const E *__restrict__ src, uint64_t l
   }
 }
 
+// Build: fire-and-forget LDS ORs (no returned value to wait for); a repeated
+// fragment is found afterwards as fewer set bits than inserted fragments
+// (bmCheckDup).  Returns this thread's inserted count.
 template <typename E, int U, class Src>
-__device__ __forceinline__ void bmBuild(uint32_t *bm, const E *__restrict__ r, const Src &rs, uint32_t shift,
-                                        uint64_t limit, uint32_t &flags) {
+__device__ __forceinline__ uint64_t bmBuild(uint32_t *bm, const E *__restrict__ r, const Src &rs, uint32_t shift,
+                                            uint64_t limit, uint32_t &flags) {
   const uint32_t d = blockIdx.x;
+  uint32_t inserted = 0;
   for (uint32_t g = 0; g < rs.groups(); ++g) {
     uint64_t b, len;
     rs.get(d, g, b, len, flags);
@@ -132,10 +146,23 @@ __device__ __forceinline__ void bmBuild(uint32_t *bm, const E *__restrict__ r, c
         flags |= BM_FLAG_DUP;
         return;
       }
-      const uint32_t bit = 1u << (f & 31);
-      if (atomicOr(&bm[f >> 5], bit) & bit) flags |= BM_FLAG_DUP;
+      __hip_atomic_fetch_or(&bm[f >> 5], 1u << (f & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      ++inserted;
     });
   }
+  return inserted;
+}
+
+// After the build's barrier: set bits of the bitmap vs fragments inserted by
+// the whole workgroup; fewer bits = a repeated inner key.  Returns the bits.
+__device__ __forceinline__ uint64_t bmCheckDup(const uint32_t *bm, uint32_t words, uint64_t inserted, uint32_t &flags,
+                                               uint64_t *wt) {
+  uint64_t bits = 0;
+  for (uint32_t w = threadIdx.x; w < words; w += BM_NTH) bits += __popc(bm[w]);
+  const uint64_t setBits = blockReduceSum<BM_NTH, uint64_t>(bits, wt);
+  const uint64_t total = blockReduceSum<BM_NTH, uint64_t>(inserted, wt);
+  if (setBits != total) flags |= BM_FLAG_DUP;
+  return setBits;
 }
 
 template <typename E, int U, class Src>
@@ -171,12 +198,14 @@ __global__ __launch_bounds__(BM_NTH) void bitmapJoinKernel(const E *__restrict__
                                                            Src ss, uint32_t shift, uint32_t words,
                                                            BitmapCounters *__restrict__ out) {
   extern __shared__ uint32_t bm[];
+  __shared__ uint64_t wt[BM_NTH / WAVE];
   for (uint32_t w = threadIdx.x; w < words; w += BM_NTH) bm[w] = 0;
   __syncthreads();
   const uint64_t limit = (uint64_t)words * 32;
   uint32_t flags = 0;
-  bmBuild<E, U>(bm, r, rs, shift, limit, flags);
+  const uint64_t inserted = bmBuild<E, U>(bm, r, rs, shift, limit, flags);
   __syncthreads();
+  bmCheckDup(bm, words, inserted, flags, wt);
   const uint64_t cnt = bmProbe<E, U>(bm, s, ss, shift, limit, flags);
   bmFinish(out, cnt, 0, flags);
 }
@@ -186,11 +215,13 @@ __global__ __launch_bounds__(BM_NTH) void bitmapBuildKernel(const E *__restrict_
                                                             uint32_t words, uint32_t *__restrict__ bitmaps,
                                                             BitmapCounters *__restrict__ out) {
   extern __shared__ uint32_t bm[];
+  __shared__ uint64_t wt[BM_NTH / WAVE];
   for (uint32_t w = threadIdx.x; w < words; w += BM_NTH) bm[w] = 0;
   __syncthreads();
   uint32_t flags = 0;
-  bmBuild<E, U>(bm, r, rs, shift, (uint64_t)words * 32, flags);
+  const uint64_t inserted = bmBuild<E, U>(bm, r, rs, shift, (uint64_t)words * 32, flags);
   __syncthreads();
+  bmCheckDup(bm, words, inserted, flags, wt);
   uint32_t *dst = bitmaps + (size_t)blockIdx.x * words;
   for (uint32_t w = threadIdx.x; w < words; w += BM_NTH) dst[w] = bm[w];
   bmFinish(out, 0, 0, flags);
