@@ -921,6 +921,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   meas.def("store_all", &performance::Measurements::storeAllMeasurements);
   meas.def("snapshot", &performance::Measurements::snapshot);
+  meas.def("reference_keys", &performance::Measurements::referenceKeys,
+           "The reference's .perf keys (performance/Measurements.cpp:136-542), all present after every join");
   meas.def("serialize", &performance::Measurements::serializeResults);
 
   auto ops = m.def_submodule("ops", "kernel-level entry points on torch tensors (device or host)");

@@ -4,6 +4,7 @@
 
 #include "../comm/Communicator.h"
 #include "../memory/Arena.h"
+#include "../performance/Timeline.h"
 #include "../utils/Fault.h"
 #include "../utils/Hip.h"
 
@@ -20,6 +21,7 @@ ExecContext::ExecContext(Location loc, int device, comm::Communicator *comm)
   // Pinned on a device engine: host->device uploads and device->host result
   // copies through it are true DMA transfers that never block the host.
   staging_.reset(new memory::Arena(onDevice() ? Location::Pinned : Location::Host, device_));
+  timeline_.reset(new performance::Timeline(onDevice()));
   if (onDevice()) {
     HIP_CHECK(hipSetDevice(device_));
     HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
@@ -30,6 +32,7 @@ ExecContext::ExecContext(Location loc, int device, comm::Communicator *comm)
 
 ExecContext::~ExecContext() {
   for (hipEvent_t e : events_) (void)hipEventDestroy(e);
+  timeline_.reset();
   workspace_.reset();
   staging_.reset();
   if (stream_) (void)hipStreamDestroy(stream_);

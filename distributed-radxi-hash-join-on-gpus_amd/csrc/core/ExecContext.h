@@ -18,6 +18,9 @@ class Communicator;
 namespace memory {
 class Arena;
 }
+namespace performance {
+class Timeline;
+}
 
 namespace core {
 
@@ -40,6 +43,7 @@ class ExecContext {
   uint32_t numberOfNodes() const;
   memory::Arena &workspace() { return *workspace_; }  // data-side scratch (HBM or host), reset per join
   memory::Arena &staging() { return *staging_; }      // pinned host scratch for plans/results, reset per join
+  performance::Timeline &timeline() { return *timeline_; }  // sub-phase spans of the current join (.perf keys)
 
   void synchronize() const;                 // compute + comm streams
   void copy(void *dst, const void *src, uint64_t bytes, bool toDevice, bool fromDevice) const;  // async on stream()
@@ -60,6 +64,7 @@ class ExecContext {
   hipStream_t decodeStream_ = nullptr;
   std::unique_ptr<memory::Arena> workspace_;
   std::unique_ptr<memory::Arena> staging_;
+  std::unique_ptr<performance::Timeline> timeline_;
 };
 
 }  // namespace core

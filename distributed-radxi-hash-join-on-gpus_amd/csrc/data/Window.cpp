@@ -6,6 +6,8 @@
 #include "../comm/Communicator.h"
 #include "../host/HostOps.h"
 #include "../memory/Arena.h"
+#include "../performance/Measurements.h"
+#include "../performance/Timeline.h"
 #include "../utils/Hip.h"
 
 namespace hpcjoin {
@@ -62,6 +64,11 @@ std::unique_ptr<Window> Window::chunkView(uint32_t chunk) const {
 }
 
 Window::~Window() = default;  // events belong to the context pool
+
+hipStream_t Window::completionStream() const {
+  if (!ctx->onDevice() || plan.numberOfNodes == 1) return ctx->stream();
+  return codec.w ? ctx->decodeStream() : ctx->commStream();
+}
 
 void Window::setWireCodec(const kernels::WireCodec &c, const std::vector<uint64_t> &bases) {
   JOIN_ASSERT(!wide || c.w == 0, "Window", "the wire codec packs 8-byte CompressedTuples only");
@@ -122,11 +129,13 @@ void Window::exchangePacked(const uint64_t *send, uint32_t chunk) {
     kernels::wirePack(send, wsend, dS, (uint32_t)ss.size(), sGroups, codec, ctx->stream());
     HIP_CHECK(hipEventRecord(ready[chunk], ctx->stream()));
     HIP_CHECK(hipStreamWaitEvent(ctx->commStream(), ready[chunk], 0));
+    ctx->timeline().begin("MWINPUT", ctx->commStream());
     if (selfN)
       HIP_CHECK(hipMemcpyAsync(dst + selfDst, send + selfSrc, selfN * 8, hipMemcpyDeviceToDevice,
                                ctx->commStream()));
     ctx->comm()->allToAllV(wsend, sc.data(), sd.data(), wrecv, rc.data(), rd.data(), Location::Device,
                            ctx->commStream());
+    ctx->timeline().end("MWINPUT", ctx->commStream());
     HIP_CHECK(hipEventRecord(wired[chunk], ctx->commStream()));
     HIP_CHECK(hipStreamWaitEvent(ctx->decodeStream(), wired[chunk], 0));
     kernels::wireUnpack(wrecv, dst, dR, (uint32_t)rs.size(), rGroups, codec, ctx->decodeStream());
@@ -134,8 +143,10 @@ void Window::exchangePacked(const uint64_t *send, uint32_t chunk) {
   } else {
     host::wirePack(send, wsend, ss.data(), (uint32_t)ss.size(), codec);
     if (selfN) std::memcpy(dst + selfDst, send + selfSrc, selfN * 8);
+    ctx->timeline().begin("MWINPUT");
     ctx->comm()->allToAllV(wsend, sc.data(), sd.data(), wrecv, rc.data(), rd.data(), ctx->location(),
                            ctx->stream());
+    ctx->timeline().end("MWINPUT");
     host::wireUnpack(wrecv, dst, rs.data(), (uint32_t)rs.size(), codec);
   }
 }
@@ -144,6 +155,7 @@ void Window::start() { open = true; }
 
 void Window::exchange(const void *sendBuffer, uint32_t chunk) {
   JOIN_ASSERT(chunk < plan.chunks, "Window", "chunk %u out of range", chunk);
+  performance::Measurements::add("MWINPUTCNT", 1, "calls");  // one all-to-allv per chunk (the MPI_Put analog)
   if (codec.w && plan.numberOfNodes > 1) {
     exchangePacked(static_cast<const uint64_t *>(sendBuffer), chunk);
     exchanged[chunk] = true;
@@ -165,11 +177,15 @@ void Window::exchange(const void *sendBuffer, uint32_t chunk) {
   if (ctx->onDevice() && N > 1) {
     HIP_CHECK(hipEventRecord(ready[chunk], ctx->stream()));
     HIP_CHECK(hipStreamWaitEvent(ctx->commStream(), ready[chunk], 0));
+    ctx->timeline().begin("MWINPUT", ctx->commStream());
     ctx->comm()->allToAllV(src, sc.data(), sd.data(), dst, rc.data(), rd.data(), Location::Device,
                            ctx->commStream());
+    ctx->timeline().end("MWINPUT", ctx->commStream());
     HIP_CHECK(hipEventRecord(done[chunk], ctx->commStream()));
   } else {
+    ctx->timeline().begin("MWINPUT");
     ctx->comm()->allToAllV(src, sc.data(), sd.data(), dst, rc.data(), rd.data(), ctx->location(), ctx->stream());
+    ctx->timeline().end("MWINPUT");
   }
   exchanged[chunk] = true;
 }
@@ -183,6 +199,7 @@ void Window::stop() {
   if (ctx->onDevice() && plan.numberOfNodes > 1)
     for (uint32_t c = 0; c < plan.chunks; ++c)
       if (exchanged[c]) HIP_CHECK(hipStreamWaitEvent(ctx->stream(), done[c], 0));
+  if (plan.numberOfNodes > 1 && open) performance::Measurements::add("MWINWAITCNT", 1, "calls");
   open = false;
 }
 

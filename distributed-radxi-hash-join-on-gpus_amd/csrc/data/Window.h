@@ -48,6 +48,8 @@ class Window {
   // Enqueue the all-to-allv of one chunk once the compute stream reaches this
   // point (the chunk's scatter kernel is already enqueued on it).
   void exchange(const void *sendBuffer, uint32_t chunk);
+  // Stream on which this window's last exchange step completes.
+  hipStream_t completionStream() const;
   // Bit-pack tuples on the wire (kernels.h, WireCodec); ridBase[rank * C + c]
   // is the rid base of sender `rank`'s chunk c (C = ridBase.size() / ranks).
   // Call before the first exchange.

@@ -18,7 +18,7 @@ struct State {
   std::string tag = "experiment", dir;
   std::map<std::string, std::string> meta;
   std::map<std::string, std::pair<double, std::string>> values;
-  uint64_t joinStart = 0, joinStop = 0;
+  uint64_t joinStart = 0, joinStop = 0, cycleStart = 0;
   uint64_t phaseStart[8] = {0};
   uint64_t phaseTime[8] = {0};
   uint64_t tuples = 0;
@@ -33,6 +33,48 @@ void end(int p) { st().phaseTime[p] = nowUs() - st().phaseStart[p]; }
 }  // namespace
 
 void Measurements::put(const std::string &key, double v, const char *unit) { st().values[key] = {v, unit}; }
+void Measurements::add(const std::string &key, double v, const char *unit) {
+  auto &e = st().values[key];
+  e.first += v;
+  e.second = unit;
+}
+
+// The reference's .perf keys (performance/Measurements.cpp:136-542) and units.
+static const std::vector<std::pair<std::string, const char *>> &refKeyUnits() {
+  static const std::vector<std::pair<std::string, const char *>> k = {
+      {"CTOTAL", "cycles"},     {"JTOTAL", "us"},         {"JHIST", "us"},          {"JMPI", "us"},
+      {"JPROC", "us"},          {"SWINALLOC", "us"},      {"SNETCOMPL", "us"},      {"SLOCPREP", "us"},
+      {"HILOCAL", "us"},        {"HILOCELEM", "tuples"},  {"HILOCRATE", "Mbytes/sec"}, {"HOLOCAL", "us"},
+      {"HOLOCELEM", "tuples"},  {"HOLOCRATE", "Mbytes/sec"}, {"HIGLOBAL", "us"},    {"HOGLOBAL", "us"},
+      {"HASSIGN", "us"},        {"HIOFFCOMP", "us"},      {"HOOFFCOMP", "us"},      {"MIMEMALLOC", "us"},
+      {"MIMAINPART", "us"},     {"MIFLUSHPART", "us"},    {"MOMEMALLOC", "us"},     {"MOMAINPART", "us"},
+      {"MOFLUSHPART", "us"},    {"MWINPUT", "us"},        {"MWINPUTCNT", "calls"},  {"MWINWAIT", "us"},
+      {"MWINWAITCNT", "calls"}, {"LPTASKTIME", "us"},     {"LPTASKCOUNT", "tasks"}, {"LPHISTCOMP", "us"},
+      {"LPHISTELEM", "tuples"}, {"LPOFFSET", "us"},       {"LPMEMALLOC", "us"},     {"LPMEMSIZE", "bytes"},
+      {"LPPART", "us"},         {"LPELEMENTS", "tuples"}, {"BPTASKTIME", "us"},     {"BPTASKCOUNT", "tasks"},
+      {"BPMEMALLOC", "us"},     {"BPMEMSIZE", "bytes"},   {"BPBUILD", "us"},        {"BPBUILDELEM", "tuples"},
+      {"BPPROBE", "us"},        {"BPPROBEELEM", "tuples"}};
+  return k;
+}
+
+const std::vector<std::string> &Measurements::referenceKeys() {
+  static const std::vector<std::string> keys = [] {
+    std::vector<std::string> v;
+    for (auto &ku : refKeyUnits()) v.push_back(ku.first);
+    return v;
+  }();
+  return keys;
+}
+
+// Host CPU cycles (the reference reads PAPI_TOT_CYC, Measurements.cpp:90-107;
+// PAPI is not in this image, the TSC is the same clock on x86).
+static uint64_t cycles() {
+#if defined(__x86_64__)
+  return __builtin_ia32_rdtsc();
+#else
+  return 0;
+#endif
+}
 
 void Measurements::init(uint32_t nodeId, uint32_t numberOfNodes, const std::string &tag, const std::string &dir) {
   State &s = st();
@@ -52,11 +94,25 @@ void Measurements::init(uint32_t nodeId, uint32_t numberOfNodes, const std::stri
 void Measurements::writeMetaData(const char *key, const char *value) { st().meta[key] = value; }
 void Measurements::writeMetaData(const char *key, uint64_t value) { st().meta[key] = std::to_string(value); }
 
-void Measurements::startJoin() { st().joinStart = nowUs(); }
+void Measurements::startJoin() {
+  State &s = st();
+  s.values.clear();
+  for (auto &ku : refKeyUnits()) s.values[ku.first] = {0.0, ku.second};
+  for (uint64_t &t : s.phaseTime) t = 0;
+  s.joinStart = nowUs();
+  s.cycleStart = cycles();
+}
 void Measurements::stopJoin() {
   State &s = st();
   s.joinStop = nowUs();
+  put("CTOTAL", (double)(cycles() - s.cycleStart), "cycles");
   put("JTOTAL", (double)(s.joinStop - s.joinStart), "us");
+  put("MWINWAIT", (double)s.phaseTime[NETWAIT], "us");
+  for (const char *side : {"I", "O"}) {  // histogram read rate: 16-byte tuples per µs = MB/s
+    const double us = s.values[std::string("H") + side + "LOCAL"].first;
+    const double el = s.values[std::string("H") + side + "LOCELEM"].first;
+    put(std::string("H") + side + "LOCRATE", us > 0 ? el * 16.0 / us : 0.0, "Mbytes/sec");
+  }
   put("JHIST", (double)s.phaseTime[HIST], "us");
   put("JMPI", (double)(s.phaseTime[WINALLOC] + s.phaseTime[NET] + s.phaseTime[NETWAIT]), "us");
   put("JPROC", (double)(s.phaseTime[LOCPREP] + s.phaseTime[LOCAL]), "us");
@@ -83,24 +139,23 @@ void Measurements::storeHistogramDetails(uint64_t localUs, uint64_t innerElement
                                          uint64_t globalUs, uint64_t assignUs, uint64_t offsetUs) {
   // The device computes both relations' histograms in one enqueue + sync; the
   // time is split by element count for the per-relation keys.
-  const double tot = (double)(innerElements + outerElements);
-  const double fi = tot > 0 ? innerElements / tot : 0.5;
-  put("HILOCAL", localUs * fi, "us");
+  // HILOCAL / HOLOCAL: each relation's histogram kernels (Timeline spans);
+  // the rates follow at stopJoin().
+  (void)localUs;
   put("HILOCELEM", (double)innerElements, "tuples");
-  put("HILOCRATE", localUs ? innerElements * 16.0 / (localUs * fi) : 0, "Mbytes/sec");
-  put("HOLOCAL", localUs * (1 - fi), "us");
   put("HOLOCELEM", (double)outerElements, "tuples");
-  put("HOLOCRATE", localUs ? outerElements * 16.0 / (localUs * (1 - fi)) : 0, "Mbytes/sec");
-  put("HIGLOBAL", (double)globalUs, "us");
-  put("HOGLOBAL", 0, "us");  // fused into HIGLOBAL (one all-gather for both relations)
+  // One fused all-gather carries both relations' histograms (unless the
+  // outer one runs behind the inner exchange: HOGLOBAL is then timed on its
+  // own stream by the Timeline): each relation is charged half of it.
+  put("HIGLOBAL", globalUs / 2.0, "us");
+  put("HOGLOBAL", globalUs / 2.0, "us");
   put("HASSIGN", (double)assignUs, "us");
   put("HIOFFCOMP", offsetUs / 2.0, "us");
   put("HOOFFCOMP", offsetUs / 2.0, "us");
 }
 
 void Measurements::storeNetworkDetails(uint64_t innerElements, uint64_t outerElements, uint64_t chunks) {
-  put("MIMAINPART", (double)st().phaseTime[NET], "us");
-  put("MWINPUTCNT", (double)chunks, "calls");
+  (void)chunks;  // MWINPUTCNT counts the exchanges themselves (Window::exchange)
   put("MIELEM", (double)innerElements, "tuples");
   put("MOELEM", (double)outerElements, "tuples");
 }

@@ -57,8 +57,12 @@ class Measurements {
 
   static uint64_t joinUs();
 
- private:
+  // Detailed keys (sub-phases, counts, bytes): set / accumulate into this
+  // join's table.  Every reference key exists from startJoin() on (0 when a
+  // plan has no such step), so reports always carry the full key set.
   static void put(const std::string &key, double v, const char *unit);
+  static void add(const std::string &key, double v, const char *unit);
+  static const std::vector<std::string> &referenceKeys();
 };
 
 }  // namespace performance

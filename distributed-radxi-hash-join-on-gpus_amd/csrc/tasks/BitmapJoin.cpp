@@ -5,6 +5,8 @@
 
 #include "../comm/Communicator.h"
 #include "../memory/Arena.h"
+#include "../performance/Measurements.h"
+#include "../performance/Timeline.h"
 #include "../performance/Trace.h"
 #include "../utils/Fault.h"
 #include "../utils/Hip.h"
@@ -38,6 +40,9 @@ void BitmapJoin::partitionSide(Side &s, bool exact) {
   memory::Arena &ws = ctx->workspace();
   const hipStream_t st = ctx->stream();
   const kernels::KeyMix mix{plan.keyMix ? 1u : 0u, plan.keyBits};
+  const bool isInner = s.relation == inner;
+  performance::Timeline &tl = ctx->timeline();
+  tl.begin(isInner ? "HILOCAL" : "HOLOCAL", st);
   s.geom = kernels::partitionGeometry(n, maxBlocks);
   uint32_t *blockHist = ws.getArray<uint32_t>((uint64_t)F * s.geom.blocks);
   uint64_t *totals = ws.getArray<uint64_t>((uint64_t)G * F);
@@ -51,9 +56,12 @@ void BitmapJoin::partitionSide(Side &s, bool exact) {
   void *gstart = ws.get((size_t)G * F * cb), *gcur = ws.get((size_t)G * F * cb), *gend = ws.get((size_t)G * F * cb);
   unsigned long long *used = ws.getArray<unsigned long long>(1);
   kernels::netSampledLayout(totals, F, sc, gstart, gcur, gend, narrow, used, st);
+  tl.end(isInner ? "HILOCAL" : "HOLOCAL", st);
   s.frags = ws.getArray<uint32_t>(std::max<uint64_t>(cap, 16));
+  tl.begin(isInner ? "MIMAINPART" : "MOMAINPART", st);
   kernels::netScatterFrag(s.relation->getData(), n, bits, s.geom, 0, s.geom.blocks, gcur, s.frags, st, plan.keyBits,
                           mix, gend, narrow ? 1 : 0);
+  tl.end(isInner ? "MIMAINPART" : "MOMAINPART", st);
   s.slices = BitmapSlices();
   s.slices.kind = BitmapSlices::Claim;
   s.slices.start = gstart;
@@ -82,17 +90,31 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
     HIP_CHECK(hipEventRecord(ev[3], st));
     utils::faultPoint("local");
     utils::faultPoint("build_probe");
+    // One kernel builds and probes: charged to BPBUILD / BPPROBE by tuples read.
+    ctx->timeline().begin("BPTASKTIME", st);
+    ctx->timeline().beginSplit("BPKERNEL", "BPBUILD", (double)inner->getLocalSize(), "BPPROBE",
+                               (double)outer->getLocalSize(), st);
     kernels::bitmapJoin(4, si.frags, so.frags, si.slices, so.slices, F, 0, bits, cnt, st);
+    ctx->timeline().end("BPKERNEL", st);
+    ctx->timeline().end("BPTASKTIME", st);
   } else {
     const uint32_t words = kernels::bitmapWords(bits);
     uint32_t *bm = ws.getArray<uint32_t>((size_t)F * words);
     utils::faultPoint("local");
+    performance::Timeline &tl = ctx->timeline();
+    tl.begin("BPTASKTIME", st);
+    tl.begin("BPBUILD", st);
     kernels::bitmapBuild(4, si.frags, si.slices, F, 0, bits, bm, cnt, st);
+    tl.end("BPBUILD", st);
     hipEvent_t built = ctx->acquireEvent(), reduced = ctx->acquireEvent();
     HIP_CHECK(hipEventRecord(built, st));
     HIP_CHECK(hipStreamWaitEvent(ctx->commStream(), built, 0));
-    // The all-reduce (exchange stream) overlaps the outer side's network pass.
+    // The all-reduce (exchange stream) overlaps the outer side's network pass:
+    // the plan's one link transfer (the reference's puts, MWINPUT).
+    performance::Measurements::add("MWINPUTCNT", 1, "calls");
+    tl.begin("MWINPUT", ctx->commStream());
     ctx->comm()->allReduceSumDevice(reinterpret_cast<uint64_t *>(bm), (size_t)F * words / 2, ctx->commStream());
+    tl.end("MWINPUT", ctx->commStream());
     HIP_CHECK(hipEventRecord(reduced, ctx->commStream()));
     o.linkBytes = (uint64_t)(2.0 * (N - 1) / N * (double)F * words * 4);
     partitionSide(so, exact);
@@ -100,8 +122,15 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
     HIP_CHECK(hipStreamWaitEvent(st, reduced, 0));
     HIP_CHECK(hipEventRecord(ev[3], st));
     utils::faultPoint("build_probe");
+    tl.begin("BPPROBE", st);
     kernels::bitmapProbe(4, so.frags, so.slices, F, 0, bits, bm, cnt, st);
+    tl.end("BPPROBE", st);
+    tl.end("BPTASKTIME", st);
   }
+  performance::Measurements::add("BPBUILDELEM", (double)inner->getLocalSize(), "tuples");
+  performance::Measurements::add("BPPROBEELEM", (double)outer->getLocalSize(), "tuples");
+  performance::Measurements::add("BPMEMSIZE", (double)(N > 1 ? (uint64_t)F * kernels::bitmapWords(bits) * 4 : 0),
+                                 "bytes");
   HIP_CHECK(hipEventRecord(ev[4], st));
   BitmapCounters *back = ctx->staging().getArray<BitmapCounters>(1);
   HIP_CHECK(hipMemcpyAsync(back, cnt, sizeof(BitmapCounters), hipMemcpyDeviceToHost, st));
@@ -142,10 +171,17 @@ BitmapJoin::Outcome BitmapJoin::runHost() {
   };
   std::vector<uint32_t> rf, sf;
   std::vector<uint64_t> rb, sb;
+  performance::Timeline &tl = ctx->timeline();
   utils::faultPoint("network");
+  tl.begin("MIMAINPART");
   partition(inner, rf, rb);
+  tl.end("MIMAINPART");
+  tl.begin("MOMAINPART");
   partition(outer, sf, sb);
+  tl.end("MOMAINPART");
   utils::faultPoint("local");
+  tl.begin("BPTASKTIME");
+  tl.begin("BPBUILD");
   std::vector<uint64_t> bm64((size_t)F * words / 2, 0);
   uint32_t *bm = reinterpret_cast<uint32_t *>(bm64.data());
   uint32_t flags = 0;
@@ -161,18 +197,26 @@ BitmapJoin::Outcome BitmapJoin::runHost() {
       if (w & bit) flags |= kernels::BM_FLAG_DUP;
       w |= bit;
     }
+  tl.end("BPBUILD");
   Outcome o;
   if (N > 1) {
+    performance::Measurements::add("MWINPUTCNT", 1, "calls");
+    tl.begin("MWINPUT");
     ctx->comm()->allReduceSumHost(bm64.data(), bm64.size());
+    tl.end("MWINPUT");
     o.linkBytes = (uint64_t)(2.0 * (N - 1) / N * (double)bm64.size() * 8);
     for (uint64_t w : bm64) o.popcount += (uint64_t)__builtin_popcountll(w);
   }
   utils::faultPoint("build_probe");
+  tl.begin("BPPROBE");
   for (uint32_t p = 0; p < F; ++p)
     for (uint64_t i = sb[p]; i < sb[p + 1]; ++i) {
       const uint64_t f = sf[i];
       if (f < limit) o.localMatches += (bm[(size_t)p * words + (f >> 5)] >> (f & 31)) & 1u;
     }
+  tl.end("BPPROBE");
+  tl.end("BPTASKTIME");
+  performance::Measurements::add("BPMEMSIZE", (double)(bm64.size() * 8), "bytes");
   agree(o, flags);
   return o;
 }

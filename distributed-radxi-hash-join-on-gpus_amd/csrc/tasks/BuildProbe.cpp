@@ -5,6 +5,9 @@
 
 #include "../host/HostOps.h"
 #include "../memory/Arena.h"
+#include "../performance/Clock.h"
+#include "../performance/Measurements.h"
+#include "../performance/Timeline.h"
 #include "../operators/HashJoin.h"
 #include "../utils/Hip.h"
 
@@ -85,14 +88,27 @@ void BuildProbe::execute() {
     args.outPairs = outPairs;
     args.outCapacity = outputCapacity;
   }
+  performance::Timeline &tl = ctx->timeline();
+  // The build and the probe of one LDS table run in one kernel (one work
+  // item = build + probe): its time is charged to BPBUILD / BPPROBE in
+  // proportion to the tuples each reads.
+  const double wb = (double)innerPartitionSize, wp = (double)outerPartitionSize;
+  performance::Measurements::add("BPBUILDELEM", wb, "tuples");
+  performance::Measurements::add("BPPROBEELEM", wp, "tuples");
   if (!dev) {
     hostCursor = 0;
     args.outCursor = reinterpret_cast<unsigned long long *>(&hostCursor);
+    tl.begin("BPTASKTIME");
+    tl.beginSplit("BPKERNEL", "BPBUILD", wb, "BPPROBE", wp);
     matches = host::buildProbe(args);
+    tl.end("BPKERNEL");
+    tl.end("BPTASKTIME");
     outputCount = hostCursor;
     workItems = args.P;
     return;
   }
+  tl.begin("BPTASKTIME", ctx->stream());
+  const uint64_t tAlloc = performance::nowUs();
   counters = ws.getArray<unsigned long long>(4);
   HIP_CHECK(hipMemsetAsync(counters, 0, 4 * sizeof(unsigned long long), ctx->stream()));
   args.result = counters;
@@ -102,11 +118,19 @@ void BuildProbe::execute() {
   uint32_t *offsets = ws.getArray<uint32_t>(std::max<uint32_t>(args.P, 1));
   void *scanWs = ws.get(kernels::scanWorkspaceBytes(args.P));
   kernels::BPItem *items = ws.getArray<kernels::BPItem>(capacity);
+  performance::Measurements::add("BPMEMALLOC", (double)(performance::nowUs() - tAlloc), "us");
+  performance::Measurements::add("BPMEMSIZE",
+                                 (double)(2ull * std::max<uint32_t>(args.P, 1) * 4 + kernels::scanWorkspaceBytes(args.P) +
+                                          (uint64_t)capacity * sizeof(kernels::BPItem) + kernels::bpLdsBytes(args)),
+                                 "bytes");
   kernels::bpPlanCounts(args, counts, ctx->stream());
   kernels::scanExclusiveU32(counts, offsets, args.P, nItems, scanWs, ctx->stream());
   kernels::bpEmit(args, counts, offsets, items, capacity, ctx->stream());
   if (!plan.materialize) {
+    tl.beginSplit("BPKERNEL", "BPBUILD", wb, "BPPROBE", wp, ctx->stream());
     kernels::buildProbe(args, items, nItems, capacity, ctx->stream());
+    tl.end("BPKERNEL", ctx->stream());
+    tl.end("BPTASKTIME", ctx->stream());
     readBackCounters();
     return;
   }
@@ -118,11 +142,14 @@ void BuildProbe::execute() {
   kernels::BPArgs countArgs = args;
   countArgs.materialize = false;
   countArgs.itemCounts = itemCounts;
+  tl.beginSplit("BPKERNEL", "BPBUILD", wb, "BPPROBE", wp, ctx->stream());
   kernels::buildProbe(countArgs, items, nItems, capacity, ctx->stream());  // -> counters[0] = matches
   kernels::scanExclusiveU32to64(itemCounts, itemOffsets, capacity, args.outCursor, scanWs64, ctx->stream());
   args.itemOffsets = itemOffsets;
   args.result = counters + 3;  // the count pass already counted
   kernels::buildProbe(args, items, nItems, capacity, ctx->stream());
+  tl.end("BPKERNEL", ctx->stream());
+  tl.end("BPTASKTIME", ctx->stream());
   readBackCounters();
 }
 

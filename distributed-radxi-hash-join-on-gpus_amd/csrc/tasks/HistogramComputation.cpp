@@ -3,6 +3,8 @@
 #include "../comm/Communicator.h"
 #include "../memory/Arena.h"
 #include "../performance/Clock.h"
+#include "../performance/Measurements.h"
+#include "../performance/Timeline.h"
 #include "../utils/Debug.h"
 #include "../utils/Fault.h"
 #include "../utils/Hip.h"
@@ -35,8 +37,13 @@ HistogramComputation::~HistogramComputation() = default;  // events belong to th
 
 void HistogramComputation::executeInner(uint32_t sampleStride) {
   uint64_t t0 = performance::nowUs();
+  performance::Timeline &tl = ctx->timeline();
+  tl.begin("HILOCAL", ctx->stream());
   innerRelationLocalHistogram->computeLocalHistogram();
+  tl.end("HILOCAL", ctx->stream());
+  tl.begin("HOLOCAL", ctx->stream());
   outerRelationLocalHistogram->computeSampledEstimate(sampleStride);
+  tl.end("HOLOCAL", ctx->stream());
   ctx->synchronize();
   outerRelationLocalHistogram->scaleEstimate();
   localUs = performance::nowUs() - t0;
@@ -55,21 +62,29 @@ void HistogramComputation::launchOuter(hipStream_t exchangeStream) {
   histograms::LocalHistogram *h = outerRelationLocalHistogram.get();
   const size_t per = (size_t)h->getChunkCount() * h->getPartitionCount();
   if (!ctx->onDevice()) {  // host path: the same sequence, completed in place
+    ctx->timeline().begin("HOLOCAL");
     h->computeLocalHistogram();
+    ctx->timeline().end("HOLOCAL");
     outerGatherHostVec.resize(per * numberOfNodes);
+    ctx->timeline().begin("HOGLOBAL");
     ctx->comm()->allGatherHost(h->getChunkHistograms(), outerGatherHostVec.data(), per);
+    ctx->timeline().end("HOGLOBAL");
     outerGatherHost = outerGatherHostVec.data();
     outerLaunched = true;
     return;
   }
   if (!outerHistDone) outerHistDone = ctx->acquireEvent();
   if (!outerGatherDone) outerGatherDone = ctx->acquireEvent();
+  ctx->timeline().begin("HOLOCAL", ctx->stream());
   h->computeLocalHistogramDevice();
+  ctx->timeline().end("HOLOCAL", ctx->stream());
   HIP_CHECK(hipEventRecord(outerHistDone, ctx->stream()));
   uint64_t *gatherDev = ctx->workspace().getArray<uint64_t>(per * numberOfNodes);
   outerGatherHost = ctx->staging().getArray<uint64_t>(per * numberOfNodes);
   HIP_CHECK(hipStreamWaitEvent(exchangeStream, outerHistDone, 0));
+  ctx->timeline().begin("HOGLOBAL", exchangeStream);
   ctx->comm()->allGatherDevice(h->chunkTotalsDevice(), gatherDev, per, exchangeStream);
+  ctx->timeline().end("HOGLOBAL", exchangeStream);
   HIP_CHECK(hipMemcpyAsync(outerGatherHost, gatherDev, per * numberOfNodes * 8, hipMemcpyDeviceToHost,
                            exchangeStream));
   HIP_CHECK(hipEventRecord(outerGatherDone, exchangeStream));
@@ -94,8 +109,13 @@ void HistogramComputation::execute() {
 
 void HistogramComputation::computeLocalHistograms() {
   const uint64_t t0 = performance::nowUs();
+  performance::Timeline &tl = ctx->timeline();
+  tl.begin("HILOCAL", ctx->stream());
   innerRelationLocalHistogram->computeLocalHistogram();
+  tl.end("HILOCAL", ctx->stream());
+  tl.begin("HOLOCAL", ctx->stream());
   outerRelationLocalHistogram->computeLocalHistogram();
+  tl.end("HOLOCAL", ctx->stream());
   ctx->synchronize();  // the host needs the totals for the collective
   localUs = performance::nowUs() - t0;
 }

@@ -2,6 +2,9 @@
 
 #include "../host/HostOps.h"
 #include "../memory/Arena.h"
+#include "../performance/Clock.h"
+#include "../performance/Measurements.h"
+#include "../performance/Timeline.h"
 #include "../utils/Hip.h"
 
 namespace hpcjoin {
@@ -30,6 +33,23 @@ bool LocalPartitioning::overflowed() const {
 
 void LocalPartitioning::partition(data::Window *w, int which) {
   w->stop();  // compute stream now waits for this window's exchanges
+  performance::Timeline &tl = ctx->timeline();
+  tl.begin("LPTASKTIME", ctx->stream());
+  partitionImpl(w, which);
+  tl.end("LPTASKTIME", ctx->stream());
+}
+
+// Bytes and host time of this pass's workspace carve-outs (LPMEMSIZE / LPMEMALLOC).
+void *LocalPartitioning::alloc(uint64_t bytes) {
+  const uint64_t t0 = performance::nowUs();
+  void *p = ctx->workspace().get(bytes);
+  performance::Measurements::add("LPMEMALLOC", (double)(performance::nowUs() - t0), "us");
+  performance::Measurements::add("LPMEMSIZE", (double)bytes, "bytes");
+  return p;
+}
+
+void LocalPartitioning::partitionImpl(data::Window *w, int which) {
+  performance::Timeline &tl = ctx->timeline();
   const histograms::ExchangePlan &xp = w->getPlan();
   const uint32_t owned = (uint32_t)xp.owned.size();
   const bool wide = w->isWide();
@@ -86,8 +106,8 @@ void LocalPartitioning::partition(data::Window *w, int which) {
     const uint64_t P = (uint64_t)owned * F;
     const uint32_t S = plan.localSampleStride;
     const uint64_t cap = kernels::localSampledCapacityBound(xp.recvTotal, P, S, align);
-    void *sout = ctx->workspace().get(std::max<uint64_t>(cap, 1) * ob);
-    if (split.on) split.hi = ctx->workspace().getArray<uint16_t>(std::max<uint64_t>(cap, 1));
+    void *sout = alloc(std::max<uint64_t>(cap, 1) * ob);
+    if (split.on) split.hi = static_cast<uint16_t *>(alloc(std::max<uint64_t>(cap, 1) * 2));
     uint32_t *caps = ctx->workspace().getArray<uint32_t>(std::max<uint64_t>(P, 1));
     auto *starts = ctx->workspace().getArray<unsigned long long>(std::max<uint64_t>(P, 1));
     void *scanWs = ctx->workspace().get(kernels::scanWorkspaceBytes(std::max<uint64_t>(P, 1)));
@@ -102,11 +122,18 @@ void LocalPartitioning::partition(data::Window *w, int which) {
       overflowFlag = ctx->workspace().getArray<unsigned int>(1);
       HIP_CHECK(hipMemsetAsync(overflowFlag, 0, sizeof(unsigned int), ctx->stream()));
     }
+    performance::Measurements::add("LPHISTELEM", (double)(xp.recvTotal / S), "tuples");
+    tl.begin("LPHISTCOMP", ctx->stream());
     kernels::localHistogram(w->getData(), wide, dItems, nItems, shift, bits, itemHist, ctx->stream(), S);
+    tl.end("LPHISTCOMP", ctx->stream());
+    tl.begin("LPOFFSET", ctx->stream());
     kernels::localSampledLayout(itemHist, dLb, dItems, owned, bits, S, caps, starts, scanWs, gcur, gend, pbeg, cap,
                                 ctx->stream(), align);
+    tl.end("LPOFFSET", ctx->stream());
+    tl.begin("LPPART", ctx->stream());
     kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, gcur, false, sout, ctx->stream(), gend,
                           split, plan.localGeometry);
+    tl.end("LPPART", ctx->stream());
     kernels::claimOverflow(gcur, gend, P, overflowFlag, ctx->stream());
     // Read back with the join's final synchronisation (the flag accumulates
     // over sides; the last copy enqueued sees them all).
@@ -116,8 +143,8 @@ void LocalPartitioning::partition(data::Window *w, int which) {
     w->setPartitioned(sout, pbeg, bits, reinterpret_cast<const uint64_t *>(gcur), split.hi);
     return;
   }
-  void *out = ctx->workspace().get(std::max<uint64_t>(xp.recvTotal, 1) * ob);
-  if (split.on) split.hi = ctx->workspace().getArray<uint16_t>(std::max<uint64_t>(xp.recvTotal, 1));
+  void *out = alloc(std::max<uint64_t>(xp.recvTotal, 1) * ob);
+  if (split.on) split.hi = static_cast<uint16_t *>(alloc(std::max<uint64_t>(xp.recvTotal, 1) * 2));
   uint64_t *partBegin = ctx->workspace().getArray<uint64_t>((uint64_t)owned * F + 1);
   if (ctx->onDevice()) {
     const uint32_t streams = kernels::assignLocalStreams(it.data(), nItems);
@@ -133,16 +160,30 @@ void LocalPartitioning::partition(data::Window *w, int which) {
       zero.assign(1, 0);
       ctx->copy(partBegin, zero.data(), 8, true, false);
     }
+    performance::Measurements::add("LPHISTELEM", (double)xp.recvTotal, "tuples");
+    tl.begin("LPHISTCOMP", ctx->stream());
     kernels::localHistogram(w->getData(), wide, dItems, nItems, shift, bits, itemHist, ctx->stream());
+    tl.end("LPHISTCOMP", ctx->stream());
+    tl.begin("LPOFFSET", ctx->stream());
     kernels::localCursors(itemHist, dLb, owned, bits, dBase, dItems, gcur, narrow, partBegin, ctx->stream());
+    tl.end("LPOFFSET", ctx->stream());
+    tl.begin("LPPART", ctx->stream());
     kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, gcur, narrow, out, ctx->stream(), nullptr,
                           split);
+    tl.end("LPPART", ctx->stream());
   } else {
     uint64_t *itemCursors = ctx->workspace().getArray<uint64_t>(std::max<uint64_t>(1, (uint64_t)nItems * F));
     if (owned == 0) partBegin[0] = 0;
+    performance::Measurements::add("LPHISTELEM", (double)xp.recvTotal, "tuples");
+    tl.begin("LPHISTCOMP");
     host::localHistogram(w->getData(), wide, it.data(), nItems, shift, bits, itemHist);
+    tl.end("LPHISTCOMP");
+    tl.begin("LPOFFSET");
     host::localCursors(itemHist, lb.data(), owned, bits, xp.lpBase.data(), itemCursors, partBegin);
+    tl.end("LPOFFSET");
+    tl.begin("LPPART");
     host::localScatter(w->getData(), wide, it.data(), nItems, shift, bits, itemCursors, out);
+    tl.end("LPPART");
   }
   w->setPartitioned(out, partBegin, bits, nullptr, split.hi);
 }

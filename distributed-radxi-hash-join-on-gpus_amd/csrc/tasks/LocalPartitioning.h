@@ -53,6 +53,8 @@ class LocalPartitioning : public Task {
 
  protected:
   void partition(data::Window *window, int which);
+  void partitionImpl(data::Window *window, int which);
+  void *alloc(uint64_t bytes);
 
  private:
   data::Window *windows[2];

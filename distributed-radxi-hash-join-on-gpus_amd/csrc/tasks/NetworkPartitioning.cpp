@@ -2,6 +2,9 @@
 
 #include "../host/HostOps.h"
 #include "../memory/Arena.h"
+#include "../performance/Clock.h"
+#include "../performance/Measurements.h"
+#include "../performance/Timeline.h"
 #include "../utils/Hip.h"
 
 namespace hpcjoin {
@@ -42,9 +45,16 @@ void NetworkPartitioning::partition(data::Relation *relation, data::Window *wind
   const uint32_t bpc = local->blocksPerChunk(), chunks = local->getChunkCount();
   const bool single = xp.numberOfNodes == 1;
   const uint32_t tb = window->tupleBytes();
+  const bool isInner = relation == innerRelation;
+  const char *kMain = isInner ? "MIMAINPART" : "MOMAINPART";
+  const char *kFlush = isInner ? "MIFLUSHPART" : "MOFLUSHPART";
+  const uint64_t tAlloc = performance::nowUs();
   void *send = single ? window->getData() : ctx->workspace().get(n * tb);
+  performance::Measurements::add(isInner ? "MIMEMALLOC" : "MOMEMALLOC", (double)(performance::nowUs() - tAlloc), "us");
   window->start();
   const kernels::KeyMix mix{plan.keyMix ? 1u : 0u, plan.keyBits};
+  performance::Timeline &tl = ctx->timeline();
+  tl.begin(kMain, ctx->stream());
   if (ctx->onDevice()) {
     // Claim-mode scatter: per-(chunk, XCD group, digit) slices, one device
     // atomic per digit per 8192-tuple tile (kernels.h, CLAIM_GROUPS).
@@ -77,6 +87,11 @@ void NetworkPartitioning::partition(data::Relation *relation, data::Window *wind
       if (afterChunk) afterChunk(c);
     }
   }
+  // The reference's MxFLUSHPART is its tail flush + flush_local_all: here the
+  // time from the last scatter to the last exchange chunk having landed.
+  tl.end(kMain, ctx->stream());
+  tl.begin(kFlush, ctx->stream());
+  tl.end(kFlush, window->completionStream());
 }
 
 }  // namespace tasks

@@ -5,6 +5,7 @@
 #include <cstring>
 
 #include "../memory/Arena.h"
+#include "../performance/Timeline.h"
 #include "../utils/Hip.h"
 
 namespace hpcjoin {
@@ -27,6 +28,8 @@ void SampledNetworkPartitioning::sample() {
   const uint32_t F = 1u << plan.networkBits;
   const kernels::KeyMix mix{plan.keyMix ? 1u : 0u, plan.keyBits};
   for (Side &s : sides) {
+    const char *key = &s == &sides[0] ? "HILOCAL" : "HOLOCAL";
+    ctx->timeline().begin(key, ctx->stream());
     const uint64_t n = s.relation->getLocalSize();
     s.geom = kernels::partitionGeometry(n, maxBlocks);
     uint32_t *blockHist = ctx->workspace().getArray<uint32_t>((uint64_t)F * s.geom.blocks);
@@ -34,6 +37,7 @@ void SampledNetworkPartitioning::sample() {
     kernels::netHistogram(s.relation->getData(), n, plan.networkBits, s.geom, blockHist, ctx->stream(), mix,
                           sampleStride);
     kernels::netGroupTotals(blockHist, F, s.geom.blocks, s.groupTotalsDev, ctx->stream());
+    ctx->timeline().end(key, ctx->stream());
     s.sampled = ctx->staging().getArray<uint64_t>((uint64_t)CLAIM_GROUPS * F);
     HIP_CHECK(hipMemcpyAsync(s.sampled, s.groupTotalsDev, (size_t)CLAIM_GROUPS * F * 8, hipMemcpyDeviceToHost,
                              ctx->stream()));
@@ -140,12 +144,15 @@ void SampledNetworkPartitioning::scatterSide(int k) {
   const uint64_t n = s.relation->getLocalSize();
   s.window->start();
   const int nm = s.narrow ? 1 : 0;
+  const char *key = k == 0 ? "MIMAINPART" : "MOMAINPART";
+  ctx->timeline().begin(key, ctx->stream());
   if (plan.wide)
     kernels::netScatterWide(s.relation->getData(), n, plan.networkBits, s.geom, 0, s.geom.blocks, s.gcur,
                             static_cast<data::Tuple *>(s.window->getData()), ctx->stream(), mix, s.gend, nm);
   else
     kernels::netScatter(s.relation->getData(), n, plan.networkBits, plan.keyShift, s.geom, 0, s.geom.blocks, s.gcur,
                         static_cast<uint64_t *>(s.window->getData()), ctx->stream(), plan.keyBits, mix, s.gend, nm, !plan.keyOnly);
+  ctx->timeline().end(key, ctx->stream());
   const size_t bytes = (size_t)G * F * (s.narrow ? 4 : 8);
   s.cursorsBack = ctx->staging().get(bytes);
   HIP_CHECK(hipMemcpyAsync(s.cursorsBack, s.gcur, bytes, hipMemcpyDeviceToHost, ctx->stream()));

@@ -242,3 +242,52 @@ def test_generated_relations_skip_planning_scans(C):
     S2 = C.Relation.from_tensor(S.to_tensor(), G)
     p2 = C.HashJoin(R2, S2, ctx, C.JoinConfig()).plan
     assert repr(p1) == repr(p2)
+
+
+@pytest.mark.parametrize("dev", devices())
+@pytest.mark.parametrize("mode", ["shuffle", "replicated", "shuffle-chunks3"])
+def test_measurement_keys_two_ranks(C, dev, mode):
+    """Every .perf key of the reference (performance/Measurements.cpp:136-542)
+    is present and non-negative after a 2-rank join, on both N > 1 plans; the
+    phases that ran are timed (> 0)."""
+    loc = "device" if dev == "cuda" else "host"
+    G = 400_009
+    group = C.InProcessGroup(2)
+    snaps, errs = [None, None], []
+
+    def work(r):
+        try:
+            ctx = C.ExecContext(loc, 0 if loc == "device" else -1, group.communicator(r))
+            R = C.Relation(C.Relation.local_size_for(G, r, 2), G, loc, 0)
+            S = C.Relation(C.Relation.local_size_for(G, r, 2), G, loc, 0)
+            R.generate(C.GenSpec(seed=1), C.Relation.local_offset_for(G, r, 2))
+            S.generate(C.GenSpec(seed=2), C.Relation.local_offset_for(G, r, 2))
+            cfg = C.JoinConfig()
+            if mode == "replicated":
+                cfg.replicate_bitmap = C.PlanChoice.ON
+            else:
+                cfg.bitmap_join = False
+                cfg.chunks = 3 if mode.endswith("3") else 1
+            res = C.HashJoin(R, S, ctx, cfg).run()
+            assert res["global_matches"] == G
+            snaps[r] = C.measurements.snapshot()
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(2)]
+    [t.start() for t in ts]
+    [t.join(timeout=300) for t in ts]
+    assert not errs, errs
+    keys = C.measurements.reference_keys()
+    assert len(keys) == 46
+    for snap in snaps:
+        for k in keys:
+            assert k in snap and snap[k] >= 0, k
+        assert snap["JTOTAL"] > 0 and snap["CTOTAL"] > 0
+        assert snap["MIMAINPART"] > 0 and snap["MOMAINPART"] > 0 and snap["BPTASKTIME"] > 0
+        assert snap["MWINPUTCNT"] >= 1 and snap["MWINPUT"] > 0
+        assert snap["BPBUILD"] > 0 and snap["BPPROBE"] > 0
+        if mode != "replicated":
+            assert snap["HILOCAL"] > 0 and snap["HOLOCAL"] > 0 and snap["HOGLOBAL"] > 0
+            assert snap["LPPART"] > 0 and snap["LPHISTCOMP"] > 0 and snap["LPMEMSIZE"] > 0
+            assert snap["MWINPUTCNT"] == 2 * (3 if mode.endswith("3") else 1)
