@@ -174,8 +174,9 @@ def main():
     ap.add_argument("--chunks", type=int, default=0, help="exchange pipeline slices (0 = auto)")
     ap.add_argument("--input", default="device", choices=["device", "pinned"],
                     help="where the relations live: HBM, or pinned host memory read in place over the host link")
-    ap.add_argument("--general", default="on", choices=["on", "off"],
-                    help="also time the general path: the same join on sparse random 63-bit keys")
+    ap.add_argument("--general", default="on", choices=["on", "off", "only"],
+                    help="also time the general path: the same join on sparse random 63-bit keys "
+                         "(only: just that, for sweeps)")
     ap.add_argument("--json-out", default="")
     args = ap.parse_args()
 
@@ -206,7 +207,8 @@ def main():
         inner.sparse64 = outer.sparse64 = sparse
         return inner, outer
 
-    head = measure(C, info, ctx, comm, on_gpu, G_R, G_S, *specs(False), cfg, rel_loc, args.steps, args.warmup)
+    head = measure(C, info, ctx, comm, on_gpu, G_R, G_S, *specs(args.general == "only"), cfg, rel_loc, args.steps,
+                   args.warmup)
     join, results = head.pop("join"), head.pop("results")
     plan = join.plan
     engine = {"reruns": results[-1]["reruns"], "build_probe_items": results[-1]["build_probe_items"],

@@ -425,6 +425,20 @@ static size_t bpMatSplitLds(const BPArgs &a) { return (size_t(8) << ceilLog2(2ul
 template <int MODE, bool ITEMS>
 constexpr int bpMinBlocks() { return MODE == 0 ? (ITEMS ? 3 : 4) : 2; }
 
+// Counting modes with a hash table (CCOUNT without direct addressing, KCOUNT,
+// WCOUNT): the table key and its hash for a register-held element.
+template <int MODE, typename L>
+__device__ __forceinline__ auto bpKey(const L &v) {
+  if constexpr (MODE == BP_CCOUNT) return (uint32_t)v;
+  else if constexpr (MODE == BP_KCOUNT) return (unsigned long long)v;
+  else return (unsigned long long)v.x;  // BP_WCOUNT: ulonglong2 {key, rid}
+}
+template <int MODE, typename K>
+__device__ __forceinline__ uint32_t bpHash(K key, uint32_t tbits) {
+  if constexpr (MODE == BP_CCOUNT) return hash32((uint32_t)key, tbits);
+  else return hash64((uint64_t)key, tbits);
+}
+
 template <int MODE, bool ITEMS = false, bool SPLIT = false, bool DIRECT = false>
 __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeKernel(BPArgs a, const BPItem *__restrict__ items,
                                                         const uint32_t *__restrict__ nItemsPtr, uint32_t capacity) {
@@ -478,9 +492,36 @@ __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeK
     for (uint32_t i = t; i < slots; i += BPT) table[i] = DIRECT ? (Entry)0 : (Entry)(MODE == BP_CCOUNT ? EMPTY32 : EMPTY64);
     __syncthreads();
 
+    // Counting hash tables: the BP_K elements of a lane walk their probe
+    // sequences together -- each round issues one LDS access per pending
+    // element back to back, so a round costs one LDS latency instead of BP_K
+    // (a lane otherwise waits out every element's chain one after another).
+    constexpr bool INTERLEAVED = !MAT && !DIRECT;
     // ---- build
     for (uint32_t b0 = 0; b0 < nr; b0 += BATCH) {
       if (b0) bpLoadSide<MODE, SPLIT, L, false>(a.R, a.Rhi, rb, nr, b0, a, rv);
+      if constexpr (INTERLEAVED) {
+        using K = decltype(bpKey<MODE, L>(rv[0]));
+        const K empty = (K)(MODE == BP_CCOUNT ? EMPTY32 : EMPTY64);
+        uint32_t hh[BP_K], pend = 0;
+#pragma unroll
+        for (int k = 0; k < BP_K; ++k) {
+          hh[k] = bpHash<MODE>(bpKey<MODE, L>(rv[k]), tbits);
+          if (b0 + k * BPT + t < nr) pend |= 1u << k;
+        }
+        while (pend) {
+#pragma unroll
+          for (int k = 0; k < BP_K; ++k)
+            if (pend & (1u << k)) {
+              const K key = bpKey<MODE, L>(rv[k]);
+              if (atomicCAS(reinterpret_cast<K *>(&table[hh[k]]), empty, key) == empty)
+                pend &= ~(1u << k);
+              else
+                hh[k] = (hh[k] + 1) & mask;
+            }
+        }
+        continue;
+      }
 #pragma unroll
       for (int k = 0; k < BP_K; ++k) {
         const uint32_t idx = b0 + k * BPT + t;
@@ -516,6 +557,31 @@ __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeK
       if (b0) {
         if (b0 + BATCH <= ns) bpLoadSide<MODE, SPLIT, L, true>(a.S, a.Shi, sb, ns, b0, a, sv);
         else bpLoadSide<MODE, SPLIT, L, false>(a.S, a.Shi, sb, ns, b0, a, sv);
+      }
+      if constexpr (INTERLEAVED) {
+        using K = decltype(bpKey<MODE, L>(sv[0]));
+        const K empty = (K)(MODE == BP_CCOUNT ? EMPTY32 : EMPTY64);
+        uint32_t hh[BP_K], live = 0, found = 0;
+#pragma unroll
+        for (int k = 0; k < BP_K; ++k) {
+          hh[k] = bpHash<MODE>(bpKey<MODE, L>(sv[k]), tbits);
+          if (b0 + k * BPT + t < ns) live |= 1u << k;
+        }
+        while (live) {
+#pragma unroll
+          for (int k = 0; k < BP_K; ++k)
+            if (live & (1u << k)) {
+              const K e = reinterpret_cast<const K *>(table)[hh[k]];
+              if (e == empty) {
+                live &= ~(1u << k);
+              } else {
+                found += (e == bpKey<MODE, L>(sv[k]));
+                hh[k] = (hh[k] + 1) & mask;
+              }
+            }
+        }
+        matches += found;
+        continue;
       }
 #pragma unroll
       for (int k = 0; k < BP_K; ++k) {
