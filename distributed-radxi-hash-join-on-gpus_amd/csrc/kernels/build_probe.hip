@@ -510,11 +510,20 @@ __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeK
           if (b0 + k * BPT + t < nr) pend |= 1u << k;
         }
         while (pend) {
+          // Every CAS of the round is issued before any result is used, and
+          // without branches: an element that is not pending (already placed,
+          // or a lane past the batch end) swaps its key for itself, which
+          // never changes the table.
+          K old[BP_K];
+#pragma unroll
+          for (int k = 0; k < BP_K; ++k) {
+            const K key = bpKey<MODE, L>(rv[k]);
+            old[k] = atomicCAS(reinterpret_cast<K *>(&table[hh[k]]), (pend & (1u << k)) ? empty : key, key);
+          }
 #pragma unroll
           for (int k = 0; k < BP_K; ++k)
             if (pend & (1u << k)) {
-              const K key = bpKey<MODE, L>(rv[k]);
-              if (atomicCAS(reinterpret_cast<K *>(&table[hh[k]]), empty, key) == empty)
+              if (old[k] == empty)
                 pend &= ~(1u << k);
               else
                 hh[k] = (hh[k] + 1) & mask;
@@ -568,14 +577,16 @@ __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeK
           if (b0 + k * BPT + t < ns) live |= 1u << k;
         }
         while (live) {
+          K e[BP_K];  // every pending read of the round is issued before any is compared
+#pragma unroll
+          for (int k = 0; k < BP_K; ++k) e[k] = reinterpret_cast<const K *>(table)[hh[k]];
 #pragma unroll
           for (int k = 0; k < BP_K; ++k)
             if (live & (1u << k)) {
-              const K e = reinterpret_cast<const K *>(table)[hh[k]];
-              if (e == empty) {
+              if (e[k] == empty) {
                 live &= ~(1u << k);
               } else {
-                found += (e == bpKey<MODE, L>(sv[k]));
+                found += (e[k] == bpKey<MODE, L>(sv[k]));
                 hh[k] = (hh[k] + 1) & mask;
               }
             }
