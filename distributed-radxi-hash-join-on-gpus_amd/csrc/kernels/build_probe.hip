@@ -496,7 +496,16 @@ __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeK
     // sequences together -- each round issues one LDS access per pending
     // element back to back, so a round costs one LDS latency instead of BP_K
     // (a lane otherwise waits out every element's chain one after another).
+    // Measured on MI355X (sparse 63-bit keys, 1B x 1B, KCOUNT): 23 ms with
+    // interleaved rounds vs 14 ms walking the elements one after another --
+    // a round re-issues the LDS access of every element until the longest
+    // chain of the wave ends, and 64-bit LDS CAS throughput is what binds.
+    // Kept for experiments: compile with -DHPCJOIN_BP_INTERLEAVE.
+#ifdef HPCJOIN_BP_INTERLEAVE
     constexpr bool INTERLEAVED = !MAT && !DIRECT;
+#else
+    constexpr bool INTERLEAVED = false;
+#endif
     // ---- build
     for (uint32_t b0 = 0; b0 < nr; b0 += BATCH) {
       if (b0) bpLoadSide<MODE, SPLIT, L, false>(a.R, a.Rhi, rb, nr, b0, a, rv);
