@@ -591,6 +591,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .value("AUTO", core::PlanChoice::Auto)
       .value("OFF", core::PlanChoice::Off)
       .value("ON", core::PlanChoice::On);
+  py::enum_<core::ExchangeMode>(m, "ExchangeMode")
+      .value("RCCL", core::ExchangeMode::Rccl)
+      .value("ONE_SIDED", core::ExchangeMode::OneSided);
   py::class_<core::JoinConfig>(m, "JoinConfig")
       .def(py::init<>())
       .def_readwrite("network_bits", &core::JoinConfig::networkBits)
@@ -609,6 +612,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("direct_count", &core::JoinConfig::directCount)
       .def_readwrite("bitmap_join", &core::JoinConfig::bitmapJoin)
       .def_readwrite("replicate_bitmap", &core::JoinConfig::replicateBitmap)
+      .def_readwrite("exchange", &core::JoinConfig::exchange)
       .def_readwrite("split_histogram", &core::JoinConfig::splitHistogram)
       .def_readwrite("pipeline_outer", &core::JoinConfig::pipelineOuter)
       .def_readwrite("local_item_tiles", &core::JoinConfig::localItemTiles)
@@ -632,6 +636,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("bitmap_bits", &core::JoinPlan::bitmapBits)
       .def_readonly("bitmap_replicated", &core::JoinPlan::bitmapReplicated)
       .def_readonly("key_only", &core::JoinPlan::keyOnly)
+      .def_readonly("one_sided", &core::JoinPlan::oneSided)
       .def_readonly("replicated_link_bytes", &core::JoinPlan::replicatedLinkBytes)
       .def_readonly("shuffle_link_bytes", &core::JoinPlan::shuffleLinkBytes)
       .def_readonly("link_gbps", &core::JoinPlan::linkGBps)

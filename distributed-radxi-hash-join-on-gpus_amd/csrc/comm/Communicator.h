@@ -29,6 +29,9 @@ class Communicator {
   // Where allToAllV buffers must live (Device for RCCL, Host for gloo).
   virtual bool supports(Location loc) const = 0;
   virtual std::string name() const = 0;
+  // True when every rank runs in this process (threads): one-sided windows
+  // are then plain pointers instead of IPC-mapped allocations.
+  virtual bool sharesAddressSpace() const { return size() == 1; }
   // Failure detection: throw if the communicator has seen an asynchronous
   // error (RCCL) or a peer aborted (in-process).  Polled by blocking waits.
   virtual void checkHealth() {}

@@ -50,6 +50,7 @@ class InProcessCommunicator : public Communicator {
   uint32_t size() const override { return group_->size(); }
   bool supports(Location) const override { return true; }
   std::string name() const override { return "in_process"; }
+  bool sharesAddressSpace() const override { return true; }
   void allGatherHost(const uint64_t *send, uint64_t *recv, size_t count) override;
   void allReduceSumHost(uint64_t *data, size_t count) override;
   void barrier() override { group_->barrier(); }

@@ -31,6 +31,7 @@ ExecContext::ExecContext(Location loc, int device, comm::Communicator *comm)
 }
 
 ExecContext::~ExecContext() {
+  for (auto &m : ipcImported_) (void)hipIpcCloseMemHandle(m.second);
   for (hipEvent_t e : events_) (void)hipEventDestroy(e);
   timeline_.reset();
   workspace_.reset();
@@ -81,6 +82,29 @@ void ExecContext::resetScratch() {
   workspace_->reset();
   staging_->reset();
   eventsUsed_ = 0;
+}
+
+void ExecContext::ipcExport(const void *p, uint64_t handle[8], uint64_t *offset) {
+  static_assert(sizeof(hipIpcMemHandle_t) == 64, "unexpected hipIpcMemHandle_t size");
+  JOIN_ASSERT(onDevice(), "ExecContext", "IPC export of host memory");
+  void *base = workspace_->allocationOf(p);
+  JOIN_ASSERT(base != nullptr, "ExecContext", "IPC export: %p is not in the workspace", p);
+  hipIpcMemHandle_t h;
+  HIP_CHECK(hipIpcGetMemHandle(&h, base));
+  std::memcpy(handle, &h, sizeof(h));
+  *offset = (uint64_t)(static_cast<const uint8_t *>(p) - static_cast<const uint8_t *>(base));
+}
+
+void *ExecContext::ipcImport(const uint64_t handle[8]) {
+  std::vector<uint64_t> key(handle, handle + 8);
+  for (auto &m : ipcImported_)
+    if (m.first == key) return m.second;
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof(h));
+  void *ptr = nullptr;
+  HIP_CHECK(hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess));
+  ipcImported_.emplace_back(std::move(key), ptr);
+  return ptr;
 }
 
 hipEvent_t ExecContext::acquireEvent() {

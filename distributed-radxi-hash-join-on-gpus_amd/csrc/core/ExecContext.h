@@ -52,6 +52,11 @@ class ExecContext {
   // until the next resetScratch(): joins reuse the same events instead of
   // creating and destroying several per join.
   hipEvent_t acquireEvent();
+  // One-sided exchange (JoinConfig::exchange = OneSided): the IPC handle of
+  // the device allocation holding `p` (8 words) and p's offset in it; and the
+  // mapping of a peer's exported allocation (opened once, cached).
+  void ipcExport(const void *p, uint64_t handle[8], uint64_t *offset);
+  void *ipcImport(const uint64_t handle[8]);
 
  private:
   Location loc_;
@@ -65,6 +70,7 @@ class ExecContext {
   std::unique_ptr<memory::Arena> workspace_;
   std::unique_ptr<memory::Arena> staging_;
   std::unique_ptr<performance::Timeline> timeline_;
+  std::vector<std::pair<std::vector<uint64_t>, void *>> ipcImported_;  // peer handle -> mapped base
 };
 
 }  // namespace core

@@ -59,6 +59,13 @@ enum class PlanChoice : int {
   On = 2,
 };
 
+// How NetworkPartitioning moves tuples to their owners (N > 1).
+enum class ExchangeMode : int {
+  Rccl = 0,      // two-sided: grouped ncclSend/ncclRecv all-to-allv per chunk (default)
+  OneSided = 1,  // the MPI_Put analog: each rank copies its runs straight into the owner's window
+                 // (IPC-mapped peer allocations; plain pointers for in-process ranks), then a barrier
+};
+
 struct JoinConfig {
   uint32_t networkBits = 0;   // radix bits of the network pass (0 = auto)
   uint32_t localBits = 0;     // radix bits of the local pass (0 = auto; ignored if !twoLevel)
@@ -94,6 +101,7 @@ struct JoinConfig {
   // (2 (N-1)/N * 2^keyBits / 8) undercut the shuffle's; On: whenever the key
   // range fits (host path and N == 1 included); Off: never.
   PlanChoice replicateBitmap = PlanChoice::Auto;
+  ExchangeMode exchange = ExchangeMode::Rccl;
   uint32_t localItemTiles = 64; // local pass work item: up to this many 4096-tuple tiles of one segment
   uint32_t localGeometry = 0;   // local scatter workgroup geometry (0 = 1024 x 8; 1-4: sweep alternatives)
 
@@ -126,6 +134,7 @@ struct JoinPlan {
   bool bitmapJoin = false;      // single-level bitmap join (kernels::bitmapJoin) after the sampled network pass
   uint32_t bitmapBits = 0;      // fragment bits per network partition (bitmap size 2^bitmapBits)
   bool bitmapReplicated = false;  // bitmaps all-reduced over ranks, outer probed in place (tasks/BitmapJoin)
+  bool oneSided = false;          // ExchangeMode::OneSided in effect (data::Window::enableOneSided)
   // Cost model of the N > 1 plan choice: bytes one rank puts on its links per
   // join for the replicated bitmaps and for the tuple shuffle, and the
   // predicted link time of each at linkGBps per rank (7 xGMI peers).

@@ -1,5 +1,7 @@
 #include "Window.h"
 
+#include <unistd.h>
+
 #include <algorithm>
 #include <cstring>
 
@@ -8,6 +10,7 @@
 #include "../memory/Arena.h"
 #include "../performance/Measurements.h"
 #include "../performance/Timeline.h"
+#include "../utils/Fault.h"
 #include "../utils/Hip.h"
 
 namespace hpcjoin {
@@ -153,8 +156,73 @@ void Window::exchangePacked(const uint64_t *send, uint32_t chunk) {
 
 void Window::start() { open = true; }
 
+void Window::enableOneSided() {
+  const uint32_t N = plan.numberOfNodes, me = plan.nodeId, C = plan.chunks;
+  JOIN_ASSERT(N > 1 && codec.w == 0, "Window", "one-sided windows: N > 1, raw tuples (no wire codec)");
+  const bool shared = ctx->comm()->sharesAddressSpace();
+  JOIN_ASSERT(shared || ctx->onDevice(), "Window", "one-sided host windows need in-process ranks");
+  // Per rank: {pid, raw pointer, IPC handle (8 words), offset, recvDispls[C][N]}.
+  const size_t R = 11 + (size_t)C * N;
+  std::vector<uint64_t> mine(R, 0), all(R * N);
+  mine[0] = (uint64_t)getpid();
+  mine[1] = (uint64_t)(uintptr_t)data;
+  if (!shared) ctx->ipcExport(data, &mine[2], &mine[10]);
+  for (size_t i = 0; i < (size_t)C * N; ++i) mine[11 + i] = plan.recvDispls[i];
+  ctx->comm()->allGatherHost(mine.data(), all.data(), R);
+  peerBase.assign(N, nullptr);
+  peerOffset.assign((size_t)N * C, 0);
+  for (uint32_t p = 0; p < N; ++p) {
+    const uint64_t *r = &all[R * p];
+    if (p == me)
+      peerBase[p] = static_cast<uint8_t *>(data);
+    else if (shared)
+      peerBase[p] = reinterpret_cast<uint8_t *>((uintptr_t)r[1]);
+    else
+      peerBase[p] = static_cast<uint8_t *>(ctx->ipcImport(&r[2])) + r[10];
+    for (uint32_t c = 0; c < C; ++c) peerOffset[(size_t)p * C + c] = r[11 + (size_t)c * N + me];
+  }
+  oneSided = true;
+  oneSidedComplete = false;
+}
+
+// This rank's runs of chunk c, each copied into its owner's window at the
+// owner's receive displacement for (c, this rank) -- MPI_Put at an exact,
+// disjoint offset.  Device: peer copies on the exchange stream once the
+// chunk's scatter is done.
+void Window::putChunk(const void *send, uint32_t chunk) {
+  const uint32_t N = plan.numberOfNodes, me = plan.nodeId, C = plan.chunks;
+  const uint64_t tb = tupleBytes();
+  const uint8_t *src = static_cast<const uint8_t *>(send);
+  const bool dev = ctx->onDevice();
+  if (dev) {
+    HIP_CHECK(hipEventRecord(ready[chunk], ctx->stream()));
+    HIP_CHECK(hipStreamWaitEvent(ctx->commStream(), ready[chunk], 0));
+  }
+  ctx->timeline().begin("MWINPUT", dev ? ctx->commStream() : nullptr);
+  for (uint32_t k = 0; k < N; ++k) {
+    const uint32_t p = (me + k) % N;  // staggered: every link busy, none oversubscribed
+    const uint64_t n = plan.sendCounts[(size_t)chunk * N + p];
+    if (!n) continue;
+    uint8_t *dst = peerBase[p] + peerOffset[(size_t)p * C + chunk] * tb;
+    const uint8_t *from = src + plan.sendDispls[(size_t)chunk * N + p] * tb;
+    if (dev)
+      HIP_CHECK(hipMemcpyAsync(dst, from, n * tb, hipMemcpyDeviceToDevice, ctx->commStream()));
+    else
+      std::memcpy(dst, from, n * tb);
+    if (p != me) wireSent += n * tb / 8;
+    performance::Measurements::add("MWINPUTCNT", 1, "calls");
+  }
+  ctx->timeline().end("MWINPUT", dev ? ctx->commStream() : nullptr);
+  if (dev) HIP_CHECK(hipEventRecord(done[chunk], ctx->commStream()));
+}
+
 void Window::exchange(const void *sendBuffer, uint32_t chunk) {
   JOIN_ASSERT(chunk < plan.chunks, "Window", "chunk %u out of range", chunk);
+  if (oneSided) {
+    putChunk(sendBuffer, chunk);
+    exchanged[chunk] = true;
+    return;
+  }
   performance::Measurements::add("MWINPUTCNT", 1, "calls");  // one all-to-allv per chunk (the MPI_Put analog)
   if (codec.w && plan.numberOfNodes > 1) {
     exchangePacked(static_cast<const uint64_t *>(sendBuffer), chunk);
@@ -193,6 +261,17 @@ void Window::exchange(const void *sendBuffer, uint32_t chunk) {
 void Window::stop() {
   if (ownedPlan) {  // chunk view
     if (viewArrived) HIP_CHECK(hipStreamWaitEvent(ctx->stream(), viewArrived, 0));
+    open = false;
+    return;
+  }
+  if (oneSided) {
+    if (!oneSidedComplete) {
+      // unlock_all + barrier: my puts have landed, then everyone's have.
+      if (ctx->onDevice()) utils::waitStream(ctx->commStream(), ctx->comm(), "one-sided puts");
+      ctx->comm()->barrier();
+      oneSidedComplete = true;
+      performance::Measurements::add("MWINWAITCNT", 1, "calls");
+    }
     open = false;
     return;
   }

@@ -50,6 +50,16 @@ class Window {
   void exchange(const void *sendBuffer, uint32_t chunk);
   // Stream on which this window's last exchange step completes.
   hipStream_t completionStream() const;
+  // One-sided exchange (the reference's MPI_Win_create + MPI_Put,
+  // data/Window.cpp:35-144): collective.  Every rank publishes where its
+  // window lives (an IPC handle of the allocation + offset, or a plain
+  // pointer for in-process ranks) and where each source's chunks land in
+  // it; exchange() then copies this rank's runs straight into the owners'
+  // windows, and stop() is the unlock_all + barrier: this rank's puts are
+  // complete, then every rank's (HashJoin.cpp:119-121).  No receive-side
+  // RCCL call, no staging through a second buffer on the receiver.
+  void enableOneSided();
+  bool isOneSided() const { return oneSided; }
   // Bit-pack tuples on the wire (kernels.h, WireCodec); ridBase[rank * C + c]
   // is the rid base of sender `rank`'s chunk c (C = ridBase.size() / ranks).
   // Call before the first exchange.
@@ -110,6 +120,12 @@ class Window {
   const uint64_t *partEnd = nullptr;
   uint32_t localBits = 0;
   uint16_t *partitionedHi = nullptr;
+  // One-sided state: peer p's window base (mapped), and the tuple offset of
+  // this rank's chunk-c run in it: peerOffset[p * chunks + c].
+  bool oneSided = false, oneSidedComplete = false;
+  std::vector<uint8_t *> peerBase;
+  std::vector<uint64_t> peerOffset;
+  void putChunk(const void *send, uint32_t chunk);
 };
 
 }  // namespace data

@@ -115,6 +115,16 @@ bool Arena::owns(const void *p) const {
   return base_ && q >= base_ && q < base_ + capacity_;
 }
 
+void *Arena::allocationOf(const void *p) const {
+  if (owns(p)) return base_;
+  const uint8_t *q = static_cast<const uint8_t *>(p);
+  for (const auto &f : fallbacks_) {
+    const uint8_t *b = static_cast<const uint8_t *>(f.first);
+    if (q >= b && q < b + f.second) return f.first;
+  }
+  return nullptr;
+}
+
 void Arena::freeFallback(void *p) {
   for (size_t i = 0; i < fallbacks_.size(); ++i)
     if (fallbacks_[i].first == p) {

@@ -43,6 +43,8 @@ class Arena {
   uint64_t peak() const { return peak_; }
   uint64_t fallbackBytes() const { return fallbackBytes_; }
   bool owns(const void *p) const;
+  // Start of the raw allocation (main block or fallback) holding p; null if none.
+  void *allocationOf(const void *p) const;
   void freeFallback(void *p);         // frees one fallback allocation (no-op for arena memory)
 
   static void *rawAlloc(Location loc, uint64_t bytes, int device);

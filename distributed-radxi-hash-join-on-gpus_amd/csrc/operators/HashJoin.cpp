@@ -139,6 +139,16 @@ void HashJoin::makeJoinPlan() {
   // logic, covered by the CPU tests).
   plan.splitHistogram = config.splitHistogram && numberOfNodes > 1;
   plan.pipelineOuter = config.pipelineOuter && numberOfNodes > 1 && !plan.materialize && plan.twoLevel;
+  // One-sided windows: device engines (IPC-mapped peers) or in-process ranks.
+  // Puts move raw tuples and complete at a barrier, so neither the wire codec
+  // nor per-chunk pipelining of the outer relation applies.
+  plan.oneSided = config.exchange == core::ExchangeMode::OneSided && numberOfNodes > 1 &&
+                  (ctx->onDevice() || ctx->comm()->sharesAddressSpace());
+  if (plan.oneSided) {
+    plan.wireBits[0] = plan.wireBits[1] = 0;
+    plan.wireRidBits[0] = plan.wireRidBits[1] = 0;
+    plan.pipelineOuter = false;
+  }
   basePlan = plan;  // the two-level plan: what a bitmap plan falls back to
   bitmapExact = !(ctx->onDevice() && sampleable);
   planBitmap();
@@ -434,6 +444,7 @@ JoinResult HashJoin::runImpl() {
       std::unique_ptr<data::Window> w(new data::Window(
           (r == 0 ? hc->innerOffsetMap() : hc->outerOffsetMap())->getExchangePlan(),
           r == 0 ? hc->innerGlobal() : hc->outerGlobal(), hc->assignmentMap(), ctx, plan.wide));
+      if (plan.oneSided) w->enableOneSided();
       if (plan.wireBits[r]) {
         kernels::WireCodec c;
         c.w = plan.wireBits[r];
@@ -482,6 +493,10 @@ JoinResult HashJoin::runImpl() {
                                       hc->assignmentMap(), ctx, plan.wide));
     innerWindow = innerOwned.get();
     outerWindow = outerOwned.get();
+    if (plan.oneSided) {
+      innerWindow->enableOneSided();
+      outerWindow->enableOneSided();
+    }
     for (int r = 0; r < 2; ++r)
       if (plan.wireBits[r]) {
         kernels::WireCodec c;

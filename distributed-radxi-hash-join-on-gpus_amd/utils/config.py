@@ -21,6 +21,8 @@ def config_to_dict(cfg) -> dict:
     d["network_histogram"] = str(cfg.network_histogram).split(".")[-1]
     d["local_histogram"] = str(cfg.local_histogram).split(".")[-1]
     d["wire_codec"] = str(cfg.wire_codec).split(".")[-1]
+    d["replicate_bitmap"] = str(cfg.replicate_bitmap).split(".")[-1]
+    d["exchange"] = str(cfg.exchange).split(".")[-1]
     return d
 
 
@@ -29,7 +31,8 @@ def config_from_dict(d: dict | None = None, env_prefix: str = "HPCJOIN_"):
     C = require_native()
     cfg = C.JoinConfig()
     merged = dict(d or {})
-    for f in _FIELDS + ["assignment", "format", "key_hashing", "network_histogram", "local_histogram", "wire_codec"]:
+    for f in _FIELDS + ["assignment", "format", "key_hashing", "network_histogram", "local_histogram", "wire_codec",
+                        "replicate_bitmap", "exchange"]:
         v = os.environ.get(env_prefix + f.upper())
         if v is not None:
             merged[f] = v
@@ -46,6 +49,10 @@ def config_from_dict(d: dict | None = None, env_prefix: str = "HPCJOIN_"):
             setattr(cfg, k, v if isinstance(v, bool) else str(v).lower() in ("1", "true", "yes"))
         elif k == "wire_codec":
             cfg.wire_codec = getattr(C.WireCodecMode, str(v).upper())
+        elif k == "replicate_bitmap":
+            cfg.replicate_bitmap = getattr(C.PlanChoice, str(v).upper())
+        elif k == "exchange":
+            cfg.exchange = getattr(C.ExchangeMode, str(v).upper())
         elif k in _FIELDS:
             setattr(cfg, k, int(v))
         else:

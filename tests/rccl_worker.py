@@ -33,6 +33,11 @@ def main():
         ("unique-shuffle", C.GenSpec(seed=99), G_R, {"bitmap_join": False}),
         ("zipf-shuffle-chunks3", C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=78, domain=G_R, zipf_theta=0.9),
          G_S, {"bitmap_join": False, "chunks": 3}),
+        # one-sided puts into IPC-mapped peer windows (processes on one GPU here)
+        ("one-sided", C.GenSpec(distribution=C.KeyDistribution.UNIFORM, seed=6, domain=G_R), G_S,
+         {"bitmap_join": False, "chunks": 2, "exchange": C.ExchangeMode.ONE_SIDED}),
+        ("one-sided-materialize", C.GenSpec(seed=99), G_R,
+         {"exchange": C.ExchangeMode.ONE_SIDED, "materialize": True}),
     ]
     R = C.Relation(C.Relation.local_size_for(G_R, info.rank, info.world), G_R, "device", info.local_rank)
     R.generate(inner, C.Relation.local_offset_for(G_R, info.rank, info.world))
@@ -48,6 +53,7 @@ def main():
         # (one ncclAllReduce) unless the shuffle is forced
         want_bitmap = not opts.get("materialize") and "format" not in opts and opts.get("bitmap_join", True)
         assert j.plan.bitmap_join == want_bitmap and j.plan.bitmap_replicated == want_bitmap, (name, j.plan)
+        assert j.plan.one_sided == ("exchange" in opts), (name, j.plan)
         for _ in range(2):
             res = j.run()
             assert res["global_matches"] == exp, (name, res["global_matches"], exp)

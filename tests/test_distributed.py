@@ -294,3 +294,35 @@ def test_rccl_multiprocess_shared_gpu(world):
     for p, o in zip(procs, outs):
         assert p.returncode == 0, o[-4000:]
     assert "OK" in outs[0], outs[0][-4000:]
+
+
+@pytest.mark.parametrize("dev", devices())
+@pytest.mark.parametrize("n_ranks,chunks,opts", [(2, 1, ""), (3, 3, "mat"), (4, 2, "wide"), (8, 1, "")])
+def test_one_sided_exchange(C, dev, n_ranks, chunks, opts):
+    """The MPI_Put analog (JoinConfig.exchange = ONE_SIDED): every rank copies
+    its runs straight into the owners' windows at their exact offsets, then a
+    barrier; counts (and materialized pairs) equal the RCCL / two-sided path."""
+    import torch
+    got = {}
+    for mode in ("ONE_SIDED", "RCCL"):
+        pairs = [None] * n_ranks
+
+        def cfg_fn(c, mode=mode):
+            c.exchange = getattr(C.ExchangeMode, mode)
+            c.bitmap_join = False
+            c.chunks = chunks
+            c.materialize = opts == "mat"
+            if opts == "wide":
+                c.format = C.TupleFormat.WIDE
+        results, exp = run_ranks(C, n_ranks, "device" if dev == "cuda" else "host", 300_007, 500_009, cfg_fn=cfg_fn,
+                                 outer_dist="ZIPF", theta=0.8, outputs=pairs if opts == "mat" else None)
+        for res, plan in results:
+            assert plan.one_sided == (mode == "ONE_SIDED")
+            assert res["global_matches"] == exp
+        got[mode] = [r[0]["local_matches"] for r in results]
+        if opts == "mat":
+            p = torch.cat([x.cpu() for x in pairs])
+            got[mode + "pairs"] = p[torch.argsort(p[:, 1] * (1 << 32) + p[:, 0])]
+    assert got["ONE_SIDED"] == got["RCCL"]
+    if opts == "mat":
+        assert torch.equal(got["ONE_SIDEDpairs"], got["RCCLpairs"])
