@@ -685,6 +685,131 @@ __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeK
   if (t == 0 && total) atomicAdd(a.result, total);
 }
 
+// ---------------------------------------------------------------- key-only
+// Count kernel of key-only 8-byte words (JoinPlan::keyOnly: wide keys, no
+// rids).  Bucketized table: buckets of 4 u64 slots (32 B) plus one u32 fill
+// counter per bucket.  Build: one returning LDS add on the home bucket's
+// counter gives the slot; an element finding its bucket full moves to the
+// next bucket (rare at load 1/2).  Probe: the counter and the whole bucket
+// are read with one u32 and two 16-byte LDS loads, all 16 elements of a lane
+// issued back to back; a counter above 4 means elements passed through to the
+// next bucket, so the walk continues there.  Against one 64-bit CAS / read
+// per probe-chain step this needs no returned CAS and no dependent chain
+// (1B x 1B sparse keys: 14 ms -> see profiles).  Only the counters are
+// cleared per item.
+constexpr int BPK_T = 256;
+constexpr int BPK_K = 16;
+constexpr uint32_t BPK_SLOTS = 4;
+
+size_t bpKeyLdsBytes(uint32_t rChunk) {
+  const uint64_t slots = uint64_t(1) << ceilLog2(2ull * rChunk);
+  return slots * 8 + (slots / BPK_SLOTS) * 4 + 64;
+}
+
+__global__ __launch_bounds__(BPK_T, 2) void bpKeyCountKernel(BPArgs a, const BPItem *__restrict__ items,
+                                                             const uint32_t *__restrict__ nItemsPtr, uint32_t capacity) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t maxSlots = 1u << ceilLog2(2ull * a.rChunk);
+  unsigned long long *table = reinterpret_cast<unsigned long long *>(smem);
+  uint32_t *fill = reinterpret_cast<uint32_t *>(table + maxSlots);
+  unsigned long long *wsum = reinterpret_cast<unsigned long long *>(fill + maxSlots / BPK_SLOTS);
+  const uint64_t *R = static_cast<const uint64_t *>(a.R);
+  const uint64_t *S = static_cast<const uint64_t *>(a.S);
+  constexpr uint32_t BATCH = BPK_T * BPK_K;
+  const uint32_t t = threadIdx.x;
+  const uint32_t nItems = min(*nItemsPtr, capacity);
+  uint64_t matches = 0;
+  for (uint32_t w = blockIdx.x; w < nItems; w += gridDim.x) {
+    const BPItem it = items[w];
+    const uint64_t rb = a.partR[it.part] + (uint64_t)it.rChunk * a.rChunk;
+    const uint64_t re = min(a.partREnd[it.part], rb + a.rChunk);
+    const uint64_t sb = a.partS[it.part] + (uint64_t)it.sChunk * a.sChunk;
+    const uint64_t se = min(a.partSEnd[it.part], sb + a.sChunk);
+    const uint32_t nr = (uint32_t)(re - rb), ns = (uint32_t)(se - sb);
+    uint32_t tbits = ceilLog2(2ull * nr);
+    if (tbits < 6) tbits = 6;
+    const uint32_t buckets = (1u << tbits) / BPK_SLOTS, bmask = buckets - 1;
+    uint64_t rv[BPK_K], sv[BPK_K];
+#pragma unroll
+    for (int k = 0; k < BPK_K; ++k) {
+      const uint32_t i = k * BPK_T + t;
+      if (i < nr) rv[k] = R[rb + i];
+      if (i < ns) sv[k] = S[sb + i];
+    }
+    for (uint32_t i = t; i < buckets; i += BPK_T) fill[i] = 0;
+    __syncthreads();
+    // ---- build
+    for (uint32_t b0 = 0; b0 < nr; b0 += BATCH) {
+      if (b0) {
+#pragma unroll
+        for (int k = 0; k < BPK_K; ++k) {
+          const uint32_t i = b0 + k * BPK_T + t;
+          if (i < nr) rv[k] = R[rb + i];
+        }
+      }
+      uint32_t bk[BPK_K], pos[BPK_K];
+#pragma unroll
+      for (int k = 0; k < BPK_K; ++k) {
+        const bool valid = b0 + k * BPK_T + t < nr;
+        bk[k] = hash64(rv[k], tbits - 2);
+        pos[k] = atomicAdd(&fill[bk[k]], valid ? 1u : 0u);  // branch-free: invalid lanes add 0
+        pos[k] = valid ? pos[k] : 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for (int k = 0; k < BPK_K; ++k) {
+        if (pos[k] == 0xFFFFFFFFu) continue;
+        uint32_t b = bk[k], p = pos[k];
+        while (p >= BPK_SLOTS) {  // home bucket full: the next one (its counter marks the pass)
+          b = (b + 1) & bmask;
+          p = atomicAdd(&fill[b], 1u);
+        }
+        table[b * BPK_SLOTS + p] = rv[k];
+      }
+    }
+    __syncthreads();
+    // ---- probe
+    for (uint32_t b0 = 0; b0 < ns; b0 += BATCH) {
+      if (b0) {
+#pragma unroll
+        for (int k = 0; k < BPK_K; ++k) {
+          const uint32_t i = b0 + k * BPK_T + t;
+          if (i < ns) sv[k] = S[sb + i];
+        }
+      }
+      uint32_t bk[BPK_K], f[BPK_K];
+      ulonglong2 e0[BPK_K], e1[BPK_K];
+#pragma unroll
+      for (int k = 0; k < BPK_K; ++k) {
+        bk[k] = hash64(sv[k], tbits - 2);
+        f[k] = fill[bk[k]];
+        const ulonglong2 *q = reinterpret_cast<const ulonglong2 *>(table + bk[k] * BPK_SLOTS);
+        e0[k] = q[0];
+        e1[k] = q[1];
+      }
+#pragma unroll
+      for (int k = 0; k < BPK_K; ++k) {
+        if (b0 + k * BPK_T + t >= ns) continue;
+        const uint64_t v = sv[k];
+        uint32_t n = min(f[k], BPK_SLOTS);
+        uint32_t c = (n > 0 && e0[k].x == v) + (n > 1 && e0[k].y == v) + (n > 2 && e1[k].x == v) +
+                     (n > 3 && e1[k].y == v);
+        uint32_t b = bk[k], fb = f[k];
+        while (fb > BPK_SLOTS) {  // elements passed through: continue in the next bucket
+          b = (b + 1) & bmask;
+          fb = fill[b];
+          const unsigned long long *q = table + b * BPK_SLOTS;
+          const uint32_t m = min(fb, BPK_SLOTS);
+          for (uint32_t j = 0; j < m; ++j) c += q[j] == v;
+        }
+        matches += c;
+      }
+    }
+    __syncthreads();  // the next item clears the counters
+  }
+  const unsigned long long total = blockReduceSum<BPK_T, unsigned long long>((unsigned long long)matches, wsum);
+  if (t == 0 && total) atomicAdd(a.result, total);
+}
+
 void buildProbe(const BPArgs &args, const BPItem *items, const uint32_t *nItems, uint32_t capacity, hipStream_t s) {
   if (capacity == 0) return;
   BPArgs a = args;
@@ -701,7 +826,11 @@ void buildProbe(const BPArgs &args, const BPItem *items, const uint32_t *nItems,
            "buildProbe: fragShift=%u < 32 (the rid field of a CompressedTuple is >= 32 bits)", a.fragShift);
   HJ_CHECK(!(a.keyOnly && (a.materialize || a.wide || a.split)), "buildProbe: key-only words count only, unsplit");
   if (bpMode(a) == BP_KCOUNT) {
-    hipLaunchKernelGGL(buildProbeKernel<BP_KCOUNT>, dim3(blocks), dim3(BPT), lds, s, a, items, nItems, capacity);
+    const size_t ldsK = bpKeyLdsBytes(a.rChunk);
+    HJ_CHECK(ldsK <= 160 * 1024, "buildProbe: key-only table %zu B exceeds 160 KiB (rChunk=%u)", ldsK, a.rChunk);
+    const uint32_t perCuK = (uint32_t)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / ldsK));
+    hipLaunchKernelGGL(bpKeyCountKernel, dim3(std::min<uint32_t>(capacity, 256 * perCuK)), dim3(BPK_T), ldsK, s, a,
+                       items, nItems, capacity);
     HIP_CHECK_LAUNCH();
     return;
   }
