@@ -698,7 +698,8 @@ __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeK
 // (1B x 1B sparse keys: 14 ms -> see profiles).  Only the counters are
 // cleared per item.
 constexpr int BPK_T = 256;
-constexpr int BPK_K = 16;
+constexpr int BPK_K = 8;
+constexpr int BPK_H = 4;
 constexpr uint32_t BPK_SLOTS = 4;
 
 size_t bpKeyLdsBytes(uint32_t rChunk) {
@@ -706,7 +707,7 @@ size_t bpKeyLdsBytes(uint32_t rChunk) {
   return slots * 8 + (slots / BPK_SLOTS) * 4 + 64;
 }
 
-__global__ __launch_bounds__(BPK_T, 2) void bpKeyCountKernel(BPArgs a, const BPItem *__restrict__ items,
+__global__ __launch_bounds__(BPK_T, 4) void bpKeyCountKernel(BPArgs a, const BPItem *__restrict__ items,
                                                              const uint32_t *__restrict__ nItemsPtr, uint32_t capacity) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t maxSlots = 1u << ceilLog2(2ull * a.rChunk);
@@ -776,32 +777,38 @@ __global__ __launch_bounds__(BPK_T, 2) void bpKeyCountKernel(BPArgs a, const BPI
           if (i < ns) sv[k] = S[sb + i];
         }
       }
-      uint32_t bk[BPK_K], f[BPK_K];
-      ulonglong2 e0[BPK_K], e1[BPK_K];
+      // Two half-batches of BPK_H elements keep the 32-byte buckets of the
+      // in-flight reads within the register budget of 4 workgroups per CU.
 #pragma unroll
-      for (int k = 0; k < BPK_K; ++k) {
-        bk[k] = hash64(sv[k], tbits - 2);
-        f[k] = fill[bk[k]];
-        const ulonglong2 *q = reinterpret_cast<const ulonglong2 *>(table + bk[k] * BPK_SLOTS);
-        e0[k] = q[0];
-        e1[k] = q[1];
-      }
+      for (int h = 0; h < BPK_K / BPK_H; ++h) {
+        uint32_t bk[BPK_H], f[BPK_H];
+        ulonglong2 e0[BPK_H], e1[BPK_H];
 #pragma unroll
-      for (int k = 0; k < BPK_K; ++k) {
-        if (b0 + k * BPK_T + t >= ns) continue;
-        const uint64_t v = sv[k];
-        uint32_t n = min(f[k], BPK_SLOTS);
-        uint32_t c = (n > 0 && e0[k].x == v) + (n > 1 && e0[k].y == v) + (n > 2 && e1[k].x == v) +
-                     (n > 3 && e1[k].y == v);
-        uint32_t b = bk[k], fb = f[k];
-        while (fb > BPK_SLOTS) {  // elements passed through: continue in the next bucket
-          b = (b + 1) & bmask;
-          fb = fill[b];
-          const unsigned long long *q = table + b * BPK_SLOTS;
-          const uint32_t m = min(fb, BPK_SLOTS);
-          for (uint32_t j = 0; j < m; ++j) c += q[j] == v;
+        for (int j = 0; j < BPK_H; ++j) {
+          bk[j] = hash64(sv[h * BPK_H + j], tbits - 2);
+          f[j] = fill[bk[j]];
+          const ulonglong2 *q = reinterpret_cast<const ulonglong2 *>(table + bk[j] * BPK_SLOTS);
+          e0[j] = q[0];
+          e1[j] = q[1];
         }
-        matches += c;
+#pragma unroll
+        for (int j = 0; j < BPK_H; ++j) {
+          const int k = h * BPK_H + j;
+          if (b0 + k * BPK_T + t >= ns) continue;
+          const uint64_t v = sv[k];
+          const uint32_t n = min(f[j], BPK_SLOTS);
+          uint32_t c = (n > 0 && e0[j].x == v) + (n > 1 && e0[j].y == v) + (n > 2 && e1[j].x == v) +
+                       (n > 3 && e1[j].y == v);
+          uint32_t b = bk[j], fb = f[j];
+          while (fb > BPK_SLOTS) {  // elements passed through: continue in the next bucket
+            b = (b + 1) & bmask;
+            fb = fill[b];
+            const unsigned long long *q = table + b * BPK_SLOTS;
+            const uint32_t m = min(fb, BPK_SLOTS);
+            for (uint32_t i = 0; i < m; ++i) c += q[i] == v;
+          }
+          matches += c;
+        }
       }
     }
     __syncthreads();  // the next item clears the counters
@@ -828,7 +835,7 @@ void buildProbe(const BPArgs &args, const BPItem *items, const uint32_t *nItems,
   if (bpMode(a) == BP_KCOUNT) {
     const size_t ldsK = bpKeyLdsBytes(a.rChunk);
     HJ_CHECK(ldsK <= 160 * 1024, "buildProbe: key-only table %zu B exceeds 160 KiB (rChunk=%u)", ldsK, a.rChunk);
-    const uint32_t perCuK = (uint32_t)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / ldsK));
+    const uint32_t perCuK = (uint32_t)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / ldsK));
     hipLaunchKernelGGL(bpKeyCountKernel, dim3(std::min<uint32_t>(capacity, 256 * perCuK)), dim3(BPK_T), ldsK, s, a,
                        items, nItems, capacity);
     HIP_CHECK_LAUNCH();
