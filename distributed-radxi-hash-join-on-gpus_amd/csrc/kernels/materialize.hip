@@ -11,6 +11,8 @@
 #include "kernels.h"
 #include "device_common.h"
 
+#include <cstdlib>
+
 namespace hpcjoin {
 namespace kernels {
 
@@ -139,7 +141,11 @@ using u64x2 = unsigned long long __attribute__((ext_vector_type(2)));
 // SF100: direct stores 42.3 ms, LDS-staged 39.3, + XCD walk 38.6 (variants
 // without NT within 1%); the rest is the random 32-byte row gathers, fetched
 // as 64-byte requests (FETCH_SIZE 89 GB for 600M pairs).
-template <bool NT, bool XCD>
+// BNT: the lineitem-side (B) rows, each read once at a random position, are
+// loaded non-temporally so their lines do not push the ~4x-reused inner (A)
+// rows out of the XCD's L2 (FETCH_SIZE showed 64 B fetched per A access: no
+// reuse survived the B stream).
+template <bool NT, bool XCD, bool BNT = false>
 __global__ __launch_bounds__(MT) void materializeLocalKernel(const ulonglong2 *__restrict__ pairs, uint64_t n,
                                                              const ulonglong2 *__restrict__ rowsA, uint64_t offA,
                                                              const ulonglong2 *__restrict__ rowsB, uint64_t offB,
@@ -168,7 +174,12 @@ __global__ __launch_bounds__(MT) void materializeLocalKernel(const ulonglong2 *_
       const uint64_t x = __shfl(p.x, j, 64), y = __shfl(p.y, j, 64);
       if (j < m) {
         ra[k] = rowsA[2 * (x - offA) + half];
-        rb[k] = rowsB[2 * (y - offB) + half];
+        if (BNT) {
+          const u64x2 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(rowsB + 2 * (y - offB) + half));
+          rb[k] = make_ulonglong2(v.x, v.y);
+        } else {
+          rb[k] = rowsB[2 * (y - offB) + half];
+        }
       }
     }
     w[5 * lane] = p;
@@ -206,9 +217,19 @@ void materializeLocal(const ulonglong2 *pairs, uint64_t n, const uint64_t *rowsA
   if (!n) return;
   const uint64_t blocks = ceilDiv(ceilDiv(n, 64), MAT_WAVES);
   const uint32_t grid = (uint32_t)(blocks < 8192 ? (blocks + 7) / 8 * 8 : 8192);
-  hipLaunchKernelGGL((materializeLocalKernel<true, true>), dim3(grid), dim3(MT), 0, s, pairs, n,
-                     reinterpret_cast<const ulonglong2 *>(rowsA), offA, reinterpret_cast<const ulonglong2 *>(rowsB),
-                     offB, reinterpret_cast<ulonglong2 *>(out));
+  static const int variant = [] {
+    const char *e = std::getenv("HPCJOIN_MAT_VARIANT");
+    return e ? std::atoi(e) : 1;
+  }();
+  const auto *ra = reinterpret_cast<const ulonglong2 *>(rowsA);
+  const auto *rb = reinterpret_cast<const ulonglong2 *>(rowsB);
+  auto *o = reinterpret_cast<ulonglong2 *>(out);
+  switch (variant) {  // sweep: NT stores / non-temporal B loads
+    case 0: hipLaunchKernelGGL((materializeLocalKernel<true, true, false>), dim3(grid), dim3(MT), 0, s, pairs, n, ra, offA, rb, offB, o); break;
+    case 2: hipLaunchKernelGGL((materializeLocalKernel<false, true, true>), dim3(grid), dim3(MT), 0, s, pairs, n, ra, offA, rb, offB, o); break;
+    case 3: hipLaunchKernelGGL((materializeLocalKernel<false, true, false>), dim3(grid), dim3(MT), 0, s, pairs, n, ra, offA, rb, offB, o); break;
+    default: hipLaunchKernelGGL((materializeLocalKernel<true, true, true>), dim3(grid), dim3(MT), 0, s, pairs, n, ra, offA, rb, offB, o); break;
+  }
   HIP_CHECK_LAUNCH();
 }
 
