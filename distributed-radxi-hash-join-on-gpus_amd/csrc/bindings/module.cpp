@@ -516,6 +516,7 @@ py::dict resultToDict(const operators::JoinResult &r) {
   d["global_matches"] = r.globalMatches;
   d["output_pairs"] = r.outputPairs;
   d["output_overflow"] = r.outputOverflow;
+  d["rows_fused"] = r.rowsFused;
   d["reruns"] = r.reruns;
   d["sampled_network"] = r.sampledNetwork;
   d["network_fallbacks"] = r.networkFallbacks;
@@ -871,6 +872,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              uint64_t innerGlobal, at::Tensor outerRows, uint64_t outerOffset, uint64_t outerGlobal) {
             // Collective.  Returns [pairs, 10] int64: rid_inner, rid_outer, inner row (4), outer row (4).
             TORCH_CHECK(j.getConfig().materialize, "join was not run with materialize=True");
+            TORCH_CHECK(!j.lastResult().rowsFused, "the last run wrote rows directly (join_materialized)");
             TORCH_CHECK(innerRows.dim() == 2 && innerRows.size(1) == (int64_t)kernels::ROW_WORDS &&
                             outerRows.dim() == 2 && outerRows.size(1) == (int64_t)kernels::ROW_WORDS,
                         "payload rows must be [n, 4] int64 (32 bytes)");
@@ -886,6 +888,68 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
               lm.materialize(j.getOutput(), n, ptr<uint64_t>(out));
             }
             return out;
+          },
+          py::arg("context"), py::arg("inner_rows"), py::arg("inner_rid_offset"), py::arg("inner_global_rows"),
+          py::arg("outer_rows"), py::arg("outer_rid_offset"), py::arg("outer_global_rows"))
+      .def_property_readonly("can_fuse_rows", &operators::HashJoin::canFuseRows)
+      .def(
+          "join_materialized",
+          [](operators::HashJoin &j, std::shared_ptr<core::ExecContext> ctx, at::Tensor innerRows, uint64_t innerOffset,
+             uint64_t innerGlobal, at::Tensor outerRows, uint64_t outerOffset, uint64_t outerGlobal) {
+            // Collective.  One join + both payload rows of every result pair:
+            // returns (result dict, [pairs, 10] int64 rows).  Device joins at
+            // N = 1 write the rows from the build/probe's materialize pass
+            // (no pair array); otherwise run() + LateMaterialization.
+            TORCH_CHECK(j.getConfig().materialize, "join_materialized needs materialize=True");
+            TORCH_CHECK(innerRows.dim() == 2 && innerRows.size(1) == (int64_t)kernels::ROW_WORDS &&
+                            outerRows.dim() == 2 && outerRows.size(1) == (int64_t)kernels::ROW_WORDS,
+                        "payload rows must be [n, 4] int64 (32 bytes)");
+            TORCH_CHECK(innerRows.is_contiguous() && outerRows.is_contiguous(), "payload rows must be contiguous");
+            const auto opts = at::TensorOptions().dtype(at::kLong).device(innerRows.device());
+            constexpr int64_t W = operators::LateMaterialization::OUT_WORDS;
+            operators::JoinResult r;
+            if (innerRows.is_cuda()) HIP_CHECK(hipDeviceSynchronize());  // payloads written on other streams
+            if (innerRows.is_cuda() && outerRows.is_cuda() && j.canFuseRows()) {
+              struct Clear {
+                operators::HashJoin &j;
+                ~Clear() { j.clearRowSink(); }
+              } clear{j};
+              uint64_t cap = j.getConfig().outputCapacity ? j.getConfig().outputCapacity
+                                                          : (uint64_t)outerRows.size(0) + 1024;
+              for (int attempt = 0; attempt < 2; ++attempt) {
+                at::Tensor out = at::empty({(int64_t)cap, W}, opts);
+                kernels::RowSink sk;
+                sk.rowsA = ptr<uint64_t>(innerRows);
+                sk.offA = innerOffset;
+                sk.rowsB = ptr<uint64_t>(outerRows);
+                sk.offB = outerOffset;
+                sk.out = ptr<uint64_t>(out);
+                sk.capacity = cap;
+                j.setRowSink(sk);
+                {
+                  py::gil_scoped_release nogil;
+                  r = j.run();
+                }
+                if (!r.rowsFused) break;  // this run took another layout: materialize the pairs below
+                if (!r.outputOverflow)
+                  return py::make_tuple(resultToDict(r), out.narrow(0, 0, (int64_t)r.outputPairs));
+                cap = r.outputPairs;  // more matches than the first guess: once more, exactly sized
+              }
+              TORCH_CHECK(!r.rowsFused, "join_materialized: row output overflowed twice");
+            } else {
+              py::gil_scoped_release nogil;
+              r = j.run();
+            }
+            operators::PayloadColumn a{ptr<uint64_t>(innerRows), (uint64_t)innerRows.size(0), innerOffset, innerGlobal};
+            operators::PayloadColumn b{ptr<uint64_t>(outerRows), (uint64_t)outerRows.size(0), outerOffset, outerGlobal};
+            const uint64_t n = r.outputPairs;
+            at::Tensor out = at::empty({(int64_t)n, W}, opts);
+            {
+              py::gil_scoped_release nogil;
+              operators::LateMaterialization lm(ctx.get(), a, b);
+              lm.materialize(j.getOutput(), n, ptr<uint64_t>(out));
+            }
+            return py::make_tuple(resultToDict(r), out);
           },
           py::arg("context"), py::arg("inner_rows"), py::arg("inner_rid_offset"), py::arg("inner_global_rows"),
           py::arg("outer_rows"), py::arg("outer_rid_offset"), py::arg("outer_global_rows"))

@@ -48,7 +48,12 @@ JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t global
   const uint32_t maxBits = Configuration::GPU_MAX_FANOUT_BITS - 1;  // 1024-way per pass
   // Materializing compressed tuples: final partitions of <= 2048 inner tuples
   // fit one 32 KiB (fragment, rid) table of the split materializing kernel.
+  // At N = 1 (where rows can be written by the build/probe itself) the target
+  // is 1024: with their 32-byte payload rows (32 KiB) they fit the LDS of the
+  // fused row-output kernel, 3 workgroups per CU (kernels/build_probe.hip,
+  // bpMatRowsKernel).  SF100: 35.6 ms fused vs 42.0 ms join + separate pass.
   const bool matNarrow = p.materialize && !p.wide && !cfg.rChunk;
+  const uint32_t matTarget = numberOfNodes == 1 ? 1024 : 2048;
   // >= 8 network partitions per node so LPT has room to balance.
   const uint32_t minNet = std::max<uint32_t>(4, ceilLog2(numberOfNodes) + 3);
   auto splitBits = [&](uint64_t target) {
@@ -68,7 +73,7 @@ JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t global
       p.localBits = totalBits > p.networkBits ? std::min(maxBits, totalBits - p.networkBits) : 1;
     }
   };
-  splitBits(matNarrow ? std::min<uint64_t>(cfg.buildTarget, 2048) : cfg.buildTarget);
+  splitBits(matNarrow ? std::min<uint64_t>(cfg.buildTarget, matTarget) : cfg.buildTarget);
   JOIN_ASSERT(p.networkBits >= 1 && p.networkBits <= Configuration::GPU_MAX_FANOUT_BITS, "Plan",
               "networkBits=%u out of range", p.networkBits);
   JOIN_ASSERT(p.localBits <= Configuration::GPU_MAX_FANOUT_BITS, "Plan", "localBits=%u out of range", p.localBits);
@@ -133,7 +138,7 @@ JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t global
     p.rChunk = cfg.rChunk;
   } else {
     const uint32_t entry = p.wide ? (p.materialize ? 16 : 8) : (p.materialize || p.keyOnly ? 8 : 4);
-    const uint32_t budget = (entry == 4 || matNarrow || p.keyOnly) ? 32 * 1024 : 64 * 1024;
+    const uint32_t budget = (entry == 4 || p.keyOnly) ? 32 * 1024 : matNarrow ? 16 * matTarget : 64 * 1024;
     p.rChunk = (budget / entry) / 2;
   }
   return p;

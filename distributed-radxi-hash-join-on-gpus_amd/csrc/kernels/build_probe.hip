@@ -23,6 +23,7 @@
 #include "kernels.h"
 #include "device_common.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace hpcjoin {
@@ -291,11 +292,11 @@ __global__ __launch_bounds__(BPD_T, MINB) void bpDirectSplitKernel(BPArgs a, con
 constexpr int BPM_T = 256;
 constexpr int BPM_K = 8;
 
-template <bool FULL>
+template <bool FULL, int K>
 __device__ __forceinline__ void bpmLoad(const uint32_t *__restrict__ rid, const uint16_t *__restrict__ hi, uint64_t off,
-                                        uint32_t n, uint32_t b0, uint32_t (&r)[BPM_K], uint32_t (&f)[BPM_K]) {
+                                        uint32_t n, uint32_t b0, uint32_t (&r)[K], uint32_t (&f)[K]) {
 #pragma unroll
-  for (int k = 0; k < BPM_K; ++k) {
+  for (int k = 0; k < K; ++k) {
     const uint32_t idx = b0 + k * BPM_T + threadIdx.x;
     if (FULL || idx < n) {
       r[k] = rid[off + idx];
@@ -304,10 +305,93 @@ __device__ __forceinline__ void bpmLoad(const uint32_t *__restrict__ rid, const 
   }
 }
 
-__global__ __launch_bounds__(BPM_T, 4) void bpMatSplitKernel(BPArgs a, const BPItem *__restrict__ items,
+__device__ __forceinline__ void waveSync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+using u64x2 = unsigned long long __attribute__((ext_vector_type(2)));
+
+// Fused row output (ROWS): a wave's matches of one probe batch occupy output
+// rows [base, base + T).  Per window of BPM_LIST (= 128) rows their
+// (inner, outer) rid pairs are listed at the head of the wave's 5 KiB LDS
+// stage; lane pair (2j, 2j + 1) takes list entries j, j + 32, j + 64, j + 96
+// and issues the eight 16-byte half-row loads of their payloads at once
+// (inner rows plain: each is re-read ~4x while its work item is hot; outer
+// rows, each read once, non-temporal so they do not push the inner rows out
+// of L2).  The rows are then assembled 64 at a time in the stage (over the
+// consumed list) and written by 5 store instructions of 64 consecutive
+// 16-byte pieces (per-lane 80-byte row stores measured 2x slower).  Same
+// layout as operators/LateMaterialization, whose separate pass this replaces
+// at N = 1: no pair array is written and read back.
+constexpr uint32_t BPM_LIST = 128;
+
+__device__ __forceinline__ void bpmLoadRow(const BPArgs &a, const uint2 *list, uint32_t j, uint32_t m, uint32_t half,
+                                           uint2 &p, ulonglong2 &va, ulonglong2 &vb) {
+  p = list[j < m ? j : 0];
+  va = a.rowsA[2 * ((uint64_t)p.x - a.offA) + half];
+  const u64x2 v =
+      __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(a.rowsB + 2 * ((uint64_t)p.y - a.offB) + half));
+  vb = make_ulonglong2(v.x, v.y);
+}
+
+__device__ __forceinline__ void bpmStageRow(ulonglong2 *stage, uint32_t j, uint32_t mh, uint32_t half, uint2 p,
+                                            ulonglong2 va, ulonglong2 vb) {
+  if (j < mh) {
+    if (half == 0) stage[5 * j] = make_ulonglong2(p.x, p.y);
+    stage[5 * j + 1 + half] = va;
+    stage[5 * j + 3 + half] = vb;
+  }
+}
+
+__device__ __forceinline__ void bpmStoreRows(const BPArgs &a, const ulonglong2 *stage, uint32_t mh,
+                                             unsigned long long r0, uint32_t lane) {
+  ulonglong2 *o = a.outRows + 5 * r0;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const uint32_t q = WAVE * k + lane;
+    if (q < 5 * mh && r0 + q / 5 < a.outCapacity) {
+      const ulonglong2 v = stage[q];
+      const u64x2 vv = {v.x, v.y};
+      __builtin_nontemporal_store(vv, reinterpret_cast<u64x2 *>(o + q));
+    }
+  }
+}
+
+__device__ __forceinline__ void bpmGatherRows(const BPArgs &a, ulonglong2 *stage, uint32_t m,
+                                              unsigned long long row0, uint32_t lane) {
+  const uint32_t half = lane & 1, j0 = lane >> 1;
+  const uint2 *list = reinterpret_cast<const uint2 *>(stage);
+  uint2 p0, p1, p2, p3;
+  ulonglong2 a0, a1, a2, a3, b0, b1, b2, b3;
+  bpmLoadRow(a, list, j0, m, half, p0, a0, b0);
+  bpmLoadRow(a, list, j0 + 32, m, half, p1, a1, b1);
+  bpmLoadRow(a, list, j0 + 64, m, half, p2, a2, b2);
+  bpmLoadRow(a, list, j0 + 96, m, half, p3, a3, b3);
+  waveSync();  // the list is consumed: the stage is reused for the rows
+  const uint32_t m0 = min(64u, m);
+  bpmStageRow(stage, j0, m0, half, p0, a0, b0);
+  bpmStageRow(stage, j0 + 32, m0, half, p1, a1, b1);
+  waveSync();
+  bpmStoreRows(a, stage, m0, row0, lane);
+  waveSync();
+  if (m > 64) {  // wave-uniform
+    const uint32_t m1 = m - 64;
+    bpmStageRow(stage, j0, m1, half, p2, a2, b2);
+    bpmStageRow(stage, j0 + 32, m1, half, p3, a3, b3);
+    waveSync();
+    bpmStoreRows(a, stage, m1, row0 + 64, lane);
+    waveSync();
+  }
+}
+
+template <bool ROWS>
+__global__ __launch_bounds__(BPM_T, ROWS ? 3 : 4) void bpMatSplitKernel(BPArgs a, const BPItem *__restrict__ items,
                                                               const uint32_t *__restrict__ nItemsPtr,
                                                               uint32_t capacity) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ ulonglong2 rowStage[ROWS ? BPM_T / WAVE : 1][ROWS ? 5 * WAVE : 1];
   const uint32_t maxSlots = 1u << ceilLog2(2ull * a.rChunk);
   uint32_t *fragT = reinterpret_cast<uint32_t *>(smem);
   uint32_t *ridT = fragT + maxSlots;
@@ -315,7 +399,9 @@ __global__ __launch_bounds__(BPM_T, 4) void bpMatSplitKernel(BPArgs a, const BPI
   __shared__ uint32_t itemCursor;
   const uint32_t *Rr = reinterpret_cast<const uint32_t *>(a.R);
   const uint32_t *Sr = reinterpret_cast<const uint32_t *>(a.S);
-  constexpr uint32_t BATCH = BPM_T * BPM_K;
+  // Rows: 4 outer tuples per thread per batch (the gather state needs the registers).
+  constexpr int K = ROWS ? 4 : BPM_K;
+  constexpr uint32_t BATCH = BPM_T * K;
   const uint32_t t = threadIdx.x, lane = t & (WAVE - 1);
   const bool perItem = a.itemOffsets != nullptr;
   const uint32_t nItems = min(*nItemsPtr, capacity);
@@ -331,7 +417,7 @@ __global__ __launch_bounds__(BPM_T, 4) void bpMatSplitKernel(BPArgs a, const BPI
     if (tbits < 6) tbits = 6;
     const uint32_t slots = 1u << tbits, mask = slots - 1;
     const unsigned long long itemBase = perItem ? a.itemOffsets[w] : 0ull;
-    uint32_t rr[BPM_K], rf[BPM_K], sr[BPM_K], sf[BPM_K];
+    uint32_t rr[K], rf[K], sr[K], sf[K];
     if (nr >= BATCH) bpmLoad<true>(Rr, a.Rhi, rb, nr, 0, rr, rf);
     else bpmLoad<false>(Rr, a.Rhi, rb, nr, 0, rr, rf);
     if (ns >= BATCH) bpmLoad<true>(Sr, a.Shi, sb, ns, 0, sr, sf);
@@ -344,7 +430,7 @@ __global__ __launch_bounds__(BPM_T, 4) void bpMatSplitKernel(BPArgs a, const BPI
     for (uint32_t b0 = 0; b0 < nr; b0 += BATCH) {
       if (b0) bpmLoad<false>(Rr, a.Rhi, rb, nr, b0, rr, rf);
 #pragma unroll
-      for (int k = 0; k < BPM_K; ++k) {
+      for (int k = 0; k < K; ++k) {
         if (b0 + k * BPM_T + t < nr) {
           uint32_t h = hash32(rf[k], tbits);
           while (atomicCAS(&fragT[h], EMPTY32, rf[k]) != EMPTY32) h = (h + 1) & mask;
@@ -360,11 +446,11 @@ __global__ __launch_bounds__(BPM_T, 4) void bpMatSplitKernel(BPArgs a, const BPI
         if (b0 + BATCH <= ns) bpmLoad<true>(Sr, a.Shi, sb, ns, b0, sr, sf);
         else bpmLoad<false>(Sr, a.Shi, sb, ns, b0, sr, sf);
       }
-      const uint32_t kmax = min((uint32_t)BPM_K, (uint32_t)ceilDiv(ns - b0, BPM_T));  // block-uniform
-      uint32_t found[BPM_K], first[BPM_K], incl[BPM_K];
+      const uint32_t kmax = min((uint32_t)K, (uint32_t)ceilDiv(ns - b0, BPM_T));  // block-uniform
+      uint32_t found[K], first[K], incl[K];
       uint32_t waveTotal = 0;
 #pragma unroll
-      for (int k = 0; k < BPM_K; ++k) {
+      for (int k = 0; k < K; ++k) {
         found[k] = 0;
         first[k] = 0;
         incl[k] = 0;
@@ -389,8 +475,38 @@ __global__ __launch_bounds__(BPM_T, 4) void bpMatSplitKernel(BPArgs a, const BPI
         base = perItem ? itemBase + atomicAdd(&itemCursor, waveTotal)
                        : atomicAdd(a.outCursor, (unsigned long long)waveTotal);
       base = __shfl(base, WAVE - 1, WAVE);
+      if constexpr (ROWS) {
+        ulonglong2 *stg = rowStage[t / WAVE];
+        uint2 *list = reinterpret_cast<uint2 *>(stg);
+        for (uint32_t w0 = 0; w0 < waveTotal; w0 += BPM_LIST) {  // wave-uniform; > 1 window only with duplicates
+          uint32_t kb = 0;  // rows of columns < k
 #pragma unroll
-      for (int k = 0; k < BPM_K; ++k) {
+          for (int k = 0; k < K; ++k) {
+            if ((uint32_t)k >= kmax) break;
+            const uint32_t r0 = kb + incl[k] - found[k];
+            if (found[k] && r0 < w0 + BPM_LIST && r0 + found[k] > w0) {
+              if (r0 >= w0) list[r0 - w0] = make_uint2(first[k], sr[k]);
+              if (found[k] > 1) {  // duplicate inner keys: the chain's other matches
+                const uint32_t frag = sf[k];
+                uint32_t h = hash32(frag, tbits), e, j = 0;
+                while ((e = fragT[h]) != EMPTY32) {
+                  if (e == frag) {
+                    if (j && r0 + j >= w0 && r0 + j < w0 + BPM_LIST) list[r0 + j - w0] = make_uint2(ridT[h], sr[k]);
+                    ++j;
+                  }
+                  h = (h + 1) & mask;
+                }
+              }
+            }
+            kb += __shfl(incl[k], WAVE - 1, WAVE);
+          }
+          waveSync();
+          bpmGatherRows(a, stg, min(BPM_LIST, waveTotal - w0), base + w0, lane);
+        }
+        continue;
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
         if ((uint32_t)k >= kmax) break;
         const unsigned long long pos = base + incl[k] - found[k];
         if (found[k]) emitPair(a, pos, first[k], sr[k]);
@@ -411,6 +527,205 @@ __global__ __launch_bounds__(BPM_T, 4) void bpMatSplitKernel(BPArgs a, const BPI
     __syncthreads();  // the next item clears the table and the cursor
   }
   const unsigned long long total = blockReduceSum<BPM_T, unsigned long long>((unsigned long long)matches, wsum);
+  if (t == 0 && total) atomicAdd(a.result, total);
+}
+
+// Fused row output with the inner payload rows in LDS (split layout, inner
+// chunks of <= BPR_MAX_R tuples).  The build also gathers the chunk's inner
+// rows once into LDS (each random 32-byte row costs one 64-byte line fetch;
+// re-reading them from L2 per match lost all reuse with ~1500 items in flight:
+// the inner side then fetched 37 GB for SF100 instead of 9.6).  Per probe batch
+// a wave reserves one contiguous output range, lists its matches (inner index,
+// outer rid) in LDS, and writes each window of <= 128 rows in 16-byte pieces
+// q = 64 i + lane of the window's 5 m pieces: piece q is field q % 5 of row
+// q / 5 -- rid pair and inner halves from LDS, outer halves loaded from
+// global memory (non-temporal, each outer row is read once).  All loads of a
+// window are issued before its stores, and every store instruction writes
+// 1 KiB of contiguous output: no staging buffer, no partial lines inside a
+// window.  LDS for 1024-tuple chunks: 52 KiB (3 blocks of 4 waves per CU).
+constexpr int BPR_T = 256;
+constexpr int BPR_K = 2;  // outer tuples per thread per batch: ~128 matches per wave (one window)
+constexpr uint32_t BPR_MAX_R = 1024;
+constexpr uint32_t BPR_LIST = 128;
+
+static size_t bpMatRowsLds(uint32_t rChunk) {
+  const size_t slots = size_t(1) << ceilLog2(2ull * rChunk);
+  return (size_t)rChunk * 32 + (BPR_T / WAVE) * BPR_LIST * 8 + slots * 4 + (size_t)rChunk * 4 + slots * 2 + 64;
+}
+
+__device__ __forceinline__ void bprEmitWindow(const BPArgs &a, const uint2 *list, const ulonglong2 *rowsL,
+                                              const uint32_t *ridL, uint32_t m, unsigned long long row0,
+                                              uint32_t lane) {
+  const uint32_t P = 5 * m;
+  ulonglong2 v0, v1, v2, v3, v4, v5, v6, v7, v8, v9;
+#define BPR_FETCH(I, V)                                                                                       \
+  {                                                                                                           \
+    const uint32_t q = WAVE * (I) + lane;                                                                     \
+    if (q < P) {                                                                                              \
+      const uint32_t row = q / 5, f = q - 5 * row;                                                            \
+      const uint2 e = list[row];                                                                              \
+      if (f >= 3) {                                                                                           \
+        const u64x2 x = __builtin_nontemporal_load(                                                           \
+            reinterpret_cast<const u64x2 *>(a.rowsB + 2 * ((uint64_t)e.y - a.offB) + (f - 3)));               \
+        V = make_ulonglong2(x.x, x.y);                                                                        \
+      } else if (f == 0) {                                                                                    \
+        V = make_ulonglong2(ridL[e.x], e.y);                                                                  \
+      } else {                                                                                                \
+        V = rowsL[2 * e.x + (f - 1)];                                                                         \
+      }                                                                                                       \
+    }                                                                                                         \
+  }
+  BPR_FETCH(0, v0) BPR_FETCH(1, v1) BPR_FETCH(2, v2) BPR_FETCH(3, v3) BPR_FETCH(4, v4)
+  BPR_FETCH(5, v5) BPR_FETCH(6, v6) BPR_FETCH(7, v7) BPR_FETCH(8, v8) BPR_FETCH(9, v9)
+#undef BPR_FETCH
+  ulonglong2 *o = a.outRows + 5 * row0;
+  const unsigned long long lim = a.outCapacity > row0 ? 5 * (a.outCapacity - row0) : 0;  // pieces below capacity
+#define BPR_STORE(I, V)                                                                                       \
+  {                                                                                                           \
+    const uint32_t q = WAVE * (I) + lane;                                                                     \
+    if (q < P && q < lim) {                                                                                   \
+      const u64x2 x = {V.x, V.y};                                                                             \
+      __builtin_nontemporal_store(x, reinterpret_cast<u64x2 *>(o + q));                                       \
+    }                                                                                                         \
+  }
+  BPR_STORE(0, v0) BPR_STORE(1, v1) BPR_STORE(2, v2) BPR_STORE(3, v3) BPR_STORE(4, v4)
+  BPR_STORE(5, v5) BPR_STORE(6, v6) BPR_STORE(7, v7) BPR_STORE(8, v8) BPR_STORE(9, v9)
+#undef BPR_STORE
+}
+
+// (HIP launch bounds: the second value is waves per SIMD: 3 blocks of 4 waves per CU.)
+__global__ __launch_bounds__(BPR_T, 3) void bpMatRowsKernel(BPArgs a, const BPItem *__restrict__ items,
+                                                            const uint32_t *__restrict__ nItemsPtr,
+                                                            uint32_t capacity) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t maxSlots = 1u << ceilLog2(2ull * a.rChunk);
+  ulonglong2 *rowsL = reinterpret_cast<ulonglong2 *>(smem);                        // [rChunk][2]
+  uint2 *lists = reinterpret_cast<uint2 *>(rowsL + 2 * (size_t)a.rChunk);          // [waves][BPR_LIST]
+  uint32_t *fragT = reinterpret_cast<uint32_t *>(lists + (BPR_T / WAVE) * BPR_LIST);  // [slots]
+  uint32_t *ridL = fragT + maxSlots;                                               // [rChunk]
+  uint16_t *idxT = reinterpret_cast<uint16_t *>(ridL + a.rChunk);                  // [slots]
+  unsigned long long *wsum = reinterpret_cast<unsigned long long *>(
+      reinterpret_cast<uintptr_t>(idxT + maxSlots + 3) & ~uintptr_t(7));
+  __shared__ uint32_t itemCursor;
+  const uint32_t *Rr = reinterpret_cast<const uint32_t *>(a.R);
+  const uint32_t *Sr = reinterpret_cast<const uint32_t *>(a.S);
+  constexpr uint32_t BATCH = BPR_T * BPR_K;
+  const uint32_t t = threadIdx.x, lane = t & (WAVE - 1);
+  uint2 *list = lists + (t / WAVE) * BPR_LIST;
+  const uint32_t nItems = min(*nItemsPtr, capacity);
+  uint64_t matches = 0;
+  for (uint32_t w = blockIdx.x; w < nItems; w += gridDim.x) {
+    const BPItem it = items[w];
+    const uint64_t rb = a.partR[it.part] + (uint64_t)it.rChunk * a.rChunk;
+    const uint64_t re = min(a.partREnd[it.part], rb + a.rChunk);
+    const uint64_t sb = a.partS[it.part] + (uint64_t)it.sChunk * a.sChunk;
+    const uint64_t se = min(a.partSEnd[it.part], sb + a.sChunk);
+    const uint32_t nr = (uint32_t)(re - rb), ns = (uint32_t)(se - sb);
+    uint32_t tbits = ceilLog2(2ull * nr);
+    if (tbits < 6) tbits = 6;
+    const uint32_t slots = 1u << tbits, mask = slots - 1;
+    const unsigned long long itemBase = a.itemOffsets[w];
+    uint32_t sr[BPR_K], sf[BPR_K];  // first outer batch: in flight during the build
+#pragma unroll
+    for (int k = 0; k < BPR_K; ++k) {
+      const uint32_t i = k * BPR_T + t;
+      sr[k] = i < ns ? Sr[sb + i] : 0u;
+      sf[k] = i < ns ? (uint32_t)a.Shi[sb + i] : 0u;
+    }
+    for (uint32_t i = t; i < slots; i += BPR_T) fragT[i] = EMPTY32;
+    if (t == 0) itemCursor = 0;
+    __syncthreads();
+
+    // ---- build: table (fragment -> chunk index), rids, then the inner rows
+    for (uint32_t i = t; i < nr; i += BPR_T) {
+      const uint32_t r = Rr[rb + i], f = a.Rhi[rb + i];
+      ridL[i] = r;
+      uint32_t h = hash32(f, tbits);
+      while (atomicCAS(&fragT[h], EMPTY32, f) != EMPTY32) h = (h + 1) & mask;
+      idxT[h] = (uint16_t)i;
+    }
+    __syncthreads();
+    for (uint32_t i0 = t; i0 < 2 * nr; i0 += 4 * BPR_T) {  // 4 independent 16-byte loads per thread
+      const uint32_t i1 = i0 + BPR_T, i2 = i0 + 2 * BPR_T, i3 = i0 + 3 * BPR_T;
+      ulonglong2 x0, x1, x2, x3;
+      x0 = a.rowsA[2 * ((uint64_t)ridL[i0 >> 1] - a.offA) + (i0 & 1)];
+      if (i1 < 2 * nr) x1 = a.rowsA[2 * ((uint64_t)ridL[i1 >> 1] - a.offA) + (i1 & 1)];
+      if (i2 < 2 * nr) x2 = a.rowsA[2 * ((uint64_t)ridL[i2 >> 1] - a.offA) + (i2 & 1)];
+      if (i3 < 2 * nr) x3 = a.rowsA[2 * ((uint64_t)ridL[i3 >> 1] - a.offA) + (i3 & 1)];
+      rowsL[i0] = x0;
+      if (i1 < 2 * nr) rowsL[i1] = x1;
+      if (i2 < 2 * nr) rowsL[i2] = x2;
+      if (i3 < 2 * nr) rowsL[i3] = x3;
+    }
+    __syncthreads();
+
+    // ---- probe + rows (the next batch's outer tuples are loaded while this
+    // batch's rows are gathered and written)
+    for (uint32_t b0 = 0; b0 < ns; b0 += BATCH) {
+      uint32_t found[BPR_K], first[BPR_K], incl[BPR_K];
+      uint32_t waveTotal = 0;
+#pragma unroll
+      for (int k = 0; k < BPR_K; ++k) {
+        const uint32_t i = b0 + k * BPR_T + t;
+        found[k] = 0;
+        first[k] = 0;
+        if (i < ns) {
+          uint32_t h = hash32(sf[k], tbits), e;
+          while ((e = fragT[h]) != EMPTY32) {
+            if (e == sf[k]) {
+              if (found[k] == 0) first[k] = idxT[h];
+              ++found[k];
+            }
+            h = (h + 1) & mask;
+          }
+        }
+        incl[k] = waveInclusiveScan<uint32_t>(found[k]);
+        waveTotal += __shfl(incl[k], WAVE - 1, WAVE);
+        matches += found[k];
+      }
+      uint32_t nsr[BPR_K], nsf[BPR_K];
+#pragma unroll
+      for (int k = 0; k < BPR_K; ++k) {
+        const uint32_t i = b0 + BATCH + k * BPR_T + t;
+        nsr[k] = i < ns ? Sr[sb + i] : 0u;
+        nsf[k] = i < ns ? (uint32_t)a.Shi[sb + i] : 0u;
+      }
+      unsigned long long base = 0;
+      if (lane == WAVE - 1 && waveTotal) base = itemBase + atomicAdd(&itemCursor, waveTotal);
+      base = __shfl(base, WAVE - 1, WAVE);
+      for (uint32_t w0 = 0; w0 < waveTotal; w0 += BPR_LIST) {  // wave-uniform; > 1 window only with duplicates
+        uint32_t kb = 0;
+#pragma unroll
+        for (int k = 0; k < BPR_K; ++k) {
+          const uint32_t r0 = kb + incl[k] - found[k];
+          if (found[k] && r0 < w0 + BPR_LIST && r0 + found[k] > w0) {
+            if (r0 >= w0) list[r0 - w0] = make_uint2(first[k], sr[k]);
+            if (found[k] > 1) {  // duplicate inner keys: the chain's other matches
+              uint32_t h = hash32(sf[k], tbits), e, j = 0;
+              while ((e = fragT[h]) != EMPTY32) {
+                if (e == sf[k]) {
+                  if (j && r0 + j >= w0 && r0 + j < w0 + BPR_LIST) list[r0 + j - w0] = make_uint2(idxT[h], sr[k]);
+                  ++j;
+                }
+                h = (h + 1) & mask;
+              }
+            }
+          }
+          kb += __shfl(incl[k], WAVE - 1, WAVE);
+        }
+        waveSync();
+        bprEmitWindow(a, list, rowsL, ridL, min(BPR_LIST, waveTotal - w0), base + w0, lane);
+        waveSync();
+      }
+#pragma unroll
+      for (int k = 0; k < BPR_K; ++k) {
+        sr[k] = nsr[k];
+        sf[k] = nsf[k];
+      }
+    }
+    __syncthreads();  // the next item rebuilds the table, rows and cursor
+  }
+  const unsigned long long total = blockReduceSum<BPR_T, unsigned long long>((unsigned long long)matches, wsum);
   if (t == 0 && total) atomicAdd(a.result, total);
 }
 
@@ -870,10 +1185,27 @@ void buildProbe(const BPArgs &args, const BPItem *items, const uint32_t *nItems,
   }
   if (a.split) {  // materialize
     const size_t ldsM = bpMatSplitLds(a);
-    HJ_CHECK(ldsM <= 160 * 1024, "buildProbe: LDS request %zu exceeds 160 KiB (rChunk=%u)", ldsM, a.rChunk);
-    const uint32_t perCuM = (uint32_t)std::min<size_t>(4, (160 * 1024) / ldsM);
+    const bool rows = a.outRows != nullptr;
+    const size_t stageBytes = rows ? (BPM_T / WAVE) * 5 * WAVE * sizeof(ulonglong2) : 0;  // 20 KiB
+    HJ_CHECK(ldsM + stageBytes <= 160 * 1024, "buildProbe: LDS request %zu exceeds 160 KiB (rChunk=%u)",
+             ldsM + stageBytes, a.rChunk);
+    const uint32_t perCuM = (uint32_t)std::min<size_t>(4, (160 * 1024) / (ldsM + stageBytes + 64));
     const uint32_t blocksM = std::min<uint32_t>(capacity, 256 * std::max<uint32_t>(perCuM, 1));
-    hipLaunchKernelGGL(bpMatSplitKernel, dim3(blocksM), dim3(BPM_T), ldsM, s, a, items, nItems, capacity);
+    if (rows) HJ_CHECK(a.rowsA && a.rowsB && a.itemOffsets, "buildProbe: row output needs payload columns and item offsets");
+    static const bool rowsLds = [] {
+      const char *e = std::getenv("HPCJOIN_ROWS_LDS");
+      return !e || std::atoi(e) != 0;
+    }();
+    if (rows && rowsLds && a.rChunk <= BPR_MAX_R) {
+      const size_t ldsR = bpMatRowsLds(a.rChunk);
+      const uint32_t perCuR = (uint32_t)std::max<size_t>(1, std::min<size_t>(3, (160 * 1024) / (ldsR + 16)));
+      const uint32_t blocksR = std::min<uint32_t>(capacity, 256 * perCuR);
+      hipLaunchKernelGGL(bpMatRowsKernel, dim3(blocksR), dim3(BPR_T), ldsR, s, a, items, nItems, capacity);
+    } else if (rows) {
+      hipLaunchKernelGGL(bpMatSplitKernel<true>, dim3(blocksM), dim3(BPM_T), ldsM, s, a, items, nItems, capacity);
+    } else {
+      hipLaunchKernelGGL(bpMatSplitKernel<false>, dim3(blocksM), dim3(BPM_T), ldsM, s, a, items, nItems, capacity);
+    }
     HIP_CHECK_LAUNCH();
     return;
   }

@@ -279,6 +279,22 @@ struct BPArgs {
   // atomic per wave (measured 9.4M of them at 600M pairs).
   uint32_t *itemCounts = nullptr;
   const unsigned long long *itemOffsets = nullptr;
+  // Fused row output (materialize pass of the split layout, both payload
+  // columns local): whole 80-byte rows [rid_inner, rid_outer, inner row,
+  // outer row] go to outRows (outCapacity rows) instead of pairs to outPairs.
+  const ulonglong2 *rowsA = nullptr;  // inner payload rows, 2 x 16 B each
+  const ulonglong2 *rowsB = nullptr;  // outer payload rows
+  uint64_t offA = 0, offB = 0;        // rid of row 0 of each column
+  ulonglong2 *outRows = nullptr;
+};
+// Payload columns + output of a fused materializing join (HashJoin::setRowSink).
+struct RowSink {
+  const uint64_t *rowsA = nullptr;
+  uint64_t offA = 0;
+  const uint64_t *rowsB = nullptr;
+  uint64_t offB = 0;
+  uint64_t *out = nullptr;  // [capacity][10] u64
+  uint64_t capacity = 0;
 };
 size_t bpLdsBytes(const BPArgs &a);
 void bpPlanCounts(const BPArgs &a, uint32_t *counts, hipStream_t s);

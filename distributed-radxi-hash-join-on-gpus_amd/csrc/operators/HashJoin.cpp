@@ -283,6 +283,10 @@ void HashJoin::join() {
   RESULT_COUNTER = result.localMatches;
 }
 
+bool HashJoin::canFuseRows() const {
+  return ctx->onDevice() && ctx->comm()->size() == 1 && plan.materialize && plan.splitLocal && !plan.wide;
+}
+
 JoinResult HashJoin::run() {
   try {
     return runImpl();
@@ -561,6 +565,7 @@ JoinResult HashJoin::runImpl() {
         if (c + 1 == outerChunks && dev) HIP_CHECK(hipEventRecord(ev[3], ctx->stream()));
         if (c == 0) utils::faultPoint("build_probe");
         bps.emplace_back(new tasks::BuildProbe(innerWindow, outerViews.back().get(), ctx, plan, config.outputCapacity));
+        if (hasSink && canFuseRows()) bps.back()->setRowSink(&sink);
         bps.back()->execute();
       }
       result.localItems = lp->workItems();
@@ -580,6 +585,7 @@ JoinResult HashJoin::runImpl() {
           if (dev) HIP_CHECK(hipEventRecord(ev[3], ctx->stream()));
           result.localItems = lp->workItems();
           bps.emplace_back(new tasks::BuildProbe(innerWindow, outerWindow, ctx, plan, config.outputCapacity));
+          if (hasSink && canFuseRows()) bps.back()->setRowSink(&sink);
           TASK_QUEUE.push(bps.back().get());
         }
       }
@@ -601,6 +607,7 @@ JoinResult HashJoin::runImpl() {
       lp->execute();
       result.localItems = lp->workItems();
       bps.emplace_back(new tasks::BuildProbe(innerWindow, outerWindow, ctx, plan, config.outputCapacity));
+      if (hasSink && canFuseRows()) bps.back()->setRowSink(&sink);
       bps.back()->execute();
       if (dev) HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
       ctx->synchronize();
@@ -627,6 +634,7 @@ JoinResult HashJoin::runImpl() {
   result.outputPairs =
       plan.materialize && !bps.empty() ? std::min<uint64_t>(bps.front()->getOutputCount(), UINT64_MAX) : 0;
   result.outputOverflow = !bps.empty() && bps.front()->outputOverflowed();
+  result.rowsFused = !bps.empty() && bps.front()->rowsFused();
   output = bps.empty() ? nullptr : bps.front()->getOutput();
   bps.clear();
   outerViews.clear();

@@ -33,6 +33,7 @@ struct JoinResult {
   uint64_t globalMatches = 0;
   uint64_t outputPairs = 0;        // materialize: pairs written on this rank
   bool outputOverflow = false;
+  bool rowsFused = false;          // materialize: whole rows went to the RowSink (no pair array)
   uint32_t reruns = 0;             // build/probe re-launches after an item/output overflow
   double joinMs = 0;               // host wall: histogram start -> local result available
   double histogramMs = 0, windowMs = 0, networkMs = 0, localMs = 0;  // host phases
@@ -73,6 +74,13 @@ class HashJoin {
   // Materialized (rid_inner, rid_outer) pairs of the last run, in ctx memory
   // (valid until the next run on this context).
   const ulonglong2 *getOutput() const { return output; }
+  // Fused materialization: while a sink is set, a device join at N = 1 over
+  // the split layout writes whole output rows (LateMaterialization's layout)
+  // from its materialize pass instead of pairs.  canFuseRows() says whether
+  // this plan does; the caller keeps the sink's buffers alive over run().
+  bool canFuseRows() const;
+  void setRowSink(const kernels::RowSink &s) { sink = s; hasSink = true; }
+  void clearRowSink() { hasSink = false; }
 
  protected:
   uint32_t numberOfNodes;
@@ -102,6 +110,8 @@ class HashJoin {
   core::JoinPlan basePlan;         // two-level plan (what a bitmap plan falls back to)
   bool bitmapExact = false;        // bitmap plan: exact histograms (small inputs, or after an overflow)
   const ulonglong2 *output = nullptr;
+  kernels::RowSink sink;
+  bool hasSink = false;
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
 };
 

@@ -82,7 +82,17 @@ void BuildProbe::execute() {
   configure();
   const bool dev = ctx->onDevice();
   memory::Arena &ws = ctx->workspace();
-  if (plan.materialize) {
+  fused = plan.materialize && sink && dev && args.split;
+  if (fused) {
+    outputCapacity = sink->capacity;
+    outPairs = nullptr;
+    args.outRows = reinterpret_cast<ulonglong2 *>(sink->out);
+    args.rowsA = reinterpret_cast<const ulonglong2 *>(sink->rowsA);
+    args.rowsB = reinterpret_cast<const ulonglong2 *>(sink->rowsB);
+    args.offA = sink->offA;
+    args.offB = sink->offB;
+    args.outCapacity = outputCapacity;
+  } else if (plan.materialize) {
     if (outputCapacity == 0) outputCapacity = outerPartitionSize + 1024;
     outPairs = static_cast<ulonglong2 *>(ws.get(outputCapacity * sizeof(ulonglong2)));
     args.outPairs = outPairs;
@@ -180,8 +190,12 @@ bool BuildProbe::collect() {
     again = true;
   }
   if (plan.materialize && outputCount > outputCapacity) {
-    outputCapacity = outputCount;
-    again = true;
+    if (fused) {
+      overflowOut = true;  // the sink is the caller's: it re-runs with a larger one
+    } else {
+      outputCapacity = outputCount;
+      again = true;
+    }
   }
   return again;
 }

@@ -45,6 +45,11 @@ class BuildProbe : public Task {
   uint32_t getWorkItems() const { return workItems; }
   const ulonglong2 *getOutput() const { return outPairs; }
   bool outputOverflowed() const { return overflowOut; }
+  // Fused row output (device, split layout): the materialize pass writes whole
+  // rows to the sink.  A sink overflow is reported, not re-run (the caller
+  // owns the buffer).
+  void setRowSink(const kernels::RowSink *s) { sink = s; }
+  bool rowsFused() const { return fused; }
 
  protected:
   uint64_t innerPartitionSize;
@@ -66,7 +71,8 @@ class BuildProbe : public Task {
   std::vector<uint64_t> refBounds;  // reference ctor: partition begin arrays
   uint64_t matches = 0, outputCount = 0;
   uint32_t workItems = 0;
-  bool reference = false, overflowOut = false;
+  bool reference = false, overflowOut = false, fused = false;
+  const kernels::RowSink *sink = nullptr;
   uint64_t hostCursor = 0;
 };
 

@@ -341,6 +341,53 @@ def test_materialize_split_duplicates(C, cuda, r_chunk):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("r_chunk,cap", [(0, 0), (512, 1000), (2048, 0)])
+def test_fused_row_materialization(C, cuda, r_chunk, cap):
+    """join_materialized at N = 1: the split layout's materialize pass writes
+    whole 80-byte rows (bpMatRowsKernel for inner chunks <= 1024, else
+    bpMatSplitKernel<true>).  16 duplicates of every inner
+    key (windows of more than 64 rows per wave), Zipf outer; the rows equal
+    those of run() + materialize_payloads as a multiset, and a capacity that is
+    too small (cap=1000) is re-run exactly sized."""
+    import torch
+    G_R, G_S = 160_000, 300_000
+    ctx = C.ExecContext("device", 0, C.LocalCommunicator())
+    inner = C.GenSpec(distribution=C.KeyDistribution.MODULO, seed=91, domain=G_R // 16)
+    outer = C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=92, domain=G_R // 8, zipf_theta=0.5)
+    R = C.Relation(G_R, G_R, "device", 0)
+    S = C.Relation(G_S, G_S, "device", 0)
+    R.generate(inner, 0)
+    S.generate(outer, 0)
+    rows_a = C.ops.generate_payload(G_R, 0, 0x51, "cuda:0")
+    rows_b = C.ops.generate_payload(G_S, 0, 0x52, "cuda:0")
+    cfg = C.JoinConfig()
+    cfg.materialize = True
+    cfg.r_chunk = r_chunk
+    cfg.output_capacity = cap
+    j = C.HashJoin(R, S, ctx, cfg)
+    assert j.can_fuse_rows
+    res, rows = j.join_materialized(ctx, rows_a, 0, G_R, rows_b, 0, G_S)
+    Rt, St = R.to_tensor().cpu(), S.to_tensor().cpu()
+    dom = int(max(Rt[:, 0].max(), St[:, 0].max())) + 1
+    exp = int((torch.bincount(Rt[:, 0], minlength=dom) * torch.bincount(St[:, 0], minlength=dom)).sum())
+    assert res["rows_fused"] and not res["output_overflow"]
+    assert res["global_matches"] == exp == res["output_pairs"] == rows.shape[0]
+    cfg2 = C.JoinConfig()
+    cfg2.materialize = True
+    cfg2.r_chunk = r_chunk
+    j2 = C.HashJoin(R, S, ctx, cfg2)
+    res2 = j2.run()
+    assert not res2["rows_fused"]
+    ref = j2.materialize_payloads(ctx, rows_a, 0, G_R, rows_b, 0, G_S)
+
+    def canon(t):
+        t = t.cpu()
+        return t[torch.argsort(t[:, 0] * G_S + t[:, 1])]
+
+    assert torch.equal(canon(rows), canon(ref))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dist", ["UNIQUE", "UNIFORM", "ZIPF"])
 def test_bitmap_join(C, cuda, dist):
     """Single-level bitmap join (N == 1, counting, sampled network pass): one

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--sf-per-gpu", type=float, default=100.0)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--unfused", action="store_true",
+                    help="join, then a separate late-materialization pass (the N>1 path) even at N=1")
     args = ap.parse_args()
     hpcjoin.require_native()
     info = init_distributed()
@@ -37,7 +39,7 @@ def main():
     if not torch.cuda.is_available():
         sf = min(sf, 0.01)
     wl = W.get("tpch_sf1000").scaled(sf / 1000.0)
-    t = TpchJoin(wl, info=info)
+    t = TpchJoin(wl, info=info, fused=not args.unfused)
     for _ in range(args.warmup):
         t.run()
     t.ctx.reset_scratch()  # arena grown to the warmup peak before timing
@@ -66,7 +68,7 @@ def main():
             "output_rows_local": int(out.shape[0]), "output_bytes_per_row": int(out.shape[1]) * 8,
             "median_total_ms": tot, "median_join_ms": sorted(join_ms)[len(join_ms) // 2],
             "median_materialize_ms": sorted(mat_ms)[len(mat_ms) // 2],
-            "matches": int(res["global_matches"]), "correct": bool(ok),
+            "matches": int(res["global_matches"]), "correct": bool(ok), "rows_fused": bool(res["rows_fused"]),
             "phases_ms": {k: round(res[k], 3) for k in ("histogram_ms", "network_ms", "local_ms", "dev_histogram_ms",
                                                          "dev_network_ms", "dev_local_partition_ms",
                                                          "dev_build_probe_ms", "setup_ms")},
