@@ -185,6 +185,25 @@ void Window::enableOneSided() {
   oneSidedComplete = false;
 }
 
+std::vector<uint64_t> Window::directDigitBase() const {
+  JOIN_ASSERT(oneSided && assignment, "Window", "direct scatter needs a one-sided window with an assignment");
+  const uint32_t N = plan.numberOfNodes, C = plan.chunks, F = plan.partitions;
+  const uint64_t tb = tupleBytes();
+  const uint32_t *owner = assignment->getPartitionAssignment();
+  std::vector<uint64_t> db((size_t)C * F, 0);
+  for (uint32_t c = 0; c < C; ++c)
+    for (uint32_t p = 0; p < F; ++p) {
+      // The owner lays out source me's chunk-c runs exactly as my send buffer
+      // does for that destination: same partitions, same order, same counts.
+      const uint32_t d = owner[p];
+      const uint64_t within = plan.digitBase[(size_t)c * F + p] - plan.sendDispls[(size_t)c * N + d];
+      const uintptr_t addr = (uintptr_t)peerBase[d] + (peerOffset[(size_t)d * C + c] + within) * tb;
+      JOIN_ASSERT(addr % tb == 0, "Window", "peer window misaligned for %lu-byte tuples", (unsigned long)tb);
+      db[(size_t)c * F + p] = addr / tb;
+    }
+  return db;
+}
+
 // This rank's runs of chunk c, each copied into its owner's window at the
 // owner's receive displacement for (c, this rank) -- MPI_Put at an exact,
 // disjoint offset.  Device: peer copies on the exchange stream once the
@@ -192,6 +211,13 @@ void Window::enableOneSided() {
 void Window::putChunk(const void *send, uint32_t chunk) {
   const uint32_t N = plan.numberOfNodes, me = plan.nodeId, C = plan.chunks;
   const uint64_t tb = tupleBytes();
+  if (directScatter()) {  // the scatter kernel already wrote the runs into the owners' windows
+    for (uint32_t p = 0; p < N; ++p)
+      if (p != me) wireSent += plan.sendCounts[(size_t)chunk * N + p] * tb / 8;
+    HIP_CHECK(hipEventRecord(done[chunk], ctx->stream()));
+    performance::Measurements::add("MWINPUTCNT", 1, "calls");
+    return;
+  }
   const uint8_t *src = static_cast<const uint8_t *>(send);
   const bool dev = ctx->onDevice();
   if (dev) {
@@ -267,7 +293,8 @@ void Window::stop() {
   if (oneSided) {
     if (!oneSidedComplete) {
       // unlock_all + barrier: my puts have landed, then everyone's have.
-      if (ctx->onDevice()) utils::waitStream(ctx->commStream(), ctx->comm(), "one-sided puts");
+      if (ctx->onDevice())
+        utils::waitStream(directScatter() ? ctx->stream() : ctx->commStream(), ctx->comm(), "one-sided puts");
       ctx->comm()->barrier();
       oneSidedComplete = true;
       performance::Measurements::add("MWINWAITCNT", 1, "calls");

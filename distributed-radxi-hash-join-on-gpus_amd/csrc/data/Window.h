@@ -60,6 +60,13 @@ class Window {
   // RCCL call, no staging through a second buffer on the receiver.
   void enableOneSided();
   bool isOneSided() const { return oneSided; }
+  // Device one-sided windows: the network scatter writes every run straight
+  // into its owner's window (no local send buffer, no copy afterwards).
+  // directDigitBase() gives, per (chunk, partition), the absolute tuple index
+  // (address / tuple bytes) of the run's first slot in the owner's window --
+  // the scatter's cursors then address peer memory from a null base.
+  bool directScatter() const { return oneSided && ctx->onDevice(); }
+  std::vector<uint64_t> directDigitBase() const;
   // Bit-pack tuples on the wire (kernels.h, WireCodec); ridBase[rank * C + c]
   // is the rid base of sender `rank`'s chunk c (C = ridBase.size() / ranks).
   // Call before the first exchange.

@@ -49,7 +49,9 @@ void NetworkPartitioning::partition(data::Relation *relation, data::Window *wind
   const char *kMain = isInner ? "MIMAINPART" : "MOMAINPART";
   const char *kFlush = isInner ? "MIFLUSHPART" : "MOFLUSHPART";
   const uint64_t tAlloc = performance::nowUs();
-  void *send = single ? window->getData() : ctx->workspace().get(n * tb);
+  // One-sided device windows take the scatter's stores directly: no send buffer.
+  const bool direct = !single && window->directScatter();
+  void *send = single ? window->getData() : direct ? nullptr : ctx->workspace().get(n * tb);
   performance::Measurements::add(isInner ? "MIMEMALLOC" : "MOMEMALLOC", (double)(performance::nowUs() - tAlloc), "us");
   window->start();
   const kernels::KeyMix mix{plan.keyMix ? 1u : 0u, plan.keyBits};
@@ -58,20 +60,27 @@ void NetworkPartitioning::partition(data::Relation *relation, data::Window *wind
   if (ctx->onDevice()) {
     // Claim-mode scatter: per-(chunk, XCD group, digit) slices, one device
     // atomic per digit per 8192-tuple tile (kernels.h, CLAIM_GROUPS).
-    const bool narrow = kernels::cursorsNarrow(n);
+    // Direct scatter: cursors are absolute tuple indices (8 bytes wide).
+    const bool narrow = !direct && kernels::cursorsNarrow(n);
     const uint64_t cb = narrow ? 4 : 8, perChunk = (uint64_t)kernels::CLAIM_GROUPS * F * cb;
     uint8_t *gcur = static_cast<uint8_t *>(ctx->workspace().get(chunks * perChunk));
     uint64_t *base = ctx->workspace().getArray<uint64_t>((uint64_t)chunks * F);
-    ctx->copy(base, xp.digitBase.data(), xp.digitBase.size() * 8, true, false);
+    if (direct) {
+      const std::vector<uint64_t> db = window->directDigitBase();
+      ctx->copy(base, db.data(), db.size() * 8, true, false);
+    } else {
+      ctx->copy(base, xp.digitBase.data(), xp.digitBase.size() * 8, true, false);
+    }
     kernels::netGroupCursors(local->blockHistogram(), F, g.blocks, bpc, base, gcur, narrow, ctx->stream());
     for (uint32_t c = 0; c < chunks; ++c) {
       const uint32_t b0 = c * bpc, b1 = std::min(g.blocks, b0 + bpc);
+      const int narrowMode = narrow ? 1 : 0;
       if (plan.wide)
         kernels::netScatterWide(relation->getData(), n, bits, g, b0, b1, gcur + c * perChunk,
-                                static_cast<data::Tuple *>(send), ctx->stream(), mix);
+                                static_cast<data::Tuple *>(send), ctx->stream(), mix, nullptr, narrowMode);
       else
         kernels::netScatter(relation->getData(), n, bits, plan.keyShift, g, b0, b1, gcur + c * perChunk,
-                            static_cast<uint64_t *>(send), ctx->stream(), plan.keyBits, mix, nullptr, -1,
+                            static_cast<uint64_t *>(send), ctx->stream(), plan.keyBits, mix, nullptr, narrowMode,
                             !plan.keyOnly);
       if (!single) window->exchange(send, c);
       if (afterChunk) afterChunk(c);

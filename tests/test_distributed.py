@@ -16,7 +16,7 @@ import pytest
 from conftest import ROOT, devices
 
 
-def run_ranks(C, n_ranks, loc, G_R, G_S, cfg_fn=None, outer_dist="UNIQUE", theta=0.75, outputs=None):
+def run_ranks(C, n_ranks, loc, G_R, G_S, cfg_fn=None, outer_dist="UNIQUE", theta=0.75, outputs=None, peaks=None):
     group = C.InProcessGroup(n_ranks)
     inner = C.GenSpec(seed=1234)
     outer = C.GenSpec(distribution=getattr(C.KeyDistribution, outer_dist), seed=4321,
@@ -41,6 +41,8 @@ def run_ranks(C, n_ranks, loc, G_R, G_S, cfg_fn=None, outer_dist="UNIQUE", theta
             results[r] = (res, j.plan)
             if outputs is not None:
                 outputs[r] = j.output()
+            if peaks is not None:
+                peaks[r] = ctx.workspace_peak()
         except Exception as e:  # surface in the main thread
             errors.append((r, repr(e)))
 
@@ -299,13 +301,16 @@ def test_rccl_multiprocess_shared_gpu(world):
 @pytest.mark.parametrize("dev", devices())
 @pytest.mark.parametrize("n_ranks,chunks,opts", [(2, 1, ""), (3, 3, "mat"), (4, 2, "wide"), (8, 1, "")])
 def test_one_sided_exchange(C, dev, n_ranks, chunks, opts):
-    """The MPI_Put analog (JoinConfig.exchange = ONE_SIDED): every rank copies
-    its runs straight into the owners' windows at their exact offsets, then a
-    barrier; counts (and materialized pairs) equal the RCCL / two-sided path."""
+    """The MPI_Put analog (JoinConfig.exchange = ONE_SIDED): every rank writes
+    its runs straight into the owners' windows at their exact offsets (device:
+    the network scatter stores into the peers' windows, no send buffer; host:
+    copies), then a barrier; counts (and materialized pairs) equal the RCCL /
+    two-sided path, and on the device the workspace peak is smaller."""
     import torch
-    got = {}
+    got, peak = {}, {}
     for mode in ("ONE_SIDED", "RCCL"):
         pairs = [None] * n_ranks
+        peaks = [0] * n_ranks
 
         def cfg_fn(c, mode=mode):
             c.exchange = getattr(C.ExchangeMode, mode)
@@ -315,7 +320,9 @@ def test_one_sided_exchange(C, dev, n_ranks, chunks, opts):
             if opts == "wide":
                 c.format = C.TupleFormat.WIDE
         results, exp = run_ranks(C, n_ranks, "device" if dev == "cuda" else "host", 300_007, 500_009, cfg_fn=cfg_fn,
-                                 outer_dist="ZIPF", theta=0.8, outputs=pairs if opts == "mat" else None)
+                                 outer_dist="ZIPF", theta=0.8, outputs=pairs if opts == "mat" else None,
+                                 peaks=peaks)
+        peak[mode] = sum(peaks)
         for res, plan in results:
             assert plan.one_sided == (mode == "ONE_SIDED")
             assert res["global_matches"] == exp
@@ -324,5 +331,7 @@ def test_one_sided_exchange(C, dev, n_ranks, chunks, opts):
             p = torch.cat([x.cpu() for x in pairs])
             got[mode + "pairs"] = p[torch.argsort(p[:, 1] * (1 << 32) + p[:, 0])]
     assert got["ONE_SIDED"] == got["RCCL"]
+    if dev == "cuda":
+        assert peak["ONE_SIDED"] < peak["RCCL"], peak
     if opts == "mat":
         assert torch.equal(got["ONE_SIDEDpairs"], got["RCCLpairs"])
