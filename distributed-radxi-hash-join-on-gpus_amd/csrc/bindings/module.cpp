@@ -517,6 +517,7 @@ py::dict resultToDict(const operators::JoinResult &r) {
   d["output_pairs"] = r.outputPairs;
   d["output_overflow"] = r.outputOverflow;
   d["rows_fused"] = r.rowsFused;
+  d["split_partitions"] = r.splitPartitions;
   d["reruns"] = r.reruns;
   d["sampled_network"] = r.sampledNetwork;
   d["network_fallbacks"] = r.networkFallbacks;
@@ -610,6 +611,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("sample_stride", &core::JoinConfig::sampleStride)
       .def_readwrite("wire_codec", &core::JoinConfig::wireCodec)
       .def_readwrite("split_local", &core::JoinConfig::splitLocal)
+      .def_readwrite("skew_split", &core::JoinConfig::skewSplit)
       .def_readwrite("direct_count", &core::JoinConfig::directCount)
       .def_readwrite("bitmap_join", &core::JoinConfig::bitmapJoin)
       .def_readwrite("replicate_bitmap", &core::JoinConfig::replicateBitmap)
@@ -648,6 +650,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("frag_shift", &core::JoinPlan::fragShift)
       .def_readonly("key_bits", &core::JoinPlan::keyBits)
       .def_readonly("split_local", &core::JoinPlan::splitLocal)
+      .def_readonly("skew_split", &core::JoinPlan::skewSplit)
       .def_property_readonly("wire_bits", [](const core::JoinPlan &p) {
         return std::vector<uint32_t>{p.wireBits[0], p.wireBits[1]};
       })

@@ -39,6 +39,7 @@ JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t global
   p.localItemTiles = std::max<uint32_t>(1, std::min<uint32_t>(cfg.localItemTiles, 1024));
   p.localGeometry = cfg.localGeometry;
   p.assignment = cfg.assignment;
+  p.skewSplit = cfg.skewSplit && cfg.assignment == AssignmentPolicy::LPT && numberOfNodes > 1;
   p.chunks = std::max<uint32_t>(1, cfg.chunks);
   p.localHistogram = cfg.localHistogram;
   p.sampleStride = std::max<uint32_t>(1, cfg.sampleStride);

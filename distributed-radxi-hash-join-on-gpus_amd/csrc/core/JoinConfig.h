@@ -88,6 +88,10 @@ struct JoinConfig {
   uint32_t localSampleStride = 16;  // sampled local pass: 1 tile in localSampleStride of every work item
   WireCodecMode wireCodec = WireCodecMode::Auto;
   bool splitLocal = true;       // device: split local pass output (u32 rid + u16 fragment columns) when they fit
+  // N > 1, LPT: a network partition above one rank's fair share of |R| + |S|
+  // is joined by several ranks (larger side divided, smaller replicated;
+  // histograms/AssignmentMap).
+  bool skewSplit = true;
   bool directCount = true;      // count-only build/probe: direct-addressed LDS counts when fragments are <= 13 bits
   bool splitHistogram = true;   // N > 1 on device: outer exact histogram overlaps the inner exchange
   bool pipelineOuter = true;    // N > 1 on device, counting: outer local pass + build/probe per received chunk
@@ -148,6 +152,7 @@ struct JoinPlan {
   // rid bits, and the rid base of every (rank, exchange chunk), rank-major.
   // Set by HashJoin::planWireCodec.
   bool splitLocal = false;    // local pass writes split columns (kernels.h, SplitLayout)
+  bool skewSplit = false;     // hot network partitions may be split across ranks
   bool directCount = true;    // build/probe may use direct-addressed count tables
   uint32_t localItemTiles = 64;
   uint32_t localGeometry = 0;

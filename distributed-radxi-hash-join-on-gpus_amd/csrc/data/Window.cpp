@@ -189,13 +189,13 @@ std::vector<uint64_t> Window::directDigitBase() const {
   JOIN_ASSERT(oneSided && assignment, "Window", "direct scatter needs a one-sided window with an assignment");
   const uint32_t N = plan.numberOfNodes, C = plan.chunks, F = plan.partitions;
   const uint64_t tb = tupleBytes();
-  const uint32_t *owner = assignment->getPartitionAssignment();
+  JOIN_ASSERT(plan.replicas.empty(), "Window", "replicated runs need a send buffer");
   std::vector<uint64_t> db((size_t)C * F, 0);
   for (uint32_t c = 0; c < C; ++c)
     for (uint32_t p = 0; p < F; ++p) {
-      // The owner lays out source me's chunk-c runs exactly as my send buffer
-      // does for that destination: same partitions, same order, same counts.
-      const uint32_t d = owner[p];
+      // The destination lays out source me's chunk-c runs exactly as my send
+      // buffer does for it: same partitions, same order, same counts.
+      const uint32_t d = plan.digitDest[(size_t)c * F + p];
       const uint64_t within = plan.digitBase[(size_t)c * F + p] - plan.sendDispls[(size_t)c * N + d];
       const uintptr_t addr = (uintptr_t)peerBase[d] + (peerOffset[(size_t)d * C + c] + within) * tb;
       JOIN_ASSERT(addr % tb == 0, "Window", "peer window misaligned for %lu-byte tuples", (unsigned long)tb);
@@ -350,11 +350,15 @@ uint64_t Window::computeLocalWindowSize() { return plan.recvTotal; }
 
 uint64_t Window::computeWindowSize(uint32_t nodeId) {
   if (!globalHistogram) return nodeId == plan.nodeId ? plan.recvTotal : 0;
-  const uint32_t *owner = assignment->getPartitionAssignment();
-  const uint64_t *g = globalHistogram->getGlobalHistogram();
+  const int side = assignment->sideOf(globalHistogram);
+  const uint32_t C = globalHistogram->getChunkCount();
   uint64_t s = 0;
-  for (uint32_t p = 0; p < plan.partitions; ++p)
-    if (owner[p] == nodeId) s += g[p];
+  for (uint32_t p = 0; p < plan.partitions; ++p) {
+    if (!assignment->owns(p, nodeId)) continue;
+    for (uint32_t r = 0; r < plan.numberOfNodes; ++r)
+      for (uint32_t c = 0; c < C; ++c)
+        if (assignment->receives(side, r, c, C, p, nodeId)) s += globalHistogram->rankCount(r, c, p);
+  }
   return s;
 }
 

@@ -65,7 +65,8 @@ class Window {
   // directDigitBase() gives, per (chunk, partition), the absolute tuple index
   // (address / tuple bytes) of the run's first slot in the owner's window --
   // the scatter's cursors then address peer memory from a null base.
-  bool directScatter() const { return oneSided && ctx->onDevice(); }
+  // (Not with replicated runs of split hot partitions: those need a send buffer.)
+  bool directScatter() const { return oneSided && ctx->onDevice() && plan.replicas.empty(); }
   std::vector<uint64_t> directDigitBase() const;
   // Bit-pack tuples on the wire (kernels.h, WireCodec); ridBase[rank * C + c]
   // is the rid base of sender `rank`'s chunk c (C = ridBase.size() / ranks).

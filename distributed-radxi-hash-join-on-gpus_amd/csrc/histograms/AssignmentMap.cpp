@@ -23,6 +23,9 @@ void AssignmentMap::computePartitionAssignment() {
   const uint64_t *s = outerRelationGlobalHistogram->getGlobalHistogram();
   assignment.assign(F, 0);
   loads.assign(numberOfNodes, 0);
+  helpers.assign(F, {});
+  splitSide.assign(F, 0);
+  nSplit = 0;
   if (pol == core::AssignmentPolicy::RoundRobin) {
     for (uint32_t p = 0; p < F; ++p) {
       assignment[p] = p % numberOfNodes;
@@ -34,7 +37,28 @@ void AssignmentMap::computePartitionAssignment() {
   std::iota(order.begin(), order.end(), 0u);
   std::stable_sort(order.begin(), order.end(),
                    [&](uint32_t a, uint32_t b) { return r[a] + s[a] > r[b] + s[b]; });
+  uint64_t total = 0;
+  for (uint32_t p = 0; p < F; ++p) total += r[p] + s[p];
+  const uint64_t fair = total / numberOfNodes;
   for (uint32_t p : order) {
+    const uint64_t load = r[p] + s[p];
+    const uint64_t big = std::max(r[p], s[p]), small = std::min(r[p], s[p]);
+    if (split && numberOfNodes > 1 && fair > 0 && load > fair && big > small) {
+      // Hot partition: k = ceil(load / fair) helpers (at least 2), the least
+      // loaded ranks (ties: lowest id).
+      const uint32_t k = (uint32_t)std::min<uint64_t>(numberOfNodes, std::max<uint64_t>(2, (load + fair - 1) / fair));
+      std::vector<uint32_t> byLoad(numberOfNodes);
+      std::iota(byLoad.begin(), byLoad.end(), 0u);
+      std::stable_sort(byLoad.begin(), byLoad.end(), [&](uint32_t a, uint32_t b) { return loads[a] < loads[b]; });
+      std::vector<uint32_t> h(byLoad.begin(), byLoad.begin() + k);
+      std::sort(h.begin(), h.end());
+      for (uint32_t n : h) loads[n] += small + (big + k - 1) / k;
+      assignment[p] = h[0];
+      splitSide[p] = s[p] >= r[p] ? 1 : 0;
+      helpers[p] = std::move(h);
+      ++nSplit;
+      continue;
+    }
     uint32_t best = 0;
     for (uint32_t n = 1; n < numberOfNodes; ++n)
       if (loads[n] < loads[best]) best = n;
@@ -44,6 +68,19 @@ void AssignmentMap::computePartitionAssignment() {
 }
 
 uint32_t *AssignmentMap::getPartitionAssignment() { return assignment.data(); }
+
+bool AssignmentMap::receives(int side, uint32_t source, uint32_t chunk, uint32_t chunks, uint32_t p,
+                             uint32_t node) const {
+  if (!isSplit(p)) return assignment[p] == node;
+  const std::vector<uint32_t> &h = helpers[p];
+  if (side == splitSide[p]) return h[((uint64_t)source * chunks + chunk) % h.size()] == node;
+  return std::binary_search(h.begin(), h.end(), node);
+}
+
+bool AssignmentMap::owns(uint32_t p, uint32_t node) const {
+  if (!isSplit(p)) return assignment[p] == node;
+  return std::binary_search(helpers[p].begin(), helpers[p].end(), node);
+}
 
 }  // namespace histograms
 }  // namespace hpcjoin

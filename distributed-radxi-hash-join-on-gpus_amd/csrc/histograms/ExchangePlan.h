@@ -23,6 +23,14 @@ struct Segment {
   uint32_t source;
 };
 
+// A run the scatter writes once but that goes to several destinations (the
+// replicated side of a split hot partition, AssignmentMap): copied inside the
+// send buffer after the chunk's scatter.
+struct Replica {
+  uint32_t chunk;
+  uint64_t src, dst, len;  // send-buffer tuple offsets
+};
+
 struct ExchangePlan {
   uint32_t numberOfNodes = 1, nodeId = 0, partitions = 0, chunks = 1;
   std::vector<uint32_t> owned;        // lp -> partition id (ascending)
@@ -33,6 +41,9 @@ struct ExchangePlan {
   std::vector<uint64_t> recvCounts;   // [chunks][N]
   std::vector<uint64_t> recvDispls;   // [chunks][N]
   uint64_t sendTotal = 0, recvTotal = 0;
+  uint64_t scatterTotal = 0;          // tuples the scatter writes (sendTotal minus replicas)
+  std::vector<uint32_t> digitDest;    // [chunks][F] destination of the scattered (chunk, partition) run
+  std::vector<Replica> replicas;
   std::vector<uint64_t> partSize;     // [owned]
   std::vector<uint64_t> lpBase;       // [owned + 1]
   std::vector<Segment> segments;      // by lp, then chunk, then source

@@ -57,47 +57,72 @@ void OffsetMap::computeAbsolutePrivateOffsets() {
 void OffsetMap::computeExchangePlan() {
   const uint32_t N = numberOfProcesses, F = globalHistogram->getPartitionCount(),
                  C = globalHistogram->getChunkCount(), me = nodeId;
-  const uint32_t *owner = assignment->getPartitionAssignment();
+  const int side = assignment->sideOf(globalHistogram);
+  const AssignmentMap &am = *assignment;
   ExchangePlan &x = plan;
   x = ExchangePlan();
   x.numberOfNodes = N;
   x.nodeId = me;
   x.partitions = F;
   x.chunks = C;
+  // Partitions each rank joins: its own, plus the hot ones it helps with.
   std::vector<std::vector<uint32_t>> ownedBy(N);
-  for (uint32_t p = 0; p < F; ++p) ownedBy[owner[p]].push_back(p);
+  for (uint32_t p = 0; p < F; ++p)
+    for (uint32_t d = 0; d < N; ++d)
+      if (am.owns(p, d)) ownedBy[d].push_back(p);
   x.owned = ownedBy[me];
   x.localIndex.assign(F, -1);
   for (uint32_t lp = 0; lp < x.owned.size(); ++lp) x.localIndex[x.owned[lp]] = (int32_t)lp;
 
-  // send side
-  x.digitBase.assign((size_t)C * F, 0);
+  // send side: the scatter writes each (chunk, partition) run once, into the
+  // first destination that receives it; replicated runs are copied after.
+  constexpr uint64_t UNSET = ~0ull;
+  x.digitBase.assign((size_t)C * F, UNSET);
+  x.digitDest.assign((size_t)C * F, 0);
   x.sendCounts.assign((size_t)C * N, 0);
   x.sendDispls.assign((size_t)C * N, 0);
   uint64_t cur = 0;
-  for (uint32_t c = 0; c < C; ++c)
+  for (uint32_t c = 0; c < C; ++c) {
     for (uint32_t d = 0; d < N; ++d) {
       x.sendDispls[(size_t)c * N + d] = cur;
       for (uint32_t p : ownedBy[d]) {
-        x.digitBase[(size_t)c * F + p] = cur;
-        cur += globalHistogram->rankCount(me, c, p);
+        if (!am.receives(side, me, c, C, p, d)) continue;
+        const uint64_t n = globalHistogram->rankCount(me, c, p);
+        uint64_t &db = x.digitBase[(size_t)c * F + p];
+        if (db == UNSET) {
+          db = cur;
+          x.digitDest[(size_t)c * F + p] = d;
+          x.scatterTotal += n;
+        } else if (n) {
+          x.replicas.push_back(Replica{c, db, cur, n});
+        }
+        cur += n;
       }
       x.sendCounts[(size_t)c * N + d] = cur - x.sendDispls[(size_t)c * N + d];
     }
+    for (uint32_t p = 0; p < F; ++p) {
+      uint64_t &db = x.digitBase[(size_t)c * F + p];
+      JOIN_ASSERT(db != UNSET || globalHistogram->rankCount(me, c, p) == 0, "OffsetMap",
+                  "partition %u (chunk %u) has no destination", p, c);
+      if (db == UNSET) db = cur;  // empty run
+    }
+  }
   x.sendTotal = cur;
 
   // receive side
   const uint32_t owned = (uint32_t)x.owned.size();
   x.recvCounts.assign((size_t)C * N, 0);
   x.recvDispls.assign((size_t)C * N, 0);
-  std::vector<uint64_t> segStart((size_t)C * N * owned, 0);
+  std::vector<uint64_t> segStart((size_t)C * N * owned, 0), segLen((size_t)C * N * owned, 0);
   cur = 0;
   for (uint32_t c = 0; c < C; ++c)
     for (uint32_t s = 0; s < N; ++s) {
       x.recvDispls[(size_t)c * N + s] = cur;
       for (uint32_t lp = 0; lp < owned; ++lp) {
-        segStart[((size_t)c * N + s) * owned + lp] = cur;
-        cur += globalHistogram->rankCount(s, c, x.owned[lp]);
+        const size_t i = ((size_t)c * N + s) * owned + lp;
+        segStart[i] = cur;
+        segLen[i] = am.receives(side, s, c, C, x.owned[lp], me) ? globalHistogram->rankCount(s, c, x.owned[lp]) : 0;
+        cur += segLen[i];
       }
       x.recvCounts[(size_t)c * N + s] = cur - x.recvDispls[(size_t)c * N + s];
     }
@@ -108,9 +133,9 @@ void OffsetMap::computeExchangePlan() {
   for (uint32_t lp = 0; lp < owned; ++lp) {
     for (uint32_t c = 0; c < C; ++c)
       for (uint32_t s = 0; s < N; ++s) {
-        const uint64_t len = globalHistogram->rankCount(s, c, x.owned[lp]);
-        x.partSize[lp] += len;
-        if (len) x.segments.push_back(Segment{segStart[((size_t)c * N + s) * owned + lp], len, lp, c, s});
+        const size_t i = ((size_t)c * N + s) * owned + lp;
+        x.partSize[lp] += segLen[i];
+        if (segLen[i]) x.segments.push_back(Segment{segStart[i], segLen[i], lp, c, s});
       }
     x.lpBase[lp + 1] = x.lpBase[lp] + x.partSize[lp];
   }

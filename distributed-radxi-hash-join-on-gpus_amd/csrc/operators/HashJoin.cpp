@@ -542,6 +542,7 @@ JoinResult HashJoin::runImpl() {
   // -------------------------------------------------------------------- local
   Measurements::startLocalProcessingPreparations();
   trace.reset();  // roctx ranges nest: pop before the next push
+  result.splitPartitions = hc ? hc->assignmentMap()->splitPartitions() : 0;
   utils::faultPoint("local");
   trace.reset(new performance::TraceRange("local_processing"));
   // Every build/probe of this join (one, or one per outer chunk when pipelined).

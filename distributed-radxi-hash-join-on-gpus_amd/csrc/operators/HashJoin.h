@@ -48,6 +48,7 @@ struct JoinResult {
   bool sampledLocal = false;       // local pass sized from a sampled histogram
   bool bitmapJoin = false;         // single-level bitmap join counted the matches (no local pass)
   uint32_t localFallbacks = 0;     // sampled local pass overflowed -> exact re-run
+  uint32_t splitPartitions = 0;    // hot network partitions joined by several ranks (AssignmentMap)
 };
 
 // Achievable one-way bandwidth of one xGMI peer link (MI355X: 7 links of

@@ -27,6 +27,7 @@ HistogramComputation::HistogramComputation(uint32_t numberOfNodes, uint32_t node
   outerRelationGlobalHistogram.reset(new histograms::GlobalHistogram(outerRelationLocalHistogram.get(), ctx->comm()));
   assignment.reset(new histograms::AssignmentMap(numberOfNodes, innerRelationGlobalHistogram.get(),
                                                  outerRelationGlobalHistogram.get(), plan.assignment));
+  assignment->setSkewSplit(plan.skewSplit);
   innerOffsets.reset(new histograms::OffsetMap(numberOfNodes, nodeId, innerRelationLocalHistogram.get(),
                                                innerRelationGlobalHistogram.get(), assignment.get()));
   outerOffsets.reset(new histograms::OffsetMap(numberOfNodes, nodeId, outerRelationLocalHistogram.get(),

@@ -1,5 +1,8 @@
 #include "NetworkPartitioning.h"
 
+#include <algorithm>
+#include <cstring>
+
 #include "../host/HostOps.h"
 #include "../memory/Arena.h"
 #include "../performance/Clock.h"
@@ -38,8 +41,8 @@ void NetworkPartitioning::partition(data::Relation *relation, data::Window *wind
                                     histograms::LocalHistogram *local, const histograms::ExchangePlan &xp,
                                     const std::function<void(uint32_t)> &afterChunk) {
   const uint64_t n = relation->getLocalSize();
-  JOIN_ASSERT(xp.sendTotal == n, "NetworkPartitioning", "plan sends %lu of %lu tuples",
-              (unsigned long)xp.sendTotal, (unsigned long)n);
+  JOIN_ASSERT(xp.scatterTotal == n, "NetworkPartitioning", "plan scatters %lu of %lu tuples",
+              (unsigned long)xp.scatterTotal, (unsigned long)n);
   const uint32_t bits = plan.networkBits, F = 1u << bits;
   const kernels::PartitionGeometry &g = local->geometry();
   const uint32_t bpc = local->blocksPerChunk(), chunks = local->getChunkCount();
@@ -50,8 +53,20 @@ void NetworkPartitioning::partition(data::Relation *relation, data::Window *wind
   const char *kFlush = isInner ? "MIFLUSHPART" : "MOFLUSHPART";
   const uint64_t tAlloc = performance::nowUs();
   // One-sided device windows take the scatter's stores directly: no send buffer.
+  // Replicated runs (split hot partitions) are copied inside a send buffer.
   const bool direct = !single && window->directScatter();
-  void *send = single ? window->getData() : direct ? nullptr : ctx->workspace().get(n * tb);
+  void *send = single ? window->getData() : direct ? nullptr : ctx->workspace().get(std::max<uint64_t>(xp.sendTotal, 1) * tb);
+  // Copies of chunk c's replicated runs, once its scatter is done.
+  auto replicate = [&](uint32_t c) {
+    for (const histograms::Replica &r : xp.replicas) {
+      if (r.chunk != c) continue;
+      uint8_t *b = static_cast<uint8_t *>(send);
+      if (ctx->onDevice())
+        HIP_CHECK(hipMemcpyAsync(b + r.dst * tb, b + r.src * tb, r.len * tb, hipMemcpyDeviceToDevice, ctx->stream()));
+      else
+        std::memcpy(b + r.dst * tb, b + r.src * tb, r.len * tb);
+    }
+  };
   performance::Measurements::add(isInner ? "MIMEMALLOC" : "MOMEMALLOC", (double)(performance::nowUs() - tAlloc), "us");
   window->start();
   const kernels::KeyMix mix{plan.keyMix ? 1u : 0u, plan.keyBits};
@@ -82,6 +97,7 @@ void NetworkPartitioning::partition(data::Relation *relation, data::Window *wind
         kernels::netScatter(relation->getData(), n, bits, plan.keyShift, g, b0, b1, gcur + c * perChunk,
                             static_cast<uint64_t *>(send), ctx->stream(), plan.keyBits, mix, nullptr, narrowMode,
                             !plan.keyOnly);
+      replicate(c);
       if (!single) window->exchange(send, c);
       if (afterChunk) afterChunk(c);
     }
@@ -92,6 +108,7 @@ void NetworkPartitioning::partition(data::Relation *relation, data::Window *wind
       const uint32_t b0 = c * bpc, b1 = std::min(g.blocks, b0 + bpc);
       host::netScatter(relation->getData(), n, bits, plan.keyShift, g, b0, b1, cursors, send, plan.wide, mix,
                        !plan.keyOnly);
+      replicate(c);
       if (!single) window->exchange(send, c);
       if (afterChunk) afterChunk(c);
     }

@@ -104,6 +104,7 @@ void SampledNetworkPartitioning::layoutSide(int k) {
       x.localIndex[p] = (int32_t)p;
     }
     x.sendTotal = n;
+    x.scatterTotal = n;
     x.recvTotal = 0;
     s.window.reset(new data::Window(x, cur, ctx, plan.wide));
     // Claim cursors (slice starts) and slice ends, in the scatter's cursor width.

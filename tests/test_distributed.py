@@ -16,11 +16,12 @@ import pytest
 from conftest import ROOT, devices
 
 
-def run_ranks(C, n_ranks, loc, G_R, G_S, cfg_fn=None, outer_dist="UNIQUE", theta=0.75, outputs=None, peaks=None):
+def run_ranks(C, n_ranks, loc, G_R, G_S, cfg_fn=None, outer_dist="UNIQUE", theta=0.75, outputs=None, peaks=None,
+              inner=None, outer=None):
     group = C.InProcessGroup(n_ranks)
-    inner = C.GenSpec(seed=1234)
-    outer = C.GenSpec(distribution=getattr(C.KeyDistribution, outer_dist), seed=4321,
-                      domain=0 if outer_dist == "UNIQUE" else G_R, zipf_theta=theta)
+    inner = inner or C.GenSpec(seed=1234)
+    outer = outer or C.GenSpec(distribution=getattr(C.KeyDistribution, outer_dist), seed=4321,
+                               domain=0 if outer_dist == "UNIQUE" else G_R, zipf_theta=theta)
     results, errors = [None] * n_ranks, []
 
     def rank_main(r):
@@ -335,3 +336,53 @@ def test_one_sided_exchange(C, dev, n_ranks, chunks, opts):
         assert peak["ONE_SIDED"] < peak["RCCL"], peak
     if opts == "mat":
         assert torch.equal(got["ONE_SIDEDpairs"], got["RCCLpairs"])
+
+
+@pytest.mark.parametrize("dev", devices())
+@pytest.mark.parametrize("n_ranks,chunks,opts", [(4, 1, ""), (8, 2, ""), (4, 1, "mat"), (3, 3, "inner-hot"),
+                                                  (4, 2, "one-sided")])
+def test_hot_partition_split(C, dev, n_ranks, chunks, opts):
+    """Cross-rank splitting of a hot network partition (AssignmentMap,
+    skew_split): Zipf(0.99) over 5 keys puts ~43 % of the skewed side in one
+    partition, more than a rank's fair share.  Its larger side is divided over
+    helper ranks by (source, chunk) and its smaller side replicated, so the
+    counts (and materialized pairs) equal the unsplit join and the oracle,
+    while the most loaded rank receives fewer tuples."""
+    import torch
+    G_R, G_S = 20_000, 400_000
+    hot = C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=77, domain=5, zipf_theta=0.99)
+    if opts == "inner-hot":  # duplicates on the build side: the inner side is divided, the outer replicated
+        inner, outer, G_R, G_S = hot, C.GenSpec(seed=4321), G_S, G_R
+    else:
+        inner, outer = C.GenSpec(seed=1234), hot
+    got, load = {}, {}
+    for split in (True, False):
+        pairs = [None] * n_ranks
+
+        def cfg_fn(c, split=split):
+            c.skew_split = split
+            c.bitmap_join = False
+            c.chunks = chunks
+            c.materialize = opts == "mat"
+            c.key_hashing = C.KeyHashing.OFF  # the hot key stays in one network partition
+            if opts == "one-sided":  # replicated inner runs: send buffer; divided outer runs: direct scatter
+                c.exchange = C.ExchangeMode.ONE_SIDED
+
+        results, exp = run_ranks(C, n_ranks, "device" if dev == "cuda" else "host", G_R, G_S, cfg_fn=cfg_fn,
+                                 outputs=pairs if opts == "mat" else None, inner=inner, outer=outer)
+        if exp is None:  # inner-hot: every inner key (0..4) meets exactly one unique outer key
+            exp = G_R
+        for res, plan in results:
+            assert res["global_matches"] == exp
+            assert (res["split_partitions"] >= 1) == split
+            assert plan.skew_split == split
+        got[split] = sum(r[0]["local_matches"] for r in results)
+        load[split] = max(r[0]["inner_received"] + r[0]["outer_received"] for r in results)
+        if opts == "mat":
+            p = torch.cat([x.cpu() for x in pairs])
+            got[(split, "pairs")] = p[torch.argsort(p[:, 1] * (1 << 32) + p[:, 0])]
+            assert p.shape[0] == exp
+    assert got[True] == got[False] == exp
+    assert load[True] < load[False], load
+    if opts == "mat":
+        assert torch.equal(got[(True, "pairs")], got[(False, "pairs")])
