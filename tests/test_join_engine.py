@@ -20,6 +20,20 @@ def run_join(C, dev, G_R, G_S, outer_dist="UNIQUE", cfg=None, theta=0.75):
 
 
 @pytest.mark.parametrize("dev", devices())
+def test_bitmap_key_shift_edge(C, dev):
+    """key_shift + bitmap bits == 64 (2^20 dense keys, 10 network bits, 10
+    bitmap bits, key_shift 54): the bitmap pass reads 4-byte key fragments,
+    and partial probe batches must not count padding lanes as matches."""
+    cfg = C.JoinConfig()
+    cfg.key_shift = 54
+    cfg.network_bits = 10  # (with fewer network bits the fragments outgrow the word: key-only plan)
+    cfg.replicate_bitmap = C.PlanChoice.ON  # the host path takes the bitmap only when forced
+    res, exp, j = run_join(C, dev, 1 << 20, (1 << 20) + 12_345, "UNIFORM", cfg=cfg)
+    assert j.plan.bitmap_join and j.plan.key_shift + j.plan.bitmap_bits == 64, j.plan
+    assert res["global_matches"] == exp
+
+
+@pytest.mark.parametrize("dev", devices())
 @pytest.mark.parametrize("dist", ["UNIQUE", "UNIFORM", "ZIPF", "MODULO"])
 @pytest.mark.parametrize("bitmap", [True, False])
 def test_join_matches_oracle(C, dev, dist, bitmap):
