@@ -1039,17 +1039,22 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   // Single un-timed launches on the null stream (MALL probe, tools/mall_probe.py).
   ops.def(
       "gather_rows",
-      [](const at::Tensor &rids, uint64_t ridOffset, const at::Tensor &payload) {
-        // out[i] = payload[rids[i] - ridOffset] for 32-byte rows (device; microbenchmark of the random row gather)
+      [](const at::Tensor &rids, uint64_t ridOffset, const at::Tensor &payload, int mode) {
+        // out[i] = payload[rids[i] - ridOffset] for 32-byte rows (device; microbenchmark of the random row
+        // gather).  mode -1: the operator's gatherRows; 0..3: kernels::gatherVariant shapes (rid_offset 0).
         TORCH_CHECK(rids.is_cuda() && payload.is_cuda() && rids.scalar_type() == at::kLong &&
                         payload.dim() == 2 && payload.size(1) == 4 && payload.is_contiguous() && rids.is_contiguous(),
                     "gather_rows: device int64 rids and [n, 4] int64 payload");
         at::Tensor out = at::empty({rids.size(0), 4}, payload.options());
-        kernels::gatherRows(ptr<uint64_t>(rids), (uint64_t)rids.size(0), ridOffset, ptr<uint64_t>(payload),
-                            ptr<uint64_t>(out), nullptr);
+        if (mode < 0)
+          kernels::gatherRows(ptr<uint64_t>(rids), (uint64_t)rids.size(0), ridOffset, ptr<uint64_t>(payload),
+                              ptr<uint64_t>(out), nullptr);
+        else
+          kernels::gatherVariant(mode, ptr<uint64_t>(rids), (uint64_t)rids.size(0), ptr<const ulonglong2>(payload),
+                                 ptr<ulonglong2>(out), nullptr);
         return out;
       },
-      py::arg("rids"), py::arg("rid_offset"), py::arg("payload"));
+      py::arg("rids"), py::arg("rid_offset"), py::arg("payload"), py::arg("mode") = -1);
   ops.def("copy_into", [](const at::Tensor &src, const at::Tensor &dst) {
     setDevice(src);
     HJ_CHECK(dst.numel() * dst.element_size() >= src.numel() * src.element_size(), "copy_into: dst too small");

@@ -26,6 +26,63 @@ __global__ __launch_bounds__(256) void readKernelImpl(const ulonglong2 *__restri
   if (acc == 0x9E3779B97F4A7C15ull) *sink = acc;  // keeps the loads live
 }
 
+// Random 32-byte row gather shapes (tools/gather_bench.py): MODE 0 a lane
+// per 16-byte half row; 1 a lane per whole row (two loads); 2 as 0 with four
+// rows per lane pair in flight; 3 as 0 with non-temporal loads.
+using gx2 = unsigned long long __attribute__((ext_vector_type(2)));
+template <int MODE>
+__global__ __launch_bounds__(256) void gatherVariantKernel(const uint64_t *__restrict__ rids, uint64_t n,
+                                                           const ulonglong2 *__restrict__ rows,
+                                                           ulonglong2 *__restrict__ out) {
+  const uint64_t tid = (uint64_t)blockIdx.x * 256 + threadIdx.x, stride = (uint64_t)gridDim.x * 256;
+  if constexpr (MODE == 1) {
+    for (uint64_t j = tid; j < n; j += stride) {
+      const uint64_t r = rids[j];
+      const ulonglong2 a = rows[2 * r], b = rows[2 * r + 1];
+      out[2 * j] = a;
+      out[2 * j + 1] = b;
+    }
+  } else if constexpr (MODE == 2) {
+    // lane pair p handles rows 4p .. 4p+3 of each 4-row group step
+    for (uint64_t t = tid; t < 2 * ((n + 3) / 4); t += stride) {
+      const uint64_t g = t >> 1, half = t & 1;
+      ulonglong2 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint64_t j = 4 * g + k;
+        if (j < n) v[k] = rows[2 * rids[j] + half];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint64_t j = 4 * g + k;
+        if (j < n) out[2 * j + half] = v[k];
+      }
+    }
+  } else {
+    for (uint64_t t = tid; t < 2 * n; t += stride) {
+      const uint64_t j = t >> 1, half = t & 1;
+      if constexpr (MODE == 3) {
+        const gx2 x = __builtin_nontemporal_load(reinterpret_cast<const gx2 *>(rows + 2 * rids[j] + half));
+        out[2 * j + half] = make_ulonglong2(x.x, x.y);
+      } else {
+        out[2 * j + half] = rows[2 * rids[j] + half];
+      }
+    }
+  }
+}
+
+void gatherVariant(int mode, const uint64_t *rids, uint64_t n, const ulonglong2 *rows, ulonglong2 *out,
+                   hipStream_t s) {
+  const uint32_t grid = 256 * 8;
+  switch (mode) {
+    case 1: hipLaunchKernelGGL(gatherVariantKernel<1>, dim3(grid), dim3(256), 0, s, rids, n, rows, out); break;
+    case 2: hipLaunchKernelGGL(gatherVariantKernel<2>, dim3(grid), dim3(256), 0, s, rids, n, rows, out); break;
+    case 3: hipLaunchKernelGGL(gatherVariantKernel<3>, dim3(grid), dim3(256), 0, s, rids, n, rows, out); break;
+    default: hipLaunchKernelGGL(gatherVariantKernel<0>, dim3(grid), dim3(256), 0, s, rids, n, rows, out); break;
+  }
+  HIP_CHECK_LAUNCH();
+}
+
 __global__ __launch_bounds__(256) void keyRidMaxKernel(const ulonglong2 *__restrict__ in, uint64_t n,
                                                        unsigned long long *out) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;
