@@ -33,7 +33,14 @@ BitmapJoin::Outcome BitmapJoin::run(bool exact) { return ctx->onDevice() ? runDe
 
 // Sampled (or exact) histogram -> device layout of bounded claim slices ->
 // bounded claim scatter of u32 fragments.  Nothing here waits for the device.
-void BitmapJoin::partitionSide(Side &s, bool exact) {
+bool BitmapJoin::sideNarrow(data::Relation *r, bool exact) const {
+  const uint64_t n = r->getLocalSize();
+  const kernels::PartitionGeometry g = kernels::partitionGeometry(n, maxBlocks);
+  const kernels::SampleScale sc = kernels::sampleScale(g, n, exact ? 1 : sampleStride, exact);
+  return kernels::cursorsNarrow(kernels::sampledLayoutCapacityBound(sc, 1u << plan.networkBits) + n);
+}
+
+void BitmapJoin::partitionSide(Side &s, bool exact, bool narrowOk) {
   const uint32_t bits = plan.networkBits, F = 1u << bits, G = CLAIM_GROUPS;
   const uint64_t n = s.relation->getLocalSize();
   const uint32_t stride = exact ? 1 : sampleStride;
@@ -51,7 +58,7 @@ void BitmapJoin::partitionSide(Side &s, bool exact) {
   const kernels::SampleScale sc = kernels::sampleScale(s.geom, n, stride, exact);
   const uint64_t cap = kernels::sampledLayoutCapacityBound(sc, F);
   // Claims may run past a slice end by up to n before the overflow is seen.
-  const bool narrow = kernels::cursorsNarrow(cap + n);
+  const bool narrow = narrowOk && kernels::cursorsNarrow(cap + n);
   const size_t cb = narrow ? 4 : 8;
   void *gstart = ws.get((size_t)G * F * cb), *gcur = ws.get((size_t)G * F * cb), *gend = ws.get((size_t)G * F * cb);
   unsigned long long *used = ws.getArray<unsigned long long>(1);
@@ -78,14 +85,17 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
   HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(BitmapCounters), st));
   Side si{inner, {}, nullptr, {}}, so{outer, {}, nullptr, {}};
   Outcome o;
+  // One cursor width for both sides (the fused N = 1 kernel reads both with
+  // one slice type; e.g. 1B inner x 4B outer needs 8-byte cursors on both).
+  const bool narrowOk = sideNarrow(inner, exact) && sideNarrow(outer, exact);
   {
     performance::TraceRange tr("bitmap_network_inner");
     utils::faultPoint("network");
-    partitionSide(si, exact);
+    partitionSide(si, exact, narrowOk);
   }
   HIP_CHECK(hipEventRecord(ev[1], st));
   if (N == 1) {
-    partitionSide(so, exact);
+    partitionSide(so, exact, narrowOk);
     HIP_CHECK(hipEventRecord(ev[2], st));
     HIP_CHECK(hipEventRecord(ev[3], st));
     utils::faultPoint("local");
@@ -117,7 +127,7 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
     tl.end("MWINPUT", ctx->commStream());
     HIP_CHECK(hipEventRecord(reduced, ctx->commStream()));
     o.linkBytes = (uint64_t)(2.0 * (N - 1) / N * (double)F * words * 4);
-    partitionSide(so, exact);
+    partitionSide(so, exact, narrowOk);
     HIP_CHECK(hipEventRecord(ev[2], st));
     HIP_CHECK(hipStreamWaitEvent(st, reduced, 0));
     HIP_CHECK(hipEventRecord(ev[3], st));

@@ -69,7 +69,10 @@ class BitmapJoin {
     uint32_t *frags = nullptr;
     kernels::BitmapSlices slices;
   };
-  void partitionSide(Side &s, bool exact);
+  // narrowOk: 4-byte claim cursors are allowed (both sides of a fused bitmap
+  // join must use the same cursor width; sideNarrow() says what one side needs).
+  void partitionSide(Side &s, bool exact, bool narrowOk);
+  bool sideNarrow(data::Relation *r, bool exact) const;
   Outcome runDevice(bool exact);
   Outcome runHost();
   void agree(Outcome &o, uint64_t localFlags);

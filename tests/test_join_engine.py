@@ -19,6 +19,17 @@ def run_join(C, dev, G_R, G_S, outer_dist="UNIQUE", cfg=None, theta=0.75):
     return res, C.Relation.expected_matches(inner, G_R, outer, G_S), j
 
 
+@pytest.mark.gpu
+def test_bitmap_mixed_cursor_widths(C, cuda):
+    """1M inner x 2.2B outer: the outer side's claim slices need 8-byte
+    cursors, so the inner side must use them too (the fused bitmap kernel
+    reads both with one slice type; this used to fail a CHECK)."""
+    cfg = C.JoinConfig()
+    res, exp, j = run_join(C, "cuda", 1 << 20, 2_200_000_000, "UNIFORM", cfg=cfg)
+    assert j.plan.bitmap_join
+    assert res["global_matches"] == exp
+
+
 @pytest.mark.parametrize("dev", devices())
 def test_bitmap_key_shift_edge(C, dev):
     """key_shift + bitmap bits == 64 (2^20 dense keys, 10 network bits, 10
