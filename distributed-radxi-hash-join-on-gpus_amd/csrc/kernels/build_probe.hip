@@ -1022,7 +1022,9 @@ size_t bpKeyLdsBytes(uint32_t rChunk) {
   return slots * 8 + (slots / BPK_SLOTS) * 4 + 64;
 }
 
-template <bool PF>
+// (Measured and dropped: loading the next item's first batches during this
+// item's probe, build/probe 7.35 vs 6.30 ms; a split u32 + u16 column layout of
+// the local pass output for 44-bit fragments, 7.2 vs 6.0 ms.)
 __global__ __launch_bounds__(BPK_T, 4) void bpKeyCountKernel(BPArgs a, const BPItem *__restrict__ items,
                                                              const uint32_t *__restrict__ nItemsPtr, uint32_t capacity) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1036,43 +1038,18 @@ __global__ __launch_bounds__(BPK_T, 4) void bpKeyCountKernel(BPArgs a, const BPI
   const uint32_t t = threadIdx.x;
   const uint32_t nItems = min(*nItemsPtr, capacity);
   uint64_t matches = 0;
-  // PF: the first batch of both sides of the next item is loaded while this
-  // item is probed (inner) and right after (outer).  Measured slower (1B x 1B
-  // sparse keys: build/probe 7.35 vs 6.30 ms, HPCJOIN_BPK_PREFETCH=1), so the
-  // default loads each item at its start and lets the 4 workgroups of a CU
-  // cover each other's loads.
-  auto range = [&](uint32_t w, uint64_t &rb, uint32_t &nr, uint64_t &sb, uint32_t &ns) {
+  for (uint32_t w = blockIdx.x; w < nItems; w += gridDim.x) {
     const BPItem it = items[w];
-    rb = a.partR[it.part] + (uint64_t)it.rChunk * a.rChunk;
-    nr = (uint32_t)(min(a.partREnd[it.part], rb + a.rChunk) - rb);
-    sb = a.partS[it.part] + (uint64_t)it.sChunk * a.sChunk;
-    ns = (uint32_t)(min(a.partSEnd[it.part], sb + a.sChunk) - sb);
-  };
-  uint64_t rv[BPK_K], sv[BPK_K];
-  uint64_t rb = 0, sb = 0;
-  uint32_t nr = 0, ns = 0;
-  if (blockIdx.x < nItems) {
-    range(blockIdx.x, rb, nr, sb, ns);
+    const uint64_t rb = a.partR[it.part] + (uint64_t)it.rChunk * a.rChunk;
+    const uint32_t nr = (uint32_t)(min(a.partREnd[it.part], rb + a.rChunk) - rb);
+    const uint64_t sb = a.partS[it.part] + (uint64_t)it.sChunk * a.sChunk;
+    const uint32_t ns = (uint32_t)(min(a.partSEnd[it.part], sb + a.sChunk) - sb);
+    uint64_t rv[BPK_K], sv[BPK_K];
 #pragma unroll
     for (int k = 0; k < BPK_K; ++k) {
       const uint32_t i = k * BPK_T + t;
       if (i < nr) rv[k] = R[rb + i];
       if (i < ns) sv[k] = S[sb + i];
-    }
-  }
-  for (uint32_t w = blockIdx.x; w < nItems; w += gridDim.x) {
-    const bool hasNext = PF && w + gridDim.x < nItems;
-    uint64_t nrb = 0, nsb = 0;
-    uint32_t nnr = 0, nns = 0;
-    if (hasNext) range(w + gridDim.x, nrb, nnr, nsb, nns);
-    if (!PF && w != blockIdx.x) {
-      range(w, rb, nr, sb, ns);
-#pragma unroll
-      for (int k = 0; k < BPK_K; ++k) {
-        const uint32_t i = k * BPK_T + t;
-        if (i < nr) rv[k] = R[rb + i];
-        if (i < ns) sv[k] = S[sb + i];
-      }
     }
     uint32_t tbits = ceilLog2(2ull * nr);
     if (tbits < 6) tbits = 6;
@@ -1105,13 +1082,6 @@ __global__ __launch_bounds__(BPK_T, 4) void bpKeyCountKernel(BPArgs a, const BPI
           p = atomicAdd(&fill[b], 1u);
         }
         table[b * BPK_SLOTS + p] = rv[k];
-      }
-    }
-    if (hasNext) {  // rv is free: the next item's first inner batch
-#pragma unroll
-      for (int k = 0; k < BPK_K; ++k) {
-        const uint32_t i = k * BPK_T + t;
-        if (i < nnr) rv[k] = R[nrb + i];
       }
     }
     __syncthreads();
@@ -1158,19 +1128,6 @@ __global__ __launch_bounds__(BPK_T, 4) void bpKeyCountKernel(BPArgs a, const BPI
         }
       }
     }
-    if (hasNext) {  // sv is free: the next item's first outer batch
-#pragma unroll
-      for (int k = 0; k < BPK_K; ++k) {
-        const uint32_t i = k * BPK_T + t;
-        if (i < nns) sv[k] = S[nsb + i];
-      }
-    }
-    if (PF) {
-      rb = nrb;
-      nr = nnr;
-      sb = nsb;
-      ns = nns;
-    }
     __syncthreads();  // the next item clears the counters
   }
   const unsigned long long total = blockReduceSum<BPK_T, unsigned long long>((unsigned long long)matches, wsum);
@@ -1196,16 +1153,8 @@ void buildProbe(const BPArgs &args, const BPItem *items, const uint32_t *nItems,
     const size_t ldsK = bpKeyLdsBytes(a.rChunk);
     HJ_CHECK(ldsK <= 160 * 1024, "buildProbe: key-only table %zu B exceeds 160 KiB (rChunk=%u)", ldsK, a.rChunk);
     const uint32_t perCuK = (uint32_t)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / ldsK));
-    static const bool pf = [] {
-      const char *e = std::getenv("HPCJOIN_BPK_PREFETCH");
-      return e && std::atoi(e) != 0;
-    }();
-    if (pf)
-      hipLaunchKernelGGL(bpKeyCountKernel<true>, dim3(std::min<uint32_t>(capacity, 256 * perCuK)), dim3(BPK_T), ldsK,
-                         s, a, items, nItems, capacity);
-    else
-      hipLaunchKernelGGL(bpKeyCountKernel<false>, dim3(std::min<uint32_t>(capacity, 256 * perCuK)), dim3(BPK_T), ldsK,
-                         s, a, items, nItems, capacity);
+    hipLaunchKernelGGL(bpKeyCountKernel, dim3(std::min<uint32_t>(capacity, 256 * perCuK)), dim3(BPK_T), ldsK, s, a,
+                       items, nItems, capacity);
     HIP_CHECK_LAUNCH();
     return;
   }
