@@ -1055,6 +1055,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         return out;
       },
       py::arg("rids"), py::arg("rid_offset"), py::arg("payload"), py::arg("mode") = -1);
+  ops.def(
+      "project_keys",
+      [](const at::Tensor &tuples, uint32_t shift, int ipt) {
+        // [n, 2] int64 tuples -> [n] int32 (key >> shift): the count-only network pass's byte mix, no partitioning
+        TORCH_CHECK(tuples.is_cuda() && tuples.dim() == 2 && tuples.size(1) == 2 && tuples.is_contiguous(),
+                    "project_keys: device [n, 2] int64 tuples");
+        at::Tensor out = at::empty({tuples.size(0)}, tuples.options().dtype(at::kInt));
+        kernels::projectKeys(ptr<const ulonglong2>(tuples), (uint64_t)tuples.size(0), shift, ptr<uint32_t>(out), ipt,
+                             nullptr);
+        return out;
+      },
+      py::arg("tuples"), py::arg("shift") = 10, py::arg("ipt") = 8);
   ops.def("copy_into", [](const at::Tensor &src, const at::Tensor &dst) {
     setDevice(src);
     HJ_CHECK(dst.numel() * dst.element_size() >= src.numel() * src.element_size(), "copy_into: dst too small");

@@ -83,6 +83,34 @@ void gatherVariant(int mode, const uint64_t *rids, uint64_t n, const ulonglong2 
   HIP_CHECK_LAUNCH();
 }
 
+// Streaming ceiling of the count-only network pass's byte mix: read a
+// 16-byte tuple, write a 4-byte fragment (no partitioning), IPT tuples per
+// thread per step.
+template <int IPT>
+__global__ __launch_bounds__(256) void projectKeysKernel(const ulonglong2 *__restrict__ in, uint64_t n,
+                                                         uint32_t shift, uint32_t *__restrict__ out) {
+  const uint64_t step = (uint64_t)gridDim.x * 256 * IPT;
+  for (uint64_t b = (uint64_t)blockIdx.x * 256 * IPT + threadIdx.x; b < n; b += step) {
+    ulonglong2 v[IPT];
+#pragma unroll
+    for (int k = 0; k < IPT; ++k)
+      if (b + (uint64_t)k * 256 < n) v[k] = in[b + (uint64_t)k * 256];
+#pragma unroll
+    for (int k = 0; k < IPT; ++k)
+      if (b + (uint64_t)k * 256 < n) out[b + (uint64_t)k * 256] = (uint32_t)(v[k].x >> shift);
+  }
+}
+
+void projectKeys(const ulonglong2 *in, uint64_t n, uint32_t shift, uint32_t *out, int ipt, hipStream_t s) {
+  const uint32_t grid = 256 * 8;
+  switch (ipt) {
+    case 1: hipLaunchKernelGGL(projectKeysKernel<1>, dim3(grid), dim3(256), 0, s, in, n, shift, out); break;
+    case 4: hipLaunchKernelGGL(projectKeysKernel<4>, dim3(grid), dim3(256), 0, s, in, n, shift, out); break;
+    default: hipLaunchKernelGGL(projectKeysKernel<8>, dim3(grid), dim3(256), 0, s, in, n, shift, out); break;
+  }
+  HIP_CHECK_LAUNCH();
+}
+
 __global__ __launch_bounds__(256) void keyRidMaxKernel(const ulonglong2 *__restrict__ in, uint64_t n,
                                                        unsigned long long *out) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;

@@ -835,6 +835,30 @@ void scatterAblation(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t 
     else if (mode == 2) launchNet<P, uint32_t, NTH, IPT, 2>(p, in, n, bits, g, 0, g.blocks, cursors, out, s);     \
     else launchNet<P, uint32_t, NTH, IPT, 0>(p, in, n, bits, g, 0, g.blocks, cursors, out, s);                    \
   } while (0)
+  // 10: the count-only fragment scatter of the bitmap plan (4-byte output,
+  // 1024 x 16 tiles): mode 0 real, 1 coalesced write-out, 2 no write-out.
+  // Measured at 1B tuples, bits 8/9/10/11: 4.18/4.30/4.45/4.70 ms real against
+  // ~3.87 coalesced and ~2.6 without writes (streaming ceiling of the byte mix
+  // 3.47 ms, tools/stream_mix_bench.py): the scatter pays for runs of ~16
+  // fragments per partition and tile.  Key-only loads with 24-key tiles
+  // (longer runs) spilled and ran 4.56 ms at bits 10.
+  NetFragPol fpol;
+  fpol.mask = (1ull << bits) - 1;
+  fpol.bits = bits;
+  using FragLayout = ScatterLayout<NetFragPol, uint32_t, 1024 * 16>;
+  const size_t fragLds = FragLayout::bytes(1u << bits);
+#define HJ_FRAG(M)                                                                                                \
+  hipLaunchKernelGGL((netScatterClaimKernel<NetFragPol, uint32_t, 1024, 16, M>), dim3(g.blocks), dim3(1024),      \
+                     fragLds, s, reinterpret_cast<const ulonglong2 *>(in), n, g.tilesPerBlock, 1u << bits, fpol,  \
+                     0u, reinterpret_cast<uint32_t *>(gcur), reinterpret_cast<uint32_t *>(out))
+  if (geometry == 10) {
+    if (mode == 1) HJ_FRAG(1);
+    else if (mode == 2) HJ_FRAG(2);
+    else HJ_FRAG(0);
+    HIP_CHECK_LAUNCH();
+    return;
+  }
+#undef HJ_FRAG
   switch (geometry) {
     case 1: HJ_ABL(NetCompressedPol, pol, 512, 16); break;
     case 2: HJ_ABL(NetCompressedPol, pol, 1024, 8); break;

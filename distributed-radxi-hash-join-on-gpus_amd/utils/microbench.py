@@ -81,7 +81,7 @@ def npj_phase(n=1 << 26, iters=3):
 
 
 GEOMETRIES = {0: "256x16", 1: "512x16", 2: "1024x8", 3: "1024x16", 4: "256x16+digarray", 5: "256x8",
-              6: "claim256x16", 7: "claim512x16", 8: "claim1024x16", 9: "claim1024x8"}
+              6: "claim256x16", 7: "claim512x16", 8: "claim1024x16", 9: "claim1024x8", 10: "frag-claim1024x16"}
 
 
 def scatter_ablation(n=1 << 28, bits_list=(4, 8, 10), iters=5, geometries=(0,)):
@@ -94,9 +94,9 @@ def scatter_ablation(n=1 << 28, bits_list=(4, 8, 10), iters=5, geometries=(0,)):
         for b in bits_list:
             row = {"geometry": GEOMETRIES[geo], "bits": b}
             try:
-                for mode, name in ((0, "scatter_ms"), (1, "coalesced_ms"), (2, "no_write_ms"))[: (2 if geo >= 6 else 3)]:
+                for mode, name in ((0, "scatter_ms"), (1, "coalesced_ms"), (2, "no_write_ms"))[: (2 if 6 <= geo < 10 else 3)]:
                     row[name] = round(C.ops.bench_scatter_ms(t, b, mode, iters, 2048, geo), 4)
-                row["scatter_TBps"] = round(n * 24 / row["scatter_ms"] / 1e9, 3)
+                row["scatter_TBps"] = round(n * (20 if geo == 10 else 24) / row["scatter_ms"] / 1e9, 3)
             except RuntimeError as e:  # e.g. LDS budget exceeded for this geometry
                 row["error"] = str(e).split("(")[0]
             out.append(row)
