@@ -1067,6 +1067,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         return out;
       },
       py::arg("tuples"), py::arg("shift") = 10, py::arg("ipt") = 8);
+  ops.def(
+      "probe_bitmap_global",
+      [](const at::Tensor &tuples, const at::Tensor &bitmap, uint64_t keyMask, int ipt) {
+        // Count tuples whose key bit is set in a global bitmap (microbenchmark of a whole-key-space probe)
+        TORCH_CHECK(tuples.is_cuda() && bitmap.is_cuda() && tuples.dim() == 2 && tuples.size(1) == 2 &&
+                        bitmap.scalar_type() == at::kInt && bitmap.is_contiguous(),
+                    "probe_bitmap_global: device [n, 2] int64 tuples and an int32 bitmap");
+        TORCH_CHECK((uint64_t)bitmap.numel() * 32 > keyMask, "probe_bitmap_global: bitmap smaller than the key mask");
+        at::Tensor cnt = at::zeros({1}, tuples.options());
+        kernels::probeBitmapGlobal(ptr<const ulonglong2>(tuples), (uint64_t)tuples.size(0), ptr<uint32_t>(bitmap),
+                                   keyMask, reinterpret_cast<unsigned long long *>(cnt.data_ptr()), ipt, nullptr);
+        return cnt;
+      },
+      py::arg("tuples"), py::arg("bitmap"), py::arg("key_mask"), py::arg("ipt") = 8);
   ops.def("copy_into", [](const at::Tensor &src, const at::Tensor &dst) {
     setDevice(src);
     HJ_CHECK(dst.numel() * dst.element_size() >= src.numel() * src.element_size(), "copy_into: dst too small");

@@ -400,6 +400,8 @@ void npjProbe(const data::Tuple *S, uint64_t nS, const unsigned long long *table
 void copyKernel(const ulonglong2 *in, ulonglong2 *out, uint64_t n16, hipStream_t s);
 void readKernel(const ulonglong2 *in, uint64_t n16, unsigned long long *sink, hipStream_t s);
 void projectKeys(const ulonglong2 *in, uint64_t n, uint32_t shift, uint32_t *out, int ipt, hipStream_t s);
+void probeBitmapGlobal(const ulonglong2 *in, uint64_t n, const uint32_t *bm, uint64_t keyMask,
+                       unsigned long long *count, int ipt, hipStream_t s);
 void gatherVariant(int mode, const uint64_t *rids, uint64_t n, const ulonglong2 *rows, ulonglong2 *out,
                    hipStream_t s);
 

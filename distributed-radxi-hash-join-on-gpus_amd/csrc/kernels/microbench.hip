@@ -111,6 +111,39 @@ void projectKeys(const ulonglong2 *in, uint64_t n, uint32_t shift, uint32_t *out
   HIP_CHECK_LAUNCH();
 }
 
+// Probe ceiling of a whole-key-space bitmap kept in the Infinity Cache: every
+// tuple's key tests one bit of a 2^bits-bit global bitmap (random 4-byte
+// reads), keys streamed from 16-byte tuples, IPT tuples in flight per lane.
+template <int IPT>
+__global__ __launch_bounds__(256) void probeBitmapGlobalKernel(const ulonglong2 *__restrict__ in, uint64_t n,
+                                                               const uint32_t *__restrict__ bm, uint64_t keyMask,
+                                                               unsigned long long *count) {
+  const uint64_t step = (uint64_t)gridDim.x * 256 * IPT;
+  uint32_t c = 0;
+  for (uint64_t b = (uint64_t)blockIdx.x * 256 * IPT + threadIdx.x; b < n; b += step) {
+    uint64_t k[IPT];
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) k[j] = b + (uint64_t)j * 256 < n ? (in[b + (uint64_t)j * 256].x & keyMask) : 0;
+    uint32_t w[IPT];
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) w[j] = bm[k[j] >> 5];
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) c += (b + (uint64_t)j * 256 < n) ? (w[j] >> (k[j] & 31)) & 1u : 0u;
+  }
+  c = waveReduceSum<uint32_t>(c);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(count, (unsigned long long)c);
+}
+
+void probeBitmapGlobal(const ulonglong2 *in, uint64_t n, const uint32_t *bm, uint64_t keyMask,
+                       unsigned long long *count, int ipt, hipStream_t s) {
+  const uint32_t grid = 256 * 16;
+  if (ipt == 16)
+    hipLaunchKernelGGL(probeBitmapGlobalKernel<16>, dim3(grid), dim3(256), 0, s, in, n, bm, keyMask, count);
+  else
+    hipLaunchKernelGGL(probeBitmapGlobalKernel<8>, dim3(grid), dim3(256), 0, s, in, n, bm, keyMask, count);
+  HIP_CHECK_LAUNCH();
+}
+
 __global__ __launch_bounds__(256) void keyRidMaxKernel(const ulonglong2 *__restrict__ in, uint64_t n,
                                                        unsigned long long *out) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;
