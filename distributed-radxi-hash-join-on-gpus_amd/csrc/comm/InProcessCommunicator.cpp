@@ -1,5 +1,7 @@
 #include "InProcessCommunicator.h"
 
+#include "../kernels/kernels.h"
+
 #include <chrono>
 #include <cstring>
 
@@ -70,6 +72,35 @@ void InProcessCommunicator::allReduceSumHost(uint64_t *data, size_t count) {
     for (uint32_t r = 0; r < size(); ++r) s += all[r * count + i];
     data[i] = s;
   }
+}
+
+void InProcessCommunicator::allReduceSumDevice(uint64_t *data, size_t count, hipStream_t stream) {
+  const uint32_t N = size(), me = rank_;
+  if (N == 1 || count == 0) return;
+  hipPointerAttribute_t attr;
+  const bool dev = hipPointerGetAttributes(&attr, data) == hipSuccess && attr.type == hipMemoryTypeDevice;
+  (void)hipGetLastError();
+  std::vector<uint64_t> ptrs(N);
+  const uint64_t mine[2] = {(uint64_t)(uintptr_t)data, dev ? (uint64_t)attr.device : ~0ull};
+  std::vector<uint64_t> all(2 * N);
+  HIP_CHECK(hipStreamSynchronize(stream));  // my buffer is final
+  allGatherHost(mine, all.data(), 2);       // (a barrier: every buffer is final)
+  bool sameDevice = dev;
+  for (uint32_t r = 0; r < N; ++r) {
+    ptrs[r] = all[2 * r];
+    sameDevice = sameDevice && all[2 * r + 1] == mine[1];
+  }
+  if (!sameDevice) {  // ranks on different devices (or host memory): the staged default
+    Communicator::allReduceSumDevice(data, count, stream);
+    return;
+  }
+  uint64_t *const *dptrs = nullptr;
+  HIP_CHECK(hipMallocAsync((void **)&dptrs, N * sizeof(uint64_t), stream));
+  HIP_CHECK(hipMemcpyAsync((void *)dptrs, ptrs.data(), N * sizeof(uint64_t), hipMemcpyHostToDevice, stream));
+  kernels::sumSlices(dptrs, N, count * me / N, count * (me + 1) / N, stream);
+  HIP_CHECK(hipFreeAsync((void *)dptrs, stream));
+  HIP_CHECK(hipStreamSynchronize(stream));
+  group_->barrier();  // every slice of every buffer written
 }
 
 void InProcessCommunicator::allToAllV(const uint64_t *send, const uint64_t *sendCounts, const uint64_t *sendDispls,

@@ -53,6 +53,9 @@ class InProcessCommunicator : public Communicator {
   bool sharesAddressSpace() const override { return true; }
   void allGatherHost(const uint64_t *send, uint64_t *recv, size_t count) override;
   void allReduceSumHost(uint64_t *data, size_t count) override;
+  // Device buffers of ranks on one device: each rank sums its slice of all
+  // buffers with one kernel (no host staging); completes before returning.
+  void allReduceSumDevice(uint64_t *data, size_t count, hipStream_t stream) override;
   void barrier() override { group_->barrier(); }
   void checkHealth() override;
   void abort(const std::string &why) override { group_->abort(why); }

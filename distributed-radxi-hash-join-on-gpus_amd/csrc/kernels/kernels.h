@@ -402,6 +402,10 @@ void readKernel(const ulonglong2 *in, uint64_t n16, unsigned long long *sink, hi
 void projectKeys(const ulonglong2 *in, uint64_t n, uint32_t shift, uint32_t *out, int ipt, hipStream_t s);
 void probeBitmapGlobal(const ulonglong2 *in, uint64_t n, const uint32_t *bm, uint64_t keyMask,
                        unsigned long long *count, int ipt, hipStream_t s);
+// In-process all-reduce step (comm/InProcessCommunicator): devBufs is a device
+// array of the n ranks' buffers; element i in [lo, hi) of every buffer becomes
+// the sum over ranks.
+void sumSlices(uint64_t *const *devBufs, uint32_t n, uint64_t lo, uint64_t hi, hipStream_t s);
 void gatherVariant(int mode, const uint64_t *rids, uint64_t n, const ulonglong2 *rows, ulonglong2 *out,
                    hipStream_t s);
 
