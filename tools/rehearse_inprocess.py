@@ -23,12 +23,16 @@ def main():
     ap.add_argument("--ranks", type=int, default=4)
     ap.add_argument("--size", type=float, default=1e9)
     ap.add_argument("--chunks", type=int, default=4)
+    ap.add_argument("--sparse", action="store_true", help="unique random 63-bit keys (the general path)")
+    ap.add_argument("--shuffle", action="store_true", help="hash-partition shuffle instead of replicated bitmaps")
+    ap.add_argument("--one-sided", action="store_true")
     args = ap.parse_args()
     C = hpcjoin.require_native()
     n, G = args.ranks, int(args.size)
     group = C.InProcessGroup(n)
     inner = C.GenSpec(seed=1234)
     outer = C.GenSpec(seed=4321)
+    inner.sparse64 = outer.sparse64 = args.sparse
     out, errors = [None] * n, []
 
     def rank_main(r):
@@ -41,6 +45,10 @@ def main():
             S.generate(outer, lo)
             cfg = C.JoinConfig()
             cfg.chunks = args.chunks
+            if args.shuffle:
+                cfg.bitmap_join = False
+            if args.one_sided:
+                cfg.exchange = C.ExchangeMode.ONE_SIDED
             j = C.HashJoin(R, S, ctx, cfg)
             res = [j.run() for _ in range(2)]
             out[r] = {"plan": repr(j.plan), "global_matches": [x["global_matches"] for x in res],
