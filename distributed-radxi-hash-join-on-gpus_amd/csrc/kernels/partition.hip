@@ -841,7 +841,11 @@ void scatterAblation(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t 
   // ~3.87 coalesced and ~2.6 without writes (streaming ceiling of the byte mix
   // 3.47 ms, tools/stream_mix_bench.py): the scatter pays for runs of ~16
   // fragments per partition and tile.  Key-only loads with 24-key tiles
-  // (longer runs) spilled and ran 4.56 ms at bits 10.
+  // (longer runs) spilled and ran 4.56 ms at bits 10; key-only loads through a
+  // buffer resource with two register tiles (the next tile's loads issued
+  // before this one is ranked) ran 2 % slower in the 1B join (network pass
+  // 8.78 vs 8.60 ms): the pass is bound by the scattered writes, not by load
+  // latency.
   NetFragPol fpol;
   fpol.mask = (1ull << bits) - 1;
   fpol.bits = bits;
