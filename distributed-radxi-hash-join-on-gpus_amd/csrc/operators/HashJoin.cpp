@@ -220,8 +220,17 @@ void HashJoin::planWireCodec(const std::vector<uint64_t> &all, size_t stride, ui
     plan.wireRidBits[r] = 0;
     plan.ridBase[r].assign((size_t)numberOfNodes * chunks, 0);
   }
-  if (plan.wide || plan.keyOnly || numberOfNodes == 1 || config.wireCodec == core::WireCodecMode::Off) return;
+  if (plan.wide || numberOfNodes == 1 || config.wireCodec == core::WireCodecMode::Off) return;
   const uint32_t keyW = plan.keyBits > plan.networkBits ? plan.keyBits - plan.networkBits : 0;
+  if (plan.keyOnly) {
+    // Key-only words (keyShift 0) are the key above the network digit: only
+    // those keyBits - networkBits bits travel (53 of 64 for 63-bit keys), no
+    // rid and no rid base (decode then returns the word itself).
+    const bool on = config.wireCodec == core::WireCodecMode::On ? keyW < 64 : (ctx->onDevice() && keyW <= 56);
+    if (on && keyW >= 1)
+      for (int r = 0; r < 2; ++r) plan.wireBits[r] = keyW;
+    return;
+  }
   for (int r = 0; r < 2; ++r) {
     uint64_t span = 1;
     for (uint32_t n = 0; n < numberOfNodes; ++n)

@@ -209,7 +209,8 @@ def test_sparse64_join_auto_wide(C, dev):
 @pytest.mark.parametrize("n_ranks", [2, 4])
 def test_sparse64_key_only_ranks(C, dev, n_ranks):
     """Key-only words through the N-rank shuffle (exchange, local pass, KCOUNT
-    build/probe), chunked exchange included."""
+    build/probe), chunked exchange included; the wire codec carries only the
+    key bits above the network digit (no rid, no rid base)."""
     loc = "device" if dev == "cuda" else "host"
     G_R, G_S = 120_011, 300_007
     inner = C.GenSpec(seed=31)
@@ -219,10 +220,12 @@ def test_sparse64_key_only_ranks(C, dev, n_ranks):
 
     def cfg_fn(c):
         c.chunks = 2
+        c.wire_codec = C.WireCodecMode.ON
     out = run_ranks(C, n_ranks, loc, generated(C, loc, inner, G_R, n_ranks), generated(C, loc, outer, G_S, n_ranks),
                     G_R, G_S, cfg_fn)
     for res_list, plan in out:
         assert plan.key_only and not plan.bitmap_join
+        assert list(plan.wire_bits) == [plan.key_bits - plan.network_bits] * 2, (plan.wire_bits, plan)
         for res in res_list:
             assert res["global_matches"] == G_S
 
