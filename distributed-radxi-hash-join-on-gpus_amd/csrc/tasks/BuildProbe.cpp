@@ -145,6 +145,9 @@ void BuildProbe::execute() {
     return;
   }
   // Two-pass exact materialization: count per item -> 64-bit offsets -> place.
+  // (A single pass with one device atomic per wave and batch on a shared
+  // output cursor measured 65 ms instead of 29 for the SF100 row output: 4.7M
+  // atomics on one address serialize.)
   uint32_t *itemCounts = ws.getArray<uint32_t>(capacity);
   unsigned long long *itemOffsets = ws.getArray<unsigned long long>(capacity);
   void *scanWs64 = ws.get(kernels::scanWorkspaceBytes(capacity));
