@@ -47,6 +47,27 @@ def main():
     ]
     R = C.Relation(C.Relation.local_size_for(G_R, info.rank, info.world), G_R, "device", info.local_rank)
     R.generate(inner, C.Relation.local_offset_for(G_R, info.rank, info.world))
+    # General path: unique random 63-bit keys on both sides -> key-only words,
+    # wire codec carrying only the key bits above the network digit.
+    sparse_in = C.GenSpec(seed=1234)
+    sparse_in.sparse64 = True
+    sparse_out = C.GenSpec(seed=99)
+    sparse_out.sparse64 = True
+    Rs = C.Relation(C.Relation.local_size_for(G_R, info.rank, info.world), G_R, "device", info.local_rank)
+    Rs.generate(sparse_in, C.Relation.local_offset_for(G_R, info.rank, info.world))
+    Ss = C.Relation(C.Relation.local_size_for(G_R, info.rank, info.world), G_R, "device", info.local_rank)
+    Ss.generate(sparse_out, C.Relation.local_offset_for(G_R, info.rank, info.world))
+    cfg = C.JoinConfig()
+    cfg.wire_codec = C.WireCodecMode.ON  # auto packs only <= 56 bits (this size plans 6 network bits: 57)
+    j = C.HashJoin(Rs, Ss, ctx, cfg)
+    assert j.plan.key_only and list(j.plan.wire_bits) == [j.plan.key_bits - j.plan.network_bits] * 2, j.plan
+    exp = C.Relation.expected_matches(sparse_in, G_R, sparse_out, G_R)
+    for _ in range(2):
+        res = j.run()
+        assert res["global_matches"] == exp, ("sparse-key-only", res["global_matches"], exp)
+    if info.rank == 0:
+        print(f"sparse-key-only: {res['global_matches']} == {exp}, plan {j.plan}", flush=True)
+    del j, Rs, Ss
     for name, spec, G, opts in cases:
         S = C.Relation(C.Relation.local_size_for(G, info.rank, info.world), G, "device", info.local_rank)
         S.generate(spec, C.Relation.local_offset_for(G, info.rank, info.world))
