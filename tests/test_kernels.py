@@ -201,3 +201,36 @@ def test_wire_codec_roundtrip(C, dev, w, rid_bits):
         dback = torch.full_like(raw, -1).cuda()
         C.ops.wire_unpack(dwire, dback, w, rid_bits, key_shift, segs)
         assert torch.equal(dback.cpu(), back)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [-1, 0, 1, 2, 3])
+def test_gather_rows_shapes(C, cuda, mode):
+    """The random row gather (operator kernel and the microbenchmark shapes)
+    equals torch indexing of the 32-byte rows."""
+    import torch
+    n = 100_003
+    payload = C.ops.generate_payload(n, 0, 5, "cuda:0")
+    rids = torch.randperm(n, device="cuda", dtype=torch.int64)
+    out = C.ops.gather_rows(rids, 0, payload, mode)
+    assert torch.equal(out, payload[rids])
+
+
+@pytest.mark.gpu
+def test_project_keys_and_global_bitmap_probe(C, cuda):
+    """Streaming-ceiling and whole-key-space probe microbenchmark kernels
+    compute what they claim (key >> shift; count of keys whose bit is set)."""
+    import torch
+    n = 1 << 18
+    R = C.Relation(n, n, "device", 0)
+    R.generate(C.GenSpec(seed=9), 0)
+    t = R.to_tensor()
+    for ipt in (1, 4, 8):
+        assert torch.equal(C.ops.project_keys(t, 10, ipt).to(torch.int64) & 0xFFFFFFFF,
+                           (t[:, 0] >> 10) & 0xFFFFFFFF)
+    even = torch.arange(0, 1 << 18, 2, device="cuda")  # set the bits of even keys
+    words = torch.zeros((1 << 18) // 32, dtype=torch.int64, device="cuda")
+    words.index_add_(0, even >> 5, torch.ones_like(even) << (even & 31))  # distinct bits: sum == OR
+    bm = words.to(torch.int32)
+    got = int(C.ops.probe_bitmap_global(t, bm, (1 << 18) - 1, 8).item())
+    assert got == int(((t[:, 0] & ((1 << 18) - 1)) % 2 == 0).sum().item())
