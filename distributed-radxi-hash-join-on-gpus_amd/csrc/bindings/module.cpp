@@ -650,6 +650,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("frag_shift", &core::JoinPlan::fragShift)
       .def_readonly("key_bits", &core::JoinPlan::keyBits)
       .def_readonly("split_local", &core::JoinPlan::splitLocal)
+      .def_readonly("fragments", &core::JoinPlan::fragments)
       .def_readonly("skew_split", &core::JoinPlan::skewSplit)
       .def_property_readonly("wire_bits", [](const core::JoinPlan &p) {
         return std::vector<uint32_t>{p.wireBits[0], p.wireBits[1]};

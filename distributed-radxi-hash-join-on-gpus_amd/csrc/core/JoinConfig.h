@@ -152,6 +152,10 @@ struct JoinPlan {
   // rid bits, and the rid base of every (rank, exchange chunk), rank-major.
   // Set by HashJoin::planWireCodec.
   bool splitLocal = false;    // local pass writes split columns (kernels.h, SplitLayout)
+  // Count-only two-level pass (N = 1, sampled network pass): the network pass
+  // writes u32 key fragments and the local pass only the u16 fragment column
+  // -- no rid is written, since a count never reads one.
+  bool fragments = false;
   bool skewSplit = false;     // hot network partitions may be split across ranks
   bool directCount = true;    // build/probe may use direct-addressed count tables
   uint32_t localItemTiles = 64;

@@ -32,8 +32,9 @@ Window::Window(const histograms::ExchangePlan &plan, histograms::GlobalHistogram
   }
 }
 
-Window::Window(const histograms::ExchangePlan &plan, uint64_t capacityTuples, core::ExecContext *ctx, bool wide)
-    : plan(plan), globalHistogram(nullptr), assignment(nullptr), ctx(ctx), wide(wide) {
+Window::Window(const histograms::ExchangePlan &plan, uint64_t capacityTuples, core::ExecContext *ctx, bool wide,
+               uint32_t elemBytes)
+    : plan(plan), globalHistogram(nullptr), assignment(nullptr), ctx(ctx), wide(wide), elemBytes(elemBytes) {
   localWindowSize = capacityTuples;
   data = ctx->workspace().get(std::max<uint64_t>(capacityTuples, 1) * tupleBytes());
   exchanged.assign(std::max<uint32_t>(plan.chunks, 1), false);

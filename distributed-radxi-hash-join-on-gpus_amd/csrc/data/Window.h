@@ -33,7 +33,9 @@ class Window {
          histograms::AssignmentMap *assignment, core::ExecContext *ctx, bool wide);
   // Single-rank window of `capacityTuples` whose plan is filled in after the
   // scatter (sampled network pass: no histograms, no exchange).
-  Window(const histograms::ExchangePlan &plan, uint64_t capacityTuples, core::ExecContext *ctx, bool wide);
+  // elemBytes 4: the window holds u32 key fragments (JoinPlan::fragments).
+  Window(const histograms::ExchangePlan &plan, uint64_t capacityTuples, core::ExecContext *ctx, bool wide,
+         uint32_t elemBytes = 0);
   ~Window();
   // View of exchange chunk c alone (its segments; the data is shared): stop()
   // waits for that chunk only, so the local pass and build/probe can run on a
@@ -83,7 +85,8 @@ class Window {
   void assertAllTuplesWritten();
 
   void *getData() { return data; }
-  uint32_t tupleBytes() const { return wide ? 16 : 8; }
+  uint32_t tupleBytes() const { return elemBytes ? elemBytes : (wide ? 16 : 8); }
+  bool holdsFragments() const { return elemBytes == 4; }
   bool isWide() const { return wide; }
   const histograms::ExchangePlan &getPlan() const { return plan; }
   // Local partitioning hands back its partition-major output.
@@ -112,6 +115,7 @@ class Window {
   histograms::AssignmentMap *assignment;
   core::ExecContext *ctx;
   bool wide;
+  uint32_t elemBytes = 0;  // 0: the tuple format's size
   bool open = false;
   std::vector<hipEvent_t> ready, done;
   std::vector<bool> exchanged;

@@ -187,9 +187,10 @@ constexpr uint32_t LOCAL_ITEM_TILES = 16;
 constexpr uint32_t LOCAL_ITEM_MAX = LOCAL_ITEM_TILES * PART_TILE;  // 65536
 
 // digit = (word >> shift) & (2^bits - 1).  For compressed tuples word = value,
-// shift = keyShift; for wide tuples word = key, shift = networkBits.
+// shift = keyShift; for wide tuples word = key, shift = networkBits; for u32
+// key fragments (frag) word = fragment, shift = 0.
 void localHistogram(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift,
-                    uint32_t bits, uint32_t *itemHist, hipStream_t s, uint32_t sampleStride = 1);
+                    uint32_t bits, uint32_t *itemHist, hipStream_t s, uint32_t sampleStride = 1, bool frag = false);
 // gcur[stream][F] (u32 if narrow else u64) claim slices + partBegin[owned*F+1].
 void localCursors(const uint32_t *itemHist, const uint32_t *lpItemBegin, uint32_t owned, uint32_t bits,
                   const uint64_t *lpBase, const LocalItem *items, void *gcur, bool narrow, uint64_t *partBegin,
@@ -212,9 +213,11 @@ constexpr uint32_t SPLIT_BYTES = 6;
 
 // split.on (compressed input only): out is the u32 rid column, split.hi the
 // u16 fragment column (kernels.h, SplitLayout).
+// frag: the input is u32 key fragments (JoinPlan::fragments) and the output
+// the u16 column of fragment >> bits alone (out; split.hi unused).
 void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift,
                   uint32_t bits, void *gcur, bool narrow, void *out, hipStream_t s, const void *gend = nullptr,
-                  SplitLayout split = SplitLayout(), uint32_t geometry = 0);
+                  SplitLayout split = SplitLayout(), uint32_t geometry = 0, bool frag = false);
 // Sampled local pass (no exact local histogram): itemHist from
 // localHistogram(sampleStride) -> per-final-partition capacities (estimate +
 // 8 sigma + 2% + 64) -> gapped partition-major layout: gcur = partBegin =

@@ -64,6 +64,10 @@ template <>
 struct Loader<uint64_t> {
   static __device__ __forceinline__ uint64_t load(const uint64_t *p) { return __builtin_nontemporal_load(p); }
 };
+template <>
+struct Loader<uint32_t> {
+  static __device__ __forceinline__ uint32_t load(const uint32_t *p) { return __builtin_nontemporal_load(p); }
+};
 
 // ------------------------------------------------------- histogram (pass 1)
 __global__ __launch_bounds__(NT) void netHistogramKernel(const ulonglong2 *__restrict__ in, uint64_t n,
@@ -324,6 +328,22 @@ struct LocalWidePol {  // 16 B -> 16 B, digit = (key >> shift) & mask
   __device__ __forceinline__ StageT stage(const InT &x, uint32_t) const { return x; }
   __device__ __forceinline__ uint32_t stagedDigit(const StageT &v) const { return digit(v); }
   __device__ __forceinline__ OutT out(const StageT &v) const { return v; }
+  __device__ __forceinline__ void store(OutT *o, uint64_t pos, const StageT &v) const { o[pos] = out(v); }
+};
+// u32 key fragment -> u16 of the bits above the local digit (count-only
+// two-level pass, JoinPlan::fragments): 2 bytes written per tuple.
+struct LocalFragPol {
+  using InT = uint32_t;
+  using StageT = uint32_t;
+  using OutT = uint16_t;
+  static constexpr bool kDigArray = false;
+  uint64_t mask;
+  uint32_t shift;
+  uint32_t fragShift;
+  __device__ __forceinline__ uint32_t digit(const InT &x) const { return (uint32_t)((x >> shift) & mask); }
+  __device__ __forceinline__ StageT stage(const InT &x, uint32_t) const { return x; }
+  __device__ __forceinline__ uint32_t stagedDigit(const StageT &v) const { return digit(v); }
+  __device__ __forceinline__ OutT out(const StageT &v) const { return (uint16_t)(v >> fragShift); }
   __device__ __forceinline__ void store(OutT *o, uint64_t pos, const StageT &v) const { o[pos] = out(v); }
 };
 struct LocalSplitPol : LocalCompressedPol {  // 8 B -> u32 rid + u16 fragment (kernels.h, SplitLayout)
@@ -904,15 +924,19 @@ void netScatterGlobalAtomic(const data::Tuple *in, uint64_t n, uint32_t bits, ui
 }
 
 // ------------------------------------------------------ pass 2 (local) kernels
-template <bool WIDE>
+// KIND: 0 = 8-byte CompressedTuple / key-only word, 1 = 16-byte tuple (its
+// key), 2 = u32 key fragment (JoinPlan::fragments).
+template <int KIND>
 __device__ __forceinline__ uint64_t localWord(const void *in, uint64_t i) {
-  if constexpr (WIDE)
+  if constexpr (KIND == 1)
     return reinterpret_cast<const ulonglong2 *>(in)[i].x;
+  else if constexpr (KIND == 2)
+    return reinterpret_cast<const uint32_t *>(in)[i];
   else
     return reinterpret_cast<const uint64_t *>(in)[i];
 }
 
-template <bool WIDE>
+template <int WIDE>
 __global__ __launch_bounds__(NT) void localHistogramKernel(const void *__restrict__ in,
                                                            const LocalItem *__restrict__ items, uint32_t shift,
                                                            uint32_t bits, uint32_t *__restrict__ itemHist,
@@ -944,16 +968,20 @@ __global__ __launch_bounds__(NT) void localHistogramKernel(const void *__restric
 }
 
 void localHistogram(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift,
-                    uint32_t bits, uint32_t *itemHist, hipStream_t s, uint32_t sampleStride) {
+                    uint32_t bits, uint32_t *itemHist, hipStream_t s, uint32_t sampleStride, bool frag) {
   HJ_CHECK(bits <= MAX_PART_BITS, "localHistogram: bits=%u out of range", bits);
   HJ_CHECK(sampleStride >= 1, "localHistogram: sampleStride must be >= 1");
+  HJ_CHECK(!(wide && frag), "localHistogram: fragments are not wide tuples");
   if (nItems == 0) return;
   const size_t lds = size_t(4) << bits << 2;
-  if (wide)
-    hipLaunchKernelGGL(localHistogramKernel<true>, dim3(nItems), dim3(NT), lds, s, in, items, shift, bits, itemHist,
+  if (frag)
+    hipLaunchKernelGGL(localHistogramKernel<2>, dim3(nItems), dim3(NT), lds, s, in, items, shift, bits, itemHist,
+                       sampleStride);
+  else if (wide)
+    hipLaunchKernelGGL(localHistogramKernel<1>, dim3(nItems), dim3(NT), lds, s, in, items, shift, bits, itemHist,
                        sampleStride);
   else
-    hipLaunchKernelGGL(localHistogramKernel<false>, dim3(nItems), dim3(NT), lds, s, in, items, shift, bits, itemHist,
+    hipLaunchKernelGGL(localHistogramKernel<0>, dim3(nItems), dim3(NT), lds, s, in, items, shift, bits, itemHist,
                        sampleStride);
   HIP_CHECK_LAUNCH();
 }
@@ -1168,6 +1196,7 @@ __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void localScatterClaim
 
 template <class P>
 static void setSplit(P &, const SplitLayout &) {}
+static void setSplit(LocalFragPol &p, const SplitLayout &sl) { p.fragShift = sl.fragShift; }
 static void setSplit(LocalSplitPol &p, const SplitLayout &sl) {
   p.hi = sl.hi;
   p.fragShift = sl.fragShift;
@@ -1189,15 +1218,16 @@ static void launchLocalSplitGeom(const void *in, const LocalItem *items, uint32_
 
 void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift, uint32_t bits,
                   void *gcur, bool narrow, void *out, hipStream_t s, const void *gend, SplitLayout split,
-                  uint32_t geometry) {
+                  uint32_t geometry, bool frag) {
   HJ_CHECK(!(wide && split.on), "localScatter: the split layout needs compressed input");
-  HJ_CHECK(!split.on || split.hi, "localScatter: split layout without a fragment column");
+  HJ_CHECK(!split.on || frag || split.hi, "localScatter: split layout without a fragment column");
+  HJ_CHECK(!(frag && wide), "localScatter: fragments are not wide tuples");
   HJ_CHECK(bits <= MAX_PART_BITS, "localScatter: bits=%u out of range", bits);
   if (nItems == 0) return;
   const uint32_t F = 1u << bits;
   const uint64_t mask = F - 1;
   const uint32_t grid = ((nItems + NGROUPS - 1) / NGROUPS) * NGROUPS;
-  if (geometry != 0 && split.on && !wide && !narrow && gend) {
+  if (geometry != 0 && split.on && !wide && !frag && !narrow && gend) {
     LocalSplitPol pol;
     pol.mask = mask;
     pol.shift = shift;
@@ -1228,7 +1258,9 @@ void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nI
                          reinterpret_cast<const typename P::InT *>(in), items, nItems, F, pol,                 \
                          reinterpret_cast<C *>(gcur), reinterpret_cast<typename P::OutT *>(out), nullptr);     \
   } while (0)
-  if (wide && narrow) HJ_LOCAL(LocalWidePol, uint32_t);
+  if (frag && narrow) HJ_LOCAL(LocalFragPol, uint32_t);
+  else if (frag) HJ_LOCAL(LocalFragPol, unsigned long long);
+  else if (wide && narrow) HJ_LOCAL(LocalWidePol, uint32_t);
   else if (wide) HJ_LOCAL(LocalWidePol, unsigned long long);
   else if (split.on && narrow) HJ_LOCAL(LocalSplitPol, uint32_t);
   else if (split.on) HJ_LOCAL(LocalSplitPol, unsigned long long);

@@ -135,6 +135,11 @@ void HashJoin::makeJoinPlan() {
       config.networkHistogram == core::HistogramMode::Sampled ||
       (config.networkHistogram == core::HistogramMode::Auto && small >= (16ull << 20));
   plan.sampledNetwork = numberOfNodes == 1 && ctx->onDevice() && plan.chunks == 1 && sampleable;
+  // Counting on the split layout reads only the u16 fragment column: the
+  // sampled network pass can then write u32 fragments and the local pass the
+  // fragment column alone (4 + 2 bytes per tuple instead of 8 + 6).
+  plan.fragments = plan.sampledNetwork && !plan.materialize && !plan.wide && !plan.keyOnly && plan.twoLevel &&
+                   plan.splitLocal && kernels::fragWordFits(plan.keyBits, plan.networkBits);
   // N > 1 pipelines (also on the host path, where they run in place: same
   // logic, covered by the CPU tests).
   plan.splitHistogram = config.splitHistogram && numberOfNodes > 1;
@@ -322,6 +327,7 @@ bool HashJoin::runBitmap(uint64_t t0) {
     // rank redoes the join with exact histograms, as do later joins.
     bitmapExact = true;
     plan.sampledNetwork = false;
+    plan.fragments = false;
     ++result.networkFallbacks;
     if (ctx->onDevice()) HIP_CHECK(hipEventRecord(ev[0], ctx->stream()));
     o = bj.run(true);

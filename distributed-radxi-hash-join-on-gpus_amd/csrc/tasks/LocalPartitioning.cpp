@@ -5,6 +5,7 @@
 #include "../performance/Clock.h"
 #include "../performance/Measurements.h"
 #include "../performance/Timeline.h"
+#include "../utils/Fault.h"
 #include "../utils/Hip.h"
 
 namespace hpcjoin {
@@ -84,12 +85,17 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
   lb[owned] = (uint32_t)it.size();
   const uint32_t nItems = (uint32_t)it.size();
   itemTotal += nItems;
-  const uint32_t shift = wide ? plan.networkBits : plan.keyShift;
+  // Count-only fragments (JoinPlan::fragments): the window holds u32 words
+  // key >> networkBits; the local digit is their low bits and the output is
+  // only the u16 fragment column (no rid column exists).
+  const bool frag = w->holdsFragments();
+  const uint32_t shift = frag ? 0 : wide ? plan.networkBits : plan.keyShift;
   // Split output columns (kernels.h, SplitLayout): device, compressed, planned to fit.
   kernels::SplitLayout split;
-  split.on = ctx->onDevice() && !wide && plan.splitLocal ? 1u : 0u;
-  split.fragShift = plan.fragShift;
-  const uint32_t ob = split.on ? 4 : tb;       // bytes per tuple of the main output column
+  split.on = ctx->onDevice() && !wide && (plan.splitLocal || frag) ? 1u : 0u;
+  split.fragShift = frag ? bits : plan.fragShift;
+  JOIN_ASSERT(!frag || (ctx->onDevice() && plan.twoLevel), "LocalPartitioning", "fragments need the device two-level path");
+  const uint32_t ob = frag ? 2 : split.on ? 4 : tb;  // bytes per tuple of the main output column
   const uint32_t align = split.on ? 64 : 16;   // slot granularity: whole 128-byte lines of every column
 
   uint32_t *itemHist = ctx->workspace().getArray<uint32_t>(std::max<uint64_t>(1, (uint64_t)nItems * F));
@@ -107,7 +113,8 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
     const uint32_t S = plan.localSampleStride;
     const uint64_t cap = kernels::localSampledCapacityBound(xp.recvTotal, P, S, align);
     void *sout = alloc(std::max<uint64_t>(cap, 1) * ob);
-    if (split.on) split.hi = static_cast<uint16_t *>(alloc(std::max<uint64_t>(cap, 1) * 2));
+    if (frag) split.hi = static_cast<uint16_t *>(sout);
+    else if (split.on) split.hi = static_cast<uint16_t *>(alloc(std::max<uint64_t>(cap, 1) * 2));
     uint32_t *caps = ctx->workspace().getArray<uint32_t>(std::max<uint64_t>(P, 1));
     auto *starts = ctx->workspace().getArray<unsigned long long>(std::max<uint64_t>(P, 1));
     void *scanWs = ctx->workspace().get(kernels::scanWorkspaceBytes(std::max<uint64_t>(P, 1)));
@@ -124,7 +131,7 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
     }
     performance::Measurements::add("LPHISTELEM", (double)(xp.recvTotal / S), "tuples");
     tl.begin("LPHISTCOMP", ctx->stream());
-    kernels::localHistogram(w->getData(), wide, dItems, nItems, shift, bits, itemHist, ctx->stream(), S);
+    kernels::localHistogram(w->getData(), wide, dItems, nItems, shift, bits, itemHist, ctx->stream(), S, frag);
     tl.end("LPHISTCOMP", ctx->stream());
     tl.begin("LPOFFSET", ctx->stream());
     kernels::localSampledLayout(itemHist, dLb, dItems, owned, bits, S, caps, starts, scanWs, gcur, gend, pbeg, cap,
@@ -132,7 +139,7 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
     tl.end("LPOFFSET", ctx->stream());
     tl.begin("LPPART", ctx->stream());
     kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, gcur, false, sout, ctx->stream(), gend,
-                          split, plan.localGeometry);
+                          split, plan.localGeometry, frag);
     tl.end("LPPART", ctx->stream());
     kernels::claimOverflow(gcur, gend, P, overflowFlag, ctx->stream());
     // Read back with the join's final synchronisation (the flag accumulates
@@ -144,7 +151,8 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
     return;
   }
   void *out = alloc(std::max<uint64_t>(xp.recvTotal, 1) * ob);
-  if (split.on) split.hi = static_cast<uint16_t *>(alloc(std::max<uint64_t>(xp.recvTotal, 1) * 2));
+  if (frag) split.hi = static_cast<uint16_t *>(out);
+  else if (split.on) split.hi = static_cast<uint16_t *>(alloc(std::max<uint64_t>(xp.recvTotal, 1) * 2));
   uint64_t *partBegin = ctx->workspace().getArray<uint64_t>((uint64_t)owned * F + 1);
   if (ctx->onDevice()) {
     const uint32_t streams = kernels::assignLocalStreams(it.data(), nItems);
@@ -162,14 +170,14 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
     }
     performance::Measurements::add("LPHISTELEM", (double)xp.recvTotal, "tuples");
     tl.begin("LPHISTCOMP", ctx->stream());
-    kernels::localHistogram(w->getData(), wide, dItems, nItems, shift, bits, itemHist, ctx->stream());
+    kernels::localHistogram(w->getData(), wide, dItems, nItems, shift, bits, itemHist, ctx->stream(), 1, frag);
     tl.end("LPHISTCOMP", ctx->stream());
     tl.begin("LPOFFSET", ctx->stream());
     kernels::localCursors(itemHist, dLb, owned, bits, dBase, dItems, gcur, narrow, partBegin, ctx->stream());
     tl.end("LPOFFSET", ctx->stream());
     tl.begin("LPPART", ctx->stream());
     kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, gcur, narrow, out, ctx->stream(), nullptr,
-                          split);
+                          split, 0, frag);
     tl.end("LPPART", ctx->stream());
   } else {
     uint64_t *itemCursors = ctx->workspace().getArray<uint64_t>(std::max<uint64_t>(1, (uint64_t)nItems * F));

@@ -106,7 +106,7 @@ void SampledNetworkPartitioning::layoutSide(int k) {
     x.sendTotal = n;
     x.scatterTotal = n;
     x.recvTotal = 0;
-    s.window.reset(new data::Window(x, cur, ctx, plan.wide));
+    s.window.reset(new data::Window(x, cur, ctx, plan.wide, plan.fragments ? 4u : 0u));
     // Claim cursors (slice starts) and slice ends, in the scatter's cursor width.
     const size_t cb = s.narrow ? 4 : 8;
     s.gcur = ctx->workspace().get((size_t)G * F * cb);
@@ -147,7 +147,10 @@ void SampledNetworkPartitioning::scatterSide(int k) {
   const int nm = s.narrow ? 1 : 0;
   const char *key = k == 0 ? "MIMAINPART" : "MOMAINPART";
   ctx->timeline().begin(key, ctx->stream());
-  if (plan.wide)
+  if (plan.fragments)  // count-only: u32 key fragments (key >> networkBits), no rid
+    kernels::netScatterFrag(s.relation->getData(), n, plan.networkBits, s.geom, 0, s.geom.blocks, s.gcur,
+                            static_cast<uint32_t *>(s.window->getData()), ctx->stream(), plan.keyBits, mix, s.gend, nm);
+  else if (plan.wide)
     kernels::netScatterWide(s.relation->getData(), n, plan.networkBits, s.geom, 0, s.geom.blocks, s.gcur,
                             static_cast<data::Tuple *>(s.window->getData()), ctx->stream(), mix, s.gend, nm);
   else

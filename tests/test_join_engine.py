@@ -312,6 +312,49 @@ def test_split_local_output(C, cuda, sampled, G):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("local", ["SAMPLED", "EXACT"])
+@pytest.mark.parametrize("dist", ["UNIQUE", "ZIPF", "MODULO"])
+def test_fragment_two_level(C, cuda, dist, local):
+    """Count-only two-level plan on fragments (JoinPlan::fragments): the
+    sampled network pass writes u32 key fragments, the local pass only the
+    u16 fragment column; counts equal the reference, duplicates included,
+    repeated runs included."""
+    cfg = C.JoinConfig()
+    cfg.bitmap_join = False
+    cfg.local_histogram = getattr(C.HistogramMode, local)
+    G = 20_000_003
+    res, exp, j = run_join(C, "cuda", G, G + 4321, dist, cfg=cfg, theta=0.9)
+    assert j.plan.fragments and j.plan.sampled_network and j.plan.split_local, j.plan
+    assert res["global_matches"] == exp and res["network_fallbacks"] == 0
+    for _ in range(2):
+        assert j.run()["global_matches"] == exp
+
+
+@pytest.mark.gpu
+def test_fragment_two_level_network_overflow(C, cuda):
+    """A sampled network pass that overflows on the fragment plan re-runs on
+    the exact 8-byte path (the local pass follows each window's format)."""
+    import torch
+    n = 1 << 22
+    i = torch.arange(n, device="cuda")
+    keys = i * 512 + (i // 4096) % 512
+    R = torch.stack([keys, i], 1).contiguous()
+    S = torch.stack([keys.flip(0), i], 1).contiguous()
+    ctx = C.ExecContext("device", 0, C.LocalCommunicator())
+    cfg = C.JoinConfig()
+    cfg.network_histogram = C.HistogramMode.SAMPLED
+    cfg.key_hashing = C.KeyHashing.OFF
+    cfg.network_bits, cfg.local_bits = 9, 6  # 31-bit keys: 16-bit fragments after both passes
+    cfg.bitmap_join = False
+    cfg.max_partition_blocks = 16
+    j = C.HashJoin(C.Relation.from_tensor(R, n), C.Relation.from_tensor(S, n), ctx, cfg)
+    assert j.plan.fragments, j.plan
+    res = j.run()
+    assert res["network_fallbacks"] == 1 and res["global_matches"] == n
+    assert j.run()["global_matches"] == n
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dist", ["UNIQUE", "ZIPF", "MODULO"])
 @pytest.mark.parametrize("split", [True, False])
 def test_direct_count_table(C, cuda, dist, split):
