@@ -1013,8 +1013,6 @@ __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeK
 // (1B x 1B sparse keys: 14 ms -> see profiles).  Only the counters are
 // cleared per item.
 constexpr int BPK_T = 256;
-constexpr int BPK_K = 8;
-constexpr int BPK_H = 4;
 constexpr uint32_t BPK_SLOTS = 4;
 
 size_t bpKeyLdsBytes(uint32_t rChunk) {
@@ -1022,10 +1020,25 @@ size_t bpKeyLdsBytes(uint32_t rChunk) {
   return slots * 8 + (slots / BPK_SLOTS) * 4 + 64;
 }
 
+// Bucket of a key-only word.  FOLD: xor-fold to 32 bits and one 32-bit
+// multiply (one quarter-rate v_mul instead of the three of a 64-bit product).
+template <bool FOLD>
+__device__ __forceinline__ uint32_t bpkBucket(uint64_t v, uint32_t bbits) {
+  if constexpr (FOLD)
+    return (((uint32_t)v ^ (uint32_t)(v >> 32)) * 0x9E3779B1u) >> (32 - bbits);
+  else
+    return hash64(v, bbits);
+}
+
 // (Measured and dropped: loading the next item's first batches during this
 // item's probe, build/probe 7.35 vs 6.30 ms; a split u32 + u16 column layout of
 // the local pass output for 44-bit fragments, 7.2 vs 6.0 ms.)
-__global__ __launch_bounds__(BPK_T, 4) void bpKeyCountKernel(BPArgs a, const BPItem *__restrict__ items,
+// T threads x K elements per batch (T * K = 2048); H elements' buckets in
+// flight per half-batch.  CLEAR: empty slots hold ~0 (never a key-only word,
+// which is at most 64 - networkBits bits), so the probe compares all four
+// slots without masking by the fill count.
+template <int T, int K, int H, bool FOLD, bool CLEAR, int MINW>
+__global__ __launch_bounds__(T, MINW) void bpKeyCountKernel(BPArgs a, const BPItem *__restrict__ items,
                                                              const uint32_t *__restrict__ nItemsPtr, uint32_t capacity) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t maxSlots = 1u << ceilLog2(2ull * a.rChunk);
@@ -1034,7 +1047,7 @@ __global__ __launch_bounds__(BPK_T, 4) void bpKeyCountKernel(BPArgs a, const BPI
   unsigned long long *wsum = reinterpret_cast<unsigned long long *>(fill + maxSlots / BPK_SLOTS);
   const uint64_t *R = static_cast<const uint64_t *>(a.R);
   const uint64_t *S = static_cast<const uint64_t *>(a.S);
-  constexpr uint32_t BATCH = BPK_T * BPK_K;
+  constexpr uint32_t BATCH = T * K;
   const uint32_t t = threadIdx.x;
   const uint32_t nItems = min(*nItemsPtr, capacity);
   uint64_t matches = 0;
@@ -1044,37 +1057,41 @@ __global__ __launch_bounds__(BPK_T, 4) void bpKeyCountKernel(BPArgs a, const BPI
     const uint32_t nr = (uint32_t)(min(a.partREnd[it.part], rb + a.rChunk) - rb);
     const uint64_t sb = a.partS[it.part] + (uint64_t)it.sChunk * a.sChunk;
     const uint32_t ns = (uint32_t)(min(a.partSEnd[it.part], sb + a.sChunk) - sb);
-    uint64_t rv[BPK_K], sv[BPK_K];
+    uint64_t rv[K], sv[K];
 #pragma unroll
-    for (int k = 0; k < BPK_K; ++k) {
-      const uint32_t i = k * BPK_T + t;
+    for (int k = 0; k < K; ++k) {
+      const uint32_t i = k * T + t;
       if (i < nr) rv[k] = R[rb + i];
       if (i < ns) sv[k] = S[sb + i];
     }
     uint32_t tbits = ceilLog2(2ull * nr);
     if (tbits < 6) tbits = 6;
     const uint32_t buckets = (1u << tbits) / BPK_SLOTS, bmask = buckets - 1;
-    for (uint32_t i = t; i < buckets; i += BPK_T) fill[i] = 0;
+    for (uint32_t i = t; i < buckets; i += T) fill[i] = 0;
+    if constexpr (CLEAR) {
+      ulonglong2 *t2 = reinterpret_cast<ulonglong2 *>(table);
+      for (uint32_t i = t; i < (1u << tbits) / 2; i += T) t2[i] = make_ulonglong2(~0ull, ~0ull);
+    }
     __syncthreads();
     // ---- build
     for (uint32_t b0 = 0; b0 < nr; b0 += BATCH) {
       if (b0) {
 #pragma unroll
-        for (int k = 0; k < BPK_K; ++k) {
-          const uint32_t i = b0 + k * BPK_T + t;
+        for (int k = 0; k < K; ++k) {
+          const uint32_t i = b0 + k * T + t;
           if (i < nr) rv[k] = R[rb + i];
         }
       }
-      uint32_t bk[BPK_K], pos[BPK_K];
+      uint32_t bk[K], pos[K];
 #pragma unroll
-      for (int k = 0; k < BPK_K; ++k) {
-        const bool valid = b0 + k * BPK_T + t < nr;
-        bk[k] = hash64(rv[k], tbits - 2);
+      for (int k = 0; k < K; ++k) {
+        const bool valid = b0 + k * T + t < nr;
+        bk[k] = bpkBucket<FOLD>(rv[k], tbits - 2);
         pos[k] = atomicAdd(&fill[bk[k]], valid ? 1u : 0u);  // branch-free: invalid lanes add 0
         pos[k] = valid ? pos[k] : 0xFFFFFFFFu;
       }
 #pragma unroll
-      for (int k = 0; k < BPK_K; ++k) {
+      for (int k = 0; k < K; ++k) {
         if (pos[k] == 0xFFFFFFFFu) continue;
         uint32_t b = bk[k], p = pos[k];
         while (p >= BPK_SLOTS) {  // home bucket full: the next one (its counter marks the pass)
@@ -1089,33 +1106,37 @@ __global__ __launch_bounds__(BPK_T, 4) void bpKeyCountKernel(BPArgs a, const BPI
     for (uint32_t b0 = 0; b0 < ns; b0 += BATCH) {
       if (b0) {
 #pragma unroll
-        for (int k = 0; k < BPK_K; ++k) {
-          const uint32_t i = b0 + k * BPK_T + t;
+        for (int k = 0; k < K; ++k) {
+          const uint32_t i = b0 + k * T + t;
           if (i < ns) sv[k] = S[sb + i];
         }
       }
-      // Two half-batches of BPK_H elements keep the 32-byte buckets of the
-      // in-flight reads within the register budget of 4 workgroups per CU.
+      // Groups of H elements keep the 32-byte buckets of the in-flight reads
+      // within the register budget.
 #pragma unroll
-      for (int h = 0; h < BPK_K / BPK_H; ++h) {
-        uint32_t bk[BPK_H], f[BPK_H];
-        ulonglong2 e0[BPK_H], e1[BPK_H];
+      for (int h = 0; h < K / H; ++h) {
+        uint32_t bk[H], f[H];
+        ulonglong2 e0[H], e1[H];
 #pragma unroll
-        for (int j = 0; j < BPK_H; ++j) {
-          bk[j] = hash64(sv[h * BPK_H + j], tbits - 2);
+        for (int j = 0; j < H; ++j) {
+          bk[j] = bpkBucket<FOLD>(sv[h * H + j], tbits - 2);
           f[j] = fill[bk[j]];
           const ulonglong2 *q = reinterpret_cast<const ulonglong2 *>(table + bk[j] * BPK_SLOTS);
           e0[j] = q[0];
           e1[j] = q[1];
         }
 #pragma unroll
-        for (int j = 0; j < BPK_H; ++j) {
-          const int k = h * BPK_H + j;
-          if (b0 + k * BPK_T + t >= ns) continue;
+        for (int j = 0; j < H; ++j) {
+          const int k = h * H + j;
+          if (b0 + k * T + t >= ns) continue;
           const uint64_t v = sv[k];
-          const uint32_t n = min(f[j], BPK_SLOTS);
-          uint32_t c = (n > 0 && e0[j].x == v) + (n > 1 && e0[j].y == v) + (n > 2 && e1[j].x == v) +
-                       (n > 3 && e1[j].y == v);
+          uint32_t c;
+          if constexpr (CLEAR) {
+            c = (e0[j].x == v) + (e0[j].y == v) + (e1[j].x == v) + (e1[j].y == v);
+          } else {
+            const uint32_t n = min(f[j], BPK_SLOTS);
+            c = (n > 0 && e0[j].x == v) + (n > 1 && e0[j].y == v) + (n > 2 && e1[j].x == v) + (n > 3 && e1[j].y == v);
+          }
           uint32_t b = bk[j], fb = f[j];
           while (fb > BPK_SLOTS) {  // elements passed through: continue in the next bucket
             b = (b + 1) & bmask;
@@ -1130,8 +1151,35 @@ __global__ __launch_bounds__(BPK_T, 4) void bpKeyCountKernel(BPArgs a, const BPI
     }
     __syncthreads();  // the next item clears the counters
   }
-  const unsigned long long total = blockReduceSum<BPK_T, unsigned long long>((unsigned long long)matches, wsum);
+  const unsigned long long total = blockReduceSum<T, unsigned long long>((unsigned long long)matches, wsum);
   if (t == 0 && total) atomicAdd(a.result, total);
+}
+
+// Key-count variant (HPCJOIN_KCOUNT, A/B switch).  Measured on MI355X, 1B x
+// 1B sparse 63-bit keys, build/probe ms: 0 = 256 x 8 (90 VGPRs, 16 waves per
+// CU) 6.07; 1 = 512 x 4, 2 buckets in flight (48 VGPRs, 32 waves per CU)
+// 4.99 -- the default; 2 = 1 + folded hash 4.88 (dropped as default: keys
+// whose halves are equal would all share one bucket); 3 = 2 + cleared slots
+// 4.98; 4 = 0 + folded hash + cleared slots 6.10; 5 = 512 x 4 with 4 buckets
+// in flight 5.41.
+static int keyCountVariant() {
+  static const int v = [] {
+    const char *e = std::getenv("HPCJOIN_KCOUNT");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+
+template <int T, int K, int H, bool FOLD, bool CLEAR, int MINW>
+static void launchKeyCount(const BPArgs &a, const BPItem *items, const uint32_t *nItems, uint32_t capacity,
+                           hipStream_t s) {
+  const size_t ldsK = bpKeyLdsBytes(a.rChunk);
+  HJ_CHECK(ldsK <= 160 * 1024, "buildProbe: key-only table %zu B exceeds 160 KiB (rChunk=%u)", ldsK, a.rChunk);
+  HJ_CHECK(T * K >= 2 * BPK_T, "buildProbe: key-count batch too small");
+  const uint32_t perCuK = (uint32_t)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / ldsK));
+  hipLaunchKernelGGL((bpKeyCountKernel<T, K, H, FOLD, CLEAR, MINW>), dim3(std::min<uint32_t>(capacity, 256 * perCuK)),
+                     dim3(T), ldsK, s, a, items, nItems, capacity);
+  HIP_CHECK_LAUNCH();
 }
 
 void buildProbe(const BPArgs &args, const BPItem *items, const uint32_t *nItems, uint32_t capacity, hipStream_t s) {
@@ -1150,12 +1198,14 @@ void buildProbe(const BPArgs &args, const BPItem *items, const uint32_t *nItems,
            "buildProbe: fragShift=%u < 32 (the rid field of a CompressedTuple is >= 32 bits)", a.fragShift);
   HJ_CHECK(!(a.keyOnly && (a.materialize || a.wide || a.split)), "buildProbe: key-only words count only, unsplit");
   if (bpMode(a) == BP_KCOUNT) {
-    const size_t ldsK = bpKeyLdsBytes(a.rChunk);
-    HJ_CHECK(ldsK <= 160 * 1024, "buildProbe: key-only table %zu B exceeds 160 KiB (rChunk=%u)", ldsK, a.rChunk);
-    const uint32_t perCuK = (uint32_t)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / ldsK));
-    hipLaunchKernelGGL(bpKeyCountKernel, dim3(std::min<uint32_t>(capacity, 256 * perCuK)), dim3(BPK_T), ldsK, s, a,
-                       items, nItems, capacity);
-    HIP_CHECK_LAUNCH();
+    switch (keyCountVariant()) {
+      case 2: launchKeyCount<512, 4, 2, true, false, 8>(a, items, nItems, capacity, s); break;
+      case 3: launchKeyCount<512, 4, 2, true, true, 8>(a, items, nItems, capacity, s); break;
+      case 4: launchKeyCount<256, 8, 4, true, true, 4>(a, items, nItems, capacity, s); break;
+      case 5: launchKeyCount<512, 4, 4, true, true, 8>(a, items, nItems, capacity, s); break;
+      case 0: launchKeyCount<256, 8, 4, false, false, 4>(a, items, nItems, capacity, s); break;
+      default: launchKeyCount<512, 4, 2, false, false, 8>(a, items, nItems, capacity, s); break;
+    }
     return;
   }
   if (bpMode(a) == BP_CCOUNT && a.split && bpDirect(a) && !a.itemCounts) {

@@ -205,6 +205,36 @@ def test_sparse64_join_auto_wide(C, dev):
     assert torch.equal(Rt[pairs[:, 0], 0], St[pairs[:, 1], 0])
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("dup", [1, 37, 3000])
+def test_key_only_count_duplicates(C, cuda, dup):
+    """KCOUNT build/probe (key-only words, bucketized LDS table) with every
+    inner key repeated `dup` times: long bucket pass-through chains (3000
+    copies overflow hundreds of 4-slot buckets) and partial batches; the
+    count equals a torch oracle."""
+    import torch
+    g = torch.Generator().manual_seed(dup)
+    nb = 3_000_000 // dup + 1
+    base = torch.randint(1 << 40, (1 << 62) - 1, (nb,), generator=g, dtype=torch.int64).unique()
+    rk = base.repeat_interleave(dup)[:3_000_000]
+    pick = torch.randint(0, base.numel(), (5_000_000,), generator=g)
+    miss = torch.randint(1 << 40, (1 << 62) - 1, (1_000_000,), generator=g, dtype=torch.int64)
+    sk = torch.cat([base[pick], miss])
+    sk = sk[torch.randperm(sk.numel(), generator=g)]
+    mult = torch.zeros(base.numel(), dtype=torch.int64)
+    mult.index_add_(0, torch.searchsorted(base, rk), torch.ones_like(rk))
+    pos = torch.searchsorted(base, sk).clamp(max=base.numel() - 1)
+    exp = int(torch.where(base[pos] == sk, mult[pos], torch.zeros_like(pos)).sum())
+    rows = lambda k: torch.stack([k, torch.arange(k.numel())], 1).contiguous().cuda()
+    R, S = rows(rk), rows(sk)
+    ctx = C.ExecContext("device", 0, C.LocalCommunicator())
+    cfg = C.JoinConfig()
+    j = C.HashJoin(C.Relation.from_tensor(R, R.shape[0]), C.Relation.from_tensor(S, S.shape[0]), ctx, cfg)
+    assert j.plan.key_only and not j.plan.bitmap_join, j.plan
+    for _ in range(2):
+        assert j.run()["global_matches"] == exp
+
+
 @pytest.mark.parametrize("dev", devices())
 @pytest.mark.parametrize("n_ranks", [2, 4])
 def test_sparse64_key_only_ranks(C, dev, n_ranks):
