@@ -42,8 +42,11 @@ class Workload:
         return C.Relation.expected_matches(i, self.inner_size, o, self.outer_size)
 
     def join_config(self):
+        """Default JoinConfig for this workload, HPCJOIN_<FIELD> environment
+        overrides applied (utils.config.config_from_dict)."""
+        from ..utils.config import config_from_dict
         C = require_native()
-        cfg = C.JoinConfig()
+        cfg = config_from_dict()
         if self.wide:
             cfg.format = C.TupleFormat.WIDE
         cfg.materialize = self.materialize
