@@ -99,6 +99,10 @@ void netHistogram(const data::Tuple *in, uint64_t n, uint32_t bits, const Partit
 // 2S, ... of its own range (estimates for the single-rank sampled network pass).
 // totals[g][d] (u64): blockHist summed over the workgroups of XCD group g.
 void netGroupTotals(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint64_t *totals, hipStream_t s);
+// Sampled [NGROUPS][F] totals: every sampleStride-th tile of each XCD group
+// (the tile set sampleScale() counts as seen); totals are cleared first.
+void netSampledTotals(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
+                      uint64_t *totals, hipStream_t s, KeyMix mix, uint32_t sampleStride);
 // totals[c][F] = sum of blockHist over the blocks of chunk c (blocksPerChunk each).
 void digitTotals(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint32_t blocksPerChunk,
                  uint32_t chunks, uint64_t *totals, hipStream_t s);
@@ -332,6 +336,9 @@ struct BitmapSlices {
   // Table: [F][groups] segment starts and lengths (device arrays).
   const uint64_t *segStart = nullptr, *segLen = nullptr;
   uint32_t groups = 0;
+  // Elements over all partitions (0 = unknown): picks the slice walk of the
+  // u32 kernels (one flat walk per partition when partitions are short).
+  uint64_t count = 0;
 };
 // u32 words of one partition's bitmap (a power of two >= 4).
 uint32_t bitmapWords(uint32_t bits);
