@@ -99,6 +99,11 @@ void netHistogram(const data::Tuple *in, uint64_t n, uint32_t bits, const Partit
 // 2S, ... of its own range (estimates for the single-rank sampled network pass).
 // totals[g][d] (u64): blockHist summed over the workgroups of XCD group g.
 void netGroupTotals(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint64_t *totals, hipStream_t s);
+// Tile stride of a sampled pass over n tuples into F digits: the requested
+// stride, lowered so that every (XCD group, digit) cell gets >= 32 sampled
+// tuples on average (small inputs; a cell sampled 0 times is the usual
+// overflow cause).
+uint32_t sampleStrideFor(const PartitionGeometry &g, uint64_t n, uint32_t F, uint32_t stride);
 // Sampled [NGROUPS][F] totals: every sampleStride-th tile of each XCD group
 // (the tile set sampleScale() counts as seen); totals are cleared first.
 void netSampledTotals(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,

@@ -110,6 +110,93 @@ void netHistogram(const data::Tuple *in, uint64_t n, uint32_t bits, const Partit
   HIP_CHECK_LAUNCH();
 }
 
+// ---------------------------------------- sampled per-(group, digit) totals
+// A sampled pass only needs per-(XCD group, digit) totals.  Group g's tiles
+// (those of blocks b = g mod NGROUPS, block by block) are numbered 0, 1, ...;
+// every stride-th of them is sampled, one workgroup per sampled tile, and its
+// LDS histogram is added into totals[g][d] with one device atomic per
+// non-empty digit.  Against netHistogram + netGroupTotals (every block of the
+// geometry runs, samples its own tiles and writes F block counts) this reads
+// 1/stride of the input at every size -- a block range shorter than stride
+// tiles still sampled one full tile, 1/15 of a 125M-tuple input -- and writes
+// no per-block array (47-57 us -> see profiles at 125M).  sampleScale()
+// computes the same tile set on the host.
+__host__ __device__ inline uint64_t sampledTile(uint64_t local, uint32_t g, uint32_t tpb) {
+  return ((local / tpb) * NGROUPS + g) * tpb + local % tpb;
+}
+
+__global__ __launch_bounds__(NT) void netSampledTotalsKernel(const ulonglong2 *__restrict__ in, uint64_t n,
+                                                             uint32_t tpb, uint32_t blocks, uint32_t bits,
+                                                             uint32_t stride, unsigned long long *__restrict__ totals,
+                                                             KeyMix mix) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t hsh[];
+  const uint32_t g = blockIdx.x % NGROUPS;
+  const uint64_t local = (uint64_t)(blockIdx.x / NGROUPS) * stride;
+  const uint64_t tile = sampledTile(local, g, tpb);
+  const uint64_t begin = tile * PART_TILE;
+  if (tile / tpb >= blocks || begin >= n) return;  // uniform over the workgroup
+  const uint64_t end = min(n, begin + PART_TILE);
+  const uint32_t F = 1u << bits, mask = F - 1;
+  for (uint32_t i = threadIdx.x; i < 4 * F; i += NT) hsh[i] = 0;
+  __syncthreads();
+  uint32_t *wh = hsh + (threadIdx.x / WAVE) * F;
+  uint64_t k[PART_ITEMS];
+#pragma unroll
+  for (int i = 0; i < (int)PART_ITEMS; ++i) {
+    const uint64_t idx = begin + (uint64_t)i * NT + threadIdx.x;
+    k[i] = idx < end ? mix.apply(in[idx].x) : 0;
+  }
+#pragma unroll
+  for (int i = 0; i < (int)PART_ITEMS; ++i) {
+    const uint64_t idx = begin + (uint64_t)i * NT + threadIdx.x;
+    if (idx < end) atomicAdd(&wh[k[i] & mask], 1u);
+  }
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < F; d += NT) {
+    const uint32_t c = hsh[d] + hsh[F + d] + hsh[2 * F + d] + hsh[3 * F + d];
+    if (c) atomicAdd(&totals[(uint64_t)g * F + d], (unsigned long long)c);
+  }
+}
+
+// Tiles of XCD group g in geometry gm (blocks b = g mod NGROUPS).
+static uint64_t groupTiles(const PartitionGeometry &gm, uint64_t n, uint32_t g) {
+  const uint64_t tiles = ceilDiv(n, PART_TILE);
+  uint64_t t = 0;
+  for (uint32_t b = g; b < gm.blocks; b += NGROUPS) {
+    const uint64_t b0 = (uint64_t)b * gm.tilesPerBlock;
+    if (b0 < tiles) t += std::min<uint64_t>(gm.tilesPerBlock, tiles - b0);
+  }
+  return t;
+}
+
+uint32_t sampleStrideFor(const PartitionGeometry &g, uint64_t n, uint32_t F, uint32_t stride) {
+  uint64_t minTiles = UINT64_MAX;
+  for (uint32_t gr = 0; gr < NGROUPS; ++gr) {
+    const uint64_t t = groupTiles(g, n, gr);
+    if (t) minTiles = std::min(minTiles, t);
+  }
+  if (minTiles == UINT64_MAX || stride <= 1) return 1;
+  const uint64_t most = minTiles * PART_TILE / (32ull * std::max<uint32_t>(F, 1));
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(stride, most));
+}
+
+void netSampledTotals(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
+                      uint64_t *totals, hipStream_t s, KeyMix mix, uint32_t sampleStride) {
+  HJ_CHECK(bits >= 1 && bits <= MAX_PART_BITS, "netSampledTotals: bits=%u out of range", bits);
+  HJ_CHECK(sampleStride >= 1, "netSampledTotals: sampleStride must be >= 1");
+  const uint32_t F = 1u << bits;
+  HIP_CHECK(hipMemsetAsync(totals, 0, (size_t)NGROUPS * F * sizeof(uint64_t), s));
+  uint64_t perGroup = 0;  // sampled tiles of the largest group
+  for (uint32_t gr = 0; gr < NGROUPS; ++gr) perGroup = std::max(perGroup, ceilDiv(groupTiles(g, n, gr), sampleStride));
+  if (perGroup == 0) return;
+  HJ_CHECK(perGroup * NGROUPS < (1ull << 31), "netSampledTotals: %llu sampled tiles", (unsigned long long)perGroup);
+  const size_t lds = size_t(4) << bits << 2;
+  hipLaunchKernelGGL(netSampledTotalsKernel, dim3((uint32_t)(perGroup * NGROUPS)), dim3(NT), lds, s,
+                     reinterpret_cast<const ulonglong2 *>(in), n, g.tilesPerBlock, g.blocks, bits, sampleStride,
+                     reinterpret_cast<unsigned long long *>(totals), mix);
+  HIP_CHECK_LAUNCH();
+}
+
 // --------------------------------------------------- digit totals / cursors
 __global__ __launch_bounds__(NT) void digitTotalsKernel(const uint32_t *__restrict__ blockHist, uint32_t F,
                                                         uint32_t blocks, uint32_t bpc, uint64_t *totals) {
@@ -752,7 +839,9 @@ __global__ __launch_bounds__(LAY_NT) void netSampledLayoutKernel(const unsigned 
       if (seen > 0) {
         const double scale = total / seen;
         const double est = (double)sampled[(size_t)g * F + d] * scale;
-        const double margin = sc.sigmas * sqrt(fmax(est, 1.0) * scale) + sc.frac * est + sc.floor;
+        // sigma of a count scaled by `scale` from k samples: scale * sqrt(k);
+        // at least one sample's worth (k = 0 says little about a cell).
+        const double margin = sc.sigmas * sqrt(fmax(est, scale) * scale) + sc.frac * est + sc.floor;
         c = fmin(ceil(est + margin), total);
       }
       cap[k] = ((unsigned long long)c + 15ull) & ~15ull;
@@ -799,10 +888,15 @@ SampleScale sampleScale(const PartitionGeometry &g, uint64_t n, uint32_t sampleS
   const uint64_t span = (uint64_t)g.tilesPerBlock * PART_TILE;
   for (uint32_t b = 0; b < g.blocks; ++b) {
     const uint64_t begin = (uint64_t)b * span, end = std::min(n, begin + span);
-    if (begin >= end) continue;
-    sc.total[b % NGROUPS] += (double)(end - begin);
-    for (uint64_t t = begin; t < end; t += (uint64_t)PART_TILE * sampleStride)
-      sc.seen[b % NGROUPS] += (double)std::min<uint64_t>(PART_TILE, end - t);
+    if (begin < end) sc.total[b % NGROUPS] += (double)(end - begin);
+  }
+  // The tiles netSampledTotals reads (every tile when sampleStride == 1).
+  for (uint32_t gr = 0; gr < NGROUPS; ++gr) {
+    const uint64_t tiles = groupTiles(g, n, gr);
+    for (uint64_t local = 0; local < tiles; local += sampleStride) {
+      const uint64_t begin = sampledTile(local, gr, g.tilesPerBlock) * PART_TILE;
+      if (begin < n) sc.seen[gr] += (double)std::min<uint64_t>(PART_TILE, n - begin);
+    }
   }
   if (exact) {
     sc.sigmas = sc.frac = sc.floor = 0;
@@ -815,14 +909,14 @@ SampleScale sampleScale(const PartitionGeometry &g, uint64_t n, uint32_t sampleS
 }
 
 uint64_t sampledLayoutCapacityBound(const SampleScale &sc, uint32_t F) {
-  // Per group: sum_d est_d = total_g; sum_d sqrt(max(est_d,1) * scale) <=
-  // sqrt(F * scale * (total_g + F)) (Cauchy-Schwarz); + ceil and the 16-tuple
+  // Per group: sum_d est_d = total_g; sum_d sqrt(max(est_d,scale) * scale) <=
+  // sqrt(F * scale * (total_g + F * scale)) (Cauchy-Schwarz); + ceil and the 16-tuple
   // line rounding per slice.
   double b = 0;
   for (uint32_t g = 0; g < NGROUPS; ++g) {
     if (sc.total[g] <= 0) continue;
     const double scale = sc.seen[g] > 0 ? sc.total[g] / sc.seen[g] : 1.0;
-    b += (1.0 + sc.frac) * sc.total[g] + sc.sigmas * std::sqrt((double)F * scale * (sc.total[g] + F)) +
+    b += (1.0 + sc.frac) * sc.total[g] + sc.sigmas * std::sqrt((double)F * scale * (sc.total[g] + F * scale)) +
          (sc.floor + 17.0) * F;
   }
   return (uint64_t)(b * 1.0001) + 4096;

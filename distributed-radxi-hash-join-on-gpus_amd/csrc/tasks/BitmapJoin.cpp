@@ -36,14 +36,14 @@ BitmapJoin::Outcome BitmapJoin::run(bool exact) { return ctx->onDevice() ? runDe
 bool BitmapJoin::sideNarrow(data::Relation *r, bool exact) const {
   const uint64_t n = r->getLocalSize();
   const kernels::PartitionGeometry g = kernels::partitionGeometry(n, maxBlocks);
-  const kernels::SampleScale sc = kernels::sampleScale(g, n, exact ? 1 : sampleStride, exact);
+  const uint32_t stride = exact ? 1 : kernels::sampleStrideFor(g, n, 1u << plan.networkBits, sampleStride);
+  const kernels::SampleScale sc = kernels::sampleScale(g, n, stride, exact);
   return kernels::cursorsNarrow(kernels::sampledLayoutCapacityBound(sc, 1u << plan.networkBits) + n);
 }
 
 void BitmapJoin::partitionSide(Side &s, bool exact, bool narrowOk) {
   const uint32_t bits = plan.networkBits, F = 1u << bits, G = CLAIM_GROUPS;
   const uint64_t n = s.relation->getLocalSize();
-  const uint32_t stride = exact ? 1 : sampleStride;
   memory::Arena &ws = ctx->workspace();
   const hipStream_t st = ctx->stream();
   const kernels::KeyMix mix{plan.keyMix ? 1u : 0u, plan.keyBits};
@@ -51,10 +51,15 @@ void BitmapJoin::partitionSide(Side &s, bool exact, bool narrowOk) {
   performance::Timeline &tl = ctx->timeline();
   tl.begin(isInner ? "HILOCAL" : "HOLOCAL", st);
   s.geom = kernels::partitionGeometry(n, maxBlocks);
-  uint32_t *blockHist = ws.getArray<uint32_t>((uint64_t)F * s.geom.blocks);
+  const uint32_t stride = exact ? 1 : kernels::sampleStrideFor(s.geom, n, F, sampleStride);
   uint64_t *totals = ws.getArray<uint64_t>((uint64_t)G * F);
-  kernels::netHistogram(s.relation->getData(), n, bits, s.geom, blockHist, st, mix, stride);
-  kernels::netGroupTotals(blockHist, F, s.geom.blocks, totals, st);
+  if (stride > 1) {
+    kernels::netSampledTotals(s.relation->getData(), n, bits, s.geom, totals, st, mix, stride);
+  } else {
+    uint32_t *blockHist = ws.getArray<uint32_t>((uint64_t)F * s.geom.blocks);
+    kernels::netHistogram(s.relation->getData(), n, bits, s.geom, blockHist, st, mix, 1);
+    kernels::netGroupTotals(blockHist, F, s.geom.blocks, totals, st);
+  }
   const kernels::SampleScale sc = kernels::sampleScale(s.geom, n, stride, exact);
   const uint64_t cap = kernels::sampledLayoutCapacityBound(sc, F);
   // Claims may run past a slice end by up to n before the overflow is seen.
@@ -75,6 +80,7 @@ void BitmapJoin::partitionSide(Side &s, bool exact, bool narrowOk) {
   s.slices.cur = gcur;
   s.slices.end = gend;
   s.slices.narrow = narrow;
+  s.slices.count = n;
 }
 
 BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {

@@ -32,11 +32,16 @@ void SampledNetworkPartitioning::sample() {
     ctx->timeline().begin(key, ctx->stream());
     const uint64_t n = s.relation->getLocalSize();
     s.geom = kernels::partitionGeometry(n, maxBlocks);
-    uint32_t *blockHist = ctx->workspace().getArray<uint32_t>((uint64_t)F * s.geom.blocks);
+    s.stride = kernels::sampleStrideFor(s.geom, n, F, sampleStride);
     s.groupTotalsDev = ctx->workspace().getArray<uint64_t>((uint64_t)CLAIM_GROUPS * F);
-    kernels::netHistogram(s.relation->getData(), n, plan.networkBits, s.geom, blockHist, ctx->stream(), mix,
-                          sampleStride);
-    kernels::netGroupTotals(blockHist, F, s.geom.blocks, s.groupTotalsDev, ctx->stream());
+    if (s.stride > 1) {
+      kernels::netSampledTotals(s.relation->getData(), n, plan.networkBits, s.geom, s.groupTotalsDev, ctx->stream(),
+                                mix, s.stride);
+    } else {
+      uint32_t *blockHist = ctx->workspace().getArray<uint32_t>((uint64_t)F * s.geom.blocks);
+      kernels::netHistogram(s.relation->getData(), n, plan.networkBits, s.geom, blockHist, ctx->stream(), mix, 1);
+      kernels::netGroupTotals(blockHist, F, s.geom.blocks, s.groupTotalsDev, ctx->stream());
+    }
     ctx->timeline().end(key, ctx->stream());
     s.sampled = ctx->staging().getArray<uint64_t>((uint64_t)CLAIM_GROUPS * F);
     HIP_CHECK(hipMemcpyAsync(s.sampled, s.groupTotalsDev, (size_t)CLAIM_GROUPS * F * 8, hipMemcpyDeviceToHost,
@@ -58,15 +63,7 @@ void SampledNetworkPartitioning::layoutSide(int k) {
     HIP_CHECK(hipEventSynchronize(s.sampledReady));
     const uint64_t n = s.relation->getLocalSize();
     // Tuples each group scatters, and how many of them the sample read.
-    std::vector<double> total(G, 0.0), seen(G, 0.0);
-    const uint64_t span = (uint64_t)s.geom.tilesPerBlock * kernels::PART_TILE;
-    for (uint32_t b = 0; b < s.geom.blocks; ++b) {
-      const uint64_t begin = (uint64_t)b * span, end = std::min(n, begin + span);
-      if (begin >= end) continue;
-      total[b % G] += (double)(end - begin);
-      for (uint64_t t = begin; t < end; t += (uint64_t)kernels::PART_TILE * sampleStride)
-        seen[b % G] += (double)std::min<uint64_t>(kernels::PART_TILE, end - t);
-    }
+    const kernels::SampleScale sc = kernels::sampleScale(s.geom, n, s.stride, false);
     s.start.assign((size_t)G * F, 0);
     s.cap.assign((size_t)G * F, 0);
     uint64_t cur = 0;
@@ -74,13 +71,14 @@ void SampledNetworkPartitioning::layoutSide(int k) {
       for (uint32_t g = 0; g < G; ++g) {
         const size_t i = (size_t)g * F + d;
         double est = 0;
-        if (seen[g] > 0) est = (double)s.sampled[i] * total[g] / seen[g];
-        // Sampling error of a count scaled by total/seen is ~sqrt(est * total/seen);
-        // 6 sigma + 2% + a fixed floor keeps overflows (and their exact re-run) rare.
-        const double scale = seen[g] > 0 ? total[g] / seen[g] : 1.0;
-        const double margin = 6.0 * std::sqrt(std::max(est, 1.0) * scale) + 0.02 * est + 256.0;
+        if (sc.seen[g] > 0) est = (double)s.sampled[i] * sc.total[g] / sc.seen[g];
+        // Sampling error of a count scaled by total/seen is ~sqrt(est * total/seen)
+        // (at least one sample's worth); 6 sigma + 2% + a fixed floor keeps
+        // overflows (and their exact re-run) rare.
+        const double scale = sc.seen[g] > 0 ? sc.total[g] / sc.seen[g] : 1.0;
+        const double margin = sc.sigmas * std::sqrt(std::max(est, scale) * scale) + sc.frac * est + sc.floor;
         // whole 128-byte lines per slice (16 tuples): slices never share a line
-        const uint64_t cap = (std::min<uint64_t>((uint64_t)std::ceil(est + margin), (uint64_t)total[g]) + 15) & ~15ull;
+        const uint64_t cap = (std::min<uint64_t>((uint64_t)std::ceil(est + margin), (uint64_t)sc.total[g]) + 15) & ~15ull;
         s.start[i] = cur;
         s.cap[i] = cap;
         cur += cap;

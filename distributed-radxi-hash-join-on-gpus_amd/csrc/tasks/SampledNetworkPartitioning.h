@@ -59,6 +59,7 @@ class SampledNetworkPartitioning {
   struct Side {
     data::Relation *relation = nullptr;
     kernels::PartitionGeometry geom;
+    uint32_t stride = 1;  // sampled tile stride (kernels::sampleStrideFor)
     histograms::ExchangePlan xp;
     std::unique_ptr<data::Window> window;
     uint64_t *groupTotalsDev = nullptr;
