@@ -1,5 +1,6 @@
 #include "Timeline.h"
 
+#include <cstdlib>
 #include <map>
 
 #include "../utils/Hip.h"
@@ -27,7 +28,18 @@ void Timeline::reset() {
   used_ = 0;
 }
 
+// HPCJOIN_TIMELINE=0: no device sub-phase events (their keys stay 0); for
+// measuring what the timing events cost inside a join.
+static bool timelineOff() {
+  static const bool off = [] {
+    const char *e = std::getenv("HPCJOIN_TIMELINE");
+    return e && std::atoi(e) == 0;
+  }();
+  return off;
+}
+
 void Timeline::begin(const char *key, hipStream_t s) {
+  if (device_ && timelineOff()) return;
   Span sp;
   sp.key = key;
   if (device_) {
@@ -41,6 +53,7 @@ void Timeline::begin(const char *key, hipStream_t s) {
 
 void Timeline::beginSplit(const char *key, const char *a, double wa, const char *b, double wb, hipStream_t s) {
   begin(key, s);
+  if (device_ && timelineOff()) return;
   spans_.back().ka = a;
   spans_.back().kb = b;
   spans_.back().wa = wa;
@@ -48,6 +61,7 @@ void Timeline::beginSplit(const char *key, const char *a, double wa, const char 
 }
 
 void Timeline::end(const char *key, hipStream_t s) {
+  if (device_ && timelineOff()) return;
   for (auto it = spans_.rbegin(); it != spans_.rend(); ++it) {
     if (it->closed || it->key != key) continue;
     if (device_) {
@@ -60,6 +74,47 @@ void Timeline::end(const char *key, hipStream_t s) {
     return;
   }
   JOIN_ASSERT(false, "Timeline", "end(%s) without begin", key);
+}
+
+hipEvent_t Timeline::mark(hipStream_t s) {
+  if (!device_ || timelineOff()) return nullptr;
+  hipEvent_t e = event();
+  HIP_CHECK(hipEventRecord(e, s));
+  return e;
+}
+
+void Timeline::beginAt(const char *key, hipEvent_t at) {
+  if (device_ && timelineOff()) return;
+  Span sp;
+  sp.key = key;
+  if (device_)
+    sp.b = at;
+  else
+    sp.hb = nowUs();
+  spans_.push_back(sp);
+}
+
+void Timeline::beginSplitAt(const char *key, const char *a, double wa, const char *b, double wb, hipEvent_t at) {
+  beginAt(key, at);
+  if (device_ && timelineOff()) return;
+  spans_.back().ka = a;
+  spans_.back().kb = b;
+  spans_.back().wa = wa;
+  spans_.back().wb = wb;
+}
+
+void Timeline::endAt(const char *key, hipEvent_t at) {
+  if (device_ && timelineOff()) return;
+  for (auto it = spans_.rbegin(); it != spans_.rend(); ++it) {
+    if (it->closed || it->key != key) continue;
+    if (device_)
+      it->e = at;
+    else
+      it->he = nowUs();
+    it->closed = true;
+    return;
+  }
+  JOIN_ASSERT(false, "Timeline", "endAt(%s) without begin", key);
 }
 
 void Timeline::resolve() {

@@ -32,6 +32,16 @@ class Timeline {
   // One span charged to two keys in proportion wa : wb (a fused kernel doing
   // two reference phases, e.g. build + probe of one LDS table).
   void beginSplit(const char *key, const char *a, double wa, const char *b, double wb, hipStream_t s = nullptr);
+  // Shared time points (device): mark() records one event on s; spans can
+  // begin / end at an existing event, so back-to-back spans (one phase ends
+  // where the next begins) cost one event instead of two.  Every timing event
+  // is a packet the stream waits on (~4-5 us each: 17 per bitmap join were
+  // 50 us of a 1.4 ms join at 125M, profiles/r2s).  Host path: mark() returns
+  // nullptr and the *At calls take the host clock.
+  hipEvent_t mark(hipStream_t s = nullptr);
+  void beginAt(const char *key, hipEvent_t at);
+  void endAt(const char *key, hipEvent_t at);
+  void beginSplitAt(const char *key, const char *a, double wa, const char *b, double wb, hipEvent_t at);
   void resolve();                                 // after the final sync: spans -> Measurements (µs, summed)
 
  private:

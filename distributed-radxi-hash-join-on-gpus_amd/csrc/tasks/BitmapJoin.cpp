@@ -41,7 +41,7 @@ bool BitmapJoin::sideNarrow(data::Relation *r, bool exact) const {
   return kernels::cursorsNarrow(kernels::sampledLayoutCapacityBound(sc, 1u << plan.networkBits) + n);
 }
 
-void BitmapJoin::partitionSide(Side &s, bool exact, bool narrowOk) {
+void BitmapJoin::partitionSide(Side &s, bool exact, bool narrowOk, hipEvent_t from, hipEvent_t to) {
   const uint32_t bits = plan.networkBits, F = 1u << bits, G = CLAIM_GROUPS;
   const uint64_t n = s.relation->getLocalSize();
   memory::Arena &ws = ctx->workspace();
@@ -49,7 +49,8 @@ void BitmapJoin::partitionSide(Side &s, bool exact, bool narrowOk) {
   const kernels::KeyMix mix{plan.keyMix ? 1u : 0u, plan.keyBits};
   const bool isInner = s.relation == inner;
   performance::Timeline &tl = ctx->timeline();
-  tl.begin(isInner ? "HILOCAL" : "HOLOCAL", st);
+  const char *histKey = isInner ? "HILOCAL" : "HOLOCAL", *partKey = isInner ? "MIMAINPART" : "MOMAINPART";
+  tl.beginAt(histKey, from);
   s.geom = kernels::partitionGeometry(n, maxBlocks);
   const uint32_t stride = exact ? 1 : kernels::sampleStrideFor(s.geom, n, F, sampleStride);
   uint64_t *totals = ws.getArray<uint64_t>((uint64_t)G * F);
@@ -68,12 +69,14 @@ void BitmapJoin::partitionSide(Side &s, bool exact, bool narrowOk) {
   void *gstart = ws.get((size_t)G * F * cb), *gcur = ws.get((size_t)G * F * cb), *gend = ws.get((size_t)G * F * cb);
   unsigned long long *used = ws.getArray<unsigned long long>(1);
   kernels::netSampledLayout(totals, F, sc, gstart, gcur, gend, narrow, used, st);
-  tl.end(isInner ? "HILOCAL" : "HOLOCAL", st);
+  hipEvent_t mid = tl.mark(st);  // one event ends the histogram and begins the scatter
+  tl.endAt(histKey, mid);
   s.frags = ws.getArray<uint32_t>(std::max<uint64_t>(cap, 16));
-  tl.begin(isInner ? "MIMAINPART" : "MOMAINPART", st);
+  tl.beginAt(partKey, mid);
   kernels::netScatterFrag(s.relation->getData(), n, bits, s.geom, 0, s.geom.blocks, gcur, s.frags, st, plan.keyBits,
                           mix, gend, narrow ? 1 : 0);
-  tl.end(isInner ? "MIMAINPART" : "MOMAINPART", st);
+  if (to) HIP_CHECK(hipEventRecord(to, st));
+  tl.endAt(partKey, to);
   s.slices = BitmapSlices();
   s.slices.kind = BitmapSlices::Claim;
   s.slices.start = gstart;
@@ -94,60 +97,71 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
   // One cursor width for both sides (the fused N = 1 kernel reads both with
   // one slice type; e.g. 1B inner x 4B outer needs 8-byte cursors on both).
   const bool narrowOk = sideNarrow(inner, exact) && sideNarrow(outer, exact);
+  // Time points (one event each, shared by the spans that meet there):
+  // ev[0] join start, ev[1] inner side partitioned, ev[2] outer side
+  // partitioned, ev[3] probe start (N > 1: after the all-reduce), ev[4] end.
+  performance::Timeline &tl = ctx->timeline();
   {
     performance::TraceRange tr("bitmap_network_inner");
     utils::faultPoint("network");
-    partitionSide(si, exact, narrowOk);
+    partitionSide(si, exact, narrowOk, ev[0], ev[1]);
   }
-  HIP_CHECK(hipEventRecord(ev[1], st));
+  hipEvent_t joinStart = ev[2];
   if (N == 1) {
-    partitionSide(so, exact, narrowOk);
-    HIP_CHECK(hipEventRecord(ev[2], st));
-    HIP_CHECK(hipEventRecord(ev[3], st));
+    partitionSide(so, exact, narrowOk, ev[1], ev[2]);
     utils::faultPoint("local");
     utils::faultPoint("build_probe");
     // One kernel builds and probes: charged to BPBUILD / BPPROBE by tuples read.
-    ctx->timeline().begin("BPTASKTIME", st);
-    ctx->timeline().beginSplit("BPKERNEL", "BPBUILD", (double)inner->getLocalSize(), "BPPROBE",
-                               (double)outer->getLocalSize(), st);
+    tl.beginAt("BPTASKTIME", ev[2]);
+    tl.beginSplitAt("BPKERNEL", "BPBUILD", (double)inner->getLocalSize(), "BPPROBE", (double)outer->getLocalSize(),
+                    ev[2]);
     kernels::bitmapJoin(4, si.frags, so.frags, si.slices, so.slices, F, 0, bits, cnt, st);
-    ctx->timeline().end("BPKERNEL", st);
-    ctx->timeline().end("BPTASKTIME", st);
+    HIP_CHECK(hipEventRecord(ev[4], st));
+    tl.endAt("BPKERNEL", ev[4]);
+    tl.endAt("BPTASKTIME", ev[4]);
   } else {
     const uint32_t words = kernels::bitmapWords(bits);
     uint32_t *bm = ws.getArray<uint32_t>((size_t)F * words);
     utils::faultPoint("local");
-    performance::Timeline &tl = ctx->timeline();
-    tl.begin("BPTASKTIME", st);
-    tl.begin("BPBUILD", st);
+    tl.beginAt("BPTASKTIME", ev[1]);
+    tl.beginAt("BPBUILD", ev[1]);
     kernels::bitmapBuild(4, si.frags, si.slices, F, 0, bits, bm, cnt, st);
-    tl.end("BPBUILD", st);
-    hipEvent_t built = ctx->acquireEvent(), reduced = ctx->acquireEvent();
-    HIP_CHECK(hipEventRecord(built, st));
+    // A time point the streams also synchronise on (a timing event when the
+    // timeline is on, a pooled sync-only event otherwise).
+    auto point = [&](hipStream_t s) {
+      hipEvent_t e = tl.mark(s);
+      if (!e) {
+        e = ctx->acquireEvent();
+        HIP_CHECK(hipEventRecord(e, s));
+      }
+      return e;
+    };
+    hipEvent_t built = point(st);
+    tl.endAt("BPBUILD", built);
     HIP_CHECK(hipStreamWaitEvent(ctx->commStream(), built, 0));
     // The all-reduce (exchange stream) overlaps the outer side's network pass:
     // the plan's one link transfer (the reference's puts, MWINPUT).
     performance::Measurements::add("MWINPUTCNT", 1, "calls");
-    tl.begin("MWINPUT", ctx->commStream());
+    tl.beginAt("MWINPUT", built);
     ctx->comm()->allReduceSumDevice(reinterpret_cast<uint64_t *>(bm), (size_t)F * words / 2, ctx->commStream());
-    tl.end("MWINPUT", ctx->commStream());
-    HIP_CHECK(hipEventRecord(reduced, ctx->commStream()));
+    hipEvent_t reduced = point(ctx->commStream());
+    tl.endAt("MWINPUT", reduced);
     o.linkBytes = (uint64_t)(2.0 * (N - 1) / N * (double)F * words * 4);
-    partitionSide(so, exact, narrowOk);
-    HIP_CHECK(hipEventRecord(ev[2], st));
+    partitionSide(so, exact, narrowOk, built, ev[2]);
     HIP_CHECK(hipStreamWaitEvent(st, reduced, 0));
     HIP_CHECK(hipEventRecord(ev[3], st));
+    joinStart = ev[3];
     utils::faultPoint("build_probe");
-    tl.begin("BPPROBE", st);
+    tl.beginAt("BPPROBE", ev[3]);
     kernels::bitmapProbe(4, so.frags, so.slices, F, 0, bits, bm, cnt, st);
-    tl.end("BPPROBE", st);
-    tl.end("BPTASKTIME", st);
+    HIP_CHECK(hipEventRecord(ev[4], st));
+    tl.endAt("BPPROBE", ev[4]);
+    tl.endAt("BPTASKTIME", ev[4]);
   }
   performance::Measurements::add("BPBUILDELEM", (double)inner->getLocalSize(), "tuples");
   performance::Measurements::add("BPPROBEELEM", (double)outer->getLocalSize(), "tuples");
   performance::Measurements::add("BPMEMSIZE", (double)(N > 1 ? (uint64_t)F * kernels::bitmapWords(bits) * 4 : 0),
                                  "bytes");
-  HIP_CHECK(hipEventRecord(ev[4], st));
   BitmapCounters *back = ctx->staging().getArray<BitmapCounters>(1);
   HIP_CHECK(hipMemcpyAsync(back, cnt, sizeof(BitmapCounters), hipMemcpyDeviceToHost, st));
   ctx->synchronize();
@@ -156,7 +170,7 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
   o.devSampleMs = ms;
   HIP_CHECK(hipEventElapsedTime(&ms, ev[1], ev[2]));
   o.devScatterMs = ms;
-  HIP_CHECK(hipEventElapsedTime(&ms, ev[3], ev[4]));
+  HIP_CHECK(hipEventElapsedTime(&ms, joinStart, ev[4]));
   o.devJoinMs = ms;
   o.localMatches = back->matches;
   o.popcount = back->popcount;

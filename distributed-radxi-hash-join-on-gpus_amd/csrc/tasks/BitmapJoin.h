@@ -71,7 +71,9 @@ class BitmapJoin {
   };
   // narrowOk: 4-byte claim cursors are allowed (both sides of a fused bitmap
   // join must use the same cursor width; sideNarrow() says what one side needs).
-  void partitionSide(Side &s, bool exact, bool narrowOk);
+  // Device: the side's spans run from `from` (already recorded) to `to`,
+  // which is recorded on the compute stream when its scatter is enqueued.
+  void partitionSide(Side &s, bool exact, bool narrowOk, hipEvent_t from = nullptr, hipEvent_t to = nullptr);
   bool sideNarrow(data::Relation *r, bool exact) const;
   Outcome runDevice(bool exact);
   Outcome runHost();

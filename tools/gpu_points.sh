@@ -1,0 +1,17 @@
+#!/bin/bash
+# Shared timeline points in the bitmap join: full GPU suite, then 125M / 1B
+# joins with the timeline on (default) and off, a kernel trace at 125M.
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
+TAG=${1:-pts}
+timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1 || { tail -30 gpurun_out/${TAG}_pytest.log; exit 1; }
+tail -1 gpurun_out/${TAG}_pytest.log
+for size in 1.25e8 1e9; do
+  for tl in 1 0; do
+    L=gpurun_out/${TAG}_${size}_${tl}.log
+    HPCJOIN_TIMELINE=$tl timeout -k 10 200 python bench.py --inner $size --outer $size --steps 20 --warmup 3 --general off > $L 2>&1 || { tail -20 $L; exit 1; }
+    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], 'timeline', sys.argv[3], d['ms_per_step'], d['correct'], d['phases_ms'])" $L $size $tl
+  done
+done
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${TAG}_p125m -o run --output-format csv -- python $R/bench.py --inner 1.25e8 --outer 1.25e8 --steps 20 --warmup 3 --general off > $R/gpurun_out/${TAG}_p125m.log 2>&1 || { tail -20 $R/gpurun_out/${TAG}_p125m.log; exit 1; }
+echo done
