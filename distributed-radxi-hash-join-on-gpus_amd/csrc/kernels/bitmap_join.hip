@@ -141,7 +141,7 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// fn(fragment) for every u32 fragment of partition blockIdx.x: its
+// fn(fragment) for every u32 fragment of partition d: its
 // CLAIM_GROUPS claim slices walked as ONE stream of 16-byte vectors (slices
 // start on 16-element boundaries).  The slice table is read once per
 // workgroup (one round trip) and kept in scalar registers; batch k+1 is in
@@ -152,14 +152,15 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
 // 15K fragments per slice, one batch).  Each slice's last len % 4 elements
 // are visited at the end.
 template <int NTH, int U, class Src, typename Fn>
-__device__ __forceinline__ void visitClaim(const uint32_t *__restrict__ src, const Src &cs, uint32_t &flags, Fn &&fn) {
+__device__ __forceinline__ void visitClaim(const uint32_t *__restrict__ src, const Src &cs, uint32_t d, uint32_t &flags,
+                                           Fn &&fn) {
   constexpr uint32_t G = CLAIM_GROUPS;
   __shared__ uint64_t sBase[G], sLen[G], sPre[G], sAdj[G];
   const uint32_t t = threadIdx.x;
   __syncthreads();  // an earlier walk's readers of the slice table are done
   if (t < G) {
     uint64_t b, len;
-    cs.get(blockIdx.x, t, b, len, flags);
+    cs.get(d, t, b, len, flags);
     sBase[t] = b;
     sLen[t] = len;
   }
@@ -229,26 +230,26 @@ __device__ __forceinline__ void visitClaim(const uint32_t *__restrict__ src, con
   }
 }
 
-// Every element of partition blockIdx.x of one side.  u32 fragments: one
+// Every element of partition d of one side.  u32 fragments: one
 // flat walk over all claim slices (flat != 0: short partitions) or one
 // pipelined walk per slice (long partitions).
 template <int NTH, typename E, int U, class Src, typename Fn>
-__device__ __forceinline__ void visitPartition(const E *__restrict__ src, const Src &ss, uint32_t shift, uint32_t flat,
-                                               uint32_t &flags, Fn &&fn) {
+__device__ __forceinline__ void visitPartition(const E *__restrict__ src, const Src &ss, uint32_t d, uint32_t shift,
+                                               uint32_t flat, uint32_t &flags, Fn &&fn) {
   if constexpr (sizeof(E) == 4) {
     if (flat) {
-      visitClaim<NTH, U>(src, ss, flags, fn);
+      visitClaim<NTH, U>(src, ss, d, flags, fn);
       return;
     }
     for (uint32_t g = 0; g < ss.groups(); ++g) {
       uint64_t b, len;
-      ss.get(blockIdx.x, g, b, len, flags);
+      ss.get(d, g, b, len, flags);
       visitSlice32<NTH, U>(src + b, len, fn);
     }
   } else {
     for (uint32_t g = 0; g < ss.groups(); ++g) {
       uint64_t b, len;
-      ss.get(blockIdx.x, g, b, len, flags);
+      ss.get(d, g, b, len, flags);
       visitSlice64<NTH, U>(src + b, len, shift, fn);
     }
   }
@@ -258,10 +259,10 @@ __device__ __forceinline__ void visitPartition(const E *__restrict__ src, const 
 // fragment is found afterwards as fewer set bits than inserted fragments
 // (bmCheckDup).  Returns this thread's inserted count.
 template <int NTH, typename E, int U, class Src>
-__device__ __forceinline__ uint64_t bmBuild(uint32_t *bm, const E *__restrict__ r, const Src &rs, uint32_t shift,
-                                            uint32_t flat, uint64_t limit, uint32_t &flags) {
+__device__ __forceinline__ uint64_t bmBuild(uint32_t *bm, const E *__restrict__ r, const Src &rs, uint32_t d,
+                                            uint32_t shift, uint32_t flat, uint64_t limit, uint32_t &flags) {
   uint32_t inserted = 0;
-  visitPartition<NTH, E, U>(r, rs, shift, flat, flags, [&](uint64_t f) {
+  visitPartition<NTH, E, U>(r, rs, d, shift, flat, flags, [&](uint64_t f) {
     if (f >= limit) {  // outside the planned fragment range: the caller falls back
       flags |= BM_FLAG_DUP;
       return;
@@ -286,10 +287,10 @@ __device__ __forceinline__ uint64_t bmCheckDup(const uint32_t *bm, uint32_t word
 }
 
 template <int NTH, typename E, int U, class Src>
-__device__ __forceinline__ uint64_t bmProbe(const uint32_t *bm, const E *__restrict__ s, const Src &ss, uint32_t shift,
-                                            uint32_t flat, uint64_t limit, uint32_t &flags) {
+__device__ __forceinline__ uint64_t bmProbe(const uint32_t *bm, const E *__restrict__ s, const Src &ss, uint32_t d,
+                                            uint32_t shift, uint32_t flat, uint64_t limit, uint32_t &flags) {
   uint32_t cnt = 0;
-  visitPartition<NTH, E, U>(s, ss, shift, flat, flags, [&](uint64_t f) {
+  visitPartition<NTH, E, U>(s, ss, d, shift, flat, flags, [&](uint64_t f) {
     if (f < limit) cnt += (bm[f >> 5] >> (f & 31)) & 1u;
   });
   return cnt;
@@ -305,7 +306,11 @@ __device__ __forceinline__ void bmFinish(BitmapCounters *out, uint64_t matches, 
     if (matches) atomicAdd(&out->matches, (unsigned long long)matches);
     if (bits) atomicAdd(&out->popcount, (unsigned long long)bits);
   }
-  if (flags) atomicOr(&out->flags, flags);
+  const bool dup = __ballot(flags & BM_FLAG_DUP) != 0, ovf = __ballot(flags & BM_FLAG_OVERFLOW) != 0;
+  if ((threadIdx.x & (WAVE - 1)) == 0) {
+    if (dup) atomicAdd(&out->dup, 1ull);
+    if (ovf) atomicAdd(&out->overflow, 1ull);
+  }
 }
 
 template <typename E, int U, class Src, int NTH>
@@ -318,10 +323,10 @@ __global__ __launch_bounds__(NTH) void bitmapJoinKernel(const E *__restrict__ r,
   __syncthreads();
   const uint64_t limit = (uint64_t)words * 32;
   uint32_t flags = 0;
-  const uint64_t inserted = bmBuild<NTH, E, U>(bm, r, rs, shift, flat, limit, flags);
+  const uint64_t inserted = bmBuild<NTH, E, U>(bm, r, rs, blockIdx.x, shift, flat, limit, flags);
   __syncthreads();
   bmCheckDup<NTH>(bm, words, inserted, flags, wt);
-  const uint64_t cnt = bmProbe<NTH, E, U>(bm, s, ss, shift, flat, limit, flags);
+  const uint64_t cnt = bmProbe<NTH, E, U>(bm, s, ss, blockIdx.x, shift, flat, limit, flags);
   bmFinish(out, cnt, 0, flags);
 }
 
@@ -334,7 +339,7 @@ __global__ __launch_bounds__(NTH) void bitmapBuildKernel(const E *__restrict__ r
   for (uint32_t w = threadIdx.x; w < words; w += NTH) bm[w] = 0;
   __syncthreads();
   uint32_t flags = 0;
-  const uint64_t inserted = bmBuild<NTH, E, U>(bm, r, rs, shift, flat, (uint64_t)words * 32, flags);
+  const uint64_t inserted = bmBuild<NTH, E, U>(bm, r, rs, blockIdx.x, shift, flat, (uint64_t)words * 32, flags);
   __syncthreads();
   bmCheckDup<NTH>(bm, words, inserted, flags, wt);
   uint32_t *dst = bitmaps + (size_t)blockIdx.x * words;
@@ -344,11 +349,12 @@ __global__ __launch_bounds__(NTH) void bitmapBuildKernel(const E *__restrict__ r
 
 template <typename E, int U, class Src, int NTH>
 __global__ __launch_bounds__(NTH) void bitmapProbeKernel(const E *__restrict__ s, Src ss, uint32_t shift,
-                                                         uint32_t words, uint32_t flat,
+                                                         uint32_t words, uint32_t flat, uint32_t partBase,
                                                          const uint32_t *__restrict__ bitmaps,
                                                          BitmapCounters *__restrict__ out) {
   extern __shared__ uint32_t bm[];
-  const u32x4 *src = reinterpret_cast<const u32x4 *>(bitmaps + (size_t)blockIdx.x * words);
+  const uint32_t d = partBase + blockIdx.x;
+  const u32x4 *src = reinterpret_cast<const u32x4 *>(bitmaps + (size_t)d * words);
   uint64_t bits = 0;
   for (uint32_t w = threadIdx.x; w < words / 4; w += NTH) {  // words is a power of two >= 32
     const u32x4 x = __builtin_nontemporal_load(src + w);
@@ -360,7 +366,7 @@ __global__ __launch_bounds__(NTH) void bitmapProbeKernel(const E *__restrict__ s
   }
   __syncthreads();
   uint32_t flags = 0;
-  const uint64_t cnt = bmProbe<NTH, E, U>(bm, s, ss, shift, flat, (uint64_t)words * 32, flags);
+  const uint64_t cnt = bmProbe<NTH, E, U>(bm, s, ss, d, shift, flat, (uint64_t)words * 32, flags);
   bmFinish(out, cnt, bits, flags);
 }
 
@@ -490,13 +496,17 @@ void bitmapBuild(uint32_t elemBytes, const void *r, const BitmapSlices &src, uin
 }
 
 void bitmapProbe(uint32_t elemBytes, const void *s, const BitmapSlices &src, uint32_t partitions, uint32_t keyShift,
-                 uint32_t bits, const uint32_t *bitmaps, BitmapCounters *out, hipStream_t st) {
+                 uint32_t bits, const uint32_t *bitmaps, BitmapCounters *out, hipStream_t st, uint32_t first,
+                 uint32_t count) {
   checkBits(bits, keyShift, elemBytes);
-  if (partitions == 0) return;
+  if (count == UINT32_MAX) count = partitions - std::min(first, partitions);
+  HJ_CHECK(first <= partitions && count <= partitions - first, "bitmapProbe: partitions [%u, +%u) of %u", first, count,
+           partitions);
+  if (partitions == 0 || count == 0) return;
   const uint32_t words = bitmapWords(bits);
   const uint32_t flat = bmFlat(src, nullptr, partitions);
-  HJ_BM_DISPATCH(hipLaunchKernelGGL((bitmapProbeKernel<E, U, S, NTH>), dim3(partitions), dim3(NTH), (size_t)words * 4, st,
-                                    static_cast<const E *>(s), makeSrc<S>(src, partitions), keyShift, words, flat, bitmaps,
+  HJ_BM_DISPATCH(hipLaunchKernelGGL((bitmapProbeKernel<E, U, S, NTH>), dim3(count), dim3(NTH), (size_t)words * 4, st,
+                                    static_cast<const E *>(s), makeSrc<S>(src, partitions), keyShift, words, flat, first, bitmaps,
                                     out));
   HIP_CHECK_LAUNCH();
 }

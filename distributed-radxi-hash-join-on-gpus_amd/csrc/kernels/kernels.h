@@ -326,11 +326,13 @@ void buildProbe(const BPArgs &a, const BPItem *items, const uint32_t *nItems, ui
 constexpr uint32_t BITMAP_MAX_BITS = 20;  // 128 KiB of LDS
 constexpr uint32_t BM_FLAG_DUP = 1;       // an inner fragment repeats or leaves the range: fall back
 constexpr uint32_t BM_FLAG_OVERFLOW = 2;  // a sampled claim slice overflowed: redo with exact slices
+// Four u64 sums, so that one all-reduce of the struct combines every rank's
+// outcome on the device (dup / overflow: waves that raised the flag).
 struct BitmapCounters {
   unsigned long long matches;
   unsigned long long popcount;  // bitmapProbe: set bits of the probed bitmaps
-  unsigned int flags;
-  unsigned int pad;
+  unsigned long long dup;       // BM_FLAG_DUP raised
+  unsigned long long overflow;  // BM_FLAG_OVERFLOW raised
 };
 struct BitmapSlices {
   enum Kind : int { Claim = 0, Table = 1 };
@@ -353,8 +355,11 @@ void bitmapJoin(uint32_t elemBytes, const void *r, const void *s, const BitmapSl
 void bitmapBuild(uint32_t elemBytes, const void *r, const BitmapSlices &rs, uint32_t partitions, uint32_t keyShift,
                  uint32_t bits, uint32_t *bitmaps, BitmapCounters *out, hipStream_t st);
 // Probes s against bitmaps (e.g. all-reduced over ranks); out->popcount += set bits.
+// Partitions [first, first + count) only (count = UINT32_MAX: to the end);
+// slices and bitmaps are indexed by the global partition number.
 void bitmapProbe(uint32_t elemBytes, const void *s, const BitmapSlices &ss, uint32_t partitions, uint32_t keyShift,
-                 uint32_t bits, const uint32_t *bitmaps, BitmapCounters *out, hipStream_t st);
+                 uint32_t bits, const uint32_t *bitmaps, BitmapCounters *out, hipStream_t st, uint32_t first = 0,
+                 uint32_t count = UINT32_MAX);
 
 // ------------------------------------------------------------ wire codec
 // Exchange wire format for 8-byte CompressedTuples (N > 1).  On the wire a

@@ -1,6 +1,7 @@
 #include "BitmapJoin.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "../comm/Communicator.h"
@@ -86,6 +87,20 @@ void BitmapJoin::partitionSide(Side &s, bool exact, bool narrowOk, hipEvent_t fr
   s.slices.count = n;
 }
 
+// Partition ranges of the replicated plan's all-reduce: one per 32 MiB of
+// bitmaps, at most 4 (1B dense keys: 4 x 32 MiB).  Each range is one more
+// collective (~10-30 us of launch and handshake over xGMI), against the probe
+// of all but the last range moving behind the all-reduce.
+// HPCJOIN_REDUCE_CHUNKS=k forces k.
+static uint32_t reduceChunks(uint64_t bitmapBytes) {
+  static const int forced = [] {
+    const char *e = std::getenv("HPCJOIN_REDUCE_CHUNKS");
+    return e ? std::max(1, std::min(std::atoi(e), 64)) : 0;
+  }();
+  if (forced) return (uint32_t)forced;
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4, bitmapBytes >> 25));
+}
+
 BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
   const uint32_t F = 1u << plan.networkBits, N = ctx->numberOfNodes(), bits = plan.bitmapBits;
   const hipStream_t st = ctx->stream();
@@ -140,20 +155,32 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
     tl.endAt("BPBUILD", built);
     HIP_CHECK(hipStreamWaitEvent(ctx->commStream(), built, 0));
     // The all-reduce (exchange stream) overlaps the outer side's network pass:
-    // the plan's one link transfer (the reference's puts, MWINPUT).
-    performance::Measurements::add("MWINPUTCNT", 1, "calls");
+    // the plan's one link transfer (the reference's puts, MWINPUT).  It runs
+    // in K partition ranges; the probe of a range starts as soon as the range
+    // is reduced, so after the last range lands only its probe is left.
+    const uint32_t K = std::min<uint32_t>(reduceChunks((uint64_t)F * words * 4), F);
     tl.beginAt("MWINPUT", built);
-    ctx->comm()->allReduceSumDevice(reinterpret_cast<uint64_t *>(bm), (size_t)F * words / 2, ctx->commStream());
-    hipEvent_t reduced = point(ctx->commStream());
-    tl.endAt("MWINPUT", reduced);
+    std::vector<hipEvent_t> reduced(K);
+    for (uint32_t c = 0; c < K; ++c) {
+      const uint32_t p0 = (uint32_t)((uint64_t)F * c / K), p1 = (uint32_t)((uint64_t)F * (c + 1) / K);
+      performance::Measurements::add("MWINPUTCNT", 1, "calls");
+      ctx->comm()->allReduceSumDevice(reinterpret_cast<uint64_t *>(bm + (size_t)p0 * words),
+                                      (size_t)(p1 - p0) * words / 2, ctx->commStream());
+      reduced[c] = point(ctx->commStream());
+    }
+    tl.endAt("MWINPUT", reduced[K - 1]);
     o.linkBytes = (uint64_t)(2.0 * (N - 1) / N * (double)F * words * 4);
     partitionSide(so, exact, narrowOk, built, ev[2]);
-    HIP_CHECK(hipStreamWaitEvent(st, reduced, 0));
+    HIP_CHECK(hipStreamWaitEvent(st, reduced[0], 0));
     HIP_CHECK(hipEventRecord(ev[3], st));
     joinStart = ev[3];
     utils::faultPoint("build_probe");
     tl.beginAt("BPPROBE", ev[3]);
-    kernels::bitmapProbe(4, so.frags, so.slices, F, 0, bits, bm, cnt, st);
+    for (uint32_t c = 0; c < K; ++c) {
+      const uint32_t p0 = (uint32_t)((uint64_t)F * c / K), p1 = (uint32_t)((uint64_t)F * (c + 1) / K);
+      if (c) HIP_CHECK(hipStreamWaitEvent(st, reduced[c], 0));
+      kernels::bitmapProbe(4, so.frags, so.slices, F, 0, bits, bm, cnt, st, p0, p1 - p0);
+    }
     HIP_CHECK(hipEventRecord(ev[4], st));
     tl.endAt("BPPROBE", ev[4]);
     tl.endAt("BPTASKTIME", ev[4]);
@@ -162,8 +189,15 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
   performance::Measurements::add("BPPROBEELEM", (double)outer->getLocalSize(), "tuples");
   performance::Measurements::add("BPMEMSIZE", (double)(N > 1 ? (uint64_t)F * kernels::bitmapWords(bits) * 4 : 0),
                                  "bytes");
-  BitmapCounters *back = ctx->staging().getArray<BitmapCounters>(1);
+  // back[0]: this rank's counters; back[1] (N > 1): all ranks' sums, combined
+  // on the device behind the probe (one synchronisation per join).
+  BitmapCounters *back = ctx->staging().getArray<BitmapCounters>(2);
   HIP_CHECK(hipMemcpyAsync(back, cnt, sizeof(BitmapCounters), hipMemcpyDeviceToHost, st));
+  if (N > 1) {
+    static_assert(sizeof(BitmapCounters) == 4 * sizeof(uint64_t), "BitmapCounters: four u64 sums");
+    ctx->comm()->allReduceSumDevice(reinterpret_cast<uint64_t *>(cnt), 4, st);
+    HIP_CHECK(hipMemcpyAsync(back + 1, cnt, sizeof(BitmapCounters), hipMemcpyDeviceToHost, st));
+  }
   ctx->synchronize();
   float ms = 0;
   HIP_CHECK(hipEventElapsedTime(&ms, ev[0], ev[1]));
@@ -172,9 +206,16 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
   o.devScatterMs = ms;
   HIP_CHECK(hipEventElapsedTime(&ms, joinStart, ev[4]));
   o.devJoinMs = ms;
-  o.localMatches = back->matches;
-  o.popcount = back->popcount;
-  agree(o, back->flags);
+  o.localMatches = back[0].matches;
+  o.popcount = back[0].popcount;
+  if (N > 1) {
+    o.globalMatches = back[1].matches;
+    o.dup = back[1].dup > 0;
+    o.overflow = back[1].overflow > 0;
+    if (!o.overflow && o.popcount != inner->getGlobalSize()) o.dup = true;
+  } else {
+    agree(o, (back[0].dup ? kernels::BM_FLAG_DUP : 0u) | (back[0].overflow ? kernels::BM_FLAG_OVERFLOW : 0u));
+  }
   return o;
 }
 
