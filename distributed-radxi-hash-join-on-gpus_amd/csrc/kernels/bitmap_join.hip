@@ -386,11 +386,9 @@ static void checkBits(uint32_t bits, uint32_t keyShift, uint32_t elemBytes) {
 // -- one rank's share at N = 8 -- overlap each other's latencies).
 // HPCJOIN_BM_NTH=256|1024 forces one (sweeps).
 static int bmThreads(uint32_t bits) {
-  static const int forced = [] {
-    const char *e = std::getenv("HPCJOIN_BM_NTH");
-    const int v = e ? std::atoi(e) : 0;
-    return v == 256 || v == 1024 ? v : 0;
-  }();
+  const char *e = std::getenv("HPCJOIN_BM_NTH");  // read per launch: tests switch it
+  const int v = e ? std::atoi(e) : 0;
+  const int forced = v == 256 || v == 1024 ? v : 0;
   return forced ? forced : bits <= 18 ? 256 : 1024;
 }
 
@@ -399,10 +397,8 @@ static int bmThreads(uint32_t bits) {
 // thread join kernel: 1B (977K per partition) per-slice 1.40 ms vs flat 1.49;
 // 125M (122K per partition) per-slice 0.358 ms vs flat 0.33.
 static uint32_t bmFlat(const BitmapSlices &a, const BitmapSlices *b, uint32_t partitions) {
-  static const int forced = [] {
-    const char *e = std::getenv("HPCJOIN_BM_FLAT");
-    return e ? (std::atoi(e) ? 1 : 0) : -1;
-  }();
+  const char *e = std::getenv("HPCJOIN_BM_FLAT");  // read per launch: tests switch it
+  const int forced = e ? (std::atoi(e) ? 1 : 0) : -1;
   if (forced >= 0) return (uint32_t)forced;
   const uint64_t n = std::max<uint64_t>(a.count, b ? b->count : 0);
   return n > 0 && n / std::max<uint32_t>(partitions, 1) < (1ull << 18) ? 1u : 0u;

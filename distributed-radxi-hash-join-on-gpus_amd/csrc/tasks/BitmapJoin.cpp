@@ -93,10 +93,8 @@ void BitmapJoin::partitionSide(Side &s, bool exact, bool narrowOk, hipEvent_t fr
 // of all but the last range moving behind the all-reduce.
 // HPCJOIN_REDUCE_CHUNKS=k forces k.
 static uint32_t reduceChunks(uint64_t bitmapBytes) {
-  static const int forced = [] {
-    const char *e = std::getenv("HPCJOIN_REDUCE_CHUNKS");
-    return e ? std::max(1, std::min(std::atoi(e), 64)) : 0;
-  }();
+  const char *e = std::getenv("HPCJOIN_REDUCE_CHUNKS");  // read per join: tests switch it
+  const int forced = e ? std::max(1, std::min(std::atoi(e), 64)) : 0;
   if (forced) return (uint32_t)forced;
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4, bitmapBytes >> 25));
 }

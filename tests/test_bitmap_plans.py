@@ -78,6 +78,49 @@ def test_replicated_bitmap_ranks(C, dev, n_ranks, outer_dist):
     assert sum(o[0][0]["local_matches"] for o in out) == exp
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("nth,flat", [("256", "0"), ("256", "1"), ("1024", "0"), ("1024", "1")])
+def test_bitmap_walk_variants(C, monkeypatch, nth, flat):
+    """Both slice walks of the bitmap kernels (one pipelined walk per claim
+    slice / one flat walk over all slices of a partition) at both workgroup
+    sizes give the exact count: short partitions (many empty and sub-vector
+    slices, tails of 1-3 fragments) and long ones, N = 1 fused kernel and the
+    replicated build / probe kernels at N = 2."""
+    monkeypatch.setenv("HPCJOIN_BM_NTH", nth)
+    monkeypatch.setenv("HPCJOIN_BM_FLAT", flat)
+    for G_R, G_S, n_ranks in [(40_009, 70_001, 1), (1 << 20, 3 << 19, 1), (3_000_017, 1_000_003, 1),
+                              (300_007, 450_011, 2)]:
+        inner = C.GenSpec(seed=77)
+        outer = C.GenSpec(distribution=C.KeyDistribution.UNIFORM, seed=5, domain=G_R)
+        exp = C.Relation.expected_matches(inner, G_R, outer, G_S)
+        out = run_ranks(C, n_ranks, "device", generated(C, "device", inner, G_R, n_ranks),
+                        generated(C, "device", outer, G_S, n_ranks), G_R, G_S, lambda c: force_replicated(c, C))
+        for res_list, plan in out:
+            assert plan.bitmap_join
+            for res in res_list:
+                assert res["bitmap_join"] and res["global_matches"] == exp, (G_R, G_S, n_ranks, res)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunks", ["1", "3", "7"])
+def test_replicated_bitmap_reduce_ranges(C, monkeypatch, chunks):
+    """The replicated plan's all-reduce in k partition ranges (k not dividing
+    the partition count), each range probed behind its own all-reduce: exact
+    counts on every rank."""
+    monkeypatch.setenv("HPCJOIN_REDUCE_CHUNKS", chunks)
+    G_R, G_S, n = 1_000_003, 2_000_029, 4
+    inner = C.GenSpec(seed=11)
+    outer = C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=12, domain=G_R, zipf_theta=0.75)
+    exp = C.Relation.expected_matches(inner, G_R, outer, G_S)
+    out = run_ranks(C, n, "device", generated(C, "device", inner, G_R, n), generated(C, "device", outer, G_S, n),
+                    G_R, G_S, lambda c: force_replicated(c, C))
+    for res_list, plan in out:
+        assert plan.bitmap_join and plan.bitmap_replicated
+        for res in res_list:
+            assert res["global_matches"] == exp and res["network_fallbacks"] == 0
+    assert sum(o[0][0]["local_matches"] for o in out) == exp
+
+
 @pytest.mark.parametrize("dev", devices())
 @pytest.mark.parametrize("n_ranks", [2, 4])
 def test_replicated_bitmap_cross_rank_duplicate_falls_back(C, dev, n_ranks):
