@@ -1163,13 +1163,13 @@ __global__ __launch_bounds__(T, MINW) void bpKeyCountKernel(BPArgs a, const BPIt
 // 4.99 -- the default; 2 = 1 + folded hash 4.88 (dropped as default: keys
 // whose halves are equal would all share one bucket); 3 = 2 + cleared slots
 // 4.98; 4 = 0 + folded hash + cleared slots 6.10; 5 = 512 x 4 with 4 buckets
-// in flight 5.41.
+// in flight 5.41.  Measured and dropped: 16-byte two-slot buckets with
+// packed 16-bit fill counters (one 16-byte LDS read per probe instead of two,
+// against 3.0 bank-conflict cycles per LDS instruction in the PMC of variant
+// 1): 5.43-5.53 ms vs 4.93-4.95 (profiles/r2v).
 static int keyCountVariant() {
-  static const int v = [] {
-    const char *e = std::getenv("HPCJOIN_KCOUNT");
-    return e ? std::atoi(e) : 1;
-  }();
-  return v;
+  const char *e = std::getenv("HPCJOIN_KCOUNT");  // read per launch: tests switch it
+  return e ? std::atoi(e) : 1;
 }
 
 template <int T, int K, int H, bool FOLD, bool CLEAR, int MINW>

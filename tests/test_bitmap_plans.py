@@ -215,6 +215,30 @@ def test_sparse64_generator(C):
     assert C.Relation.expected_matches(spec, n, plain, 3 * n) is None  # transforms must match
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["1", "0", "2", "3", "4", "5"])
+def test_key_only_count_variants(C, monkeypatch, variant):
+    """Every key-only count kernel variant against a torch reference, with heavily repeated inner keys (Zipf over sparse
+    63-bit keys: long overflow chains through the next buckets)."""
+    from helpers import ref_join_count
+    monkeypatch.setenv("HPCJOIN_KCOUNT", variant)
+    ctx = C.ExecContext("device", 0, C.LocalCommunicator())
+    for (G_R, G_S, theta) in [(200_003, 300_007, 0.99), (1 << 20, 1 << 21, 0.5)]:
+        inner = C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=31, domain=G_R // 4, zipf_theta=theta)
+        inner.sparse64 = True
+        outer = C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=32, domain=G_R // 4, zipf_theta=0.8)
+        outer.sparse64 = True
+        R = C.Relation(G_R, G_R, "device", 0)
+        S = C.Relation(G_S, G_S, "device", 0)
+        R.generate(inner, 0)
+        S.generate(outer, 0)
+        j = C.HashJoin(R, S, ctx, C.JoinConfig())
+        assert j.plan.key_only
+        exp = ref_join_count(R.to_tensor()[:, 0].cpu(), S.to_tensor()[:, 0].cpu())
+        for _ in range(2):
+            assert j.run()["global_matches"] == exp, (variant, G_R, theta)
+
+
 @pytest.mark.parametrize("dev", devices())
 def test_sparse64_join_auto_wide(C, dev):
     """63-bit keys do not fit a CompressedTuple: the planner switches by itself
