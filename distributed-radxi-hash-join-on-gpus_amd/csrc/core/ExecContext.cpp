@@ -25,7 +25,13 @@ ExecContext::ExecContext(Location loc, int device, comm::Communicator *comm)
   if (onDevice()) {
     HIP_CHECK(hipSetDevice(device_));
     HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    HIP_CHECK(hipStreamCreateWithFlags(&commStream_, hipStreamNonBlocking));
+    // The exchange stream (RCCL collectives, window copies) gets the highest
+    // priority: its few long-running blocks are dispatched ahead of the
+    // remaining blocks of a partitioning kernel it overlaps, instead of
+    // waiting for CUs behind them.
+    int leastPrio = 0, greatestPrio = 0;
+    HIP_CHECK(hipDeviceGetStreamPriorityRange(&leastPrio, &greatestPrio));
+    HIP_CHECK(hipStreamCreateWithPriority(&commStream_, hipStreamNonBlocking, greatestPrio));
     HIP_CHECK(hipStreamCreateWithFlags(&decodeStream_, hipStreamNonBlocking));
   }
 }
