@@ -104,6 +104,21 @@ PHASES = ("histogram_ms", "network_ms", "local_ms", "dev_histogram_ms", "dev_net
           "dev_build_probe_ms")
 
 
+def link_prediction(info, plan, results):
+    """The plan's own link-traffic prediction (both N > 1 alternatives), so a
+    measured multi-GPU step can be checked against what the links allow."""
+    if info.world <= 1:
+        return None
+    gbps = plan.link_gbps
+    return {"chosen": "replicated_bitmap" if plan.bitmap_replicated else "shuffle",
+            "replicated_bytes_per_rank": int(plan.replicated_link_bytes),
+            "shuffle_bytes_per_rank": int(plan.shuffle_link_bytes),
+            "link_GBps_per_rank": gbps,
+            "predicted_replicated_ms": round(plan.replicated_link_bytes / gbps / 1e6, 3) if gbps else None,
+            "predicted_shuffle_ms": round(plan.shuffle_link_bytes / gbps / 1e6, 3) if gbps else None,
+            "measured_wire_bytes_rank0": results[-1]["wire_bytes"]}
+
+
 def measure(C, info, ctx, comm, on_gpu, G_R, G_S, inner, outer, cfg, rel_loc, steps, warmup):
     """Generate this rank's slices, build the join (timed with its first run:
     the cold-join cost incl. planning), warm up, then time `steps` joins
@@ -219,18 +234,7 @@ def main():
               "workspace_peak_GB": round(ctx.workspace_peak() / 1e9, 2),
               "step_ms": [round(r["join_ms"], 2) for r in results],
               "step_phases_ms": [[round(r[k], 2) for k in PHASES] for r in results]}
-    # The plan's own link-traffic prediction (both N > 1 alternatives), so a
-    # measured multi-GPU step can be checked against what the links allow.
-    links = None
-    if info.world > 1:
-        gbps = plan.link_gbps
-        links = {"chosen": "replicated_bitmap" if plan.bitmap_replicated else "shuffle",
-                 "replicated_bytes_per_rank": int(plan.replicated_link_bytes),
-                 "shuffle_bytes_per_rank": int(plan.shuffle_link_bytes),
-                 "link_GBps_per_rank": gbps,
-                 "predicted_replicated_ms": round(plan.replicated_link_bytes / gbps / 1e6, 3) if gbps else None,
-                 "predicted_shuffle_ms": round(plan.shuffle_link_bytes / gbps / 1e6, 3) if gbps else None,
-                 "measured_wire_bytes_rank0": results[-1]["wire_bytes"]}
+    links = link_prediction(info, plan, results)
     del join
     ctx.reset_scratch()
 
@@ -243,8 +247,9 @@ def main():
         try:
             g = measure(C, info, ctx, comm, on_gpu, G_R, G_S, *specs(True), cfg, rel_loc,
                         max(2, args.steps // 2), max(1, args.warmup))
-            g.pop("join")
-            g.pop("results")
+            gj, gres = g.pop("join"), g.pop("results")
+            g["links"] = link_prediction(info, gj.plan, gres)
+            del gj
             general = {"data": "synthetic: unique random 63-bit keys (a fixed bijection of 0..G-1 over [0, 2^63)), "
                                "same join, generated on device",
                        **g}
