@@ -259,15 +259,20 @@ __device__ __forceinline__ void visitPartition(const E *__restrict__ src, const 
 // fragment is found afterwards as fewer set bits than inserted fragments
 // (bmCheckDup).  Returns this thread's inserted count.
 template <int NTH, typename E, int U, class Src>
+// This workgroup's bitmap covers fragments [base, base + limit) of the
+// partition's range [0, limit << split).
 __device__ __forceinline__ uint64_t bmBuild(uint32_t *bm, const E *__restrict__ r, const Src &rs, uint32_t d,
-                                            uint32_t shift, uint32_t flat, uint64_t limit, uint32_t &flags) {
+                                            uint32_t shift, uint32_t flat, uint64_t limit, uint32_t &flags,
+                                            uint64_t base = 0, uint32_t split = 0) {
   uint32_t inserted = 0;
+  const uint64_t range = limit << split;
   visitPartition<NTH, E, U>(r, rs, d, shift, flat, flags, [&](uint64_t f) {
-    if (f >= limit) {  // outside the planned fragment range: the caller falls back
-      flags |= BM_FLAG_DUP;
-      return;
+    const uint64_t g = f - base;
+    if (g >= limit) {
+      if (f >= range) flags |= BM_FLAG_DUP;  // outside the planned fragment range: the caller falls back
+      return;                                // else: another workgroup's piece
     }
-    __hip_atomic_fetch_or(&bm[f >> 5], 1u << (f & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_or(&bm[g >> 5], 1u << (g & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     ++inserted;
   });
   return inserted;
@@ -288,10 +293,12 @@ __device__ __forceinline__ uint64_t bmCheckDup(const uint32_t *bm, uint32_t word
 
 template <int NTH, typename E, int U, class Src>
 __device__ __forceinline__ uint64_t bmProbe(const uint32_t *bm, const E *__restrict__ s, const Src &ss, uint32_t d,
-                                            uint32_t shift, uint32_t flat, uint64_t limit, uint32_t &flags) {
+                                            uint32_t shift, uint32_t flat, uint64_t limit, uint32_t &flags,
+                                            uint64_t base = 0) {
   uint32_t cnt = 0;
   visitPartition<NTH, E, U>(s, ss, d, shift, flat, flags, [&](uint64_t f) {
-    if (f < limit) cnt += (bm[f >> 5] >> (f & 31)) & 1u;
+    const uint64_t g = f - base;
+    if (g < limit) cnt += (bm[g >> 5] >> (g & 31)) & 1u;
   });
   return cnt;
 }
@@ -316,17 +323,19 @@ __device__ __forceinline__ void bmFinish(BitmapCounters *out, uint64_t matches, 
 template <typename E, int U, class Src, int NTH>
 __global__ __launch_bounds__(NTH) void bitmapJoinKernel(const E *__restrict__ r, const E *__restrict__ s, Src rs,
                                                         Src ss, uint32_t shift, uint32_t words, uint32_t flat,
-                                                        BitmapCounters *__restrict__ out) {
+                                                        uint32_t split, BitmapCounters *__restrict__ out) {
   extern __shared__ uint32_t bm[];
   __shared__ uint64_t wt[NTH / WAVE];
   for (uint32_t w = threadIdx.x; w < words; w += NTH) bm[w] = 0;
   __syncthreads();
-  const uint64_t limit = (uint64_t)words * 32;
+  // Workgroup = (partition d, piece h of its fragment range); split = 0: one piece.
+  const uint32_t d = blockIdx.x >> split;
+  const uint64_t limit = (uint64_t)words * 32, base = (uint64_t)(blockIdx.x & ((1u << split) - 1)) * limit;
   uint32_t flags = 0;
-  const uint64_t inserted = bmBuild<NTH, E, U>(bm, r, rs, blockIdx.x, shift, flat, limit, flags);
+  const uint64_t inserted = bmBuild<NTH, E, U>(bm, r, rs, d, shift, flat, limit, flags, base, split);
   __syncthreads();
   bmCheckDup<NTH>(bm, words, inserted, flags, wt);
-  const uint64_t cnt = bmProbe<NTH, E, U>(bm, s, ss, blockIdx.x, shift, flat, limit, flags);
+  const uint64_t cnt = bmProbe<NTH, E, U>(bm, s, ss, d, shift, flat, limit, flags, base);
   bmFinish(out, cnt, 0, flags);
 }
 
@@ -372,9 +381,9 @@ __global__ __launch_bounds__(NTH) void bitmapProbeKernel(const E *__restrict__ s
 
 uint32_t bitmapWords(uint32_t bits) { return bits > 7 ? 1u << (bits - 5) : 4u; }
 
-static void checkBits(uint32_t bits, uint32_t keyShift, uint32_t elemBytes) {
-  HJ_CHECK(bits <= BITMAP_MAX_BITS, "bitmap join: %u fragment bits exceed the %u-bit LDS bitmap", bits,
-           BITMAP_MAX_BITS);
+static void checkBits(uint32_t bits, uint32_t keyShift, uint32_t elemBytes, uint32_t maxSplit = 0) {
+  HJ_CHECK(bits <= BITMAP_MAX_BITS + maxSplit, "bitmap join: %u fragment bits exceed the %u-bit LDS bitmap", bits,
+           BITMAP_MAX_BITS + maxSplit);
   HJ_CHECK(elemBytes == 4 || elemBytes == 8, "bitmap join: %u-byte elements", elemBytes);
   HJ_CHECK(elemBytes == 8 ? keyShift < 64 : keyShift == 0, "bitmap join: keyShift=%u for %u-byte elements", keyShift,
            elemBytes);
@@ -467,15 +476,17 @@ TableSrc makeSrc(const BitmapSlices &b, uint32_t) {
 
 void bitmapJoin(uint32_t elemBytes, const void *r, const void *s, const BitmapSlices &rsl, const BitmapSlices &ssl,
                 uint32_t partitions, uint32_t keyShift, uint32_t bits, BitmapCounters *out, hipStream_t st) {
-  checkBits(bits, keyShift, elemBytes);
+  checkBits(bits, keyShift, elemBytes, BITMAP_MAX_SPLIT);
   HJ_CHECK(rsl.kind == ssl.kind && rsl.narrow == ssl.narrow, "bitmap join: inner and outer slices differ in kind");
   if (partitions == 0) return;
-  const uint32_t words = bitmapWords(bits);
+  const uint32_t split = bits > BITMAP_MAX_BITS ? bits - BITMAP_MAX_BITS : 0;
+  const uint32_t words = bitmapWords(bits - split);
   const uint32_t flat = bmFlat(rsl, &ssl, partitions);
   const BitmapSlices &src = rsl;
-  HJ_BM_DISPATCH(hipLaunchKernelGGL((bitmapJoinKernel<E, U, S, NTH>), dim3(partitions), dim3(NTH), (size_t)words * 4, st,
+  HJ_BM_DISPATCH(hipLaunchKernelGGL((bitmapJoinKernel<E, U, S, NTH>), dim3(partitions << split), dim3(NTH),
+                                    (size_t)words * 4, st,
                                     static_cast<const E *>(r), static_cast<const E *>(s), makeSrc<S>(rsl, partitions),
-                                    makeSrc<S>(ssl, partitions), keyShift, words, flat, out));
+                                    makeSrc<S>(ssl, partitions), keyShift, words, flat, split, out));
   HIP_CHECK_LAUNCH();
 }
 

@@ -324,6 +324,10 @@ void buildProbe(const BPArgs &a, const BPItem *items, const uint32_t *nItems, ui
 //   elemBytes 8: CompressedTuples (fragment = value >> keyShift), partitions
 //                given as a segment table [F][groups] (exchanged windows)
 constexpr uint32_t BITMAP_MAX_BITS = 20;  // 128 KiB of LDS
+// The fused N = 1 kernel may split a partition's fragment range over 2^split
+// workgroups (each holds one 128 KiB piece and reads all of the partition's
+// fragments): 21 fragment bits, e.g. 3B dense keys over a 2048-way digit.
+constexpr uint32_t BITMAP_MAX_SPLIT = 1;
 constexpr uint32_t BM_FLAG_DUP = 1;       // an inner fragment repeats or leaves the range: fall back
 constexpr uint32_t BM_FLAG_OVERFLOW = 2;  // a sampled claim slice overflowed: redo with exact slices
 // Four u64 sums, so that one all-reduce of the struct combines every rank's
@@ -349,6 +353,8 @@ struct BitmapSlices {
 };
 // u32 words of one partition's bitmap (a power of two >= 4).
 uint32_t bitmapWords(uint32_t bits);
+// bits may exceed BITMAP_MAX_BITS by up to BITMAP_MAX_SPLIT: each partition
+// is then joined by 2^(bits - BITMAP_MAX_BITS) workgroups.
 void bitmapJoin(uint32_t elemBytes, const void *r, const void *s, const BitmapSlices &rs, const BitmapSlices &ss,
                 uint32_t partitions, uint32_t keyShift, uint32_t bits, BitmapCounters *out, hipStream_t st);
 // bitmaps[d * bitmapWords(bits) ...] = partition d's bitmap of r.

@@ -102,6 +102,42 @@ def test_bitmap_walk_variants(C, monkeypatch, nth, flat):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nb,dup", [(1, False), (3, False), (2, True)])
+def test_bitmap_split_pieces(C, nb, dup):
+    """21 fragment bits above the network digit (forced small digit): each
+    partition is joined by two workgroups holding one 128 KiB piece of its
+    fragment range each; counts are exact, and a repeated inner key still
+    sends the join to the two-level plan."""
+    G = 1 << (21 + nb)
+    ctx = C.ExecContext("device", 0, C.LocalCommunicator())
+    inner = C.GenSpec(seed=3)
+    outer = C.GenSpec(distribution=C.KeyDistribution.UNIFORM, seed=4, domain=G)
+    R = C.Relation(G, G, "device", 0)
+    S = C.Relation(G // 2, G // 2, "device", 0)
+    R.generate(inner, 0)
+    S.generate(outer, 0)
+    exp = C.Relation.expected_matches(inner, G, outer, G // 2)
+    if dup:
+        import torch
+        t = R.to_tensor()
+        t[5, 0] = t[9, 0]  # one repeated inner key
+        R = C.Relation.from_tensor(t.contiguous(), G)
+        exp = None
+    cfg = C.JoinConfig()
+    cfg.network_bits = nb
+    j = C.HashJoin(R, S, ctx, cfg)
+    assert j.plan.bitmap_join and j.plan.bitmap_bits == 21
+    res = j.run()
+    if dup:
+        from helpers import ref_join_count
+        exp = ref_join_count(R.to_tensor()[:, 0].cpu(), S.to_tensor()[:, 0].cpu())
+        assert not res["bitmap_join"] and res["global_matches"] == exp
+    else:
+        assert res["bitmap_join"] and res["global_matches"] == exp
+        assert j.run()["global_matches"] == exp
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("chunks", ["1", "3", "7"])
 def test_replicated_bitmap_reduce_ranges(C, monkeypatch, chunks):
     """The replicated plan's all-reduce in k partition ranges (k not dividing
