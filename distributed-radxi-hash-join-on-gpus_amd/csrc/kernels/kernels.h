@@ -108,6 +108,15 @@ uint32_t sampleStrideFor(const PartitionGeometry &g, uint64_t n, uint32_t F, uin
 // (the tile set sampleScale() counts as seen); totals are cleared first.
 void netSampledTotals(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
                       uint64_t *totals, hipStream_t s, KeyMix mix, uint32_t sampleStride);
+// Both sides of a join in one launch (one clear when the totals are adjacent).
+struct SampledInput {
+  const data::Tuple *data;
+  uint64_t n;
+  PartitionGeometry geom;
+  uint32_t stride;
+  uint64_t *totals;  // [NGROUPS][F]
+};
+void netSampledTotals(const SampledInput *sides, uint32_t count, uint32_t bits, hipStream_t s, KeyMix mix);
 // totals[c][F] = sum of blockHist over the blocks of chunk c (blocksPerChunk each).
 void digitTotals(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint32_t blocksPerChunk,
                  uint32_t chunks, uint64_t *totals, hipStream_t s);
@@ -160,6 +169,14 @@ SampleScale sampleScale(const PartitionGeometry &g, uint64_t n, uint32_t sampleS
 uint64_t sampledLayoutCapacityBound(const SampleScale &sc, uint32_t F);
 void netSampledLayout(const uint64_t *sampled, uint32_t F, const SampleScale &sc, void *gstart, void *gcur, void *gend,
                       bool narrow, unsigned long long *capacityUsed, hipStream_t s);
+// One or two sides per launch (same cursor width).
+struct LayoutInput {
+  const uint64_t *sampled;
+  SampleScale sc;
+  void *gstart, *gcur, *gend;
+  unsigned long long *capacityUsed;
+};
+void netSampledLayout(const LayoutInput *sides, uint32_t count, uint32_t F, bool narrow, hipStream_t s);
 // gend (optional, same layout and width as gcur): end of every group slice.
 // Positions claimed past a slice end are not written; the final gcur values
 // tell the caller each slice's demand (the sampled pass re-runs exactly on

@@ -125,17 +125,28 @@ __host__ __device__ inline uint64_t sampledTile(uint64_t local, uint32_t g, uint
   return ((local / tpb) * NGROUPS + g) * tpb + local % tpb;
 }
 
-__global__ __launch_bounds__(NT) void netSampledTotalsKernel(const ulonglong2 *__restrict__ in, uint64_t n,
-                                                             uint32_t tpb, uint32_t blocks, uint32_t bits,
-                                                             uint32_t stride, unsigned long long *__restrict__ totals,
-                                                             KeyMix mix) {
+struct SampledSideArgs {
+  const ulonglong2 *in;
+  uint64_t n;
+  uint32_t tpb, blocks, stride;
+  unsigned long long *totals;  // [NGROUPS][F]
+};
+
+// Workgroups [0, wgA) sample side a, the rest side b (both sides of a join
+// in one launch).
+__global__ __launch_bounds__(NT) void netSampledTotalsKernel(SampledSideArgs a, SampledSideArgs b, uint32_t wgA,
+                                                             uint32_t bits, KeyMix mix) {
   extern __shared__ __attribute__((aligned(16))) uint32_t hsh[];
-  const uint32_t g = blockIdx.x % NGROUPS;
-  const uint64_t local = (uint64_t)(blockIdx.x / NGROUPS) * stride;
-  const uint64_t tile = sampledTile(local, g, tpb);
-  const uint64_t begin = tile * PART_TILE;
-  if (tile / tpb >= blocks || begin >= n) return;  // uniform over the workgroup
+  const bool onB = blockIdx.x >= wgA;
+  const SampledSideArgs &sd = onB ? b : a;
+  const uint32_t w = onB ? blockIdx.x - wgA : blockIdx.x;
+  const uint32_t g = w % NGROUPS;
+  const uint64_t local = (uint64_t)(w / NGROUPS) * sd.stride;
+  const uint64_t tile = sampledTile(local, g, sd.tpb);
+  const uint64_t begin = tile * PART_TILE, n = sd.n;
+  if (tile / sd.tpb >= sd.blocks || begin >= n) return;  // uniform over the workgroup
   const uint64_t end = min(n, begin + PART_TILE);
+  const ulonglong2 *__restrict__ in = sd.in;
   const uint32_t F = 1u << bits, mask = F - 1;
   for (uint32_t i = threadIdx.x; i < 4 * F; i += NT) hsh[i] = 0;
   __syncthreads();
@@ -154,7 +165,7 @@ __global__ __launch_bounds__(NT) void netSampledTotalsKernel(const ulonglong2 *_
   __syncthreads();
   for (uint32_t d = threadIdx.x; d < F; d += NT) {
     const uint32_t c = hsh[d] + hsh[F + d] + hsh[2 * F + d] + hsh[3 * F + d];
-    if (c) atomicAdd(&totals[(uint64_t)g * F + d], (unsigned long long)c);
+    if (c) atomicAdd(&sd.totals[(uint64_t)g * F + d], (unsigned long long)c);
   }
 }
 
@@ -180,21 +191,44 @@ uint32_t sampleStrideFor(const PartitionGeometry &g, uint64_t n, uint32_t F, uin
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(stride, most));
 }
 
+// Workgroups one side needs (sampled tiles of its largest XCD group x groups).
+static uint32_t sampledWorkgroups(const PartitionGeometry &g, uint64_t n, uint32_t stride) {
+  uint64_t perGroup = 0;
+  for (uint32_t gr = 0; gr < NGROUPS; ++gr) perGroup = std::max(perGroup, ceilDiv(groupTiles(g, n, gr), stride));
+  HJ_CHECK(perGroup * NGROUPS < (1ull << 30), "netSampledTotals: %llu sampled tiles", (unsigned long long)perGroup);
+  return (uint32_t)(perGroup * NGROUPS);
+}
+
+static SampledSideArgs sampledSide(const SampledInput &x) {
+  HJ_CHECK(x.stride >= 1, "netSampledTotals: sampleStride must be >= 1");
+  return SampledSideArgs{reinterpret_cast<const ulonglong2 *>(x.data), x.n, x.geom.tilesPerBlock, x.geom.blocks,
+                         x.stride, reinterpret_cast<unsigned long long *>(x.totals)};
+}
+
+void netSampledTotals(const SampledInput *sides, uint32_t count, uint32_t bits, hipStream_t s, KeyMix mix) {
+  HJ_CHECK(bits >= 1 && bits <= MAX_PART_BITS, "netSampledTotals: bits=%u out of range", bits);
+  HJ_CHECK(count == 1 || count == 2, "netSampledTotals: %u sides", count);
+  const uint32_t F = 1u << bits;
+  const size_t bytes = (size_t)NGROUPS * F * sizeof(uint64_t);
+  // Both sides' totals adjacent: one clear.
+  if (count == 2 && sides[1].totals == sides[0].totals + (size_t)NGROUPS * F) {
+    HIP_CHECK(hipMemsetAsync(sides[0].totals, 0, 2 * bytes, s));
+  } else {
+    for (uint32_t i = 0; i < count; ++i) HIP_CHECK(hipMemsetAsync(sides[i].totals, 0, bytes, s));
+  }
+  const SampledSideArgs a = sampledSide(sides[0]), b = count == 2 ? sampledSide(sides[1]) : a;
+  const uint32_t wgA = sampledWorkgroups(sides[0].geom, sides[0].n, sides[0].stride);
+  const uint32_t wgB = count == 2 ? sampledWorkgroups(sides[1].geom, sides[1].n, sides[1].stride) : 0;
+  if (wgA + wgB == 0) return;
+  const size_t lds = size_t(4) << bits << 2;
+  hipLaunchKernelGGL(netSampledTotalsKernel, dim3(wgA + wgB), dim3(NT), lds, s, a, b, wgA, bits, mix);
+  HIP_CHECK_LAUNCH();
+}
+
 void netSampledTotals(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
                       uint64_t *totals, hipStream_t s, KeyMix mix, uint32_t sampleStride) {
-  HJ_CHECK(bits >= 1 && bits <= MAX_PART_BITS, "netSampledTotals: bits=%u out of range", bits);
-  HJ_CHECK(sampleStride >= 1, "netSampledTotals: sampleStride must be >= 1");
-  const uint32_t F = 1u << bits;
-  HIP_CHECK(hipMemsetAsync(totals, 0, (size_t)NGROUPS * F * sizeof(uint64_t), s));
-  uint64_t perGroup = 0;  // sampled tiles of the largest group
-  for (uint32_t gr = 0; gr < NGROUPS; ++gr) perGroup = std::max(perGroup, ceilDiv(groupTiles(g, n, gr), sampleStride));
-  if (perGroup == 0) return;
-  HJ_CHECK(perGroup * NGROUPS < (1ull << 31), "netSampledTotals: %llu sampled tiles", (unsigned long long)perGroup);
-  const size_t lds = size_t(4) << bits << 2;
-  hipLaunchKernelGGL(netSampledTotalsKernel, dim3((uint32_t)(perGroup * NGROUPS)), dim3(NT), lds, s,
-                     reinterpret_cast<const ulonglong2 *>(in), n, g.tilesPerBlock, g.blocks, bits, sampleStride,
-                     reinterpret_cast<unsigned long long *>(totals), mix);
-  HIP_CHECK_LAUNCH();
+  const SampledInput one{in, n, g, sampleStride, totals};
+  netSampledTotals(&one, 1, bits, s, mix);
 }
 
 // --------------------------------------------------- digit totals / cursors
@@ -816,10 +850,24 @@ void netScatterFrag(const data::Tuple *in, uint64_t n, uint32_t bits, const Part
 // exact histogram: the slices are then exactly the counts, rounded to lines).
 constexpr int LAY_NT = 1024;
 template <typename CurT>
-__global__ __launch_bounds__(LAY_NT) void netSampledLayoutKernel(const unsigned long long *__restrict__ sampled,
-                                                                  uint32_t F, SampleScale sc, CurT *__restrict__ gstart,
-                                                                  CurT *__restrict__ gcur, CurT *__restrict__ gend,
-                                                                  unsigned long long *__restrict__ capacityUsed) {
+struct LayoutSideArgs {
+  const unsigned long long *sampled;
+  SampleScale sc;
+  CurT *gstart, *gcur, *gend;
+  unsigned long long *capacityUsed;
+};
+
+// Workgroup i lays out side i (one or two sides per launch).
+template <typename CurT>
+__global__ __launch_bounds__(LAY_NT) void netSampledLayoutKernel(LayoutSideArgs<CurT> s0, LayoutSideArgs<CurT> s1,
+                                                                  uint32_t F) {
+  const LayoutSideArgs<CurT> &ls = blockIdx.x ? s1 : s0;
+  const unsigned long long *__restrict__ sampled = ls.sampled;
+  const SampleScale &sc = ls.sc;
+  CurT *__restrict__ gstart = ls.gstart;
+  CurT *__restrict__ gcur = ls.gcur;
+  CurT *__restrict__ gend = ls.gend;
+  unsigned long long *__restrict__ capacityUsed = ls.capacityUsed;
   __shared__ unsigned long long wt[LAY_NT / WAVE];
   constexpr uint32_t G = NGROUPS;
   const uint32_t n = F * G;
@@ -868,19 +916,30 @@ __global__ __launch_bounds__(LAY_NT) void netSampledLayoutKernel(const unsigned 
   if (t == LAY_NT - 1) *capacityUsed = run;
 }
 
+template <typename CurT>
+static LayoutSideArgs<CurT> layoutSide(const LayoutInput &x) {
+  return LayoutSideArgs<CurT>{reinterpret_cast<const unsigned long long *>(x.sampled), x.sc,
+                              static_cast<CurT *>(x.gstart), static_cast<CurT *>(x.gcur), static_cast<CurT *>(x.gend),
+                              x.capacityUsed};
+}
+
+void netSampledLayout(const LayoutInput *sides, uint32_t count, uint32_t F, bool narrow, hipStream_t s) {
+  HJ_CHECK(F >= 1 && F <= (1u << MAX_PART_BITS), "netSampledLayout: F=%u", F);
+  HJ_CHECK(count == 1 || count == 2, "netSampledLayout: %u sides", count);
+  const LayoutInput &b = sides[count - 1];
+  if (narrow)
+    hipLaunchKernelGGL(netSampledLayoutKernel<uint32_t>, dim3(count), dim3(LAY_NT), 0, s,
+                       layoutSide<uint32_t>(sides[0]), layoutSide<uint32_t>(b), F);
+  else
+    hipLaunchKernelGGL(netSampledLayoutKernel<unsigned long long>, dim3(count), dim3(LAY_NT), 0, s,
+                       layoutSide<unsigned long long>(sides[0]), layoutSide<unsigned long long>(b), F);
+  HIP_CHECK_LAUNCH();
+}
+
 void netSampledLayout(const uint64_t *sampled, uint32_t F, const SampleScale &sc, void *gstart, void *gcur, void *gend,
                       bool narrow, unsigned long long *capacityUsed, hipStream_t s) {
-  HJ_CHECK(F >= 1 && F <= (1u << MAX_PART_BITS), "netSampledLayout: F=%u", F);
-  const auto *src = reinterpret_cast<const unsigned long long *>(sampled);
-  if (narrow)
-    hipLaunchKernelGGL(netSampledLayoutKernel<uint32_t>, dim3(1), dim3(LAY_NT), 0, s, src, F, sc,
-                       static_cast<uint32_t *>(gstart), static_cast<uint32_t *>(gcur), static_cast<uint32_t *>(gend),
-                       capacityUsed);
-  else
-    hipLaunchKernelGGL(netSampledLayoutKernel<unsigned long long>, dim3(1), dim3(LAY_NT), 0, s, src, F, sc,
-                       static_cast<unsigned long long *>(gstart), static_cast<unsigned long long *>(gcur),
-                       static_cast<unsigned long long *>(gend), capacityUsed);
-  HIP_CHECK_LAUNCH();
+  const LayoutInput one{sampled, sc, gstart, gcur, gend, capacityUsed};
+  netSampledLayout(&one, 1, F, narrow, s);
 }
 
 SampleScale sampleScale(const PartitionGeometry &g, uint64_t n, uint32_t sampleStride, bool exact) {

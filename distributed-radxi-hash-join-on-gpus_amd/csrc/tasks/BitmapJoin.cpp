@@ -1,6 +1,8 @@
 #include "BitmapJoin.h"
 
 #include <algorithm>
+#include <map>
+#include <tuple>
 #include <cstdlib>
 #include <vector>
 
@@ -32,59 +34,107 @@ BitmapJoin::BitmapJoin(data::Relation *innerRelation, data::Relation *outerRelat
 
 BitmapJoin::Outcome BitmapJoin::run(bool exact) { return ctx->onDevice() ? runDevice(exact) : runHost(); }
 
+// Geometry, sample stride, scale and capacity bound of one side: pure
+// functions of the sizes, but their host loops (every block and sampled tile)
+// took ~20 us per join in front of the first kernel, so they are computed
+// once per thread (in-process ranks are threads) and size.
+const BitmapJoin::SidePlan &BitmapJoin::sidePlan(uint64_t n, bool exact, uint32_t stride) const {
+  struct Key {
+    uint64_t n;
+    uint32_t maxBlocks, bits, stride;
+    bool exact;
+    bool operator<(const Key &o) const {
+      return std::tie(n, maxBlocks, bits, stride, exact) < std::tie(o.n, o.maxBlocks, o.bits, o.stride, o.exact);
+    }
+  };
+  thread_local std::map<Key, SidePlan> cache;
+  const uint32_t F = 1u << plan.networkBits;
+  const Key k{n, maxBlocks, plan.networkBits, stride, exact};
+  auto it = cache.find(k);
+  if (it != cache.end()) return it->second;
+  if (cache.size() > 64) cache.clear();
+  SidePlan sp;
+  sp.geom = kernels::partitionGeometry(n, maxBlocks);
+  sp.stride = exact ? 1 : kernels::sampleStrideFor(sp.geom, n, F, stride);
+  sp.sc = kernels::sampleScale(sp.geom, n, sp.stride, exact);
+  sp.cap = kernels::sampledLayoutCapacityBound(sp.sc, F);
+  return cache.emplace(k, sp).first->second;
+}
+
 // Sampled (or exact) histogram -> device layout of bounded claim slices ->
 // bounded claim scatter of u32 fragments.  Nothing here waits for the device.
 bool BitmapJoin::sideNarrow(data::Relation *r, bool exact) const {
   const uint64_t n = r->getLocalSize();
-  const kernels::PartitionGeometry g = kernels::partitionGeometry(n, maxBlocks);
-  const uint32_t stride = exact ? 1 : kernels::sampleStrideFor(g, n, 1u << plan.networkBits, sampleStride);
-  const kernels::SampleScale sc = kernels::sampleScale(g, n, stride, exact);
-  return kernels::cursorsNarrow(kernels::sampledLayoutCapacityBound(sc, 1u << plan.networkBits) + n);
+  return kernels::cursorsNarrow(sidePlan(n, exact, sampleStride).cap + n);
 }
 
-void BitmapJoin::partitionSide(Side &s, bool exact, bool narrowOk, hipEvent_t from, hipEvent_t to) {
+// Sampled (or exact) totals and the device layout of the bounded claim
+// slices of one or both sides: one totals launch and one layout launch for
+// both (every kernel boundary is ~5 us of idle GPU).
+void BitmapJoin::layoutSides(Side *sides, uint32_t count, bool exact, bool narrowOk) {
   const uint32_t bits = plan.networkBits, F = 1u << bits, G = CLAIM_GROUPS;
-  const uint64_t n = s.relation->getLocalSize();
   memory::Arena &ws = ctx->workspace();
   const hipStream_t st = ctx->stream();
   const kernels::KeyMix mix{plan.keyMix ? 1u : 0u, plan.keyBits};
-  const bool isInner = s.relation == inner;
-  performance::Timeline &tl = ctx->timeline();
-  const char *histKey = isInner ? "HILOCAL" : "HOLOCAL", *partKey = isInner ? "MIMAINPART" : "MOMAINPART";
-  tl.beginAt(histKey, from);
-  s.geom = kernels::partitionGeometry(n, maxBlocks);
-  const uint32_t stride = exact ? 1 : kernels::sampleStrideFor(s.geom, n, F, sampleStride);
-  uint64_t *totals = ws.getArray<uint64_t>((uint64_t)G * F);
-  if (stride > 1) {
-    kernels::netSampledTotals(s.relation->getData(), n, bits, s.geom, totals, st, mix, stride);
-  } else {
-    uint32_t *blockHist = ws.getArray<uint32_t>((uint64_t)F * s.geom.blocks);
-    kernels::netHistogram(s.relation->getData(), n, bits, s.geom, blockHist, st, mix, 1);
-    kernels::netGroupTotals(blockHist, F, s.geom.blocks, totals, st);
+  uint64_t *totals = ws.getArray<uint64_t>((uint64_t)count * G * F);  // adjacent: one clear
+  kernels::SampledInput in[2];
+  kernels::LayoutInput lay[2];
+  bool sampled = !exact;
+  bool narrow = narrowOk;
+  for (uint32_t i = 0; i < count; ++i) {
+    Side &s = sides[i];
+    const uint64_t n = s.relation->getLocalSize();
+    const SidePlan &sp = sidePlan(n, exact, sampleStride);
+    s.geom = sp.geom;
+    const uint32_t stride = sp.stride;
+    sampled = sampled && stride > 1;
+    in[i] = kernels::SampledInput{s.relation->getData(), n, s.geom, stride, totals + (size_t)i * G * F};
+    const kernels::SampleScale &sc = sp.sc;
+    s.cap = sp.cap;
+    // Claims may run past a slice end by up to n before the overflow is seen.
+    narrow = narrow && kernels::cursorsNarrow(s.cap + n);
+    lay[i].sampled = in[i].totals;
+    lay[i].sc = sc;
   }
-  const kernels::SampleScale sc = kernels::sampleScale(s.geom, n, stride, exact);
-  const uint64_t cap = kernels::sampledLayoutCapacityBound(sc, F);
-  // Claims may run past a slice end by up to n before the overflow is seen.
-  const bool narrow = narrowOk && kernels::cursorsNarrow(cap + n);
+  if (sampled) {
+    kernels::netSampledTotals(in, count, bits, st, mix);
+  } else {  // exact histograms (or an input too small to sample): every tile, per block
+    for (uint32_t i = 0; i < count; ++i) {
+      uint32_t *blockHist = ws.getArray<uint32_t>((uint64_t)F * in[i].geom.blocks);
+      kernels::netHistogram(in[i].data, in[i].n, bits, in[i].geom, blockHist, st, mix, 1);
+      kernels::netGroupTotals(blockHist, F, in[i].geom.blocks, in[i].totals, st);
+      if (in[i].stride > 1) {  // sampled side next to an exact one: its scale counts every tile now
+        const SidePlan &one = sidePlan(in[i].n, exact, 1);
+        lay[i].sc = one.sc;
+        sides[i].cap = one.cap;
+      }
+    }
+  }
   const size_t cb = narrow ? 4 : 8;
-  void *gstart = ws.get((size_t)G * F * cb), *gcur = ws.get((size_t)G * F * cb), *gend = ws.get((size_t)G * F * cb);
-  unsigned long long *used = ws.getArray<unsigned long long>(1);
-  kernels::netSampledLayout(totals, F, sc, gstart, gcur, gend, narrow, used, st);
-  hipEvent_t mid = tl.mark(st);  // one event ends the histogram and begins the scatter
-  tl.endAt(histKey, mid);
-  s.frags = ws.getArray<uint32_t>(std::max<uint64_t>(cap, 16));
-  tl.beginAt(partKey, mid);
-  kernels::netScatterFrag(s.relation->getData(), n, bits, s.geom, 0, s.geom.blocks, gcur, s.frags, st, plan.keyBits,
-                          mix, gend, narrow ? 1 : 0);
-  if (to) HIP_CHECK(hipEventRecord(to, st));
-  tl.endAt(partKey, to);
-  s.slices = BitmapSlices();
-  s.slices.kind = BitmapSlices::Claim;
-  s.slices.start = gstart;
-  s.slices.cur = gcur;
-  s.slices.end = gend;
-  s.slices.narrow = narrow;
-  s.slices.count = n;
+  for (uint32_t i = 0; i < count; ++i) {
+    lay[i].gstart = ws.get((size_t)G * F * cb);
+    lay[i].gcur = ws.get((size_t)G * F * cb);
+    lay[i].gend = ws.get((size_t)G * F * cb);
+    lay[i].capacityUsed = ws.getArray<unsigned long long>(1);
+    Side &s = sides[i];
+    s.slices = BitmapSlices();
+    s.slices.kind = BitmapSlices::Claim;
+    s.slices.start = lay[i].gstart;
+    s.slices.cur = lay[i].gcur;
+    s.slices.end = lay[i].gend;
+    s.slices.narrow = narrow;
+    s.slices.count = s.relation->getLocalSize();
+    s.frags = ws.getArray<uint32_t>(std::max<uint64_t>(s.cap, 16));
+  }
+  kernels::netSampledLayout(lay, count, F, narrow, st);
+}
+
+// The bounded claim scatter of one side's u32 fragments into its slices.
+void BitmapJoin::scatterSide(Side &s) {
+  const kernels::KeyMix mix{plan.keyMix ? 1u : 0u, plan.keyBits};
+  kernels::netScatterFrag(s.relation->getData(), s.relation->getLocalSize(), plan.networkBits, s.geom, 0,
+                          s.geom.blocks, const_cast<void *>(s.slices.cur), s.frags, ctx->stream(), plan.keyBits, mix,
+                          s.slices.end, s.slices.narrow ? 1 : 0);
 }
 
 // Partition ranges of the replicated plan's all-reduce: one per 32 MiB of
@@ -105,7 +155,6 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
   memory::Arena &ws = ctx->workspace();
   BitmapCounters *cnt = ws.getArray<BitmapCounters>(1);
   HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(BitmapCounters), st));
-  Side si{inner, {}, nullptr, {}}, so{outer, {}, nullptr, {}};
   Outcome o;
   // One cursor width for both sides (the fused N = 1 kernel reads both with
   // one slice type; e.g. 1B inner x 4B outer needs 8-byte cursors on both).
@@ -114,21 +163,36 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
   // ev[0] join start, ev[1] inner side partitioned, ev[2] outer side
   // partitioned, ev[3] probe start (N > 1: after the all-reduce), ev[4] end.
   performance::Timeline &tl = ctx->timeline();
+  Side both[2] = {Side{inner, {}, nullptr, {}}, Side{outer, {}, nullptr, {}}};
   {
     performance::TraceRange tr("bitmap_network_inner");
     utils::faultPoint("network");
-    partitionSide(si, exact, narrowOk, ev[0], ev[1]);
+    // Both sides' histograms and layouts first (one launch each), charged to
+    // HILOCAL / HOLOCAL by tuples; then the scatters.
+    tl.beginSplitAt("HLOCAL", "HILOCAL", (double)inner->getLocalSize(), "HOLOCAL", (double)outer->getLocalSize(),
+                    ev[0]);
+    layoutSides(both, 2, exact, narrowOk);
+    hipEvent_t mid = tl.mark(st);
+    tl.endAt("HLOCAL", mid);
+    tl.beginAt("MIMAINPART", mid);
+    scatterSide(both[0]);
+    HIP_CHECK(hipEventRecord(ev[1], st));
+    tl.endAt("MIMAINPART", ev[1]);
   }
+  Side &ri = both[0], &ro = both[1];
   hipEvent_t joinStart = ev[2];
   if (N == 1) {
-    partitionSide(so, exact, narrowOk, ev[1], ev[2]);
+    tl.beginAt("MOMAINPART", ev[1]);
+    scatterSide(ro);
+    HIP_CHECK(hipEventRecord(ev[2], st));
+    tl.endAt("MOMAINPART", ev[2]);
     utils::faultPoint("local");
     utils::faultPoint("build_probe");
     // One kernel builds and probes: charged to BPBUILD / BPPROBE by tuples read.
     tl.beginAt("BPTASKTIME", ev[2]);
     tl.beginSplitAt("BPKERNEL", "BPBUILD", (double)inner->getLocalSize(), "BPPROBE", (double)outer->getLocalSize(),
                     ev[2]);
-    kernels::bitmapJoin(4, si.frags, so.frags, si.slices, so.slices, F, 0, bits, cnt, st);
+    kernels::bitmapJoin(4, ri.frags, ro.frags, ri.slices, ro.slices, F, 0, bits, cnt, st);
     HIP_CHECK(hipEventRecord(ev[4], st));
     tl.endAt("BPKERNEL", ev[4]);
     tl.endAt("BPTASKTIME", ev[4]);
@@ -138,7 +202,7 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
     utils::faultPoint("local");
     tl.beginAt("BPTASKTIME", ev[1]);
     tl.beginAt("BPBUILD", ev[1]);
-    kernels::bitmapBuild(4, si.frags, si.slices, F, 0, bits, bm, cnt, st);
+    kernels::bitmapBuild(4, ri.frags, ri.slices, F, 0, bits, bm, cnt, st);
     // A time point the streams also synchronise on (a timing event when the
     // timeline is on, a pooled sync-only event otherwise).
     auto point = [&](hipStream_t s) {
@@ -168,7 +232,10 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
     }
     tl.endAt("MWINPUT", reduced[K - 1]);
     o.linkBytes = (uint64_t)(2.0 * (N - 1) / N * (double)F * words * 4);
-    partitionSide(so, exact, narrowOk, built, ev[2]);
+    tl.beginAt("MOMAINPART", built);
+    scatterSide(ro);
+    HIP_CHECK(hipEventRecord(ev[2], st));
+    tl.endAt("MOMAINPART", ev[2]);
     HIP_CHECK(hipStreamWaitEvent(st, reduced[0], 0));
     HIP_CHECK(hipEventRecord(ev[3], st));
     joinStart = ev[3];
@@ -177,7 +244,7 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
     for (uint32_t c = 0; c < K; ++c) {
       const uint32_t p0 = (uint32_t)((uint64_t)F * c / K), p1 = (uint32_t)((uint64_t)F * (c + 1) / K);
       if (c) HIP_CHECK(hipStreamWaitEvent(st, reduced[c], 0));
-      kernels::bitmapProbe(4, so.frags, so.slices, F, 0, bits, bm, cnt, st, p0, p1 - p0);
+      kernels::bitmapProbe(4, ro.frags, ro.slices, F, 0, bits, bm, cnt, st, p0, p1 - p0);
     }
     HIP_CHECK(hipEventRecord(ev[4], st));
     tl.endAt("BPPROBE", ev[4]);

@@ -68,12 +68,19 @@ class BitmapJoin {
     kernels::PartitionGeometry geom;
     uint32_t *frags = nullptr;
     kernels::BitmapSlices slices;
+    uint64_t cap = 0;  // fragment capacity of all slices
   };
   // narrowOk: 4-byte claim cursors are allowed (both sides of a fused bitmap
   // join must use the same cursor width; sideNarrow() says what one side needs).
-  // Device: the side's spans run from `from` (already recorded) to `to`,
-  // which is recorded on the compute stream when its scatter is enqueued.
-  void partitionSide(Side &s, bool exact, bool narrowOk, hipEvent_t from = nullptr, hipEvent_t to = nullptr);
+  struct SidePlan {
+    kernels::PartitionGeometry geom;
+    uint32_t stride = 1;
+    kernels::SampleScale sc{};
+    uint64_t cap = 0;
+  };
+  const SidePlan &sidePlan(uint64_t n, bool exact, uint32_t stride) const;
+  void layoutSides(Side *sides, uint32_t count, bool exact, bool narrowOk);
+  void scatterSide(Side &s);
   bool sideNarrow(data::Relation *r, bool exact) const;
   Outcome runDevice(bool exact);
   Outcome runHost();
