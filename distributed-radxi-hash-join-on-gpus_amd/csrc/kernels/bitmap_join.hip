@@ -31,16 +31,10 @@
 namespace hpcjoin {
 namespace kernels {
 
-constexpr int BM_U = 4;  // default 16-byte loads in flight per lane (64 B, as 8 x 8-byte loads before)
-
-// Loads in flight per lane: 4 (default) or 8 (HPCJOIN_BM_U=8, sweep).
-static int bmUnroll() {
-  static const int v = [] {
-    const char *e = std::getenv("HPCJOIN_BM_U");
-    return e && std::atoi(e) == 8 ? 8 : BM_U;
-  }();
-  return v;
-}
+// 16-byte loads in flight per lane.  (HPCJOIN_BM_U=8 was a sweep variant:
+// 2.71 -> 2.66 ms on the pre-pipelined kernel; with the pipelined walks it
+// needs 128 VGPRs and spills, so only 4 is built.)
+constexpr int BM_U = 4;
 
 using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
 
@@ -434,14 +428,8 @@ static uint32_t bmFlat(const BitmapSlices &a, const BitmapSlices *b, uint32_t pa
       using E = uint32_t;                                                                                        \
       if (src.narrow) {                                                                                          \
         using S = ClaimSrc<uint32_t>;                                                                            \
-        if (bmUnroll() == 8 && nth == 1024) {                                                                    \
-          constexpr int U = 8;                                                                                   \
-          constexpr int NTH = 1024;                                                                              \
-          __VA_ARGS__;                                                                                           \
-        } else {                                                                                                 \
-          constexpr int U = BM_U;                                                                                \
-          HJ_BM_NTH(__VA_ARGS__);                                                                                   \
-        }                                                                                                        \
+        constexpr int U = BM_U;                                                                                  \
+        HJ_BM_NTH(__VA_ARGS__);                                                                                  \
       } else {                                                                                                   \
         using S = ClaimSrc<unsigned long long>;                                                                  \
         constexpr int U = BM_U;                                                                                  \
