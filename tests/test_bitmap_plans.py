@@ -138,6 +138,23 @@ def test_bitmap_split_pieces(C, nb, dup):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_ranks", [1, 4])
+@pytest.mark.parametrize("G_R,G_S", [(1000, 0), (37, 5000), (3, 3), (100_000, 1)])
+def test_bitmap_tiny_and_empty_sides(C, n_ranks, G_R, G_S):
+    """Tiny and empty relations (some ranks hold no tuples at all): the
+    sampled layout falls back to exact counts, one-launch histograms and
+    layouts of both sides, exact results."""
+    inner = C.GenSpec(seed=8)
+    outer = C.GenSpec(distribution=C.KeyDistribution.UNIFORM, seed=9, domain=G_R)
+    exp = C.Relation.expected_matches(inner, G_R, outer, G_S) if G_S else 0
+    out = run_ranks(C, n_ranks, "device", generated(C, "device", inner, G_R, n_ranks),
+                    generated(C, "device", outer, G_S, n_ranks), G_R, G_S, lambda c: force_replicated(c, C))
+    for res_list, _ in out:
+        for res in res_list:
+            assert res["global_matches"] == exp, (G_R, G_S, n_ranks, res["global_matches"], exp)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("chunks", ["1", "3", "7"])
 def test_replicated_bitmap_reduce_ranges(C, monkeypatch, chunks):
     """The replicated plan's all-reduce in k partition ranges (k not dividing
