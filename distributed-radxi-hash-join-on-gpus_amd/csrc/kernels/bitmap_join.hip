@@ -335,17 +335,19 @@ __global__ __launch_bounds__(NTH) void bitmapJoinKernel(const E *__restrict__ r,
 
 template <typename E, int U, class Src, int NTH>
 __global__ __launch_bounds__(NTH) void bitmapBuildKernel(const E *__restrict__ r, Src rs, uint32_t shift,
-                                                         uint32_t words, uint32_t flat, uint32_t *__restrict__ bitmaps,
+                                                         uint32_t words, uint32_t flat, uint32_t partBase,
+                                                         uint32_t *__restrict__ bitmaps,
                                                          BitmapCounters *__restrict__ out) {
   extern __shared__ uint32_t bm[];
   __shared__ uint64_t wt[NTH / WAVE];
   for (uint32_t w = threadIdx.x; w < words; w += NTH) bm[w] = 0;
   __syncthreads();
+  const uint32_t d = partBase + blockIdx.x;
   uint32_t flags = 0;
-  const uint64_t inserted = bmBuild<NTH, E, U>(bm, r, rs, blockIdx.x, shift, flat, (uint64_t)words * 32, flags);
+  const uint64_t inserted = bmBuild<NTH, E, U>(bm, r, rs, d, shift, flat, (uint64_t)words * 32, flags);
   __syncthreads();
   bmCheckDup<NTH>(bm, words, inserted, flags, wt);
-  uint32_t *dst = bitmaps + (size_t)blockIdx.x * words;
+  uint32_t *dst = bitmaps + (size_t)d * words;
   for (uint32_t w = threadIdx.x; w < words; w += NTH) dst[w] = bm[w];
   bmFinish(out, 0, 0, flags);
 }
@@ -479,14 +481,18 @@ void bitmapJoin(uint32_t elemBytes, const void *r, const void *s, const BitmapSl
 }
 
 void bitmapBuild(uint32_t elemBytes, const void *r, const BitmapSlices &src, uint32_t partitions, uint32_t keyShift,
-                 uint32_t bits, uint32_t *bitmaps, BitmapCounters *out, hipStream_t st) {
+                 uint32_t bits, uint32_t *bitmaps, BitmapCounters *out, hipStream_t st, uint32_t first,
+                 uint32_t count) {
   checkBits(bits, keyShift, elemBytes);
-  if (partitions == 0) return;
+  if (count == UINT32_MAX) count = partitions - std::min(first, partitions);
+  HJ_CHECK(first <= partitions && count <= partitions - first, "bitmapBuild: partitions [%u, +%u) of %u", first, count,
+           partitions);
+  if (partitions == 0 || count == 0) return;
   const uint32_t words = bitmapWords(bits);
   const uint32_t flat = bmFlat(src, nullptr, partitions);
-  HJ_BM_DISPATCH(hipLaunchKernelGGL((bitmapBuildKernel<E, U, S, NTH>), dim3(partitions), dim3(NTH), (size_t)words * 4, st,
-                                    static_cast<const E *>(r), makeSrc<S>(src, partitions), keyShift, words, flat, bitmaps,
-                                    out));
+  HJ_BM_DISPATCH(hipLaunchKernelGGL((bitmapBuildKernel<E, U, S, NTH>), dim3(count), dim3(NTH), (size_t)words * 4, st,
+                                    static_cast<const E *>(r), makeSrc<S>(src, partitions), keyShift, words, flat,
+                                    first, bitmaps, out));
   HIP_CHECK_LAUNCH();
 }
 

@@ -375,8 +375,10 @@ uint32_t bitmapWords(uint32_t bits);
 void bitmapJoin(uint32_t elemBytes, const void *r, const void *s, const BitmapSlices &rs, const BitmapSlices &ss,
                 uint32_t partitions, uint32_t keyShift, uint32_t bits, BitmapCounters *out, hipStream_t st);
 // bitmaps[d * bitmapWords(bits) ...] = partition d's bitmap of r.
+// Partitions [first, first + count) only (count = UINT32_MAX: to the end).
 void bitmapBuild(uint32_t elemBytes, const void *r, const BitmapSlices &rs, uint32_t partitions, uint32_t keyShift,
-                 uint32_t bits, uint32_t *bitmaps, BitmapCounters *out, hipStream_t st);
+                 uint32_t bits, uint32_t *bitmaps, BitmapCounters *out, hipStream_t st, uint32_t first = 0,
+                 uint32_t count = UINT32_MAX);
 // Probes s against bitmaps (e.g. all-reduced over ranks); out->popcount += set bits.
 // Partitions [first, first + count) only (count = UINT32_MAX: to the end);
 // slices and bitmaps are indexed by the global partition number.

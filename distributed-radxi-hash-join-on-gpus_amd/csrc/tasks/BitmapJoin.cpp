@@ -202,7 +202,6 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
     utils::faultPoint("local");
     tl.beginAt("BPTASKTIME", ev[1]);
     tl.beginAt("BPBUILD", ev[1]);
-    kernels::bitmapBuild(4, ri.frags, ri.slices, F, 0, bits, bm, cnt, st);
     // A time point the streams also synchronise on (a timing event when the
     // timeline is on, a pooled sync-only event otherwise).
     auto point = [&](hipStream_t s) {
@@ -213,26 +212,29 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
       }
       return e;
     };
-    hipEvent_t built = point(st);
-    tl.endAt("BPBUILD", built);
-    HIP_CHECK(hipStreamWaitEvent(ctx->commStream(), built, 0));
     // The all-reduce (exchange stream) overlaps the outer side's network pass:
-    // the plan's one link transfer (the reference's puts, MWINPUT).  It runs
-    // in K partition ranges; the probe of a range starts as soon as the range
-    // is reduced, so after the last range lands only its probe is left.
+    // the plan's one link transfer (the reference's puts, MWINPUT).  Build and
+    // all-reduce run in K partition ranges: range c's all-reduce starts when
+    // its bitmaps are built (while range c + 1 builds), and the probe of a
+    // range starts as soon as it is reduced, so after the last range lands
+    // only its probe is left.
     const uint32_t K = std::min<uint32_t>(reduceChunks((uint64_t)F * words * 4), F);
-    tl.beginAt("MWINPUT", built);
-    std::vector<hipEvent_t> reduced(K);
+    std::vector<hipEvent_t> built(K), reduced(K);
     for (uint32_t c = 0; c < K; ++c) {
       const uint32_t p0 = (uint32_t)((uint64_t)F * c / K), p1 = (uint32_t)((uint64_t)F * (c + 1) / K);
+      kernels::bitmapBuild(4, ri.frags, ri.slices, F, 0, bits, bm, cnt, st, p0, p1 - p0);
+      built[c] = point(st);
+      if (c == 0) tl.beginAt("MWINPUT", built[0]);
+      HIP_CHECK(hipStreamWaitEvent(ctx->commStream(), built[c], 0));
       performance::Measurements::add("MWINPUTCNT", 1, "calls");
       ctx->comm()->allReduceSumDevice(reinterpret_cast<uint64_t *>(bm + (size_t)p0 * words),
                                       (size_t)(p1 - p0) * words / 2, ctx->commStream());
       reduced[c] = point(ctx->commStream());
     }
+    tl.endAt("BPBUILD", built[K - 1]);
     tl.endAt("MWINPUT", reduced[K - 1]);
     o.linkBytes = (uint64_t)(2.0 * (N - 1) / N * (double)F * words * 4);
-    tl.beginAt("MOMAINPART", built);
+    tl.beginAt("MOMAINPART", built[K - 1]);
     scatterSide(ro);
     HIP_CHECK(hipEventRecord(ev[2], st));
     tl.endAt("MOMAINPART", ev[2]);
