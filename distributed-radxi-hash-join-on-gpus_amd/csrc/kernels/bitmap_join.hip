@@ -335,31 +335,36 @@ __global__ __launch_bounds__(NTH) void bitmapJoinKernel(const E *__restrict__ r,
 
 template <typename E, int U, class Src, int NTH>
 __global__ __launch_bounds__(NTH) void bitmapBuildKernel(const E *__restrict__ r, Src rs, uint32_t shift,
-                                                         uint32_t words, uint32_t flat, uint32_t partBase,
-                                                         uint32_t *__restrict__ bitmaps,
+                                                         uint32_t words, uint32_t flat, uint32_t pieceBase,
+                                                         uint32_t split, uint32_t *__restrict__ bitmaps,
                                                          BitmapCounters *__restrict__ out) {
   extern __shared__ uint32_t bm[];
   __shared__ uint64_t wt[NTH / WAVE];
   for (uint32_t w = threadIdx.x; w < words; w += NTH) bm[w] = 0;
   __syncthreads();
-  const uint32_t d = partBase + blockIdx.x;
+  // Piece q = (partition d, h-th 2^-split of its fragment range); pieces of a
+  // partition are adjacent in `bitmaps`, so the array is the partitions' full
+  // bitmaps in order whatever the split.
+  const uint32_t q = pieceBase + blockIdx.x, d = q >> split;
+  const uint64_t limit = (uint64_t)words * 32, base = (uint64_t)(q & ((1u << split) - 1)) * limit;
   uint32_t flags = 0;
-  const uint64_t inserted = bmBuild<NTH, E, U>(bm, r, rs, d, shift, flat, (uint64_t)words * 32, flags);
+  const uint64_t inserted = bmBuild<NTH, E, U>(bm, r, rs, d, shift, flat, limit, flags, base, split);
   __syncthreads();
   bmCheckDup<NTH>(bm, words, inserted, flags, wt);
-  uint32_t *dst = bitmaps + (size_t)d * words;
+  uint32_t *dst = bitmaps + (size_t)q * words;
   for (uint32_t w = threadIdx.x; w < words; w += NTH) dst[w] = bm[w];
   bmFinish(out, 0, 0, flags);
 }
 
 template <typename E, int U, class Src, int NTH>
 __global__ __launch_bounds__(NTH) void bitmapProbeKernel(const E *__restrict__ s, Src ss, uint32_t shift,
-                                                         uint32_t words, uint32_t flat, uint32_t partBase,
-                                                         const uint32_t *__restrict__ bitmaps,
+                                                         uint32_t words, uint32_t flat, uint32_t pieceBase,
+                                                         uint32_t split, const uint32_t *__restrict__ bitmaps,
                                                          BitmapCounters *__restrict__ out) {
   extern __shared__ uint32_t bm[];
-  const uint32_t d = partBase + blockIdx.x;
-  const u32x4 *src = reinterpret_cast<const u32x4 *>(bitmaps + (size_t)d * words);
+  const uint32_t q = pieceBase + blockIdx.x, d = q >> split;
+  const uint64_t limit = (uint64_t)words * 32, base = (uint64_t)(q & ((1u << split) - 1)) * limit;
+  const u32x4 *src = reinterpret_cast<const u32x4 *>(bitmaps + (size_t)q * words);
   uint64_t bits = 0;
   for (uint32_t w = threadIdx.x; w < words / 4; w += NTH) {  // words is a power of two >= 32
     const u32x4 x = __builtin_nontemporal_load(src + w);
@@ -371,7 +376,7 @@ __global__ __launch_bounds__(NTH) void bitmapProbeKernel(const E *__restrict__ s
   }
   __syncthreads();
   uint32_t flags = 0;
-  const uint64_t cnt = bmProbe<NTH, E, U>(bm, s, ss, d, shift, flat, (uint64_t)words * 32, flags);
+  const uint64_t cnt = bmProbe<NTH, E, U>(bm, s, ss, d, shift, flat, limit, flags, base);
   bmFinish(out, cnt, bits, flags);
 }
 
@@ -483,32 +488,34 @@ void bitmapJoin(uint32_t elemBytes, const void *r, const void *s, const BitmapSl
 void bitmapBuild(uint32_t elemBytes, const void *r, const BitmapSlices &src, uint32_t partitions, uint32_t keyShift,
                  uint32_t bits, uint32_t *bitmaps, BitmapCounters *out, hipStream_t st, uint32_t first,
                  uint32_t count) {
-  checkBits(bits, keyShift, elemBytes);
+  checkBits(bits, keyShift, elemBytes, BITMAP_MAX_SPLIT);
   if (count == UINT32_MAX) count = partitions - std::min(first, partitions);
   HJ_CHECK(first <= partitions && count <= partitions - first, "bitmapBuild: partitions [%u, +%u) of %u", first, count,
            partitions);
   if (partitions == 0 || count == 0) return;
-  const uint32_t words = bitmapWords(bits);
+  const uint32_t split = bits > BITMAP_MAX_BITS ? bits - BITMAP_MAX_BITS : 0;
+  const uint32_t words = bitmapWords(bits - split);
   const uint32_t flat = bmFlat(src, nullptr, partitions);
-  HJ_BM_DISPATCH(hipLaunchKernelGGL((bitmapBuildKernel<E, U, S, NTH>), dim3(count), dim3(NTH), (size_t)words * 4, st,
-                                    static_cast<const E *>(r), makeSrc<S>(src, partitions), keyShift, words, flat,
-                                    first, bitmaps, out));
+  HJ_BM_DISPATCH(hipLaunchKernelGGL((bitmapBuildKernel<E, U, S, NTH>), dim3(count << split), dim3(NTH),
+                                    (size_t)words * 4, st, static_cast<const E *>(r), makeSrc<S>(src, partitions),
+                                    keyShift, words, flat, first << split, split, bitmaps, out));
   HIP_CHECK_LAUNCH();
 }
 
 void bitmapProbe(uint32_t elemBytes, const void *s, const BitmapSlices &src, uint32_t partitions, uint32_t keyShift,
                  uint32_t bits, const uint32_t *bitmaps, BitmapCounters *out, hipStream_t st, uint32_t first,
                  uint32_t count) {
-  checkBits(bits, keyShift, elemBytes);
+  checkBits(bits, keyShift, elemBytes, BITMAP_MAX_SPLIT);
   if (count == UINT32_MAX) count = partitions - std::min(first, partitions);
   HJ_CHECK(first <= partitions && count <= partitions - first, "bitmapProbe: partitions [%u, +%u) of %u", first, count,
            partitions);
   if (partitions == 0 || count == 0) return;
-  const uint32_t words = bitmapWords(bits);
+  const uint32_t split = bits > BITMAP_MAX_BITS ? bits - BITMAP_MAX_BITS : 0;
+  const uint32_t words = bitmapWords(bits - split);
   const uint32_t flat = bmFlat(src, nullptr, partitions);
-  HJ_BM_DISPATCH(hipLaunchKernelGGL((bitmapProbeKernel<E, U, S, NTH>), dim3(count), dim3(NTH), (size_t)words * 4, st,
-                                    static_cast<const E *>(s), makeSrc<S>(src, partitions), keyShift, words, flat, first, bitmaps,
-                                    out));
+  HJ_BM_DISPATCH(hipLaunchKernelGGL((bitmapProbeKernel<E, U, S, NTH>), dim3(count << split), dim3(NTH),
+                                    (size_t)words * 4, st, static_cast<const E *>(s), makeSrc<S>(src, partitions),
+                                    keyShift, words, flat, first << split, split, bitmaps, out));
   HIP_CHECK_LAUNCH();
 }
 #undef HJ_BM_DISPATCH

@@ -341,7 +341,7 @@ void buildProbe(const BPArgs &a, const BPItem *items, const uint32_t *nItems, ui
 //   elemBytes 8: CompressedTuples (fragment = value >> keyShift), partitions
 //                given as a segment table [F][groups] (exchanged windows)
 constexpr uint32_t BITMAP_MAX_BITS = 20;  // 128 KiB of LDS
-// The fused N = 1 kernel may split a partition's fragment range over 2^split
+// The bitmap kernels may split a partition's fragment range over 2^split
 // workgroups (each holds one 128 KiB piece and reads all of the partition's
 // fragments): 21 fragment bits, e.g. 3B dense keys over a 2048-way digit.
 constexpr uint32_t BITMAP_MAX_SPLIT = 1;

@@ -193,10 +193,10 @@ void HashJoin::planBitmap() {
   const uint32_t nb =
       config.networkBits ? config.networkBits : std::min<uint32_t>(kernels::MAX_PART_BITS, std::max<uint32_t>(10, want));
   const uint32_t bits = plan.keyBits > nb ? plan.keyBits - nb : 0;
-  // One rank may split a partition's fragment range over two workgroups of
-  // the fused kernel (21 bits: e.g. 3B dense keys); replicated bitmaps travel
-  // whole, so N > 1 stays at 128 KiB per partition.
-  const uint32_t maxBits = kernels::BITMAP_MAX_BITS + (N == 1 ? kernels::BITMAP_MAX_SPLIT : 0);
+  // A partition's fragment range may be split over two workgroups of the
+  // bitmap kernels (21 bits: e.g. 3B dense keys; the replicated bitmaps
+  // travel whole, 256 KiB per partition).
+  const uint32_t maxBits = kernels::BITMAP_MAX_BITS + kernels::BITMAP_MAX_SPLIT;
   if (bits > maxBits || !kernels::fragWordFits(plan.keyBits, nb)) return;
   const double bitmapBytes = (double)(1ull << nb) * kernels::bitmapWords(bits) * 4;
   plan.replicatedLinkBytes = N > 1 ? 2.0 * (N - 1) / N * bitmapBytes : 0.0;

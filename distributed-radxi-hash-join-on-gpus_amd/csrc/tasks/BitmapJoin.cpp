@@ -26,8 +26,8 @@ BitmapJoin::BitmapJoin(data::Relation *innerRelation, data::Relation *outerRelat
     : inner(innerRelation), outer(outerRelation), ctx(ctx), plan(plan), maxBlocks(maxBlocks),
       sampleStride(std::max<uint32_t>(1, sampleStride)), ev(ev) {
   JOIN_ASSERT(plan.bitmapJoin && !plan.materialize && !plan.wide, "BitmapJoin", "needs a counting bitmap plan");
-  JOIN_ASSERT(plan.bitmapBits <= kernels::BITMAP_MAX_BITS + (ctx->numberOfNodes() == 1 ? kernels::BITMAP_MAX_SPLIT : 0),
-              "BitmapJoin", "%u fragment bits do not fit a bitmap", plan.bitmapBits);
+  JOIN_ASSERT(plan.bitmapBits <= kernels::BITMAP_MAX_BITS + kernels::BITMAP_MAX_SPLIT, "BitmapJoin",
+              "%u fragment bits do not fit a bitmap", plan.bitmapBits);
   JOIN_ASSERT(kernels::fragWordFits(plan.keyBits, plan.networkBits), "BitmapJoin",
               "%u-bit keys do not leave a u32 fragment above %u radix bits", plan.keyBits, plan.networkBits);
 }

@@ -137,6 +137,36 @@ def test_bitmap_split_pieces(C, nb, dup):
         assert j.run()["global_matches"] == exp
 
 
+@pytest.mark.parametrize("dev", devices())
+@pytest.mark.parametrize("n_ranks", [2, 4])
+def test_replicated_bitmap_split_pieces(C, dev, n_ranks):
+    """21 fragment bits on the replicated plan: each partition's bitmap is
+    built and probed as two 128 KiB pieces (adjacent in the all-reduced
+    array), in 1 and 3 all-reduce ranges; exact on every rank."""
+    import os
+    loc = "device" if dev == "cuda" else "host"
+    nb = 2
+    G_R, G_S = 1 << (21 + nb), 3 << (19 + nb)
+    inner = C.GenSpec(seed=41)
+    outer = C.GenSpec(distribution=C.KeyDistribution.UNIFORM, seed=42, domain=G_R)
+    exp = C.Relation.expected_matches(inner, G_R, outer, G_S)
+
+    def cfg(c):
+        force_replicated(c, C)
+        c.network_bits = nb
+    for chunks in ("1", "3"):
+        os.environ["HPCJOIN_REDUCE_CHUNKS"] = chunks
+        try:
+            out = run_ranks(C, n_ranks, loc, generated(C, loc, inner, G_R, n_ranks),
+                            generated(C, loc, outer, G_S, n_ranks), G_R, G_S, cfg)
+        finally:
+            del os.environ["HPCJOIN_REDUCE_CHUNKS"]
+        for res_list, plan in out:
+            assert plan.bitmap_join and plan.bitmap_replicated and plan.bitmap_bits == 21
+            for res in res_list:
+                assert res["bitmap_join"] and res["global_matches"] == exp, (chunks, res["global_matches"], exp)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("n_ranks", [1, 4])
 @pytest.mark.parametrize("G_R,G_S", [(1000, 0), (37, 5000), (3, 3), (100_000, 1)])
