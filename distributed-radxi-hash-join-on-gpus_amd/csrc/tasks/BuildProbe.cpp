@@ -139,8 +139,9 @@ void BuildProbe::execute() {
   if (!plan.materialize) {
     tl.beginSplit("BPKERNEL", "BPBUILD", wb, "BPPROBE", wp, ctx->stream());
     kernels::buildProbe(args, items, nItems, capacity, ctx->stream());
-    tl.end("BPKERNEL", ctx->stream());
-    tl.end("BPTASKTIME", ctx->stream());
+    hipEvent_t done = tl.mark(ctx->stream());  // one event ends both spans
+    tl.endAt("BPKERNEL", done);
+    tl.endAt("BPTASKTIME", done);
     readBackCounters();
     return;
   }
@@ -161,8 +162,9 @@ void BuildProbe::execute() {
   args.itemOffsets = itemOffsets;
   args.result = counters + 3;  // the count pass already counted
   kernels::buildProbe(args, items, nItems, capacity, ctx->stream());
-  tl.end("BPKERNEL", ctx->stream());
-  tl.end("BPTASKTIME", ctx->stream());
+  hipEvent_t done = tl.mark(ctx->stream());
+  tl.endAt("BPKERNEL", done);
+  tl.endAt("BPTASKTIME", done);
   readBackCounters();
 }
 

@@ -130,17 +130,21 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
       HIP_CHECK(hipMemsetAsync(overflowFlag, 0, sizeof(unsigned int), ctx->stream()));
     }
     performance::Measurements::add("LPHISTELEM", (double)(xp.recvTotal / S), "tuples");
-    tl.begin("LPHISTCOMP", ctx->stream());
+    // Back-to-back spans on one stream share their boundary events.
+    hipEvent_t p0 = tl.mark(ctx->stream());
+    tl.beginAt("LPHISTCOMP", p0);
     kernels::localHistogram(w->getData(), wide, dItems, nItems, shift, bits, itemHist, ctx->stream(), S, frag);
-    tl.end("LPHISTCOMP", ctx->stream());
-    tl.begin("LPOFFSET", ctx->stream());
+    hipEvent_t p1 = tl.mark(ctx->stream());
+    tl.endAt("LPHISTCOMP", p1);
+    tl.beginAt("LPOFFSET", p1);
     kernels::localSampledLayout(itemHist, dLb, dItems, owned, bits, S, caps, starts, scanWs, gcur, gend, pbeg, cap,
                                 ctx->stream(), align);
-    tl.end("LPOFFSET", ctx->stream());
-    tl.begin("LPPART", ctx->stream());
+    hipEvent_t p2 = tl.mark(ctx->stream());
+    tl.endAt("LPOFFSET", p2);
+    tl.beginAt("LPPART", p2);
     kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, gcur, false, sout, ctx->stream(), gend,
                           split, plan.localGeometry, frag);
-    tl.end("LPPART", ctx->stream());
+    tl.endAt("LPPART", tl.mark(ctx->stream()));
     kernels::claimOverflow(gcur, gend, P, overflowFlag, ctx->stream());
     // Read back with the join's final synchronisation (the flag accumulates
     // over sides; the last copy enqueued sees them all).
@@ -169,16 +173,19 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
       ctx->copy(partBegin, zero.data(), 8, true, false);
     }
     performance::Measurements::add("LPHISTELEM", (double)xp.recvTotal, "tuples");
-    tl.begin("LPHISTCOMP", ctx->stream());
+    hipEvent_t p0 = tl.mark(ctx->stream());
+    tl.beginAt("LPHISTCOMP", p0);
     kernels::localHistogram(w->getData(), wide, dItems, nItems, shift, bits, itemHist, ctx->stream(), 1, frag);
-    tl.end("LPHISTCOMP", ctx->stream());
-    tl.begin("LPOFFSET", ctx->stream());
+    hipEvent_t p1 = tl.mark(ctx->stream());
+    tl.endAt("LPHISTCOMP", p1);
+    tl.beginAt("LPOFFSET", p1);
     kernels::localCursors(itemHist, dLb, owned, bits, dBase, dItems, gcur, narrow, partBegin, ctx->stream());
-    tl.end("LPOFFSET", ctx->stream());
-    tl.begin("LPPART", ctx->stream());
+    hipEvent_t p2 = tl.mark(ctx->stream());
+    tl.endAt("LPOFFSET", p2);
+    tl.beginAt("LPPART", p2);
     kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, gcur, narrow, out, ctx->stream(), nullptr,
                           split, 0, frag);
-    tl.end("LPPART", ctx->stream());
+    tl.endAt("LPPART", tl.mark(ctx->stream()));
   } else {
     uint64_t *itemCursors = ctx->workspace().getArray<uint64_t>(std::max<uint64_t>(1, (uint64_t)nItems * F));
     if (owned == 0) partBegin[0] = 0;
