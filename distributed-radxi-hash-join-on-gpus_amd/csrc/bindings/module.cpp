@@ -553,6 +553,18 @@ struct PyRelation {
 
 }  // namespace
 
+// Payload columns must hold a row for every rid of this rank's relation
+// slices: the gather kernels index rows by rid - offset on the device.
+static void checkPayloadCover(const operators::HashJoin &j, const at::Tensor &a, uint64_t offA, const at::Tensor &b,
+                              uint64_t offB) {
+  const uint64_t off[2] = {offA, offB}, rows[2] = {(uint64_t)a.size(0), (uint64_t)b.size(0)};
+  for (int r = 0; r < 2; ++r) {
+    const uint64_t lo = j.ridMin(r), hi = j.ridMax(r);
+    TORCH_CHECK(lo > hi || (lo >= off[r] && hi - off[r] < rows[r]), r ? "outer" : "inner", " payload rows [", off[r],
+                ", ", off[r] + rows[r], ") do not cover this rank's rids [", lo, ", ", hi, "]");
+  }
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X-native distributed radix hash join engine (native core)";
   m.attr("ARCH") = "gfx950";
@@ -628,6 +640,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("chunks", &core::JoinConfig::chunks)
       .def_readwrite("checks", &core::JoinConfig::checks)
       .def_readwrite("max_partition_blocks", &core::JoinConfig::maxPartitionBlocks)
+      // KernelVariants, flattened (sweeps / A-B tests; core/Types.h)
+      .def_property("net_ipt", [](const core::JoinConfig &c) { return c.variants.netIpt; },
+                    [](core::JoinConfig &c, uint32_t v) { c.variants.netIpt = v; })
+      .def_property("bm_threads", [](const core::JoinConfig &c) { return c.variants.bmThreads; },
+                    [](core::JoinConfig &c, uint32_t v) { c.variants.bmThreads = v; })
+      .def_property("bm_flat", [](const core::JoinConfig &c) { return c.variants.bmFlat; },
+                    [](core::JoinConfig &c, int32_t v) { c.variants.bmFlat = v; })
+      .def_property("reduce_chunks", [](const core::JoinConfig &c) { return c.variants.reduceChunks; },
+                    [](core::JoinConfig &c, uint32_t v) { c.variants.reduceChunks = v; })
+      .def_property("key_count", [](const core::JoinConfig &c) { return c.variants.keyCount; },
+                    [](core::JoinConfig &c, uint32_t v) { c.variants.keyCount = v; })
+      .def_property("rows_lds", [](const core::JoinConfig &c) { return c.variants.rowsLds; },
+                    [](core::JoinConfig &c, uint32_t v) { c.variants.rowsLds = v; })
+      .def_property("mat_variant", [](const core::JoinConfig &c) { return c.variants.matVariant; },
+                    [](core::JoinConfig &c, uint32_t v) { c.variants.matVariant = v; })
       .def("__repr__", &core::JoinConfig::describe);
 
   py::class_<core::JoinPlan>(m, "JoinPlan")
@@ -880,6 +907,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
             TORCH_CHECK(innerRows.dim() == 2 && innerRows.size(1) == (int64_t)kernels::ROW_WORDS &&
                             outerRows.dim() == 2 && outerRows.size(1) == (int64_t)kernels::ROW_WORDS,
                         "payload rows must be [n, 4] int64 (32 bytes)");
+            checkPayloadCover(j, innerRows, innerOffset, outerRows, outerOffset);
             operators::PayloadColumn a{ptr<uint64_t>(innerRows), (uint64_t)innerRows.size(0), innerOffset, innerGlobal};
             operators::PayloadColumn b{ptr<uint64_t>(outerRows), (uint64_t)outerRows.size(0), outerOffset, outerGlobal};
             const uint64_t n = j.lastResult().outputPairs;
@@ -888,7 +916,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
             if (innerRows.is_cuda()) HIP_CHECK(hipDeviceSynchronize());
             {
               py::gil_scoped_release nogil;
-              operators::LateMaterialization lm(ctx.get(), a, b);
+              operators::LateMaterialization lm(ctx.get(), a, b, j.getConfig().variants.matVariant);
               lm.materialize(j.getOutput(), n, ptr<uint64_t>(out));
             }
             return out;
@@ -909,6 +937,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                             outerRows.dim() == 2 && outerRows.size(1) == (int64_t)kernels::ROW_WORDS,
                         "payload rows must be [n, 4] int64 (32 bytes)");
             TORCH_CHECK(innerRows.is_contiguous() && outerRows.is_contiguous(), "payload rows must be contiguous");
+            checkPayloadCover(j, innerRows, innerOffset, outerRows, outerOffset);
             const auto opts = at::TensorOptions().dtype(at::kLong).device(innerRows.device());
             constexpr int64_t W = operators::LateMaterialization::OUT_WORDS;
             operators::JoinResult r;
@@ -925,8 +954,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                 kernels::RowSink sk;
                 sk.rowsA = ptr<uint64_t>(innerRows);
                 sk.offA = innerOffset;
+                sk.rowsAN = (uint64_t)innerRows.size(0);
                 sk.rowsB = ptr<uint64_t>(outerRows);
                 sk.offB = outerOffset;
+                sk.rowsBN = (uint64_t)outerRows.size(0);
                 sk.out = ptr<uint64_t>(out);
                 sk.capacity = cap;
                 j.setRowSink(sk);
@@ -950,7 +981,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
             at::Tensor out = at::empty({(int64_t)n, W}, opts);
             {
               py::gil_scoped_release nogil;
-              operators::LateMaterialization lm(ctx.get(), a, b);
+              operators::LateMaterialization lm(ctx.get(), a, b, j.getConfig().variants.matVariant);
               lm.materialize(j.getOutput(), n, ptr<uint64_t>(out));
             }
             return py::make_tuple(resultToDict(r), out);

@@ -37,7 +37,7 @@ ExecContext::ExecContext(Location loc, int device, comm::Communicator *comm)
 }
 
 ExecContext::~ExecContext() {
-  for (auto &m : ipcImported_) (void)hipIpcCloseMemHandle(m.second);
+  for (auto &m : ipcImported_) (void)hipIpcCloseMemHandle(m.base);
   for (hipEvent_t e : events_) (void)hipEventDestroy(e);
   timeline_.reset();
   workspace_.reset();
@@ -90,7 +90,7 @@ void ExecContext::resetScratch() {
   eventsUsed_ = 0;
 }
 
-void ExecContext::ipcExport(const void *p, uint64_t handle[8], uint64_t *offset) {
+void ExecContext::ipcExport(const void *p, uint64_t handle[8], uint64_t *offset, uint64_t *generation) {
   static_assert(sizeof(hipIpcMemHandle_t) == 64, "unexpected hipIpcMemHandle_t size");
   JOIN_ASSERT(onDevice(), "ExecContext", "IPC export of host memory");
   void *base = workspace_->allocationOf(p);
@@ -99,17 +99,26 @@ void ExecContext::ipcExport(const void *p, uint64_t handle[8], uint64_t *offset)
   HIP_CHECK(hipIpcGetMemHandle(&h, base));
   std::memcpy(handle, &h, sizeof(h));
   *offset = (uint64_t)(static_cast<const uint8_t *>(p) - static_cast<const uint8_t *>(base));
+  *generation = workspace_->generation();
 }
 
-void *ExecContext::ipcImport(const uint64_t handle[8]) {
+void *ExecContext::ipcImport(uint32_t peer, const uint64_t handle[8], uint64_t generation) {
   std::vector<uint64_t> key(handle, handle + 8);
-  for (auto &m : ipcImported_)
-    if (m.first == key) return m.second;
+  for (size_t i = 0; i < ipcImported_.size();) {
+    IpcMapping &m = ipcImported_[i];
+    if (m.peer == peer && m.generation != generation) {  // stale: the peer's allocations changed
+      HIP_CHECK(hipIpcCloseMemHandle(m.base));
+      ipcImported_.erase(ipcImported_.begin() + i);
+      continue;
+    }
+    if (m.peer == peer && m.handle == key) return m.base;
+    ++i;
+  }
   hipIpcMemHandle_t h;
   std::memcpy(&h, handle, sizeof(h));
   void *ptr = nullptr;
   HIP_CHECK(hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess));
-  ipcImported_.emplace_back(std::move(key), ptr);
+  ipcImported_.push_back(IpcMapping{peer, std::move(key), generation, ptr});
   return ptr;
 }
 

@@ -53,10 +53,15 @@ class ExecContext {
   // creating and destroying several per join.
   hipEvent_t acquireEvent();
   // One-sided exchange (JoinConfig::exchange = OneSided): the IPC handle of
-  // the device allocation holding `p` (8 words) and p's offset in it; and the
-  // mapping of a peer's exported allocation (opened once, cached).
-  void ipcExport(const void *p, uint64_t handle[8], uint64_t *offset);
-  void *ipcImport(const uint64_t handle[8]);
+  // the device allocation holding `p` (8 words), p's offset in it and the
+  // workspace generation (memory::Arena::generation); and the mapping of a
+  // peer's exported allocation, cached per (peer, handle) while the peer's
+  // generation is unchanged.  A peer whose generation moved may have freed
+  // what we mapped (and ROCm may reuse handle bytes): its mappings are closed
+  // and re-opened.
+  void ipcExport(const void *p, uint64_t handle[8], uint64_t *offset, uint64_t *generation);
+  void *ipcImport(uint32_t peer, const uint64_t handle[8], uint64_t generation);
+  size_t ipcMappings() const { return ipcImported_.size(); }
 
  private:
   Location loc_;
@@ -70,7 +75,13 @@ class ExecContext {
   std::unique_ptr<memory::Arena> workspace_;
   std::unique_ptr<memory::Arena> staging_;
   std::unique_ptr<performance::Timeline> timeline_;
-  std::vector<std::pair<std::vector<uint64_t>, void *>> ipcImported_;  // peer handle -> mapped base
+  struct IpcMapping {
+    uint32_t peer;
+    std::vector<uint64_t> handle;
+    uint64_t generation;
+    void *base;
+  };
+  std::vector<IpcMapping> ipcImported_;
 };
 
 }  // namespace core

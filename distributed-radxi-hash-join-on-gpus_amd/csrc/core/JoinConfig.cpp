@@ -38,6 +38,7 @@ JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t global
   p.directCount = cfg.directCount;
   p.localItemTiles = std::max<uint32_t>(1, std::min<uint32_t>(cfg.localItemTiles, 1024));
   p.localGeometry = cfg.localGeometry;
+  p.variants = cfg.variants;
   p.assignment = cfg.assignment;
   p.skewSplit = cfg.skewSplit && cfg.assignment == AssignmentPolicy::LPT && numberOfNodes > 1;
   p.chunks = std::max<uint32_t>(1, cfg.chunks);
@@ -126,10 +127,12 @@ JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t global
                 "key fragment (%u bits) would reach the LDS empty marker 0xFFFFFFFF", keyHighBits);
   }
 
-  if (!p.wide && !p.keyOnly && p.twoLevel) {
+  if (!p.wide && p.twoLevel) {
     const uint32_t passBits = p.networkBits + p.localBits;
     const uint32_t fragBits = p.keyBits > passBits ? p.keyBits - passBits : 0;
-    p.splitLocal = cfg.splitLocal && ridBits <= 32 && fragBits <= 16;
+    // Compressed: u32 rid + u16 fragment.  Key-only: the fragment above both
+    // digits as u32 + u16 (<= 48 bits: 63-bit keys leave 44 after 10 + 9).
+    p.splitLocal = cfg.splitLocal && (p.keyOnly ? fragBits <= 48 : ridBits <= 32 && fragBits <= 16);
   }
 
   // LDS budget: a 32 KiB table (counting, 4-byte fragments) lets 5 workgroups

@@ -108,6 +108,7 @@ struct JoinConfig {
   ExchangeMode exchange = ExchangeMode::Rccl;
   uint32_t localItemTiles = 64; // local pass work item: up to this many 4096-tuple tiles of one segment
   uint32_t localGeometry = 0;   // local scatter workgroup geometry (0 = 1024 x 8; 1-4: sweep alternatives)
+  KernelVariants variants;      // kernel-shape variants (sweeps; core/Types.h)
 
   std::string describe() const;
 };
@@ -160,6 +161,7 @@ struct JoinPlan {
   bool directCount = true;    // build/probe may use direct-addressed count tables
   uint32_t localItemTiles = 64;
   uint32_t localGeometry = 0;
+  KernelVariants variants;
   uint32_t wireBits[2] = {0, 0};
   uint32_t wireRidBits[2] = {0, 0};
   std::vector<uint64_t> ridBase[2];

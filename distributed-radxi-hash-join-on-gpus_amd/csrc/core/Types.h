@@ -36,4 +36,19 @@ HJ_HD uint32_t ceilLog2(uint64_t x) {
 
 HJ_HD uint64_t ceilDiv(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
+// Kernel-shape variants kept for sweeps and A/B tests (defaults = the
+// measured best).  They live in the JoinConfig, are copied into the JoinPlan
+// once, and reach the launchers through their argument structs: no kernel
+// launcher reads the environment (Python: HPCJOIN_<FIELD> is resolved once by
+// utils.config.config_from_dict).
+struct KernelVariants {
+  uint32_t netIpt = 0;        // claim-scatter tile: 0 = auto (16 x 1024 for u32 words, 8 x 1024 else), 15 = 15K tiles at 2048-way
+  uint32_t bmThreads = 0;     // bitmap kernels' workgroup size: 0 = auto (256 for <= 32 KiB bitmaps, else 1024)
+  int32_t bmFlat = -1;        // bitmap slice walk: -1 = auto, 0 = per claim slice, 1 = one flat walk per partition
+  uint32_t reduceChunks = 0;  // replicated bitmap plan: all-reduce ranges (0 = auto: one per 32 MiB, <= 4)
+  uint32_t keyCount = 6;      // key-only count kernel: 6 = span work queue (bpKeySpanKernel), 0-5 = item kernel variants
+  uint32_t rowsLds = 1;       // fused row output with the inner rows cached in LDS (0 = staged kernel)
+  uint32_t matVariant = 1;    // late-materialization store/load flavour (materialize.hip)
+};
+
 }  // namespace hpcjoin

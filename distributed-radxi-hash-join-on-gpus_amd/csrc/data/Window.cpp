@@ -162,25 +162,42 @@ void Window::enableOneSided() {
   JOIN_ASSERT(N > 1 && codec.w == 0, "Window", "one-sided windows: N > 1, raw tuples (no wire codec)");
   const bool shared = ctx->comm()->sharesAddressSpace();
   JOIN_ASSERT(shared || ctx->onDevice(), "Window", "one-sided host windows need in-process ranks");
-  // Per rank: {pid, raw pointer, IPC handle (8 words), offset, recvDispls[C][N]}.
-  const size_t R = 11 + (size_t)C * N;
+  // Per rank: {pid, raw pointer, IPC handle (8 words), offset, workspace
+  // generation, device, recvDispls[C][N]}.
+  const size_t H = 13, R = H + (size_t)C * N;
   std::vector<uint64_t> mine(R, 0), all(R * N);
   mine[0] = (uint64_t)getpid();
   mine[1] = (uint64_t)(uintptr_t)data;
-  if (!shared) ctx->ipcExport(data, &mine[2], &mine[10]);
-  for (size_t i = 0; i < (size_t)C * N; ++i) mine[11 + i] = plan.recvDispls[i];
+  if (!shared) ctx->ipcExport(data, &mine[2], &mine[10], &mine[11]);
+  mine[12] = ctx->onDevice() ? (uint64_t)ctx->device() : ~0ull;
+  for (size_t i = 0; i < (size_t)C * N; ++i) mine[H + i] = plan.recvDispls[i];
   ctx->comm()->allGatherHost(mine.data(), all.data(), R);
   peerBase.assign(N, nullptr);
   peerOffset.assign((size_t)N * C, 0);
   for (uint32_t p = 0; p < N; ++p) {
     const uint64_t *r = &all[R * p];
-    if (p == me)
+    if (p == me) {
       peerBase[p] = static_cast<uint8_t *>(data);
-    else if (shared)
+    } else if (shared) {
+      // In-process ranks pass raw pointers: the scatter kernel and the peer
+      // copies dereference them from this rank's device, which needs peer
+      // access when the ranks sit on different GPUs.
+      if (ctx->onDevice() && r[12] != mine[12]) {
+        int can = 0;
+        HIP_CHECK(hipDeviceCanAccessPeer(&can, ctx->device(), (int)r[12]));
+        JOIN_ASSERT(can, "Window", "one-sided window: device %d cannot access peer device %d", ctx->device(),
+                    (int)r[12]);
+        const hipError_t e = hipDeviceEnablePeerAccess((int)r[12], 0);
+        if (e == hipErrorPeerAccessAlreadyEnabled)
+          (void)hipGetLastError();
+        else
+          HIP_CHECK(e);
+      }
       peerBase[p] = reinterpret_cast<uint8_t *>((uintptr_t)r[1]);
-    else
-      peerBase[p] = static_cast<uint8_t *>(ctx->ipcImport(&r[2])) + r[10];
-    for (uint32_t c = 0; c < C; ++c) peerOffset[(size_t)p * C + c] = r[11 + (size_t)c * N + me];
+    } else {
+      peerBase[p] = static_cast<uint8_t *>(ctx->ipcImport(p, &r[2], r[11])) + r[10];
+    }
+    for (uint32_t c = 0; c < C; ++c) peerOffset[(size_t)p * C + c] = r[H + (size_t)c * N + me];
   }
   oneSided = true;
   oneSidedComplete = false;

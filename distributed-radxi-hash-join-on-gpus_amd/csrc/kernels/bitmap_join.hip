@@ -394,22 +394,17 @@ static void checkBits(uint32_t bits, uint32_t keyShift, uint32_t elemBytes, uint
 // holds the LDS; 16 waves keep the loads in flight), 256 when the bitmap is
 // at most 32 KiB (bits <= 18: several workgroups per CU, so short partitions
 // -- one rank's share at N = 8 -- overlap each other's latencies).
-// HPCJOIN_BM_NTH=256|1024 forces one (sweeps).
-static int bmThreads(uint32_t bits) {
-  const char *e = std::getenv("HPCJOIN_BM_NTH");  // read per launch: tests switch it
-  const int v = e ? std::atoi(e) : 0;
-  const int forced = v == 256 || v == 1024 ? v : 0;
-  return forced ? forced : bits <= 18 ? 256 : 1024;
+// BitmapSlices::threads = 256|1024 forces one (KernelVariants::bmThreads).
+static int bmThreads(uint32_t bits, uint32_t forced) {
+  return forced == 256 || forced == 1024 ? (int)forced : bits <= 18 ? 256 : 1024;
 }
 
 // Flat walk over a partition's claim slices when the average partition is
-// short (< 2^18 elements; HPCJOIN_BM_FLAT=0|1 forces it).  Measured 1024-
+// short (< 2^18 elements; BitmapSlices::flat = 0|1 forces it).  Measured 1024-
 // thread join kernel: 1B (977K per partition) per-slice 1.40 ms vs flat 1.49;
 // 125M (122K per partition) per-slice 0.358 ms vs flat 0.33.
 static uint32_t bmFlat(const BitmapSlices &a, const BitmapSlices *b, uint32_t partitions) {
-  const char *e = std::getenv("HPCJOIN_BM_FLAT");  // read per launch: tests switch it
-  const int forced = e ? (std::atoi(e) ? 1 : 0) : -1;
-  if (forced >= 0) return (uint32_t)forced;
+  if (a.flat >= 0) return a.flat ? 1u : 0u;
   const uint64_t n = std::max<uint64_t>(a.count, b ? b->count : 0);
   return n > 0 && n / std::max<uint32_t>(partitions, 1) < (1ull << 18) ? 1u : 0u;
 }
@@ -429,7 +424,7 @@ static uint32_t bmFlat(const BitmapSlices &a, const BitmapSlices *b, uint32_t pa
 
 #define HJ_BM_DISPATCH(...)                                                                                      \
   do {                                                                                                           \
-    const int nth = bmThreads(bits);                                                                             \
+    const int nth = bmThreads(bits, src.threads);                                                                             \
     if (elemBytes == 4) {                                                                                        \
       HJ_CHECK(src.kind == BitmapSlices::Claim, "bitmap join: u32 fragments need claim slices");                \
       using E = uint32_t;                                                                                        \

@@ -1157,7 +1157,7 @@ __global__ __launch_bounds__(T, MINW) void bpKeyCountKernel(BPArgs a, const BPIt
   if (t == 0 && total) atomicAdd(a.result, total);
 }
 
-// Key-count variant (HPCJOIN_KCOUNT, A/B switch).  Measured on MI355X, 1B x
+// Key-count variant (BPArgs::keyCount = KernelVariants::keyCount, A/B switch).  Measured on MI355X, 1B x
 // 1B sparse 63-bit keys, build/probe ms: 0 = 256 x 8 (90 VGPRs, 16 waves per
 // CU) 6.07; 1 = 512 x 4, 2 buckets in flight (48 VGPRs, 32 waves per CU)
 // 4.99 -- the default; 2 = 1 + folded hash 4.88 (dropped as default: keys
@@ -1167,11 +1167,6 @@ __global__ __launch_bounds__(T, MINW) void bpKeyCountKernel(BPArgs a, const BPIt
 // packed 16-bit fill counters (one 16-byte LDS read per probe instead of two,
 // against 3.0 bank-conflict cycles per LDS instruction in the PMC of variant
 // 1): 5.43-5.53 ms vs 4.93-4.95 (profiles/r2v).
-static int keyCountVariant() {
-  const char *e = std::getenv("HPCJOIN_KCOUNT");  // read per launch: tests switch it
-  return e ? std::atoi(e) : 1;
-}
-
 template <int T, int K, int H, bool FOLD, bool CLEAR, int MINW>
 static void launchKeyCount(const BPArgs &a, const BPItem *items, const uint32_t *nItems, uint32_t capacity,
                            hipStream_t s) {
@@ -1181,6 +1176,252 @@ static void launchKeyCount(const BPArgs &a, const BPItem *items, const uint32_t 
   const uint32_t perCuK = (uint32_t)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / ldsK));
   hipLaunchKernelGGL((bpKeyCountKernel<T, K, H, FOLD, CLEAR, MINW>), dim3(std::min<uint32_t>(capacity, 256 * perCuK)),
                      dim3(T), ldsK, s, a, items, nItems, capacity);
+  HIP_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------- key-only spans (v2)
+// The key-only count as a work queue of resolved spans.  Measured on the
+// item kernel above (1B x 1B sparse keys, 4.93 ms, 3.3 TB/s, 63 % wait):
+// every item started with a chain of dependent scalar loads (item -> four
+// partition bounds) and only then issued its data loads, so each workgroup
+// paid ~3 memory latencies per ~30 KB item.  Here
+//  * spans carry their resolved bounds (bpEmitSpans), 32 B each;
+//  * a workgroup grabs KS_CHUNK consecutive spans from a device counter
+//    (dynamic: hot partitions' spans spread over workgroups), stages their
+//    descriptors in LDS with one load, and walks them in order;
+//  * the next span's inner and outer words are loaded into registers while
+//    the current span probes, so its latency hides behind the LDS work;
+//  * loads are unpredicated (indices clamped into the span) and the bucket
+//    hash is one 32-bit multiply of the folded word (the 64-bit product of
+//    hash64 is three quarter-rate multiplies).
+// Table: the same 4-slot buckets + fill counters as bpKeyCountKernel.
+constexpr uint32_t KS_CHUNK = 32;
+
+__global__ __launch_bounds__(BPT) void bpEmitSpansKernel(const uint64_t *__restrict__ partR,
+                                                         const uint64_t *__restrict__ partREnd,
+                                                         const uint64_t *__restrict__ partS,
+                                                         const uint64_t *__restrict__ partSEnd, uint32_t P,
+                                                         uint32_t rc, uint32_t sc, const uint32_t *__restrict__ counts,
+                                                         const uint32_t *__restrict__ offsets, BPSpan *spans,
+                                                         uint32_t capacity) {
+  const uint32_t p = blockIdx.x * BPT + threadIdx.x;
+  if (p >= P) return;
+  const uint32_t c = counts[p];
+  if (c == 0) return;
+  const uint64_t r0 = partR[p], r1 = partREnd[p], s0 = partS[p], s1 = partSEnd[p];
+  const uint32_t nsChunks = (uint32_t)ceilDiv(s1 - s0, sc);
+  const uint32_t o = offsets[p];
+  for (uint32_t i = 0; i < c && o + i < capacity; ++i) {
+    const uint64_t rb = r0 + (uint64_t)(i / nsChunks) * rc, sb = s0 + (uint64_t)(i % nsChunks) * sc;
+    BPSpan sp;
+    sp.rb = rb;
+    sp.sb = sb;
+    sp.nr = (uint32_t)(min(r1, rb + rc) - rb);
+    sp.ns = (uint32_t)(min(s1, sb + sc) - sb);
+    sp.pad0 = sp.pad1 = 0;
+    spans[o + i] = sp;
+  }
+}
+
+void bpEmitSpans(const BPArgs &a, const uint32_t *counts, const uint32_t *offsets, BPSpan *spans, uint32_t capacity,
+                 hipStream_t s) {
+  if (a.P == 0) return;
+  hipLaunchKernelGGL(bpEmitSpansKernel, dim3(ceilDiv(a.P, BPT)), dim3(BPT), 0, s, a.partR,
+                     a.partREnd ? a.partREnd : a.partR + 1, a.partS, a.partSEnd ? a.partSEnd : a.partS + 1, a.P,
+                     a.rChunk, a.sChunk, counts, offsets, spans, capacity);
+  HIP_CHECK_LAUNCH();
+}
+
+// Bucket of a key-only word: fold the high half in with a 24-bit multiply
+// (full rate), one 32-bit multiplicative hash of the result.  Within a final
+// partition the word's low localBits bits are equal: they only offset the
+// product, whose top bits still come from the varying bits above them.
+__device__ __forceinline__ uint32_t ksBucket(uint64_t w, uint32_t bbits) {
+  const uint32_t x = (uint32_t)w ^ __umul24((uint32_t)(w >> 32), 0x2C1B3Cu);
+  return (x * 0x9E3779B1u) >> (32 - bbits);
+}
+
+// K words of a span per lane (indices clamped into the span: no predication).
+// Split layout (SplitLayout::loShift = localBits): the u32 low column and the
+// u16 high column compose the key fragment lo | hi << 32.
+template <int T, int K, bool SPLIT>
+struct KsSrc {
+  const void *lo;
+  const uint16_t *hi;
+  __device__ __forceinline__ void load(uint64_t base, uint32_t n, uint64_t (&v)[K]) const {
+    const uint32_t last = n ? n - 1 : 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint64_t i = base + min((uint32_t)(k * T) + threadIdx.x, last);
+      if constexpr (SPLIT)
+        v[k] = (uint64_t)__builtin_nontemporal_load(static_cast<const uint32_t *>(lo) + i) |
+               ((uint64_t)__builtin_nontemporal_load(hi + i) << 32);
+      else
+        v[k] = __builtin_nontemporal_load(static_cast<const uint64_t *>(lo) + i);
+    }
+  }
+};
+
+// One batch of T x K outer words (the first `valid` of them counted) against
+// the bucketized table; returns this lane's matches.
+template <int T, int K, int H>
+__device__ __forceinline__ uint32_t ksProbeBatch(const uint64_t (&sv)[K], uint32_t valid,
+                                                 const unsigned long long *table, const uint32_t *fill, uint32_t bbits,
+                                                 uint32_t bmask) {
+  uint32_t matches = 0;
+#pragma unroll
+  for (int h = 0; h < K / H; ++h) {
+    uint32_t bk[H], f[H];
+    ulonglong2 e0[H], e1[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      bk[j] = ksBucket(sv[h * H + j], bbits);
+      f[j] = fill[bk[j]];
+      const ulonglong2 *q = reinterpret_cast<const ulonglong2 *>(table + bk[j] * BPK_SLOTS);
+      e0[j] = q[0];
+      e1[j] = q[1];
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      const int k = h * H + j;
+      const uint64_t v = sv[k];
+      const uint32_t m = f[j];  // slots in use (> 4: passed through)
+      // Non-short-circuit tests: the whole 32-byte bucket is read up front.
+      uint32_t c = (uint32_t)((m > 0) & (e0[j].x == v)) + (uint32_t)((m > 1) & (e0[j].y == v)) +
+                   (uint32_t)((m > 2) & (e1[j].x == v)) + (uint32_t)((m > 3) & (e1[j].y == v));
+      // Elements passed through (~4 % of buckets at load 1/2, so most waves
+      // have a lane here): continue bucket by bucket, each step one round
+      // trip (counter and both halves of the bucket read together).
+      uint32_t b = bk[j], fb = m;
+      while (fb > BPK_SLOTS) {
+        b = (b + 1) & bmask;
+        fb = fill[b];
+        const ulonglong2 *q = reinterpret_cast<const ulonglong2 *>(table + b * BPK_SLOTS);
+        const ulonglong2 x0 = q[0], x1 = q[1];
+        c += (uint32_t)((fb > 0) & (x0.x == v)) + (uint32_t)((fb > 1) & (x0.y == v)) +
+             (uint32_t)((fb > 2) & (x1.x == v)) + (uint32_t)((fb > 3) & (x1.y == v));
+      }
+      matches += (uint32_t)(k * T) + threadIdx.x < valid ? c : 0u;
+    }
+  }
+  return matches;
+}
+
+template <int T, int K, int H, int MINW, bool SPLIT>
+__global__ __launch_bounds__(T, MINW) void bpKeySpanKernel(KsSrc<T, K, SPLIT> R, KsSrc<T, K, SPLIT> S,
+                                                           const BPSpan *__restrict__ spans,
+                                                           const uint32_t *__restrict__ nSpansPtr, uint32_t capacity,
+                                                           uint32_t *__restrict__ queue, uint32_t maxR,
+                                                           unsigned long long *__restrict__ result) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t maxSlots = 1u << ceilLog2(2ull * maxR);
+  unsigned long long *table = reinterpret_cast<unsigned long long *>(smem);
+  uint32_t *fill = reinterpret_cast<uint32_t *>(table + maxSlots);
+  BPSpan *desc = reinterpret_cast<BPSpan *>(fill + maxSlots / BPK_SLOTS);
+  unsigned long long *wsum = reinterpret_cast<unsigned long long *>(desc + KS_CHUNK);
+  uint32_t *qbase = reinterpret_cast<uint32_t *>(wsum + T / WAVE);
+  constexpr uint32_t BATCH = T * K;
+  const uint32_t t = threadIdx.x;
+  const uint32_t n = min(*nSpansPtr, capacity);
+  uint64_t matches = 0;
+  uint64_t rv[K], sv[K], nrv[K], nsv[K];
+  for (;;) {
+    if (t == 0) *qbase = atomicAdd(queue, KS_CHUNK);
+    __syncthreads();
+    const uint32_t base = __builtin_amdgcn_readfirstlane(*qbase);
+    if (base >= n) break;
+    const uint32_t cnt = min(KS_CHUNK, n - base);
+    if (t < cnt) desc[t] = spans[base + t];
+    __syncthreads();
+    {
+      const BPSpan d = desc[0];
+      R.load(d.rb, d.nr, rv);
+      S.load(d.sb, d.ns, sv);
+    }
+    for (uint32_t i = 0; i < cnt; ++i) {
+      const uint64_t rb = __builtin_amdgcn_readfirstlane((uint32_t)desc[i].rb) |
+                          ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(desc[i].rb >> 32)) << 32);
+      const uint64_t sb = __builtin_amdgcn_readfirstlane((uint32_t)desc[i].sb) |
+                          ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(desc[i].sb >> 32)) << 32);
+      const uint32_t nr = __builtin_amdgcn_readfirstlane(desc[i].nr);
+      const uint32_t ns = __builtin_amdgcn_readfirstlane(desc[i].ns);
+      uint32_t tbits = nr > 1 ? 32 - __clz(2 * nr - 1) : 1;
+      if (tbits < 6) tbits = 6;
+      const uint32_t bbits = tbits - 2, bmask = (1u << bbits) - 1;
+      for (uint32_t j = t; j <= bmask; j += T) fill[j] = 0;
+      __syncthreads();
+      // ---- build (nr <= maxR <= BATCH: one batch, from registers)
+      {
+        uint32_t bk[K], pos[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const bool valid = (uint32_t)(k * T) + t < nr;
+          bk[k] = ksBucket(rv[k], bbits);
+          pos[k] = atomicAdd(&fill[bk[k]], valid ? 1u : 0u);
+          pos[k] = valid ? pos[k] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          if (pos[k] == 0xFFFFFFFFu) continue;
+          uint32_t b = bk[k], p = pos[k];
+          while (p >= BPK_SLOTS) {  // home bucket full: the next one (its counter marks the pass)
+            b = (b + 1) & bmask;
+            p = atomicAdd(&fill[b], 1u);
+          }
+          table[b * BPK_SLOTS + p] = rv[k];
+        }
+      }
+      __syncthreads();
+      // ---- the next span's words stream in while this one probes
+      if (i + 1 < cnt) {
+        const BPSpan d = desc[i + 1];
+        R.load(d.rb, d.nr, nrv);
+        S.load(d.sb, d.ns, nsv);
+      }
+      // ---- probe: the first batch from registers (no wait on the prefetch
+      // above: vmcnt is in order, so a load issued here would make the first
+      // use wait for the next span's words too), later batches loaded inline.
+      matches += ksProbeBatch<T, K, H>(sv, ns, table, fill, bbits, bmask);
+      for (uint32_t b0 = BATCH; b0 < ns; b0 += BATCH) {
+        uint64_t xv[K];
+        S.load(sb + b0, ns - b0, xv);
+        matches += ksProbeBatch<T, K, H>(xv, ns - b0, table, fill, bbits, bmask);
+      }
+      __syncthreads();  // the next span clears the counters
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        rv[k] = nrv[k];
+        sv[k] = nsv[k];
+      }
+    }
+  }
+  const unsigned long long total = blockReduceSum<T, unsigned long long>((unsigned long long)matches, wsum);
+  if (t == 0 && total) atomicAdd(result, total);
+}
+
+size_t bpKeySpanLdsBytes(uint32_t maxR) {
+  const uint64_t slots = uint64_t(1) << ceilLog2(2ull * maxR);
+  return slots * 8 + (slots / BPK_SLOTS) * 4 + KS_CHUNK * sizeof(BPSpan) + 16 * 8 + 16;
+}
+
+void buildProbeKeySpans(const BPArgs &a, const BPSpan *spans, const uint32_t *nSpans, uint32_t capacity,
+                        uint32_t *queue, hipStream_t s) {
+  if (capacity == 0) return;
+  constexpr int T = 512, K = 4, H = 2;
+  HJ_CHECK(a.keyOnly && !a.materialize && !a.wide, "buildProbeKeySpans: key-only counting joins only");
+  HJ_CHECK(!a.split || (a.Rhi && a.Shi), "buildProbeKeySpans: split layout without high columns");
+  HJ_CHECK(a.rChunk <= (uint32_t)(T * K), "buildProbeKeySpans: rChunk %u above one %d-word batch", a.rChunk, T * K);
+  const size_t lds = bpKeySpanLdsBytes(a.rChunk);
+  HJ_CHECK(lds <= 160 * 1024, "buildProbeKeySpans: LDS %zu B exceeds 160 KiB (rChunk=%u)", lds, a.rChunk);
+  const uint32_t perCu = (uint32_t)std::max<size_t>(1, std::min<size_t>(4, (160 * 1024) / lds));
+  const dim3 grid(std::min<uint32_t>(ceilDiv(capacity, KS_CHUNK), 256 * perCu));
+  HIP_CHECK(hipMemsetAsync(queue, 0, sizeof(uint32_t), s));
+  if (a.split)
+    hipLaunchKernelGGL((bpKeySpanKernel<T, K, H, 8, true>), grid, dim3(T), lds, s, KsSrc<T, K, true>{a.R, a.Rhi},
+                       KsSrc<T, K, true>{a.S, a.Shi}, spans, nSpans, capacity, queue, a.rChunk, a.result);
+  else
+    hipLaunchKernelGGL((bpKeySpanKernel<T, K, H, 8, false>), grid, dim3(T), lds, s, KsSrc<T, K, false>{a.R, nullptr},
+                       KsSrc<T, K, false>{a.S, nullptr}, spans, nSpans, capacity, queue, a.rChunk, a.result);
   HIP_CHECK_LAUNCH();
 }
 
@@ -1200,7 +1441,7 @@ void buildProbe(const BPArgs &args, const BPItem *items, const uint32_t *nItems,
            "buildProbe: fragShift=%u < 32 (the rid field of a CompressedTuple is >= 32 bits)", a.fragShift);
   HJ_CHECK(!(a.keyOnly && (a.materialize || a.wide || a.split)), "buildProbe: key-only words count only, unsplit");
   if (bpMode(a) == BP_KCOUNT) {
-    switch (keyCountVariant()) {
+    switch (a.keyCount) {
       case 2: launchKeyCount<512, 4, 2, true, false, 8>(a, items, nItems, capacity, s); break;
       case 3: launchKeyCount<512, 4, 2, true, true, 8>(a, items, nItems, capacity, s); break;
       case 4: launchKeyCount<256, 8, 4, true, true, 4>(a, items, nItems, capacity, s); break;
@@ -1246,11 +1487,7 @@ void buildProbe(const BPArgs &args, const BPItem *items, const uint32_t *nItems,
     const uint32_t perCuM = (uint32_t)std::min<size_t>(4, (160 * 1024) / (ldsM + stageBytes + 64));
     const uint32_t blocksM = std::min<uint32_t>(capacity, 256 * std::max<uint32_t>(perCuM, 1));
     if (rows) HJ_CHECK(a.rowsA && a.rowsB && a.itemOffsets, "buildProbe: row output needs payload columns and item offsets");
-    static const bool rowsLds = [] {
-      const char *e = std::getenv("HPCJOIN_ROWS_LDS");
-      return !e || std::atoi(e) != 0;
-    }();
-    if (rows && rowsLds && a.rChunk <= BPR_MAX_R) {
+    if (rows && a.rowsLds && a.rChunk <= BPR_MAX_R) {
       const size_t ldsR = bpMatRowsLds(a.rChunk);
       const uint32_t perCuR = (uint32_t)std::max<size_t>(1, std::min<size_t>(3, (160 * 1024) / (ldsR + 16)));
       const uint32_t blocksR = std::min<uint32_t>(capacity, 256 * perCuR);

@@ -33,6 +33,7 @@ constexpr uint32_t MAX_PART_BITS = 11;   // LDS cursor/count arrays sized for 20
 struct PartitionGeometry {
   uint32_t blocks = 0;         // workgroups of the pass (each owns a contiguous tile range)
   uint32_t tilesPerBlock = 0;  // tiles per workgroup
+  uint32_t ipt = 0;            // claim-scatter tile variant (KernelVariants::netIpt; 0 = auto)
   uint64_t tuplesPerBlock() const { return uint64_t(tilesPerBlock) * PART_TILE; }
 };
 // Cap the grid at ~8 workgroups per CU (2048) and give each workgroup a
@@ -232,6 +233,12 @@ void localCursors(const uint32_t *itemHist, const uint32_t *lpItemBegin, uint32_
 struct SplitLayout {
   uint32_t on = 0;
   uint32_t fragShift = 32;   // CompressedTuple fragment position (value >> fragShift)
+  // Low column = (u32)(value >> loShift): 0 for CompressedTuples (the rid);
+  // localBits for key-only words (JoinPlan::keyOnly), whose 6-byte split is
+  // the key fragment above both radix digits (lo = its low 32 bits, hi = the
+  // next 16: fragShift = localBits + 32), 2 bytes less per tuple than the
+  // 8-byte word in the local pass output and the count kernel's reads.
+  uint32_t loShift = 0;
   uint16_t *hi = nullptr;    // fragment column (element i <-> lo[i])
   HJ_HD uint64_t value(uint32_t rid, uint16_t frag) const { return (uint64_t)rid | ((uint64_t)frag << fragShift); }
 };
@@ -315,13 +322,18 @@ struct BPArgs {
   const ulonglong2 *rowsB = nullptr;  // outer payload rows
   uint64_t offA = 0, offB = 0;        // rid of row 0 of each column
   ulonglong2 *outRows = nullptr;
+  // Kernel variants (KernelVariants::keyCount / rowsLds).
+  uint32_t keyCount = 6;
+  uint32_t rowsLds = 1;
 };
 // Payload columns + output of a fused materializing join (HashJoin::setRowSink).
 struct RowSink {
   const uint64_t *rowsA = nullptr;
   uint64_t offA = 0;
+  uint64_t rowsAN = 0;      // rows in rowsA: rids [offA, offA + rowsAN)
   const uint64_t *rowsB = nullptr;
   uint64_t offB = 0;
+  uint64_t rowsBN = 0;
   uint64_t *out = nullptr;  // [capacity][10] u64
   uint64_t capacity = 0;
 };
@@ -332,6 +344,19 @@ void bpEmit(const BPArgs &a, const uint32_t *counts, const uint32_t *offsets, BP
 // Grid-strides over min(*nItems, capacity) items; nItems is a device word
 // written by the scan, so no host round trip sits between plan and probe.
 void buildProbe(const BPArgs &a, const BPItem *items, const uint32_t *nItems, uint32_t capacity, hipStream_t s);
+// Key-only counting (BPArgs::keyOnly) over resolved spans: the item list with
+// every item's bounds looked up once (bpEmitSpans), consumed through a device
+// work queue (queue: one u32, cleared by the launcher) with the next span's
+// words prefetched during the current probe.
+struct BPSpan {
+  unsigned long long rb, sb;  // first inner / outer word of the span
+  uint32_t nr, ns;            // inner (<= rChunk) / outer (<= sChunk) words
+  uint32_t pad0, pad1;
+};
+void bpEmitSpans(const BPArgs &a, const uint32_t *counts, const uint32_t *offsets, BPSpan *spans, uint32_t capacity,
+                 hipStream_t s);
+void buildProbeKeySpans(const BPArgs &a, const BPSpan *spans, const uint32_t *nSpans, uint32_t capacity,
+                        uint32_t *queue, hipStream_t s);
 
 // Single-level counting join of unique inner keys (bitmap_join.hip): one
 // workgroup per network partition sets a 2^bits LDS bitmap from the inner
@@ -367,6 +392,10 @@ struct BitmapSlices {
   // Elements over all partitions (0 = unknown): picks the slice walk of the
   // u32 kernels (one flat walk per partition when partitions are short).
   uint64_t count = 0;
+  // Forced kernel shape (KernelVariants::bmThreads / bmFlat; read from the
+  // inner side's slices): 0 / -1 = auto.
+  uint32_t threads = 0;
+  int32_t flat = -1;
 };
 // u32 words of one partition's bitmap (a power of two >= 4).
 uint32_t bitmapWords(uint32_t bits);
@@ -485,7 +514,7 @@ void gatherRows(const uint64_t *rids, uint64_t n, uint64_t ridOffset, const uint
 // out[idx[j] * stride + col .. + ROW_WORDS) = rows[j]
 // Single rank: out[i] = {pair, rowsA[pair.x - offA], rowsB[pair.y - offB]} (10 words).
 void materializeLocal(const ulonglong2 *pairs, uint64_t n, const uint64_t *rowsA, uint64_t offA,
-                      const uint64_t *rowsB, uint64_t offB, uint64_t *out, hipStream_t s);
+                      const uint64_t *rowsB, uint64_t offB, uint64_t *out, hipStream_t s, uint32_t variant = 1);
 void placeRows(const uint64_t *rows, const uint64_t *idx, uint64_t n, uint64_t *out, uint32_t strideWords,
                uint32_t colWord, hipStream_t s);
 }  // namespace kernels

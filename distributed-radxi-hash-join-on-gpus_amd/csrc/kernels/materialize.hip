@@ -214,14 +214,10 @@ __global__ __launch_bounds__(MT) void materializeLocalKernel(const ulonglong2 *_
 }
 
 void materializeLocal(const ulonglong2 *pairs, uint64_t n, const uint64_t *rowsA, uint64_t offA,
-                      const uint64_t *rowsB, uint64_t offB, uint64_t *out, hipStream_t s) {
+                      const uint64_t *rowsB, uint64_t offB, uint64_t *out, hipStream_t s, uint32_t variant) {
   if (!n) return;
   const uint64_t blocks = ceilDiv(ceilDiv(n, 64), MAT_WAVES);
   const uint32_t grid = (uint32_t)(blocks < 8192 ? (blocks + 7) / 8 * 8 : 8192);
-  static const int variant = [] {
-    const char *e = std::getenv("HPCJOIN_MAT_VARIANT");
-    return e ? std::atoi(e) : 1;
-  }();
   const auto *ra = reinterpret_cast<const ulonglong2 *>(rowsA);
   const auto *rb = reinterpret_cast<const ulonglong2 *>(rowsB);
   auto *o = reinterpret_cast<ulonglong2 *>(out);

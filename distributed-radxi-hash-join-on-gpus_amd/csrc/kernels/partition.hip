@@ -467,12 +467,13 @@ struct LocalFragPol {
   __device__ __forceinline__ OutT out(const StageT &v) const { return (uint16_t)(v >> fragShift); }
   __device__ __forceinline__ void store(OutT *o, uint64_t pos, const StageT &v) const { o[pos] = out(v); }
 };
-struct LocalSplitPol : LocalCompressedPol {  // 8 B -> u32 rid + u16 fragment (kernels.h, SplitLayout)
+struct LocalSplitPol : LocalCompressedPol {  // 8 B -> u32 rid / key low word + u16 fragment (kernels.h, SplitLayout)
   using OutT = uint32_t;
   uint16_t *hi;
   uint32_t fragShift;
+  uint32_t loShift = 0;
   __device__ __forceinline__ void store(OutT *o, uint64_t pos, const StageT &v) const {
-    o[pos] = (uint32_t)v;
+    o[pos] = (uint32_t)(v >> loShift);
     hi[pos] = (uint16_t)(v >> fragShift);
   }
 };
@@ -753,30 +754,22 @@ static void launchNetClaimIpt(const Pol &pol, const data::Tuple *in, uint64_t n,
   HIP_CHECK_LAUNCH();
 }
 
-// Tile of the claim scatter: 8192 tuples, or 15360 when the fan-out is 2048
-// (HPCJOIN_NET_IPT=15): longer runs per partition and tile, one workgroup per CU.
-static int netIpt() {
-  static const int v = [] {
-    const char *e = std::getenv("HPCJOIN_NET_IPT");
-    return e ? std::atoi(e) : CL_IPT_DEFAULT;
-  }();
-  return v;
-}
-
+// Tile of the claim scatter (PartitionGeometry::ipt = KernelVariants::netIpt):
+// 8192 tuples by default; 16384 for 4-byte staged words (count-only
+// fragments leave LDS room for twice the run length per partition and tile;
+// measured on MI355X, 1B x 1B: 10.58 vs 10.78 ms per join); 15360 at 2048-way
+// (ipt 15): longer runs per partition and tile, one workgroup per CU.
 template <class Pol>
 static void launchNetClaim(const Pol &pol, const data::Tuple *in, uint64_t n, uint32_t bits,
                            const PartitionGeometry &g, uint32_t blockBegin, uint32_t blockEnd, void *gcur,
                            void *out, hipStream_t s, const void *gend, bool narrow) {
-  // 4-byte staged words (count-only fragments) leave LDS room for 16384-tuple
-  // tiles: twice the run length per partition and tile (HPCJOIN_NET_IPT=16).
-  // Default for them (measured on MI355X, 1B x 1B: 10.58 vs 10.78 ms per join).
   if constexpr (sizeof(typename Pol::StageT) == 4) {
-    if (!std::getenv("HPCJOIN_NET_IPT") || netIpt() == 16) {
+    if (g.ipt == 0 || g.ipt == 16) {
       launchNetClaimIpt<Pol, 16>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
       return;
     }
   }
-  if (netIpt() == 15 && narrow && bits == MAX_PART_BITS)
+  if (g.ipt == 15 && narrow && bits == MAX_PART_BITS)
     launchNetClaimIpt<Pol, 15>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
   else
     launchNetClaimIpt<Pol, CL_IPT_DEFAULT>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
@@ -1353,6 +1346,7 @@ static void setSplit(LocalFragPol &p, const SplitLayout &sl) { p.fragShift = sl.
 static void setSplit(LocalSplitPol &p, const SplitLayout &sl) {
   p.hi = sl.hi;
   p.fragShift = sl.fragShift;
+  p.loShift = sl.loShift;
 }
 
 // Alternative workgroup geometries of the production local scatter (split

@@ -2,7 +2,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
+#include <cstring>
 #include <cstdio>
 #include <cstdlib>
 
@@ -65,17 +67,48 @@ void Arena::releaseAll() {
   for (auto &f : fallbacks_) rawFree(loc_, f.first);
   fallbacks_.clear();
   fallbackBytes_ = 0;
-  rawFree(loc_, base_);
-  base_ = nullptr;
-  capacity_ = used_ = 0;
+  for (auto &c : chunks_) rawFree(loc_, c.base);
+  chunks_.clear();
+  ++generation_;
+}
+
+uint64_t Arena::capacity() const {
+  uint64_t s = 0;
+  for (const auto &c : chunks_) s += c.cap;
+  return s;
+}
+
+uint64_t Arena::used() const {
+  uint64_t s = 0;
+  for (const auto &c : chunks_) s += c.used;
+  return s;
+}
+
+void Arena::addChunk(uint64_t bytes, bool touch) {
+  bytes = ceilDiv(std::max<uint64_t>(bytes, ALIGNMENT), BIG_ALIGNMENT) * BIG_ALIGNMENT;
+  uint8_t *p = static_cast<uint8_t *>(rawAlloc(loc_, bytes, device_));
+  if (touch) {
+    if (loc_ == Location::Device) {
+      HIP_CHECK(hipSetDevice(device_));
+      HIP_CHECK(hipMemset(p, 0, bytes));
+    } else {
+      std::memset(p, 0, bytes);
+    }
+  }
+  chunks_.push_back(Chunk{p, bytes, 0});
+  ++generation_;
 }
 
 void Arena::reserve(uint64_t bytes) {
   releaseAll();
-  bytes = ceilDiv(bytes, ALIGNMENT) * ALIGNMENT;
-  if (bytes) base_ = static_cast<uint8_t *>(rawAlloc(loc_, bytes, device_));
-  capacity_ = bytes;
-  used_ = 0;
+  if (bytes) addChunk(bytes, false);
+}
+
+uint64_t Arena::ensure(uint64_t bytes, bool touch) {
+  const uint64_t have = capacity();
+  if (have >= bytes) return 0;
+  addChunk(bytes - have, touch);
+  return capacity() - have;
 }
 
 void *Arena::get(uint64_t bytes) {
@@ -84,40 +117,50 @@ void *Arena::get(uint64_t bytes) {
   // fresh hipMalloc would: sub-allocating them at 256-B offsets measurably
   // slowed the build/probe reads of the partitioned relations.
   const uint64_t align = sz >= BIG_BYTES ? BIG_ALIGNMENT : ALIGNMENT;
-  const uint64_t start = ceilDiv(used_, align) * align;
-  if (base_ && start + sz <= capacity_) {
-    void *p = base_ + start;
-    used_ = start + sz;
-    if (used_ + fallbackBytes_ > peak_) peak_ = used_ + fallbackBytes_;
-    return p;
+  for (auto &c : chunks_) {  // first fit, in chunk order (deterministic per allocation sequence)
+    const uint64_t start = ceilDiv(c.used, align) * align;
+    if (start + sz <= c.cap) {
+      c.used = start + sz;
+      const uint64_t u = used() + fallbackBytes_;
+      if (u > peak_) peak_ = u;
+      return c.base + start;
+    }
   }
   void *p = rawAlloc(loc_, sz, device_);
   const uint64_t accounted = sz + (align > ALIGNMENT ? align : 0);  // room for the padding once sub-allocated
   fallbacks_.emplace_back(p, accounted);
   fallbackBytes_ += accounted;
-  if (used_ + fallbackBytes_ > peak_) peak_ = used_ + fallbackBytes_;
+  peakFallback_ = std::max(peakFallback_, fallbackBytes_);
+  const uint64_t u = used() + fallbackBytes_;
+  if (u > peak_) peak_ = u;
+  ++generation_;
   return p;
 }
 
 void Arena::reset() {
-  if (!fallbacks_.empty()) {
-    const uint64_t want = peak_ + peak_ / 8;
+  if (!fallbacks_.empty() || peakFallback_) {
     for (auto &f : fallbacks_) rawFree(loc_, f.first);
     fallbacks_.clear();
     fallbackBytes_ = 0;
-    reserve(want);
+    // One new chunk holds every allocation that overflowed (+1/8 slack); the
+    // existing chunks keep their memory (and peers' mappings of it).
+    addChunk(peakFallback_ + peakFallback_ / 8, false);
+    peakFallback_ = 0;
   }
-  used_ = 0;
+  for (auto &c : chunks_) c.used = 0;
 }
 
 bool Arena::owns(const void *p) const {
   const uint8_t *q = static_cast<const uint8_t *>(p);
-  return base_ && q >= base_ && q < base_ + capacity_;
+  for (const auto &c : chunks_)
+    if (q >= c.base && q < c.base + c.cap) return true;
+  return false;
 }
 
 void *Arena::allocationOf(const void *p) const {
-  if (owns(p)) return base_;
   const uint8_t *q = static_cast<const uint8_t *>(p);
+  for (const auto &c : chunks_)
+    if (q >= c.base && q < c.base + c.cap) return c.base;
   for (const auto &f : fallbacks_) {
     const uint8_t *b = static_cast<const uint8_t *>(f.first);
     if (q >= b && q < b + f.second) return f.first;
@@ -131,6 +174,7 @@ void Arena::freeFallback(void *p) {
       rawFree(loc_, p);
       fallbackBytes_ -= fallbacks_[i].second;
       fallbacks_.erase(fallbacks_.begin() + i);
+      ++generation_;
       return;
     }
 }

@@ -1,13 +1,22 @@
-// Bump allocator over one big HBM (hipMalloc) or host (posix_memalign) block.
+// Bump allocator over a few big HBM (hipMalloc) or host (posix_memalign) chunks.
 //
 // The reference's memory::Pool (/root/reference/memory/Pool.cpp:25-79) is a
 // process-global host bump allocator with a posix_memalign fallback.  On
 // MI355X the same idea is what keeps hipMalloc/hipFree (which synchronise the
-// device) out of the timed join: a join's windows, send buffers and
-// workspaces are carved from a per-engine Arena that is rewound with reset()
-// at the start of every join.  When a join needs more than the arena holds,
-// the overflow is served by individual allocations and the arena grows to the
-// observed peak at the next reset(), so steady-state joins never allocate.
+// device, and on a fresh box can take seconds when the driver has to clear
+// the pages: profiles/r3a) out of the timed join: a join's windows, send
+// buffers and workspaces are carved from a per-engine Arena that is rewound
+// with reset() at the start of every join.
+//
+// Growth never moves or frees memory a previous join used: when a join needs
+// more than the chunks hold, the overflow is served by individual
+// allocations and reset() adds ONE new chunk sized for that overflow, so the
+// next join with the same allocation sequence fits (first fit over the chunks
+// in order) and steady-state joins never allocate.  ensure() grows ahead of
+// time (HashJoin reserves its plan's estimate at construction) and can touch
+// the new pages once, so a first join does not pay the first-touch cost.
+// Every change of the set of live allocations bumps generation(): peers that
+// mapped this arena's memory (one-sided windows) re-open their mappings.
 #pragma once
 
 #include <cstdint>
@@ -29,21 +38,27 @@ class Arena {
   Arena(const Arena &) = delete;
   Arena &operator=(const Arena &) = delete;
 
-  void reserve(uint64_t bytes);       // (re)allocate the main block (frees everything)
+  void reserve(uint64_t bytes);       // one chunk of `bytes` (frees everything first)
+  // Grow (never shrink, never move) so that the chunks hold >= bytes in all;
+  // touch = write the new chunk once (device: a memset) so its pages are
+  // mapped before the first join uses them.  Returns the bytes added.
+  uint64_t ensure(uint64_t bytes, bool touch = false);
   void *get(uint64_t bytes);          // bump-allocate (fallback allocation when exhausted)
   template <typename T>
   T *getArray(uint64_t count) { return reinterpret_cast<T *>(get(count * sizeof(T))); }
-  void reset();                       // rewind; grow to the last peak if it overflowed
+  void reset();                       // rewind; add a chunk for the last overflow, if any
   void releaseAll();
 
   Location location() const { return loc_; }
   int device() const { return device_; }
-  uint64_t capacity() const { return capacity_; }
-  uint64_t used() const { return used_; }
+  uint64_t capacity() const;          // bytes over all chunks
+  uint64_t used() const;              // bytes handed out from the chunks since the last reset
   uint64_t peak() const { return peak_; }
   uint64_t fallbackBytes() const { return fallbackBytes_; }
+  size_t chunkCount() const { return chunks_.size(); }
+  uint64_t generation() const { return generation_; }
   bool owns(const void *p) const;
-  // Start of the raw allocation (main block or fallback) holding p; null if none.
+  // Start of the raw allocation (chunk or fallback) holding p; null if none.
   void *allocationOf(const void *p) const;
   void freeFallback(void *p);         // frees one fallback allocation (no-op for arena memory)
 
@@ -51,13 +66,19 @@ class Arena {
   static void rawFree(Location loc, void *p);
 
  private:
+  struct Chunk {
+    uint8_t *base;
+    uint64_t cap;
+    uint64_t used;
+  };
+  void addChunk(uint64_t bytes, bool touch);
   Location loc_;
   int device_;
-  uint8_t *base_ = nullptr;
-  uint64_t capacity_ = 0;
-  uint64_t used_ = 0;
+  std::vector<Chunk> chunks_;
   uint64_t peak_ = 0;
   uint64_t fallbackBytes_ = 0;
+  uint64_t peakFallback_ = 0;  // largest fallbackBytes_ since the last reset
+  uint64_t generation_ = 0;
   std::vector<std::pair<void *, uint64_t>> fallbacks_;
 };
 

@@ -71,6 +71,8 @@ void HashJoin::makeJoinPlan() {
   // (Relation::keyBoundKnown / ridsPositional): no pass over the data; others
   // are scanned once here (kernels::keyRidMax).
   const uint32_t C = std::max<uint32_t>(1, config.chunks);
+  ridLo[0] = ridLo[1] = ~0ull;
+  ridHi[0] = ridHi[1] = 0;
   const size_t STATS = 3 + 4 * (size_t)C;
   std::vector<uint64_t> st(STATS, 0);
   int which = 0;
@@ -102,6 +104,10 @@ void HashJoin::makeJoinPlan() {
       }
       st[0] = std::max(st[0], h[0]);
       st[1] = std::max(st[1], h[1]);
+      if (h[2] <= h[1]) {
+        ridLo[which] = std::min(ridLo[which], h[2]);
+        ridHi[which] = std::max(ridHi[which], h[1]);
+      }
       st[2 + ((size_t)which * C + c) * 2] = h[2];
       st[3 + ((size_t)which * C + c) * 2] = h[1];
     }
@@ -299,6 +305,17 @@ bool HashJoin::lowKeyBitsSkewed() {
 void HashJoin::join() {
   run();
   RESULT_COUNTER = result.localMatches;
+}
+
+void HashJoin::setRowSink(const kernels::RowSink &s) {
+  const uint64_t off[2] = {s.offA, s.offB}, rows[2] = {s.rowsAN, s.rowsBN};
+  for (int r = 0; r < 2; ++r)
+    JOIN_ASSERT(ridLo[r] > ridHi[r] || (ridLo[r] >= off[r] && ridHi[r] - off[r] < rows[r]), "HashJoin",
+                "row sink: %s payload rows [%lu, %lu) do not cover this rank's rids [%lu, %lu]",
+                r ? "outer" : "inner", (unsigned long)off[r], (unsigned long)(off[r] + rows[r]),
+                (unsigned long)ridLo[r], (unsigned long)ridHi[r]);
+  sink = s;
+  hasSink = true;
 }
 
 bool HashJoin::canFuseRows() const {

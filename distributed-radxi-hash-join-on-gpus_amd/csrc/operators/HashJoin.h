@@ -80,7 +80,13 @@ class HashJoin {
   // from its materialize pass instead of pairs.  canFuseRows() says whether
   // this plan does; the caller keeps the sink's buffers alive over run().
   bool canFuseRows() const;
-  void setRowSink(const kernels::RowSink &s) { sink = s; hasSink = true; }
+  // Throws unless the sink's payload columns cover this rank's rids of both
+  // relations (the fused kernel indexes rows by rid - offset on the device).
+  void setRowSink(const kernels::RowSink &s);
+  // Smallest / largest rid of this rank's slice of relation 0 (inner) or 1
+  // (outer); lo > hi for an empty slice.
+  uint64_t ridMin(int which) const { return ridLo[which]; }
+  uint64_t ridMax(int which) const { return ridHi[which]; }
   void clearRowSink() { hasSink = false; }
 
  protected:
@@ -113,6 +119,7 @@ class HashJoin {
   const ulonglong2 *output = nullptr;
   kernels::RowSink sink;
   bool hasSink = false;
+  uint64_t ridLo[2] = {~0ull, ~0ull}, ridHi[2] = {0, 0};
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
 };
 

@@ -15,8 +15,8 @@ namespace operators {
 using kernels::ROW_WORDS;
 
 LateMaterialization::LateMaterialization(core::ExecContext *ctx, const PayloadColumn &inner,
-                                         const PayloadColumn &outer)
-    : ctx(ctx) {
+                                         const PayloadColumn &outer, uint32_t matVariant)
+    : ctx(ctx), matVariant(matVariant) {
   cols[0] = inner;
   cols[1] = outer;
 }
@@ -30,7 +30,7 @@ void LateMaterialization::materialize(const ulonglong2 *pairs, uint64_t n, uint6
   static_assert(OUT_WORDS == 2 + 2 * ROW_WORDS, "output row layout");
   if (ctx->onDevice() && ctx->comm()->size() == 1) {
     kernels::materializeLocal(pairs, n, cols[0].rows, cols[0].ridOffset, cols[1].rows, cols[1].ridOffset, out,
-                              ctx->stream());
+                              ctx->stream(), matVariant);
     HIP_CHECK(hipStreamSynchronize(ctx->stream()));
     return;
   }

@@ -28,7 +28,9 @@ class LateMaterialization {
  public:
   static constexpr uint32_t OUT_WORDS = 2 + 2 * 4;  // rid_inner, rid_outer, inner row, outer row
 
-  LateMaterialization(core::ExecContext *ctx, const PayloadColumn &inner, const PayloadColumn &outer);
+  // matVariant: KernelVariants::matVariant of the single-rank gather kernel.
+  LateMaterialization(core::ExecContext *ctx, const PayloadColumn &inner, const PayloadColumn &outer,
+                      uint32_t matVariant = 1);
   // out: [n][OUT_WORDS] u64 in the context's memory.  Collective: every rank calls it.
   void materialize(const ulonglong2 *pairs, uint64_t n, uint64_t *out);
 
@@ -37,6 +39,7 @@ class LateMaterialization {
   void fetchHost(const ulonglong2 *pairs, uint64_t n, int side, const PayloadColumn &col, uint64_t *out);
   core::ExecContext *ctx;
   PayloadColumn cols[2];
+  uint32_t matVariant = 1;
 };
 
 }  // namespace operators

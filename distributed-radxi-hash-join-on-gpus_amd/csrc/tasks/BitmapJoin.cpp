@@ -41,20 +41,22 @@ BitmapJoin::Outcome BitmapJoin::run(bool exact) { return ctx->onDevice() ? runDe
 const BitmapJoin::SidePlan &BitmapJoin::sidePlan(uint64_t n, bool exact, uint32_t stride) const {
   struct Key {
     uint64_t n;
-    uint32_t maxBlocks, bits, stride;
+    uint32_t maxBlocks, bits, stride, ipt;
     bool exact;
     bool operator<(const Key &o) const {
-      return std::tie(n, maxBlocks, bits, stride, exact) < std::tie(o.n, o.maxBlocks, o.bits, o.stride, o.exact);
+      return std::tie(n, maxBlocks, bits, stride, ipt, exact) <
+             std::tie(o.n, o.maxBlocks, o.bits, o.stride, o.ipt, o.exact);
     }
   };
   thread_local std::map<Key, SidePlan> cache;
   const uint32_t F = 1u << plan.networkBits;
-  const Key k{n, maxBlocks, plan.networkBits, stride, exact};
+  const Key k{n, maxBlocks, plan.networkBits, stride, plan.variants.netIpt, exact};
   auto it = cache.find(k);
   if (it != cache.end()) return it->second;
   if (cache.size() > 64) cache.clear();
   SidePlan sp;
   sp.geom = kernels::partitionGeometry(n, maxBlocks);
+  sp.geom.ipt = plan.variants.netIpt;
   sp.stride = exact ? 1 : kernels::sampleStrideFor(sp.geom, n, F, stride);
   sp.sc = kernels::sampleScale(sp.geom, n, sp.stride, exact);
   sp.cap = kernels::sampledLayoutCapacityBound(sp.sc, F);
@@ -124,6 +126,8 @@ void BitmapJoin::layoutSides(Side *sides, uint32_t count, bool exact, bool narro
     s.slices.end = lay[i].gend;
     s.slices.narrow = narrow;
     s.slices.count = s.relation->getLocalSize();
+    s.slices.threads = plan.variants.bmThreads;
+    s.slices.flat = plan.variants.bmFlat;
     s.frags = ws.getArray<uint32_t>(std::max<uint64_t>(s.cap, 16));
   }
   kernels::netSampledLayout(lay, count, F, narrow, st);
@@ -141,11 +145,9 @@ void BitmapJoin::scatterSide(Side &s) {
 // bitmaps, at most 4 (1B dense keys: 4 x 32 MiB).  Each range is one more
 // collective (~10-30 us of launch and handshake over xGMI), against the probe
 // of all but the last range moving behind the all-reduce.
-// HPCJOIN_REDUCE_CHUNKS=k forces k.
-static uint32_t reduceChunks(uint64_t bitmapBytes) {
-  const char *e = std::getenv("HPCJOIN_REDUCE_CHUNKS");  // read per join: tests switch it
-  const int forced = e ? std::max(1, std::min(std::atoi(e), 64)) : 0;
-  if (forced) return (uint32_t)forced;
+// KernelVariants::reduceChunks = k forces k.
+static uint32_t reduceChunks(uint64_t bitmapBytes, uint32_t forced) {
+  if (forced) return std::max<uint32_t>(1, std::min<uint32_t>(forced, 64));
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4, bitmapBytes >> 25));
 }
 
@@ -218,7 +220,7 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
     // its bitmaps are built (while range c + 1 builds), and the probe of a
     // range starts as soon as it is reduced, so after the last range lands
     // only its probe is left.
-    const uint32_t K = std::min<uint32_t>(reduceChunks((uint64_t)F * words * 4), F);
+    const uint32_t K = std::min<uint32_t>(reduceChunks((uint64_t)F * words * 4, plan.variants.reduceChunks), F);
     std::vector<hipEvent_t> built(K), reduced(K);
     for (uint32_t c = 0; c < K; ++c) {
       const uint32_t p0 = (uint32_t)((uint64_t)F * c / K), p1 = (uint32_t)((uint64_t)F * (c + 1) / K);

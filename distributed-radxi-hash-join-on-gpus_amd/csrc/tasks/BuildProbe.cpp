@@ -61,6 +61,8 @@ void BuildProbe::configure() {
   args.wide = plan.wide;
   args.keyOnly = plan.keyOnly;
   args.materialize = plan.materialize;
+  args.keyCount = plan.variants.keyCount;
+  args.rowsLds = plan.variants.rowsLds;
   if (wi->getPartitionedHi()) {
     JOIN_ASSERT(wo->getPartitionedHi(), "BuildProbe", "one side split, the other not");
     args.split = 1;
@@ -135,6 +137,19 @@ void BuildProbe::execute() {
                                  "bytes");
   kernels::bpPlanCounts(args, counts, ctx->stream());
   kernels::scanExclusiveU32(counts, offsets, args.P, nItems, scanWs, ctx->stream());
+  if (args.keyOnly && (args.keyCount == 6 || args.split)) {  // the item kernels read unsplit words only
+    // Key-only counting: resolved spans through a device work queue.
+    auto *spans = ws.getArray<kernels::BPSpan>(capacity);
+    uint32_t *queue = ws.getArray<uint32_t>(1);
+    kernels::bpEmitSpans(args, counts, offsets, spans, capacity, ctx->stream());
+    tl.beginSplit("BPKERNEL", "BPBUILD", wb, "BPPROBE", wp, ctx->stream());
+    kernels::buildProbeKeySpans(args, spans, nItems, capacity, queue, ctx->stream());
+    hipEvent_t done = tl.mark(ctx->stream());
+    tl.endAt("BPKERNEL", done);
+    tl.endAt("BPTASKTIME", done);
+    readBackCounters();
+    return;
+  }
   kernels::bpEmit(args, counts, offsets, items, capacity, ctx->stream());
   if (!plan.materialize) {
     tl.beginSplit("BPKERNEL", "BPBUILD", wb, "BPPROBE", wp, ctx->stream());

@@ -94,6 +94,10 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
   kernels::SplitLayout split;
   split.on = ctx->onDevice() && !wide && (plan.splitLocal || frag) ? 1u : 0u;
   split.fragShift = frag ? bits : plan.fragShift;
+  if (plan.keyOnly) {  // key fragment above both digits: low 32 bits + next 16 (makePlan checked it fits)
+    split.loShift = bits;
+    split.fragShift = bits + 32;
+  }
   JOIN_ASSERT(!frag || (ctx->onDevice() && plan.twoLevel), "LocalPartitioning", "fragments need the device two-level path");
   const uint32_t ob = frag ? 2 : split.on ? 4 : tb;  // bytes per tuple of the main output column
   const uint32_t align = split.on ? 64 : 16;   // slot granularity: whole 128-byte lines of every column

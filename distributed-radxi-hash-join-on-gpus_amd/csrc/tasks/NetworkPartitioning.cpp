@@ -44,7 +44,8 @@ void NetworkPartitioning::partition(data::Relation *relation, data::Window *wind
   JOIN_ASSERT(xp.scatterTotal == n, "NetworkPartitioning", "plan scatters %lu of %lu tuples",
               (unsigned long)xp.scatterTotal, (unsigned long)n);
   const uint32_t bits = plan.networkBits, F = 1u << bits;
-  const kernels::PartitionGeometry &g = local->geometry();
+  kernels::PartitionGeometry g = local->geometry();
+  g.ipt = plan.variants.netIpt;
   const uint32_t bpc = local->blocksPerChunk(), chunks = local->getChunkCount();
   const bool single = xp.numberOfNodes == 1;
   const uint32_t tb = window->tupleBytes();

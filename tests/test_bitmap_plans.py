@@ -80,21 +80,23 @@ def test_replicated_bitmap_ranks(C, dev, n_ranks, outer_dist):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("nth,flat", [("256", "0"), ("256", "1"), ("1024", "0"), ("1024", "1")])
-def test_bitmap_walk_variants(C, monkeypatch, nth, flat):
+def test_bitmap_walk_variants(C, nth, flat):
     """Both slice walks of the bitmap kernels (one pipelined walk per claim
     slice / one flat walk over all slices of a partition) at both workgroup
     sizes give the exact count: short partitions (many empty and sub-vector
     slices, tails of 1-3 fragments) and long ones, N = 1 fused kernel and the
     replicated build / probe kernels at N = 2."""
-    monkeypatch.setenv("HPCJOIN_BM_NTH", nth)
-    monkeypatch.setenv("HPCJOIN_BM_FLAT", flat)
+    def cfg(c):
+        force_replicated(c, C)
+        c.bm_threads = int(nth)
+        c.bm_flat = int(flat)
     for G_R, G_S, n_ranks in [(40_009, 70_001, 1), (1 << 20, 3 << 19, 1), (3_000_017, 1_000_003, 1),
                               (300_007, 450_011, 2)]:
         inner = C.GenSpec(seed=77)
         outer = C.GenSpec(distribution=C.KeyDistribution.UNIFORM, seed=5, domain=G_R)
         exp = C.Relation.expected_matches(inner, G_R, outer, G_S)
         out = run_ranks(C, n_ranks, "device", generated(C, "device", inner, G_R, n_ranks),
-                        generated(C, "device", outer, G_S, n_ranks), G_R, G_S, lambda c: force_replicated(c, C))
+                        generated(C, "device", outer, G_S, n_ranks), G_R, G_S, cfg)
         for res_list, plan in out:
             assert plan.bitmap_join
             for res in res_list:
@@ -143,7 +145,6 @@ def test_replicated_bitmap_split_pieces(C, dev, n_ranks):
     """21 fragment bits on the replicated plan: each partition's bitmap is
     built and probed as two 128 KiB pieces (adjacent in the all-reduced
     array), in 1 and 3 all-reduce ranges; exact on every rank."""
-    import os
     loc = "device" if dev == "cuda" else "host"
     nb = 2
     G_R, G_S = 1 << (21 + nb), 3 << (19 + nb)
@@ -151,16 +152,13 @@ def test_replicated_bitmap_split_pieces(C, dev, n_ranks):
     outer = C.GenSpec(distribution=C.KeyDistribution.UNIFORM, seed=42, domain=G_R)
     exp = C.Relation.expected_matches(inner, G_R, outer, G_S)
 
-    def cfg(c):
-        force_replicated(c, C)
-        c.network_bits = nb
-    for chunks in ("1", "3"):
-        os.environ["HPCJOIN_REDUCE_CHUNKS"] = chunks
-        try:
-            out = run_ranks(C, n_ranks, loc, generated(C, loc, inner, G_R, n_ranks),
-                            generated(C, loc, outer, G_S, n_ranks), G_R, G_S, cfg)
-        finally:
-            del os.environ["HPCJOIN_REDUCE_CHUNKS"]
+    for chunks in (1, 3):
+        def cfg(c):
+            force_replicated(c, C)
+            c.network_bits = nb
+            c.reduce_chunks = chunks
+        out = run_ranks(C, n_ranks, loc, generated(C, loc, inner, G_R, n_ranks),
+                        generated(C, loc, outer, G_S, n_ranks), G_R, G_S, cfg)
         for res_list, plan in out:
             assert plan.bitmap_join and plan.bitmap_replicated and plan.bitmap_bits == 21
             for res in res_list:
@@ -186,17 +184,20 @@ def test_bitmap_tiny_and_empty_sides(C, n_ranks, G_R, G_S):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("chunks", ["1", "3", "7"])
-def test_replicated_bitmap_reduce_ranges(C, monkeypatch, chunks):
+def test_replicated_bitmap_reduce_ranges(C, chunks):
     """The replicated plan's all-reduce in k partition ranges (k not dividing
     the partition count), each range probed behind its own all-reduce: exact
     counts on every rank."""
-    monkeypatch.setenv("HPCJOIN_REDUCE_CHUNKS", chunks)
     G_R, G_S, n = 1_000_003, 2_000_029, 4
+
+    def cfg(c):
+        force_replicated(c, C)
+        c.reduce_chunks = int(chunks)
     inner = C.GenSpec(seed=11)
     outer = C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=12, domain=G_R, zipf_theta=0.75)
     exp = C.Relation.expected_matches(inner, G_R, outer, G_S)
     out = run_ranks(C, n, "device", generated(C, "device", inner, G_R, n), generated(C, "device", outer, G_S, n),
-                    G_R, G_S, lambda c: force_replicated(c, C))
+                    G_R, G_S, cfg)
     for res_list, plan in out:
         assert plan.bitmap_join and plan.bitmap_replicated
         for res in res_list:
@@ -299,12 +300,11 @@ def test_sparse64_generator(C):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", ["1", "0", "2", "3", "4", "5"])
-def test_key_only_count_variants(C, monkeypatch, variant):
+@pytest.mark.parametrize("variant", ["6", "6s", "1", "0", "2", "3", "4", "5"])
+def test_key_only_count_variants(C, variant):
     """Every key-only count kernel variant against a torch reference, with heavily repeated inner keys (Zipf over sparse
     63-bit keys: long overflow chains through the next buckets)."""
     from helpers import ref_join_count
-    monkeypatch.setenv("HPCJOIN_KCOUNT", variant)
     ctx = C.ExecContext("device", 0, C.LocalCommunicator())
     for (G_R, G_S, theta) in [(200_003, 300_007, 0.99), (1 << 20, 1 << 21, 0.5)]:
         inner = C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=31, domain=G_R // 4, zipf_theta=theta)
@@ -315,8 +315,13 @@ def test_key_only_count_variants(C, monkeypatch, variant):
         S = C.Relation(G_S, G_S, "device", 0)
         R.generate(inner, 0)
         S.generate(outer, 0)
-        j = C.HashJoin(R, S, ctx, C.JoinConfig())
-        assert j.plan.key_only
+        cfg = C.JoinConfig()
+        cfg.key_count = int(variant[0])
+        # "6s": span kernel over the split (u32 + u16) local output; the item
+        # kernels (0-5) read unsplit 8-byte words only
+        cfg.split_local = variant == "6s"
+        j = C.HashJoin(R, S, ctx, cfg)
+        assert j.plan.key_only and j.plan.split_local == (variant == "6s")
         exp = ref_join_count(R.to_tensor()[:, 0].cpu(), S.to_tensor()[:, 0].cpu())
         for _ in range(2):
             assert j.run()["global_matches"] == exp, (variant, G_R, theta)
