@@ -119,6 +119,103 @@ def link_prediction(info, plan, results):
             "measured_wire_bytes_rank0": results[-1]["wire_bytes"]}
 
 
+def rccl_debug_env(info):
+    """Ask RCCL to log its transport choices to a per-rank file (not stdout:
+    rank 0 prints one JSON line), unless the caller configured RCCL logging.
+    Must run before any RCCL communicator exists."""
+    if info.world <= 1 or "NCCL_DEBUG" in os.environ:
+        return None
+    import tempfile
+    path = os.path.join(tempfile.gettempdir(), f"hpcjoin_rccl.{os.getpid()}.log")
+    os.environ["NCCL_DEBUG"] = "INFO"
+    os.environ["NCCL_DEBUG_SUBSYS"] = "INIT,P2P,SHM,NET"
+    os.environ["NCCL_DEBUG_FILE"] = path
+    return path
+
+
+def rccl_transports(path):
+    """Counts of RCCL channel connections by transport in this rank's log."""
+    out = {"P2P": 0, "SHM": 0, "NET": 0}
+    if not path or not os.path.exists(path):
+        return {"log": None}
+    with open(path, errors="replace") as f:
+        for line in f:
+            if " via " not in line:
+                continue
+            for k in out:
+                if f"via {k}" in line:
+                    out[k] += 1
+    try:
+        os.unlink(path)
+    except OSError:
+        pass
+    return out
+
+
+def topology(C, info, on_gpu):
+    """Per-rank device identity (ordinal, PCI bus id, host), gathered on every
+    rank.  Two ranks on one device of one host are refused unless the run is
+    an explicit shared-GPU rehearsal (HPCJOIN_SHARE_GPU=1)."""
+    me = {"rank": info.rank, "local_rank": info.local_rank, "host": socket.gethostname()}
+    if on_gpu:
+        d = C.device_info(torch.cuda.current_device())
+        me.update(device=d["device"], pci_bus_id=d["pci_bus_id"], arch=d["arch"], compute_units=d["compute_units"],
+                  visible_devices=d["visible_devices"])
+    ranks = [me]
+    if info.world > 1:
+        ranks = [None] * info.world
+        dist.all_gather_object(ranks, me)
+    seen = {}
+    for r in ranks:
+        key = (r["host"], r.get("pci_bus_id"))
+        if on_gpu and key in seen and os.environ.get("HPCJOIN_SHARE_GPU") != "1":
+            raise SystemExit(f"bench.py: ranks {seen[key]} and {r['rank']} share device {key[1]} on {key[0]}; "
+                             "one rank per GPU (set HPCJOIN_SHARE_GPU=1 only for a shared-GPU rehearsal)")
+        seen.setdefault(key, r["rank"])
+    return {"ranks": ranks, "distinct_devices": len(seen), "shared_gpu_rehearsal": os.environ.get("HPCJOIN_SHARE_GPU") == "1"}
+
+
+def calibrate_links(comm, info, on_gpu, mb_per_peer=256, iters=5):
+    """Measured link bandwidth for the plan's link model: an RCCL all-to-allv
+    on the engine's own communicator (each rank sends mb_per_peer MiB to every
+    peer) and a torch.distributed RCCL all-reduce of 128 MiB."""
+    if info.world <= 1 or not on_gpu:
+        return None
+    n = info.world
+    words = (mb_per_peer << 20) // 8
+    send = torch.ones(words * n, dtype=torch.int64, device="cuda")
+    recv = torch.empty_like(send)
+    counts = [words] * n
+    for _ in range(2):
+        comm.all_to_all_v(send, counts, recv, counts)
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        comm.all_to_all_v(send, counts, recv, counts)
+    t_a2a = (time.perf_counter() - t0) / iters
+    red = torch.ones((128 << 20) // 4, dtype=torch.float32, device="cuda")
+    for _ in range(2):
+        dist.all_reduce(red)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        dist.all_reduce(red)
+    torch.cuda.synchronize()
+    t_ar = (time.perf_counter() - t0) / iters
+    mine = [int(t_a2a * 1e9), int(t_ar * 1e9)]
+    allv = comm.all_gather(mine)
+    t_a2a, t_ar = max(allv[0::2]) / 1e9, max(allv[1::2]) / 1e9
+    peer_bytes = words * 8
+    del send, recv, red
+    torch.cuda.empty_cache()
+    return {"source": f"measured: RCCL all-to-allv of {mb_per_peer} MiB per peer on the engine communicator, "
+                      f"torch.distributed all-reduce of 128 MiB, {iters} iterations each (max over ranks)",
+            "all_to_all_GBps_per_peer": round(peer_bytes / t_a2a / 1e9, 2),
+            "all_to_all_GBps_per_rank": round((n - 1) * peer_bytes / t_a2a / 1e9, 2),
+            "all_reduce_busbw_GBps": round(2 * (n - 1) / n * (128 << 20) / t_ar / 1e9, 2),
+            "all_to_all_ms": round(t_a2a * 1e3, 3), "all_reduce_ms": round(t_ar * 1e3, 3)}
+
+
 def measure(C, info, ctx, comm, on_gpu, G_R, G_S, inner, outer, cfg, rel_loc, steps, warmup):
     """Generate this rank's slices, build the join (timed with its first run:
     the cold-join cost incl. planning), warm up, then time `steps` joins
@@ -137,20 +234,25 @@ def measure(C, info, ctx, comm, on_gpu, G_R, G_S, inner, outer, cfg, rel_loc, st
             torch.cuda.synchronize()
 
     barrier()
+    # Construction plans the join and grows the engine's workspace to the
+    # plan's estimate (pages touched once): reported as setup_ms.  The first
+    # run() after it is the cold join (first kernel launches, first use of the
+    # arena): first_join_ms.
     t0 = time.perf_counter()
     join = C.HashJoin(R, S, ctx, cfg)
-    t_built = time.perf_counter()
+    barrier()
+    setup_ms = (time.perf_counter() - t0) * 1e3
+    t0 = time.perf_counter()
     first = join.run()
     barrier()
     first_ms = (time.perf_counter() - t0) * 1e3
     if os.environ.get("HPCJOIN_TRACE_FIRST") == "1":
         keys = ("join_ms", "setup_ms", "teardown_ms") + PHASES
         print(json.dumps({"first_join": {k: round(first[k], 3) for k in keys if k in first},
-                          "construct_ms": round((t_built - t0) * 1e3, 3), "first_ms": round(first_ms, 3)}),
+                          "setup_ms": round(setup_ms, 3), "first_ms": round(first_ms, 3)}),
               file=sys.stderr, flush=True)
-    # Grow the engine arena to the first join's peak right after it, so the
-    # remaining warmups (not the first timed join) are the first to run on the
-    # freshly reserved workspace; the first join pays a one-time hipMalloc.
+    # If the first join still spilled past the reserved workspace, the arena
+    # adds a chunk for it here (never inside a timed join).
     ctx.reset_scratch()
     for _ in range(max(0, warmup - 1)):
         join.run()
@@ -162,15 +264,17 @@ def measure(C, info, ctx, comm, on_gpu, G_R, G_S, inner, outer, cfg, rel_loc, st
         results.append(join.run())
     barrier()
     elapsed = time.perf_counter() - t0
-    mine = [int(elapsed * 1e9), int(first_ms * 1e6)]
+    mine = [int(elapsed * 1e9), int(first_ms * 1e6), int(setup_ms * 1e6)]
     if info.world > 1:
         allv = comm.all_gather(mine)
-        elapsed, first_ms = max(allv[0::2]) / 1e9, max(allv[1::2]) / 1e6
+        elapsed, first_ms, setup_ms = max(allv[0::3]) / 1e9, max(allv[1::3]) / 1e6, max(allv[2::3]) / 1e6
     ms = elapsed * 1e3 / steps
     out = {
         "ms_per_step": round(ms, 3),
         "value": round((G_R + G_S) * steps / elapsed / 1e9, 4),
         "first_join_ms": round(first_ms, 3),
+        "setup_ms": round(setup_ms, 3),
+        "workspace_reserved_GB": round(join.reserved_bytes / 1e9, 2),
         "matches": results[-1]["global_matches"],
         "expected_matches": expected,
         "correct": all(r["global_matches"] == expected for r in [first] + results) if expected is not None else None,
@@ -202,12 +306,17 @@ def main():
     args = ap.parse_args()
 
     C = hpcjoin.require_native()
+    from hpcjoin.parallel import DistInfo
+    rccl_log = rccl_debug_env(DistInfo(world=int(os.environ.get("WORLD_SIZE", "1"))))
     info = init_distributed()
     if info.world != args.gpus and not (args.gpus == 1 and info.world == 1):
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={info.world}")
     on_gpu = torch.cuda.is_available()
     loc = "device" if on_gpu else "host"
+    topo = topology(C, info, on_gpu)
     ctx, comm = make_context(info, loc)
+    topo["communicator"] = {"name": comm.name(), "size": comm.size()}
+    calib = calibrate_links(comm, info, on_gpu)
 
     G_R, G_S = int(args.inner), int(args.outer)
     if not on_gpu:  # CPU fallback for plumbing only: keep it small
@@ -220,6 +329,8 @@ def main():
         cfg.chunks = args.chunks
     elif "HPCJOIN_CHUNKS" not in os.environ:
         cfg.chunks = 1 if info.world == 1 else 4
+    if calib:
+        cfg.link_gbps_per_peer = calib["all_to_all_GBps_per_peer"]
 
     def specs(sparse):
         inner = C.GenSpec(distribution=C.KeyDistribution.UNIQUE, seed=1234)
@@ -241,12 +352,37 @@ def main():
               "step_ms": [round(r["join_ms"], 2) for r in results],
               "step_phases_ms": [[round(r[k], 2) for k in PHASES] for r in results]}
     links = link_prediction(info, plan, results)
+    if links is not None:
+        links["bandwidth"] = calib or {"source": "model: 64 GB/s per peer (no calibration run)"}
     del join
     ctx.reset_scratch()
 
-    general = None
+    shuffle = None
     comm_ok = True
-    if args.general == "on" and args.dist in ("unique", "uniform", "zipf"):
+    if info.world > 1 and plan.bitmap_replicated:
+        # The reference's own N > 1 algorithm on the headline workload: hash-
+        # partition shuffle (claim scatter + chunked RCCL all-to-allv, the
+        # MPI_Put analog) instead of the replicated bitmaps the planner prefers.
+        try:
+            cfg_sh = config_from_dict({"replicate_bitmap": "OFF"})
+            cfg_sh.chunks = cfg.chunks
+            cfg_sh.link_gbps_per_peer = cfg.link_gbps_per_peer
+            sh = measure(C, info, ctx, comm, on_gpu, G_R, G_S, *specs(args.general == "only"), cfg_sh, rel_loc,
+                         max(2, args.steps // 2), max(1, args.warmup))
+            sj, sres = sh.pop("join"), sh.pop("results")
+            sh["links"] = link_prediction(info, sj.plan, sres)
+            sh["wire_bytes_rank0"] = sres[-1]["wire_bytes"]
+            sh["received_tuples_rank0"] = [sres[-1]["inner_received"], sres[-1]["outer_received"]]
+            del sj
+            shuffle = {"data": "same relations as the headline, plan forced to the hash-partition shuffle", **sh}
+            ctx.reset_scratch()
+        except Exception as e:  # noqa: BLE001
+            shuffle = {"error": f"{type(e).__name__}: {e}"[:500], "correct": False}
+            comm_ok = False
+            print(f"bench.py: shuffle path failed on rank {info.rank}: {e}", file=sys.stderr, flush=True)
+
+    general = None
+    if args.general == "on" and args.dist in ("unique", "uniform", "zipf") and comm_ok:
         # The secondary measurement must not cost the headline line: a failure
         # here (the engine aborts the communicator on every rank) is reported
         # in general_path and the headline is still printed.
@@ -266,6 +402,10 @@ def main():
             print(f"bench.py: general path failed on rank {info.rank}: {e}", file=sys.stderr, flush=True)
 
     correct = head["correct"] is not False
+    if info.world > 1:
+        tr = [None] * info.world
+        dist.all_gather_object(tr, rccl_transports(rccl_log))
+        topo["rccl_transports"] = tr
     if info.rank == 0:
         line = {
             "metric": "billion tuples/sec (whole node), 1B x 1B uniform int64 keys, 1/2/4/8 MI355X",
@@ -292,13 +432,16 @@ def main():
                 "input": rel_loc,
             },
             "first_join_ms": head["first_join_ms"],
+            "setup_ms": head["setup_ms"],
             "matches": head["matches"],
             "expected_matches": head["expected_matches"],
             "correct": head["correct"],
             "phases_ms": head["phases_ms"],
             "links": links,
+            "shuffle_path": shuffle,
             "general_path": general,
             "engine": engine,
+            "topology": topo,
             "device": torch.cuda.get_device_name(0) if on_gpu else "cpu",
         }
         print(json.dumps(line), flush=True)

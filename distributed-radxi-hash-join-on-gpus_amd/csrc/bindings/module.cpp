@@ -640,6 +640,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("chunks", &core::JoinConfig::chunks)
       .def_readwrite("checks", &core::JoinConfig::checks)
       .def_readwrite("max_partition_blocks", &core::JoinConfig::maxPartitionBlocks)
+      .def_readwrite("reserve_workspace", &core::JoinConfig::reserveWorkspace)
+      .def_readwrite("link_gbps_per_peer", &core::JoinConfig::linkGBpsPerPeer)
       // KernelVariants, flattened (sweeps / A-B tests; core/Types.h)
       .def_property("net_ipt", [](const core::JoinConfig &c) { return c.variants.netIpt; },
                     [](core::JoinConfig &c, uint32_t v) { c.variants.netIpt = v; })
@@ -753,6 +755,24 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("communicator", [](std::shared_ptr<comm::InProcessGroup> g, uint32_t rank) {
         return std::static_pointer_cast<comm::Communicator>(std::make_shared<comm::InProcessCommunicator>(g, rank));
       });
+  m.def("device_info", [](int dev) {
+    // Identity of a device as this process sees it (bench.py topology record).
+    hipDeviceProp_t pr;
+    HIP_CHECK(hipGetDeviceProperties(&pr, dev));
+    char bus[64] = {0};
+    HIP_CHECK(hipDeviceGetPCIBusId(bus, sizeof(bus), dev));
+    int count = 0;
+    HIP_CHECK(hipGetDeviceCount(&count));
+    py::dict d;
+    d["device"] = dev;
+    d["pci_bus_id"] = std::string(bus);
+    d["name"] = std::string(pr.name);
+    d["arch"] = std::string(pr.gcnArchName);
+    d["compute_units"] = pr.multiProcessorCount;
+    d["hbm_bytes"] = (uint64_t)pr.totalGlobalMem;
+    d["visible_devices"] = count;
+    return d;
+  }, py::arg("device"));
   m.def("rccl_unique_id", []() {
     auto v = comm::RcclCommunicator::uniqueId();
     return py::bytes(reinterpret_cast<const char *>(v.data()), v.size());
@@ -897,6 +917,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         j.join();
       })
       .def_property_readonly("plan", &operators::HashJoin::getPlan)
+      .def("workspace_estimate", &operators::HashJoin::workspaceEstimate)
+      .def_property_readonly("reserved_bytes", &operators::HashJoin::reservedBytes)
       .def(
           "materialize_payloads",
           [](operators::HashJoin &j, std::shared_ptr<core::ExecContext> ctx, at::Tensor innerRows, uint64_t innerOffset,

@@ -109,6 +109,14 @@ struct JoinConfig {
   uint32_t localItemTiles = 64; // local pass work item: up to this many 4096-tuple tiles of one segment
   uint32_t localGeometry = 0;   // local scatter workgroup geometry (0 = 1024 x 8; 1-4: sweep alternatives)
   KernelVariants variants;      // kernel-shape variants (sweeps; core/Types.h)
+  // Device engines: grow the workspace arena to the plan's size estimate at
+  // HashJoin construction (and touch the new pages once), so that the first
+  // join allocates nothing (HashJoin::workspaceEstimate).
+  bool reserveWorkspace = true;
+  // Link model of the N > 1 plan choice / prediction: one-way GB/s one rank
+  // reaches to one peer (0 = kDefaultLinkGBpsPerPeer; bench.py calibrates it
+  // with an RCCL all-to-all).
+  double linkGBpsPerPeer = 0;
 
   std::string describe() const;
 };

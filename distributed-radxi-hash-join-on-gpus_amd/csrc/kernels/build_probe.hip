@@ -1262,12 +1262,34 @@ struct KsSrc {
   }
 };
 
+// The bucket table: 4 slots (32 B) per bucket.  AoS keeps a bucket's two
+// 16-byte halves adjacent; SoA (KernelVariants::keyCount 7) stores all first
+// halves, then all second halves: a random ds_read_b128 then starts at one of
+// 16 bank quads instead of 8 (32-byte buckets), halving the expected lane
+// collisions per 16-lane group.
+template <bool SOA>
+struct KsTable {
+  unsigned long long *t;
+  uint32_t maxBuckets;
+  __device__ __forceinline__ const ulonglong2 *half(uint32_t b, int h) const {
+    if constexpr (SOA)
+      return reinterpret_cast<const ulonglong2 *>(t + (h ? 2 * maxBuckets : 0)) + b;
+    else
+      return reinterpret_cast<const ulonglong2 *>(t + (size_t)b * BPK_SLOTS) + h;
+  }
+  __device__ __forceinline__ unsigned long long &slot(uint32_t b, uint32_t p) const {
+    if constexpr (SOA)
+      return t[(p >> 1) * 2 * maxBuckets + 2 * b + (p & 1)];
+    else
+      return t[(size_t)b * BPK_SLOTS + p];
+  }
+};
+
 // One batch of T x K outer words (the first `valid` of them counted) against
 // the bucketized table; returns this lane's matches.
-template <int T, int K, int H>
-__device__ __forceinline__ uint32_t ksProbeBatch(const uint64_t (&sv)[K], uint32_t valid,
-                                                 const unsigned long long *table, const uint32_t *fill, uint32_t bbits,
-                                                 uint32_t bmask) {
+template <int T, int K, int H, bool SOA>
+__device__ __forceinline__ uint32_t ksProbeBatch(const uint64_t (&sv)[K], uint32_t valid, const KsTable<SOA> &table,
+                                                 const uint32_t *fill, uint32_t bbits, uint32_t bmask) {
   uint32_t matches = 0;
 #pragma unroll
   for (int h = 0; h < K / H; ++h) {
@@ -1277,9 +1299,8 @@ __device__ __forceinline__ uint32_t ksProbeBatch(const uint64_t (&sv)[K], uint32
     for (int j = 0; j < H; ++j) {
       bk[j] = ksBucket(sv[h * H + j], bbits);
       f[j] = fill[bk[j]];
-      const ulonglong2 *q = reinterpret_cast<const ulonglong2 *>(table + bk[j] * BPK_SLOTS);
-      e0[j] = q[0];
-      e1[j] = q[1];
+      e0[j] = *table.half(bk[j], 0);
+      e1[j] = *table.half(bk[j], 1);
     }
 #pragma unroll
     for (int j = 0; j < H; ++j) {
@@ -1296,8 +1317,7 @@ __device__ __forceinline__ uint32_t ksProbeBatch(const uint64_t (&sv)[K], uint32
       while (fb > BPK_SLOTS) {
         b = (b + 1) & bmask;
         fb = fill[b];
-        const ulonglong2 *q = reinterpret_cast<const ulonglong2 *>(table + b * BPK_SLOTS);
-        const ulonglong2 x0 = q[0], x1 = q[1];
+        const ulonglong2 x0 = *table.half(b, 0), x1 = *table.half(b, 1);
         c += (uint32_t)((fb > 0) & (x0.x == v)) + (uint32_t)((fb > 1) & (x0.y == v)) +
              (uint32_t)((fb > 2) & (x1.x == v)) + (uint32_t)((fb > 3) & (x1.y == v));
       }
@@ -1307,7 +1327,7 @@ __device__ __forceinline__ uint32_t ksProbeBatch(const uint64_t (&sv)[K], uint32
   return matches;
 }
 
-template <int T, int K, int H, int MINW, bool SPLIT>
+template <int T, int K, int H, int MINW, bool SPLIT, bool SOA>
 __global__ __launch_bounds__(T, MINW) void bpKeySpanKernel(KsSrc<T, K, SPLIT> R, KsSrc<T, K, SPLIT> S,
                                                            const BPSpan *__restrict__ spans,
                                                            const uint32_t *__restrict__ nSpansPtr, uint32_t capacity,
@@ -1315,8 +1335,8 @@ __global__ __launch_bounds__(T, MINW) void bpKeySpanKernel(KsSrc<T, K, SPLIT> R,
                                                            unsigned long long *__restrict__ result) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t maxSlots = 1u << ceilLog2(2ull * maxR);
-  unsigned long long *table = reinterpret_cast<unsigned long long *>(smem);
-  uint32_t *fill = reinterpret_cast<uint32_t *>(table + maxSlots);
+  const KsTable<SOA> table{reinterpret_cast<unsigned long long *>(smem), maxSlots / BPK_SLOTS};
+  uint32_t *fill = reinterpret_cast<uint32_t *>(table.t + maxSlots);
   BPSpan *desc = reinterpret_cast<BPSpan *>(fill + maxSlots / BPK_SLOTS);
   unsigned long long *wsum = reinterpret_cast<unsigned long long *>(desc + KS_CHUNK);
   uint32_t *qbase = reinterpret_cast<uint32_t *>(wsum + T / WAVE);
@@ -1368,7 +1388,7 @@ __global__ __launch_bounds__(T, MINW) void bpKeySpanKernel(KsSrc<T, K, SPLIT> R,
             b = (b + 1) & bmask;
             p = atomicAdd(&fill[b], 1u);
           }
-          table[b * BPK_SLOTS + p] = rv[k];
+          table.slot(b, p) = rv[k];
         }
       }
       __syncthreads();
@@ -1381,11 +1401,11 @@ __global__ __launch_bounds__(T, MINW) void bpKeySpanKernel(KsSrc<T, K, SPLIT> R,
       // ---- probe: the first batch from registers (no wait on the prefetch
       // above: vmcnt is in order, so a load issued here would make the first
       // use wait for the next span's words too), later batches loaded inline.
-      matches += ksProbeBatch<T, K, H>(sv, ns, table, fill, bbits, bmask);
+      matches += ksProbeBatch<T, K, H, SOA>(sv, ns, table, fill, bbits, bmask);
       for (uint32_t b0 = BATCH; b0 < ns; b0 += BATCH) {
         uint64_t xv[K];
         S.load(sb + b0, ns - b0, xv);
-        matches += ksProbeBatch<T, K, H>(xv, ns - b0, table, fill, bbits, bmask);
+        matches += ksProbeBatch<T, K, H, SOA>(xv, ns - b0, table, fill, bbits, bmask);
       }
       __syncthreads();  // the next span clears the counters
 #pragma unroll
@@ -1416,12 +1436,17 @@ void buildProbeKeySpans(const BPArgs &a, const BPSpan *spans, const uint32_t *nS
   const uint32_t perCu = (uint32_t)std::max<size_t>(1, std::min<size_t>(4, (160 * 1024) / lds));
   const dim3 grid(std::min<uint32_t>(ceilDiv(capacity, KS_CHUNK), 256 * perCu));
   HIP_CHECK(hipMemsetAsync(queue, 0, sizeof(uint32_t), s));
-  if (a.split)
-    hipLaunchKernelGGL((bpKeySpanKernel<T, K, H, 8, true>), grid, dim3(T), lds, s, KsSrc<T, K, true>{a.R, a.Rhi},
-                       KsSrc<T, K, true>{a.S, a.Shi}, spans, nSpans, capacity, queue, a.rChunk, a.result);
-  else
-    hipLaunchKernelGGL((bpKeySpanKernel<T, K, H, 8, false>), grid, dim3(T), lds, s, KsSrc<T, K, false>{a.R, nullptr},
-                       KsSrc<T, K, false>{a.S, nullptr}, spans, nSpans, capacity, queue, a.rChunk, a.result);
+#define HJ_KS(SPLIT, SOA)                                                                                        \
+  hipLaunchKernelGGL((bpKeySpanKernel<T, K, H, 8, SPLIT, SOA>), grid, dim3(T), lds, s,                            \
+                     KsSrc<T, K, SPLIT>{a.R, SPLIT ? a.Rhi : nullptr}, KsSrc<T, K, SPLIT>{a.S, SPLIT ? a.Shi : nullptr}, \
+                     spans, nSpans, capacity, queue, a.rChunk, a.result)
+  const bool soa = a.keyCount == 7;
+  if (a.split) {
+    if (soa) HJ_KS(true, true); else HJ_KS(true, false);
+  } else {
+    if (soa) HJ_KS(false, true); else HJ_KS(false, false);
+  }
+#undef HJ_KS
   HIP_CHECK_LAUNCH();
 }
 

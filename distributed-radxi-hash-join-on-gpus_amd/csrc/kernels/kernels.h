@@ -323,7 +323,7 @@ struct BPArgs {
   uint64_t offA = 0, offB = 0;        // rid of row 0 of each column
   ulonglong2 *outRows = nullptr;
   // Kernel variants (KernelVariants::keyCount / rowsLds).
-  uint32_t keyCount = 6;
+  uint32_t keyCount = 7;
   uint32_t rowsLds = 1;
 };
 // Payload columns + output of a fused materializing join (HashJoin::setRowSink).

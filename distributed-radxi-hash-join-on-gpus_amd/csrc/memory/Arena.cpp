@@ -107,7 +107,9 @@ void Arena::reserve(uint64_t bytes) {
 uint64_t Arena::ensure(uint64_t bytes, bool touch) {
   const uint64_t have = capacity();
   if (have >= bytes) return 0;
-  addChunk(bytes - have, touch);
+  // One chunk of the whole request: first fit over the older chunks could
+  // otherwise leave a big buffer without a chunk that holds it.
+  addChunk(bytes, touch);
   return capacity() - have;
 }
 

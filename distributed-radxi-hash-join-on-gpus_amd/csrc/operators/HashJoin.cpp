@@ -167,6 +167,55 @@ void HashJoin::makeJoinPlan() {
   if (ctx->onDevice())
     for (auto &e : ev)
       if (!e) HIP_CHECK(hipEventCreate(&e));
+  if (ctx->onDevice() && config.reserveWorkspace) {
+    // Capped by what HBM has free (the estimate is generous for N > 1, where
+    // received sizes are only known after the histogram): a short estimate
+    // only means the first join falls back to hipMalloc, as without it.
+    size_t freeB = 0, totalB = 0;
+    HIP_CHECK(hipMemGetInfo(&freeB, &totalB));
+    const uint64_t want = std::min<uint64_t>(workspaceEstimate(), (uint64_t)(freeB * 0.85));
+    reserved = ctx->workspace().ensure(want, true);
+    JOIN_DEBUG("HashJoin", "workspace: estimate %.2f GB, added %.2f GB", want / 1e9, reserved / 1e9);
+  }
+}
+
+uint64_t HashJoin::workspaceEstimate() const {
+  const uint32_t N = numberOfNodes, F = 1u << plan.networkBits;
+  const uint64_t n[2] = {innerRelation->getLocalSize(), outerRelation->getLocalSize()};
+  const uint64_t g[2] = {innerRelation->getGlobalSize(), outerRelation->getGlobalSize()};
+  uint64_t b = 64ull << 20;  // plans, histograms, cursors, counters, scan scratch
+  auto sampledCap = [&](uint64_t m) {
+    const kernels::PartitionGeometry geom = kernels::partitionGeometry(m, config.maxPartitionBlocks);
+    const uint32_t stride = kernels::sampleStrideFor(geom, m, F, std::max<uint32_t>(1, config.sampleStride));
+    return kernels::sampledLayoutCapacityBound(kernels::sampleScale(geom, m, stride, false), F);
+  };
+  if (plan.bitmapJoin) {
+    for (int r = 0; r < 2; ++r) b += (sampledCap(n[r]) + 64) * 4;  // u32 fragments in claim slices
+    if (plan.bitmapReplicated) b += 2ull * F * kernels::bitmapWords(plan.bitmapBits) * 4;
+    return b;
+  }
+  const uint64_t wordB = plan.fragments ? 4 : plan.wide ? 16 : 8;
+  const uint64_t owned = N == 1 ? F : ceilDiv(F, N) + 1;
+  const uint64_t P = plan.twoLevel ? owned << plan.localBits : owned;
+  uint64_t recvTotal[2];
+  for (int r = 0; r < 2; ++r) {
+    // N > 1: the fair share plus a quarter (LPT balances partitions; skew
+    // beyond that falls back to allocation inside the first join).
+    const uint64_t recv = N == 1 ? (plan.sampledNetwork ? sampledCap(n[r]) : n[r]) : g[r] / N + g[r] / (4 * N) + (1 << 20);
+    recvTotal[r] = recv;
+    b += recv * wordB;
+    if (N > 1 && !plan.oneSided) b += n[r] * wordB;                                 // send buffer
+    if (plan.wireBits[r]) b += (n[r] + recv) * ((plan.wireBits[r] + 7) / 8) + (64ull << 10);  // wire buffers
+    if (plan.twoLevel) {
+      const uint64_t ob = plan.fragments ? 2 : plan.splitLocal ? kernels::SPLIT_BYTES : (plan.wide ? 16 : 8);
+      b += kernels::localSampledCapacityBound(recv, P, std::max<uint32_t>(1, plan.localSampleStride), 64) * ob;
+    }
+  }
+  // Build/probe work lists (items or spans, 32 B) and materialized pairs.
+  b += (2 * P + recvTotal[1] / std::max<uint32_t>(plan.sChunk, 1) + recvTotal[0] / std::max<uint32_t>(plan.rChunk, 1) +
+        2048) * 48;
+  if (plan.materialize) b += (config.outputCapacity ? config.outputCapacity : recvTotal[1] + 1024) * 16;
+  return b;
 }
 
 // Count-only single-level bitmap plans (tasks/BitmapJoin) and the N > 1 cost
@@ -185,7 +234,8 @@ void HashJoin::planBitmap() {
   const uint32_t N = numberOfNodes;
   plan.bitmapJoin = false;
   plan.bitmapReplicated = false;
-  plan.linkGBps = N > 1 ? kLinkGBpsPerPeer * (double)std::min<uint32_t>(N - 1, 7) : 0.0;
+  const double perPeer = config.linkGBpsPerPeer > 0 ? config.linkGBpsPerPeer : kDefaultLinkGBpsPerPeer;
+  plan.linkGBps = N > 1 ? perPeer * (double)std::min<uint32_t>(N - 1, 7) : 0.0;
   {
     const double share = N > 1 ? (double)(N - 1) / N : 0.0;
     const double wR = plan.wide ? 128 : (plan.wireBits[0] ? plan.wireBits[0] : 64);

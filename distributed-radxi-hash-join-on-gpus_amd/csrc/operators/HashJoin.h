@@ -54,7 +54,7 @@ struct JoinResult {
 // Achievable one-way bandwidth of one xGMI peer link (MI355X: 7 links of
 // ~153 GB/s bidirectional, ~77 GB/s each way; ~64 GB/s is what a grouped
 // RCCL send/recv reaches per peer).  Only the planner's cost model uses it.
-constexpr double kLinkGBpsPerPeer = 64.0;
+constexpr double kDefaultLinkGBpsPerPeer = 64.0;
 
 class HashJoin {
  public:
@@ -105,6 +105,15 @@ class HashJoin {
   void planBitmap();
   bool runBitmap(uint64_t t0);
   bool lowKeyBitsSkewed();
+ public:
+  // Upper estimate of the workspace bytes one run() of this plan carves from
+  // the arena (windows, send/wire buffers, local pass output, work lists).
+  uint64_t workspaceEstimate() const;
+  // Bytes the constructor added to the arena (0 if it already held the estimate).
+  uint64_t reservedBytes() const { return reserved; }
+
+ private:
+  uint64_t reserved = 0;
   void planWireCodec(const std::vector<uint64_t> &rankStats, size_t stride, uint32_t chunks);
   JoinResult runImpl();
   core::ExecContext *ctx;

@@ -137,7 +137,7 @@ void BuildProbe::execute() {
                                  "bytes");
   kernels::bpPlanCounts(args, counts, ctx->stream());
   kernels::scanExclusiveU32(counts, offsets, args.P, nItems, scanWs, ctx->stream());
-  if (args.keyOnly && (args.keyCount == 6 || args.split)) {  // the item kernels read unsplit words only
+  if (args.keyOnly && (args.keyCount >= 6 || args.split)) {  // the item kernels read unsplit words only
     // Key-only counting: resolved spans through a device work queue.
     auto *spans = ws.getArray<kernels::BPSpan>(capacity);
     uint32_t *queue = ws.getArray<uint32_t>(1);

@@ -300,7 +300,7 @@ def test_sparse64_generator(C):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", ["6", "6s", "1", "0", "2", "3", "4", "5"])
+@pytest.mark.parametrize("variant", ["6", "6s", "7", "7s", "1", "0", "2", "3", "4", "5"])
 def test_key_only_count_variants(C, variant):
     """Every key-only count kernel variant against a torch reference, with heavily repeated inner keys (Zipf over sparse
     63-bit keys: long overflow chains through the next buckets)."""
@@ -317,11 +317,14 @@ def test_key_only_count_variants(C, variant):
         S.generate(outer, 0)
         cfg = C.JoinConfig()
         cfg.key_count = int(variant[0])
-        # "6s": span kernel over the split (u32 + u16) local output; the item
-        # kernels (0-5) read unsplit 8-byte words only
-        cfg.split_local = variant == "6s"
+        # 6 / 7: span kernel (AoS / SoA buckets); "s": over the split (u32 +
+        # u16) local output; the item kernels (0-5) read unsplit words only
+        split = variant.endswith("s")
+        cfg.split_local = split
+        if split:  # 63-bit keys: the fragment above 8 + 7 radix bits fits the 48-bit split
+            cfg.network_bits, cfg.local_bits = 8, 7
         j = C.HashJoin(R, S, ctx, cfg)
-        assert j.plan.key_only and j.plan.split_local == (variant == "6s")
+        assert j.plan.key_only and j.plan.split_local == split
         exp = ref_join_count(R.to_tensor()[:, 0].cpu(), S.to_tensor()[:, 0].cpu())
         for _ in range(2):
             assert j.run()["global_matches"] == exp, (variant, G_R, theta)
