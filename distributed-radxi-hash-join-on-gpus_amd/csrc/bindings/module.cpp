@@ -518,6 +518,7 @@ py::dict resultToDict(const operators::JoinResult &r) {
   d["output_overflow"] = r.outputOverflow;
   d["rows_fused"] = r.rowsFused;
   d["split_partitions"] = r.splitPartitions;
+  d["direct_scatter"] = r.directScatter;
   d["reruns"] = r.reruns;
   d["sampled_network"] = r.sampledNetwork;
   d["network_fallbacks"] = r.networkFallbacks;

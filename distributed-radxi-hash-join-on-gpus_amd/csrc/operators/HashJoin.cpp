@@ -14,11 +14,7 @@
 #include "../performance/Timeline.h"
 #include "../performance/Trace.h"
 #include "../tasks/BitmapJoin.h"
-#include "../tasks/BuildProbe.h"
-#include "../tasks/HistogramComputation.h"
-#include "../tasks/LocalPartitioning.h"
-#include "../tasks/NetworkPartitioning.h"
-#include "../tasks/SampledNetworkPartitioning.h"
+#include "JoinStrategies.h"
 #include "../utils/Fault.h"
 #include "../utils/Hip.h"
 
@@ -382,61 +378,6 @@ JoinResult HashJoin::run() {
   }
 }
 
-// The count-only bitmap plan (tasks/BitmapJoin).  false: the inner relation
-// has a repeated key (on some rank) -- the plan falls back to the two-level
-// one for this and every later join, and runImpl continues with it.
-bool HashJoin::runBitmap(uint64_t t0) {
-  std::unique_ptr<performance::TraceRange> trace(new performance::TraceRange("bitmap_join"));
-  Measurements::startHistogramComputation();
-  utils::faultPoint("histogram");
-  Measurements::stopHistogramComputation();
-  Measurements::startNetworkPartitioning();
-  tasks::BitmapJoin bj(innerRelation, outerRelation, ctx, plan, config.maxPartitionBlocks, config.sampleStride, ev);
-  tasks::BitmapJoin::Outcome o = bj.run(bitmapExact);
-  if (o.overflow) {
-    // A sampled slice overflowed on some rank (skew the sample missed): every
-    // rank redoes the join with exact histograms, as do later joins.
-    bitmapExact = true;
-    plan.sampledNetwork = false;
-    plan.fragments = false;
-    ++result.networkFallbacks;
-    if (ctx->onDevice()) HIP_CHECK(hipEventRecord(ev[0], ctx->stream()));
-    o = bj.run(true);
-    JOIN_ASSERT(!o.overflow, "HashJoin", "exact bitmap pass overflowed");
-  }
-  Measurements::stopNetworkPartitioning();
-  if (o.dup) {
-    plan = basePlan;
-    ++result.localFallbacks;
-    JOIN_DEBUG("HashJoin", "bitmap join: repeated inner key -> %s", plan.describe().c_str());
-    return false;
-  }
-  Measurements::startLocalProcessing();
-  Measurements::stopLocalProcessing();
-  const uint64_t t4 = nowUs();
-  ctx->timeline().resolve();  // BitmapJoin synchronised all streams
-  result.bitmapJoin = true;
-  result.sampledNetwork = !bitmapExact;
-  result.localMatches = o.localMatches;
-  result.globalMatches = o.globalMatches;
-  result.buildProbeItems = 1ull << plan.networkBits;
-  result.innerReceived = innerRelation->getLocalSize();
-  result.outerReceived = outerRelation->getLocalSize();
-  result.wireBytes = o.linkBytes;
-  result.joinMs = (t4 - t0) / 1000.0;
-  result.networkMs = result.joinMs;
-  result.devNetworkMs = o.devSampleMs + o.devScatterMs;
-  result.devBuildProbeMs = o.devJoinMs;
-  Measurements::storeNetworkDetails(innerRelation->getLocalSize(), outerRelation->getLocalSize(), 1);
-  Measurements::storeBuildProbeDetails(result.innerReceived, result.outerReceived, result.buildProbeItems);
-  Measurements::storeResultTuples(result.localMatches);
-  Measurements::storeDevicePhase("DNET", result.devNetworkMs);
-  Measurements::storeDevicePhase("DBP", result.devBuildProbeMs);
-  Measurements::stopJoin();
-  RESULT_COUNTER = result.localMatches;
-  return true;
-}
-
 JoinResult HashJoin::runImpl() {
   performance::TraceRange traceJoin("hpcjoin::join");
   result = JoinResult();
@@ -447,313 +388,72 @@ JoinResult HashJoin::runImpl() {
   result.setupMs = (nowUs() - tSetup) / 1000.0;
   const bool dev = ctx->onDevice();
   if (dev) HIP_CHECK(hipSetDevice(ctx->device()));
+  JoinEnv env{ctx, config, plan, innerRelation, outerRelation, ev, numberOfNodes, nodeId};
 
   Measurements::startJoin();
   ctx->timeline().reset();
-  const uint64_t t0 = nowUs();
+  JoinRun run;
+  run.t0 = nowUs();
   if (dev) HIP_CHECK(hipEventRecord(ev[0], ctx->stream()));
-  if (plan.bitmapJoin && runBitmap(t0)) return result;
+  if (plan.bitmapJoin) {
+    if (BitmapPlan(env, bitmapExact).run(run.t0, result)) {
+      RESULT_COUNTER = result.localMatches;
+      return result;
+    }
+    plan = basePlan;  // a repeated inner key: this and every later join on the two-level plan
+    ++result.localFallbacks;
+    JOIN_DEBUG("HashJoin", "bitmap join: repeated inner key -> %s", plan.describe().c_str());
+  }
 
-  // ---------------------------------------------------------------- histogram
+  // ----------------------------------------------- histogram, windows, network
   Measurements::startHistogramComputation();
   utils::faultPoint("histogram");
-  std::unique_ptr<performance::TraceRange> trace(new performance::TraceRange("histogram"));
-  std::unique_ptr<tasks::HistogramComputation> hc;
-  std::unique_ptr<tasks::SampledNetworkPartitioning> sp;
-  std::unique_ptr<data::Window> innerOwned, outerOwned;
-  data::Window *innerWindow = nullptr, *outerWindow = nullptr;
+  run.trace.reset(new performance::TraceRange("histogram"));
   const bool sampled = plan.sampledNetwork && !sampledOverflowed;
-  uint64_t t1, t2;
-  // Local pass (created early on the single-rank sampled path, which starts
-  // the inner relation's local pass while the outer scatter still runs).
-  std::unique_ptr<tasks::LocalPartitioning> lp;
-  bool networkEventRecorded = false;
+  bool done = false;
   if (sampled) {
-    // ---------------------------------------- single-rank sampled network pass
-    sp.reset(new tasks::SampledNetworkPartitioning(innerRelation, outerRelation, ctx, plan,
-                                                   config.maxPartitionBlocks, config.sampleStride));
-    const uint64_t h0 = nowUs();
-    sp->sample();
-    if (dev) HIP_CHECK(hipEventRecord(ev[1], ctx->stream()));
-    Measurements::stopHistogramComputation();
-    Measurements::storeHistogramDetails(nowUs() - h0, innerRelation->getLocalSize(), outerRelation->getLocalSize(),
-                                        0, 0, 0);
-    t1 = nowUs();
-    Measurements::startWindowAllocation();
-    sp->layoutSide(0);
-    Measurements::stopWindowAllocation();
-    t2 = nowUs();
-    Measurements::startNetworkPartitioning();
-    trace.reset();  // roctx ranges nest: pop before the next push
-    utils::faultPoint("network");
-    trace.reset(new performance::TraceRange("network_partitioning"));
-    // Host work of each side runs while the GPU works on the other: the
-    // outer layout during the inner scatter, the inner plan and local-pass
-    // setup during the outer scatter, the outer plan during the inner local
-    // pass.
-    sp->scatterSide(0);
-    sp->layoutSide(1);
-    sp->scatterSide(1);
-    if (dev) HIP_CHECK(hipEventRecord(ev[2], ctx->stream()));
-    networkEventRecorded = true;
-    bool ok = sp->finishSide(0);
-    if (ok) {
-      lp.reset(new tasks::LocalPartitioning(sp->innerWindow(), sp->outerWindow(), ctx, plan, localOverflowed));
-      lp->partitionSide(sp->innerWindow(), 0);
-      ok = sp->finishSide(1);
-    }
-    if (ok) {
-      innerWindow = sp->innerWindow();
-      outerWindow = sp->outerWindow();
-    } else {
-      lp.reset();  // an inner local pass may be queued: harmless, its output is dropped
-      networkEventRecorded = false;
-      // A slice overflowed: the sample missed skew.  Redo this join (and all
-      // later ones) with the exact histogram path.
+    done = SampledSingleRankExchange(env, localOverflowed).exchange(run);
+    if (!done) {  // a slice overflowed (skew the sample missed): exact from now on
       sampledOverflowed = true;
       ++result.networkFallbacks;
     }
   }
-  if (!innerWindow && plan.splitHistogram && !sampled) {
-    // ------------------------ N > 1: outer histogram overlaps the inner exchange
-    hc.reset(new tasks::HistogramComputation(numberOfNodes, nodeId, innerRelation, outerRelation, ctx, plan,
-                                             config.maxPartitionBlocks));
-    hc->executeInner(config.sampleStride);
-    if (dev) HIP_CHECK(hipEventRecord(ev[1], ctx->stream()));
-    Measurements::stopHistogramComputation();
-    Measurements::storeHistogramDetails(hc->localUs, innerRelation->getLocalSize(), outerRelation->getLocalSize(),
-                                        hc->globalUs, hc->assignUs, hc->offsetUs);
-    // Split pipeline: the head all-gather is the inner relation's; the outer
-    // exact histogram's all-gather runs later on the exchange stream (HOGLOBAL
-    // Timeline span).
-    Measurements::put("HIGLOBAL", (double)hc->globalUs, "us");
-    Measurements::put("HOGLOBAL", 0, "us");
-    t1 = nowUs();
-    Measurements::startWindowAllocation();
-    auto makeWindow = [&](int r) {
-      std::unique_ptr<data::Window> w(new data::Window(
-          (r == 0 ? hc->innerOffsetMap() : hc->outerOffsetMap())->getExchangePlan(),
-          r == 0 ? hc->innerGlobal() : hc->outerGlobal(), hc->assignmentMap(), ctx, plan.wide));
-      if (plan.oneSided) w->enableOneSided();
-      if (plan.wireBits[r]) {
-        kernels::WireCodec c;
-        c.w = plan.wireBits[r];
-        c.ridBits = plan.wireRidBits[r];
-        c.keyShift = plan.keyShift;
-        w->setWireCodec(c, plan.ridBase[r]);
-      }
-      return w;
-    };
-    innerOwned = makeWindow(0);
-    innerWindow = innerOwned.get();
-    Measurements::stopWindowAllocation();
-    t2 = nowUs();
-    Measurements::startNetworkPartitioning();
-    trace.reset();  // roctx ranges nest: pop before the next push
-    utils::faultPoint("network");
-    trace.reset(new performance::TraceRange("network_partitioning"));
-    tasks::NetworkPartitioning np(nodeId, innerRelation, outerRelation, innerWindow, nullptr, hc.get(), ctx, plan);
-    np.partitionInner([&](uint32_t c) {
-      if (c == 0) hc->launchOuter(ctx->commStream());
-    });
-    hc->finishOuter();
-    outerOwned = makeWindow(1);
-    outerWindow = outerOwned.get();
-    np.partitionOuter(outerWindow);
-  }
-  if (!innerWindow) {
-    if (!sampled) {
-      hc.reset(new tasks::HistogramComputation(numberOfNodes, nodeId, innerRelation, outerRelation, ctx, plan,
-                                               config.maxPartitionBlocks));
-      hc->execute();
-      if (dev) HIP_CHECK(hipEventRecord(ev[1], ctx->stream()));
-      Measurements::stopHistogramComputation();
-      Measurements::storeHistogramDetails(hc->localUs, innerRelation->getLocalSize(), outerRelation->getLocalSize(),
-                                          hc->globalUs, hc->assignUs, hc->offsetUs);
-      t1 = nowUs();
-      Measurements::startWindowAllocation();
-    } else {
-      hc.reset(new tasks::HistogramComputation(numberOfNodes, nodeId, innerRelation, outerRelation, ctx, plan,
-                                               config.maxPartitionBlocks));
-      hc->execute();
-    }
-    innerOwned.reset(new data::Window(hc->innerOffsetMap()->getExchangePlan(), hc->innerGlobal(),
-                                      hc->assignmentMap(), ctx, plan.wide));
-    outerOwned.reset(new data::Window(hc->outerOffsetMap()->getExchangePlan(), hc->outerGlobal(),
-                                      hc->assignmentMap(), ctx, plan.wide));
-    innerWindow = innerOwned.get();
-    outerWindow = outerOwned.get();
-    if (plan.oneSided) {
-      innerWindow->enableOneSided();
-      outerWindow->enableOneSided();
-    }
-    for (int r = 0; r < 2; ++r)
-      if (plan.wireBits[r]) {
-        kernels::WireCodec c;
-        c.w = plan.wireBits[r];
-        c.ridBits = plan.wireRidBits[r];
-        c.keyShift = plan.keyShift;
-        (r == 0 ? innerWindow : outerWindow)->setWireCodec(c, plan.ridBase[r]);
-      }
-    if (!sampled) {
-      Measurements::stopWindowAllocation();
-      t2 = nowUs();
-      // ---------------------------------------------------------------- network
-      Measurements::startNetworkPartitioning();
-      trace.reset();  // roctx ranges nest: pop before the next push
-      utils::faultPoint("network");
-      trace.reset(new performance::TraceRange("network_partitioning"));
-    }
-    tasks::NetworkPartitioning np(nodeId, innerRelation, outerRelation, innerWindow, outerWindow, hc.get(), ctx,
-                                  plan);
-    np.execute();
-  }
+  if (!done && plan.splitHistogram && !sampled) done = SplitHistogramExchange(env).exchange(run);
+  if (!done) ExactExchange(env, sampled).exchange(run);
   Measurements::stopNetworkPartitioning();
   Measurements::storeNetworkDetails(innerRelation->getLocalSize(), outerRelation->getLocalSize(),
-                                    hc ? hc->innerLocal()->getChunkCount() : 1);
+                                    run.hc ? run.hc->innerLocal()->getChunkCount() : 1);
   Measurements::startWaitingForNetworkCompletion();
   // Only the inner window is awaited here (a stream wait, no host sync): the
   // outer relation's all-to-all keeps running on the exchange stream while the
   // inner relation's local radix pass runs; LocalPartitioning waits for the
   // outer window right before its own pass.
-  innerWindow->stop();
-  if (config.checks && hc) {
-    innerWindow->assertAllTuplesWritten();
-    outerWindow->assertAllTuplesWritten();
+  run.inner->stop();
+  if (config.checks && run.hc) {
+    run.inner->assertAllTuplesWritten();
+    run.outer->assertAllTuplesWritten();
   }
-  if (dev && !networkEventRecorded) HIP_CHECK(hipEventRecord(ev[2], ctx->stream()));
+  if (dev && !run.networkEventRecorded) HIP_CHECK(hipEventRecord(ev[2], ctx->stream()));
   Measurements::stopWaitingForNetworkCompletion();
-  const uint64_t t3 = nowUs();
+  run.t3 = nowUs();
 
-  // -------------------------------------------------------------------- local
-  Measurements::startLocalProcessingPreparations();
-  trace.reset();  // roctx ranges nest: pop before the next push
-  result.splitPartitions = hc ? hc->assignmentMap()->splitPartitions() : 0;
-  utils::faultPoint("local");
-  trace.reset(new performance::TraceRange("local_processing"));
-  // Every build/probe of this join (one, or one per outer chunk when pipelined).
-  std::vector<std::unique_ptr<tasks::BuildProbe>> bps;
-  std::vector<std::unique_ptr<data::Window>> outerViews;
-  {
-    if (!lp) lp.reset(new tasks::LocalPartitioning(innerWindow, outerWindow, ctx, plan, localOverflowed));
-    Measurements::stopLocalProcessingPreparations();
-    Measurements::startLocalProcessing();
-    const uint32_t outerChunks = outerWindow->getPlan().chunks;
-    if (plan.pipelineOuter && !localOverflowed && outerChunks > 1) {
-      // ---- N > 1, counting: the outer relation is local-partitioned and probed
-      // chunk by chunk as its exchange chunks land (chunk views of the window),
-      // so after the last chunk arrives only its own share is left to do.  The
-      // inner tables are rebuilt per chunk (2-byte fragments, off the critical
-      // path while later chunks are on the links).
-      lp->partitionSide(innerWindow, 0);
-      for (uint32_t c = 0; c < outerChunks; ++c) {
-        outerViews.push_back(outerWindow->chunkView(c));
-        lp->partitionSide(outerViews.back().get(), 1 + (int)c);
-        if (c + 1 == outerChunks && dev) HIP_CHECK(hipEventRecord(ev[3], ctx->stream()));
-        if (c == 0) utils::faultPoint("build_probe");
-        bps.emplace_back(new tasks::BuildProbe(innerWindow, outerViews.back().get(), ctx, plan, config.outputCapacity));
-        if (hasSink && canFuseRows()) bps.back()->setRowSink(&sink);
-        bps.back()->execute();
-      }
-      result.localItems = lp->workItems();
-    } else {
-      TASK_QUEUE.push(lp.get());
-      // Both tasks are owned here (lp is re-created if its sampled layout overflows).
-      while (!TASK_QUEUE.empty()) {
-        tasks::Task *t = TASK_QUEUE.front();
-        TASK_QUEUE.pop();
-        if (t->getType() == TASK_BUILD_PROBE) {
-          utils::faultPoint("build_probe");
-          t->execute();
-          continue;
-        }
-        t->execute();
-        if (t->getType() == TASK_PARTITION) {
-          if (dev) HIP_CHECK(hipEventRecord(ev[3], ctx->stream()));
-          result.localItems = lp->workItems();
-          bps.emplace_back(new tasks::BuildProbe(innerWindow, outerWindow, ctx, plan, config.outputCapacity));
-          if (hasSink && canFuseRows()) bps.back()->setRowSink(&sink);
-          TASK_QUEUE.push(bps.back().get());
-        }
-      }
-    }
-    trace.reset();  // roctx ranges nest: pop before the next push
-    if (dev) HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
-    ctx->synchronize();
-    result.sampledLocal = lp->sampled();
-    if (lp->sampled() && lp->overflowed()) {
-      // A sampled slot overflowed (skew the sample missed): the build/probe ran
-      // on incomplete partitions.  Redo the local pass exactly over the whole
-      // windows, then the build/probe; later joins stay exact.
-      localOverflowed = true;
-      ++result.localFallbacks;
-      result.sampledLocal = false;
-      bps.clear();
-      outerViews.clear();
-      lp.reset(new tasks::LocalPartitioning(innerWindow, outerWindow, ctx, plan, true));
-      lp->execute();
-      result.localItems = lp->workItems();
-      bps.emplace_back(new tasks::BuildProbe(innerWindow, outerWindow, ctx, plan, config.outputCapacity));
-      if (hasSink && canFuseRows()) bps.back()->setRowSink(&sink);
-      bps.back()->execute();
-      if (dev) HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
-      ctx->synchronize();
-    }
-    for (auto &bp : bps)
-      while (bp->collect()) {  // rare: item list or output buffer overflowed -> exact re-run
-        ++result.reruns;
-        bp->execute();
-        if (dev) HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
-        ctx->synchronize();
-      }
-  }
-  Measurements::stopLocalProcessing();
+  // --------------------------------------------- local pass and build/probe
+  LocalPhase local(env, localOverflowed, hasSink && canFuseRows() ? &sink : nullptr);
+  local.run(run, result);
   const uint64_t t4 = nowUs();
   ctx->timeline().resolve();  // every stream was synchronised above
-
-  result.localMatches = 0;
-  result.buildProbeItems = 0;
-  for (auto &bp : bps) {
-    result.localMatches += bp->getMatches();
-    result.buildProbeItems += bp->getWorkItems();
-  }
-  // Materializing joins have exactly one build/probe (never pipelined).
-  result.outputPairs =
-      plan.materialize && !bps.empty() ? std::min<uint64_t>(bps.front()->getOutputCount(), UINT64_MAX) : 0;
-  result.outputOverflow = !bps.empty() && bps.front()->outputOverflowed();
-  result.rowsFused = !bps.empty() && bps.front()->rowsFused();
-  output = bps.empty() ? nullptr : bps.front()->getOutput();
-  bps.clear();
-  outerViews.clear();
-  result.wireBytes = innerWindow->wireBytesSent() + outerWindow->wireBytesSent();
-  result.innerReceived = innerWindow->computeLocalWindowSize();
-  result.outerReceived = outerWindow->computeLocalWindowSize();
-  result.sampledNetwork = sampled && !sampledOverflowed;
+  output = local.buildProbes().empty() ? nullptr : local.buildProbes().front()->getOutput();
+  local.release();
+  result.wireBytes = run.inner->wireBytesSent() + run.outer->wireBytesSent();
+  result.innerReceived = run.inner->computeLocalWindowSize();
+  result.outerReceived = run.outer->computeLocalWindowSize();
+  result.sampledNetwork = run.sampled;
+  result.directScatter = run.inner->directScatter() || run.outer->directScatter();
   Measurements::storeLocalPartitioningDetails(result.innerReceived + result.outerReceived, result.localItems);
   Measurements::storeBuildProbeDetails(result.innerReceived, result.outerReceived, result.buildProbeItems);
   Measurements::storeResultTuples(result.localMatches);
   Measurements::stopJoin();
-
-  result.joinMs = (t4 - t0) / 1000.0;
-  result.histogramMs = (t1 - t0) / 1000.0;
-  result.windowMs = (t2 - t1) / 1000.0;
-  result.networkMs = (t3 - t2) / 1000.0;
-  result.localMs = (t4 - t3) / 1000.0;
-  if (dev) {
-    float ms;
-    HIP_CHECK(hipEventElapsedTime(&ms, ev[0], ev[1]));
-    result.devHistogramMs = ms;
-    HIP_CHECK(hipEventElapsedTime(&ms, ev[1], ev[2]));
-    result.devNetworkMs = ms;
-    HIP_CHECK(hipEventElapsedTime(&ms, ev[2], ev[3]));
-    result.devLocalPartitionMs = ms;
-    HIP_CHECK(hipEventElapsedTime(&ms, ev[3], ev[4]));
-    result.devBuildProbeMs = ms;
-    Measurements::storeDevicePhase("DHIST", result.devHistogramMs);
-    Measurements::storeDevicePhase("DNET", result.devNetworkMs);
-    Measurements::storeDevicePhase("DLOCPART", result.devLocalPartitionMs);
-    Measurements::storeDevicePhase("DBP", result.devBuildProbeMs);
-  }
+  recordTimes(run, t4);
 
   uint64_t g = result.localMatches;
   ctx->comm()->allReduceSumHost(&g, 1);
@@ -761,6 +461,29 @@ JoinResult HashJoin::runImpl() {
   result.teardownMs = (nowUs() - t4) / 1000.0;
   RESULT_COUNTER = result.localMatches;
   return result;
+}
+
+// Host phase spans and the device spans between the join's five events.
+void HashJoin::recordTimes(const JoinRun &run, uint64_t t4) {
+  result.joinMs = (t4 - run.t0) / 1000.0;
+  result.histogramMs = (run.t1 - run.t0) / 1000.0;
+  result.windowMs = (run.t2 - run.t1) / 1000.0;
+  result.networkMs = (run.t3 - run.t2) / 1000.0;
+  result.localMs = (t4 - run.t3) / 1000.0;
+  if (!ctx->onDevice()) return;
+  float ms;
+  HIP_CHECK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+  result.devHistogramMs = ms;
+  HIP_CHECK(hipEventElapsedTime(&ms, ev[1], ev[2]));
+  result.devNetworkMs = ms;
+  HIP_CHECK(hipEventElapsedTime(&ms, ev[2], ev[3]));
+  result.devLocalPartitionMs = ms;
+  HIP_CHECK(hipEventElapsedTime(&ms, ev[3], ev[4]));
+  result.devBuildProbeMs = ms;
+  Measurements::storeDevicePhase("DHIST", result.devHistogramMs);
+  Measurements::storeDevicePhase("DNET", result.devNetworkMs);
+  Measurements::storeDevicePhase("DLOCPART", result.devLocalPartitionMs);
+  Measurements::storeDevicePhase("DBP", result.devBuildProbeMs);
 }
 
 }  // namespace operators

@@ -27,6 +27,7 @@ namespace data {
 class Window;
 }
 namespace operators {
+struct JoinRun;
 
 struct JoinResult {
   uint64_t localMatches = 0;
@@ -49,6 +50,9 @@ struct JoinResult {
   bool bitmapJoin = false;         // single-level bitmap join counted the matches (no local pass)
   uint32_t localFallbacks = 0;     // sampled local pass overflowed -> exact re-run
   uint32_t splitPartitions = 0;    // hot network partitions joined by several ranks (AssignmentMap)
+  bool directScatter = false;      // one-sided windows: the scatter kernel wrote into the owners' windows
+                                   // (false with ExchangeMode::OneSided = staged send buffer + peer copies,
+                                   // e.g. when a split hot partition adds replicas)
 };
 
 // Achievable one-way bandwidth of one xGMI peer link (MI355X: 7 links of
@@ -103,7 +107,7 @@ class HashJoin {
  private:
   void makeJoinPlan();
   void planBitmap();
-  bool runBitmap(uint64_t t0);
+  void recordTimes(const JoinRun &run, uint64_t t4);
   bool lowKeyBitsSkewed();
  public:
   // Upper estimate of the workspace bytes one run() of this plan carves from
