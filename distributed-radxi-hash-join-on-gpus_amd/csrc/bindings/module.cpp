@@ -889,6 +889,22 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                std::memcpy(out.data_ptr(), rel->getData(), rel->getLocalSize() * 16);
              return out;
            })
+      .def("count_keys",
+           [](PyRelation &r, at::Tensor counts, uint64_t lo) {
+             // Oracle of skewed joins: counts (int32, zeroed, on the relation's
+             // device) += one per key in [lo, lo + counts.numel()); returns the
+             // number of keys outside that range.
+             const auto &rel = r.rel;
+             TORCH_CHECK(rel->location() == Location::Device && counts.is_cuda(), "count_keys: device relations");
+             TORCH_CHECK(counts.scalar_type() == at::kInt && counts.is_contiguous(), "count_keys: contiguous int32");
+             at::Tensor out = at::zeros({1}, at::TensorOptions().dtype(at::kLong).device(counts.device()));
+             kernels::countKeys(rel->getData(), rel->getLocalSize(), lo, (uint64_t)counts.numel(),
+                                reinterpret_cast<uint32_t *>(counts.data_ptr()),
+                                reinterpret_cast<unsigned long long *>(out.data_ptr()), nullptr);
+             HIP_CHECK(hipDeviceSynchronize());
+             return out.item<int64_t>();
+           },
+           py::arg("counts"), py::arg("lo") = 0)
       .def_static("local_size_for", &data::Relation::localSizeFor)
       .def_static("local_offset_for", &data::Relation::localOffsetFor)
       .def_static("expected_matches", [](const data::GenSpec &i, uint64_t gi, const data::GenSpec &o, uint64_t go) {

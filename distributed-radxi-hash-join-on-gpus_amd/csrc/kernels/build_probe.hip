@@ -63,6 +63,8 @@ static bool bpDirect(const BPArgs &a) {
   return bpMode(a) == BP_CCOUNT && a.fragBits > 0 && a.fragBits <= BP_DIRECT_MAX_BITS;
 }
 
+bool bpDirectSplit(const BPArgs &a) { return bpDirect(a) && a.split && !a.itemCounts; }
+
 size_t bpLdsBytes(const BPArgs &a) {
   if (bpDirect(a)) return (size_t(4) << a.fragBits) + 64;
   const uint64_t slots = uint64_t(1) << ceilLog2(2ull * a.rChunk);

@@ -48,6 +48,34 @@ __global__ __launch_bounds__(256) void generateKernel(ulonglong2 *__restrict__ o
   }
 }
 
+// Oracle support for skewed joins (no closed form for Zipf x Zipf):
+// counts[key - lo] += 1 for keys in [lo, lo + domain), *outside += the rest.
+// Global atomics (u32 counts, memory-side adds); the match count is then
+// sum_k countsR[k] * countsS[k], computed independently of the join.
+__global__ __launch_bounds__(256) void countKeysKernel(const ulonglong2 *__restrict__ in, uint64_t n, uint64_t lo,
+                                                       uint64_t domain, uint32_t *__restrict__ counts,
+                                                       unsigned long long *__restrict__ outside) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint32_t miss = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t k = in[i].x - lo;
+    if (k < domain)
+      atomicAdd(&counts[k], 1u);
+    else
+      ++miss;
+  }
+  if (miss) atomicAdd(outside, (unsigned long long)miss);
+}
+
+void countKeys(const data::Tuple *in, uint64_t n, uint64_t lo, uint64_t domain, uint32_t *counts,
+               unsigned long long *outside, hipStream_t s) {
+  if (n == 0) return;
+  const uint64_t want = ceilDiv(n, 256);
+  hipLaunchKernelGGL(countKeysKernel, dim3((uint32_t)(want < 16384 ? want : 16384)), dim3(256), 0, s,
+                     reinterpret_cast<const ulonglong2 *>(in), n, lo, domain, counts, outside);
+  HIP_CHECK_LAUNCH();
+}
+
 void generate(data::Tuple *out, uint64_t n, const GenParams &p, hipStream_t s) {
   if (n == 0) return;
   const uint32_t threads = 256;

@@ -59,6 +59,10 @@ struct GenParams {
 };
 HJ_HD uint64_t tpchSparseKey(uint64_t k) { return (k >> 3) * 32 + (k & 7) + 1; }
 void generate(data::Tuple *out, uint64_t n, const GenParams &p, hipStream_t s);
+// Oracle of skewed joins: counts[key - lo] += 1 for keys in [lo, lo + domain)
+// (u32 counts, zeroed by the caller); *outside += keys outside that range.
+void countKeys(const data::Tuple *in, uint64_t n, uint64_t lo, uint64_t domain, uint32_t *counts,
+               unsigned long long *outside, hipStream_t s);
 
 // ------------------------------------------------- pass 1: network partition
 // Hash partitioning for keys whose low bits are structured (sparse TPC-H
@@ -338,6 +342,11 @@ struct RowSink {
   uint64_t capacity = 0;
 };
 size_t bpLdsBytes(const BPArgs &a);
+// True when a count over the split layout uses the direct-addressed count
+// table (fragments <= 13 bits): its LDS table does not grow with the inner
+// side, so a work item may take any number of inner tuples.
+bool bpDirectSplit(const BPArgs &a);
+constexpr uint32_t BP_DIRECT_R_CHUNK = 1u << 18;
 void bpPlanCounts(const BPArgs &a, uint32_t *counts, hipStream_t s);
 void bpEmit(const BPArgs &a, const uint32_t *counts, const uint32_t *offsets, BPItem *items,
             uint32_t capacity, hipStream_t s);

@@ -84,13 +84,15 @@ uint64_t Arena::used() const {
   return s;
 }
 
-void Arena::addChunk(uint64_t bytes, bool touch) {
+void Arena::addChunk(uint64_t bytes, bool touch, void *stream) {
   bytes = ceilDiv(std::max<uint64_t>(bytes, ALIGNMENT), BIG_ALIGNMENT) * BIG_ALIGNMENT;
   uint8_t *p = static_cast<uint8_t *>(rawAlloc(loc_, bytes, device_));
   if (touch) {
     if (loc_ == Location::Device) {
       HIP_CHECK(hipSetDevice(device_));
-      HIP_CHECK(hipMemset(p, 0, bytes));
+      const hipStream_t s = static_cast<hipStream_t>(stream);
+      HIP_CHECK(hipMemsetAsync(p, 0, bytes, s));
+      HIP_CHECK(hipStreamSynchronize(s));
     } else {
       std::memset(p, 0, bytes);
     }
@@ -104,12 +106,12 @@ void Arena::reserve(uint64_t bytes) {
   if (bytes) addChunk(bytes, false);
 }
 
-uint64_t Arena::ensure(uint64_t bytes, bool touch) {
+uint64_t Arena::ensure(uint64_t bytes, bool touch, void *stream) {
   const uint64_t have = capacity();
   if (have >= bytes) return 0;
   // One chunk of the whole request: first fit over the older chunks could
   // otherwise leave a big buffer without a chunk that holds it.
-  addChunk(bytes, touch);
+  addChunk(bytes, touch, stream);
   return capacity() - have;
 }
 

@@ -40,9 +40,11 @@ class Arena {
 
   void reserve(uint64_t bytes);       // one chunk of `bytes` (frees everything first)
   // Grow (never shrink, never move) so that the chunks hold >= bytes in all;
-  // touch = write the new chunk once (device: a memset) so its pages are
-  // mapped before the first join uses them.  Returns the bytes added.
-  uint64_t ensure(uint64_t bytes, bool touch = false);
+  // touch = write the new chunk once (device: a memset ordered on `stream`,
+  // then waited for -- the engine's streams are non-blocking, so a null-stream
+  // memset could land after a join's first writes) so its pages are mapped
+  // before the first join uses them.  Returns the bytes added.
+  uint64_t ensure(uint64_t bytes, bool touch = false, void *stream = nullptr);
   void *get(uint64_t bytes);          // bump-allocate (fallback allocation when exhausted)
   template <typename T>
   T *getArray(uint64_t count) { return reinterpret_cast<T *>(get(count * sizeof(T))); }
@@ -71,7 +73,7 @@ class Arena {
     uint64_t cap;
     uint64_t used;
   };
-  void addChunk(uint64_t bytes, bool touch);
+  void addChunk(uint64_t bytes, bool touch, void *stream = nullptr);
   Location loc_;
   int device_;
   std::vector<Chunk> chunks_;

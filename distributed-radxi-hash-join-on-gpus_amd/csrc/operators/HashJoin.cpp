@@ -170,7 +170,7 @@ void HashJoin::makeJoinPlan() {
     size_t freeB = 0, totalB = 0;
     HIP_CHECK(hipMemGetInfo(&freeB, &totalB));
     const uint64_t want = std::min<uint64_t>(workspaceEstimate(), (uint64_t)(freeB * 0.85));
-    reserved = ctx->workspace().ensure(want, true);
+    reserved = ctx->workspace().ensure(want, true, ctx->stream());
     JOIN_DEBUG("HashJoin", "workspace: estimate %.2f GB, added %.2f GB", want / 1e9, reserved / 1e9);
   }
 }

@@ -69,6 +69,13 @@ void BuildProbe::configure() {
     args.Rhi = wi->getPartitionedHi();
     args.Shi = wo->getPartitionedHi();
   }
+  // Direct-addressed counting: duplicate-heavy inner partitions (Zipf) need
+  // no inner chunking into rChunk-sized tables -- each work item counts up to
+  // 2^18 inner tuples into its count table and probes its outer chunk, so a
+  // hot partition costs (inner / 2^18) passes over its outer side instead of
+  // (inner / rChunk).
+  if (ctx && ctx->onDevice() && kernels::bpDirectSplit(args))
+    args.rChunk = std::max<uint32_t>(args.rChunk, kernels::BP_DIRECT_R_CHUNK);
   if (capacity == 0)
     capacity = (uint32_t)std::min<uint64_t>(
         0xFFFFFFF0ull, 2ull * args.P + outerPartitionSize / args.sChunk + innerPartitionSize / args.rChunk + 1024);
