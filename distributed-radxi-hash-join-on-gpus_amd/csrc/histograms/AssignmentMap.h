@@ -37,6 +37,10 @@ class AssignmentMap {
   // (each tuple of the divided side meets the whole other side on exactly one
   // rank).  Every rank derives the same map from the same histograms.
   void setSkewSplit(bool on) { split = on; }
+  // Exchange chunks per rank: a divided side travels as numberOfNodes x
+  // chunks pieces (source rank, chunk), so helper counts that divide it give
+  // every helper the same share.
+  void setPieces(uint32_t chunksPerRank) { chunks = chunksPerRank ? chunksPerRank : 1; }
   bool isSplit(uint32_t p) const { return p < helpers.size() && !helpers[p].empty(); }
   const std::vector<uint32_t> &helpersOf(uint32_t p) const { return helpers.at(p); }
   int splitSideOf(uint32_t p) const { return splitSide.at(p); }  // 0 inner, 1 outer: the divided side
@@ -58,6 +62,7 @@ class AssignmentMap {
   core::AssignmentPolicy pol;
   std::vector<uint64_t> loads;
   bool split = false;
+  uint32_t chunks = 1;
   uint32_t nSplit = 0;
   std::vector<std::vector<uint32_t>> helpers;  // [F]: empty unless split
   std::vector<uint8_t> splitSide;             // [F]

@@ -28,6 +28,7 @@ HistogramComputation::HistogramComputation(uint32_t numberOfNodes, uint32_t node
   assignment.reset(new histograms::AssignmentMap(numberOfNodes, innerRelationGlobalHistogram.get(),
                                                  outerRelationGlobalHistogram.get(), plan.assignment));
   assignment->setSkewSplit(plan.skewSplit);
+  assignment->setPieces(std::max<uint32_t>(1, plan.chunks));
   innerOffsets.reset(new histograms::OffsetMap(numberOfNodes, nodeId, innerRelationLocalHistogram.get(),
                                                innerRelationGlobalHistogram.get(), assignment.get()));
   outerOffsets.reset(new histograms::OffsetMap(numberOfNodes, nodeId, outerRelationLocalHistogram.get(),
