@@ -121,9 +121,9 @@ def link_prediction(info, plan, results):
 
 def rccl_debug_env(info):
     """Ask RCCL to log its transport choices to a per-rank file (not stdout:
-    rank 0 prints one JSON line), unless the caller configured RCCL logging.
-    Must run before any RCCL communicator exists."""
-    if info.world <= 1 or "NCCL_DEBUG" in os.environ:
+    rank 0 prints one JSON line; this overrides an inherited NCCL_DEBUG level,
+    HPCJOIN_RCCL_LOG=0 keeps it).  Must run before any RCCL communicator exists."""
+    if info.world <= 1 or os.environ.get("HPCJOIN_RCCL_LOG") == "0":
         return None
     import tempfile
     path = os.path.join(tempfile.gettempdir(), f"hpcjoin_rccl.{os.getpid()}.log")

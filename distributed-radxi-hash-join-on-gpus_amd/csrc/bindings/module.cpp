@@ -556,6 +556,18 @@ struct PyRelation {
 
 // Payload columns must hold a row for every rid of this rank's relation
 // slices: the gather kernels index rows by rid - offset on the device.
+static py::dict statsToDict(const operators::LateMaterialization::Stats &st) {
+  py::dict d;
+  d["bucket_ms"] = st.bucketMs;
+  d["request_ms"] = st.requestMs;
+  d["gather_ms"] = st.gatherMs;
+  d["response_ms"] = st.responseMs;
+  d["place_ms"] = st.placeMs;
+  d["request_bytes"] = st.requestBytes;
+  d["response_bytes"] = st.responseBytes;
+  return d;
+}
+
 static void checkPayloadCover(const operators::HashJoin &j, const at::Tensor &a, uint64_t offA, const at::Tensor &b,
                               uint64_t offB) {
   const uint64_t off[2] = {offA, offB}, rows[2] = {(uint64_t)a.size(0), (uint64_t)b.size(0)};
@@ -939,8 +951,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def(
           "materialize_payloads",
           [](operators::HashJoin &j, std::shared_ptr<core::ExecContext> ctx, at::Tensor innerRows, uint64_t innerOffset,
-             uint64_t innerGlobal, at::Tensor outerRows, uint64_t outerOffset, uint64_t outerGlobal) {
-            // Collective.  Returns [pairs, 10] int64: rid_inner, rid_outer, inner row (4), outer row (4).
+             uint64_t innerGlobal, at::Tensor outerRows, uint64_t outerOffset, uint64_t outerGlobal,
+             bool returnStats) -> py::object {
+            // Collective.  Returns [pairs, 10] int64: rid_inner, rid_outer, inner row (4), outer row (4)
+            // (return_stats: (rows, phase times and link bytes of the request/response exchange)).
             TORCH_CHECK(j.getConfig().materialize, "join was not run with materialize=True");
             TORCH_CHECK(!j.lastResult().rowsFused, "the last run wrote rows directly (join_materialized)");
             TORCH_CHECK(innerRows.dim() == 2 && innerRows.size(1) == (int64_t)kernels::ROW_WORDS &&
@@ -953,15 +967,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
             at::Tensor out = at::empty({(int64_t)n, (int64_t)operators::LateMaterialization::OUT_WORDS},
                                        at::TensorOptions().dtype(at::kLong).device(innerRows.device()));
             if (innerRows.is_cuda()) HIP_CHECK(hipDeviceSynchronize());
+            operators::LateMaterialization::Stats st;
             {
               py::gil_scoped_release nogil;
               operators::LateMaterialization lm(ctx.get(), a, b, j.getConfig().variants.matVariant);
               lm.materialize(j.getOutput(), n, ptr<uint64_t>(out));
+              st = lm.stats();
             }
-            return out;
+            if (returnStats) return py::make_tuple(out, statsToDict(st));
+            return py::cast(out);
           },
           py::arg("context"), py::arg("inner_rows"), py::arg("inner_rid_offset"), py::arg("inner_global_rows"),
-          py::arg("outer_rows"), py::arg("outer_rid_offset"), py::arg("outer_global_rows"))
+          py::arg("outer_rows"), py::arg("outer_rid_offset"), py::arg("outer_global_rows"),
+          py::arg("return_stats") = false)
       .def_property_readonly("can_fuse_rows", &operators::HashJoin::canFuseRows)
       .def(
           "join_materialized",
@@ -1018,12 +1036,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
             operators::PayloadColumn b{ptr<uint64_t>(outerRows), (uint64_t)outerRows.size(0), outerOffset, outerGlobal};
             const uint64_t n = r.outputPairs;
             at::Tensor out = at::empty({(int64_t)n, W}, opts);
+            operators::LateMaterialization::Stats st;
             {
               py::gil_scoped_release nogil;
               operators::LateMaterialization lm(ctx.get(), a, b, j.getConfig().variants.matVariant);
               lm.materialize(j.getOutput(), n, ptr<uint64_t>(out));
+              st = lm.stats();
             }
-            return py::make_tuple(resultToDict(r), out);
+            py::dict d = resultToDict(r);
+            d["materialize_phases"] = statsToDict(st);
+            return py::make_tuple(d, out);
           },
           py::arg("context"), py::arg("inner_rows"), py::arg("inner_rid_offset"), py::arg("inner_global_rows"),
           py::arg("outer_rows"), py::arg("outer_rid_offset"), py::arg("outer_global_rows"))

@@ -1,5 +1,7 @@
 #include "LateMaterialization.h"
 
+#include "../performance/Clock.h"
+
 #include <algorithm>
 #include <cstring>
 #include <vector>
@@ -74,6 +76,13 @@ void LateMaterialization::fetchDevice(const ulonglong2 *pairs, uint64_t n, int s
     return;
   }
   // Bucket requests by owner with the LDS radix kernels (digit = owner).
+  uint64_t tp = performance::nowUs();
+  auto lap = [&](double &acc) {
+    HIP_CHECK(hipStreamSynchronize(s));
+    const uint64_t now = performance::nowUs();
+    acc += (now - tp) / 1000.0;
+    tp = now;
+  };
   const uint32_t bits = std::max<uint32_t>(1, ceilLog2(N)), F = 1u << bits;
   const kernels::PartitionGeometry g = kernels::partitionGeometry(n);
   uint32_t *blockHist = ws.getArray<uint32_t>((uint64_t)F * g.blocks);
@@ -108,8 +117,14 @@ void LateMaterialization::fetchDevice(const ulonglong2 *pairs, uint64_t n, int s
     if (r) sd[r] = sd[r - 1] + sendCounts[r - 1];
   }
   uint64_t *recvRids = ws.getArray<uint64_t>(std::max<uint64_t>(m, 1));
-  HIP_CHECK(hipStreamSynchronize(s));
+  lap(st.bucketMs);
   c->allToAllV(rids, sendCounts.data(), sd.data(), recvRids, recvCounts.data(), rd.data(), Location::Device, s);
+  lap(st.requestMs);
+  for (uint32_t r = 0; r < N; ++r)
+    if (r != me) {
+      st.requestBytes += sendCounts[r] * 8;
+      st.responseBytes += recvCounts[r] * ROW_WORDS * 8;
+    }
   // serve
   uint64_t *resp = ws.getArray<uint64_t>(std::max<uint64_t>(m, 1) * ROW_WORDS);
   kernels::gatherRows(recvRids, m, col.ridOffset, col.rows, resp, s);
@@ -122,9 +137,11 @@ void LateMaterialization::fetchDevice(const ulonglong2 *pairs, uint64_t n, int s
     brd[r] = sd[r] * ROW_WORDS;
   }
   uint64_t *rowsBack = ws.getArray<uint64_t>(std::max<uint64_t>(n, 1) * ROW_WORDS);
-  HIP_CHECK(hipStreamSynchronize(s));
+  lap(st.gatherMs);
   c->allToAllV(resp, bsc.data(), bsd.data(), rowsBack, brc.data(), brd.data(), Location::Device, s);
+  lap(st.responseMs);
   kernels::placeRows(rowsBack, idx, n, out, OUT_WORDS, col0, s);
+  lap(st.placeMs);
 }
 
 void LateMaterialization::fetchHost(const ulonglong2 *pairs, uint64_t n, int side, const PayloadColumn &col,

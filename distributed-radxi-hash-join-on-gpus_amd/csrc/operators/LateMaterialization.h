@@ -27,6 +27,17 @@ struct PayloadColumn {
 class LateMaterialization {
  public:
   static constexpr uint32_t OUT_WORDS = 2 + 2 * 4;  // rid_inner, rid_outer, inner row, outer row
+  // Host-clock phase times (both sides summed; each phase ends at a stream
+  // synchronisation) and the bytes this rank put on its links.
+  struct Stats {
+    double bucketMs = 0;    // requests bucketed by owner rank (LDS radix kernels)
+    double requestMs = 0;   // all-to-allv of the requested rids
+    double gatherMs = 0;    // owner-side row gather
+    double responseMs = 0;  // all-to-allv of the rows back
+    double placeMs = 0;     // rows placed next to their pairs
+    uint64_t requestBytes = 0, responseBytes = 0;  // to other ranks
+  };
+  const Stats &stats() const { return st; }
 
   // matVariant: KernelVariants::matVariant of the single-rank gather kernel.
   LateMaterialization(core::ExecContext *ctx, const PayloadColumn &inner, const PayloadColumn &outer,
@@ -40,6 +51,7 @@ class LateMaterialization {
   core::ExecContext *ctx;
   PayloadColumn cols[2];
   uint32_t matVariant = 1;
+  Stats st;
 };
 
 }  // namespace operators

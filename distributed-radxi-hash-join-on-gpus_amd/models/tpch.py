@@ -68,12 +68,14 @@ class TpchJoin:
         t0 = time.perf_counter()
         res = self.engine.run()
         t1 = time.perf_counter()
-        out = self.engine.materialize_payloads(self.ctx, self.o_rows, self.o_off, self.workload.inner_size,
-                                               self.l_rows, self.l_off, self.workload.outer_size)
+        out, phases = self.engine.materialize_payloads(self.ctx, self.o_rows, self.o_off, self.workload.inner_size,
+                                                       self.l_rows, self.l_off, self.workload.outer_size,
+                                                       return_stats=True)
         if self.location == "device":
             torch.cuda.synchronize()
         t2 = time.perf_counter()
-        res = dict(res, join_wall_ms=(t1 - t0) * 1e3, materialize_ms=(t2 - t1) * 1e3, total_ms=(t2 - t0) * 1e3)
+        res = dict(res, join_wall_ms=(t1 - t0) * 1e3, materialize_ms=(t2 - t1) * 1e3, total_ms=(t2 - t0) * 1e3,
+                   materialize_phases=phases)
         return res, out
 
 

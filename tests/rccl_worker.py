@@ -92,6 +92,22 @@ def main():
         if info.rank == 0:
             print(f"{name}: {res['global_matches']} == {exp}, plan {j.plan}", flush=True)
         del j, S
+    # TPC-H-like join + late materialization of 32-byte payload rows across
+    # ranks (BASELINE config 5 at SF 0.5): pairs from the build/probe, rows
+    # fetched from their owner ranks by the request/response all-to-allv.
+    from hpcjoin.models import workloads as W
+    from hpcjoin.models.tpch import TpchJoin, verify_sample
+    wl = W.get("tpch_sf1000").scaled(0.0005)
+    t = TpchJoin(wl, info=info, communicator=comm)
+    for _ in range(2):
+        res, rows = t.run()
+        assert res["global_matches"] == wl.expected_matches(), ("tpch", res["global_matches"])
+        assert rows.shape[0] == res["local_matches"] and verify_sample(rows, 64), "tpch rows"
+        ph = res.get("materialize_phases")
+        assert ph is not None and ph["request_bytes"] > 0 and ph["response_bytes"] > 0, ph
+    if info.rank == 0:
+        print(f"tpch: {res['global_matches']} pairs, rows verified, phases {ph}", flush=True)
+    del t, rows
     torch.cuda.synchronize()
     comm.barrier()
     if info.rank == 0:

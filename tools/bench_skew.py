@@ -30,7 +30,8 @@ sys.path.insert(0, ROOT)
 
 
 def spawn_if_needed():
-    """Without a launcher and with --gpus N > 1: N rank processes (torchrun env)."""
+    """Without a launcher and with --gpus N > 1: N rank processes of the
+    running script (torchrun env); exits with their status."""
     if "WORLD_SIZE" in os.environ:
         return
     ap = argparse.ArgumentParser(add_help=False)
@@ -42,7 +43,7 @@ def spawn_if_needed():
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n))
-    procs = [subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *sys.argv[1:]],
+    procs = [subprocess.Popen([sys.executable, "-u", os.path.abspath(sys.argv[0]), *sys.argv[1:]],
                               env=dict(base, RANK=str(r), LOCAL_RANK=str(r)), start_new_session=True) for r in range(n)]
     rc = 0
     while procs:
