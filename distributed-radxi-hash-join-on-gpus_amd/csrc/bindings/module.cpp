@@ -658,6 +658,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       // KernelVariants, flattened (sweeps / A-B tests; core/Types.h)
       .def_property("net_ipt", [](const core::JoinConfig &c) { return c.variants.netIpt; },
                     [](core::JoinConfig &c, uint32_t v) { c.variants.netIpt = v; })
+      .def_property("net_threads", [](const core::JoinConfig &c) { return c.variants.netThreads; },
+                    [](core::JoinConfig &c, uint32_t v) { c.variants.netThreads = v; })
       .def_property("bm_threads", [](const core::JoinConfig &c) { return c.variants.bmThreads; },
                     [](core::JoinConfig &c, uint32_t v) { c.variants.bmThreads = v; })
       .def_property("bm_flat", [](const core::JoinConfig &c) { return c.variants.bmFlat; },

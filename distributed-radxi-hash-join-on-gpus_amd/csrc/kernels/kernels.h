@@ -34,6 +34,7 @@ struct PartitionGeometry {
   uint32_t blocks = 0;         // workgroups of the pass (each owns a contiguous tile range)
   uint32_t tilesPerBlock = 0;  // tiles per workgroup
   uint32_t ipt = 0;            // claim-scatter tile variant (KernelVariants::netIpt; 0 = auto)
+  uint32_t nth = 0;            // claim-scatter workgroup width (KernelVariants::netThreads; 0 = 1024)
   uint64_t tuplesPerBlock() const { return uint64_t(tilesPerBlock) * PART_TILE; }
 };
 // Cap the grid at ~8 workgroups per CU (2048) and give each workgroup a

@@ -716,11 +716,11 @@ static bool digitFitsOnTop(uint32_t bits, uint32_t keyShift, uint32_t keyBits) {
 // Production geometry of the claim-mode scatter (tools/microbench.py
 // ablation on MI355X: 1024 threads x 8 tuples per LDS tile = 8192-tuple
 // tiles, one workgroup per CU).
-constexpr int CL_NTH = 1024;
+constexpr int CL_NTH = 1024;  // production width (the local pass and the default network pass)
 constexpr int CL_IPT_DEFAULT = 8;
 constexpr int CL_IPT = CL_IPT_DEFAULT;
 
-template <class Pol, int CL_IPT>
+template <class Pol, int CL_IPT, int CL_NTH = 1024>
 static void launchNetClaimIpt(const Pol &pol, const data::Tuple *in, uint64_t n, uint32_t bits,
                               const PartitionGeometry &g, uint32_t blockBegin, uint32_t blockEnd, void *gcur,
                               void *out, hipStream_t s, const void *gend, bool narrow) {
@@ -763,6 +763,20 @@ template <class Pol>
 static void launchNetClaim(const Pol &pol, const data::Tuple *in, uint64_t n, uint32_t bits,
                            const PartitionGeometry &g, uint32_t blockBegin, uint32_t blockEnd, void *gcur,
                            void *out, hipStream_t s, const void *gend, bool narrow) {
+  // PartitionGeometry::nth = 512 (KernelVariants::netThreads): half-width
+  // workgroups with the same per-thread tile, so two or three share a CU and
+  // one's rank/scan/claim phases overlap another's loads and stores.
+  if (g.nth == 512) {
+    if constexpr (sizeof(typename Pol::StageT) == 4) {
+      if (g.ipt == 0 || g.ipt == 16) {
+        launchNetClaimIpt<Pol, 16, 512>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
+        return;
+      }
+    }
+    launchNetClaimIpt<Pol, CL_IPT_DEFAULT, 512>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend,
+                                                narrow);
+    return;
+  }
   if constexpr (sizeof(typename Pol::StageT) == 4) {
     if (g.ipt == 0 || g.ipt == 16) {
       launchNetClaimIpt<Pol, 16>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);

@@ -41,22 +41,23 @@ BitmapJoin::Outcome BitmapJoin::run(bool exact) { return ctx->onDevice() ? runDe
 const BitmapJoin::SidePlan &BitmapJoin::sidePlan(uint64_t n, bool exact, uint32_t stride) const {
   struct Key {
     uint64_t n;
-    uint32_t maxBlocks, bits, stride, ipt;
+    uint32_t maxBlocks, bits, stride, ipt, nth;
     bool exact;
     bool operator<(const Key &o) const {
-      return std::tie(n, maxBlocks, bits, stride, ipt, exact) <
-             std::tie(o.n, o.maxBlocks, o.bits, o.stride, o.ipt, o.exact);
+      return std::tie(n, maxBlocks, bits, stride, ipt, nth, exact) <
+             std::tie(o.n, o.maxBlocks, o.bits, o.stride, o.ipt, o.nth, o.exact);
     }
   };
   thread_local std::map<Key, SidePlan> cache;
   const uint32_t F = 1u << plan.networkBits;
-  const Key k{n, maxBlocks, plan.networkBits, stride, plan.variants.netIpt, exact};
+  const Key k{n, maxBlocks, plan.networkBits, stride, plan.variants.netIpt, plan.variants.netThreads, exact};
   auto it = cache.find(k);
   if (it != cache.end()) return it->second;
   if (cache.size() > 64) cache.clear();
   SidePlan sp;
   sp.geom = kernels::partitionGeometry(n, maxBlocks);
   sp.geom.ipt = plan.variants.netIpt;
+  sp.geom.nth = plan.variants.netThreads;
   sp.stride = exact ? 1 : kernels::sampleStrideFor(sp.geom, n, F, stride);
   sp.sc = kernels::sampleScale(sp.geom, n, sp.stride, exact);
   sp.cap = kernels::sampledLayoutCapacityBound(sp.sc, F);

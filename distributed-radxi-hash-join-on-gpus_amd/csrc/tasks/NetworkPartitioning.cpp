@@ -46,6 +46,7 @@ void NetworkPartitioning::partition(data::Relation *relation, data::Window *wind
   const uint32_t bits = plan.networkBits, F = 1u << bits;
   kernels::PartitionGeometry g = local->geometry();
   g.ipt = plan.variants.netIpt;
+  g.nth = plan.variants.netThreads;
   const uint32_t bpc = local->blocksPerChunk(), chunks = local->getChunkCount();
   const bool single = xp.numberOfNodes == 1;
   const uint32_t tb = window->tupleBytes();

@@ -33,6 +33,7 @@ void SampledNetworkPartitioning::sample() {
     const uint64_t n = s.relation->getLocalSize();
     s.geom = kernels::partitionGeometry(n, maxBlocks);
     s.geom.ipt = plan.variants.netIpt;
+    s.geom.nth = plan.variants.netThreads;
     s.stride = kernels::sampleStrideFor(s.geom, n, F, sampleStride);
     s.groupTotalsDev = ctx->workspace().getArray<uint64_t>((uint64_t)CLAIM_GROUPS * F);
     if (s.stride > 1) {

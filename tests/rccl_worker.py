@@ -38,8 +38,8 @@ def main():
          {"bitmap_join": False, "chunks": 2, "exchange": C.ExchangeMode.ONE_SIDED}),
         ("one-sided-materialize", C.GenSpec(seed=99), G_R,
          {"exchange": C.ExchangeMode.ONE_SIDED, "materialize": True}),
-        # ~43 % of the outer side on one key: at world >= 4 that partition is
-        # joined by several ranks (outer divided, inner replicated)
+        # ~43 % of the outer side on one key: that partition is joined by
+        # several ranks (outer divided, inner replicated)
         ("hot-split", C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=79, domain=5, zipf_theta=0.99), G_S,
          {"bitmap_join": False, "chunks": 2, "key_hashing": C.KeyHashing.OFF}),
         ("hot-split-one-sided", C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=79, domain=5, zipf_theta=0.99),
@@ -84,8 +84,8 @@ def main():
         for _ in range(2):
             res = j.run()
             assert res["global_matches"] == exp, (name, res["global_matches"], exp)
-            if name.startswith("hot-split"):
-                assert (res["split_partitions"] >= 1) == (info.world >= 4), (name, res["split_partitions"])
+            if name.startswith("hot-split"):  # 43 % of one side: above half a rank's fair share at any world
+                assert res["split_partitions"] >= 1, (name, res["split_partitions"])
         if opts.get("materialize"):
             pairs = j.output()
             assert pairs.shape[0] == res["local_matches"], (pairs.shape, res["local_matches"])
