@@ -279,6 +279,8 @@ def measure(C, info, ctx, comm, on_gpu, G_R, G_S, inner, outer, cfg, rel_loc, st
         "expected_matches": expected,
         "correct": all(r["global_matches"] == expected for r in [first] + results) if expected is not None else None,
         "plan": repr(join.plan),
+        "sampled_network": bool(results[-1]["sampled_network"]),
+        "network_fallbacks": sum(r["network_fallbacks"] for r in [first] + results),
         "phases_ms": {k: round(sum(r[k] for r in results) / len(results), 3) for k in PHASES},
         "results": results,
         "join": join,

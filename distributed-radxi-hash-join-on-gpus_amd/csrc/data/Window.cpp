@@ -22,13 +22,16 @@ Window::Window(const histograms::ExchangePlan &plan, histograms::GlobalHistogram
   localWindowSize = plan.recvTotal;
   data = ctx->workspace().get(localWindowSize * tupleBytes());
   exchanged.assign(plan.chunks, false);
-  if (ctx->onDevice() && plan.numberOfNodes > 1) {
-    ready.resize(plan.chunks);
-    done.resize(plan.chunks);
-    for (uint32_t c = 0; c < plan.chunks; ++c) {
-      ready[c] = ctx->acquireEvent();
-      done[c] = ctx->acquireEvent();
-    }
+  createExchangeEvents();
+}
+
+void Window::createExchangeEvents() {
+  if (!ctx->onDevice() || plan.numberOfNodes == 1) return;
+  ready.resize(plan.chunks);
+  done.resize(plan.chunks);
+  for (uint32_t c = 0; c < plan.chunks; ++c) {
+    ready[c] = ctx->acquireEvent();
+    done[c] = ctx->acquireEvent();
   }
 }
 
@@ -38,6 +41,7 @@ Window::Window(const histograms::ExchangePlan &plan, uint64_t capacityTuples, co
   localWindowSize = capacityTuples;
   data = ctx->workspace().get(std::max<uint64_t>(capacityTuples, 1) * tupleBytes());
   exchanged.assign(std::max<uint32_t>(plan.chunks, 1), false);
+  createExchangeEvents();
 }
 
 Window::Window(std::unique_ptr<histograms::ExchangePlan> ownPlan, void *data, core::ExecContext *ctx, bool wide,
@@ -153,6 +157,65 @@ void Window::exchangePacked(const uint64_t *send, uint32_t chunk) {
     ctx->timeline().end("MWINPUT");
     host::wireUnpack(wrecv, dst, rs.data(), (uint32_t)rs.size(), codec);
   }
+}
+
+void Window::exchangeSegmented(const uint64_t *send, uint32_t chunk, SegmentedChunk &&sc, hipEvent_t scattered) {
+  const uint32_t N = plan.numberOfNodes;
+  JOIN_ASSERT(ctx->onDevice() && N > 1 && codec.w && !wide && chunk < plan.chunks, "Window",
+              "segmented exchange: device, N > 1, wire codec, compressed tuples");
+  JOIN_ASSERT(sc.sendWords.size() == N && sc.sendDispls.size() == N && sc.recvWords.size() == N &&
+                  sc.recvDispls.size() == N,
+              "Window", "segmented exchange: per-peer word counts for %u ranks", N);
+  auto prefix = [](std::vector<kernels::WireSeg> &v) {
+    uint64_t g = 0;
+    for (kernels::WireSeg &x : v) {
+      x.group0 = g;
+      g += ceilDiv(x.n, 64);
+    }
+    return g;
+  };
+  const uint64_t sG = prefix(sc.send), rG = prefix(sc.recv), cG = prefix(sc.self);
+  uint64_t sTotal = 0, rTotal = 0;
+  for (uint32_t p = 0; p < N; ++p) {
+    sTotal = std::max(sTotal, sc.sendDispls[p] + sc.sendWords[p]);
+    rTotal = std::max(rTotal, sc.recvDispls[p] + sc.recvWords[p]);
+    if (p != plan.nodeId) wireSent += sc.sendWords[p];
+  }
+  uint64_t *wsend = ctx->workspace().getArray<uint64_t>(std::max<uint64_t>(sTotal, 1));
+  uint64_t *wrecv = ctx->workspace().getArray<uint64_t>(std::max<uint64_t>(rTotal, 1));
+  uint64_t *dst = static_cast<uint64_t *>(data);
+  hipStream_t xs = ctx->commStream();
+  HIP_CHECK(hipStreamWaitEvent(xs, scattered, 0));
+  // Segment tables: pinned staging -> HBM, ordered on the exchange stream.
+  auto upload = [&](const std::vector<kernels::WireSeg> &v) -> kernels::WireSeg * {
+    if (v.empty()) return nullptr;
+    const size_t bytes = v.size() * sizeof(kernels::WireSeg);
+    void *pinned = ctx->staging().get(bytes);
+    std::memcpy(pinned, v.data(), bytes);
+    kernels::WireSeg *d = ctx->workspace().getArray<kernels::WireSeg>(v.size());
+    HIP_CHECK(hipMemcpyAsync(d, pinned, bytes, hipMemcpyHostToDevice, xs));
+    return d;
+  };
+  kernels::WireSeg *dS = upload(sc.send), *dR = upload(sc.recv), *dC = upload(sc.self);
+  kernels::wirePack(send, wsend, dS, (uint32_t)sc.send.size(), sG, codec, xs);
+  kernels::segCopy(send, dst, dC, (uint32_t)sc.self.size(), cG, xs);
+  ctx->timeline().begin("MWINPUT", xs);
+  ctx->comm()->allToAllV(wsend, sc.sendWords.data(), sc.sendDispls.data(), wrecv, sc.recvWords.data(),
+                         sc.recvDispls.data(), Location::Device, xs);
+  ctx->timeline().end("MWINPUT", xs);
+  if (wired.size() < plan.chunks) {
+    wired.resize(plan.chunks, nullptr);
+    for (auto &e : wired)
+      if (!e) e = ctx->acquireEvent();
+  }
+  HIP_CHECK(hipEventRecord(wired[chunk], xs));
+  HIP_CHECK(hipStreamWaitEvent(ctx->decodeStream(), wired[chunk], 0));
+  kernels::wireUnpack(wrecv, dst, dR, (uint32_t)sc.recv.size(), rG, codec, ctx->decodeStream());
+  HIP_CHECK(hipEventRecord(done[chunk], ctx->decodeStream()));
+  performance::Measurements::add("MWINPUTCNT", 1, "calls");
+  if (segmented.size() < plan.chunks) segmented.resize(plan.chunks);
+  segmented[chunk] = std::move(sc);
+  exchanged[chunk] = true;
 }
 
 void Window::start() { open = true; }

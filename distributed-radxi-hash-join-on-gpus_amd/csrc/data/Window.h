@@ -31,8 +31,9 @@ class Window {
  public:
   Window(const histograms::ExchangePlan &plan, histograms::GlobalHistogram *globalHistogram,
          histograms::AssignmentMap *assignment, core::ExecContext *ctx, bool wide);
-  // Single-rank window of `capacityTuples` whose plan is filled in after the
-  // scatter (sampled network pass: no histograms, no exchange).
+  // Window of `capacityTuples` whose plan is filled in after the scatter
+  // (sampled network passes: single-rank, no exchange; or N > 1, exchanged
+  // with exchangeSegmented as the plan's chunks become known).
   // elemBytes 4: the window holds u32 key fragments (JoinPlan::fragments).
   Window(const histograms::ExchangePlan &plan, uint64_t capacityTuples, core::ExecContext *ctx, bool wide,
          uint32_t elemBytes = 0);
@@ -70,6 +71,20 @@ class Window {
   // (Not with replicated runs of split hot partitions: those need a send buffer.)
   bool directScatter() const { return oneSided && ctx->onDevice() && plan.replicas.empty(); }
   std::vector<uint64_t> directDigitBase() const;
+  // Sampled N > 1 exchange of one chunk (tasks/SampledShuffle): the send
+  // buffer holds gapped claim slices, so the caller lists the filled runs.
+  // send: runs per peer in peer order, `wire` = absolute word offset in the
+  // packed send buffer; recv: runs per source, `raw` = window tuple offset,
+  // `wire` = absolute word offset in the packed receive buffer; self: own runs,
+  // `raw` = send-buffer offset, `wire` = window offset.  Words and word
+  // displacements are per peer.  group0 is filled in here.  The pack waits
+  // for `scattered` (the chunk's scatter) on the exchange stream.  Needs the
+  // wire codec (setWireCodec); the plan's segments describe the result.
+  struct SegmentedChunk {
+    std::vector<kernels::WireSeg> send, recv, self;
+    std::vector<uint64_t> sendWords, sendDispls, recvWords, recvDispls;
+  };
+  void exchangeSegmented(const uint64_t *sendBuffer, uint32_t chunk, SegmentedChunk &&sc, hipEvent_t scattered);
   // Bit-pack tuples on the wire (kernels.h, WireCodec); ridBase[rank * C + c]
   // is the rid base of sender `rank`'s chunk c (C = ridBase.size() / ranks).
   // Call before the first exchange.
@@ -125,6 +140,8 @@ class Window {
   uint32_t ridBaseChunks = 1;
   // Per-chunk segment lists: kept alive until the join ends (async H2D source).
   std::vector<std::vector<kernels::WireSeg>> sendSegs, recvSegs;
+  std::vector<SegmentedChunk> segmented;  // exchangeSegmented chunks (host copies, for inspection)
+  void createExchangeEvents();
   std::vector<hipEvent_t> wired;  // chunk's all-to-allv done (exchange stream -> decode stream)
   uint64_t wireSent = 0;
   void *partitioned = nullptr;

@@ -123,6 +123,11 @@ struct SampledInput {
   uint64_t *totals;  // [NGROUPS][F]
 };
 void netSampledTotals(const SampledInput *sides, uint32_t count, uint32_t bits, hipStream_t s, KeyMix mix);
+// totals[c][g][d] (u64) = sum of blockHist[d][b] over the blocks b of chunk c
+// (blocksPerChunk each) with (b - first block of c) % NGROUPS == g: the claim
+// groups of chunk c's scatter launch (sampled N > 1 network pass).
+void netChunkGroupTotals(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint32_t blocksPerChunk,
+                         uint32_t chunks, uint64_t *totals, hipStream_t s);
 // totals[c][F] = sum of blockHist over the blocks of chunk c (blocksPerChunk each).
 void digitTotals(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint32_t blocksPerChunk,
                  uint32_t chunks, uint64_t *totals, hipStream_t s);
@@ -464,6 +469,10 @@ void wirePack(const uint64_t *raw, uint64_t *wire, const WireSeg *segs, uint32_t
               const WireCodec &c, hipStream_t s);
 void wireUnpack(const uint64_t *wire, uint64_t *raw, const WireSeg *segs, uint32_t nSegs, uint64_t totalGroups,
                 const WireCodec &c, hipStream_t s);
+// Raw segmented gather: dst[seg.wire + t] = src[seg.raw + t] for t < seg.n
+// (same segment list format; offsets in 8-byte words, nothing past seg.n written).
+void segCopy(const uint64_t *src, uint64_t *dst, const WireSeg *segs, uint32_t nSegs, uint64_t totalGroups,
+             hipStream_t s);
 
 // ------------------------------------------------------------------- scans
 size_t scanWorkspaceBytes(uint64_t n);

@@ -70,11 +70,9 @@ struct Loader<uint32_t> {
 };
 
 // ------------------------------------------------------- histogram (pass 1)
-__global__ __launch_bounds__(NT) void netHistogramKernel(const ulonglong2 *__restrict__ in, uint64_t n,
-                                                         uint32_t tpb, uint32_t bits,
-                                                         uint32_t *__restrict__ blockHist, KeyMix mix,
-                                                         uint32_t stride) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t hsh[];
+__device__ __forceinline__ void netHistogramBody(const ulonglong2 *__restrict__ in, uint64_t n, uint32_t tpb,
+                                                 uint32_t bits, uint32_t *__restrict__ blockHist, KeyMix mix,
+                                                 uint32_t stride, uint32_t *hsh) {
   const uint32_t F = 1u << bits, mask = F - 1;
   const int wid = threadIdx.x / WAVE;
   for (uint32_t i = threadIdx.x; i < 4 * F; i += NT) hsh[i] = 0;
@@ -100,13 +98,35 @@ __global__ __launch_bounds__(NT) void netHistogramKernel(const ulonglong2 *__res
     blockHist[(uint64_t)d * gridDim.x + blockIdx.x] = hsh[d] + hsh[F + d] + hsh[2 * F + d] + hsh[3 * F + d];
 }
 
+// Exact (every tile) and sampled (1 tile in `stride`) launches are separate
+// kernels so that a trace tells a full pre-read from a sample.
+__global__ __launch_bounds__(NT) void netHistogramKernel(const ulonglong2 *__restrict__ in, uint64_t n,
+                                                         uint32_t tpb, uint32_t bits,
+                                                         uint32_t *__restrict__ blockHist, KeyMix mix) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t hsh[];
+  netHistogramBody(in, n, tpb, bits, blockHist, mix, 1, hsh);
+}
+
+__global__ __launch_bounds__(NT) void netSampledHistogramKernel(const ulonglong2 *__restrict__ in, uint64_t n,
+                                                                uint32_t tpb, uint32_t bits,
+                                                                uint32_t *__restrict__ blockHist, KeyMix mix,
+                                                                uint32_t stride) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t hsh[];
+  netHistogramBody(in, n, tpb, bits, blockHist, mix, stride, hsh);
+}
+
 void netHistogram(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
                   uint32_t *blockHist, hipStream_t s, KeyMix mix, uint32_t sampleStride) {
   HJ_CHECK(bits >= 1 && bits <= MAX_PART_BITS, "netHistogram: bits=%u out of range", bits);
   HJ_CHECK(sampleStride >= 1, "netHistogram: sampleStride must be >= 1");
   const size_t lds = size_t(4) << bits << 2;
-  hipLaunchKernelGGL(netHistogramKernel, dim3(g.blocks), dim3(NT), lds, s,
-                     reinterpret_cast<const ulonglong2 *>(in), n, g.tilesPerBlock, bits, blockHist, mix, sampleStride);
+  if (sampleStride > 1)
+    hipLaunchKernelGGL(netSampledHistogramKernel, dim3(g.blocks), dim3(NT), lds, s,
+                       reinterpret_cast<const ulonglong2 *>(in), n, g.tilesPerBlock, bits, blockHist, mix,
+                       sampleStride);
+  else
+    hipLaunchKernelGGL(netHistogramKernel, dim3(g.blocks), dim3(NT), lds, s, reinterpret_cast<const ulonglong2 *>(in),
+                       n, g.tilesPerBlock, bits, blockHist, mix);
   HIP_CHECK_LAUNCH();
 }
 
@@ -330,6 +350,32 @@ void netGroupCursors(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uin
   else
     hipLaunchKernelGGL(netGroupCursorsKernel<unsigned long long>, dim3(F), dim3(NT), 0, s, blockHist, F, blocks,
                        blocksPerChunk, base, reinterpret_cast<unsigned long long *>(gcur));
+  HIP_CHECK_LAUNCH();
+}
+
+// totals[c][g][d]: one workgroup per (digit, chunk); thread t only sees
+// blocks of group t % NGROUPS (NT % NGROUPS == 0, b0 is where the groups start).
+__global__ __launch_bounds__(NT) void netChunkGroupTotalsKernel(const uint32_t *__restrict__ blockHist, uint32_t F,
+                                                                uint32_t blocks, uint32_t bpc,
+                                                                unsigned long long *totals) {
+  __shared__ unsigned long long gs[NGROUPS];
+  const uint32_t d = blockIdx.x, c = blockIdx.y;
+  const uint32_t b0 = c * bpc, b1 = min(blocks, b0 + bpc);
+  if (threadIdx.x < NGROUPS) gs[threadIdx.x] = 0;
+  __syncthreads();
+  unsigned long long mine = 0;
+  for (uint32_t b = b0 + threadIdx.x; b < b1; b += NT) mine += blockHist[(uint64_t)d * blocks + b];
+  atomicAdd(&gs[threadIdx.x % NGROUPS], mine);
+  __syncthreads();
+  if (threadIdx.x < NGROUPS) totals[((uint64_t)c * NGROUPS + threadIdx.x) * F + d] = gs[threadIdx.x];
+}
+
+void netChunkGroupTotals(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint32_t blocksPerChunk,
+                         uint32_t chunks, uint64_t *totals, hipStream_t s) {
+  HJ_CHECK(blocksPerChunk >= 1 && (uint64_t)chunks * blocksPerChunk >= blocks, "netChunkGroupTotals: %u x %u < %u",
+           chunks, blocksPerChunk, blocks);
+  hipLaunchKernelGGL(netChunkGroupTotalsKernel, dim3(F, chunks), dim3(NT), 0, s, blockHist, F, blocks,
+                     blocksPerChunk, reinterpret_cast<unsigned long long *>(totals));
   HIP_CHECK_LAUNCH();
 }
 

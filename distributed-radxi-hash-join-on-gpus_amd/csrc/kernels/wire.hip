@@ -25,10 +25,9 @@ constexpr uint32_t WIRE_THREADS = 256;
 constexpr uint32_t WIRE_WAVES = WIRE_THREADS / WAVE;
 constexpr uint32_t WIRE_MAX_SEGS_LDS = 256;
 
-// Segment of global group gi: segments are few (one per peer and chunk), so
-// they are cached in LDS and searched with a short binary search.
+// Segment of global group gi (last segment with group0 <= gi).
 __device__ __forceinline__ uint32_t findSeg(const WireSeg *segs, uint32_t nSegs, uint64_t gi) {
-  uint32_t lo = 0, hi = nSegs;  // last seg with group0 <= gi
+  uint32_t lo = 0, hi = nSegs;
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) / 2;
     if (segs[mid].group0 <= gi)
@@ -47,11 +46,31 @@ __device__ __forceinline__ const WireSeg *stageSegs(const WireSeg *segs, uint32_
   return lds;
 }
 
+// Every wave walks a contiguous run of `per` groups: one search for its first
+// group's segment, then a forward walk.  Segments may be many (the sampled
+// N > 1 exchange lists one per (peer, partition, XCD group) slice), so no
+// per-group search; a wave's groups are also contiguous in memory.
+struct GroupRun {
+  uint64_t gi, ge;
+  uint32_t si;
+  __device__ __forceinline__ GroupRun(const WireSeg *segs, uint32_t nSegs, uint64_t totalGroups, uint64_t per) {
+    const uint64_t wave = (uint64_t)blockIdx.x * WIRE_WAVES + threadIdx.x / WAVE;
+    gi = wave * per;
+    ge = min(totalGroups, gi + per);
+    si = gi < ge ? findSeg(segs, nSegs, gi) : 0;
+  }
+  // Segment of group gi (advanced monotonically).
+  __device__ __forceinline__ const WireSeg &seg(const WireSeg *segs, uint32_t nSegs) {
+    while (si + 1 < nSegs && segs[si + 1].group0 <= gi) ++si;
+    return segs[si];
+  }
+};
+
 template <bool kLds>
 __global__ __launch_bounds__(WIRE_THREADS) void wirePackKernel(const uint64_t *__restrict__ raw,
                                                                uint64_t *__restrict__ wire,
                                                                const WireSeg *__restrict__ gsegs, uint32_t nSegs,
-                                                               uint64_t totalGroups, WireCodec c) {
+                                                               uint64_t totalGroups, uint64_t per, WireCodec c) {
   __shared__ WireSeg lds[kLds ? WIRE_MAX_SEGS_LDS : 1];
   const WireSeg *segs = stageSegs<kLds>(gsegs, nSegs, lds);
   const uint32_t lane = threadIdx.x & (WAVE - 1);
@@ -60,10 +79,10 @@ __global__ __launch_bounds__(WIRE_THREADS) void wirePackKernel(const uint64_t *_
   // Word `lane` of a group starts at stream bit 64*lane: first overlapping value a, offset o in it.
   const uint32_t a = (64u * lane) / w, o = 64u * lane - a * w;
   const uint32_t K = (64u + w - 1) / w + 1;  // values overlapping one word (uniform)
-  for (uint64_t gi = (uint64_t)blockIdx.x * WIRE_WAVES + threadIdx.x / WAVE; gi < totalGroups;
-       gi += (uint64_t)gridDim.x * WIRE_WAVES) {
-    const WireSeg sg = segs[findSeg(segs, nSegs, gi)];
-    const uint64_t g = gi - sg.group0, t = g * 64 + lane;
+  GroupRun r(segs, nSegs, totalGroups, per);
+  for (; r.gi < r.ge; ++r.gi) {
+    const WireSeg &sg = r.seg(segs, nSegs);
+    const uint64_t g = r.gi - sg.group0, t = g * 64 + lane;
     const uint64_t e = t < sg.n ? (c.encode(raw[sg.raw + t], sg.base) & wmask) : 0ull;
     uint64_t word = 0;
     for (uint32_t k = 0; k < K; ++k) {
@@ -85,7 +104,7 @@ template <bool kLds>
 __global__ __launch_bounds__(WIRE_THREADS) void wireUnpackKernel(const uint64_t *__restrict__ wire,
                                                                  uint64_t *__restrict__ raw,
                                                                  const WireSeg *__restrict__ gsegs, uint32_t nSegs,
-                                                                 uint64_t totalGroups, WireCodec c) {
+                                                                 uint64_t totalGroups, uint64_t per, WireCodec c) {
   __shared__ WireSeg lds[kLds ? WIRE_MAX_SEGS_LDS : 1];
   const WireSeg *segs = stageSegs<kLds>(gsegs, nSegs, lds);
   const uint32_t lane = threadIdx.x & (WAVE - 1);
@@ -93,10 +112,10 @@ __global__ __launch_bounds__(WIRE_THREADS) void wireUnpackKernel(const uint64_t 
   const uint64_t wmask = w >= 64 ? ~0ull : ((1ull << w) - 1);
   const uint32_t bit0 = lane * w, j0 = bit0 >> 6, o = bit0 & 63;
   const bool two = o + w > 64;
-  for (uint64_t gi = (uint64_t)blockIdx.x * WIRE_WAVES + threadIdx.x / WAVE; gi < totalGroups;
-       gi += (uint64_t)gridDim.x * WIRE_WAVES) {
-    const WireSeg sg = segs[findSeg(segs, nSegs, gi)];
-    const uint64_t g = gi - sg.group0, t = g * 64 + lane;
+  GroupRun r(segs, nSegs, totalGroups, per);
+  for (; r.gi < r.ge; ++r.gi) {
+    const WireSeg &sg = r.seg(segs, nSegs);
+    const uint64_t g = r.gi - sg.group0, t = g * 64 + lane;
     if (t >= sg.n) continue;
     const uint64_t *gw = wire + sg.wire + g * w;
     uint64_t e = gw[j0] >> o;
@@ -105,8 +124,35 @@ __global__ __launch_bounds__(WIRE_THREADS) void wireUnpackKernel(const uint64_t 
   }
 }
 
-uint32_t wireGrid(uint64_t totalGroups) {
-  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ceilDiv(totalGroups, WIRE_WAVES), 8192));
+// Raw gather: dst[seg.wire + t] = src[seg.raw + t] (a rank's own runs, which
+// never touch the wire, into its window).
+template <bool kLds>
+__global__ __launch_bounds__(WIRE_THREADS) void segCopyKernel(const uint64_t *__restrict__ src,
+                                                              uint64_t *__restrict__ dst,
+                                                              const WireSeg *__restrict__ gsegs, uint32_t nSegs,
+                                                              uint64_t totalGroups, uint64_t per) {
+  __shared__ WireSeg lds[kLds ? WIRE_MAX_SEGS_LDS : 1];
+  const WireSeg *segs = stageSegs<kLds>(gsegs, nSegs, lds);
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  GroupRun r(segs, nSegs, totalGroups, per);
+  for (; r.gi < r.ge; ++r.gi) {
+    const WireSeg &sg = r.seg(segs, nSegs);
+    const uint64_t t = (r.gi - sg.group0) * 64 + lane;
+    if (t < sg.n) dst[sg.wire + t] = __builtin_nontemporal_load(src + sg.raw + t);
+  }
+}
+
+// Waves of a launch over totalGroups groups (~8 per SIMD of 256 CUs, or one
+// per group for small launches) and the groups each walks.
+struct WireLaunch {
+  uint32_t blocks;
+  uint64_t per;
+};
+WireLaunch wireLaunch(uint64_t totalGroups) {
+  const uint64_t maxWaves = 256ull * 4 * 8;
+  const uint64_t waves = std::max<uint64_t>(1, std::min<uint64_t>(totalGroups, maxWaves));
+  const uint64_t per = ceilDiv(totalGroups, waves);
+  return WireLaunch{(uint32_t)ceilDiv(ceilDiv(totalGroups, per), WIRE_WAVES), per};
 }
 
 }  // namespace
@@ -115,12 +161,13 @@ void wirePack(const uint64_t *raw, uint64_t *wire, const WireSeg *segs, uint32_t
               const WireCodec &c, hipStream_t s) {
   if (totalGroups == 0) return;
   HJ_CHECK(c.w >= 1 && c.w <= 64 && nSegs >= 1, "wirePack: w=%u nSegs=%u", c.w, nSegs);
+  const WireLaunch l = wireLaunch(totalGroups);
   if (nSegs <= WIRE_MAX_SEGS_LDS)
-    hipLaunchKernelGGL(wirePackKernel<true>, dim3(wireGrid(totalGroups)), dim3(WIRE_THREADS), 0, s, raw, wire, segs,
-                       nSegs, totalGroups, c);
+    hipLaunchKernelGGL(wirePackKernel<true>, dim3(l.blocks), dim3(WIRE_THREADS), 0, s, raw, wire, segs, nSegs,
+                       totalGroups, l.per, c);
   else
-    hipLaunchKernelGGL(wirePackKernel<false>, dim3(wireGrid(totalGroups)), dim3(WIRE_THREADS), 0, s, raw, wire,
-                       segs, nSegs, totalGroups, c);
+    hipLaunchKernelGGL(wirePackKernel<false>, dim3(l.blocks), dim3(WIRE_THREADS), 0, s, raw, wire, segs, nSegs,
+                       totalGroups, l.per, c);
   HIP_CHECK_LAUNCH();
 }
 
@@ -128,12 +175,27 @@ void wireUnpack(const uint64_t *wire, uint64_t *raw, const WireSeg *segs, uint32
                 const WireCodec &c, hipStream_t s) {
   if (totalGroups == 0) return;
   HJ_CHECK(c.w >= 1 && c.w <= 64 && nSegs >= 1, "wireUnpack: w=%u nSegs=%u", c.w, nSegs);
+  const WireLaunch l = wireLaunch(totalGroups);
   if (nSegs <= WIRE_MAX_SEGS_LDS)
-    hipLaunchKernelGGL(wireUnpackKernel<true>, dim3(wireGrid(totalGroups)), dim3(WIRE_THREADS), 0, s, wire, raw,
-                       segs, nSegs, totalGroups, c);
+    hipLaunchKernelGGL(wireUnpackKernel<true>, dim3(l.blocks), dim3(WIRE_THREADS), 0, s, wire, raw, segs, nSegs,
+                       totalGroups, l.per, c);
   else
-    hipLaunchKernelGGL(wireUnpackKernel<false>, dim3(wireGrid(totalGroups)), dim3(WIRE_THREADS), 0, s, wire, raw,
-                       segs, nSegs, totalGroups, c);
+    hipLaunchKernelGGL(wireUnpackKernel<false>, dim3(l.blocks), dim3(WIRE_THREADS), 0, s, wire, raw, segs, nSegs,
+                       totalGroups, l.per, c);
+  HIP_CHECK_LAUNCH();
+}
+
+void segCopy(const uint64_t *src, uint64_t *dst, const WireSeg *segs, uint32_t nSegs, uint64_t totalGroups,
+             hipStream_t s) {
+  if (totalGroups == 0) return;
+  HJ_CHECK(nSegs >= 1, "segCopy: no segments for %lu groups", (unsigned long)totalGroups);
+  const WireLaunch l = wireLaunch(totalGroups);
+  if (nSegs <= WIRE_MAX_SEGS_LDS)
+    hipLaunchKernelGGL(segCopyKernel<true>, dim3(l.blocks), dim3(WIRE_THREADS), 0, s, src, dst, segs, nSegs,
+                       totalGroups, l.per);
+  else
+    hipLaunchKernelGGL(segCopyKernel<false>, dim3(l.blocks), dim3(WIRE_THREADS), 0, s, src, dst, segs, nSegs,
+                       totalGroups, l.per);
   HIP_CHECK_LAUNCH();
 }
 

@@ -156,6 +156,12 @@ void HashJoin::makeJoinPlan() {
     plan.wireRidBits[0] = plan.wireRidBits[1] = 0;
     plan.pipelineOuter = false;
   }
+  // N > 1 (tasks/SampledShuffle): needs the wire codec on both relations --
+  // its pack kernel is what keeps the claim slices' gaps off the links -- and
+  // two-sided windows.
+  if (numberOfNodes > 1)
+    plan.sampledNetwork = ctx->onDevice() && sampleable && !plan.wide && !plan.oneSided && plan.wireBits[0] &&
+                          plan.wireBits[1];
   basePlan = plan;  // the two-level plan: what a bitmap plan falls back to
   bitmapExact = !(ctx->onDevice() && sampleable);
   planBitmap();
@@ -200,7 +206,7 @@ uint64_t HashJoin::workspaceEstimate() const {
     const uint64_t recv = N == 1 ? (plan.sampledNetwork ? sampledCap(n[r]) : n[r]) : g[r] / N + g[r] / (4 * N) + (1 << 20);
     recvTotal[r] = recv;
     b += recv * wordB;
-    if (N > 1 && !plan.oneSided) b += n[r] * wordB;                                 // send buffer
+    if (N > 1 && !plan.oneSided) b += (plan.sampledNetwork ? n[r] + n[r] / 8 : n[r]) * wordB;  // send buffer
     if (plan.wireBits[r]) b += (n[r] + recv) * ((plan.wireBits[r] + 7) / 8) + (64ull << 10);  // wire buffers
     if (plan.twoLevel) {
       const uint64_t ob = plan.fragments ? 2 : plan.splitLocal ? kernels::SPLIT_BYTES : (plan.wide ? 16 : 8);
@@ -412,7 +418,10 @@ JoinResult HashJoin::runImpl() {
   const bool sampled = plan.sampledNetwork && !sampledOverflowed;
   bool done = false;
   if (sampled) {
-    done = SampledSingleRankExchange(env, localOverflowed).exchange(run);
+    if (numberOfNodes == 1)
+      done = SampledSingleRankExchange(env, localOverflowed).exchange(run);
+    else
+      done = SampledShuffleExchange(env).exchange(run);
     if (!done) {  // a slice overflowed (skew the sample missed): exact from now on
       sampledOverflowed = true;
       ++result.networkFallbacks;

@@ -81,6 +81,45 @@ bool SampledSingleRankExchange::exchange(JoinRun &run) {
   return true;
 }
 
+// ----------------------------------------------------------- N > 1, sampled
+bool SampledShuffleExchange::exchange(JoinRun &run) {
+  core::ExecContext *ctx = env.ctx;
+  run.hc.reset(new tasks::HistogramComputation(env.nodes, env.nodeId, env.inner, env.outer, ctx, env.plan,
+                                               env.config.maxPartitionBlocks));
+  run.ss.reset(new tasks::SampledShuffle(env.nodes, env.nodeId, run.hc.get(), ctx, env.plan, env.config.sampleStride));
+  tasks::SampledShuffle &ss = *run.ss;
+  const uint64_t h0 = nowUs();
+  ss.sampleAndAssign();
+  HIP_CHECK(hipEventRecord(env.ev[1], ctx->stream()));
+  Measurements::stopHistogramComputation();
+  Measurements::storeHistogramDetails(nowUs() - h0, env.inner->getLocalSize(), env.outer->getLocalSize(),
+                                      run.hc->globalUs, run.hc->assignUs, 0);
+  run.t1 = nowUs();
+  Measurements::startWindowAllocation();
+  ss.layoutSide(0);
+  ss.layoutSide(1);
+  Measurements::stopWindowAllocation();
+  run.t2 = nowUs();
+  Measurements::startNetworkPartitioning();
+  run.trace.reset();
+  utils::faultPoint("network");
+  run.phase("network_partitioning");
+  // Both scatters are enqueued before the first wait: the host gathers the
+  // inner chunks' fills (and enqueues their exchanges) while the outer
+  // relation is still being scattered.
+  ss.scatterSide(0);
+  ss.scatterSide(1);
+  const bool ok = ss.exchangeSide(0) && ss.exchangeSide(1);
+  if (!ok) {
+    ctx->synchronize();  // drain what was enqueued; the exact re-run uses fresh buffers
+    return false;
+  }
+  run.inner = ss.window(0);
+  run.outer = ss.window(1);
+  run.sampled = true;
+  return true;
+}
+
 // --------------------------------------------------- N > 1, split histogram
 bool SplitHistogramExchange::exchange(JoinRun &run) {
   core::ExecContext *ctx = env.ctx;

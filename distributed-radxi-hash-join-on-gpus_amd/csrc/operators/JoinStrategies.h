@@ -2,6 +2,7 @@
 // operators/HashJoin.cpp:45-220).  A join is
 //   exchange   histogram -> windows -> network partitioning, one strategy per plan:
 //                SampledSingleRankExchange  N == 1, sampled histogram, bounded claim scatter
+//                SampledShuffleExchange     N > 1, sampled histogram, exact fills gathered per relation
 //                SplitHistogramExchange     N > 1, outer histogram behind the inner exchange
 //                ExactExchange              exact histograms, then windows and the chunked exchange
 //   local      second radix pass + build/probe (LocalPhase; pipelined per outer chunk at N > 1)
@@ -25,6 +26,7 @@
 #include "../tasks/HistogramComputation.h"
 #include "../tasks/LocalPartitioning.h"
 #include "../tasks/SampledNetworkPartitioning.h"
+#include "../tasks/SampledShuffle.h"
 
 namespace hpcjoin {
 namespace operators {
@@ -49,6 +51,7 @@ struct JoinRun {
   std::unique_ptr<performance::TraceRange> trace;
   std::unique_ptr<tasks::HistogramComputation> hc;
   std::unique_ptr<tasks::SampledNetworkPartitioning> sp;
+  std::unique_ptr<tasks::SampledShuffle> ss;  // N > 1 sampled pass (owns its windows' plans)
   std::unique_ptr<data::Window> innerOwned, outerOwned;
   data::Window *inner = nullptr, *outer = nullptr;
   // Local pass: created by the exchange when it starts the inner side early.
@@ -83,6 +86,17 @@ class SampledSingleRankExchange : public ExchangeStrategy {
 
  private:
   bool localExact;
+};
+
+// N > 1, sampled: estimates instead of the exact pre-read, bounded claim
+// slices, exact fills all-gathered per relation and packed runs on the wire
+// (tasks/SampledShuffle).  false = a slice or window would overflow on some
+// rank (every rank agrees; the caller re-runs with ExactExchange).
+class SampledShuffleExchange : public ExchangeStrategy {
+ public:
+  using ExchangeStrategy::ExchangeStrategy;
+  const char *name() const override { return "sampled_shuffle"; }
+  bool exchange(JoinRun &run) override;
 };
 
 // N > 1: the inner relation's exact histogram heads the join; the outer

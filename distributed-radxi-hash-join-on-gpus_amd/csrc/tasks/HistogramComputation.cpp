@@ -60,6 +60,17 @@ void HistogramComputation::executeInner(uint32_t sampleStride) {
   offsetUs = performance::nowUs() - t0;
 }
 
+void HistogramComputation::assignFromEstimates(const uint64_t *innerEstimate, const uint64_t *outerEstimate) {
+  innerRelationLocalHistogram->setChunkHistograms(innerEstimate);
+  outerRelationLocalHistogram->setChunkHistograms(outerEstimate);
+  uint64_t t0 = performance::nowUs();
+  histograms::GlobalHistogram::computeGlobalHistograms(*innerRelationGlobalHistogram, *outerRelationGlobalHistogram);
+  globalUs = performance::nowUs() - t0;
+  t0 = performance::nowUs();
+  assignment->computePartitionAssignment();
+  assignUs = performance::nowUs() - t0;
+}
+
 void HistogramComputation::launchOuter(hipStream_t exchangeStream) {
   histograms::LocalHistogram *h = outerRelationLocalHistogram.get();
   const size_t per = (size_t)h->getChunkCount() * h->getPartitionCount();

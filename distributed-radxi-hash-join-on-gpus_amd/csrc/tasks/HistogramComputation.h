@@ -36,6 +36,10 @@ class HistogramComputation : public Task {
   //    chunks already issued there), then a copy to pinned host memory.
   //  finishOuter(): waits for that copy only, then outer offsets.
   void executeInner(uint32_t sampleStride);
+  // Sampled N > 1 network pass (tasks/SampledShuffle): per-chunk estimates of
+  // both relations ([chunks][F] each) -> one fused all-gather -> assignment.
+  // No offsets: the exchange layout is built from the exact slice fills.
+  void assignFromEstimates(const uint64_t *innerEstimate, const uint64_t *outerEstimate);
   void launchOuter(hipStream_t exchangeStream);
   void finishOuter();
 

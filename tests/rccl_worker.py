@@ -44,6 +44,15 @@ def main():
          {"bitmap_join": False, "chunks": 2, "key_hashing": C.KeyHashing.OFF}),
         ("hot-split-one-sided", C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=79, domain=5, zipf_theta=0.99),
          G_S, {"bitmap_join": False, "key_hashing": C.KeyHashing.OFF, "exchange": C.ExchangeMode.ONE_SIDED}),
+        # sampled network pass (no exact pre-read): fills all-gathered per
+        # chunk, packed runs on the wire (tasks/SampledShuffle)
+        ("sampled-chunks3", C.GenSpec(distribution=C.KeyDistribution.UNIFORM, seed=7, domain=G_R), G_S,
+         {"bitmap_join": False, "chunks": 3, "network_histogram": C.HistogramMode.SAMPLED}),
+        ("sampled-materialize", C.GenSpec(seed=99), G_R,
+         {"materialize": True, "chunks": 2, "network_histogram": C.HistogramMode.SAMPLED}),
+        ("sampled-hot-split", C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=79, domain=5, zipf_theta=0.99),
+         G_S, {"bitmap_join": False, "chunks": 2, "key_hashing": C.KeyHashing.OFF,
+               "network_histogram": C.HistogramMode.SAMPLED}),
     ]
     R = C.Relation(C.Relation.local_size_for(G_R, info.rank, info.world), G_R, "device", info.local_rank)
     R.generate(inner, C.Relation.local_offset_for(G_R, info.rank, info.world))
@@ -59,15 +68,20 @@ def main():
     Ss.generate(sparse_out, C.Relation.local_offset_for(G_R, info.rank, info.world))
     cfg = C.JoinConfig()
     cfg.wire_codec = C.WireCodecMode.ON  # auto packs only <= 56 bits (this size plans 6 network bits: 57)
-    j = C.HashJoin(Rs, Ss, ctx, cfg)
-    assert j.plan.key_only and list(j.plan.wire_bits) == [j.plan.key_bits - j.plan.network_bits] * 2, j.plan
     exp = C.Relation.expected_matches(sparse_in, G_R, sparse_out, G_R)
-    for _ in range(2):
-        res = j.run()
-        assert res["global_matches"] == exp, ("sparse-key-only", res["global_matches"], exp)
-    if info.rank == 0:
-        print(f"sparse-key-only: {res['global_matches']} == {exp}, plan {j.plan}", flush=True)
-    del j, Rs, Ss
+    for mode in ("EXACT", "SAMPLED"):
+        cfg.network_histogram = getattr(C.HistogramMode, mode)
+        j = C.HashJoin(Rs, Ss, ctx, cfg)
+        assert j.plan.key_only and list(j.plan.wire_bits) == [j.plan.key_bits - j.plan.network_bits] * 2, j.plan
+        assert j.plan.sampled_network == (mode == "SAMPLED"), j.plan
+        for _ in range(2):
+            res = j.run()
+            assert res["global_matches"] == exp, ("sparse-key-only", mode, res["global_matches"], exp)
+            assert res["sampled_network"] == (mode == "SAMPLED") and res["network_fallbacks"] == 0, res
+        if info.rank == 0:
+            print(f"sparse-key-only {mode}: {res['global_matches']} == {exp}, plan {j.plan}", flush=True)
+        del j
+    del Rs, Ss
     for name, spec, G, opts in cases:
         S = C.Relation(C.Relation.local_size_for(G, info.rank, info.world), G, "device", info.local_rank)
         S.generate(spec, C.Relation.local_offset_for(G, info.rank, info.world))
@@ -84,8 +98,10 @@ def main():
         for _ in range(2):
             res = j.run()
             assert res["global_matches"] == exp, (name, res["global_matches"], exp)
-            if name.startswith("hot-split"):  # 43 % of one side: above half a rank's fair share at any world
+            if "hot-split" in name:  # 43 % of one side: above half a rank's fair share at any world
                 assert res["split_partitions"] >= 1, (name, res["split_partitions"])
+            if name.startswith("sampled"):
+                assert res["sampled_network"] and res["network_fallbacks"] == 0, (name, res)
         if opts.get("materialize"):
             pairs = j.output()
             assert pairs.shape[0] == res["local_matches"], (pairs.shape, res["local_matches"])

@@ -88,20 +88,120 @@ def test_in_process_chunked_exchange(C, dev, chunks, policy):
 @pytest.mark.parametrize("n_ranks,chunks,fmt", [(2, 1, "COMPRESSED"), (4, 3, "COMPRESSED"), (3, 2, "WIDE")])
 def test_in_process_sampled_local_pass(C, cuda, n_ranks, chunks, fmt):
     """The sampled local pass on multi-rank windows (segments per chunk and
-    source; the network pass stays exact for N > 1)."""
+    source).  The sampled network pass (tasks/SampledShuffle) needs the wire
+    codec, which wide tuples do not have: those stay on the exact exchange."""
 
     def cfg_fn(cfg):
         cfg.bitmap_join = False
         cfg.local_histogram = C.HistogramMode.SAMPLED
-        cfg.network_histogram = C.HistogramMode.SAMPLED  # ignored for N > 1
+        cfg.network_histogram = C.HistogramMode.SAMPLED
         cfg.chunks = chunks
         cfg.format = getattr(C.TupleFormat, fmt)
 
     results, exp = run_ranks(C, n_ranks, "device", 3_000_017, 4_000_037, cfg_fn, outer_dist="ZIPF", theta=0.8)
     for res, plan in results:
         assert res["global_matches"] == exp
-        assert res["sampled_local"] and not res["sampled_network"] and not plan.sampled_network
-        assert res["local_fallbacks"] == 0
+        sampled = fmt != "WIDE"
+        assert res["sampled_local"] and res["sampled_network"] == sampled and plan.sampled_network == sampled
+        assert res["local_fallbacks"] == 0 and res["network_fallbacks"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_ranks,chunks,opts", [(2, 1, ""), (3, 3, "mat"), (4, 2, "zipf"), (8, 1, ""),
+                                                  (4, 2, "hot"), (3, 2, "sparse")])
+def test_sampled_shuffle(C, cuda, n_ranks, chunks, opts):
+    """N > 1 sampled network pass (tasks/SampledShuffle): no exact pre-read of
+    either relation; slices sized from a 1-in-S tile sample, exact fills
+    all-gathered per chunk, filled runs packed onto the wire.  Counts equal
+    the oracle and the exact exchange; materialized pairs are the same set."""
+    import torch
+    G_R, G_S = 1_500_007, 2_500_009
+    inner = outer = None
+    if opts == "hot":
+        G_R, G_S = 200_000, 2_000_000
+        outer = C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=79, domain=5, zipf_theta=0.99)
+    if opts == "sparse":  # the general path: key-only words, key fragment on the wire
+        inner, outer = C.GenSpec(seed=1234), C.GenSpec(seed=99)
+        inner.sparse64 = outer.sparse64 = True
+    got = {}
+    for mode in ("SAMPLED", "EXACT"):
+        pairs = [None] * n_ranks
+
+        def cfg_fn(c, mode=mode):
+            c.network_histogram = getattr(C.HistogramMode, mode)
+            c.bitmap_join = False
+            c.chunks = chunks
+            c.materialize = opts == "mat"
+            c.wire_codec = C.WireCodecMode.ON
+            if opts == "hot":
+                c.key_hashing = C.KeyHashing.OFF
+
+        results, exp = run_ranks(C, n_ranks, "device", G_R, G_S, cfg_fn, outer_dist="ZIPF" if opts == "zipf" else "UNIFORM",
+                                 theta=0.9, outputs=pairs if opts == "mat" else None, inner=inner, outer=outer)
+        for res, plan in results:
+            assert plan.sampled_network == (mode == "SAMPLED")
+            assert res["sampled_network"] == (mode == "SAMPLED") and res["network_fallbacks"] == 0, res
+            if exp is not None:
+                assert res["global_matches"] == exp
+            if opts == "hot":
+                assert res["split_partitions"] >= 1
+        got[mode] = results[0][0]["global_matches"]
+        if opts != "hot":  # (a split partition's inner side is replicated to its helpers)
+            assert sum(r[0]["inner_received"] for r in results) == G_R
+        assert sum(r[0]["outer_received"] for r in results) == G_S
+        if opts == "mat":
+            p = torch.cat([x.cpu() for x in pairs])
+            got[mode + "pairs"] = p[torch.argsort(p[:, 1] * (1 << 32) + p[:, 0])]
+    assert got["SAMPLED"] == got["EXACT"]
+    if opts == "mat":
+        assert torch.equal(got["SAMPLEDpairs"], got["EXACTpairs"])
+
+
+@pytest.mark.gpu
+def test_sampled_shuffle_overflow_falls_back(C, cuda):
+    """Rank 0's tuples are laid out against the sample (every 4096-tuple tile
+    holds one network digit, so the sampled tiles miss most digits); rank 1's
+    are shuffled.  Rank 0's slices overflow; the flag rides in the
+    fills all-gather, so BOTH ranks abandon the sampled pass at the same point,
+    re-run exactly (one network fallback each) and stay exact afterwards."""
+    import torch
+    n_ranks, n = 2, 1 << 22
+    group = C.InProcessGroup(n_ranks)
+    out, errs = [None] * n_ranks, []
+
+    def work(r):
+        try:
+            i = torch.arange(n, device="cuda")
+            g = i + r * n
+            keys = g * 512 + (i // 4096) % 512  # unique over ranks; digit = tile index mod 512
+            if r == 1:
+                keys = keys[torch.randperm(n, device="cuda")]
+            R = torch.stack([keys, g], 1).contiguous()
+            S = torch.stack([keys.flip(0), g], 1).contiguous()
+            ctx = C.ExecContext("device", 0, group.communicator(r))
+            cfg = C.JoinConfig()
+            cfg.network_histogram = C.HistogramMode.SAMPLED
+            cfg.bitmap_join = False
+            cfg.key_hashing = C.KeyHashing.OFF
+            cfg.network_bits = 9
+            cfg.wire_codec = C.WireCodecMode.ON
+            cfg.max_partition_blocks = 16  # 64 tiles per workgroup, a few of them sampled
+            j = C.HashJoin(C.Relation.from_tensor(R, n * n_ranks), C.Relation.from_tensor(S, n * n_ranks), ctx, cfg)
+            assert j.plan.sampled_network, j.plan
+            first, second = j.run(), j.run()
+            out[r] = (first, second)
+        except Exception as e:
+            errs.append((r, repr(e)))
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(n_ranks)]
+    [t.start() for t in ts]
+    [t.join(timeout=600) for t in ts]
+    assert not errs, errs
+    for first, second in out:
+        assert first["network_fallbacks"] == 1 and not first["sampled_network"]
+        assert first["global_matches"] == n * n_ranks
+        assert second["network_fallbacks"] == 0 and not second["sampled_network"]
+        assert second["global_matches"] == n * n_ranks
 
 
 def _balance(C, n_ranks, loc, G_R, G_S, assignment, split, outer, inner=None, network_bits=0, chunks=1):
