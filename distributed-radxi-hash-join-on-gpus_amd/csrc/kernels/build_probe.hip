@@ -1421,6 +1421,206 @@ __global__ __launch_bounds__(T, MINW) void bpKeySpanKernel(KsSrc<T, K, SPLIT> R,
   if (t == 0 && total) atomicAdd(result, total);
 }
 
+// ------------------------------------------- key-only spans, quotient table (v3)
+// KernelVariants::keyCount 8.  The v2 table above spends its LDS cycles on
+// 8-byte keys: a probe is a fill-counter read plus two random ds_read_b128
+// (33 LDS cycles per wave with the measured 3.0-3.6 conflict cycles per
+// instruction; PMC: the LDS pipe ~80 % busy, the kernel at 3.7 TB/s).  Here a
+// key fragment of f <= 32 + KQ_BITS bits (63-bit keys after 10 + 9 radix bits:
+// f = 44) is split into
+//   e = frag >> s (32 bits, s = f - 32)   and   lo = frag's low s bits;
+//   bucket b = (lo ^ h(e)) mod 2^KQ_BITS   (h: multiplicative hash of e),
+// and the bucket stores only v = e ^ salt(b): (b, v) determines the fragment
+// (lo = b ^ h(e) on its low s bits), so equal (b, v) <=> equal keys, and a
+// slot is 4 bytes.  Buckets are two u32 slots = one 8-byte ds_read_b64 per
+// probe (two 32-lane groups, ~7 cycles with conflicts); 4096 buckets (32 KiB)
+// hold <= 2048 inner keys at load <= 1/4, so a bucket is full -- and the probe
+// reads the next one -- for ~1-2 % of keys.  Slots are filled by LDS CAS
+// (slot 0, then 1, then the next bucket), so a probe stops at the first
+// bucket whose slot 1 is empty and sees every duplicate of its key.
+// The empty marker KQ_EMPTY is a legal v: such "escape" keys (one fragment per
+// bucket, chance 2^-32 per random key) go to a small side list that escape
+// probes scan; more than KQ_SIDE escapes in one span set a flag and the host
+// re-runs the join's build/probe on the v2 kernel (BuildProbe::collect).
+// Slots written by a span's build are reset by the same lanes after its probe:
+// no per-span table clear.
+constexpr uint32_t KQ_BITS = 12;
+constexpr uint32_t KQ_BUCKETS = 1u << KQ_BITS;
+constexpr uint32_t KQ_EMPTY = 0xFFFFFFFFu;
+constexpr uint32_t KQ_SIDE = 64;
+constexpr uint32_t KQ_NONE = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t kqSalt(uint32_t b) { return (b + 1u) * 0x85EBCA77u; }
+
+// (bucket, stored value) of a fragment; s = fragment bits above 32 (<= KQ_BITS).
+__device__ __forceinline__ void kqKey(uint64_t frag, uint32_t s, uint32_t &b, uint32_t &v) {
+  const uint32_t e = (uint32_t)(frag >> s);
+  const uint32_t lo = (uint32_t)frag & ((1u << s) - 1u);
+  b = (lo ^ ((e * 0x9E3779B1u) >> (32 - KQ_BITS))) & (KQ_BUCKETS - 1);
+  v = e ^ kqSalt(b);
+}
+
+// One batch of T x K outer fragments (the first `valid` counted): all K
+// bucket reads in flight, then the rare walks past full buckets.
+template <int T, int K>
+__device__ __forceinline__ uint32_t kqProbeBatch(const uint64_t (&pv)[K], uint32_t valid, uint32_t s,
+                                                 const uint2 *tab2, const unsigned long long *side, uint32_t nSide) {
+  uint32_t bk[K], v[K];
+  uint2 x[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    kqKey(pv[k], s, bk[k], v[k]);
+    x[k] = tab2[bk[k]];
+  }
+  uint32_t matches = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    uint32_t c = (uint32_t)(x[k].x == v[k]) + (uint32_t)(x[k].y == v[k]);
+    uint32_t b = bk[k];
+    uint2 y = x[k];
+    while (y.y != KQ_EMPTY) {  // bucket full: keys placed past it continue in the next one
+      b = (b + 1) & (KQ_BUCKETS - 1);
+      y = tab2[b];
+      c += (uint32_t)(y.x == v[k]) + (uint32_t)(y.y == v[k]);
+    }
+    if (v[k] == KQ_EMPTY) {  // escape: the table's empty slots said nothing
+      c = 0;
+      for (uint32_t j = 0; j < nSide; ++j) c += side[j] == pv[k];
+    }
+    matches += (uint32_t)(k * T) + threadIdx.x < valid ? c : 0u;
+  }
+  return matches;
+}
+
+size_t bpKeyQuotientLdsBytes() {
+  return KQ_BUCKETS * 8 + KQ_SIDE * 8 + 16 + KS_CHUNK * sizeof(BPSpan) + 16 * 8 + 16;
+}
+
+template <int T, int K, int MINW>
+__global__ __launch_bounds__(T, MINW) void bpKeyQuotientKernel(KsSrc<T, K, true> R, KsSrc<T, K, true> S,
+                                                               const BPSpan *__restrict__ spans,
+                                                               const uint32_t *__restrict__ nSpansPtr,
+                                                               uint32_t capacity, uint32_t *__restrict__ queue,
+                                                               uint32_t s, unsigned long long *__restrict__ result,
+                                                               unsigned long long *__restrict__ sideOverflow) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t *tab = reinterpret_cast<uint32_t *>(smem);  // [bucket][2]
+  const uint2 *tab2 = reinterpret_cast<const uint2 *>(smem);
+  unsigned long long *side = reinterpret_cast<unsigned long long *>(tab + 2 * KQ_BUCKETS);
+  uint32_t *sideN = reinterpret_cast<uint32_t *>(side + KQ_SIDE);
+  BPSpan *desc = reinterpret_cast<BPSpan *>(sideN + 4);
+  unsigned long long *wsum = reinterpret_cast<unsigned long long *>(desc + KS_CHUNK);
+  uint32_t *qbase = reinterpret_cast<uint32_t *>(wsum + T / WAVE);
+  constexpr uint32_t BATCH = T * K;
+  const uint32_t t = threadIdx.x;
+  const uint32_t n = min(*nSpansPtr, capacity);
+  {
+    uint4 *t4 = reinterpret_cast<uint4 *>(tab);
+    for (uint32_t i = t; i < KQ_BUCKETS / 2; i += T) t4[i] = make_uint4(KQ_EMPTY, KQ_EMPTY, KQ_EMPTY, KQ_EMPTY);
+    if (t == 0) *sideN = 0;
+  }
+  uint64_t matches = 0;
+  bool overflow = false;
+  uint64_t rv[K], sv[K], nrv[K], nsv[K];
+  for (;;) {
+    if (t == 0) *qbase = atomicAdd(queue, KS_CHUNK);
+    __syncthreads();  // (first round: also orders the table clear before any build)
+    const uint32_t base = __builtin_amdgcn_readfirstlane(*qbase);
+    if (base >= n) break;
+    const uint32_t cnt = min(KS_CHUNK, n - base);
+    if (t < cnt) desc[t] = spans[base + t];
+    __syncthreads();
+    {
+      const BPSpan d = desc[0];
+      R.load(d.rb, d.nr, rv);
+      S.load(d.sb, d.ns, sv);
+    }
+    for (uint32_t i = 0; i < cnt; ++i) {
+      const uint64_t sb = __builtin_amdgcn_readfirstlane((uint32_t)desc[i].sb) |
+                          ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(desc[i].sb >> 32)) << 32);
+      const uint32_t nr = __builtin_amdgcn_readfirstlane(desc[i].nr);
+      const uint32_t ns = __builtin_amdgcn_readfirstlane(desc[i].ns);
+      // ---- build (nr <= BATCH: one batch, from registers)
+      uint32_t pos[K];
+      {
+        uint32_t bk[K], v[K], old[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          kqKey(rv[k], s, bk[k], v[k]);
+          const bool valid = (uint32_t)(k * T) + t < nr;
+          pos[k] = valid ? 2 * bk[k] : KQ_NONE;
+          if (valid && v[k] == KQ_EMPTY) {  // escape: side list
+            const uint32_t at = atomicAdd(sideN, 1u);
+            if (at < KQ_SIDE) side[at] = rv[k];
+            pos[k] = KQ_NONE;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) old[k] = pos[k] != KQ_NONE ? atomicCAS(&tab[pos[k]], KQ_EMPTY, v[k]) : KQ_EMPTY;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          if (old[k] == KQ_EMPTY) continue;  // placed (or nothing to place)
+          uint32_t p = pos[k] + 1;
+          while (atomicCAS(&tab[p], KQ_EMPTY, v[k]) != KQ_EMPTY)
+            p = (p & 1) ? ((((p >> 1) + 1) & (KQ_BUCKETS - 1)) << 1) : p + 1;
+          pos[k] = p;
+        }
+      }
+      __syncthreads();
+      const uint32_t nSide = min(*sideN, KQ_SIDE);
+      overflow |= *sideN > KQ_SIDE;
+      // ---- the next span's words stream in while this one probes
+      if (i + 1 < cnt) {
+        const BPSpan d = desc[i + 1];
+        R.load(d.rb, d.nr, nrv);
+        S.load(d.sb, d.ns, nsv);
+      }
+      // ---- probe: first batch from registers, later batches loaded inline
+      matches += kqProbeBatch<T, K>(sv, ns, s, tab2, side, nSide);
+      for (uint32_t b0 = BATCH; b0 < ns; b0 += BATCH) {
+        uint64_t xv[K];
+        S.load(sb + b0, ns - b0, xv);
+        matches += kqProbeBatch<T, K>(xv, ns - b0, s, tab2, side, nSide);
+      }
+      __syncthreads();  // every probe of this span is done
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        if (pos[k] != KQ_NONE) tab[pos[k]] = KQ_EMPTY;
+      if (t == 0) *sideN = 0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        rv[k] = nrv[k];
+        sv[k] = nsv[k];
+      }
+      __syncthreads();  // table empty again before the next build
+    }
+  }
+  const unsigned long long total = blockReduceSum<T, unsigned long long>((unsigned long long)matches, wsum);
+  if (t == 0 && total) atomicAdd(result, total);
+  if (overflow && t == 0) atomicOr(sideOverflow, 1ull);
+}
+
+bool bpKeyQuotientFits(const BPArgs &a) {
+  return a.keyOnly && a.split && !a.materialize && !a.wide && a.keyFragBits >= 1 &&
+         a.keyFragBits <= 32 + KQ_BITS && a.rChunk <= 2048;
+}
+
+static void launchKeyQuotient(const BPArgs &a, const BPSpan *spans, const uint32_t *nSpans, uint32_t capacity,
+                              uint32_t *queue, hipStream_t st) {
+  constexpr int T = 512, K = 4;
+  HJ_CHECK(bpKeyQuotientFits(a), "buildProbeKeySpans: quotient table needs split key-only words of <= %u bits "
+           "(got %u) and rChunk <= 2048 (got %u)", 32 + KQ_BITS, a.keyFragBits, a.rChunk);
+  HJ_CHECK(a.sideOverflow, "buildProbeKeySpans: quotient table needs a side-overflow flag");
+  const uint32_t s = a.keyFragBits > 32 ? a.keyFragBits - 32 : 0;
+  const size_t lds = bpKeyQuotientLdsBytes();
+  const uint32_t perCu = (uint32_t)std::max<size_t>(1, std::min<size_t>(4, (160 * 1024) / lds));
+  const dim3 grid(std::min<uint32_t>(ceilDiv(capacity, KS_CHUNK), 256 * perCu));
+  HIP_CHECK(hipMemsetAsync(queue, 0, sizeof(uint32_t), st));
+  hipLaunchKernelGGL((bpKeyQuotientKernel<T, K, 8>), grid, dim3(T), lds, st, KsSrc<T, K, true>{a.R, a.Rhi},
+                     KsSrc<T, K, true>{a.S, a.Shi}, spans, nSpans, capacity, queue, s, a.result, a.sideOverflow);
+  HIP_CHECK_LAUNCH();
+}
+
 size_t bpKeySpanLdsBytes(uint32_t maxR) {
   const uint64_t slots = uint64_t(1) << ceilLog2(2ull * maxR);
   return slots * 8 + (slots / BPK_SLOTS) * 4 + KS_CHUNK * sizeof(BPSpan) + 16 * 8 + 16;
@@ -1433,6 +1633,10 @@ void buildProbeKeySpans(const BPArgs &a, const BPSpan *spans, const uint32_t *nS
   HJ_CHECK(a.keyOnly && !a.materialize && !a.wide, "buildProbeKeySpans: key-only counting joins only");
   HJ_CHECK(!a.split || (a.Rhi && a.Shi), "buildProbeKeySpans: split layout without high columns");
   HJ_CHECK(a.rChunk <= (uint32_t)(T * K), "buildProbeKeySpans: rChunk %u above one %d-word batch", a.rChunk, T * K);
+  if (a.keyCount == 8 && bpKeyQuotientFits(a)) {
+    launchKeyQuotient(a, spans, nSpans, capacity, queue, s);
+    return;
+  }
   const size_t lds = bpKeySpanLdsBytes(a.rChunk);
   HJ_CHECK(lds <= 160 * 1024, "buildProbeKeySpans: LDS %zu B exceeds 160 KiB (rChunk=%u)", lds, a.rChunk);
   const uint32_t perCu = (uint32_t)std::max<size_t>(1, std::min<size_t>(4, (160 * 1024) / lds));
@@ -1442,7 +1646,7 @@ void buildProbeKeySpans(const BPArgs &a, const BPSpan *spans, const uint32_t *nS
   hipLaunchKernelGGL((bpKeySpanKernel<T, K, H, 8, SPLIT, SOA>), grid, dim3(T), lds, s,                            \
                      KsSrc<T, K, SPLIT>{a.R, SPLIT ? a.Rhi : nullptr}, KsSrc<T, K, SPLIT>{a.S, SPLIT ? a.Shi : nullptr}, \
                      spans, nSpans, capacity, queue, a.rChunk, a.result)
-  const bool soa = a.keyCount == 7;
+  const bool soa = a.keyCount == 7 || a.keyCount == 8;
   if (a.split) {
     if (soa) HJ_KS(true, true); else HJ_KS(true, false);
   } else {

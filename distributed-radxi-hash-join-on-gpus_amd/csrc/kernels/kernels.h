@@ -332,8 +332,14 @@ struct BPArgs {
   const ulonglong2 *rowsB = nullptr;  // outer payload rows
   uint64_t offA = 0, offB = 0;        // rid of row 0 of each column
   ulonglong2 *outRows = nullptr;
+  // Key-only words: bits of the fragment above both radix digits (0 =
+  // unknown); the quotient-table kernel (keyCount 8) needs <= 44.
+  uint32_t keyFragBits = 0;
+  // Quotient-table kernel: set to nonzero when a span had more escape keys
+  // than its side list holds (the count is then void: re-run on keyCount 7).
+  unsigned long long *sideOverflow = nullptr;
   // Kernel variants (KernelVariants::keyCount / rowsLds).
-  uint32_t keyCount = 7;
+  uint32_t keyCount = 8;
   uint32_t rowsLds = 1;
 };
 // Payload columns + output of a fused materializing join (HashJoin::setRowSink).
@@ -372,6 +378,9 @@ void bpEmitSpans(const BPArgs &a, const uint32_t *counts, const uint32_t *offset
                  hipStream_t s);
 void buildProbeKeySpans(const BPArgs &a, const BPSpan *spans, const uint32_t *nSpans, uint32_t capacity,
                         uint32_t *queue, hipStream_t s);
+// keyCount 8 (quotient table, build_probe.hip) applies: split key-only words
+// of <= 44 fragment bits, rChunk <= 2048.
+bool bpKeyQuotientFits(const BPArgs &a);
 
 // Single-level counting join of unique inner keys (bitmap_join.hip): one
 // workgroup per network partition sets a 2^bits LDS bitmap from the inner

@@ -61,7 +61,11 @@ void BuildProbe::configure() {
   args.wide = plan.wide;
   args.keyOnly = plan.keyOnly;
   args.materialize = plan.materialize;
-  args.keyCount = plan.variants.keyCount;
+  args.keyCount = quotientFallback && plan.variants.keyCount == 8 ? 7 : plan.variants.keyCount;
+  if (plan.keyOnly) {
+    const uint32_t passBits = plan.networkBits + wi->getLocalBits();
+    args.keyFragBits = plan.keyBits > passBits ? plan.keyBits - passBits : 1;
+  }
   args.rowsLds = plan.variants.rowsLds;
   if (wi->getPartitionedHi()) {
     JOIN_ASSERT(wo->getPartitionedHi(), "BuildProbe", "one side split, the other not");
@@ -149,6 +153,7 @@ void BuildProbe::execute() {
     auto *spans = ws.getArray<kernels::BPSpan>(capacity);
     uint32_t *queue = ws.getArray<uint32_t>(1);
     kernels::bpEmitSpans(args, counts, offsets, spans, capacity, ctx->stream());
+    args.sideOverflow = counters + 3;  // quotient table: escape side list overflowed
     tl.beginSplit("BPKERNEL", "BPBUILD", wb, "BPPROBE", wp, ctx->stream());
     kernels::buildProbeKeySpans(args, spans, nItems, capacity, queue, ctx->stream());
     hipEvent_t done = tl.mark(ctx->stream());
@@ -212,6 +217,10 @@ bool BuildProbe::collect() {
   std::memcpy(&items, &h[2], sizeof(items));
   workItems = items;
   bool again = false;
+  if (args.sideOverflow && h[3]) {  // too many escape keys in one span: count on the v2 table
+    quotientFallback = true;
+    again = true;
+  }
   if (items > capacity) {
     capacity = items;
     again = true;

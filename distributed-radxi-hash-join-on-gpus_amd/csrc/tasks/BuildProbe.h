@@ -65,13 +65,16 @@ class BuildProbe : public Task {
   kernels::BPArgs args;
   uint32_t capacity = 0;
   uint64_t outputCapacity = 0;
-  unsigned long long *counters = nullptr;  // [0] matches [1] out cursor [2] item count (u32)
+  // [0] matches [1] out cursor [2] item count (u32) [3] materialize: count-pass
+  // matches / key spans: quotient-table side-list overflow flag
+  unsigned long long *counters = nullptr;
   unsigned long long *countersBack = nullptr;  // pinned copy, enqueued at the end of execute()
   ulonglong2 *outPairs = nullptr;
   std::vector<uint64_t> refBounds;  // reference ctor: partition begin arrays
   uint64_t matches = 0, outputCount = 0;
   uint32_t workItems = 0;
   bool reference = false, overflowOut = false, fused = false;
+  bool quotientFallback = false;  // a span overflowed the quotient table's side list: keyCount 7 from now on
   const kernels::RowSink *sink = nullptr;
   uint64_t hostCursor = 0;
 };

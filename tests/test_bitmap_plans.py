@@ -300,7 +300,7 @@ def test_sparse64_generator(C):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", ["6", "6s", "7", "7s", "1", "0", "2", "3", "4", "5"])
+@pytest.mark.parametrize("variant", ["8s", "6", "6s", "7", "7s", "1", "0", "2", "3", "4", "5"])
 def test_key_only_count_variants(C, variant):
     """Every key-only count kernel variant against a torch reference, with heavily repeated inner keys (Zipf over sparse
     63-bit keys: long overflow chains through the next buckets)."""
@@ -317,17 +317,71 @@ def test_key_only_count_variants(C, variant):
         S.generate(outer, 0)
         cfg = C.JoinConfig()
         cfg.key_count = int(variant[0])
-        # 6 / 7: span kernel (AoS / SoA buckets); "s": over the split (u32 +
-        # u16) local output; the item kernels (0-5) read unsplit words only
+        # 6 / 7: span kernel (AoS / SoA buckets); 8: quotient table (44-bit
+        # fragments: 63-bit keys above 10 + 9 radix bits); "s": over the split
+        # (u32 + u16) local output; the item kernels (0-5) read unsplit words only
         split = variant.endswith("s")
         cfg.split_local = split
-        if split:  # 63-bit keys: the fragment above 8 + 7 radix bits fits the 48-bit split
+        if variant == "8s":
+            cfg.network_bits, cfg.local_bits = 10, 9
+        elif split:  # 63-bit keys: the fragment above 8 + 7 radix bits fits the 48-bit split
             cfg.network_bits, cfg.local_bits = 8, 7
         j = C.HashJoin(R, S, ctx, cfg)
         assert j.plan.key_only and j.plan.split_local == split
         exp = ref_join_count(R.to_tensor()[:, 0].cpu(), S.to_tensor()[:, 0].cpu())
         for _ in range(2):
             assert j.run()["global_matches"] == exp, (variant, G_R, theta)
+
+
+def quotient_escape_fragments(n, first_bucket=0):
+    """Fragments the quotient table (build_probe.hip, bpKeyQuotientKernel) can
+    only hold in its side list: 44-bit fragments f (63-bit keys above 10 + 9
+    radix bits) whose stored value e ^ salt(b) is the empty marker, one per
+    bucket b: e = ~salt(b), lo = b ^ h(e)."""
+    M = 0xFFFFFFFF
+    out = []
+    for b in range(first_bucket, first_bucket + n):
+        e = ~(((b + 1) * 0x85EBCA77) & M) & M
+        lo = (b ^ (((e * 0x9E3779B1) & M) >> 20)) & 0xFFF
+        out.append((e << 12) | lo)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_escape,dup", [(20, 1), (40, 3), (100, 1)])
+def test_key_quotient_escapes(C, n_escape, dup):
+    """Quotient-table build/probe with keys whose stored value is the table's
+    empty marker, all in one final partition: up to 64 per span are counted
+    through the side list; more (100 distinct, or 40 keys x 3 copies) set the
+    overflow flag and the build/probe re-runs on the v2 table.  Counts equal a
+    torch oracle either way."""
+    import torch
+    from helpers import ref_join_count
+    g = torch.Generator().manual_seed(n_escape * 7 + dup)
+    part = 0x2A5F3  # one (network, local) digit pair: the escapes share a span
+    esc = torch.tensor(quotient_escape_fragments(n_escape, first_bucket=17), dtype=torch.int64)
+    esc_keys = (esc << 19) | part
+    other = torch.randint(1 << 40, (1 << 62) - 1, (400_000,), generator=g, dtype=torch.int64).unique()
+    rk = torch.cat([esc_keys.repeat(dup), other])
+    rk = rk[torch.randperm(rk.numel(), generator=g)]
+    sk = torch.cat([esc_keys.repeat(5), other[torch.randint(0, other.numel(), (600_000,), generator=g)],
+                    (esc + 1) << 19 | part])  # + near misses in the same span
+    sk = sk[torch.randperm(sk.numel(), generator=g)]
+    exp = ref_join_count(rk, sk)
+    rows = lambda k: torch.stack([k, torch.arange(k.numel())], 1).contiguous().cuda()
+    R, S = rows(rk), rows(sk)
+    ctx = C.ExecContext("device", 0, C.LocalCommunicator())
+    cfg = C.JoinConfig()
+    cfg.network_bits, cfg.local_bits = 10, 9
+    cfg.key_hashing = C.KeyHashing.OFF
+    j = C.HashJoin(C.Relation.from_tensor(R, R.shape[0]), C.Relation.from_tensor(S, S.shape[0]), ctx, cfg)
+    assert j.plan.key_only and j.plan.split_local and j.plan.key_bits == 63, j.plan
+    over = n_escape * dup > 64
+    for i in range(2):
+        res = j.run()
+        assert res["global_matches"] == exp, (n_escape, dup, res["global_matches"], exp)
+        # the fallback sticks to the BuildProbe task of one run only
+        assert res["reruns"] == (1 if over else 0), res["reruns"]
 
 
 @pytest.mark.parametrize("dev", devices())
