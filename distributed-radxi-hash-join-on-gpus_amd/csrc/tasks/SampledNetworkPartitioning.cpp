@@ -3,6 +3,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <map>
+#include <tuple>
 
 #include "../memory/Arena.h"
 #include "../performance/Timeline.h"
@@ -24,33 +26,71 @@ SampledNetworkPartitioning::SampledNetworkPartitioning(data::Relation *innerRela
 
 SampledNetworkPartitioning::~SampledNetworkPartitioning() = default;  // events belong to the context pool
 
-void SampledNetworkPartitioning::sample() {
-  const uint32_t F = 1u << plan.networkBits;
-  const kernels::KeyMix mix{plan.keyMix ? 1u : 0u, plan.keyBits};
-  for (Side &s : sides) {
-    const char *key = &s == &sides[0] ? "HILOCAL" : "HOLOCAL";
-    ctx->timeline().begin(key, ctx->stream());
-    const uint64_t n = s.relation->getLocalSize();
-    s.geom = kernels::partitionGeometry(n, maxBlocks);
-    s.geom.ipt = plan.variants.netIpt;
-    s.geom.nth = plan.variants.netThreads;
-    s.stride = kernels::sampleStrideFor(s.geom, n, F, sampleStride);
-    s.groupTotalsDev = ctx->workspace().getArray<uint64_t>((uint64_t)CLAIM_GROUPS * F);
-    if (s.stride > 1) {
-      kernels::netSampledTotals(s.relation->getData(), n, plan.networkBits, s.geom, s.groupTotalsDev, ctx->stream(),
-                                mix, s.stride);
-    } else {
-      uint32_t *blockHist = ctx->workspace().getArray<uint32_t>((uint64_t)F * s.geom.blocks);
-      kernels::netHistogram(s.relation->getData(), n, plan.networkBits, s.geom, blockHist, ctx->stream(), mix, 1);
-      kernels::netGroupTotals(blockHist, F, s.geom.blocks, s.groupTotalsDev, ctx->stream());
+// Geometry, sample stride, scale and capacity bound of one side: pure
+// functions of the size (host loops over every block and sampled tile, ~20 us),
+// computed once per thread and size.
+const SampledNetworkPartitioning::SidePlan &SampledNetworkPartitioning::sidePlan(uint64_t n) const {
+  struct Key {
+    uint64_t n;
+    uint32_t maxBlocks, bits, stride, ipt, nth;
+    bool operator<(const Key &o) const {
+      return std::tie(n, maxBlocks, bits, stride, ipt, nth) < std::tie(o.n, o.maxBlocks, o.bits, o.stride, o.ipt, o.nth);
     }
-    ctx->timeline().end(key, ctx->stream());
-    s.sampled = ctx->staging().getArray<uint64_t>((uint64_t)CLAIM_GROUPS * F);
-    HIP_CHECK(hipMemcpyAsync(s.sampled, s.groupTotalsDev, (size_t)CLAIM_GROUPS * F * 8, hipMemcpyDeviceToHost,
-                             ctx->stream()));
-    if (!s.sampledReady) s.sampledReady = ctx->acquireEvent();
-    HIP_CHECK(hipEventRecord(s.sampledReady, ctx->stream()));
+  };
+  thread_local std::map<Key, SidePlan> cache;
+  const uint32_t F = 1u << plan.networkBits;
+  const Key k{n, maxBlocks, plan.networkBits, sampleStride, plan.variants.netIpt, plan.variants.netThreads};
+  auto it = cache.find(k);
+  if (it != cache.end()) return it->second;
+  if (cache.size() > 64) cache.clear();
+  SidePlan sp;
+  sp.geom = kernels::partitionGeometry(n, maxBlocks);
+  sp.geom.ipt = plan.variants.netIpt;
+  sp.geom.nth = plan.variants.netThreads;
+  sp.stride = kernels::sampleStrideFor(sp.geom, n, F, sampleStride);
+  sp.sc = kernels::sampleScale(sp.geom, n, sp.stride, sp.stride == 1);
+  sp.bound = kernels::sampledLayoutCapacityBound(sp.sc, F);
+  return cache.emplace(k, sp).first->second;
+}
+
+// Sampled totals of both sides (one launch when both are sampled; a side too
+// small to sample gets an exact histogram), then each side's bounded claim
+// slices are laid out on the device: nothing here waits for the GPU.
+void SampledNetworkPartitioning::sample() {
+  const uint32_t F = 1u << plan.networkBits, G = CLAIM_GROUPS;
+  const kernels::KeyMix mix{plan.keyMix ? 1u : 0u, plan.keyBits};
+  const hipStream_t st = ctx->stream();
+  uint64_t *totals = ctx->workspace().getArray<uint64_t>((uint64_t)2 * G * F);  // adjacent: one clear
+  kernels::SampledInput in[2];
+  bool bothSampled = true;
+  for (int k = 0; k < 2; ++k) {
+    Side &s = sides[k];
+    const uint64_t n = s.relation->getLocalSize();
+    const SidePlan &sp = sidePlan(n);
+    s.geom = sp.geom;
+    s.stride = sp.stride;
+    s.sc = sp.sc;
+    s.capacityTotal = sp.bound;
+    s.groupTotalsDev = totals + (size_t)k * G * F;
+    in[k] = kernels::SampledInput{s.relation->getData(), n, s.geom, s.stride, s.groupTotalsDev};
+    bothSampled = bothSampled && s.stride > 1;
   }
+  // One span for both histograms, charged to HILOCAL / HOLOCAL by tuples.
+  ctx->timeline().beginSplit("HLOCAL", "HILOCAL", (double)in[0].n, "HOLOCAL", (double)in[1].n, st);
+  if (bothSampled) {
+    kernels::netSampledTotals(in, 2, plan.networkBits, st, mix);
+  } else {
+    for (int k = 0; k < 2; ++k) {
+      if (in[k].stride > 1) {
+        kernels::netSampledTotals(&in[k], 1, plan.networkBits, st, mix);
+        continue;
+      }
+      uint32_t *blockHist = ctx->workspace().getArray<uint32_t>((uint64_t)F * in[k].geom.blocks);
+      kernels::netHistogram(in[k].data, in[k].n, plan.networkBits, in[k].geom, blockHist, st, mix, 1);
+      kernels::netGroupTotals(blockHist, F, in[k].geom.blocks, in[k].totals, st);
+    }
+  }
+  ctx->timeline().end("HLOCAL", st);
 }
 
 void SampledNetworkPartitioning::layout() {
@@ -60,74 +100,38 @@ void SampledNetworkPartitioning::layout() {
 
 void SampledNetworkPartitioning::layoutSide(int k) {
   const uint32_t F = 1u << plan.networkBits, G = CLAIM_GROUPS;
-  {
-    Side &s = sides[k];
-    HIP_CHECK(hipEventSynchronize(s.sampledReady));
-    const uint64_t n = s.relation->getLocalSize();
-    // Tuples each group scatters, and how many of them the sample read.
-    const kernels::SampleScale sc = kernels::sampleScale(s.geom, n, s.stride, false);
-    s.start.assign((size_t)G * F, 0);
-    s.cap.assign((size_t)G * F, 0);
-    uint64_t cur = 0;
-    for (uint32_t d = 0; d < F; ++d)
-      for (uint32_t g = 0; g < G; ++g) {
-        const size_t i = (size_t)g * F + d;
-        double est = 0;
-        if (sc.seen[g] > 0) est = (double)s.sampled[i] * sc.total[g] / sc.seen[g];
-        // Sampling error of a count scaled by total/seen is ~sqrt(est * total/seen)
-        // (at least one sample's worth); 6 sigma + 2% + a fixed floor keeps
-        // overflows (and their exact re-run) rare.
-        const double scale = sc.seen[g] > 0 ? sc.total[g] / sc.seen[g] : 1.0;
-        const double margin = sc.sigmas * std::sqrt(std::max(est, scale) * scale) + sc.frac * est + sc.floor;
-        // whole 128-byte lines per slice (16 tuples): slices never share a line
-        const uint64_t cap = (std::min<uint64_t>((uint64_t)std::ceil(est + margin), (uint64_t)sc.total[g]) + 15) & ~15ull;
-        s.start[i] = cur;
-        s.cap[i] = cap;
-        cur += cap;
-      }
-    s.capacityTotal = cur;
-    // Claims may run past a slice end by up to n before the overflow is seen:
-    // 32-bit cursors only if even that cannot wrap.
-    s.narrow = kernels::cursorsNarrow(cur + n);
-    // Plan skeleton (filled after the scatter); the window is sized by capacity.
-    histograms::ExchangePlan &x = s.xp;
-    x = histograms::ExchangePlan();
-    x.numberOfNodes = 1;
-    x.nodeId = 0;
-    x.partitions = F;
-    x.chunks = 1;
-    x.gapped = true;
-    x.owned.resize(F);
-    x.localIndex.resize(F);
-    for (uint32_t p = 0; p < F; ++p) {
-      x.owned[p] = p;
-      x.localIndex[p] = (int32_t)p;
-    }
-    x.sendTotal = n;
-    x.scatterTotal = n;
-    x.recvTotal = 0;
-    s.window.reset(new data::Window(x, cur, ctx, plan.wide, plan.fragments ? 4u : 0u));
-    // Claim cursors (slice starts) and slice ends, in the scatter's cursor width.
-    const size_t cb = s.narrow ? 4 : 8;
-    s.gcur = ctx->workspace().get((size_t)G * F * cb);
-    s.gend = ctx->workspace().get((size_t)G * F * cb);
-    // Asynchronous uploads from member vectors (no host round trip before the scatter).
-    if (s.narrow) {
-      s.cur32.resize((size_t)G * F);
-      s.end32.resize((size_t)G * F);
-      for (size_t i = 0; i < s.cur32.size(); ++i) {
-        s.cur32[i] = (uint32_t)s.start[i];
-        s.end32[i] = (uint32_t)(s.start[i] + s.cap[i]);
-      }
-      ctx->copy(s.gcur, s.cur32.data(), s.cur32.size() * 4, true, false);
-      ctx->copy(s.gend, s.end32.data(), s.end32.size() * 4, true, false);
-    } else {
-      s.end64.resize((size_t)G * F);
-      for (size_t i = 0; i < s.end64.size(); ++i) s.end64[i] = s.start[i] + s.cap[i];
-      ctx->copy(s.gcur, s.start.data(), s.end64.size() * 8, true, false);
-      ctx->copy(s.gend, s.end64.data(), s.end64.size() * 8, true, false);
-    }
+  Side &s = sides[k];
+  const uint64_t n = s.relation->getLocalSize();
+  // Claims may run past a slice end by up to n before the overflow is seen:
+  // 32-bit cursors only if even that cannot wrap.
+  s.narrow = kernels::cursorsNarrow(s.capacityTotal + n);
+  // Plan skeleton (filled after the scatter); the window is sized by the
+  // layout's capacity bound.
+  histograms::ExchangePlan &x = s.xp;
+  x = histograms::ExchangePlan();
+  x.numberOfNodes = 1;
+  x.nodeId = 0;
+  x.partitions = F;
+  x.chunks = 1;
+  x.gapped = true;
+  x.owned.resize(F);
+  x.localIndex.resize(F);
+  for (uint32_t p = 0; p < F; ++p) {
+    x.owned[p] = p;
+    x.localIndex[p] = (int32_t)p;
   }
+  x.sendTotal = n;
+  x.scatterTotal = n;
+  x.recvTotal = 0;
+  s.window.reset(new data::Window(x, s.capacityTotal, ctx, plan.wide, plan.fragments ? 4u : 0u));
+  // Slice starts, claim cursors and slice ends ([G][F] each, adjacent: one
+  // read-back after the scatter), laid out on the device from the totals.
+  const size_t cb = s.narrow ? 4 : 8, per = (size_t)G * F * cb;
+  s.gstart = ctx->workspace().get(3 * per);
+  s.gcur = static_cast<uint8_t *>(s.gstart) + per;
+  s.gend = static_cast<uint8_t *>(s.gstart) + 2 * per;
+  kernels::netSampledLayout(s.groupTotalsDev, F, s.sc, s.gstart, s.gcur, s.gend, s.narrow,
+                            ctx->workspace().getArray<unsigned long long>(1), ctx->stream());
 }
 
 bool SampledNetworkPartitioning::scatter() {
@@ -157,9 +161,9 @@ void SampledNetworkPartitioning::scatterSide(int k) {
     kernels::netScatter(s.relation->getData(), n, plan.networkBits, plan.keyShift, s.geom, 0, s.geom.blocks, s.gcur,
                         static_cast<uint64_t *>(s.window->getData()), ctx->stream(), plan.keyBits, mix, s.gend, nm, !plan.keyOnly);
   ctx->timeline().end(key, ctx->stream());
-  const size_t bytes = (size_t)G * F * (s.narrow ? 4 : 8);
+  const size_t bytes = 3 * (size_t)G * F * (s.narrow ? 4 : 8);  // starts, final cursors, ends
   s.cursorsBack = ctx->staging().get(bytes);
-  HIP_CHECK(hipMemcpyAsync(s.cursorsBack, s.gcur, bytes, hipMemcpyDeviceToHost, ctx->stream()));
+  HIP_CHECK(hipMemcpyAsync(s.cursorsBack, s.gstart, bytes, hipMemcpyDeviceToHost, ctx->stream()));
   if (!s.cursorsReady) s.cursorsReady = ctx->acquireEvent();
   HIP_CHECK(hipEventRecord(s.cursorsReady, ctx->stream()));
 }
@@ -168,16 +172,19 @@ bool SampledNetworkPartitioning::finishSide(int k) {
   const uint32_t F = 1u << plan.networkBits, G = CLAIM_GROUPS;
   Side &s = sides[k];
   HIP_CHECK(hipEventSynchronize(s.cursorsReady));
-  s.fill.assign((size_t)G * F, 0);
+  const size_t m = (size_t)G * F;
+  s.start.resize(m);
+  s.fill.assign(m, 0);
   const uint32_t *c32 = static_cast<const uint32_t *>(s.cursorsBack);
   const uint64_t *c64 = static_cast<const uint64_t *>(s.cursorsBack);
+  auto at = [&](size_t i) -> uint64_t { return s.narrow ? c32[i] : c64[i]; };
   bool ok = true;
   uint64_t sum = 0;
-  for (size_t i = 0; i < s.fill.size(); ++i) {
-    const uint64_t end = s.narrow ? c32[i] : c64[i];  // final claim cursor
-    s.fill[i] = end - s.start[i];
+  for (size_t i = 0; i < m; ++i) {
+    s.start[i] = at(i);
+    s.fill[i] = at(m + i) - s.start[i];  // final claim cursor - slice start
     sum += s.fill[i];
-    if (s.fill[i] > s.cap[i]) ok = false;
+    if (s.fill[i] > at(2 * m + i) - s.start[i]) ok = false;
   }
   HJ_CHECK(sum == s.relation->getLocalSize(), "sampled network pass claimed %lu of %lu tuples", (unsigned long)sum,
            (unsigned long)s.relation->getLocalSize());

@@ -39,10 +39,11 @@ class SampledNetworkPartitioning {
 
   // Per side k (0 = inner, 1 = outer), so the host work of one side overlaps
   // the other side's kernels: sample() enqueues both sampled histograms;
-  // layoutSide(k) waits for side k's counts only and uploads its slices;
+  // layoutSide(k) enqueues side k's slice layout (on the device, from the
+  // sampled totals: no wait) and sizes its window by the layout's bound;
   // scatterSide(k) enqueues the bounded scatter and the read-back of its
-  // final cursors; finishSide(k) waits for those and builds the window plan
-  // (false = a slice overflowed).
+  // slices and final cursors; finishSide(k) waits for those and builds the
+  // window plan (false = a slice overflowed).
   void sample();
   void layoutSide(int k);
   void scatterSide(int k);
@@ -56,24 +57,28 @@ class SampledNetworkPartitioning {
   uint64_t capacity(int side) const { return sides[side].capacityTotal; }
 
  private:
+  struct SidePlan {
+    kernels::PartitionGeometry geom;
+    uint32_t stride = 1;
+    kernels::SampleScale sc{};
+    uint64_t bound = 0;  // sum of the slice capacities can not exceed this
+  };
+  const SidePlan &sidePlan(uint64_t n) const;
   struct Side {
     data::Relation *relation = nullptr;
     kernels::PartitionGeometry geom;
     uint32_t stride = 1;  // sampled tile stride (kernels::sampleStrideFor)
+    kernels::SampleScale sc{};
     histograms::ExchangePlan xp;
     std::unique_ptr<data::Window> window;
-    uint64_t *groupTotalsDev = nullptr;
-    uint64_t *sampled = nullptr;       // [groups][F] sampled counts (pinned staging)
-    void *cursorsBack = nullptr;       // [groups][F] final claim cursors (pinned staging)
-    hipEvent_t sampledReady = nullptr, cursorsReady = nullptr;
-    std::vector<uint64_t> start, cap;  // [groups][F] slice start / capacity (tuples)
-    std::vector<uint64_t> fill;        // [groups][F] claimed after the scatter
-    // Host sources of the asynchronous cursor uploads (alive until the join ends).
-    std::vector<uint32_t> cur32, end32;
-    std::vector<uint64_t> end64;
-    void *gcur = nullptr, *gend = nullptr;
+    uint64_t *groupTotalsDev = nullptr;  // [groups][F] sampled (or exact) counts
+    void *cursorsBack = nullptr;         // [3][groups][F] slice starts, final claim cursors, slice ends (pinned)
+    hipEvent_t cursorsReady = nullptr;
+    std::vector<uint64_t> start;  // [groups][F] slice start (tuples), read back with the cursors
+    std::vector<uint64_t> fill;   // [groups][F] claimed after the scatter
+    void *gstart = nullptr, *gcur = nullptr, *gend = nullptr;  // device [groups][F] each, adjacent
     bool narrow = true;
-    uint64_t capacityTotal = 0;
+    uint64_t capacityTotal = 0;  // window slots: the layout's capacity bound
   };
   void finishPlan(Side &s);
 
