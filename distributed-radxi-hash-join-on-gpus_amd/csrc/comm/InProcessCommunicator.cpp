@@ -74,6 +74,10 @@ void InProcessCommunicator::allReduceSumHost(uint64_t *data, size_t count) {
   }
 }
 
+InProcessCommunicator::~InProcessCommunicator() {
+  if (ptrTable_) (void)hipFree(ptrTable_);
+}
+
 void InProcessCommunicator::allReduceSumDevice(uint64_t *data, size_t count, hipStream_t stream) {
   const uint32_t N = size(), me = rank_;
   if (N == 1 || count == 0) return;
@@ -94,11 +98,14 @@ void InProcessCommunicator::allReduceSumDevice(uint64_t *data, size_t count, hip
     Communicator::allReduceSumDevice(data, count, stream);
     return;
   }
-  uint64_t *const *dptrs = nullptr;
-  HIP_CHECK(hipMallocAsync((void **)&dptrs, N * sizeof(uint64_t), stream));
-  HIP_CHECK(hipMemcpyAsync((void *)dptrs, ptrs.data(), N * sizeof(uint64_t), hipMemcpyHostToDevice, stream));
-  kernels::sumSlices(dptrs, N, count * me / N, count * (me + 1) / N, stream);
-  HIP_CHECK(hipFreeAsync((void *)dptrs, stream));
+  if (!ptrTable_ || ptrTableDevice_ != (int)attr.device || ptrTableSize_ < N) {
+    if (ptrTable_) HIP_CHECK(hipFree(ptrTable_));
+    HIP_CHECK(hipMalloc((void **)&ptrTable_, N * sizeof(uint64_t)));
+    ptrTableDevice_ = (int)attr.device;
+    ptrTableSize_ = N;
+  }
+  HIP_CHECK(hipMemcpyAsync((void *)ptrTable_, ptrs.data(), N * sizeof(uint64_t), hipMemcpyHostToDevice, stream));
+  kernels::sumSlices(ptrTable_, N, count * me / N, count * (me + 1) / N, stream);
   HIP_CHECK(hipStreamSynchronize(stream));
   group_->barrier();  // every slice of every buffer written
 }

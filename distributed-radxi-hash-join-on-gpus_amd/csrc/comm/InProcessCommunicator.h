@@ -46,6 +46,7 @@ class InProcessGroup {
 class InProcessCommunicator : public Communicator {
  public:
   InProcessCommunicator(std::shared_ptr<InProcessGroup> group, uint32_t rank) : group_(std::move(group)), rank_(rank) {}
+  ~InProcessCommunicator() override;
   uint32_t rank() const override { return rank_; }
   uint32_t size() const override { return group_->size(); }
   bool supports(Location) const override { return true; }
@@ -55,6 +56,9 @@ class InProcessCommunicator : public Communicator {
   void allReduceSumHost(uint64_t *data, size_t count) override;
   // Device buffers of ranks on one device: each rank sums its slice of all
   // buffers with one kernel (no host staging); completes before returning.
+  // Blocking (stream sync + barriers per call): an in-process rehearsal of the
+  // replicated bitmap plan therefore runs its all-reduce ranges one after the
+  // other -- the overlap of build, reduce and probe ranges is the RCCL path's.
   void allReduceSumDevice(uint64_t *data, size_t count, hipStream_t stream) override;
   void barrier() override { group_->barrier(); }
   void checkHealth() override;
@@ -65,6 +69,9 @@ class InProcessCommunicator : public Communicator {
  private:
   std::shared_ptr<InProcessGroup> group_;
   uint32_t rank_;
+  uint64_t **ptrTable_ = nullptr;  // device table of the ranks' buffer pointers (allocated once)
+  int ptrTableDevice_ = -1;
+  uint32_t ptrTableSize_ = 0;
 };
 
 }  // namespace comm

@@ -108,6 +108,27 @@ def main():
         if info.rank == 0:
             print(f"{name}: {res['global_matches']} == {exp}, plan {j.plan}", flush=True)
         del j, S
+    # One-sided windows across a workspace growth: the large join grows every
+    # rank's arena (a new chunk and generation), so the peers' cached IPC
+    # mappings must be re-opened (core/ExecContext::ipcImport); the small join
+    # before and after it stays exact.
+    cfg1 = C.JoinConfig()
+    cfg1.bitmap_join = False
+    cfg1.exchange = C.ExchangeMode.ONE_SIDED
+    spec = C.GenSpec(distribution=C.KeyDistribution.UNIFORM, seed=8, domain=G_R)
+    caps = []
+    for G in (G_S, 40 * G_S, G_S):
+        S = C.Relation(C.Relation.local_size_for(G, info.rank, info.world), G, "device", info.local_rank)
+        S.generate(spec, C.Relation.local_offset_for(G, info.rank, info.world))
+        j = C.HashJoin(R, S, ctx, cfg1)
+        assert j.plan.one_sided, j.plan
+        res = j.run()
+        assert res["global_matches"] == C.Relation.expected_matches(inner, G_R, spec, G), ("one-sided-grow", G, res)
+        caps.append(ctx.workspace_capacity())
+        del j, S
+    assert caps[1] > caps[0], ("workspace did not grow", caps)
+    if info.rank == 0:
+        print(f"one-sided across a workspace growth: exact, workspace {caps}", flush=True)
     # TPC-H-like join + late materialization of 32-byte payload rows across
     # ranks (BASELINE config 5 at SF 0.5): pairs from the build/probe, rows
     # fetched from their owner ranks by the request/response all-to-allv.
