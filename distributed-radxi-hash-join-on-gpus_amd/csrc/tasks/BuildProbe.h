@@ -49,6 +49,9 @@ class BuildProbe : public Task {
   // rows to the sink.  A sink overflow is reported, not re-run (the caller
   // owns the buffer).
   void setRowSink(const kernels::RowSink *s) { sink = s; }
+  // A span overflowed the quotient table's side list and this task re-ran
+  // on the v2 table (collect() returned true for it).
+  bool quotientFellBack() const { return quotientFallback; }
   bool rowsFused() const { return fused; }
 
  protected:

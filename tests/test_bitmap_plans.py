@@ -380,8 +380,9 @@ def test_key_quotient_escapes(C, n_escape, dup):
     for i in range(2):
         res = j.run()
         assert res["global_matches"] == exp, (n_escape, dup, res["global_matches"], exp)
-        # the fallback sticks to the BuildProbe task of one run only
-        assert res["reruns"] == (1 if over else 0), res["reruns"]
+        # an overflowing join re-runs its build/probe once; later joins of the
+        # same HashJoin start on the v2 table (no re-run)
+        assert res["reruns"] == (1 if over and i == 0 else 0), (i, res["reruns"])
 
 
 @pytest.mark.parametrize("dev", devices())
