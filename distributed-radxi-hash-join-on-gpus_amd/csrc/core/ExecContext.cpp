@@ -1,8 +1,11 @@
 #include "ExecContext.h"
 
 #include <cstring>
+#include <mutex>
+#include <set>
 
 #include "../comm/Communicator.h"
+#include "../kernels/kernels.h"
 #include "../memory/Arena.h"
 #include "../performance/Timeline.h"
 #include "../utils/Fault.h"
@@ -24,6 +27,13 @@ ExecContext::ExecContext(Location loc, int device, comm::Communicator *comm)
   timeline_.reset(new performance::Timeline(onDevice()));
   if (onDevice()) {
     HIP_CHECK(hipSetDevice(device_));
+    {
+      // Code objects of the join kernels, once per process and device.
+      static std::mutex m;
+      static std::set<int> loaded;
+      std::lock_guard<std::mutex> g(m);
+      if (loaded.insert(device_).second) kernels::preloadCodeObjects();
+    }
     HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     // The exchange stream (RCCL collectives, window copies) gets the highest
     // priority: its few long-running blocks are dispatched ahead of the

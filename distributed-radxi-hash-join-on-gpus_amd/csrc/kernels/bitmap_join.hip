@@ -516,5 +516,12 @@ void bitmapProbe(uint32_t elemBytes, const void *s, const BitmapSlices &src, uin
 #undef HJ_BM_DISPATCH
 #undef HJ_BM_NTH
 
+// Loads this file's code object at engine start (kernels::preloadCodeObjects).
+void preloadBitmapJoin() {
+  hipFuncAttributes a;
+  HIP_CHECK(hipFuncGetAttributes(
+      &a, reinterpret_cast<const void *>(&bitmapJoinKernel<uint32_t, BM_U, ClaimSrc<uint32_t>, 1024>)));
+}
+
 }  // namespace kernels
 }  // namespace hpcjoin

@@ -1749,5 +1749,11 @@ void buildProbe(const BPArgs &args, const BPItem *items, const uint32_t *nItems,
   HIP_CHECK_LAUNCH();
 }
 
+// Loads this file's code object at engine start (kernels::preloadCodeObjects).
+void preloadBuildProbe() {
+  hipFuncAttributes a;
+  HIP_CHECK(hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&bpPlanCountsKernel)));
+}
+
 }  // namespace kernels
 }  // namespace hpcjoin

@@ -32,5 +32,11 @@ void sumSlices(uint64_t *const *devBufs, uint32_t n, uint64_t lo, uint64_t hi, h
   HIP_CHECK_LAUNCH();
 }
 
+// Loads this file's code object at engine start (kernels::preloadCodeObjects).
+void preloadCollectives() {
+  hipFuncAttributes a;
+  HIP_CHECK(hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&sumSlicesKernel)));
+}
+
 }  // namespace kernels
 }  // namespace hpcjoin

@@ -85,5 +85,11 @@ void generate(data::Tuple *out, uint64_t n, const GenParams &p, hipStream_t s) {
   HIP_CHECK_LAUNCH();
 }
 
+// Loads this file's code object at engine start (kernels::preloadCodeObjects).
+void preloadDatagen() {
+  hipFuncAttributes a;
+  HIP_CHECK(hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&generateKernel)));
+}
+
 }  // namespace kernels
 }  // namespace hpcjoin

@@ -545,5 +545,28 @@ void materializeLocal(const ulonglong2 *pairs, uint64_t n, const uint64_t *rowsA
                       const uint64_t *rowsB, uint64_t offB, uint64_t *out, hipStream_t s, uint32_t variant = 1);
 void placeRows(const uint64_t *rows, const uint64_t *idx, uint64_t n, uint64_t *out, uint32_t strideWords,
                uint32_t colWord, hipStream_t s);
+// Every HIP source file is its own code object, loaded by the runtime at the
+// first use of one of its kernels -- 1-2 ms each, which landed inside the
+// first join.  ExecContext calls this once per process and device: one
+// hipFuncGetAttributes per file loads them all up front.
+void preloadPartition();
+void preloadBuildProbe();
+void preloadBitmapJoin();
+void preloadScan();
+void preloadWire();
+void preloadCollectives();
+void preloadMaterialize();
+void preloadDatagen();
+inline void preloadCodeObjects() {
+  preloadPartition();
+  preloadBuildProbe();
+  preloadBitmapJoin();
+  preloadScan();
+  preloadWire();
+  preloadCollectives();
+  preloadMaterialize();
+  preloadDatagen();
+}
+
 }  // namespace kernels
 }  // namespace hpcjoin

@@ -230,5 +230,11 @@ void materializeLocal(const ulonglong2 *pairs, uint64_t n, const uint64_t *rowsA
   HIP_CHECK_LAUNCH();
 }
 
+// Loads this file's code object at engine start (kernels::preloadCodeObjects).
+void preloadMaterialize() {
+  hipFuncAttributes a;
+  HIP_CHECK(hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&generatePayloadKernel)));
+}
+
 }  // namespace kernels
 }  // namespace hpcjoin

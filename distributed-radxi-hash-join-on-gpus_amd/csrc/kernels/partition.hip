@@ -1487,5 +1487,11 @@ void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nI
   HIP_CHECK_LAUNCH();
 }
 
+// Loads this file's code object at engine start (kernels::preloadCodeObjects).
+void preloadPartition() {
+  hipFuncAttributes a;
+  HIP_CHECK(hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&netHistogramKernel)));
+}
+
 }  // namespace kernels
 }  // namespace hpcjoin

@@ -76,5 +76,11 @@ void scanExclusiveU32to64(const uint32_t *in, unsigned long long *out, uint64_t 
   scanExclusive<unsigned long long>(in, out, n, total, workspace, s);
 }
 
+// Loads this file's code object at engine start (kernels::preloadCodeObjects).
+void preloadScan() {
+  hipFuncAttributes a;
+  HIP_CHECK(hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&scanSumsKernel<uint32_t>)));
+}
+
 }  // namespace kernels
 }  // namespace hpcjoin

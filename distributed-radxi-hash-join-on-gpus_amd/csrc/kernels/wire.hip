@@ -199,5 +199,11 @@ void segCopy(const uint64_t *src, uint64_t *dst, const WireSeg *segs, uint32_t n
   HIP_CHECK_LAUNCH();
 }
 
+// Loads this file's code object at engine start (kernels::preloadCodeObjects).
+void preloadWire() {
+  hipFuncAttributes a;
+  HIP_CHECK(hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&wirePackKernel<true>)));
+}
+
 }  // namespace kernels
 }  // namespace hpcjoin
