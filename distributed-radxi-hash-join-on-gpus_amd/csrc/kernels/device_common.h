@@ -35,16 +35,14 @@ __device__ __forceinline__ T waveReduceSum(T x) {
 // workgroup of NT threads; each thread owns a contiguous run of entries.
 // waveTot must hold NT/64 entries of T.  Contains the barriers it needs; all
 // threads of the block must call it.
-// MASK: the scanned value is data[i] & MASK (the claim scatter keeps a write
-// limit in the upper half of its u32 counts).
-template <int NT, typename T, typename U, U MASK = U(~U(0))>
+template <int NT, typename T, typename U>
 __device__ __forceinline__ T blockExclusiveScanLds(const U *data, T *out, int n, T *waveTot) {
   const int t = threadIdx.x, lane = t & (WAVE - 1), wid = t / WAVE;
   const int per = (n + NT - 1) / NT;
   const int b = t * per;
   T local = 0;
   for (int i = 0; i < per; ++i)
-    if (b + i < n) local += T(data[b + i] & MASK);
+    if (b + i < n) local += T(data[b + i]);
   T incl = waveInclusiveScan<T>(local);
   if (lane == WAVE - 1) waveTot[wid] = incl;
   __syncthreads();
@@ -58,7 +56,7 @@ __device__ __forceinline__ T blockExclusiveScanLds(const U *data, T *out, int n,
   T run = prefix + incl - local;
   for (int i = 0; i < per; ++i)
     if (b + i < n) {
-      T v = T(data[b + i] & MASK);
+      T v = T(data[b + i]);
       out[b + i] = run;
       run += v;
     }

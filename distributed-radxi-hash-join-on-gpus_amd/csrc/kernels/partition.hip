@@ -524,20 +524,15 @@ struct LocalSplitPol : LocalCompressedPol {  // 8 B -> u32 rid / key low word + 
   }
 };
 
-// LDS per workgroup: cursor (per-workgroup cursor mode only) and wbase
-// (F x CurT), cnt and off (F x u32), scan scratch, the reordered tile (TILE x
-// StageT) and, only for NetCompressedDigPol, the tile's digits (TILE x u16).
-// Claim mode keeps no cursor array (claims come from device cursors, and a
-// bounded slice's write limit rides in cnt's upper half): at F = 1024 with
-// 32-bit cursors and 8192 8-byte words that is 77.9 KiB instead of 82.0, so
-// two 1024-thread workgroups fit a CU's 160 KiB.  (Measured same-box against
-// the LDS padded back to one workgroup per CU: no difference, 10.09-10.11 vs
-// 10.12-10.13 ms headline, 21.07-21.12 vs 21.11-21.22 ms general path -- the
-// scatter is bound by its partial-line writes, not by barrier stalls.)
-template <class Pol, typename CurT, int TILE, bool CLAIM = false>
+// LDS per workgroup: cursor and wbase (F x CurT), cnt and off (F x u32), scan
+// scratch, the reordered tile (TILE x StageT) and, only for
+// NetCompressedDigPol, the tile's digits (TILE x u16).  At F = 1024 with
+// 32-bit cursors and 8-byte words: 16 KiB + 32 KiB -> three 256-thread
+// workgroups (12 wave64s) per CU.
+template <class Pol, typename CurT, int TILE>
 struct ScatterLayout {
   static __host__ __device__ constexpr size_t valOffset(uint32_t F) {
-    return ((size_t)F * ((CLAIM ? 1 : 2) * sizeof(CurT) + 8) + 64 + 15) & ~size_t(15);
+    return ((size_t)F * (2 * sizeof(CurT) + 8) + 64 + 15) & ~size_t(15);
   }
   static __host__ __device__ constexpr size_t bytes(uint32_t F) {
     return valOffset(F) + (size_t)TILE * sizeof(typename Pol::StageT) + (Pol::kDigArray ? (size_t)TILE * 2 : 0);
@@ -545,19 +540,19 @@ struct ScatterLayout {
 };
 
 // Per-workgroup LDS carve of the scatter (see ScatterLayout).
-template <class Pol, typename CurT, int TILE, bool CLAIM = false>
+template <class Pol, typename CurT, int TILE>
 struct ScatterSmem {
   CurT *cursor, *wbase;
   uint32_t *cnt, *off, *wave;
   typename Pol::StageT *val;
   uint16_t *dig;
   __device__ __forceinline__ ScatterSmem(unsigned char *smem, uint32_t F) {
-    cursor = CLAIM ? nullptr : reinterpret_cast<CurT *>(smem);
-    wbase = reinterpret_cast<CurT *>(smem) + (CLAIM ? 0 : F);
+    cursor = reinterpret_cast<CurT *>(smem);
+    wbase = cursor + F;
     cnt = reinterpret_cast<uint32_t *>(wbase + F);
     off = cnt + F;
     wave = off + F;
-    val = reinterpret_cast<typename Pol::StageT *>(smem + ScatterLayout<Pol, CurT, TILE, CLAIM>::valOffset(F));
+    val = reinterpret_cast<typename Pol::StageT *>(smem + ScatterLayout<Pol, CurT, TILE>::valOffset(F));
     dig = reinterpret_cast<uint16_t *>(val + TILE);
   }
 };
@@ -575,19 +570,15 @@ __device__ __forceinline__ void loadTile(const typename Pol::InT *__restrict__ s
 // One tile.  FULL tiles (every tile but a range's tail) are branch-free so
 // hipcc can keep all IPT LDS atomics, loads and stores in flight with counted
 // waits; the predicated tail path is only taken once per range.
-// BOUNDED (claim mode with estimated slices): gend[d] is the end of the
+// BOUNDED (claim mode with estimated slices): l.cursor[d] holds the end of the
 // group's slice of digit d; claimed positions past it are not written (the
-// caller detects the overflow from the final claim cursors and re-runs).  The
-// tile's staged index limit of digit d (off + the claimed run's room) is kept
-// in the upper 16 bits of cnt[d], whose lower half counts the next tile.
+// caller detects the overflow from the final claim cursors and re-runs).
 template <class Pol, typename CurT, int NTH, int IPT, int MODE, bool FULL, bool CLAIM, bool BOUNDED = false>
 __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict__ in, uint64_t base, uint64_t end,
-                                            uint32_t count, uint32_t F,
-                                            const ScatterSmem<Pol, CurT, NTH * IPT, CLAIM> &l, const Pol &pol,
-                                            typename Pol::OutT *__restrict__ out, typename Pol::InT (&v)[IPT],
-                                            CurT *__restrict__ gcur, const CurT *__restrict__ gend) {
+                                            uint32_t count, uint32_t F, const ScatterSmem<Pol, CurT, NTH * IPT> &l,
+                                            const Pol &pol, typename Pol::OutT *__restrict__ out,
+                                            typename Pol::InT (&v)[IPT], CurT *__restrict__ gcur) {
   constexpr uint32_t TILE = NTH * IPT;
-  static_assert(TILE < 65536, "tile counts and limits are 16-bit");
   const uint32_t t = threadIdx.x;
   uint32_t dr[IPT];
 #pragma unroll
@@ -595,11 +586,11 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
     const uint32_t idx = i * NTH + t;
     if (FULL || idx < count) {
       const uint32_t d = pol.digit(v[i]);
-      dr[i] = (d << 16) | (atomicAdd(&l.cnt[d], 1u) & 0xFFFFu);
+      dr[i] = (d << 16) | atomicAdd(&l.cnt[d], 1u);
     }
   }
   __syncthreads();  // A: counts final; previous tile's write-out done
-  blockExclusiveScanLds<NTH, uint32_t, uint32_t, 0xFFFFu>(l.cnt, l.off, (int)F, l.wave);
+  blockExclusiveScanLds<NTH, uint32_t, uint32_t>(l.cnt, l.off, (int)F, l.wave);
   constexpr int MAXD = (1 << MAX_PART_BITS) / NTH > 0 ? (1 << MAX_PART_BITS) / NTH : 1;
   CurT claim[MAXD];
   if constexpr (CLAIM) {
@@ -607,7 +598,7 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
 #pragma unroll
     for (int k = 0; k < MAXD; ++k) {
       const uint32_t d = t + k * NTH;
-      if (d < F) claim[k] = atomicAdd(&gcur[d], (CurT)(l.cnt[d] & 0xFFFFu));
+      if (d < F) claim[k] = atomicAdd(&gcur[d], (CurT)l.cnt[d]);
     }
   } else {
     for (uint32_t d = t; d < F; d += NTH) {
@@ -638,14 +629,8 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
     for (int k = 0; k < MAXD; ++k) {
       const uint32_t d = t + k * NTH;
       if (d < F) {
-        const uint32_t o = l.off[d];
-        l.wbase[d] = claim[k] - (CurT)o;
-        uint32_t lim = 0;
-        if constexpr (BOUNDED) {
-          const CurT e = gend[d], c = (CurT)(l.cnt[d] & 0xFFFFu);
-          lim = o + (uint32_t)(claim[k] >= e ? (CurT)0 : (e - claim[k] < c ? e - claim[k] : c));
-        }
-        l.cnt[d] = lim << 16;
+        l.wbase[d] = claim[k] - (CurT)l.off[d];
+        l.cnt[d] = 0;
       }
     }
   }
@@ -663,7 +648,7 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
       if constexpr (MODE == 0) {
         const CurT pos = (CurT)(l.wbase[d] + (CurT)idx);
         if constexpr (BOUNDED) {
-          if (idx < (l.cnt[d] >> 16)) pol.store(out, (uint64_t)pos, x);
+          if (pos < l.cursor[d]) pol.store(out, (uint64_t)pos, x);
         } else {
           pol.store(out, (uint64_t)pos, x);
         }
@@ -686,10 +671,9 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
 template <class Pol, typename CurT, int NTH, int IPT, int MODE, bool CLAIM = false, bool BOUNDED = false>
 __device__ __forceinline__ void scatterRange(const typename Pol::InT *__restrict__ in, uint64_t begin, uint64_t end,
                                              uint32_t F, unsigned char *smem, const Pol &pol,
-                                             typename Pol::OutT *__restrict__ out, CurT *gcur = nullptr,
-                                             const CurT *gend = nullptr) {
+                                             typename Pol::OutT *__restrict__ out, CurT *gcur = nullptr) {
   constexpr uint32_t TILE = NTH * IPT;
-  const ScatterSmem<Pol, CurT, TILE, CLAIM> l(smem, F);
+  const ScatterSmem<Pol, CurT, TILE> l(smem, F);
   typename Pol::InT v[IPT];
   if (begin + TILE <= end)
     loadTile<Pol, NTH, IPT, true>(in + begin, TILE, v);
@@ -697,10 +681,10 @@ __device__ __forceinline__ void scatterRange(const typename Pol::InT *__restrict
     loadTile<Pol, NTH, IPT, false>(in + begin, (uint32_t)(end - begin), v);
   for (uint64_t base = begin; base < end; base += TILE) {
     if (base + TILE <= end)
-      scatterTile<Pol, CurT, NTH, IPT, MODE, true, CLAIM, BOUNDED>(in, base, end, TILE, F, l, pol, out, v, gcur, gend);
+      scatterTile<Pol, CurT, NTH, IPT, MODE, true, CLAIM, BOUNDED>(in, base, end, TILE, F, l, pol, out, v, gcur);
     else
       scatterTile<Pol, CurT, NTH, IPT, MODE, false, CLAIM, BOUNDED>(in, base, end, (uint32_t)(end - base), F, l, pol,
-                                                                    out, v, gcur, gend);
+                                                                    out, v, gcur);
   }
   __syncthreads();
 }
@@ -740,14 +724,17 @@ __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void netScatterClaimKe
     CurT *__restrict__ gcur, typename Pol::OutT *out, const CurT *__restrict__ gend = nullptr) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t blk = blockBegin + blockIdx.x;
-  const ScatterSmem<Pol, CurT, NTH * IPT, true> l(smem, F);
+  CurT *sliceEnd = reinterpret_cast<CurT *>(smem);  // the per-workgroup cursor array is unused in claim mode
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(reinterpret_cast<CurT *>(smem) + 2 * F);
   const size_t grp = (size_t)(blockIdx.x % NGROUPS) * F;
-  for (uint32_t d = threadIdx.x; d < F; d += NTH) l.cnt[d] = 0;
+  for (uint32_t d = threadIdx.x; d < F; d += NTH) {
+    cnt[d] = 0;
+    if constexpr (BOUNDED) sliceEnd[d] = gend[grp + d];
+  }
   __syncthreads();
   const uint64_t begin = (uint64_t)blk * tpb * PART_TILE;
   const uint64_t end = min(n, begin + (uint64_t)tpb * PART_TILE);
-  scatterRange<Pol, CurT, NTH, IPT, MODE, true, BOUNDED>(in, begin, end, F, smem, pol, out, gcur + grp,
-                                                         BOUNDED ? gend + grp : nullptr);
+  scatterRange<Pol, CurT, NTH, IPT, MODE, true, BOUNDED>(in, begin, end, F, smem, pol, out, gcur + grp);
 }
 
 // Default geometry (measured on MI355X, tools/microbench.py ablation).
@@ -788,7 +775,7 @@ static void launchNetClaimIpt(const Pol &pol, const data::Tuple *in, uint64_t n,
   auto *dst = reinterpret_cast<typename Pol::OutT *>(out);
   const dim3 grid(blockEnd - blockBegin);
   if (narrow) {
-    const size_t lds = ScatterLayout<Pol, uint32_t, CL_NTH * CL_IPT, true>::bytes(F);
+    const size_t lds = ScatterLayout<Pol, uint32_t, CL_NTH * CL_IPT>::bytes(F);
     HJ_CHECK(lds <= 160 * 1024, "scatter LDS %zu too large", lds);
     auto *gc = reinterpret_cast<uint32_t *>(gcur);
     if (gend)
@@ -799,7 +786,7 @@ static void launchNetClaimIpt(const Pol &pol, const data::Tuple *in, uint64_t n,
       hipLaunchKernelGGL((netScatterClaimKernel<Pol, uint32_t, CL_NTH, CL_IPT, 0>), grid, dim3(CL_NTH), lds, s, src,
                          n, g.tilesPerBlock, F, pol, blockBegin, gc, dst, nullptr);
   } else {
-    const size_t lds = ScatterLayout<Pol, unsigned long long, CL_NTH * CL_IPT, true>::bytes(F);
+    const size_t lds = ScatterLayout<Pol, unsigned long long, CL_NTH * CL_IPT>::bytes(F);
     HJ_CHECK(lds <= 160 * 1024, "scatter LDS %zu too large", lds);
     auto *gc = reinterpret_cast<unsigned long long *>(gcur);
     if (gend)
@@ -1057,7 +1044,7 @@ void scatterAblation(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t 
   static_cast<NetCompressedPol &>(dpol) = pol;
 #define HJ_CLAIM(NTH, IPT)                                                                                        \
   do {                                                                                                            \
-    const size_t lds = ScatterLayout<NetCompressedPol, uint32_t, NTH * IPT, true>::bytes(1u << bits);            \
+    const size_t lds = ScatterLayout<NetCompressedPol, uint32_t, NTH * IPT>::bytes(1u << bits);                  \
     auto *gc = reinterpret_cast<uint32_t *>(gcur);                                                                \
     if (mode == 1)                                                                                                \
       hipLaunchKernelGGL((netScatterClaimKernel<NetCompressedPol, uint32_t, NTH, IPT, 1>), dim3(g.blocks),        \
@@ -1088,7 +1075,7 @@ void scatterAblation(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t 
   NetFragPol fpol;
   fpol.mask = (1ull << bits) - 1;
   fpol.bits = bits;
-  using FragLayout = ScatterLayout<NetFragPol, uint32_t, 1024 * 16, true>;
+  using FragLayout = ScatterLayout<NetFragPol, uint32_t, 1024 * 16>;
   const size_t fragLds = FragLayout::bytes(1u << bits);
 #define HJ_FRAG(M)                                                                                                \
   hipLaunchKernelGGL((netScatterClaimKernel<NetFragPol, uint32_t, 1024, 16, M>), dim3(g.blocks), dim3(1024),      \
@@ -1401,13 +1388,16 @@ __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void localScatterClaim
   const uint32_t q = (nItems + NGROUPS - 1) / NGROUPS;
   const uint32_t item = (blockIdx.x % NGROUPS) * q + blockIdx.x / NGROUPS;  // XCD-contiguous items
   if (item >= nItems) return;  // uniform per workgroup
-  const ScatterSmem<Pol, CurT, NTH * IPT, true> l(smem, F);
+  CurT *sliceEnd = reinterpret_cast<CurT *>(smem);
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(reinterpret_cast<CurT *>(smem) + 2 * F);
   const LocalItem it = items[item];
-  for (uint32_t d = threadIdx.x; d < F; d += NTH) l.cnt[d] = 0;
+  for (uint32_t d = threadIdx.x; d < F; d += NTH) {
+    cnt[d] = 0;
+    if constexpr (BOUNDED) sliceEnd[d] = gend[(uint64_t)it.stream * F + d];
+  }
   __syncthreads();
   scatterRange<Pol, CurT, NTH, IPT, 0, true, BOUNDED>(in, it.begin, it.begin + it.len, F, smem, pol, out,
-                                                      gcur + (uint64_t)it.stream * F,
-                                                      BOUNDED ? gend + (uint64_t)it.stream * F : nullptr);
+                                                      gcur + (uint64_t)it.stream * F);
 }
 
 template <class P>
@@ -1424,7 +1414,7 @@ static void setSplit(LocalSplitPol &p, const SplitLayout &sl) {
 template <int NTH, int IPT>
 static void launchLocalSplitGeom(const void *in, const LocalItem *items, uint32_t nItems, uint32_t F,
                                  const LocalSplitPol &pol, void *gcur, void *out, const void *gend, hipStream_t s) {
-  const size_t lds = ScatterLayout<LocalSplitPol, unsigned long long, NTH * IPT, true>::bytes(F);
+  const size_t lds = ScatterLayout<LocalSplitPol, unsigned long long, NTH * IPT>::bytes(F);
   HJ_CHECK(lds <= 160 * 1024, "local scatter LDS %zu too large", lds);
   const uint32_t grid = ((nItems + NGROUPS - 1) / NGROUPS) * NGROUPS;
   hipLaunchKernelGGL((localScatterClaimKernel<LocalSplitPol, unsigned long long, NTH, IPT, true>), dim3(grid),
@@ -1464,7 +1454,7 @@ void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nI
     pol.mask = mask;                                                                                          \
     pol.shift = shift;                                                                                        \
     setSplit(pol, split);                                                                                     \
-    const size_t lds = ScatterLayout<P, C, CL_NTH * CL_IPT, true>::bytes(F);                                   \
+    const size_t lds = ScatterLayout<P, C, CL_NTH * CL_IPT>::bytes(F);                                         \
     if (gend)                                                                                                 \
       hipLaunchKernelGGL((localScatterClaimKernel<P, C, CL_NTH, CL_IPT, true>), dim3(grid), dim3(CL_NTH), lds, \
                          s, reinterpret_cast<const typename P::InT *>(in), items, nItems, F, pol,              \
