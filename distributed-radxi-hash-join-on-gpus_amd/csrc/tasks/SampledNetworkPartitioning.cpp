@@ -179,13 +179,16 @@ bool SampledNetworkPartitioning::finishSide(int k) {
   const uint64_t *c64 = static_cast<const uint64_t *>(s.cursorsBack);
   auto at = [&](size_t i) -> uint64_t { return s.narrow ? c32[i] : c64[i]; };
   bool ok = true;
-  uint64_t sum = 0;
+  uint64_t sum = 0, maxEnd = 0;
   for (size_t i = 0; i < m; ++i) {
     s.start[i] = at(i);
     s.fill[i] = at(m + i) - s.start[i];  // final claim cursor - slice start
     sum += s.fill[i];
+    maxEnd = std::max<uint64_t>(maxEnd, at(2 * m + i));
     if (s.fill[i] > at(2 * m + i) - s.start[i]) ok = false;
   }
+  HJ_CHECK(maxEnd <= s.capacityTotal, "sampled network layout: slices end at %lu, window holds %lu",
+           (unsigned long)maxEnd, (unsigned long)s.capacityTotal);
   HJ_CHECK(sum == s.relation->getLocalSize(), "sampled network pass claimed %lu of %lu tuples", (unsigned long)sum,
            (unsigned long)s.relation->getLocalSize());
   if (!ok) return false;

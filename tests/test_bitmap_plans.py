@@ -333,6 +333,37 @@ def test_key_only_count_variants(C, variant):
             assert j.run()["global_matches"] == exp, (variant, G_R, theta)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("sizes", [(1 << 20, 3 << 20), (5_000, 3 << 20), (3 << 20, 5_000), (0, 1 << 20)])
+def test_sampled_general_path_device_layout(C, sizes):
+    """Single-rank sampled network pass of the general path (key-only words):
+    slices laid out on the device from the sampled totals; a side too small
+    to sample gets an exact histogram next to a sampled one; counts equal a
+    torch oracle, no fallback."""
+    from helpers import ref_join_count
+    G_R, G_S = sizes
+    ctx = C.ExecContext("device", 0, C.LocalCommunicator())
+    inner = C.GenSpec(seed=51)
+    inner.sparse64 = True
+    outer = C.GenSpec(distribution=C.KeyDistribution.UNIFORM, seed=52, domain=max(G_R, 1))
+    outer.sparse64 = True
+    R = C.Relation(G_R, G_R, "device", 0)
+    S = C.Relation(G_S, G_S, "device", 0)
+    if G_R:
+        R.generate(inner, 0)
+    S.generate(outer, 0)
+    exp = ref_join_count(R.to_tensor()[:, 0].cpu(), S.to_tensor()[:, 0].cpu()) if G_R else 0
+    cfg = C.JoinConfig()
+    cfg.network_histogram = C.HistogramMode.SAMPLED
+    cfg.network_bits, cfg.local_bits = 10, 9
+    j = C.HashJoin(R, S, ctx, cfg)
+    assert j.plan.key_only and j.plan.sampled_network, j.plan
+    for _ in range(2):
+        res = j.run()
+        assert res["global_matches"] == exp, (sizes, res["global_matches"], exp)
+        assert res["sampled_network"] and res["network_fallbacks"] == 0, res
+
+
 def quotient_escape_fragments(n, first_bucket=0):
     """Fragments the quotient table (build_probe.hip, bpKeyQuotientKernel) can
     only hold in its side list: 44-bit fragments f (63-bit keys above 10 + 9
