@@ -3,6 +3,9 @@
 skew-aware AssignmentMap path) with an exact oracle.
 
 Configs (one JSON line each, rank 0):
+  zipf_both_sparse  zipf_both through the sparse 63-bit key bijection: the
+                general path (key-only words, quotient table) with duplicate
+                inner keys
   zipf_both     inner AND outer Zipf(theta) over the same dense domain: the
                 inner side has duplicates, so the bitmap plan cannot apply and
                 the two-level plan (+ LPT / hot-partition split at N > 1) runs
@@ -94,7 +97,7 @@ def oracle(C, info, R, S, domain):
 
 def run_config(C, info, ctx, comm, name, G_R, G_S, theta, cfg, steps, warmup):
     domain = G_R
-    if name == "zipf_both":
+    if name in ("zipf_both", "zipf_both_sparse"):
         inner = C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=1234, domain=domain, zipf_theta=theta)
         outer = C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=4321, domain=domain, zipf_theta=theta)
     elif name == "zipf_outer":
@@ -104,15 +107,29 @@ def run_config(C, info, ctx, comm, name, G_R, G_S, theta, cfg, steps, warmup):
         inner = C.GenSpec(distribution=C.KeyDistribution.UNIQUE, seed=1234)
         outer = C.GenSpec(distribution=C.KeyDistribution.UNIFORM, seed=4321, domain=domain)
     lr, ls = (C.Relation.local_size_for(G, info.rank, info.world) for G in (G_R, G_S))
-    R = C.Relation(lr, G_R, "device", info.local_rank)
-    S = C.Relation(ls, G_S, "device", info.local_rank)
-    R.generate(inner, C.Relation.local_offset_for(G_R, info.rank, info.world))
-    S.generate(outer, C.Relation.local_offset_for(G_S, info.rank, info.world))
+
+    def relations():
+        R = C.Relation(lr, G_R, "device", info.local_rank)
+        S = C.Relation(ls, G_S, "device", info.local_rank)
+        R.generate(inner, C.Relation.local_offset_for(G_R, info.rank, info.world))
+        S.generate(outer, C.Relation.local_offset_for(G_S, info.rank, info.world))
+        return R, S
+
+    R, S = relations()
     expected = C.Relation.expected_matches(inner, G_R, outer, G_S)
     oracle_source = "closed form"
     if expected is None:
         expected = oracle(C, info, R, S, domain)
         oracle_source = "per-key device counts"
+    if name == "zipf_both_sparse":
+        # The same Zipf relations through the sparse 63-bit key bijection
+        # (general path: key-only words, duplicate inner keys); the count is
+        # that of the dense relations the oracle just read.
+        del R, S
+        torch.cuda.empty_cache()
+        inner.sparse64 = outer.sparse64 = True
+        R, S = relations()
+        oracle_source += " of the dense pre-image"
 
     def barrier():
         if info.world > 1:
