@@ -129,12 +129,6 @@ __device__ __forceinline__ void visitSlice32(const uint32_t *__restrict__ src, u
   if (t < rem) fn((uint64_t)src[(nv << 2) + t]);
 }
 
-__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
-  return ((uint64_t)hi << 32) | lo;
-}
-
 // fn(fragment) for every u32 fragment of partition d: its
 // CLAIM_GROUPS claim slices walked as ONE stream of 16-byte vectors (slices
 // start on 16-element boundaries).  The slice table is read once per

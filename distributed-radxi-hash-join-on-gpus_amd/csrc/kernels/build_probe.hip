@@ -78,22 +78,44 @@ __device__ __forceinline__ uint32_t hash64(uint64_t key, uint32_t tbits) {
   return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - tbits));
 }
 
+// heavySpans (optional): partitions with more than rChunk inner tuples
+// (repeated keys) get no work items here; their spans go to heavySpans
+// instead (appended at *heavyCount, at most heavyCapacity written) for
+// bpKeyCountedSpans.
 __global__ __launch_bounds__(BPT) void bpPlanCountsKernel(const uint64_t *__restrict__ partR,
                                                           const uint64_t *__restrict__ partS,
                                                           const uint64_t *__restrict__ partREnd,
                                                           const uint64_t *__restrict__ partSEnd, uint32_t P, uint32_t rc,
-                                                          uint32_t sc, uint32_t *counts) {
+                                                          uint32_t sc, uint32_t *counts, BPSpan *__restrict__ heavySpans,
+                                                          uint32_t *__restrict__ heavyCount, uint32_t heavyCapacity) {
   const uint32_t p = blockIdx.x * BPT + threadIdx.x;
   if (p >= P) return;
   const uint64_t nr = partREnd[p] - partR[p], ns = partSEnd[p] - partS[p];
-  counts[p] = (nr == 0 || ns == 0) ? 0u : (uint32_t)(ceilDiv(nr, rc) * ceilDiv(ns, sc));
+  const uint32_t c = (nr == 0 || ns == 0) ? 0u : (uint32_t)(ceilDiv(nr, rc) * ceilDiv(ns, sc));
+  if (heavySpans && nr > rc && c) {
+    const uint32_t nsChunks = (uint32_t)ceilDiv(ns, sc);
+    const uint32_t o = atomicAdd(heavyCount, c);
+    for (uint32_t i = 0; i < c && o + i < heavyCapacity; ++i) {
+      BPSpan sp;
+      sp.rb = partR[p] + (uint64_t)(i / nsChunks) * rc;
+      sp.sb = partS[p] + (uint64_t)(i % nsChunks) * sc;
+      sp.nr = (uint32_t)(min(nr - (uint64_t)(i / nsChunks) * rc, (uint64_t)rc));
+      sp.ns = (uint32_t)(min(ns - (uint64_t)(i % nsChunks) * sc, (uint64_t)sc));
+      sp.pad0 = sp.pad1 = 0;
+      heavySpans[o + i] = sp;
+    }
+    counts[p] = 0;
+    return;
+  }
+  counts[p] = c;
 }
 
 void bpPlanCounts(const BPArgs &a, uint32_t *counts, hipStream_t s) {
   if (a.P == 0) return;
+  HJ_CHECK(!a.heavySpans || a.heavyCount, "bpPlanCounts: heavy spans without their counter");
   hipLaunchKernelGGL(bpPlanCountsKernel, dim3(ceilDiv(a.P, BPT)), dim3(BPT), 0, s, a.partR, a.partS,
                      a.partREnd ? a.partREnd : a.partR + 1, a.partSEnd ? a.partSEnd : a.partS + 1, a.P, a.rChunk,
-                     a.sChunk, counts);
+                     a.sChunk, counts, a.heavySpans, a.heavyCount, a.heavyCapacity);
   HIP_CHECK_LAUNCH();
 }
 
@@ -1361,10 +1383,8 @@ __global__ __launch_bounds__(T, MINW) void bpKeySpanKernel(KsSrc<T, K, SPLIT> R,
       S.load(d.sb, d.ns, sv);
     }
     for (uint32_t i = 0; i < cnt; ++i) {
-      const uint64_t rb = __builtin_amdgcn_readfirstlane((uint32_t)desc[i].rb) |
-                          ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(desc[i].rb >> 32)) << 32);
-      const uint64_t sb = __builtin_amdgcn_readfirstlane((uint32_t)desc[i].sb) |
-                          ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(desc[i].sb >> 32)) << 32);
+      const uint64_t rb = uniform64(desc[i].rb);
+      const uint64_t sb = uniform64(desc[i].sb);
       const uint32_t nr = __builtin_amdgcn_readfirstlane(desc[i].nr);
       const uint32_t ns = __builtin_amdgcn_readfirstlane(desc[i].ns);
       uint32_t tbits = nr > 1 ? 32 - __clz(2 * nr - 1) : 1;
@@ -1492,6 +1512,42 @@ __device__ __forceinline__ uint32_t kqProbeBatch(const uint64_t (&pv)[K], uint32
   return matches;
 }
 
+// Probe of a counted table (bpKeyCountedSpansKernel): entry e = (stored value,
+// count - 1) in the two slots of bucket e, one entry per distinct key, linear
+// probing; a probe stops at its key or at an empty entry.
+template <int T, int K>
+__device__ __forceinline__ uint32_t kqProbeCounted(const uint64_t (&pv)[K], uint32_t valid, uint32_t s,
+                                                   const uint2 *tab2, const unsigned long long *side, uint32_t nSide) {
+  uint32_t bk[K], v[K];
+  uint2 x[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    kqKey(pv[k], s, bk[k], v[k]);
+    x[k] = tab2[bk[k]];
+  }
+  uint32_t matches = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    uint32_t c = 0, e = bk[k];
+    uint2 y = x[k];
+    for (;;) {
+      if (y.x == v[k]) {
+        c = y.y + 1;
+        break;
+      }
+      if (y.x == KQ_EMPTY) break;
+      e = (e + 1) & (KQ_BUCKETS - 1);
+      y = tab2[e];
+    }
+    if (v[k] == KQ_EMPTY) {  // escape: the side list
+      c = 0;
+      for (uint32_t j = 0; j < nSide; ++j) c += side[j] == pv[k];
+    }
+    matches += (uint32_t)(k * T) + threadIdx.x < valid ? c : 0u;
+  }
+  return matches;
+}
+
 size_t bpKeyQuotientLdsBytes() {
   return KQ_BUCKETS * 8 + KQ_SIDE * 8 + 16 + KS_CHUNK * sizeof(BPSpan) + 16 * 8 + 16;
 }
@@ -1536,8 +1592,7 @@ __global__ __launch_bounds__(T, MINW) void bpKeyQuotientKernel(KsSrc<T, K, true>
       S.load(d.sb, d.ns, sv);
     }
     for (uint32_t i = 0; i < cnt; ++i) {
-      const uint64_t sb = __builtin_amdgcn_readfirstlane((uint32_t)desc[i].sb) |
-                          ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(desc[i].sb >> 32)) << 32);
+      const uint64_t sb = uniform64(desc[i].sb);
       const uint32_t nr = __builtin_amdgcn_readfirstlane(desc[i].nr);
       const uint32_t ns = __builtin_amdgcn_readfirstlane(desc[i].ns);
       // ---- build (nr <= BATCH: one batch, from registers)
@@ -1618,6 +1673,98 @@ static void launchKeyQuotient(const BPArgs &a, const BPSpan *spans, const uint32
   HIP_CHECK(hipMemsetAsync(queue, 0, sizeof(uint32_t), st));
   hipLaunchKernelGGL((bpKeyQuotientKernel<T, K, 8>), grid, dim3(T), lds, st, KsSrc<T, K, true>{a.R, a.Rhi},
                      KsSrc<T, K, true>{a.S, a.Shi}, spans, nSpans, capacity, queue, s, a.result, a.sideOverflow);
+  HIP_CHECK_LAUNCH();
+}
+
+// ------------------------------------- key-only: partitions with repeated keys
+// Partitions with more than rChunk inner tuples (with unique keys a few in a
+// thousand, just above the mean; with repeated keys the hot ones) skip the
+// span work queue, whose one-slot-per-tuple quotient table chains the copies
+// of a key: O(copies^2) CAS steps per span and a chain walk per probe.  Their
+// spans (bpPlanCounts -> heavySpans, same rChunk x sChunk tiling) are counted
+// here on a *counted* table over the same 32 KiB: entry e = (stored value,
+// count - 1) in the two slots of bucket e, one entry per distinct key with
+// linear probing, so copies only add to a count.  A span's <= 2048 inner
+// tuples fill at most half of the 4096 entries.  Escape keys use the side list
+// as in the span kernel (its overflow re-runs on v2).  A hot partition's spans
+// spread over workgroups like any others.
+template <int T, int K>
+__global__ __launch_bounds__(T) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R, KsSrc<T, K, true> S,
+                                                              const BPSpan *__restrict__ spans,
+                                                              const uint32_t *__restrict__ nSpansPtr, uint32_t capacity,
+                                                              uint32_t s, unsigned long long *__restrict__ result,
+                                                              unsigned long long *__restrict__ sideOverflow) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t *tab = reinterpret_cast<uint32_t *>(smem);  // [entry][value, count - 1]
+  const uint2 *tab2 = reinterpret_cast<const uint2 *>(smem);
+  unsigned long long *side = reinterpret_cast<unsigned long long *>(tab + 2 * KQ_BUCKETS);
+  uint32_t *ctl = reinterpret_cast<uint32_t *>(side + KQ_SIDE);  // [0] side list length
+  unsigned long long *wsum = reinterpret_cast<unsigned long long *>(ctl + 4);
+  constexpr uint32_t BATCH = T * K;
+  const uint32_t t = threadIdx.x;
+  const uint32_t n = min(*nSpansPtr, capacity);
+  uint64_t matches = 0;
+  bool overflow = false;
+  auto clear = [&]() {
+    uint4 *t4 = reinterpret_cast<uint4 *>(tab);
+    for (uint32_t i = t; i < KQ_BUCKETS / 2; i += T) t4[i] = make_uint4(KQ_EMPTY, KQ_EMPTY, KQ_EMPTY, KQ_EMPTY);
+    if (t == 0) ctl[0] = 0;
+  };
+  clear();
+  __syncthreads();
+  for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
+    const BPSpan sp = spans[w];
+    // ---- build: nr <= rChunk <= BATCH, one pass
+    uint64_t rv[K];
+    R.load(sp.rb, sp.nr, rv);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if ((uint32_t)(k * T) + t >= sp.nr) continue;
+      uint32_t e, v;
+      kqKey(rv[k], s, e, v);
+      if (v == KQ_EMPTY) {  // escape: side list
+        const uint32_t at = atomicAdd(&ctl[0], 1u);
+        if (at < KQ_SIDE) side[at] = rv[k];
+        continue;
+      }
+      for (;;) {
+        const uint32_t o = atomicCAS(&tab[2 * e], KQ_EMPTY, v);
+        if (o == KQ_EMPTY || o == v) {
+          atomicAdd(&tab[2 * e + 1], 1u);  // KQ_EMPTY + 1 = 0: the slot holds count - 1
+          break;
+        }
+        e = (e + 1) & (KQ_BUCKETS - 1);
+      }
+    }
+    __syncthreads();
+    const uint32_t nSide = min(ctl[0], KQ_SIDE);
+    overflow |= ctl[0] > KQ_SIDE;
+    // ---- probe the span's outer words
+    for (uint32_t b0 = 0; b0 < sp.ns; b0 += BATCH) {
+      const uint32_t ns = min(sp.ns - b0, BATCH);
+      uint64_t xv[K];
+      S.load(sp.sb + b0, ns, xv);
+      matches += kqProbeCounted<T, K>(xv, ns, s, tab2, side, nSide);
+    }
+    __syncthreads();
+    clear();
+    __syncthreads();
+  }
+  const unsigned long long total = blockReduceSum<T, unsigned long long>((unsigned long long)matches, wsum);
+  if (t == 0 && total) atomicAdd(result, total);
+  if (overflow && t == 0) atomicOr(sideOverflow, 1ull);
+}
+
+void bpKeyCountedSpans(const BPArgs &a, hipStream_t st) {
+  constexpr int T = 512, K = 4;
+  HJ_CHECK(bpKeyQuotientFits(a) && a.rChunk <= (uint32_t)(T * K) && a.heavySpans && a.heavyCount && a.sideOverflow,
+           "bpKeyCountedSpans: needs the quotient-table layout and the heavy span list");
+  const uint32_t s = a.keyFragBits > 32 ? a.keyFragBits - 32 : 0;
+  const size_t lds = KQ_BUCKETS * 8 + KQ_SIDE * 8 + 16 + 16 * 8 + 16;
+  const dim3 grid(std::min<uint32_t>(std::max<uint32_t>(a.heavyCapacity, 1), 256 * 4));
+  hipLaunchKernelGGL((bpKeyCountedSpansKernel<T, K>), grid, dim3(T), lds, st, KsSrc<T, K, true>{a.R, a.Rhi},
+                     KsSrc<T, K, true>{a.S, a.Shi}, a.heavySpans, a.heavyCount, a.heavyCapacity, s, a.result,
+                     a.sideOverflow);
   HIP_CHECK_LAUNCH();
 }
 

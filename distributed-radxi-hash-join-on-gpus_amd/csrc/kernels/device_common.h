@@ -24,6 +24,16 @@ __device__ __forceinline__ T waveInclusiveScan(T x) {
   return x;
 }
 
+// A wave-uniform 64-bit value moved to scalar registers.  readfirstlane
+// returns int: each half goes through uint32_t, or a low half with bit 31 set
+// would sign-extend over the high half (a silent wrong address past 2^31
+// elements, not a fault).
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
 template <typename T>
 __device__ __forceinline__ T waveReduceSum(T x) {
 #pragma unroll

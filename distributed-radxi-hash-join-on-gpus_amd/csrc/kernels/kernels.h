@@ -280,6 +280,13 @@ uint64_t localSampledCapacityBound(uint64_t n, uint64_t partitions, uint32_t sam
 void claimOverflow(unsigned long long *gcur, const unsigned long long *gend, uint64_t P, unsigned int *flag,
                    hipStream_t s);
 
+// A resolved work item of key-only counting: one inner chunk against one
+// outer chunk of a final partition.
+struct BPSpan {
+  unsigned long long rb, sb;  // first inner / outer word of the span
+  uint32_t nr, ns;            // inner (<= rChunk) / outer (<= sChunk) words
+  uint32_t pad0, pad1;
+};
 // --------------------------------------------------------------- build/probe
 struct BPItem {
   uint32_t part;
@@ -338,6 +345,13 @@ struct BPArgs {
   // Quotient-table kernel: set to nonzero when a span had more escape keys
   // than its side list holds (the count is then void: re-run on keyCount 7).
   unsigned long long *sideOverflow = nullptr;
+  // Optional (key-only spans with the quotient table): bpPlanCounts writes
+  // the spans of partitions with more than rChunk inner tuples here (at most
+  // heavyCapacity; heavyCount: u32 total, zeroed by the caller) instead of
+  // giving them work items.
+  BPSpan *heavySpans = nullptr;
+  uint32_t *heavyCount = nullptr;
+  uint32_t heavyCapacity = 0;
   // Kernel variants (KernelVariants::keyCount / rowsLds).
   uint32_t keyCount = 8;
   uint32_t rowsLds = 1;
@@ -369,11 +383,6 @@ void buildProbe(const BPArgs &a, const BPItem *items, const uint32_t *nItems, ui
 // every item's bounds looked up once (bpEmitSpans), consumed through a device
 // work queue (queue: one u32, cleared by the launcher) with the next span's
 // words prefetched during the current probe.
-struct BPSpan {
-  unsigned long long rb, sb;  // first inner / outer word of the span
-  uint32_t nr, ns;            // inner (<= rChunk) / outer (<= sChunk) words
-  uint32_t pad0, pad1;
-};
 void bpEmitSpans(const BPArgs &a, const uint32_t *counts, const uint32_t *offsets, BPSpan *spans, uint32_t capacity,
                  hipStream_t s);
 void buildProbeKeySpans(const BPArgs &a, const BPSpan *spans, const uint32_t *nSpans, uint32_t capacity,
@@ -381,6 +390,10 @@ void buildProbeKeySpans(const BPArgs &a, const BPSpan *spans, const uint32_t *nS
 // keyCount 8 (quotient table, build_probe.hip) applies: split key-only words
 // of <= 44 fragment bits, rChunk <= 2048.
 bool bpKeyQuotientFits(const BPArgs &a);
+// The spans bpPlanCounts wrote to a.heavySpans (partitions of repeated inner
+// keys): counted tables (build_probe.hip, bpKeyCountedSpansKernel); adds to
+// a.result.
+void bpKeyCountedSpans(const BPArgs &a, hipStream_t s);
 
 // Single-level counting join of unique inner keys (bitmap_join.hip): one
 // workgroup per network partition sets a 2^bits LDS bitmap from the inner

@@ -146,9 +146,18 @@ void BuildProbe::execute() {
                                  (double)(2ull * std::max<uint32_t>(args.P, 1) * 4 + kernels::scanWorkspaceBytes(args.P) +
                                           (uint64_t)capacity * sizeof(kernels::BPItem) + kernels::bpLdsBytes(args)),
                                  "bytes");
+  // Key-only counting on the quotient table: partitions of repeated keys go
+  // to the counted-table kernel instead of the span work queue.
+  const bool keySpans = args.keyOnly && (args.keyCount >= 6 || args.split);  // the item kernels read unsplit words only
+  const bool counted = keySpans && args.keyCount == 8 && kernels::bpKeyQuotientFits(args);
+  if (counted) {
+    args.heavySpans = ws.getArray<kernels::BPSpan>(capacity);
+    args.heavyCapacity = capacity;
+    args.heavyCount = nItems + 1;  // high half of counters[2]: read back with the rest
+  }
   kernels::bpPlanCounts(args, counts, ctx->stream());
   kernels::scanExclusiveU32(counts, offsets, args.P, nItems, scanWs, ctx->stream());
-  if (args.keyOnly && (args.keyCount >= 6 || args.split)) {  // the item kernels read unsplit words only
+  if (keySpans) {
     // Key-only counting: resolved spans through a device work queue.
     auto *spans = ws.getArray<kernels::BPSpan>(capacity);
     uint32_t *queue = ws.getArray<uint32_t>(1);
@@ -156,6 +165,7 @@ void BuildProbe::execute() {
     args.sideOverflow = counters + 3;  // quotient table: escape side list overflowed
     tl.beginSplit("BPKERNEL", "BPBUILD", wb, "BPPROBE", wp, ctx->stream());
     kernels::buildProbeKeySpans(args, spans, nItems, capacity, queue, ctx->stream());
+    if (counted) kernels::bpKeyCountedSpans(args, ctx->stream());
     hipEvent_t done = tl.mark(ctx->stream());
     tl.endAt("BPKERNEL", done);
     tl.endAt("BPTASKTIME", done);
@@ -213,16 +223,17 @@ bool BuildProbe::collect() {
   std::memcpy(h, countersBack, sizeof(h));
   matches = h[0];
   outputCount = h[1];
-  uint32_t items;
+  uint32_t items, heavy;
   std::memcpy(&items, &h[2], sizeof(items));
-  workItems = items;
+  std::memcpy(&heavy, reinterpret_cast<const char *>(&h[2]) + sizeof(items), sizeof(heavy));
+  workItems = items + heavy;
   bool again = false;
   if (args.sideOverflow && h[3]) {  // too many escape keys in one span: count on the v2 table
     quotientFallback = true;
     again = true;
   }
-  if (items > capacity) {
-    capacity = items;
+  if (items > capacity || heavy > capacity) {
+    capacity = std::max(items, heavy);
     again = true;
   }
   if (plan.materialize && outputCount > outputCapacity) {

@@ -364,6 +364,34 @@ def test_sampled_general_path_device_layout(C, sizes):
         assert res["sampled_network"] and res["network_fallbacks"] == 0, res
 
 
+@pytest.mark.gpu
+def test_key_only_outer_past_2g_elements(C):
+    """General path with the outer side's local output past 2^31 elements
+    (1.6e9 outer tuples in a gapped sampled layout of ~2.6e9 slots): span
+    offsets above 2^31 must reach the build/probe intact.  Regression: the
+    wave-uniform span offset was rebuilt from two readfirstlane halves whose
+    low half sign-extended, so every probe batch after the first read from
+    16 GiB below the partition (1.5076e9 of 1.6e9 matches, no fault)."""
+    G_R, G_S = 100_000_000, 1_600_000_000
+    ctx = C.ExecContext("device", 0, C.LocalCommunicator())
+    inner = C.GenSpec(seed=61)
+    inner.sparse64 = True
+    outer = C.GenSpec(distribution=C.KeyDistribution.UNIFORM, seed=62, domain=G_R)
+    outer.sparse64 = True
+    R = C.Relation(G_R, G_R, "device", 0)
+    S = C.Relation(G_S, G_S, "device", 0)
+    R.generate(inner, 0)
+    S.generate(outer, 0)
+    cfg = C.JoinConfig()
+    cfg.network_bits, cfg.local_bits = 10, 9  # ~3052 outer tuples per final partition: two probe batches
+    j = C.HashJoin(R, S, ctx, cfg)
+    assert j.plan.key_only, j.plan
+    res = j.run()
+    assert res["global_matches"] == G_S, (res["global_matches"], G_S)
+    del j, R, S
+    ctx.reset_scratch()
+
+
 def quotient_escape_fragments(n, first_bucket=0):
     """Fragments the quotient table (build_probe.hip, bpKeyQuotientKernel) can
     only hold in its side list: 44-bit fragments f (63-bit keys above 10 + 9
@@ -450,8 +478,9 @@ def test_sparse64_join_auto_wide(C, dev):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dup", [1, 37, 3000])
-def test_key_only_count_duplicates(C, cuda, dup):
+@pytest.mark.parametrize("dup,bits", [(1, None), (37, None), (3000, None), (37, (10, 9)), (3000, (10, 9)),
+                                      (200_000, (10, 9))])
+def test_key_only_count_duplicates(C, cuda, dup, bits):
     """KCOUNT build/probe (key-only words, bucketized LDS table) with every
     inner key repeated `dup` times: long bucket pass-through chains (3000
     copies overflow hundreds of 4-slot buckets) and partial batches; the
@@ -473,10 +502,14 @@ def test_key_only_count_duplicates(C, cuda, dup):
     R, S = rows(rk), rows(sk)
     ctx = C.ExecContext("device", 0, C.LocalCommunicator())
     cfg = C.JoinConfig()
+    if bits:  # 44-bit fragments: the quotient table, partitions of repeated keys on counted tables
+        cfg.network_bits, cfg.local_bits = bits
     j = C.HashJoin(C.Relation.from_tensor(R, R.shape[0]), C.Relation.from_tensor(S, S.shape[0]), ctx, cfg)
     assert j.plan.key_only and not j.plan.bitmap_join, j.plan
     for _ in range(2):
-        assert j.run()["global_matches"] == exp
+        res = j.run()
+        assert res["global_matches"] == exp, (dup, bits, res["global_matches"], exp)
+        assert res["reruns"] == 0, res["reruns"]
 
 
 @pytest.mark.parametrize("dev", devices())
