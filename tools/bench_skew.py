@@ -11,6 +11,8 @@ Configs (one JSON line each, rank 0):
                 the two-level plan (+ LPT / hot-partition split at N > 1) runs
   uniform_two   inner unique, outer uniform foreign keys, bitmap plan off: the
                 two-level reference time the Zipf run is compared with
+  uniform_sparse  uniform_two through the sparse 63-bit key bijection: the
+                general path at this size (1B x 4B: outer slots past 2^31)
   zipf_outer    inner unique, outer Zipf(theta) (default plan)
 Assignment variants at N > 1: --assign lpt,round_robin and --split on,off.
 
@@ -103,9 +105,10 @@ def run_config(C, info, ctx, comm, name, G_R, G_S, theta, cfg, steps, warmup):
     elif name == "zipf_outer":
         inner = C.GenSpec(distribution=C.KeyDistribution.UNIQUE, seed=1234)
         outer = C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=4321, domain=domain, zipf_theta=theta)
-    else:  # uniform_two
+    else:  # uniform_two, uniform_sparse
         inner = C.GenSpec(distribution=C.KeyDistribution.UNIQUE, seed=1234)
         outer = C.GenSpec(distribution=C.KeyDistribution.UNIFORM, seed=4321, domain=domain)
+        inner.sparse64 = outer.sparse64 = name == "uniform_sparse"
     lr, ls = (C.Relation.local_size_for(G, info.rank, info.world) for G in (G_R, G_S))
 
     def relations():
