@@ -78,21 +78,22 @@ __device__ __forceinline__ uint32_t hash64(uint64_t key, uint32_t tbits) {
   return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - tbits));
 }
 
-// heavySpans (optional): partitions with more than rChunk inner tuples
-// (repeated keys) get no work items here; their spans go to heavySpans
-// instead (appended at *heavyCount, at most heavyCapacity written) for
-// bpKeyCountedSpans.
+// heavySpans (optional): partitions with more than heavyMin inner tuples
+// (rChunk: more than one table; 0 once repeated keys were seen) get no work
+// items here; their spans go to heavySpans instead (appended at *heavyCount,
+// at most heavyCapacity written) for bpKeyCountedSpans.
 __global__ __launch_bounds__(BPT) void bpPlanCountsKernel(const uint64_t *__restrict__ partR,
                                                           const uint64_t *__restrict__ partS,
                                                           const uint64_t *__restrict__ partREnd,
                                                           const uint64_t *__restrict__ partSEnd, uint32_t P, uint32_t rc,
                                                           uint32_t sc, uint32_t *counts, BPSpan *__restrict__ heavySpans,
-                                                          uint32_t *__restrict__ heavyCount, uint32_t heavyCapacity) {
+                                                          uint32_t *__restrict__ heavyCount, uint32_t heavyCapacity,
+                                                          uint32_t heavyMin) {
   const uint32_t p = blockIdx.x * BPT + threadIdx.x;
   if (p >= P) return;
   const uint64_t nr = partREnd[p] - partR[p], ns = partSEnd[p] - partS[p];
   const uint32_t c = (nr == 0 || ns == 0) ? 0u : (uint32_t)(ceilDiv(nr, rc) * ceilDiv(ns, sc));
-  if (heavySpans && nr > rc && c) {
+  if (heavySpans && nr > heavyMin && c) {
     const uint32_t nsChunks = (uint32_t)ceilDiv(ns, sc);
     const uint32_t o = atomicAdd(heavyCount, c);
     for (uint32_t i = 0; i < c && o + i < heavyCapacity; ++i) {
@@ -115,7 +116,8 @@ void bpPlanCounts(const BPArgs &a, uint32_t *counts, hipStream_t s) {
   HJ_CHECK(!a.heavySpans || a.heavyCount, "bpPlanCounts: heavy spans without their counter");
   hipLaunchKernelGGL(bpPlanCountsKernel, dim3(ceilDiv(a.P, BPT)), dim3(BPT), 0, s, a.partR, a.partS,
                      a.partREnd ? a.partREnd : a.partR + 1, a.partSEnd ? a.partSEnd : a.partS + 1, a.P, a.rChunk,
-                     a.sChunk, counts, a.heavySpans, a.heavyCount, a.heavyCapacity);
+                     a.sChunk, counts, a.heavySpans, a.heavyCount, a.heavyCapacity,
+                     a.heavyMin);
   HIP_CHECK_LAUNCH();
 }
 
@@ -1469,6 +1471,11 @@ constexpr uint32_t KQ_BUCKETS = 1u << KQ_BITS;
 constexpr uint32_t KQ_EMPTY = 0xFFFFFFFFu;
 constexpr uint32_t KQ_SIDE = 64;
 constexpr uint32_t KQ_NONE = 0xFFFFFFFFu;
+// A placement that walked past this many slots saw one key's copies chained
+// (unique keys at <= 25 % load never do): the kernel reports it (bit 1 of
+// *sideOverflow) and later joins put every partition on counted spans
+// (KernelVariants::keyCount 9).
+constexpr uint32_t KQ_LONG_CHAIN = 64;
 
 __device__ __forceinline__ uint32_t kqSalt(uint32_t b) { return (b + 1u) * 0x85EBCA77u; }
 
@@ -1576,7 +1583,7 @@ __global__ __launch_bounds__(T, MINW) void bpKeyQuotientKernel(KsSrc<T, K, true>
     if (t == 0) *sideN = 0;
   }
   uint64_t matches = 0;
-  bool overflow = false;
+  bool overflow = false, chained = false;
   uint64_t rv[K], sv[K], nrv[K], nsv[K];
   for (;;) {
     if (t == 0) *qbase = atomicAdd(queue, KS_CHUNK);
@@ -1618,6 +1625,7 @@ __global__ __launch_bounds__(T, MINW) void bpKeyQuotientKernel(KsSrc<T, K, true>
           uint32_t p = pos[k] + 1;
           while (atomicCAS(&tab[p], KQ_EMPTY, v[k]) != KQ_EMPTY)
             p = (p & 1) ? ((((p >> 1) + 1) & (KQ_BUCKETS - 1)) << 1) : p + 1;
+          chained |= ((p - pos[k]) & (2 * KQ_BUCKETS - 1)) > KQ_LONG_CHAIN;
           pos[k] = p;
         }
       }
@@ -1653,6 +1661,7 @@ __global__ __launch_bounds__(T, MINW) void bpKeyQuotientKernel(KsSrc<T, K, true>
   const unsigned long long total = blockReduceSum<T, unsigned long long>((unsigned long long)matches, wsum);
   if (t == 0 && total) atomicAdd(result, total);
   if (overflow && t == 0) atomicOr(sideOverflow, 1ull);
+  if (__any(chained) && (t & (WAVE - 1)) == 0) atomicOr(sideOverflow, 2ull);
 }
 
 bool bpKeyQuotientFits(const BPArgs &a) {
@@ -1780,7 +1789,7 @@ void buildProbeKeySpans(const BPArgs &a, const BPSpan *spans, const uint32_t *nS
   HJ_CHECK(a.keyOnly && !a.materialize && !a.wide, "buildProbeKeySpans: key-only counting joins only");
   HJ_CHECK(!a.split || (a.Rhi && a.Shi), "buildProbeKeySpans: split layout without high columns");
   HJ_CHECK(a.rChunk <= (uint32_t)(T * K), "buildProbeKeySpans: rChunk %u above one %d-word batch", a.rChunk, T * K);
-  if (a.keyCount == 8 && bpKeyQuotientFits(a)) {
+  if ((a.keyCount == 8 || a.keyCount == 9) && bpKeyQuotientFits(a)) {
     launchKeyQuotient(a, spans, nSpans, capacity, queue, s);
     return;
   }
@@ -1793,7 +1802,7 @@ void buildProbeKeySpans(const BPArgs &a, const BPSpan *spans, const uint32_t *nS
   hipLaunchKernelGGL((bpKeySpanKernel<T, K, H, 8, SPLIT, SOA>), grid, dim3(T), lds, s,                            \
                      KsSrc<T, K, SPLIT>{a.R, SPLIT ? a.Rhi : nullptr}, KsSrc<T, K, SPLIT>{a.S, SPLIT ? a.Shi : nullptr}, \
                      spans, nSpans, capacity, queue, a.rChunk, a.result)
-  const bool soa = a.keyCount == 7 || a.keyCount == 8;
+  const bool soa = a.keyCount >= 7;
   if (a.split) {
     if (soa) HJ_KS(true, true); else HJ_KS(true, false);
   } else {

@@ -342,8 +342,9 @@ struct BPArgs {
   // Key-only words: bits of the fragment above both radix digits (0 =
   // unknown); the quotient-table kernel (keyCount 8) needs <= 44.
   uint32_t keyFragBits = 0;
-  // Quotient-table kernel: set to nonzero when a span had more escape keys
-  // than its side list holds (the count is then void: re-run on keyCount 7).
+  // Quotient-table kernel: bit 0 set when a span had more escape keys than
+  // its side list holds (the count is then void: re-run on keyCount 7); bit 1
+  // when a key's copies chained (count exact; keyCount 9 from then on).
   unsigned long long *sideOverflow = nullptr;
   // Optional (key-only spans with the quotient table): bpPlanCounts writes
   // the spans of partitions with more than rChunk inner tuples here (at most
@@ -352,6 +353,7 @@ struct BPArgs {
   BPSpan *heavySpans = nullptr;
   uint32_t *heavyCount = nullptr;
   uint32_t heavyCapacity = 0;
+  uint32_t heavyMin = 0xFFFFFFFFu;  // inner tuples above which a partition is heavy
   // Kernel variants (KernelVariants::keyCount / rowsLds).
   uint32_t keyCount = 8;
   uint32_t rowsLds = 1;

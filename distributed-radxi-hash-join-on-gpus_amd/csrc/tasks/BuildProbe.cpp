@@ -61,7 +61,7 @@ void BuildProbe::configure() {
   args.wide = plan.wide;
   args.keyOnly = plan.keyOnly;
   args.materialize = plan.materialize;
-  args.keyCount = quotientFallback && plan.variants.keyCount == 8 ? 7 : plan.variants.keyCount;
+  args.keyCount = quotientFallback && plan.variants.keyCount >= 8 ? 7 : plan.variants.keyCount;
   if (plan.keyOnly) {
     const uint32_t passBits = plan.networkBits + wi->getLocalBits();
     args.keyFragBits = plan.keyBits > passBits ? plan.keyBits - passBits : 1;
@@ -149,10 +149,12 @@ void BuildProbe::execute() {
   // Key-only counting on the quotient table: partitions of repeated keys go
   // to the counted-table kernel instead of the span work queue.
   const bool keySpans = args.keyOnly && (args.keyCount >= 6 || args.split);  // the item kernels read unsplit words only
-  const bool counted = keySpans && args.keyCount == 8 && kernels::bpKeyQuotientFits(args);
+  const bool counted = keySpans && args.keyCount >= 8 && kernels::bpKeyQuotientFits(args);
   if (counted) {
     args.heavySpans = ws.getArray<kernels::BPSpan>(capacity);
     args.heavyCapacity = capacity;
+    // keyCount 9 (repeated keys seen): every partition on counted tables.
+    args.heavyMin = args.keyCount == 9 ? 0 : args.rChunk;
     args.heavyCount = nItems + 1;  // high half of counters[2]: read back with the rest
   }
   kernels::bpPlanCounts(args, counts, ctx->stream());
@@ -228,7 +230,8 @@ bool BuildProbe::collect() {
   std::memcpy(&heavy, reinterpret_cast<const char *>(&h[2]) + sizeof(items), sizeof(heavy));
   workItems = items + heavy;
   bool again = false;
-  if (args.sideOverflow && h[3]) {  // too many escape keys in one span: count on the v2 table
+  if (h[3] & 2) duplicateChains = true;  // exact count; later joins use counted tables throughout
+  if (args.sideOverflow && (h[3] & 1)) {  // too many escape keys in one span: count on the v2 table
     quotientFallback = true;
     again = true;
   }

@@ -52,6 +52,8 @@ class BuildProbe : public Task {
   // A span overflowed the quotient table's side list and this task re-ran
   // on the v2 table (collect() returned true for it).
   bool quotientFellBack() const { return quotientFallback; }
+  // The quotient table chained copies of a key (repeated inner keys).
+  bool sawDuplicateChains() const { return duplicateChains; }
   bool rowsFused() const { return fused; }
 
  protected:
@@ -78,6 +80,7 @@ class BuildProbe : public Task {
   uint32_t workItems = 0;
   bool reference = false, overflowOut = false, fused = false;
   bool quotientFallback = false;  // a span overflowed the quotient table's side list: keyCount 7 from now on
+  bool duplicateChains = false;   // copies of a key chained in the quotient table
   const kernels::RowSink *sink = nullptr;
   uint64_t hostCursor = 0;
 };
