@@ -654,6 +654,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("checks", &core::JoinConfig::checks)
       .def_readwrite("max_partition_blocks", &core::JoinConfig::maxPartitionBlocks)
       .def_readwrite("reserve_workspace", &core::JoinConfig::reserveWorkspace)
+      .def_readwrite("workspace_budget", &core::JoinConfig::workspaceBudget)
       .def_readwrite("link_gbps_per_peer", &core::JoinConfig::linkGBpsPerPeer)
       // KernelVariants, flattened (sweeps / A-B tests; core/Types.h)
       .def_property("net_ipt", [](const core::JoinConfig &c) { return c.variants.netIpt; },
@@ -820,6 +821,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            "Rewind the arenas; if the last join spilled into fallback allocations, re-reserve one block of "
            "the observed peak now (so the next join does not pay for it)")
       .def("reserve_workspace", [](core::ExecContext &c, uint64_t b) { c.workspace().reserve(b); })
+      .def("trim_workspace", [](core::ExecContext &c, uint64_t keep) {
+             c.synchronize();
+             return c.workspace().trim(keep);
+           },
+           py::arg("keep") = 0,
+           "Between joins: shrink the workspace to one chunk of `keep` bytes; returns the bytes freed")
+      .def("workspace_generation", [](core::ExecContext &c) { return c.workspace().generation(); })
+      .def("ensure_workspace", [](core::ExecContext &c, uint64_t b) { return c.workspace().ensure(b); })
+      .def("workspace_scratch", [](core::ExecContext &c, uint64_t b) {
+             return reinterpret_cast<uintptr_t>(c.workspace().get(b));
+           }, "Hand out b bytes of the workspace (tests of the arena's growth rules)")
       .def("synchronize", &core::ExecContext::synchronize);
 
   py::class_<data::GenSpec>(m, "GenSpec")

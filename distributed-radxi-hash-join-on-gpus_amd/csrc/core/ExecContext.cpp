@@ -116,7 +116,12 @@ void *ExecContext::ipcImport(uint32_t peer, const uint64_t handle[8], uint64_t g
   std::vector<uint64_t> key(handle, handle + 8);
   for (size_t i = 0; i < ipcImported_.size();) {
     IpcMapping &m = ipcImported_[i];
-    if (m.peer == peer && m.generation != generation) {  // stale: the peer's allocations changed
+    // Stale: the peer FREED memory since this mapping was opened (its arena's
+    // generation counts frees only, and frees happen between joins), so no
+    // window of the current join points into it.  Growth inside a join (a
+    // fallback allocation behind the peer's second window) keeps the
+    // generation: the first window's mapping stays open.
+    if (m.peer == peer && m.generation != generation) {
       HIP_CHECK(hipIpcCloseMemHandle(m.base));
       ipcImported_.erase(ipcImported_.begin() + i);
       continue;

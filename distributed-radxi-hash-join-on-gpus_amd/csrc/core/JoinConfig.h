@@ -113,6 +113,10 @@ struct JoinConfig {
   // HashJoin construction (and touch the new pages once), so that the first
   // join allocates nothing (HashJoin::workspaceEstimate).
   bool reserveWorkspace = true;
+  // Upper bound in bytes of that reservation (0 = 85 % of the HBM free at
+  // construction).  The arena never frees on its own; ExecContext's trim
+  // (Python: ExecContext.trim_workspace) gives it back between joins.
+  uint64_t workspaceBudget = 0;
   // Link model of the N > 1 plan choice / prediction: one-way GB/s one rank
   // reaches to one peer (0 = kDefaultLinkGBpsPerPeer; bench.py calibrates it
   // with an RCCL all-to-all).

@@ -1453,83 +1453,131 @@ __global__ __launch_bounds__(T, MINW) void bpKeySpanKernel(KsSrc<T, K, SPLIT> R,
 //   e = frag >> s (32 bits, s = f - 32)   and   lo = frag's low s bits;
 //   bucket b = (lo ^ h(e)) mod 2^KQ_BITS   (h: multiplicative hash of e),
 // and the bucket stores only v = e ^ salt(b): (b, v) determines the fragment
-// (lo = b ^ h(e) on its low s bits), so equal (b, v) <=> equal keys, and a
-// slot is 4 bytes.  Buckets are two u32 slots = one 8-byte ds_read_b64 per
-// probe (two 32-lane groups, ~7 cycles with conflicts); 4096 buckets (32 KiB)
-// hold <= 2048 inner keys at load <= 1/4, so a bucket is full -- and the probe
-// reads the next one -- for ~1-2 % of keys.  Slots are filled by LDS CAS
-// (slot 0, then 1, then the next bucket), so a probe stops at the first
-// bucket whose slot 1 is empty and sees every duplicate of its key.
-// The empty marker KQ_EMPTY is a legal v: such "escape" keys (one fragment per
-// bucket, chance 2^-32 per random key) go to a small side list that escape
-// probes scan; more than KQ_SIDE escapes in one span set a flag and the host
-// re-runs the join's build/probe on the v2 kernel (BuildProbe::collect).
-// Slots written by a span's build are reset by the same lanes after its probe:
-// no per-span table clear.
+// (lo = b ^ h(e) on its low s bits), so a slot is 4 bytes.  Buckets are two
+// u32 slots = one 8-byte ds_read_b64 per probe; 4096 buckets (32 KiB) hold
+// <= 2048 inner keys at load <= 1/4.
+//
+// Exactness: (b, v) names a key only in ITS OWN bucket b.  A key therefore
+// never leaves its home bucket in the quotient table: the third and later
+// keys of a bucket, and "escape" keys whose v equals the empty marker (one
+// fragment per bucket), go to a small overflow table of full 48-bit
+// fragments (KQ_OV entries, linear probing, compared whole).  Slots fill in
+// order (slot 0, slot 1, overflow), so a probe whose home bucket has an empty
+// slot 1 has seen every copy of its key; a full home bucket (~9 % of probes
+// at 2048 keys) adds one overflow lookup, the read that used to walk into
+// the next bucket.  (Round 3 let keys spill into the next bucket, where a
+// stored v of another home could equal the probe's: a 2^-32 false match per
+// foreign comparison.)  More than KQ_OV_CAP overflow keys in one span -- a
+// key with hundreds of copies in a light partition -- stops inserting and
+// sets KQF_COUNTED: the count is void and the join's build/probe re-runs on
+// counted tables.  The lanes that built a span reset their own slots after
+// its probe: no table clear.
 constexpr uint32_t KQ_BITS = 12;
 constexpr uint32_t KQ_BUCKETS = 1u << KQ_BITS;
 constexpr uint32_t KQ_EMPTY = 0xFFFFFFFFu;
-constexpr uint32_t KQ_SIDE = 64;
+constexpr uint32_t KQ_OV_BITS = 9;
+constexpr uint32_t KQ_OV = 1u << KQ_OV_BITS;  // overflow entries (4 KiB)
+constexpr uint32_t KQ_OV_CAP = 3 * KQ_OV / 4;  // at most this many inserted: probes always find an empty entry
+constexpr unsigned long long KQ_OV_EMPTY = ~0ull;  // fragments are < 2^48
+constexpr uint32_t KQ_OV_FLAG = 0x80000000u;       // pos[]: overflow-table index
+constexpr uint32_t KQ_SIDE = 64;                   // counted table: escape list
 constexpr uint32_t KQ_NONE = 0xFFFFFFFFu;
-// A placement that walked past this many slots saw one key's copies chained
-// (unique keys at <= 25 % load never do): the kernel reports it (bit 1 of
-// *sideOverflow) and later joins put every partition on counted spans
-// (KernelVariants::keyCount 9).
+// A placement that walked past this many overflow entries saw one key's
+// copies chained (unique keys at <= 25 % overflow load never do): KQF_CHAINS,
+// and later joins put every partition on counted spans (keyCount 9).
 constexpr uint32_t KQ_LONG_CHAIN = 64;
+// BPArgs::sideOverflow bits.
+constexpr unsigned long long KQF_V2 = 1;       // counted escape list overflowed: count void, re-run on v2
+constexpr unsigned long long KQF_CHAINS = 2;   // copies of a key chained (count exact)
+constexpr unsigned long long KQF_COUNTED = 8;  // quotient overflow table full: count void, re-run counted
 
 __device__ __forceinline__ uint32_t kqSalt(uint32_t b) { return (b + 1u) * 0x85EBCA77u; }
 
-// (bucket, stored value) of a fragment; s = fragment bits above 32 (<= KQ_BITS).
-__device__ __forceinline__ void kqKey(uint64_t frag, uint32_t s, uint32_t &b, uint32_t &v) {
+// (bucket, stored value, tag) of a fragment of f <= 48 bits; s = f - 32
+// (0 when f <= 32).  The bucket absorbs the low KQ_BITS of lo, the tag holds
+// the rest of lo (f > 44 only: counted tables keep it next to the count).
+__device__ __forceinline__ void kqKey(uint64_t frag, uint32_t s, uint32_t &b, uint32_t &v, uint32_t &tag) {
   const uint32_t e = (uint32_t)(frag >> s);
   const uint32_t lo = (uint32_t)frag & ((1u << s) - 1u);
   b = (lo ^ ((e * 0x9E3779B1u) >> (32 - KQ_BITS))) & (KQ_BUCKETS - 1);
+  tag = lo >> KQ_BITS;
   v = e ^ kqSalt(b);
 }
 
+__device__ __forceinline__ uint32_t kqOvHash(uint64_t frag) {
+  return (uint32_t)((frag * 0x9E3779B97F4A7C15ull) >> (64 - KQ_OV_BITS));
+}
+
+// Copies of `frag` in the overflow table (it holds < KQ_OV entries).
+__device__ __forceinline__ uint32_t kqOvCount(const unsigned long long *ov, uint64_t frag) {
+  uint32_t h = kqOvHash(frag), c = 0;
+  for (uint32_t w = 0; w < KQ_OV; ++w) {
+    const unsigned long long y = ov[h];
+    if (y == KQ_OV_EMPTY) break;
+    c += y == frag;
+    h = (h + 1) & (KQ_OV - 1);
+  }
+  return c;
+}
+
+// Overflow placement: the entry index | KQ_OV_FLAG, or KQ_NONE when the table
+// is at its cap (full = true: the span's count is void).
+__device__ __forceinline__ uint32_t kqOvInsert(unsigned long long *ov, uint32_t *ovN, uint64_t frag, bool &chained,
+                                               bool &full) {
+  if (atomicAdd(ovN, 1u) >= KQ_OV_CAP) {
+    full = true;
+    return KQ_NONE;
+  }
+  uint32_t h = kqOvHash(frag);
+  for (uint32_t w = 0;; ++w) {  // < KQ_OV_CAP entries taken: an empty one exists
+    if (atomicCAS(&ov[h], KQ_OV_EMPTY, (unsigned long long)frag) == KQ_OV_EMPTY) {
+      chained |= w > KQ_LONG_CHAIN;
+      return KQ_OV_FLAG | h;
+    }
+    h = (h + 1) & (KQ_OV - 1);
+  }
+}
+
 // One batch of T x K outer fragments (the first `valid` counted): all K
-// bucket reads in flight, then the rare walks past full buckets.
+// bucket reads in flight, then the overflow lookups of full home buckets.
 template <int T, int K>
 __device__ __forceinline__ uint32_t kqProbeBatch(const uint64_t (&pv)[K], uint32_t valid, uint32_t s,
-                                                 const uint2 *tab2, const unsigned long long *side, uint32_t nSide) {
-  uint32_t bk[K], v[K];
+                                                 const uint2 *tab2, const unsigned long long *ov) {
+  uint32_t bk[K], v[K], tg[K];
   uint2 x[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    kqKey(pv[k], s, bk[k], v[k]);
+    kqKey(pv[k], s, bk[k], v[k], tg[k]);
     x[k] = tab2[bk[k]];
   }
   uint32_t matches = 0;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    uint32_t c = (uint32_t)(x[k].x == v[k]) + (uint32_t)(x[k].y == v[k]);
-    uint32_t b = bk[k];
-    uint2 y = x[k];
-    while (y.y != KQ_EMPTY) {  // bucket full: keys placed past it continue in the next one
-      b = (b + 1) & (KQ_BUCKETS - 1);
-      y = tab2[b];
-      c += (uint32_t)(y.x == v[k]) + (uint32_t)(y.y == v[k]);
-    }
-    if (v[k] == KQ_EMPTY) {  // escape: the table's empty slots said nothing
-      c = 0;
-      for (uint32_t j = 0; j < nSide; ++j) c += side[j] == pv[k];
-    }
+    const bool esc = v[k] == KQ_EMPTY;  // only in the overflow table
+    uint32_t c = esc ? 0u : (uint32_t)(x[k].x == v[k]) + (uint32_t)(x[k].y == v[k]);
+    if (x[k].y != KQ_EMPTY || esc) c += kqOvCount(ov, pv[k]);
     matches += (uint32_t)(k * T) + threadIdx.x < valid ? c : 0u;
   }
   return matches;
 }
 
-// Probe of a counted table (bpKeyCountedSpansKernel): entry e = (stored value,
-// count - 1) in the two slots of bucket e, one entry per distinct key, linear
-// probing; a probe stops at its key or at an empty entry.
+// Counted table (bpKeyCountedSpansKernel): entry e = one distinct key,
+//   slot 0 = stored value v, slot 1 = id << 16 | (count - 1),  id = dist << 4 | tag,
+// dist = e - home bucket (linear probing).  (v, id) at entry e names exactly
+// one fragment, so a probe compares both and never matches a key of another
+// home.  Claimed by one 64-bit CAS of (v, id, 0) on an empty entry; a copy
+// finding its (v, id) adds 1 to slot 1.  Escape keys (v = empty marker) go to
+// a side list.
+__device__ __forceinline__ uint32_t kqCountedId(uint32_t dist, uint32_t tag) { return (dist << 4) | tag; }
+
 template <int T, int K>
 __device__ __forceinline__ uint32_t kqProbeCounted(const uint64_t (&pv)[K], uint32_t valid, uint32_t s,
                                                    const uint2 *tab2, const unsigned long long *side, uint32_t nSide) {
-  uint32_t bk[K], v[K];
+  uint32_t bk[K], v[K], tg[K];
   uint2 x[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    kqKey(pv[k], s, bk[k], v[k]);
+    kqKey(pv[k], s, bk[k], v[k], tg[k]);
     x[k] = tab2[bk[k]];
   }
   uint32_t matches = 0;
@@ -1537,9 +1585,9 @@ __device__ __forceinline__ uint32_t kqProbeCounted(const uint64_t (&pv)[K], uint
   for (int k = 0; k < K; ++k) {
     uint32_t c = 0, e = bk[k];
     uint2 y = x[k];
-    for (;;) {
-      if (y.x == v[k]) {
-        c = y.y + 1;
+    for (uint32_t dist = 0; dist < KQ_BUCKETS; ++dist) {
+      if (y.x == v[k] && (y.y >> 16) == kqCountedId(dist, tg[k])) {
+        c = (y.y & 0xFFFFu) + 1;
         break;
       }
       if (y.x == KQ_EMPTY) break;
@@ -1556,7 +1604,7 @@ __device__ __forceinline__ uint32_t kqProbeCounted(const uint64_t (&pv)[K], uint
 }
 
 size_t bpKeyQuotientLdsBytes() {
-  return KQ_BUCKETS * 8 + KQ_SIDE * 8 + 16 + KS_CHUNK * sizeof(BPSpan) + 16 * 8 + 16;
+  return KQ_BUCKETS * 8 + KQ_OV * 8 + 16 + KS_CHUNK * sizeof(BPSpan) + 16 * 8 + 16;
 }
 
 template <int T, int K, int MINW>
@@ -1565,25 +1613,26 @@ __global__ __launch_bounds__(T, MINW) void bpKeyQuotientKernel(KsSrc<T, K, true>
                                                                const uint32_t *__restrict__ nSpansPtr,
                                                                uint32_t capacity, uint32_t *__restrict__ queue,
                                                                uint32_t s, unsigned long long *__restrict__ result,
-                                                               unsigned long long *__restrict__ sideOverflow) {
+                                                               unsigned long long *__restrict__ flags) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t *tab = reinterpret_cast<uint32_t *>(smem);  // [bucket][2]
   const uint2 *tab2 = reinterpret_cast<const uint2 *>(smem);
-  unsigned long long *side = reinterpret_cast<unsigned long long *>(tab + 2 * KQ_BUCKETS);
-  uint32_t *sideN = reinterpret_cast<uint32_t *>(side + KQ_SIDE);
-  BPSpan *desc = reinterpret_cast<BPSpan *>(sideN + 4);
+  unsigned long long *ov = reinterpret_cast<unsigned long long *>(tab + 2 * KQ_BUCKETS);
+  uint32_t *ovN = reinterpret_cast<uint32_t *>(ov + KQ_OV);
+  BPSpan *desc = reinterpret_cast<BPSpan *>(ovN + 4);
   unsigned long long *wsum = reinterpret_cast<unsigned long long *>(desc + KS_CHUNK);
   uint32_t *qbase = reinterpret_cast<uint32_t *>(wsum + T / WAVE);
   constexpr uint32_t BATCH = T * K;
   const uint32_t t = threadIdx.x;
   const uint32_t n = min(*nSpansPtr, capacity);
   {
-    uint4 *t4 = reinterpret_cast<uint4 *>(tab);
-    for (uint32_t i = t; i < KQ_BUCKETS / 2; i += T) t4[i] = make_uint4(KQ_EMPTY, KQ_EMPTY, KQ_EMPTY, KQ_EMPTY);
-    if (t == 0) *sideN = 0;
+    uint4 *t4 = reinterpret_cast<uint4 *>(tab);  // main table and overflow table are adjacent
+    for (uint32_t i = t; i < (KQ_BUCKETS * 8 + KQ_OV * 8) / 16; i += T)
+      t4[i] = make_uint4(KQ_EMPTY, KQ_EMPTY, KQ_EMPTY, KQ_EMPTY);
+    if (t == 0) *ovN = 0;
   }
   uint64_t matches = 0;
-  bool overflow = false, chained = false;
+  bool full = false, chained = false;
   uint64_t rv[K], sv[K], nrv[K], nsv[K];
   for (;;) {
     if (t == 0) *qbase = atomicAdd(queue, KS_CHUNK);
@@ -1602,36 +1651,28 @@ __global__ __launch_bounds__(T, MINW) void bpKeyQuotientKernel(KsSrc<T, K, true>
       const uint64_t sb = uniform64(desc[i].sb);
       const uint32_t nr = __builtin_amdgcn_readfirstlane(desc[i].nr);
       const uint32_t ns = __builtin_amdgcn_readfirstlane(desc[i].ns);
-      // ---- build (nr <= BATCH: one batch, from registers)
+      // ---- build (nr <= BATCH: one batch, from registers): slot 0, slot 1, overflow
       uint32_t pos[K];
       {
-        uint32_t bk[K], v[K], old[K];
+        uint32_t bk[K], v[K], tg[K], old[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-          kqKey(rv[k], s, bk[k], v[k]);
+          kqKey(rv[k], s, bk[k], v[k], tg[k]);
           const bool valid = (uint32_t)(k * T) + t < nr;
-          pos[k] = valid ? 2 * bk[k] : KQ_NONE;
-          if (valid && v[k] == KQ_EMPTY) {  // escape: side list
-            const uint32_t at = atomicAdd(sideN, 1u);
-            if (at < KQ_SIDE) side[at] = rv[k];
-            pos[k] = KQ_NONE;
-          }
+          pos[k] = !valid ? KQ_NONE : (v[k] == KQ_EMPTY ? KQ_OV_FLAG : 2 * bk[k]);
         }
 #pragma unroll
-        for (int k = 0; k < K; ++k) old[k] = pos[k] != KQ_NONE ? atomicCAS(&tab[pos[k]], KQ_EMPTY, v[k]) : KQ_EMPTY;
+        for (int k = 0; k < K; ++k) old[k] = pos[k] < KQ_OV_FLAG ? atomicCAS(&tab[pos[k]], KQ_EMPTY, v[k]) : KQ_EMPTY;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-          if (old[k] == KQ_EMPTY) continue;  // placed (or nothing to place)
-          uint32_t p = pos[k] + 1;
-          while (atomicCAS(&tab[p], KQ_EMPTY, v[k]) != KQ_EMPTY)
-            p = (p & 1) ? ((((p >> 1) + 1) & (KQ_BUCKETS - 1)) << 1) : p + 1;
-          chained |= ((p - pos[k]) & (2 * KQ_BUCKETS - 1)) > KQ_LONG_CHAIN;
-          pos[k] = p;
+          if (pos[k] >= KQ_OV_FLAG || old[k] == KQ_EMPTY) continue;  // placed in slot 0 (or not a main-table key)
+          pos[k] = atomicCAS(&tab[pos[k] + 1], KQ_EMPTY, v[k]) == KQ_EMPTY ? pos[k] + 1 : KQ_OV_FLAG;
         }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+          if (pos[k] == KQ_OV_FLAG) pos[k] = kqOvInsert(ov, ovN, rv[k], chained, full);
       }
       __syncthreads();
-      const uint32_t nSide = min(*sideN, KQ_SIDE);
-      overflow |= *sideN > KQ_SIDE;
       // ---- the next span's words stream in while this one probes
       if (i + 1 < cnt) {
         const BPSpan d = desc[i + 1];
@@ -1639,17 +1680,22 @@ __global__ __launch_bounds__(T, MINW) void bpKeyQuotientKernel(KsSrc<T, K, true>
         S.load(d.sb, d.ns, nsv);
       }
       // ---- probe: first batch from registers, later batches loaded inline
-      matches += kqProbeBatch<T, K>(sv, ns, s, tab2, side, nSide);
+      matches += kqProbeBatch<T, K>(sv, ns, s, tab2, ov);
       for (uint32_t b0 = BATCH; b0 < ns; b0 += BATCH) {
         uint64_t xv[K];
         S.load(sb + b0, ns - b0, xv);
-        matches += kqProbeBatch<T, K>(xv, ns - b0, s, tab2, side, nSide);
+        matches += kqProbeBatch<T, K>(xv, ns - b0, s, tab2, ov);
       }
       __syncthreads();  // every probe of this span is done
 #pragma unroll
-      for (int k = 0; k < K; ++k)
-        if (pos[k] != KQ_NONE) tab[pos[k]] = KQ_EMPTY;
-      if (t == 0) *sideN = 0;
+      for (int k = 0; k < K; ++k) {
+        if (pos[k] == KQ_NONE) continue;
+        if (pos[k] & KQ_OV_FLAG)
+          ov[pos[k] & ~KQ_OV_FLAG] = KQ_OV_EMPTY;
+        else
+          tab[pos[k]] = KQ_EMPTY;
+      }
+      if (t == 0) *ovN = 0;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         rv[k] = nrv[k];
@@ -1660,13 +1706,17 @@ __global__ __launch_bounds__(T, MINW) void bpKeyQuotientKernel(KsSrc<T, K, true>
   }
   const unsigned long long total = blockReduceSum<T, unsigned long long>((unsigned long long)matches, wsum);
   if (t == 0 && total) atomicAdd(result, total);
-  if (overflow && t == 0) atomicOr(sideOverflow, 1ull);
-  if (__any(chained) && (t & (WAVE - 1)) == 0) atomicOr(sideOverflow, 2ull);
+  if (__any(full) && (t & (WAVE - 1)) == 0) atomicOr(flags, KQF_COUNTED);
+  if (__any(chained) && (t & (WAVE - 1)) == 0) atomicOr(flags, KQF_CHAINS);
 }
 
 bool bpKeyQuotientFits(const BPArgs &a) {
-  return a.keyOnly && a.split && !a.materialize && !a.wide && a.keyFragBits >= 1 &&
-         a.keyFragBits <= 32 + KQ_BITS && a.rChunk <= 2048;
+  return bpKeyCountedFits(a) && a.keyFragBits <= 32 + KQ_BITS;
+}
+
+bool bpKeyCountedFits(const BPArgs &a) {
+  return a.keyOnly && a.split && !a.materialize && !a.wide && a.keyFragBits >= 1 && a.keyFragBits <= 48 &&
+         a.rChunk <= 2048;
 }
 
 static void launchKeyQuotient(const BPArgs &a, const BPSpan *spans, const uint32_t *nSpans, uint32_t capacity,
@@ -1674,7 +1724,7 @@ static void launchKeyQuotient(const BPArgs &a, const BPSpan *spans, const uint32
   constexpr int T = 512, K = 4;
   HJ_CHECK(bpKeyQuotientFits(a), "buildProbeKeySpans: quotient table needs split key-only words of <= %u bits "
            "(got %u) and rChunk <= 2048 (got %u)", 32 + KQ_BITS, a.keyFragBits, a.rChunk);
-  HJ_CHECK(a.sideOverflow, "buildProbeKeySpans: quotient table needs a side-overflow flag");
+  HJ_CHECK(a.sideOverflow, "buildProbeKeySpans: quotient table needs a flag word");
   const uint32_t s = a.keyFragBits > 32 ? a.keyFragBits - 32 : 0;
   const size_t lds = bpKeyQuotientLdsBytes();
   const uint32_t perCu = (uint32_t)std::max<size_t>(1, std::min<size_t>(4, (160 * 1024) / lds));
@@ -1688,23 +1738,24 @@ static void launchKeyQuotient(const BPArgs &a, const BPSpan *spans, const uint32
 // ------------------------------------- key-only: partitions with repeated keys
 // Partitions with more than rChunk inner tuples (with unique keys a few in a
 // thousand, just above the mean; with repeated keys the hot ones) skip the
-// span work queue, whose one-slot-per-tuple quotient table chains the copies
-// of a key: O(copies^2) CAS steps per span and a chain walk per probe.  Their
-// spans (bpPlanCounts -> heavySpans, same rChunk x sChunk tiling) are counted
-// here on a *counted* table over the same 32 KiB: entry e = (stored value,
-// count - 1) in the two slots of bucket e, one entry per distinct key with
-// linear probing, so copies only add to a count.  A span's <= 2048 inner
-// tuples fill at most half of the 4096 entries.  Escape keys use the side list
-// as in the span kernel (its overflow re-runs on v2).  A hot partition's spans
-// spread over workgroups like any others.
+// span work queue, whose one-slot-per-tuple quotient table holds every copy
+// of a key.  Their spans (bpPlanCounts -> heavySpans, same rChunk x sChunk
+// tiling) are counted here on a *counted* table over the same 32 KiB (see
+// kqProbeCounted): one entry per distinct key, so copies only add to a count.
+// A span's <= 2048 inner tuples fill at most half of the 4096 entries.  This
+// table also carries 45-48-bit fragments (the tag next to the count), so
+// plans whose fragments the quotient table cannot hold count every partition
+// here.  Escape keys use a 64-entry side list; more set KQF_V2 (re-run on
+// v2).  A hot partition's spans spread over workgroups like any others.
 template <int T, int K>
 __global__ __launch_bounds__(T) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R, KsSrc<T, K, true> S,
                                                               const BPSpan *__restrict__ spans,
                                                               const uint32_t *__restrict__ nSpansPtr, uint32_t capacity,
                                                               uint32_t s, unsigned long long *__restrict__ result,
-                                                              unsigned long long *__restrict__ sideOverflow) {
+                                                              unsigned long long *__restrict__ flags) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint32_t *tab = reinterpret_cast<uint32_t *>(smem);  // [entry][value, count - 1]
+  uint32_t *tab = reinterpret_cast<uint32_t *>(smem);  // [entry][value, id << 16 | count - 1]
+  unsigned long long *tab64 = reinterpret_cast<unsigned long long *>(smem);
   const uint2 *tab2 = reinterpret_cast<const uint2 *>(smem);
   unsigned long long *side = reinterpret_cast<unsigned long long *>(tab + 2 * KQ_BUCKETS);
   uint32_t *ctl = reinterpret_cast<uint32_t *>(side + KQ_SIDE);  // [0] side list length
@@ -1729,17 +1780,20 @@ __global__ __launch_bounds__(T) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       if ((uint32_t)(k * T) + t >= sp.nr) continue;
-      uint32_t e, v;
-      kqKey(rv[k], s, e, v);
+      uint32_t e, v, tg;
+      kqKey(rv[k], s, e, v, tg);
       if (v == KQ_EMPTY) {  // escape: side list
         const uint32_t at = atomicAdd(&ctl[0], 1u);
         if (at < KQ_SIDE) side[at] = rv[k];
         continue;
       }
-      for (;;) {
-        const uint32_t o = atomicCAS(&tab[2 * e], KQ_EMPTY, v);
-        if (o == KQ_EMPTY || o == v) {
-          atomicAdd(&tab[2 * e + 1], 1u);  // KQ_EMPTY + 1 = 0: the slot holds count - 1
+      // <= 2048 distinct keys in 4096 entries: an empty entry is always reached
+      for (uint32_t dist = 0;; ++dist) {
+        const uint32_t id = kqCountedId(dist, tg);
+        const unsigned long long o = atomicCAS(&tab64[e], ~0ull, ((unsigned long long)(id << 16) << 32) | v);
+        if (o == ~0ull) break;  // claimed with count - 1 = 0
+        if ((uint32_t)o == v && (uint32_t)(o >> 48) == id) {
+          atomicAdd(&tab[2 * e + 1], 1u);
           break;
         }
         e = (e + 1) & (KQ_BUCKETS - 1);
@@ -1761,13 +1815,13 @@ __global__ __launch_bounds__(T) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R
   }
   const unsigned long long total = blockReduceSum<T, unsigned long long>((unsigned long long)matches, wsum);
   if (t == 0 && total) atomicAdd(result, total);
-  if (overflow && t == 0) atomicOr(sideOverflow, 1ull);
+  if (overflow && t == 0) atomicOr(flags, KQF_V2);
 }
 
 void bpKeyCountedSpans(const BPArgs &a, hipStream_t st) {
   constexpr int T = 512, K = 4;
-  HJ_CHECK(bpKeyQuotientFits(a) && a.rChunk <= (uint32_t)(T * K) && a.heavySpans && a.heavyCount && a.sideOverflow,
-           "bpKeyCountedSpans: needs the quotient-table layout and the heavy span list");
+  HJ_CHECK(bpKeyCountedFits(a) && a.rChunk <= (uint32_t)(T * K) && a.heavySpans && a.heavyCount && a.sideOverflow,
+           "bpKeyCountedSpans: needs split key-only words of <= 48 fragment bits and the heavy span list");
   const uint32_t s = a.keyFragBits > 32 ? a.keyFragBits - 32 : 0;
   const size_t lds = KQ_BUCKETS * 8 + KQ_SIDE * 8 + 16 + 16 * 8 + 16;
   const dim3 grid(std::min<uint32_t>(std::max<uint32_t>(a.heavyCapacity, 1), 256 * 4));

@@ -340,11 +340,14 @@ struct BPArgs {
   uint64_t offA = 0, offB = 0;        // rid of row 0 of each column
   ulonglong2 *outRows = nullptr;
   // Key-only words: bits of the fragment above both radix digits (0 =
-  // unknown); the quotient-table kernel (keyCount 8) needs <= 44.
+  // unknown); the quotient-table kernel (keyCount 8) needs <= 44, the
+  // counted-table kernel <= 48.
   uint32_t keyFragBits = 0;
-  // Quotient-table kernel: bit 0 set when a span had more escape keys than
-  // its side list holds (the count is then void: re-run on keyCount 7); bit 1
-  // when a key's copies chained (count exact; keyCount 9 from then on).
+  // Flags of the quotient / counted kernels (build_probe.hip, KQF_*): bit 0
+  // a counted span had more escape keys than its side list holds (count void:
+  // re-run on keyCount 7); bit 1 a key's copies chained (count exact;
+  // keyCount 9 from then on); bit 3 a quotient span filled its overflow table
+  // (count void: re-run on counted tables).
   unsigned long long *sideOverflow = nullptr;
   // Optional (key-only spans with the quotient table): bpPlanCounts writes
   // the spans of partitions with more than rChunk inner tuples here (at most
@@ -392,6 +395,9 @@ void buildProbeKeySpans(const BPArgs &a, const BPSpan *spans, const uint32_t *nS
 // keyCount 8 (quotient table, build_probe.hip) applies: split key-only words
 // of <= 44 fragment bits, rChunk <= 2048.
 bool bpKeyQuotientFits(const BPArgs &a);
+// Counted tables (bpKeyCountedSpans) apply: split key-only words of <= 48
+// fragment bits, rChunk <= 2048.
+bool bpKeyCountedFits(const BPArgs &a);
 // The spans bpPlanCounts wrote to a.heavySpans (partitions of repeated inner
 // keys): counted tables (build_probe.hip, bpKeyCountedSpansKernel); adds to
 // a.result.

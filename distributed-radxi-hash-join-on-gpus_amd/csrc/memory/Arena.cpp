@@ -64,12 +64,12 @@ void Arena::rawFree(Location loc, void *p) {
 Arena::~Arena() { releaseAll(); }
 
 void Arena::releaseAll() {
+  if (!fallbacks_.empty() || !chunks_.empty()) ++generation_;
   for (auto &f : fallbacks_) rawFree(loc_, f.first);
   fallbacks_.clear();
   fallbackBytes_ = 0;
   for (auto &c : chunks_) rawFree(loc_, c.base);
   chunks_.clear();
-  ++generation_;
 }
 
 uint64_t Arena::capacity() const {
@@ -97,8 +97,7 @@ void Arena::addChunk(uint64_t bytes, bool touch, void *stream) {
       std::memset(p, 0, bytes);
     }
   }
-  chunks_.push_back(Chunk{p, bytes, 0});
-  ++generation_;
+  chunks_.push_back(Chunk{p, bytes, 0});  // growth: existing allocations (and peers' mappings) stay valid
 }
 
 void Arena::reserve(uint64_t bytes) {
@@ -109,10 +108,26 @@ void Arena::reserve(uint64_t bytes) {
 uint64_t Arena::ensure(uint64_t bytes, bool touch, void *stream) {
   const uint64_t have = capacity();
   if (have >= bytes) return 0;
-  // One chunk of the whole request: first fit over the older chunks could
-  // otherwise leave a big buffer without a chunk that holds it.
-  addChunk(bytes, touch, stream);
+  if (used() == 0 && fallbacks_.empty()) {
+    // Between joins nothing lives in the chunks: re-lay them out as ONE chunk
+    // of the request (first fit over several smaller chunks could leave a big
+    // buffer without a chunk that holds it), so the total is the request,
+    // not the old chunks plus the request.
+    releaseAll();
+    addChunk(bytes, touch, stream);
+    return capacity() > have ? capacity() - have : 0;
+  }
+  addChunk(bytes - have, touch, stream);  // mid-join: the shortfall (get() falls back for what misfits)
   return capacity() - have;
+}
+
+uint64_t Arena::trim(uint64_t keep) {
+  const uint64_t have = capacity() + fallbackBytes_;
+  if (have <= keep && fallbacks_.empty()) return 0;
+  releaseAll();
+  peakFallback_ = 0;
+  if (keep) addChunk(keep, false);
+  return have > capacity() ? have - capacity() : 0;
 }
 
 void *Arena::get(uint64_t bytes) {
@@ -137,13 +152,13 @@ void *Arena::get(uint64_t bytes) {
   peakFallback_ = std::max(peakFallback_, fallbackBytes_);
   const uint64_t u = used() + fallbackBytes_;
   if (u > peak_) peak_ = u;
-  ++generation_;
-  return p;
+  return p;  // a new allocation frees nothing: generation() unchanged
 }
 
 void Arena::reset() {
   if (!fallbacks_.empty() || peakFallback_) {
     for (auto &f : fallbacks_) rawFree(loc_, f.first);
+    if (!fallbacks_.empty()) ++generation_;
     fallbacks_.clear();
     fallbackBytes_ = 0;
     // One new chunk holds every allocation that overflowed (+1/8 slack); the

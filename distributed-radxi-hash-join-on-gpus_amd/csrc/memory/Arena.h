@@ -14,9 +14,14 @@
 // next join with the same allocation sequence fits (first fit over the chunks
 // in order) and steady-state joins never allocate.  ensure() grows ahead of
 // time (HashJoin reserves its plan's estimate at construction) and can touch
-// the new pages once, so a first join does not pay the first-touch cost.
-// Every change of the set of live allocations bumps generation(): peers that
-// mapped this arena's memory (one-sided windows) re-open their mappings.
+// the new pages once, so a first join does not pay the first-touch cost;
+// between joins it re-lays the chunks out as one chunk of the request (the
+// total never ratchets to old chunks + request), and trim() gives memory back.
+// generation() counts FREES only (releaseAll, reset() dropping fallbacks,
+// freeFallback, trim): an address a peer mapped (one-sided windows) stays
+// valid until then, and frees happen only between joins, so a peer's
+// mappings of one join all carry one generation and an import never has to
+// close a mapping the same join still uses (core/ExecContext::ipcImport).
 #pragma once
 
 #include <cstdint>
@@ -39,12 +44,17 @@ class Arena {
   Arena &operator=(const Arena &) = delete;
 
   void reserve(uint64_t bytes);       // one chunk of `bytes` (frees everything first)
-  // Grow (never shrink, never move) so that the chunks hold >= bytes in all;
+  // Grow so that the chunks hold >= bytes in all: with nothing handed out,
+  // by re-laying them out as one chunk of `bytes`; otherwise by the shortfall;
   // touch = write the new chunk once (device: a memset ordered on `stream`,
   // then waited for -- the engine's streams are non-blocking, so a null-stream
   // memset could land after a join's first writes) so its pages are mapped
   // before the first join uses them.  Returns the bytes added.
   uint64_t ensure(uint64_t bytes, bool touch = false, void *stream = nullptr);
+  // Between joins: drop everything handed out (previous joins' outputs
+  // included) and shrink to one chunk of `keep` bytes (0 = none) if the
+  // arena holds more.  Returns the bytes freed.
+  uint64_t trim(uint64_t keep = 0);
   void *get(uint64_t bytes);          // bump-allocate (fallback allocation when exhausted)
   template <typename T>
   T *getArray(uint64_t count) { return reinterpret_cast<T *>(get(count * sizeof(T))); }

@@ -175,7 +175,12 @@ void HashJoin::makeJoinPlan() {
     // only means the first join falls back to hipMalloc, as without it.
     size_t freeB = 0, totalB = 0;
     HIP_CHECK(hipMemGetInfo(&freeB, &totalB));
-    const uint64_t want = std::min<uint64_t>(workspaceEstimate(), (uint64_t)(freeB * 0.85));
+    uint64_t want = std::min<uint64_t>(workspaceEstimate(), (uint64_t)(freeB * 0.85));
+    if (config.workspaceBudget) want = std::min<uint64_t>(want, config.workspaceBudget);
+    // Rewound first: a previous join's buffers are dead once a new join is
+    // planned on this context, so ensure() re-lays the chunks out as one
+    // chunk of `want` instead of adding `want` on top of them.
+    ctx->workspace().reset();
     reserved = ctx->workspace().ensure(want, true, ctx->stream());
     JOIN_DEBUG("HashJoin", "workspace: estimate %.2f GB, added %.2f GB", want / 1e9, reserved / 1e9);
   }

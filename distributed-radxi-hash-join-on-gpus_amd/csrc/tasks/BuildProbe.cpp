@@ -61,7 +61,8 @@ void BuildProbe::configure() {
   args.wide = plan.wide;
   args.keyOnly = plan.keyOnly;
   args.materialize = plan.materialize;
-  args.keyCount = quotientFallback && plan.variants.keyCount >= 8 ? 7 : plan.variants.keyCount;
+  args.keyCount = plan.variants.keyCount;
+  if (plan.variants.keyCount >= 8) args.keyCount = quotientFallback ? 7 : (countedAll ? 9 : args.keyCount);
   if (plan.keyOnly) {
     const uint32_t passBits = plan.networkBits + wi->getLocalBits();
     args.keyFragBits = plan.keyBits > passBits ? plan.keyBits - passBits : 1;
@@ -147,14 +148,17 @@ void BuildProbe::execute() {
                                           (uint64_t)capacity * sizeof(kernels::BPItem) + kernels::bpLdsBytes(args)),
                                  "bytes");
   // Key-only counting on the quotient table: partitions of repeated keys go
-  // to the counted-table kernel instead of the span work queue.
+  // to the counted-table kernel instead of the span work queue.  Fragments
+  // of 45-48 bits (inputs below ~500M tuples) do not fit the quotient table:
+  // every partition is counted there.
   const bool keySpans = args.keyOnly && (args.keyCount >= 6 || args.split);  // the item kernels read unsplit words only
-  const bool counted = keySpans && args.keyCount >= 8 && kernels::bpKeyQuotientFits(args);
+  const bool counted = keySpans && args.keyCount >= 8 && kernels::bpKeyCountedFits(args);
+  const bool quotient = counted && kernels::bpKeyQuotientFits(args);
   if (counted) {
     args.heavySpans = ws.getArray<kernels::BPSpan>(capacity);
     args.heavyCapacity = capacity;
     // keyCount 9 (repeated keys seen): every partition on counted tables.
-    args.heavyMin = args.keyCount == 9 ? 0 : args.rChunk;
+    args.heavyMin = (args.keyCount == 9 || !quotient) ? 0 : args.rChunk;
     args.heavyCount = nItems + 1;  // high half of counters[2]: read back with the rest
   }
   kernels::bpPlanCounts(args, counts, ctx->stream());
@@ -164,9 +168,10 @@ void BuildProbe::execute() {
     auto *spans = ws.getArray<kernels::BPSpan>(capacity);
     uint32_t *queue = ws.getArray<uint32_t>(1);
     kernels::bpEmitSpans(args, counts, offsets, spans, capacity, ctx->stream());
-    args.sideOverflow = counters + 3;  // quotient table: escape side list overflowed
+    args.sideOverflow = counters + 3;  // quotient / counted table flags (kernels.h, BPArgs::sideOverflow)
     tl.beginSplit("BPKERNEL", "BPBUILD", wb, "BPPROBE", wp, ctx->stream());
-    kernels::buildProbeKeySpans(args, spans, nItems, capacity, queue, ctx->stream());
+    if (!counted || args.heavyMin != 0)  // otherwise every span is on the heavy list
+      kernels::buildProbeKeySpans(args, spans, nItems, capacity, queue, ctx->stream());
     if (counted) kernels::bpKeyCountedSpans(args, ctx->stream());
     hipEvent_t done = tl.mark(ctx->stream());
     tl.endAt("BPKERNEL", done);
@@ -231,8 +236,11 @@ bool BuildProbe::collect() {
   workItems = items + heavy;
   bool again = false;
   if (h[3] & 2) duplicateChains = true;  // exact count; later joins use counted tables throughout
-  if (args.sideOverflow && (h[3] & 1)) {  // too many escape keys in one span: count on the v2 table
+  if (args.sideOverflow && (h[3] & 1)) {  // too many escape keys in one counted span: count on the v2 table
     quotientFallback = true;
+    again = true;
+  } else if (args.sideOverflow && (h[3] & 8)) {  // a quotient span's overflow table filled: counted tables
+    countedAll = duplicateChains = true;
     again = true;
   }
   if (items > capacity || heavy > capacity) {

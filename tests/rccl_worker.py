@@ -129,6 +129,28 @@ def main():
     assert caps[1] > caps[0], ("workspace did not grow", caps)
     if info.rank == 0:
         print(f"one-sided across a workspace growth: exact, workspace {caps}", flush=True)
+    # One-sided windows allocated by fallback INSIDE the join: workspace
+    # trimmed to nothing and no reservation, so every window is a fallback
+    # hipMalloc and the peers import a rank's second window while its first
+    # one is in use.  Growth keeps the arena generation, so that first mapping
+    # stays open (it used to be closed at the second import).
+    ctx.trim_workspace(0)
+    comm.barrier()
+    cfg2 = C.JoinConfig()
+    cfg2.bitmap_join = False
+    cfg2.exchange = C.ExchangeMode.ONE_SIDED
+    cfg2.reserve_workspace = False
+    G = 4 * G_S
+    S = C.Relation(C.Relation.local_size_for(G, info.rank, info.world), G, "device", info.local_rank)
+    S.generate(spec, C.Relation.local_offset_for(G, info.rank, info.world))
+    j = C.HashJoin(R, S, ctx, cfg2)
+    assert j.plan.one_sided and ctx.workspace_capacity() == 0, (j.plan, ctx.workspace_capacity())
+    for _ in range(2):
+        res = j.run()
+        assert res["global_matches"] == C.Relation.expected_matches(inner, G_R, spec, G), ("one-sided-fallback", res)
+    del j, S
+    if info.rank == 0:
+        print("one-sided with in-join fallback windows: exact", flush=True)
     # TPC-H-like join + late materialization of 32-byte payload rows across
     # ranks (BASELINE config 5 at SF 0.5): pairs from the build/probe, rows
     # fetched from their owner ranks by the request/response all-to-allv.

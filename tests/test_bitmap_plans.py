@@ -300,7 +300,7 @@ def test_sparse64_generator(C):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", ["8s", "6", "6s", "7", "7s", "1", "0", "2", "3", "4", "5"])
+@pytest.mark.parametrize("variant", ["8s", "9s", "8w", "6", "6s", "7", "7s", "1", "0", "2", "3", "4", "5"])
 def test_key_only_count_variants(C, variant):
     """Every key-only count kernel variant against a torch reference, with heavily repeated inner keys (Zipf over sparse
     63-bit keys: long overflow chains through the next buckets)."""
@@ -318,11 +318,13 @@ def test_key_only_count_variants(C, variant):
         cfg = C.JoinConfig()
         cfg.key_count = int(variant[0])
         # 6 / 7: span kernel (AoS / SoA buckets); 8: quotient table (44-bit
-        # fragments: 63-bit keys above 10 + 9 radix bits); "s": over the split
-        # (u32 + u16) local output; the item kernels (0-5) read unsplit words only
-        split = variant.endswith("s")
+        # fragments: 63-bit keys above 10 + 9 radix bits); 9: counted tables
+        # throughout; "s": over the split (u32 + u16) local output; "8w": 48-bit
+        # fragments (8 + 7 radix bits) on counted tables; the item kernels (0-5)
+        # read unsplit words only
+        split = variant.endswith("s") or variant == "8w"
         cfg.split_local = split
-        if variant == "8s":
+        if variant in ("8s", "9s"):
             cfg.network_bits, cfg.local_bits = 10, 9
         elif split:  # 63-bit keys: the fragment above 8 + 7 radix bits fits the 48-bit split
             cfg.network_bits, cfg.local_bits = 8, 7
@@ -407,13 +409,18 @@ def quotient_escape_fragments(n, first_bucket=0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n_escape,dup", [(20, 1), (40, 3), (100, 1)])
-def test_key_quotient_escapes(C, n_escape, dup):
-    """Quotient-table build/probe with keys whose stored value is the table's
-    empty marker, all in one final partition: up to 64 per span are counted
-    through the side list; more (100 distinct, or 40 keys x 3 copies) set the
-    overflow flag and the build/probe re-runs on the v2 table.  Counts equal a
-    torch oracle either way."""
+@pytest.mark.parametrize("n_escape,dup,key_count,reruns",
+                         [(20, 1, 8, 0), (40, 3, 8, 0), (100, 1, 8, 0), (400, 1, 8, 2), (20, 1, 9, 0), (40, 3, 9, 1)])
+def test_key_quotient_escapes(C, n_escape, dup, key_count, reruns):
+    """Quotient / counted build/probe with keys whose stored value is the
+    table's empty marker, all in one final partition.  The quotient table
+    (key_count 8) keeps them in its overflow table of full fragments (up to
+    384 per span); 400 fill it: the count is void, the build/probe re-runs on
+    counted tables, whose 64-entry escape list overflows too, and re-runs on
+    the v2 table (2 re-runs).  Counted tables (key_count 9) hold 64 escapes
+    per span; 40 keys x 3 copies re-run on v2.  Counts equal a torch oracle
+    every time; later joins of the same HashJoin start where the first ended
+    (no re-run)."""
     import torch
     from helpers import ref_join_count
     g = torch.Generator().manual_seed(n_escape * 7 + dup)
@@ -433,15 +440,75 @@ def test_key_quotient_escapes(C, n_escape, dup):
     cfg = C.JoinConfig()
     cfg.network_bits, cfg.local_bits = 10, 9
     cfg.key_hashing = C.KeyHashing.OFF
+    cfg.key_count = key_count
     j = C.HashJoin(C.Relation.from_tensor(R, R.shape[0]), C.Relation.from_tensor(S, S.shape[0]), ctx, cfg)
     assert j.plan.key_only and j.plan.split_local and j.plan.key_bits == 63, j.plan
-    over = n_escape * dup > 64
     for i in range(2):
         res = j.run()
         assert res["global_matches"] == exp, (n_escape, dup, res["global_matches"], exp)
-        # an overflowing join re-runs its build/probe once; later joins of the
-        # same HashJoin start on the v2 table (no re-run)
-        assert res["reruns"] == (1 if over and i == 0 else 0), (i, res["reruns"])
+        assert res["reruns"] == (reruns if i == 0 else 0), (i, res["reruns"])
+
+
+KQ_M = 0xFFFFFFFF
+
+
+def kq_salt(b):
+    return ((b + 1) * 0x85EBCA77) & KQ_M
+
+
+def kq_fragment(b, e, s, tag=0):
+    """The fragment (f = 32 + s bits) whose quotient-table key is (bucket b,
+    stored value e ^ salt(b), tag): build_probe.hip kqKey inverted."""
+    lo = ((b ^ (((e * 0x9E3779B1) & KQ_M) >> 20)) & 0xFFF) | (tag << 12)
+    return (e << s) | lo
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key_count,frag_bits", [(8, 44), (9, 44), (8, 48)])
+def test_key_tables_no_foreign_matches(C, key_count, frag_bits):
+    """Quotient and counted tables store a key as (bucket, 32-bit value[, tag])
+    that names it only in its home bucket.  Three inner keys share home bucket
+    h (the third is displaced); every outer probe key B(X, d) has home h + d
+    and the SAME stored value and tag as inner key X: a table that compared a
+    displaced entry without its home would count B as X.  Exact counts
+    against a torch oracle on the quotient table (44-bit fragments), counted
+    tables (key_count 9) and the 48-bit counted path (8 + 7 radix bits)."""
+    import torch
+    from helpers import ref_join_count
+    s = frag_bits - 32
+    bits = 63 - frag_bits
+    net = 10 if bits == 19 else 8
+    part = 0x2A5F3 & ((1 << bits) - 1)
+    g = torch.Generator().manual_seed(frag_bits * 10 + key_count)
+    h = 1000
+    tags = [0, 0, 0] if s <= 12 else [3, 3, 11]
+    es = [0x80000000 | int(x) for x in torch.randint(0, 1 << 31, (3,), generator=g)]
+    inner = [kq_fragment(h, e, s, t) for e, t in zip(es, tags)]
+    vs = [e ^ kq_salt(h) for e in es]
+    probes = []
+    for v, t in zip(vs, tags):
+        for d in (1, 2, 3, 4):
+            probes.append(kq_fragment(h + d, v ^ kq_salt(h + d), s, t))
+    assert not set(probes) & set(inner)
+    key = lambda f: (torch.tensor(f, dtype=torch.int64) << bits) | part
+    other = torch.randint(1 << 40, (1 << 62) - 1, (200_000,), generator=g, dtype=torch.int64).unique()
+    rk = torch.cat([key(inner), other])
+    sk = torch.cat([key(probes).repeat(7), key(inner).repeat(3), other[:50_000]])
+    exp = ref_join_count(rk, sk)
+    assert exp == 9 + 50_000
+    rows = lambda k: torch.stack([k, torch.arange(k.numel())], 1).contiguous().cuda()
+    R, S = rows(rk), rows(sk)
+    ctx = C.ExecContext("device", 0, C.LocalCommunicator())
+    cfg = C.JoinConfig()
+    cfg.network_bits, cfg.local_bits = net, bits - net
+    cfg.key_hashing = C.KeyHashing.OFF
+    cfg.key_count = key_count
+    j = C.HashJoin(C.Relation.from_tensor(R, R.shape[0]), C.Relation.from_tensor(S, S.shape[0]), ctx, cfg)
+    assert j.plan.key_only and j.plan.split_local and j.plan.key_bits == 63, j.plan
+    for _ in range(2):
+        res = j.run()
+        assert res["global_matches"] == exp, (key_count, frag_bits, res["global_matches"], exp)
+        assert res["reruns"] == 0, res
 
 
 @pytest.mark.parametrize("dev", devices())

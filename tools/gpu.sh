@@ -1,0 +1,52 @@
+#!/bin/bash
+# One parametrized GPU-box runner (replaces the round-3 single-experiment
+# scripts).  Usage, through gpurun:
+#   bash tools/gpu.sh TAG STEP [STEP ...]
+# Steps run in order, each under its own timeout; the first failure ends the
+# run (no GPU step after a failed one).  Output goes to gpurun_out/TAG/.
+#   gputests            full `pytest -m gpu`
+#   tests=EXPR          `pytest -m gpu -k EXPR`
+#   smoke               __graft_entry__.smoke()
+#   bench=ARGS          python bench.py ARGS        (ARGS: comma-separated, e.g. --general,only,--steps,10)
+#   skew=ARGS           python tools/bench_skew.py ARGS
+#   py=SCRIPT,ARGS      python SCRIPT ARGS
+#   stats=ARGS          rocprofv3 --kernel-trace --stats of bench.py ARGS
+#   pmc=CTRS/ARGS       rocprofv3 --pmc CTRS (comma-separated) of bench.py ARGS
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R" || exit 1
+TAG=$1
+shift
+OUT=$R/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+n=0
+for step in "$@"; do
+  n=$((n + 1))
+  kind=${step%%=*}
+  arg=${step#*=}
+  [ "$arg" = "$step" ] && arg=""
+  args=${arg//,/ }
+  log=$OUT/$n.$kind.log
+  echo "[$n] $step"
+  case $kind in
+    gputests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$log" 2>&1 ;;
+    tests) timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$arg" > "$log" 2>&1 ;;
+    smoke) timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > "$log" 2>&1 ;;
+    bench) timeout -k 10 600 python -u bench.py $args > "$log" 2>&1 ;;
+    skew) timeout -k 10 900 python -u tools/bench_skew.py $args > "$log" 2>&1 ;;
+    py) timeout -k 10 900 python -u $args > "$log" 2>&1 ;;
+    stats) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/stats$n" -o run --output-format csv \
+              -- python "$R/bench.py" $args) > "$log" 2>&1 ;;
+    pmc) ctrs=${arg%%/*}; bargs=${arg#*/}; (cd /tmp && timeout -s KILL 300 rocprofv3 --kernel-trace --pmc ${ctrs//,/ } \
+              -d "$OUT/pmc$n" -o run --output-format csv -- python "$R/bench.py" ${bargs//,/ }) > "$log" 2>&1 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+  rc=$?
+  tail -3 "$log"
+  if [ $rc -ne 0 ]; then
+    echo "[$n] $step failed rc=$rc"
+    tail -40 "$log"
+    exit $rc
+  fi
+done
+echo done
