@@ -668,7 +668,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property("reduce_chunks", [](const core::JoinConfig &c) { return c.variants.reduceChunks; },
                     [](core::JoinConfig &c, uint32_t v) { c.variants.reduceChunks = v; })
       .def_property("key_count", [](const core::JoinConfig &c) { return c.variants.keyCount; },
-                    [](core::JoinConfig &c, uint32_t v) { c.variants.keyCount = v; })
+                    [](core::JoinConfig &c, uint32_t v) {
+                      HJ_CHECK(v >= 7 && v <= 9, "key_count: 7 (v2 buckets), 8 (quotient) or 9 (counted), got %u", v);
+                      c.variants.keyCount = v;
+                    })
       .def_property("rows_lds", [](const core::JoinConfig &c) { return c.variants.rowsLds; },
                     [](core::JoinConfig &c, uint32_t v) { c.variants.rowsLds = v; })
       .def_property("mat_variant", [](const core::JoinConfig &c) { return c.variants.matVariant; },
@@ -684,6 +687,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("bitmap_bits", &core::JoinPlan::bitmapBits)
       .def_readonly("bitmap_replicated", &core::JoinPlan::bitmapReplicated)
       .def_readonly("key_only", &core::JoinPlan::keyOnly)
+      .def_readonly("inner_repeats", &core::JoinPlan::innerRepeats)
       .def_readonly("one_sided", &core::JoinPlan::oneSided)
       .def_readonly("replicated_link_bytes", &core::JoinPlan::replicatedLinkBytes)
       .def_readonly("shuffle_link_bytes", &core::JoinPlan::shuffleLinkBytes)
@@ -962,6 +966,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("plan", &operators::HashJoin::getPlan)
       .def("workspace_estimate", &operators::HashJoin::workspaceEstimate)
       .def_property_readonly("reserved_bytes", &operators::HashJoin::reservedBytes)
+      .def_property_readonly("plan_ms", &operators::HashJoin::planMilliseconds)
+      .def_property_readonly("reserve_ms", &operators::HashJoin::reserveMilliseconds)
       .def(
           "materialize_payloads",
           [](operators::HashJoin &j, std::shared_ptr<core::ExecContext> ctx, at::Tensor innerRows, uint64_t innerOffset,
@@ -1193,6 +1199,26 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     HJ_CHECK(dst.numel() * dst.element_size() >= src.numel() * src.element_size(), "copy_into: dst too small");
     kernels::copyKernel(ptr<const ulonglong2>(src), ptr<ulonglong2>(dst), src.numel() * src.element_size() / 16, nullptr);
   });
+  ops.def(
+      "stream_mix",
+      [](uint64_t n, int ra, int rb, int wa, int wb, const at::Tensor &a, const at::Tensor &b, const at::Tensor &oa,
+         const at::Tensor &ob, const at::Tensor &sink) {
+        // One in-order pass over n elements with the given byte mix (stream-mix ceiling of a pass)
+        setDevice(a);
+        auto need = [&](const at::Tensor &t, int bytes, const char *what) {
+          if (bytes) HJ_CHECK(t.is_cuda() && (uint64_t)(t.numel() * t.element_size()) >= n * bytes,
+                              "stream_mix: %s holds fewer than n x %d bytes", what, bytes);
+        };
+        need(a, ra, "a");
+        need(b, rb, "b");
+        need(oa, wa, "oa");
+        need(ob, wb, "ob");
+        HJ_CHECK(n % 8 == 0, "stream_mix: n must be a multiple of 8");
+        kernels::streamMix(ra, rb, wa, wb, a.data_ptr(), b.data_ptr(), oa.data_ptr(), ob.data_ptr(), n,
+                           reinterpret_cast<unsigned long long *>(sink.data_ptr()), nullptr);
+      },
+      py::arg("n"), py::arg("ra"), py::arg("rb"), py::arg("wa"), py::arg("wb"), py::arg("a"), py::arg("b"),
+      py::arg("oa"), py::arg("ob"), py::arg("sink"));
   ops.def("read_sink", [](const at::Tensor &src, const at::Tensor &sink) {
     setDevice(src);
     kernels::readKernel(ptr<const ulonglong2>(src), src.numel() * src.element_size() / 16,

@@ -19,13 +19,14 @@ std::string JoinConfig::describe() const {
 std::string JoinPlan::describe() const {
   return utils::format("JoinPlan(nodes=%u networkBits=%u localBits=%u twoLevel=%d keyShift=%u fragShift=%u "
                        "rChunk=%u sChunk=%u chunks=%u wide=%d materialize=%d keyMix=%d sampled=%d assignment=%s wire=%u/%u "
-                       "split=%d splitHist=%d pipeOuter=%d bitmap=%d/%u%s%s%s%s)",
+                       "split=%d splitHist=%d pipeOuter=%d bitmap=%d/%u%s%s%s%s%s)",
                        numberOfNodes, networkBits, localBits, (int)twoLevel, keyShift, fragShift, rChunk, sChunk,
                        chunks, (int)wide, (int)materialize, (int)keyMix, (int)sampledNetwork,
                        assignment == AssignmentPolicy::LPT ? "lpt" : "round_robin", wireBits[0], wireBits[1],
                        (int)splitLocal, (int)splitHistogram, (int)pipelineOuter, (int)bitmapJoin, bitmapBits,
                        bitmapReplicated ? " replicated" : "", keyOnly ? " keyOnly" : "",
-                       oneSided ? " oneSided" : "", fragments && !bitmapJoin ? " fragments" : "");
+                       oneSided ? " oneSided" : "", fragments && !bitmapJoin ? " fragments" : "",
+                       innerRepeats ? " innerRepeats" : "");
 }
 
 JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t globalInner, uint64_t globalOuter,

@@ -145,6 +145,7 @@ struct JoinPlan {
   // rid: a count never reads one), keyShift = 0.  The wide format's 16 bytes
   // are kept only for materializing joins and when TupleFormat::Wide is asked.
   bool keyOnly = false;
+  bool innerRepeats = false;    // inner keys repeat (generator metadata or a plan-time sample): no bitmap plan
   bool sampledNetwork = false;  // single-rank network pass sized from a sampled histogram
   bool splitHistogram = false;  // N > 1: assignment from an outer estimate, outer exact histogram off the head
   bool pipelineOuter = false;   // N > 1 counting: outer local pass + build/probe per exchange chunk

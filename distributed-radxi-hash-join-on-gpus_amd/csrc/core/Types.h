@@ -47,10 +47,10 @@ struct KernelVariants {
   uint32_t bmThreads = 0;     // bitmap kernels' workgroup size: 0 = auto (256 for <= 32 KiB bitmaps, else 1024)
   int32_t bmFlat = -1;        // bitmap slice walk: -1 = auto, 0 = per claim slice, 1 = one flat walk per partition
   uint32_t reduceChunks = 0;  // replicated bitmap plan: all-reduce ranges (0 = auto: one per 32 MiB, <= 4)
-  uint32_t keyCount = 8;      // key-only count kernel: 8 = span work queue with the quotient table (bpKeyQuotientKernel,
-                              // falls back to 7 where it does not fit), 9 = every partition on counted tables
-                              // (bpKeyCountedSpansKernel; set after repeated keys), 7 / 6 = span work queue (bpKeySpanKernel) with
-                              // SoA / AoS buckets, 0-5 = item kernels
+  uint32_t keyCount = 8;      // key-only count kernel: 8 = span work queue with the quotient table (bpKeyQuotientKernel;
+                              // counted tables for heavy partitions and 45-48-bit fragments, v2 for unsplit words),
+                              // 9 = every partition on counted tables (bpKeyCountedSpansKernel; set after repeated
+                              // keys), 7 = the v2 bucket table (bpKeySpanKernel) everywhere
   uint32_t rowsLds = 1;       // fused row output with the inner rows cached in LDS (0 = staged kernel)
   uint32_t matVariant = 1;    // late-materialization store/load flavour (materialize.hip)
 };

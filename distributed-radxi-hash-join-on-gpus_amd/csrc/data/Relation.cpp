@@ -70,6 +70,7 @@ void Relation::fillUniqueValues(uint64_t startKeyValue, uint64_t startRidValue) 
   runGenerate(data, localSize, p, loc_, device_);
   maxKey_ = startKeyValue + (localSize ? localSize - 1 : 0);
   setGenerated(startRidValue, true);
+  keyRepeats_ = 0;  // unique here; other ranks' slices may overlap (the reference fills per rank)
 }
 
 void Relation::fillModuloValues(uint64_t startKeyValue, uint64_t startRidValue, uint64_t innerRelationSize) {
@@ -84,6 +85,7 @@ void Relation::fillModuloValues(uint64_t startKeyValue, uint64_t startRidValue, 
   runGenerate(data, localSize, p, loc_, device_);
   maxKey_ = startKeyValue + innerRelationSize - 1;
   setGenerated(startRidValue, true);
+  keyRepeats_ = localSize > innerRelationSize ? 2 : 0;
 }
 
 void Relation::generate(const GenSpec &spec, uint64_t globalOffset) {
@@ -106,6 +108,16 @@ void Relation::generate(const GenSpec &spec, uint64_t globalOffset) {
   // Keys are permutations / draws over a dense domain (or a bijective mix of
   // one): uniform low bits.  The TPC-H layout leaves digits empty.
   setGenerated(globalOffset, !spec.tpchSparse);
+  // Unique / dense draws are a permutation of the domain; uniform and Zipf
+  // draws repeat keys once the birthday bound is passed (G^2 > 2 domain);
+  // modulo keys once the relation is larger than the domain.
+  const double G = (double)globalSize, D = (double)p.domain;
+  switch (spec.distribution) {
+    case KeyDistribution::Unique:
+    case KeyDistribution::Dense: keyRepeats_ = globalSize <= p.domain || spec.distribution == KeyDistribution::Dense ? 1 : 0; break;
+    case KeyDistribution::Modulo: keyRepeats_ = globalSize > p.domain ? 2 : 1; break;
+    default: keyRepeats_ = G * G > 2.0 * D ? 2 : 0; break;
+  }
 }
 
 void Relation::setGenerated(uint64_t ridBase, bool lowBitsUniform) {

@@ -77,6 +77,11 @@ class Relation {
   bool ridsPositional() const { return ridsPositional_; }
   uint64_t ridBase() const { return ridBase_; }
   bool lowBitsUniform() const { return lowBitsUniform_; }
+  // What the generator knows about repeated keys in the GLOBAL relation:
+  // 0 unknown (external data), 1 every key unique, 2 keys repeat.  The
+  // planner decides bitmap vs two-level and the key-only table kind from it
+  // before the first join (HashJoin::makeJoinPlan samples when 0).
+  int keyRepeats() const { return keyRepeats_; }
 
  protected:
   void randomOrder();
@@ -98,6 +103,7 @@ class Relation {
   bool ridsPositional_ = false;
   uint64_t ridBase_ = 0;
   bool lowBitsUniform_ = false;
+  int keyRepeats_ = 0;
 };
 
 }  // namespace data

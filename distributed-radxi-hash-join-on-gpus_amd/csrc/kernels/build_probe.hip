@@ -34,11 +34,9 @@ constexpr uint32_t EMPTY32 = 0xFFFFFFFFu;
 constexpr unsigned long long EMPTY64 = ~0ull;
 constexpr int MAT_SLOTS = 2;  // register-held matches per probe before the overflow path
 
-// BP_KCOUNT: counting over key-only 8-byte words (whole-value compare).
-enum BPMode : int { BP_CCOUNT = 0, BP_CMAT = 1, BP_WCOUNT = 2, BP_WMAT = 3, BP_KCOUNT = 4 };
+enum BPMode : int { BP_CCOUNT = 0, BP_CMAT = 1, BP_WCOUNT = 2, BP_WMAT = 3 };
 
 static int bpMode(const BPArgs &a) {
-  if (a.keyOnly) return BP_KCOUNT;
   return (a.wide ? 2 : 0) + (a.materialize ? 1 : 0);
 }
 
@@ -47,7 +45,6 @@ static size_t bpEntryBytes(int mode) {
     case BP_CCOUNT: return 4;
     case BP_CMAT: return 8;
     case BP_WCOUNT: return 8;
-    case BP_KCOUNT: return 8;
     default: return 16;
   }
 }
@@ -768,12 +765,11 @@ static size_t bpMatSplitLds(const BPArgs &a) { return (size_t(8) << ceilLog2(2ul
 template <int MODE, bool ITEMS>
 constexpr int bpMinBlocks() { return MODE == 0 ? (ITEMS ? 3 : 4) : 2; }
 
-// Counting modes with a hash table (CCOUNT without direct addressing, KCOUNT,
+// Counting modes with a hash table (CCOUNT without direct addressing,
 // WCOUNT): the table key and its hash for a register-held element.
 template <int MODE, typename L>
 __device__ __forceinline__ auto bpKey(const L &v) {
   if constexpr (MODE == BP_CCOUNT) return (uint32_t)v;
-  else if constexpr (MODE == BP_KCOUNT) return (unsigned long long)v;
   else return (unsigned long long)v.x;  // BP_WCOUNT: ulonglong2 {key, rid}
 }
 template <int MODE, typename K>
@@ -893,10 +889,6 @@ __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeK
             const uint32_t frag = rv[k];
             uint32_t h = hash32(frag, tbits);
             while (atomicCAS(&table[h], EMPTY32, frag) != EMPTY32) h = (h + 1) & mask;
-          } else if constexpr (MODE == BP_KCOUNT) {
-            const uint64_t v = rv[k];
-            uint32_t h = hash64(v, tbits);
-            while (atomicCAS(&table[h], EMPTY64, (unsigned long long)v) != EMPTY64) h = (h + 1) & mask;
           } else if constexpr (!WIDE) {
             const uint64_t v = rv[k];
             const uint32_t frag = (uint32_t)(v >> a.fragShift);
@@ -963,14 +955,6 @@ __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeK
               found += (e == frag);
               h = (h + 1) & mask;
             }
-          } else if constexpr (MODE == BP_KCOUNT) {
-            const uint64_t v = sv[k];
-            uint32_t h = hash64(v, tbits);
-            unsigned long long e;
-            while ((e = table[h]) != EMPTY64) {
-              found += (e == v);
-              h = (h + 1) & mask;
-            }
           } else if constexpr (!WIDE) {
             const uint64_t v = sv[k];
             const uint32_t frag = (uint32_t)(v >> a.fragShift);
@@ -1029,181 +1013,11 @@ __global__ __launch_bounds__(BPT, (bpMinBlocks<MODE, ITEMS>())) void buildProbeK
 }
 
 // ---------------------------------------------------------------- key-only
-// Count kernel of key-only 8-byte words (JoinPlan::keyOnly: wide keys, no
-// rids).  Bucketized table: buckets of 4 u64 slots (32 B) plus one u32 fill
-// counter per bucket.  Build: one returning LDS add on the home bucket's
-// counter gives the slot; an element finding its bucket full moves to the
-// next bucket (rare at load 1/2).  Probe: the counter and the whole bucket
-// are read with one u32 and two 16-byte LDS loads, all 16 elements of a lane
-// issued back to back; a counter above 4 means elements passed through to the
-// next bucket, so the walk continues there.  Against one 64-bit CAS / read
-// per probe-chain step this needs no returned CAS and no dependent chain
-// (1B x 1B sparse keys: 14 ms -> see profiles).  Only the counters are
-// cleared per item.
-constexpr int BPK_T = 256;
+// Key-only 8-byte words (JoinPlan::keyOnly: wide keys, no rids) are counted
+// over resolved spans below: the v2 bucket table (keyCount 7), the quotient
+// table (8) and counted tables (9).  Round 2's per-item kernels (variants
+// 0-6) were pruned in round 4; measurements in profiles/r2v, profiles/r3k.
 constexpr uint32_t BPK_SLOTS = 4;
-
-size_t bpKeyLdsBytes(uint32_t rChunk) {
-  const uint64_t slots = uint64_t(1) << ceilLog2(2ull * rChunk);
-  return slots * 8 + (slots / BPK_SLOTS) * 4 + 64;
-}
-
-// Bucket of a key-only word.  FOLD: xor-fold to 32 bits and one 32-bit
-// multiply (one quarter-rate v_mul instead of the three of a 64-bit product).
-template <bool FOLD>
-__device__ __forceinline__ uint32_t bpkBucket(uint64_t v, uint32_t bbits) {
-  if constexpr (FOLD)
-    return (((uint32_t)v ^ (uint32_t)(v >> 32)) * 0x9E3779B1u) >> (32 - bbits);
-  else
-    return hash64(v, bbits);
-}
-
-// (Measured and dropped: loading the next item's first batches during this
-// item's probe, build/probe 7.35 vs 6.30 ms; a split u32 + u16 column layout of
-// the local pass output for 44-bit fragments, 7.2 vs 6.0 ms.)
-// T threads x K elements per batch (T * K = 2048); H elements' buckets in
-// flight per half-batch.  CLEAR: empty slots hold ~0 (never a key-only word,
-// which is at most 64 - networkBits bits), so the probe compares all four
-// slots without masking by the fill count.
-template <int T, int K, int H, bool FOLD, bool CLEAR, int MINW>
-__global__ __launch_bounds__(T, MINW) void bpKeyCountKernel(BPArgs a, const BPItem *__restrict__ items,
-                                                             const uint32_t *__restrict__ nItemsPtr, uint32_t capacity) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const uint32_t maxSlots = 1u << ceilLog2(2ull * a.rChunk);
-  unsigned long long *table = reinterpret_cast<unsigned long long *>(smem);
-  uint32_t *fill = reinterpret_cast<uint32_t *>(table + maxSlots);
-  unsigned long long *wsum = reinterpret_cast<unsigned long long *>(fill + maxSlots / BPK_SLOTS);
-  const uint64_t *R = static_cast<const uint64_t *>(a.R);
-  const uint64_t *S = static_cast<const uint64_t *>(a.S);
-  constexpr uint32_t BATCH = T * K;
-  const uint32_t t = threadIdx.x;
-  const uint32_t nItems = min(*nItemsPtr, capacity);
-  uint64_t matches = 0;
-  for (uint32_t w = blockIdx.x; w < nItems; w += gridDim.x) {
-    const BPItem it = items[w];
-    const uint64_t rb = a.partR[it.part] + (uint64_t)it.rChunk * a.rChunk;
-    const uint32_t nr = (uint32_t)(min(a.partREnd[it.part], rb + a.rChunk) - rb);
-    const uint64_t sb = a.partS[it.part] + (uint64_t)it.sChunk * a.sChunk;
-    const uint32_t ns = (uint32_t)(min(a.partSEnd[it.part], sb + a.sChunk) - sb);
-    uint64_t rv[K], sv[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const uint32_t i = k * T + t;
-      if (i < nr) rv[k] = R[rb + i];
-      if (i < ns) sv[k] = S[sb + i];
-    }
-    uint32_t tbits = ceilLog2(2ull * nr);
-    if (tbits < 6) tbits = 6;
-    const uint32_t buckets = (1u << tbits) / BPK_SLOTS, bmask = buckets - 1;
-    for (uint32_t i = t; i < buckets; i += T) fill[i] = 0;
-    if constexpr (CLEAR) {
-      ulonglong2 *t2 = reinterpret_cast<ulonglong2 *>(table);
-      for (uint32_t i = t; i < (1u << tbits) / 2; i += T) t2[i] = make_ulonglong2(~0ull, ~0ull);
-    }
-    __syncthreads();
-    // ---- build
-    for (uint32_t b0 = 0; b0 < nr; b0 += BATCH) {
-      if (b0) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          const uint32_t i = b0 + k * T + t;
-          if (i < nr) rv[k] = R[rb + i];
-        }
-      }
-      uint32_t bk[K], pos[K];
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const bool valid = b0 + k * T + t < nr;
-        bk[k] = bpkBucket<FOLD>(rv[k], tbits - 2);
-        pos[k] = atomicAdd(&fill[bk[k]], valid ? 1u : 0u);  // branch-free: invalid lanes add 0
-        pos[k] = valid ? pos[k] : 0xFFFFFFFFu;
-      }
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        if (pos[k] == 0xFFFFFFFFu) continue;
-        uint32_t b = bk[k], p = pos[k];
-        while (p >= BPK_SLOTS) {  // home bucket full: the next one (its counter marks the pass)
-          b = (b + 1) & bmask;
-          p = atomicAdd(&fill[b], 1u);
-        }
-        table[b * BPK_SLOTS + p] = rv[k];
-      }
-    }
-    __syncthreads();
-    // ---- probe
-    for (uint32_t b0 = 0; b0 < ns; b0 += BATCH) {
-      if (b0) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          const uint32_t i = b0 + k * T + t;
-          if (i < ns) sv[k] = S[sb + i];
-        }
-      }
-      // Groups of H elements keep the 32-byte buckets of the in-flight reads
-      // within the register budget.
-#pragma unroll
-      for (int h = 0; h < K / H; ++h) {
-        uint32_t bk[H], f[H];
-        ulonglong2 e0[H], e1[H];
-#pragma unroll
-        for (int j = 0; j < H; ++j) {
-          bk[j] = bpkBucket<FOLD>(sv[h * H + j], tbits - 2);
-          f[j] = fill[bk[j]];
-          const ulonglong2 *q = reinterpret_cast<const ulonglong2 *>(table + bk[j] * BPK_SLOTS);
-          e0[j] = q[0];
-          e1[j] = q[1];
-        }
-#pragma unroll
-        for (int j = 0; j < H; ++j) {
-          const int k = h * H + j;
-          if (b0 + k * T + t >= ns) continue;
-          const uint64_t v = sv[k];
-          uint32_t c;
-          if constexpr (CLEAR) {
-            c = (e0[j].x == v) + (e0[j].y == v) + (e1[j].x == v) + (e1[j].y == v);
-          } else {
-            const uint32_t n = min(f[j], BPK_SLOTS);
-            c = (n > 0 && e0[j].x == v) + (n > 1 && e0[j].y == v) + (n > 2 && e1[j].x == v) + (n > 3 && e1[j].y == v);
-          }
-          uint32_t b = bk[j], fb = f[j];
-          while (fb > BPK_SLOTS) {  // elements passed through: continue in the next bucket
-            b = (b + 1) & bmask;
-            fb = fill[b];
-            const unsigned long long *q = table + b * BPK_SLOTS;
-            const uint32_t m = min(fb, BPK_SLOTS);
-            for (uint32_t i = 0; i < m; ++i) c += q[i] == v;
-          }
-          matches += c;
-        }
-      }
-    }
-    __syncthreads();  // the next item clears the counters
-  }
-  const unsigned long long total = blockReduceSum<T, unsigned long long>((unsigned long long)matches, wsum);
-  if (t == 0 && total) atomicAdd(a.result, total);
-}
-
-// Key-count variant (BPArgs::keyCount = KernelVariants::keyCount, A/B switch).  Measured on MI355X, 1B x
-// 1B sparse 63-bit keys, build/probe ms: 0 = 256 x 8 (90 VGPRs, 16 waves per
-// CU) 6.07; 1 = 512 x 4, 2 buckets in flight (48 VGPRs, 32 waves per CU)
-// 4.99 -- the default; 2 = 1 + folded hash 4.88 (dropped as default: keys
-// whose halves are equal would all share one bucket); 3 = 2 + cleared slots
-// 4.98; 4 = 0 + folded hash + cleared slots 6.10; 5 = 512 x 4 with 4 buckets
-// in flight 5.41.  Measured and dropped: 16-byte two-slot buckets with
-// packed 16-bit fill counters (one 16-byte LDS read per probe instead of two,
-// against 3.0 bank-conflict cycles per LDS instruction in the PMC of variant
-// 1): 5.43-5.53 ms vs 4.93-4.95 (profiles/r2v).
-template <int T, int K, int H, bool FOLD, bool CLEAR, int MINW>
-static void launchKeyCount(const BPArgs &a, const BPItem *items, const uint32_t *nItems, uint32_t capacity,
-                           hipStream_t s) {
-  const size_t ldsK = bpKeyLdsBytes(a.rChunk);
-  HJ_CHECK(ldsK <= 160 * 1024, "buildProbe: key-only table %zu B exceeds 160 KiB (rChunk=%u)", ldsK, a.rChunk);
-  HJ_CHECK(T * K >= 2 * BPK_T, "buildProbe: key-count batch too small");
-  const uint32_t perCuK = (uint32_t)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / ldsK));
-  hipLaunchKernelGGL((bpKeyCountKernel<T, K, H, FOLD, CLEAR, MINW>), dim3(std::min<uint32_t>(capacity, 256 * perCuK)),
-                     dim3(T), ldsK, s, a, items, nItems, capacity);
-  HIP_CHECK_LAUNCH();
-}
 
 // ------------------------------------------------------- key-only spans (v2)
 // The key-only count as a work queue of resolved spans.  Measured on the
@@ -1288,33 +1102,25 @@ struct KsSrc {
   }
 };
 
-// The bucket table: 4 slots (32 B) per bucket.  AoS keeps a bucket's two
-// 16-byte halves adjacent; SoA (KernelVariants::keyCount 7) stores all first
-// halves, then all second halves: a random ds_read_b128 then starts at one of
-// 16 bank quads instead of 8 (32-byte buckets), halving the expected lane
-// collisions per 16-lane group.
-template <bool SOA>
+// The bucket table: 4 slots (32 B) per bucket, stored SoA: all first 16-byte
+// halves, then all second halves, so a random ds_read_b128 starts at one of
+// 16 bank quads instead of 8 (32-byte AoS buckets, round 3's variant 6):
+// half the expected lane collisions per 16-lane group.
 struct KsTable {
   unsigned long long *t;
   uint32_t maxBuckets;
   __device__ __forceinline__ const ulonglong2 *half(uint32_t b, int h) const {
-    if constexpr (SOA)
-      return reinterpret_cast<const ulonglong2 *>(t + (h ? 2 * maxBuckets : 0)) + b;
-    else
-      return reinterpret_cast<const ulonglong2 *>(t + (size_t)b * BPK_SLOTS) + h;
+    return reinterpret_cast<const ulonglong2 *>(t + (h ? 2 * maxBuckets : 0)) + b;
   }
   __device__ __forceinline__ unsigned long long &slot(uint32_t b, uint32_t p) const {
-    if constexpr (SOA)
-      return t[(p >> 1) * 2 * maxBuckets + 2 * b + (p & 1)];
-    else
-      return t[(size_t)b * BPK_SLOTS + p];
+    return t[(p >> 1) * 2 * maxBuckets + 2 * b + (p & 1)];
   }
 };
 
 // One batch of T x K outer words (the first `valid` of them counted) against
 // the bucketized table; returns this lane's matches.
-template <int T, int K, int H, bool SOA>
-__device__ __forceinline__ uint32_t ksProbeBatch(const uint64_t (&sv)[K], uint32_t valid, const KsTable<SOA> &table,
+template <int T, int K, int H>
+__device__ __forceinline__ uint32_t ksProbeBatch(const uint64_t (&sv)[K], uint32_t valid, const KsTable &table,
                                                  const uint32_t *fill, uint32_t bbits, uint32_t bmask) {
   uint32_t matches = 0;
 #pragma unroll
@@ -1353,7 +1159,7 @@ __device__ __forceinline__ uint32_t ksProbeBatch(const uint64_t (&sv)[K], uint32
   return matches;
 }
 
-template <int T, int K, int H, int MINW, bool SPLIT, bool SOA>
+template <int T, int K, int H, int MINW, bool SPLIT>
 __global__ __launch_bounds__(T, MINW) void bpKeySpanKernel(KsSrc<T, K, SPLIT> R, KsSrc<T, K, SPLIT> S,
                                                            const BPSpan *__restrict__ spans,
                                                            const uint32_t *__restrict__ nSpansPtr, uint32_t capacity,
@@ -1361,7 +1167,7 @@ __global__ __launch_bounds__(T, MINW) void bpKeySpanKernel(KsSrc<T, K, SPLIT> R,
                                                            unsigned long long *__restrict__ result) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t maxSlots = 1u << ceilLog2(2ull * maxR);
-  const KsTable<SOA> table{reinterpret_cast<unsigned long long *>(smem), maxSlots / BPK_SLOTS};
+  const KsTable table{reinterpret_cast<unsigned long long *>(smem), maxSlots / BPK_SLOTS};
   uint32_t *fill = reinterpret_cast<uint32_t *>(table.t + maxSlots);
   BPSpan *desc = reinterpret_cast<BPSpan *>(fill + maxSlots / BPK_SLOTS);
   unsigned long long *wsum = reinterpret_cast<unsigned long long *>(desc + KS_CHUNK);
@@ -1425,11 +1231,11 @@ __global__ __launch_bounds__(T, MINW) void bpKeySpanKernel(KsSrc<T, K, SPLIT> R,
       // ---- probe: the first batch from registers (no wait on the prefetch
       // above: vmcnt is in order, so a load issued here would make the first
       // use wait for the next span's words too), later batches loaded inline.
-      matches += ksProbeBatch<T, K, H, SOA>(sv, ns, table, fill, bbits, bmask);
+      matches += ksProbeBatch<T, K, H>(sv, ns, table, fill, bbits, bmask);
       for (uint32_t b0 = BATCH; b0 < ns; b0 += BATCH) {
         uint64_t xv[K];
         S.load(sb + b0, ns - b0, xv);
-        matches += ksProbeBatch<T, K, H, SOA>(xv, ns - b0, table, fill, bbits, bmask);
+        matches += ksProbeBatch<T, K, H>(xv, ns - b0, table, fill, bbits, bmask);
       }
       __syncthreads();  // the next span clears the counters
 #pragma unroll
@@ -1504,13 +1310,16 @@ __device__ __forceinline__ void kqKey(uint64_t frag, uint32_t s, uint32_t &b, ui
   v = e ^ kqSalt(b);
 }
 
-__device__ __forceinline__ uint32_t kqOvHash(uint64_t frag) {
-  return (uint32_t)((frag * 0x9E3779B97F4A7C15ull) >> (64 - KQ_OV_BITS));
+// Overflow-table home of a key from its (bucket, stored value): (b, v) is a
+// bijection of the fragment, so one 32-bit multiply spreads keys as well as
+// hashing the whole fragment would.
+__device__ __forceinline__ uint32_t kqOvHash(uint32_t b, uint32_t v) {
+  return ((v ^ (b << 20)) * 0x9E3779B1u) >> (32 - KQ_OV_BITS);
 }
 
-// Copies of `frag` in the overflow table (it holds < KQ_OV entries).
-__device__ __forceinline__ uint32_t kqOvCount(const unsigned long long *ov, uint64_t frag) {
-  uint32_t h = kqOvHash(frag), c = 0;
+// Copies of `frag` (home h) in the overflow table (it holds < KQ_OV entries).
+__device__ __forceinline__ uint32_t kqOvCount(const unsigned long long *ov, uint32_t h, uint64_t frag) {
+  uint32_t c = 0;
   for (uint32_t w = 0; w < KQ_OV; ++w) {
     const unsigned long long y = ov[h];
     if (y == KQ_OV_EMPTY) break;
@@ -1522,13 +1331,12 @@ __device__ __forceinline__ uint32_t kqOvCount(const unsigned long long *ov, uint
 
 // Overflow placement: the entry index | KQ_OV_FLAG, or KQ_NONE when the table
 // is at its cap (full = true: the span's count is void).
-__device__ __forceinline__ uint32_t kqOvInsert(unsigned long long *ov, uint32_t *ovN, uint64_t frag, bool &chained,
-                                               bool &full) {
+__device__ __forceinline__ uint32_t kqOvInsert(unsigned long long *ov, uint32_t *ovN, uint32_t h, uint64_t frag,
+                                               bool &chained, bool &full) {
   if (atomicAdd(ovN, 1u) >= KQ_OV_CAP) {
     full = true;
     return KQ_NONE;
   }
-  uint32_t h = kqOvHash(frag);
   for (uint32_t w = 0;; ++w) {  // < KQ_OV_CAP entries taken: an empty one exists
     if (atomicCAS(&ov[h], KQ_OV_EMPTY, (unsigned long long)frag) == KQ_OV_EMPTY) {
       chained |= w > KQ_LONG_CHAIN;
@@ -1555,7 +1363,7 @@ __device__ __forceinline__ uint32_t kqProbeBatch(const uint64_t (&pv)[K], uint32
   for (int k = 0; k < K; ++k) {
     const bool esc = v[k] == KQ_EMPTY;  // only in the overflow table
     uint32_t c = esc ? 0u : (uint32_t)(x[k].x == v[k]) + (uint32_t)(x[k].y == v[k]);
-    if (x[k].y != KQ_EMPTY || esc) c += kqOvCount(ov, pv[k]);
+    if (x[k].y != KQ_EMPTY || esc) c += kqOvCount(ov, kqOvHash(bk[k], v[k]), pv[k]);
     matches += (uint32_t)(k * T) + threadIdx.x < valid ? c : 0u;
   }
   return matches;
@@ -1670,7 +1478,7 @@ __global__ __launch_bounds__(T, MINW) void bpKeyQuotientKernel(KsSrc<T, K, true>
         }
 #pragma unroll
         for (int k = 0; k < K; ++k)
-          if (pos[k] == KQ_OV_FLAG) pos[k] = kqOvInsert(ov, ovN, rv[k], chained, full);
+          if (pos[k] == KQ_OV_FLAG) pos[k] = kqOvInsert(ov, ovN, kqOvHash(bk[k], v[k]), rv[k], chained, full);
       }
       __syncthreads();
       // ---- the next span's words stream in while this one probes
@@ -1852,16 +1660,14 @@ void buildProbeKeySpans(const BPArgs &a, const BPSpan *spans, const uint32_t *nS
   const uint32_t perCu = (uint32_t)std::max<size_t>(1, std::min<size_t>(4, (160 * 1024) / lds));
   const dim3 grid(std::min<uint32_t>(ceilDiv(capacity, KS_CHUNK), 256 * perCu));
   HIP_CHECK(hipMemsetAsync(queue, 0, sizeof(uint32_t), s));
-#define HJ_KS(SPLIT, SOA)                                                                                        \
-  hipLaunchKernelGGL((bpKeySpanKernel<T, K, H, 8, SPLIT, SOA>), grid, dim3(T), lds, s,                            \
+#define HJ_KS(SPLIT)                                                                                             \
+  hipLaunchKernelGGL((bpKeySpanKernel<T, K, H, 8, SPLIT>), grid, dim3(T), lds, s,                                 \
                      KsSrc<T, K, SPLIT>{a.R, SPLIT ? a.Rhi : nullptr}, KsSrc<T, K, SPLIT>{a.S, SPLIT ? a.Shi : nullptr}, \
                      spans, nSpans, capacity, queue, a.rChunk, a.result)
-  const bool soa = a.keyCount >= 7;
-  if (a.split) {
-    if (soa) HJ_KS(true, true); else HJ_KS(true, false);
-  } else {
-    if (soa) HJ_KS(false, true); else HJ_KS(false, false);
-  }
+  if (a.split)
+    HJ_KS(true);
+  else
+    HJ_KS(false);
 #undef HJ_KS
   HIP_CHECK_LAUNCH();
 }
@@ -1880,18 +1686,7 @@ void buildProbe(const BPArgs &args, const BPItem *items, const uint32_t *nItems,
   HJ_CHECK(!a.split || (a.Rhi && a.Shi), "buildProbe: split layout without fragment columns");
   HJ_CHECK(a.wide || a.keyOnly || a.fragShift >= 32,
            "buildProbe: fragShift=%u < 32 (the rid field of a CompressedTuple is >= 32 bits)", a.fragShift);
-  HJ_CHECK(!(a.keyOnly && (a.materialize || a.wide || a.split)), "buildProbe: key-only words count only, unsplit");
-  if (bpMode(a) == BP_KCOUNT) {
-    switch (a.keyCount) {
-      case 2: launchKeyCount<512, 4, 2, true, false, 8>(a, items, nItems, capacity, s); break;
-      case 3: launchKeyCount<512, 4, 2, true, true, 8>(a, items, nItems, capacity, s); break;
-      case 4: launchKeyCount<256, 8, 4, true, true, 4>(a, items, nItems, capacity, s); break;
-      case 5: launchKeyCount<512, 4, 4, true, true, 8>(a, items, nItems, capacity, s); break;
-      case 0: launchKeyCount<256, 8, 4, false, false, 4>(a, items, nItems, capacity, s); break;
-      default: launchKeyCount<512, 4, 2, false, false, 8>(a, items, nItems, capacity, s); break;
-    }
-    return;
-  }
+  HJ_CHECK(!a.keyOnly, "buildProbe: key-only words are counted over spans (buildProbeKeySpans)");
   if (bpMode(a) == BP_CCOUNT && a.split && bpDirect(a) && !a.itemCounts) {
     const size_t ldsD = ((size_t(4) << a.fragBits) + 15) / 16 * 16 + 64;
     const uint32_t perCuD = (uint32_t)std::min<size_t>(BPD_MINB, (160 * 1024) / ldsD);  // occupancy target

@@ -520,6 +520,15 @@ void npjProbe(const data::Tuple *S, uint64_t nS, const unsigned long long *table
               unsigned long long *result, hipStream_t s);
 
 // ---------------------------------------------------------- micro-benchmarks
+// Plan-time repeated-key probe (microbench.hip): S evenly spaced keys of
+// in[0, n) into a set in ws (sampleRepeatsBytes(S)); *repeats = sampled keys
+// that were already in it.
+size_t sampleRepeatsBytes(uint32_t S);
+void sampleRepeats(const data::Tuple *in, uint64_t n, uint32_t S, void *ws, unsigned int *repeats, hipStream_t s);
+// Stream-mix ceiling (microbench.hip): n elements, read streams of ra / rb
+// bytes, write streams of wa / wb bytes per element (0 = none), in order.
+void streamMix(int ra, int rb, int wa, int wb, const void *a, const void *b, void *oa, void *ob, uint64_t n,
+               unsigned long long *sink, hipStream_t s);
 void copyKernel(const ulonglong2 *in, ulonglong2 *out, uint64_t n16, hipStream_t s);
 void readKernel(const ulonglong2 *in, uint64_t n16, unsigned long long *sink, hipStream_t s);
 void projectKeys(const ulonglong2 *in, uint64_t n, uint32_t shift, uint32_t *out, int ipt, hipStream_t s);

@@ -26,6 +26,60 @@ __global__ __launch_bounds__(256) void readKernelImpl(const ulonglong2 *__restri
   if (acc == 0x9E3779B97F4A7C15ull) *sink = acc;  // keeps the loads live
 }
 
+// Stream-mix ceiling of a pass's exact byte mix (tools/stream_mix_bench.py):
+// up to two read streams of RA / RB bytes per element and two write streams
+// of WA / WB bytes per element, all in order, no partitioning.  A lane moves
+// 8 elements per step as 16-byte vectors (8 x RA / 16 loads of stream A, ...),
+// so every stream is read / written with the widest access whatever its
+// element size; written words are XORs of read words (nothing folds away).
+using mixv = unsigned int __attribute__((ext_vector_type(4)));
+template <int RA, int RB, int WA, int WB>
+__global__ __launch_bounds__(256) void streamMixKernel(const mixv *__restrict__ a, const mixv *__restrict__ b,
+                                                       mixv *__restrict__ wa, mixv *__restrict__ wb, uint64_t steps,
+                                                       unsigned long long *sink) {
+  constexpr int LA = RA / 2, LB = RB / 2, SA = WA / 2, SB = WB / 2;  // 16-byte vectors per 8 elements
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  mixv acc = {0, 0, 0, 0};
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < steps; i += stride) {
+    mixv x = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < LA; ++k) x ^= __builtin_nontemporal_load(a + i * LA + k);
+#pragma unroll
+    for (int k = 0; k < LB; ++k) x ^= __builtin_nontemporal_load(b + i * LB + k);
+#pragma unroll
+    for (int k = 0; k < SA; ++k) wa[i * SA + k] = x + (unsigned)k;
+#pragma unroll
+    for (int k = 0; k < SB; ++k) wb[i * SB + k] = x - (unsigned)k;
+    acc ^= x;
+  }
+  if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9E3779B9u) *sink = acc.x;  // keeps read-only mixes live
+}
+
+void streamMix(int ra, int rb, int wa, int wb, const void *a, const void *b, void *oa, void *ob, uint64_t n,
+               unsigned long long *sink, hipStream_t s) {
+  const uint64_t steps = n / 8;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(ceilDiv(steps, 256), 256 * 16);
+#define HJ_MIX(RA, RB, WA, WB)                                                                                    \
+  if (ra == RA && rb == RB && wa == WA && wb == WB) {                                                             \
+    hipLaunchKernelGGL((streamMixKernel<RA, RB, WA, WB>), dim3(grid), dim3(256), 0, s, (const mixv *)a,          \
+                       (const mixv *)b, (mixv *)oa, (mixv *)ob, steps, sink);                                  \
+    HIP_CHECK_LAUNCH();                                                                                            \
+    return;                                                                                                        \
+  }
+  HJ_MIX(16, 0, 8, 0)  // general-path network pass: tuple in, key-only word out
+  HJ_MIX(16, 0, 4, 0)  // count-only network pass: tuple in, u32 fragment out
+  HJ_MIX(16, 0, 16, 0) // copy
+  HJ_MIX(8, 0, 4, 2)   // split local pass: key-only word in, u32 + u16 columns out
+  HJ_MIX(8, 0, 8, 0)   // unsplit local pass
+  HJ_MIX(4, 0, 2, 0)   // fragment local pass (two-level fragments)
+  HJ_MIX(4, 2, 0, 0)   // key-only build/probe: u32 + u16 columns read
+  HJ_MIX(4, 0, 0, 0)   // bitmap join: u32 fragments read
+  HJ_MIX(2, 0, 0, 0)   // direct-count build/probe: u16 column read
+  HJ_MIX(16, 0, 0, 0)  // read only
+#undef HJ_MIX
+  HJ_CHECK(false, "streamMix: no instantiation for read %d+%d / write %d+%d bytes", ra, rb, wa, wb);
+}
+
 // Random 32-byte row gather shapes (tools/gather_bench.py): MODE 0 a lane
 // per 16-byte half row; 1 a lane per whole row (two loads); 2 as 0 with four
 // rows per lane pair in flight; 3 as 0 with non-temporal loads.
@@ -167,6 +221,44 @@ __global__ __launch_bounds__(256) void keyRidMaxKernel(const ulonglong2 *__restr
     atomicMax(&out[1], r);
     atomicMin(&out[2], rmin);
   }
+}
+
+// Plan-time duplicate probe of the inner keys (HashJoin::makeJoinPlan, for
+// relations whose generator did not say): S keys at evenly spaced positions
+// go into a global open-addressing set of 2^tbits >= 2S entries (CAS); a key
+// that finds itself already there counts one repeat.  ~0 (the empty marker)
+// is skipped.  One launch, no sort, ~20 us for 64K samples.
+__global__ __launch_bounds__(256) void sampleRepeatsKernel(const ulonglong2 *__restrict__ in, uint64_t n, uint32_t S,
+                                                           unsigned long long *__restrict__ set, uint32_t tbits,
+                                                           unsigned int *__restrict__ repeats) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= S) return;
+  const unsigned long long key = in[(uint64_t)((unsigned __int128)i * n / S)].x;
+  if (key == ~0ull) return;
+  const uint32_t mask = (1u << tbits) - 1;
+  uint32_t h = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - tbits));
+  for (uint32_t w = 0; w <= mask; ++w) {  // 2^tbits >= 2S: an empty entry is always reached
+    const unsigned long long o = atomicCAS(&set[h], ~0ull, key);
+    if (o == ~0ull) return;
+    if (o == key) {
+      atomicAdd(repeats, 1u);
+      return;
+    }
+    h = (h + 1) & mask;
+  }
+}
+
+size_t sampleRepeatsBytes(uint32_t S) { return ((size_t)8 << ceilLog2(2ull * std::max<uint32_t>(S, 1))) + 16; }
+
+void sampleRepeats(const data::Tuple *in, uint64_t n, uint32_t S, void *ws, unsigned int *repeats, hipStream_t s) {
+  if (n == 0 || S == 0) return;
+  const uint32_t tbits = ceilLog2(2ull * S);
+  auto *set = static_cast<unsigned long long *>(ws);
+  HIP_CHECK(hipMemsetAsync(set, 0xFF, (size_t)8 << tbits, s));
+  HIP_CHECK(hipMemsetAsync(repeats, 0, sizeof(unsigned int), s));
+  hipLaunchKernelGGL(sampleRepeatsKernel, dim3(ceilDiv(S, 256)), dim3(256), 0, s,
+                     reinterpret_cast<const ulonglong2 *>(in), n, S, set, tbits, repeats);
+  HIP_CHECK_LAUNCH();
 }
 
 void keyRidMax(const data::Tuple *in, uint64_t n, unsigned long long *out, hipStream_t s) {

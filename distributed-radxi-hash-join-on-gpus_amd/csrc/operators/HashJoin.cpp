@@ -1,6 +1,7 @@
 #include "HashJoin.h"
 
 #include <algorithm>
+#include <unordered_set>
 #include <cmath>
 #include <vector>
 
@@ -66,10 +67,11 @@ void HashJoin::makeJoinPlan() {
   // bits are known to be uniform}.  Generated relations know these bounds
   // (Relation::keyBoundKnown / ridsPositional): no pass over the data; others
   // are scanned once here (kernels::keyRidMax).
+  const uint64_t tPlan = nowUs();
   const uint32_t C = std::max<uint32_t>(1, config.chunks);
   ridLo[0] = ridLo[1] = ~0ull;
   ridHi[0] = ridHi[1] = 0;
-  const size_t STATS = 3 + 4 * (size_t)C;
+  const size_t STATS = 4 + 4 * (size_t)C;
   std::vector<uint64_t> st(STATS, 0);
   int which = 0;
   for (data::Relation *r : {innerRelation, outerRelation}) {
@@ -110,18 +112,26 @@ void HashJoin::makeJoinPlan() {
     ++which;
   }
   st[STATS - 1] = innerRelation->lowBitsUniform() ? 1 : 0;
+  st[STATS - 2] = (uint64_t)innerKeyRepeats();
   ctx->workspace().reset();
   std::vector<uint64_t> all(STATS * numberOfNodes);
   ctx->comm()->allGatherHost(st.data(), all.data(), STATS);
   uint64_t mx[2] = {0, 0};
-  bool lowBitsUniform = true;
+  bool lowBitsUniform = true, repeats = false;
   for (uint32_t r = 0; r < numberOfNodes; ++r) {
     mx[0] = std::max(mx[0], all[STATS * r]);
     mx[1] = std::max(mx[1], all[STATS * r + 1]);
     lowBitsUniform = lowBitsUniform && all[STATS * r + STATS - 1] == 1;
+    repeats = repeats || all[STATS * r + STATS - 2] == 2;
   }
   plan = core::makePlan(config, numberOfNodes, innerRelation->getGlobalSize(), outerRelation->getGlobalSize(), mx[0],
                         mx[1]);
+  // Repeated inner keys are known before the first join (generator metadata
+  // or the sample above): no bitmap plan to attempt and throw away, and
+  // key-only words go on counted tables from the first join instead of
+  // switching after a quotient table chained the copies.
+  plan.innerRepeats = repeats;
+  if (repeats && plan.keyOnly && plan.variants.keyCount == 8) plan.variants.keyCount = 9;
   planWireCodec(all, STATS, C);
   // Key mixing only when the inner keys' low bits are not known to be uniform
   // and a histogram of them says they are skewed (a collective: every rank
@@ -166,6 +176,8 @@ void HashJoin::makeJoinPlan() {
   bitmapExact = !(ctx->onDevice() && sampleable);
   planBitmap();
   JOIN_DEBUG("HashJoin", "%s", plan.describe().c_str());
+  planMs = (nowUs() - tPlan) / 1000.0;
+  const uint64_t tReserve = nowUs();
   if (ctx->onDevice())
     for (auto &e : ev)
       if (!e) HIP_CHECK(hipEventCreate(&e));
@@ -184,6 +196,34 @@ void HashJoin::makeJoinPlan() {
     reserved = ctx->workspace().ensure(want, true, ctx->stream());
     JOIN_DEBUG("HashJoin", "workspace: estimate %.2f GB, added %.2f GB", want / 1e9, reserved / 1e9);
   }
+  reserveMs = (nowUs() - tReserve) / 1000.0;
+}
+
+// 1 = this rank's inner keys look unique, 2 = they repeat: from the
+// generator when it knows (Relation::keyRepeats), else from 64K evenly
+// spaced keys (kernels::sampleRepeats; any repeat in the sample decides).
+// A sample can miss rare repeats; the plans stay exact either way (the bitmap
+// plan's duplicate check and the quotient table's chain flag still fall back).
+int HashJoin::innerKeyRepeats() {
+  if (innerRelation->keyRepeats()) return innerRelation->keyRepeats();
+  const uint64_t n = innerRelation->getLocalSize();
+  const uint32_t S = (uint32_t)std::min<uint64_t>(n, 65536);
+  if (S < 2) return 1;
+  const data::Tuple *t = innerRelation->getData();
+  if (ctx->onDevice()) {
+    void *ws = ctx->workspace().get(kernels::sampleRepeatsBytes(S));
+    auto *cnt = ctx->workspace().getArray<unsigned int>(1);
+    kernels::sampleRepeats(t, n, S, ws, cnt, ctx->stream());
+    unsigned int h = 0;
+    HIP_CHECK(hipMemcpyAsync(&h, cnt, sizeof(h), hipMemcpyDeviceToHost, ctx->stream()));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream()));
+    return h ? 2 : 1;
+  }
+  std::unordered_set<uint64_t> seen;
+  seen.reserve(2 * S);
+  for (uint32_t i = 0; i < S; ++i)
+    if (!seen.insert(t[(uint64_t)((unsigned __int128)i * n / S)].key).second) return 2;
+  return 1;
 }
 
 uint64_t HashJoin::workspaceEstimate() const {
@@ -252,6 +292,10 @@ void HashJoin::planBitmap() {
                             8.0 / std::max<uint32_t>(N, 1);
   }
   if (!config.bitmapJoin || plan.materialize || plan.wide || plan.keyOnly || plan.keyBits >= 64) return;
+  // Repeated inner keys would only make the bitmap plan fall back after a
+  // whole failed join; replicateBitmap = On still forces it (tests of that
+  // fallback path).
+  if (plan.innerRepeats && config.replicateBitmap != core::PlanChoice::On) return;
   const uint32_t want = plan.keyBits > kernels::BITMAP_MAX_BITS ? plan.keyBits - kernels::BITMAP_MAX_BITS : 0;
   const uint32_t nb =
       config.networkBits ? config.networkBits : std::min<uint32_t>(kernels::MAX_PART_BITS, std::max<uint32_t>(10, want));

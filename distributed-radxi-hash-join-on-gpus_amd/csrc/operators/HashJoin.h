@@ -115,9 +115,16 @@ class HashJoin {
   uint64_t workspaceEstimate() const;
   // Bytes the constructor added to the arena (0 if it already held the estimate).
   uint64_t reservedBytes() const { return reserved; }
+  // Construction cost: planning (key / rid bounds, repeated-key and low-bit
+  // scans when the generator did not record them, the all-gather) and the
+  // workspace reservation (allocation + first touch).  Host wall time, ms.
+  double planMilliseconds() const { return planMs; }
+  double reserveMilliseconds() const { return reserveMs; }
 
  private:
   uint64_t reserved = 0;
+  double planMs = 0, reserveMs = 0;
+  int innerKeyRepeats();
   void planWireCodec(const std::vector<uint64_t> &rankStats, size_t stride, uint32_t chunks);
   JoinResult runImpl();
   core::ExecContext *ctx;

@@ -151,7 +151,7 @@ void BuildProbe::execute() {
   // to the counted-table kernel instead of the span work queue.  Fragments
   // of 45-48 bits (inputs below ~500M tuples) do not fit the quotient table:
   // every partition is counted there.
-  const bool keySpans = args.keyOnly && (args.keyCount >= 6 || args.split);  // the item kernels read unsplit words only
+  const bool keySpans = args.keyOnly;
   const bool counted = keySpans && args.keyCount >= 8 && kernels::bpKeyCountedFits(args);
   const bool quotient = counted && kernels::bpKeyQuotientFits(args);
   if (counted) {

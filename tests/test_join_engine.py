@@ -517,3 +517,40 @@ def test_bitmap_join_config_and_host_plan(C, monkeypatch):
     res, exp, j = run_join(C, "cpu", 100_000, 100_000, cfg=cfg)
     assert not j.plan.bitmap_join and not res["bitmap_join"] and res["global_matches"] == exp
     assert "bitmap=0/0" in repr(j.plan)
+
+
+@pytest.mark.parametrize("dev", devices())
+def test_repeated_inner_keys_planned_before_first_join(C, dev):
+    """Repeated inner keys are known at plan time -- from the generator
+    (Zipf draws) or from a 64K-key sample of an external tensor -- so the
+    first join neither attempts a bitmap plan and falls back nor (key-only
+    words) starts on quotient tables: no fallback, no re-run, exact."""
+    import torch
+    loc = "device" if dev == "cuda" else "host"
+    ctx = C.ExecContext(loc, 0 if loc == "device" else -1, C.LocalCommunicator())
+    G = 300_000
+    for sparse in (False, True):
+        inner = C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=5, domain=G, zipf_theta=0.9)
+        outer = C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=6, domain=G, zipf_theta=0.9)
+        inner.sparse64 = outer.sparse64 = sparse
+        R = C.Relation(G, G, loc, 0)
+        S = C.Relation(G, G, loc, 0)
+        R.generate(inner, 0)
+        S.generate(outer, 0)
+        from helpers import ref_join_count
+        exp = ref_join_count(R.to_tensor()[:, 0].cpu(), S.to_tensor()[:, 0].cpu())
+        j = C.HashJoin(R, S, ctx, C.JoinConfig())
+        assert j.plan.inner_repeats and not j.plan.bitmap_join, j.plan
+        assert j.plan_ms >= 0 and j.reserve_ms >= 0
+        res = j.run()
+        assert res["global_matches"] == exp and res["local_fallbacks"] == 0 and res["reruns"] == 0, res
+    # external tensors: sampled
+    tdev = "cuda" if dev == "cuda" else "cpu"
+    i = torch.arange(G, dtype=torch.int64)
+    for keys, rep in ((i % 1000, True), (i.flip(0), False)):
+        t = torch.stack([keys, i], 1).contiguous().to(tdev)
+        o = torch.stack([i, i], 1).contiguous().to(tdev)
+        j = C.HashJoin(C.Relation.from_tensor(t, G), C.Relation.from_tensor(o, G), ctx, C.JoinConfig())
+        assert j.plan.inner_repeats == rep, (rep, j.plan)
+        from helpers import ref_join_count
+        assert j.run()["global_matches"] == ref_join_count(keys, i)
