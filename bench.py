@@ -119,6 +119,67 @@ def link_prediction(info, plan, results):
             "measured_wire_bytes_rank0": results[-1]["wire_bytes"]}
 
 
+def scale_model(C, info, ctx, comm, on_gpu, G_R, G_S, specs, cfg, rel_loc, general_cfg_ok):
+    """Predicted N = 2/4/8 step times of the three N > 1 paths, from one
+    GPU: a rank's kernel work at N is measured directly as the same join on
+    its share (G/N x G/N tuples), plus the wire pack/unpack of the (N-1)/N of
+    its tuples that leave it (measured codec rates), plus the link time the
+    plan's cost model gives for its bytes per rank at the model bandwidth,
+    minus what hides behind the other relation's network pass (the chunked
+    pipelines overlap one side's exchange with the other side's scatter).
+      value      replicated bitmaps: all-reduce of 2 (N-1)/N x 2^keyBits / 8 B
+      shuffle    hash-partition shuffle of the dense keys: w = keyBits - net bits
+      general    the same shuffle of 63-bit keys (key-only words, w = 53)
+    The driver's SCALE run is the measurement this is checked against."""
+    if info.world != 1 or not on_gpu:
+        return None
+    import math
+    from hpcjoin.utils import config_from_dict
+    per_peer = cfg.link_gbps_per_peer if cfg.link_gbps_per_peer > 0 else 64.0
+    # wire codec rates (ms per tuple) at the two widths, 64M tuples
+    raw = torch.randint(0, 1 << 62, (1 << 26,), dtype=torch.int64, device="cuda")
+    codec = {}
+    for w in (20, 53):
+        r = C.ops.bench_wire(raw, w, 0, 0, 5)
+        codec[w] = (r["pack_ms"] + r["unpack_ms"]) / raw.numel()
+    del raw
+    torch.cuda.empty_cache()
+    key_bits = max(1, math.ceil(math.log2(max(G_R, 2))))
+    out = {"link_GBps_per_peer": per_peer, "source": "measured per-rank share on one GPU + codec rates + link model",
+           "paths": {}}
+    for path in ("value", "shuffle", "general"):
+        if path == "general" and not general_cfg_ok:
+            continue
+        rows = []
+        for N in (2, 4, 8):
+            gr, gs = G_R // N, G_S // N
+            c = config_from_dict({}) if path != "shuffle" else config_from_dict({"bitmap_join": False})
+            c.chunks = 1
+            m = measure(C, info, ctx, comm, on_gpu, gr, gs, *specs(path == "general"), c, rel_loc, 3, 1)
+            m.pop("join"), m.pop("results")
+            ctx.reset_scratch()
+            link_gbps = per_peer * min(N - 1, 7)
+            share = (N - 1) / N
+            if path == "value":
+                net = 10
+                link_bytes = 2 * share * (1 << key_bits) / 8
+                codec_ms = 0.0
+            else:
+                net = 10
+                w = (key_bits - net) if path == "shuffle" else 53
+                link_bytes = share * (gr * w + gs * w) / 8
+                codec_ms = share * (gr + gs) * codec[20 if path == "shuffle" else 53]
+            link_ms = link_bytes / link_gbps / 1e6
+            hide_ms = m["phases_ms"]["dev_network_ms"] / 2  # the other relation's network pass
+            pred = m["ms_per_step"] + codec_ms + max(0.0, link_ms - hide_ms)
+            rows.append({"n_gpus": N, "rank_share_ms": m["ms_per_step"], "codec_ms": round(codec_ms, 3),
+                         "link_bytes_per_rank": int(link_bytes), "link_ms": round(link_ms, 3),
+                         "hidden_behind_scatter_ms": round(hide_ms, 3), "predicted_ms": round(pred, 3),
+                         "predicted_value": round((G_R + G_S) / pred / 1e6, 2), "rank_share_correct": m["correct"]})
+        out["paths"][path] = rows
+    return out
+
+
 def rccl_debug_env(info):
     """Ask RCCL to log its transport choices to a per-rank file (not stdout:
     rank 0 prints one JSON line; this overrides an inherited NCCL_DEBUG level,
@@ -264,16 +325,19 @@ def measure(C, info, ctx, comm, on_gpu, G_R, G_S, inner, outer, cfg, rel_loc, st
         results.append(join.run())
     barrier()
     elapsed = time.perf_counter() - t0
-    mine = [int(elapsed * 1e9), int(first_ms * 1e6), int(setup_ms * 1e6)]
+    mine = [int(elapsed * 1e9), int(first_ms * 1e6), int(setup_ms * 1e6), int(join.plan_ms * 1e6)]
+    plan_ms = join.plan_ms
     if info.world > 1:
         allv = comm.all_gather(mine)
-        elapsed, first_ms, setup_ms = max(allv[0::3]) / 1e9, max(allv[1::3]) / 1e6, max(allv[2::3]) / 1e6
+        elapsed, first_ms, setup_ms = max(allv[0::4]) / 1e9, max(allv[1::4]) / 1e6, max(allv[2::4]) / 1e6
+        plan_ms = max(allv[3::4]) / 1e6
     ms = elapsed * 1e3 / steps
     out = {
         "ms_per_step": round(ms, 3),
         "value": round((G_R + G_S) * steps / elapsed / 1e9, 4),
         "first_join_ms": round(first_ms, 3),
         "setup_ms": round(setup_ms, 3),
+        "plan_ms": round(plan_ms, 3),
         "workspace_reserved_GB": round(join.reserved_bytes / 1e9, 2),
         "matches": results[-1]["global_matches"],
         "expected_matches": expected,
@@ -304,6 +368,8 @@ def main():
     ap.add_argument("--general", default="on", choices=["on", "off", "only"],
                     help="also time the general path: the same join on sparse random 63-bit keys "
                          "(only: just that, for sweeps)")
+    ap.add_argument("--scale-model", default="on", choices=["on", "off"],
+                    help="N = 1 only: predicted N = 2/4/8 step times of the three N > 1 paths (scale_model)")
     ap.add_argument("--json-out", default="")
     args = ap.parse_args()
 
@@ -403,6 +469,14 @@ def main():
             comm_ok = info.world == 1
             print(f"bench.py: general path failed on rank {info.rank}: {e}", file=sys.stderr, flush=True)
 
+    model = None
+    if args.scale_model == "on" and info.world == 1 and on_gpu and args.dist == "unique" and comm_ok:
+        try:
+            model = scale_model(C, info, ctx, comm, on_gpu, G_R, G_S, specs, cfg, rel_loc, args.general != "off")
+        except Exception as e:  # noqa: BLE001
+            model = {"error": f"{type(e).__name__}: {e}"[:500]}
+            print(f"bench.py: scale model failed: {e}", file=sys.stderr, flush=True)
+
     correct = head["correct"] is not False
     if info.world > 1:
         tr = [None] * info.world
@@ -435,6 +509,7 @@ def main():
             },
             "first_join_ms": head["first_join_ms"],
             "setup_ms": head["setup_ms"],
+            "plan_ms": head["plan_ms"],
             "matches": head["matches"],
             "expected_matches": head["expected_matches"],
             "correct": head["correct"],
@@ -442,6 +517,7 @@ def main():
             "links": links,
             "shuffle_path": shuffle,
             "general_path": general,
+            "scale_model": model,
             "engine": engine,
             "topology": topo,
             "device": torch.cuda.get_device_name(0) if on_gpu else "cpu",

@@ -1286,14 +1286,12 @@ constexpr uint32_t KQ_OV = 1u << KQ_OV_BITS;  // overflow entries (4 KiB)
 constexpr uint32_t KQ_OV_CAP = 3 * KQ_OV / 4;  // at most this many inserted: probes always find an empty entry
 constexpr unsigned long long KQ_OV_EMPTY = ~0ull;  // fragments are < 2^48
 constexpr uint32_t KQ_OV_FLAG = 0x80000000u;       // pos[]: overflow-table index
-constexpr uint32_t KQ_SIDE = 64;                   // counted table: escape list
 constexpr uint32_t KQ_NONE = 0xFFFFFFFFu;
 // A placement that walked past this many overflow entries saw one key's
 // copies chained (unique keys at <= 25 % overflow load never do): KQF_CHAINS,
 // and later joins put every partition on counted spans (keyCount 9).
 constexpr uint32_t KQ_LONG_CHAIN = 64;
 // BPArgs::sideOverflow bits.
-constexpr unsigned long long KQF_V2 = 1;       // counted escape list overflowed: count void, re-run on v2
 constexpr unsigned long long KQF_CHAINS = 2;   // copies of a key chained (count exact)
 constexpr unsigned long long KQF_COUNTED = 8;  // quotient overflow table full: count void, re-run counted
 
@@ -1370,17 +1368,19 @@ __device__ __forceinline__ uint32_t kqProbeBatch(const uint64_t (&pv)[K], uint32
 }
 
 // Counted table (bpKeyCountedSpansKernel): entry e = one distinct key,
-//   slot 0 = stored value v, slot 1 = id << 16 | (count - 1),  id = dist << 4 | tag,
-// dist = e - home bucket (linear probing).  (v, id) at entry e names exactly
-// one fragment, so a probe compares both and never matches a key of another
-// home.  Claimed by one 64-bit CAS of (v, id, 0) on an empty entry; a copy
-// finding its (v, id) adds 1 to slot 1.  Escape keys (v = empty marker) go to
-// a side list.
+//   slot 0 = stored value, slot 1 = id << 16 | esc << 15 | (count - 1),
+//   id = dist << 4 | tag,  dist = e - home bucket (linear probing).
+// (stored value, id, esc) at entry e names exactly one fragment, so a probe
+// never matches a key of another home.  Escape keys (v = the empty marker)
+// are stored inline with esc = 1 and stored value 0: e = ~salt(b) is implied
+// by the home bucket, so (home, tag) names them.  Claimed by one 64-bit CAS
+// of (value, id, esc, 0) on an empty entry; a copy finding its own triple
+// adds 1 to slot 1 (counts <= 2048 per span stay below bit 15).
 __device__ __forceinline__ uint32_t kqCountedId(uint32_t dist, uint32_t tag) { return (dist << 4) | tag; }
 
 template <int T, int K>
 __device__ __forceinline__ uint32_t kqProbeCounted(const uint64_t (&pv)[K], uint32_t valid, uint32_t s,
-                                                   const uint2 *tab2, const unsigned long long *side, uint32_t nSide) {
+                                                   const uint2 *tab2) {
   uint32_t bk[K], v[K], tg[K];
   uint2 x[K];
 #pragma unroll
@@ -1391,20 +1391,17 @@ __device__ __forceinline__ uint32_t kqProbeCounted(const uint64_t (&pv)[K], uint
   uint32_t matches = 0;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
+    const uint32_t esc = v[k] == KQ_EMPTY, vs = esc ? 0u : v[k];
     uint32_t c = 0, e = bk[k];
     uint2 y = x[k];
     for (uint32_t dist = 0; dist < KQ_BUCKETS; ++dist) {
-      if (y.x == v[k] && (y.y >> 16) == kqCountedId(dist, tg[k])) {
-        c = (y.y & 0xFFFFu) + 1;
+      if (y.x == vs && (y.y >> 15) == ((kqCountedId(dist, tg[k]) << 1) | esc)) {
+        c = (y.y & 0x7FFFu) + 1;
         break;
       }
       if (y.x == KQ_EMPTY) break;
       e = (e + 1) & (KQ_BUCKETS - 1);
       y = tab2[e];
-    }
-    if (v[k] == KQ_EMPTY) {  // escape: the side list
-      c = 0;
-      for (uint32_t j = 0; j < nSide; ++j) c += side[j] == pv[k];
     }
     matches += (uint32_t)(k * T) + threadIdx.x < valid ? c : 0u;
   }
@@ -1551,32 +1548,28 @@ static void launchKeyQuotient(const BPArgs &a, const BPSpan *spans, const uint32
 // tiling) are counted here on a *counted* table over the same 32 KiB (see
 // kqProbeCounted): one entry per distinct key, so copies only add to a count.
 // A span's <= 2048 inner tuples fill at most half of the 4096 entries.  This
-// table also carries 45-48-bit fragments (the tag next to the count), so
-// plans whose fragments the quotient table cannot hold count every partition
-// here.  Escape keys use a 64-entry side list; more set KQF_V2 (re-run on
-// v2).  A hot partition's spans spread over workgroups like any others.
+// table also carries 45-48-bit fragments (the tag next to the count) and
+// escape keys inline, so it never needs a fallback: plans whose fragments the
+// quotient table cannot hold, and quotient spans that filled their overflow
+// table, count here.  A hot partition's spans spread over workgroups like any
+// others.
 template <int T, int K>
 __global__ __launch_bounds__(T) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R, KsSrc<T, K, true> S,
                                                               const BPSpan *__restrict__ spans,
                                                               const uint32_t *__restrict__ nSpansPtr, uint32_t capacity,
-                                                              uint32_t s, unsigned long long *__restrict__ result,
-                                                              unsigned long long *__restrict__ flags) {
+                                                              uint32_t s, unsigned long long *__restrict__ result) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint32_t *tab = reinterpret_cast<uint32_t *>(smem);  // [entry][value, id << 16 | count - 1]
+  uint32_t *tab = reinterpret_cast<uint32_t *>(smem);  // [entry][value, id << 16 | esc << 15 | count - 1]
   unsigned long long *tab64 = reinterpret_cast<unsigned long long *>(smem);
   const uint2 *tab2 = reinterpret_cast<const uint2 *>(smem);
-  unsigned long long *side = reinterpret_cast<unsigned long long *>(tab + 2 * KQ_BUCKETS);
-  uint32_t *ctl = reinterpret_cast<uint32_t *>(side + KQ_SIDE);  // [0] side list length
-  unsigned long long *wsum = reinterpret_cast<unsigned long long *>(ctl + 4);
+  unsigned long long *wsum = reinterpret_cast<unsigned long long *>(tab + 2 * KQ_BUCKETS);
   constexpr uint32_t BATCH = T * K;
   const uint32_t t = threadIdx.x;
   const uint32_t n = min(*nSpansPtr, capacity);
   uint64_t matches = 0;
-  bool overflow = false;
   auto clear = [&]() {
     uint4 *t4 = reinterpret_cast<uint4 *>(tab);
     for (uint32_t i = t; i < KQ_BUCKETS / 2; i += T) t4[i] = make_uint4(KQ_EMPTY, KQ_EMPTY, KQ_EMPTY, KQ_EMPTY);
-    if (t == 0) ctl[0] = 0;
   };
   clear();
   __syncthreads();
@@ -1590,17 +1583,13 @@ __global__ __launch_bounds__(T) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R
       if ((uint32_t)(k * T) + t >= sp.nr) continue;
       uint32_t e, v, tg;
       kqKey(rv[k], s, e, v, tg);
-      if (v == KQ_EMPTY) {  // escape: side list
-        const uint32_t at = atomicAdd(&ctl[0], 1u);
-        if (at < KQ_SIDE) side[at] = rv[k];
-        continue;
-      }
+      const uint32_t esc = v == KQ_EMPTY, vs = esc ? 0u : v;
       // <= 2048 distinct keys in 4096 entries: an empty entry is always reached
       for (uint32_t dist = 0;; ++dist) {
-        const uint32_t id = kqCountedId(dist, tg);
-        const unsigned long long o = atomicCAS(&tab64[e], ~0ull, ((unsigned long long)(id << 16) << 32) | v);
+        const uint32_t hi = (kqCountedId(dist, tg) << 16) | (esc << 15);
+        const unsigned long long o = atomicCAS(&tab64[e], ~0ull, ((unsigned long long)hi << 32) | vs);
         if (o == ~0ull) break;  // claimed with count - 1 = 0
-        if ((uint32_t)o == v && (uint32_t)(o >> 48) == id) {
+        if ((uint32_t)o == vs && ((uint32_t)(o >> 32) >> 15) == (hi >> 15)) {
           atomicAdd(&tab[2 * e + 1], 1u);
           break;
         }
@@ -1608,14 +1597,12 @@ __global__ __launch_bounds__(T) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R
       }
     }
     __syncthreads();
-    const uint32_t nSide = min(ctl[0], KQ_SIDE);
-    overflow |= ctl[0] > KQ_SIDE;
     // ---- probe the span's outer words
     for (uint32_t b0 = 0; b0 < sp.ns; b0 += BATCH) {
       const uint32_t ns = min(sp.ns - b0, BATCH);
       uint64_t xv[K];
       S.load(sp.sb + b0, ns, xv);
-      matches += kqProbeCounted<T, K>(xv, ns, s, tab2, side, nSide);
+      matches += kqProbeCounted<T, K>(xv, ns, s, tab2);
     }
     __syncthreads();
     clear();
@@ -1623,19 +1610,17 @@ __global__ __launch_bounds__(T) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R
   }
   const unsigned long long total = blockReduceSum<T, unsigned long long>((unsigned long long)matches, wsum);
   if (t == 0 && total) atomicAdd(result, total);
-  if (overflow && t == 0) atomicOr(flags, KQF_V2);
 }
 
 void bpKeyCountedSpans(const BPArgs &a, hipStream_t st) {
   constexpr int T = 512, K = 4;
-  HJ_CHECK(bpKeyCountedFits(a) && a.rChunk <= (uint32_t)(T * K) && a.heavySpans && a.heavyCount && a.sideOverflow,
+  HJ_CHECK(bpKeyCountedFits(a) && a.rChunk <= (uint32_t)(T * K) && a.heavySpans && a.heavyCount,
            "bpKeyCountedSpans: needs split key-only words of <= 48 fragment bits and the heavy span list");
   const uint32_t s = a.keyFragBits > 32 ? a.keyFragBits - 32 : 0;
-  const size_t lds = KQ_BUCKETS * 8 + KQ_SIDE * 8 + 16 + 16 * 8 + 16;
+  const size_t lds = KQ_BUCKETS * 8 + 16 * 8 + 16;
   const dim3 grid(std::min<uint32_t>(std::max<uint32_t>(a.heavyCapacity, 1), 256 * 4));
   hipLaunchKernelGGL((bpKeyCountedSpansKernel<T, K>), grid, dim3(T), lds, st, KsSrc<T, K, true>{a.R, a.Rhi},
-                     KsSrc<T, K, true>{a.S, a.Shi}, a.heavySpans, a.heavyCount, a.heavyCapacity, s, a.result,
-                     a.sideOverflow);
+                     KsSrc<T, K, true>{a.S, a.Shi}, a.heavySpans, a.heavyCount, a.heavyCapacity, s, a.result);
   HIP_CHECK_LAUNCH();
 }
 

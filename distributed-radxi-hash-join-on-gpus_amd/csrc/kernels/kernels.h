@@ -343,11 +343,10 @@ struct BPArgs {
   // unknown); the quotient-table kernel (keyCount 8) needs <= 44, the
   // counted-table kernel <= 48.
   uint32_t keyFragBits = 0;
-  // Flags of the quotient / counted kernels (build_probe.hip, KQF_*): bit 0
-  // a counted span had more escape keys than its side list holds (count void:
-  // re-run on keyCount 7); bit 1 a key's copies chained (count exact;
-  // keyCount 9 from then on); bit 3 a quotient span filled its overflow table
-  // (count void: re-run on counted tables).
+  // Flags of the quotient-table kernel (build_probe.hip, KQF_*): bit 1 a
+  // key's copies chained (count exact; keyCount 9 from then on); bit 3 a span
+  // filled its overflow table (count void: re-run on counted tables, which
+  // have no capacity limit).
   unsigned long long *sideOverflow = nullptr;
   // Optional (key-only spans with the quotient table): bpPlanCounts writes
   // the spans of partitions with more than rChunk inner tuples here (at most

@@ -267,14 +267,10 @@ void LocalPhase::run(JoinRun &run, JoinResult &r) {
       if (dev) HIP_CHECK(hipEventRecord(ev[4], ctx->stream()));
       ctx->synchronize();
     }
-  // Keys that defeat the quotient table's side list (many copies of an
-  // escape key) stay: later joins of this HashJoin start on the v2 table.
-  // Repeated inner keys chained in the quotient table: later joins count
-  // every partition on counted tables (keyCount 9).
-  for (auto &bp : bps) {
+  // Repeated inner keys chained in (or overflowed) the quotient table: later
+  // joins count every partition on counted tables (keyCount 9).
+  for (auto &bp : bps)
     if (bp->sawDuplicateChains() && env.plan.variants.keyCount == 8) env.plan.variants.keyCount = 9;
-    if (bp->quotientFellBack()) env.plan.variants.keyCount = 7;
-  }
   r.localMatches = 0;
   r.buildProbeItems = 0;
   for (auto &bp : bps) {

@@ -61,8 +61,7 @@ void BuildProbe::configure() {
   args.wide = plan.wide;
   args.keyOnly = plan.keyOnly;
   args.materialize = plan.materialize;
-  args.keyCount = plan.variants.keyCount;
-  if (plan.variants.keyCount >= 8) args.keyCount = quotientFallback ? 7 : (countedAll ? 9 : args.keyCount);
+  args.keyCount = plan.variants.keyCount >= 8 && countedAll ? 9 : plan.variants.keyCount;
   if (plan.keyOnly) {
     const uint32_t passBits = plan.networkBits + wi->getLocalBits();
     args.keyFragBits = plan.keyBits > passBits ? plan.keyBits - passBits : 1;
@@ -168,7 +167,7 @@ void BuildProbe::execute() {
     auto *spans = ws.getArray<kernels::BPSpan>(capacity);
     uint32_t *queue = ws.getArray<uint32_t>(1);
     kernels::bpEmitSpans(args, counts, offsets, spans, capacity, ctx->stream());
-    args.sideOverflow = counters + 3;  // quotient / counted table flags (kernels.h, BPArgs::sideOverflow)
+    args.sideOverflow = counters + 3;  // quotient table flags (kernels.h, BPArgs::sideOverflow)
     tl.beginSplit("BPKERNEL", "BPBUILD", wb, "BPPROBE", wp, ctx->stream());
     if (!counted || args.heavyMin != 0)  // otherwise every span is on the heavy list
       kernels::buildProbeKeySpans(args, spans, nItems, capacity, queue, ctx->stream());
@@ -236,10 +235,7 @@ bool BuildProbe::collect() {
   workItems = items + heavy;
   bool again = false;
   if (h[3] & 2) duplicateChains = true;  // exact count; later joins use counted tables throughout
-  if (args.sideOverflow && (h[3] & 1)) {  // too many escape keys in one counted span: count on the v2 table
-    quotientFallback = true;
-    again = true;
-  } else if (args.sideOverflow && (h[3] & 8)) {  // a quotient span's overflow table filled: counted tables
+  if (args.sideOverflow && (h[3] & 8)) {  // a quotient span's overflow table filled: count void, counted tables
     countedAll = duplicateChains = true;
     again = true;
   }

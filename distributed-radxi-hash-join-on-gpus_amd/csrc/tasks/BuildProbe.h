@@ -49,10 +49,8 @@ class BuildProbe : public Task {
   // rows to the sink.  A sink overflow is reported, not re-run (the caller
   // owns the buffer).
   void setRowSink(const kernels::RowSink *s) { sink = s; }
-  // A counted span overflowed its escape list and this task re-ran on the
-  // v2 table (collect() returned true for it).
-  bool quotientFellBack() const { return quotientFallback; }
-  // The quotient table chained copies of a key (repeated inner keys).
+  // The quotient table chained copies of a key (repeated inner keys), or a
+  // span filled its overflow table and this task re-ran on counted tables.
   bool sawDuplicateChains() const { return duplicateChains; }
   bool rowsFused() const { return fused; }
 
@@ -79,7 +77,6 @@ class BuildProbe : public Task {
   uint64_t matches = 0, outputCount = 0;
   uint32_t workItems = 0;
   bool reference = false, overflowOut = false, fused = false;
-  bool quotientFallback = false;  // a span overflowed the quotient table's side list: keyCount 7 from now on
   bool duplicateChains = false;   // copies of a key chained in the quotient table
   bool countedAll = false;        // a quotient span overflowed: this task counts every partition on counted tables
   const kernels::RowSink *sink = nullptr;

@@ -263,6 +263,8 @@ bool SampledShuffle::exchangeSide(int k) {
         const size_t at = (size_t)c * GF + i;
         const uint64_t fill = (s.narrow ? c32[at] : c64[at]) - s.start[at];
         over = over || fill > s.cap[at];
+        HJ_CHECK(fill <= 0xffffffffull, "sampled network pass: cell %zu holds %lu tuples (the fill all-gather packs u32)",
+                 at, (unsigned long)fill);
         sum += fill;
         mine[at / 2] |= std::min<uint64_t>(fill, 0xffffffffull) << (32 * (at & 1));
       }

@@ -409,17 +409,17 @@ def quotient_escape_fragments(n, first_bucket=0):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n_escape,dup,key_count,reruns",
-                         [(20, 1, 8, 0), (40, 3, 8, 0), (100, 1, 8, 0), (400, 1, 8, 2), (20, 1, 9, 0), (40, 3, 9, 1)])
+                         [(20, 1, 8, 0), (40, 3, 8, 0), (100, 1, 8, 0), (400, 1, 8, 1), (20, 1, 9, 0), (300, 3, 9, 0)])
 def test_key_quotient_escapes(C, n_escape, dup, key_count, reruns):
     """Quotient / counted build/probe with keys whose stored value is the
     table's empty marker, all in one final partition.  The quotient table
     (key_count 8) keeps them in its overflow table of full fragments (up to
-    384 per span); 400 fill it: the count is void, the build/probe re-runs on
-    counted tables, whose 64-entry escape list overflows too, and re-runs on
-    the v2 table (2 re-runs).  Counted tables (key_count 9) hold 64 escapes
-    per span; 40 keys x 3 copies re-run on v2.  Counts equal a torch oracle
-    every time; later joins of the same HashJoin start where the first ended
-    (no re-run)."""
+    384 per span); 400 fill it: the count is void and the build/probe re-runs
+    on counted tables (1 re-run), which hold escapes inline, as many as any
+    other key.  Repeated inner keys (dup 3) are seen at plan time: counted
+    tables from the first join.  Counts equal a torch oracle every time;
+    later joins of the same HashJoin start where the first ended (no
+    re-run)."""
     import torch
     from helpers import ref_join_count
     g = torch.Generator().manual_seed(n_escape * 7 + dup)

@@ -140,8 +140,14 @@ def run_config(C, info, ctx, comm, name, G_R, G_S, theta, cfg, steps, warmup):
         torch.cuda.synchronize()
 
     barrier()
+    t0 = time.perf_counter()
     join = C.HashJoin(R, S, ctx, cfg)
+    barrier()
+    setup_ms = (time.perf_counter() - t0) * 1e3
+    t0 = time.perf_counter()
     first = join.run()
+    barrier()
+    first_ms = (time.perf_counter() - t0) * 1e3
     for _ in range(max(0, warmup - 1)):
         join.run()
     ctx.reset_scratch()
@@ -153,20 +159,25 @@ def run_config(C, info, ctx, comm, name, G_R, G_S, theta, cfg, steps, warmup):
     barrier()
     mine_ms = (time.perf_counter() - t0) * 1e3 / steps
     per = [res[-1]["inner_received"], res[-1]["outer_received"], int(mine_ms * 1e3),
-           int(sum(r["join_ms"] for r in res) / len(res) * 1e3)]
+           int(sum(r["join_ms"] for r in res) / len(res) * 1e3), int(first_ms * 1e3), int(setup_ms * 1e3),
+           int(join.plan_ms * 1e3)]
+    K = len(per)
     allv = comm.all_gather(per) if info.world > 1 else per
-    recv = [allv[i] + allv[i + 1] for i in range(0, len(allv), 4)]
-    ms = max(allv[2::4]) / 1e3
+    recv = [allv[i] + allv[i + 1] for i in range(0, len(allv), K)]
+    ms = max(allv[2::K]) / 1e3
     mean = sum(recv) / len(recv)
     out = {
         "config": name, "n_gpus": info.world, "inner": G_R, "outer": G_S, "theta": theta,
         "ms_per_step": round(ms, 3), "value": round((G_R + G_S) / ms / 1e6, 3), "unit": "billion tuples/s",
+        "first_join_ms": max(allv[4::K]) / 1e3, "setup_ms": max(allv[5::K]) / 1e3, "plan_ms": max(allv[6::K]) / 1e3,
+        "first_over_steady": round(max(allv[4::K]) / 1e3 / ms, 3) if ms else None,
         "matches": res[-1]["global_matches"], "expected_matches": expected, "oracle": oracle_source,
         "correct": expected is not None and all(r["global_matches"] == expected for r in [first] + res),
         "plan": repr(join.plan), "assignment": str(cfg.assignment).split(".")[-1], "skew_split": cfg.skew_split,
         "split_partitions": res[-1]["split_partitions"],
         "received_per_rank": recv, "max_over_mean_received": round(max(recv) / mean, 4) if mean else None,
-        "join_ms_per_rank": [v / 1e3 for v in allv[3::4]],
+        "join_ms_per_rank": [v / 1e3 for v in allv[3::K]],
+        "first_reruns": first["reruns"], "first_local_fallbacks": first["local_fallbacks"],
         "local_fallbacks": sum(r["local_fallbacks"] for r in res), "network_fallbacks": sum(r["network_fallbacks"] for r in res),
         "reruns": res[-1]["reruns"],
         "phases_ms": {k: round(res[-1][k], 3) for k in ("dev_network_ms", "dev_local_partition_ms", "dev_build_probe_ms")},
