@@ -580,6 +580,7 @@ void placeRows(const uint64_t *rows, const uint64_t *idx, uint64_t n, uint64_t *
 // hipFuncGetAttributes per file loads them all up front.
 void preloadPartition();
 void preloadBuildProbe();
+void preloadKeyTables();
 void preloadBitmapJoin();
 void preloadScan();
 void preloadWire();
@@ -589,6 +590,7 @@ void preloadDatagen();
 inline void preloadCodeObjects() {
   preloadPartition();
   preloadBuildProbe();
+  preloadKeyTables();
   preloadBitmapJoin();
   preloadScan();
   preloadWire();

@@ -1,0 +1,669 @@
+// Key-only counting joins (JoinPlan::keyOnly: 63-bit keys, no rids) over
+// resolved spans of the split local output: the v2 bucket table, the
+// quotient table and counted tables.  Split out of build_probe.hip (the
+// rid-carrying build/probe kernels); reference semantics as there
+// (/root/reference/tasks/BuildProbe.cpp:81-106: exact key compare, every
+// copy counted).
+#include "kernels.h"
+#include "device_common.h"
+
+#include <algorithm>
+
+namespace hpcjoin {
+namespace kernels {
+
+constexpr int KT_EMIT_T = 256;
+
+// ---------------------------------------------------------------- key-only
+// Key-only 8-byte words (JoinPlan::keyOnly: wide keys, no rids) are counted
+// over resolved spans below: the v2 bucket table (keyCount 7), the quotient
+// table (8) and counted tables (9).  Round 2's per-item kernels (variants
+// 0-6) were pruned in round 4; measurements in profiles/r2v, profiles/r3k.
+constexpr uint32_t BPK_SLOTS = 4;
+
+// ------------------------------------------------------- key-only spans (v2)
+// The key-only count as a work queue of resolved spans.  Measured on the
+// item kernel above (1B x 1B sparse keys, 4.93 ms, 3.3 TB/s, 63 % wait):
+// every item started with a chain of dependent scalar loads (item -> four
+// partition bounds) and only then issued its data loads, so each workgroup
+// paid ~3 memory latencies per ~30 KB item.  Here
+//  * spans carry their resolved bounds (bpEmitSpans), 32 B each;
+//  * a workgroup grabs KS_CHUNK consecutive spans from a device counter
+//    (dynamic: hot partitions' spans spread over workgroups), stages their
+//    descriptors in LDS with one load, and walks them in order;
+//  * the next span's inner and outer words are loaded into registers while
+//    the current span probes, so its latency hides behind the LDS work;
+//  * loads are unpredicated (indices clamped into the span) and the bucket
+//    hash is one 32-bit multiply of the folded word (the 64-bit product of
+//    hash64 is three quarter-rate multiplies).
+// Table: the same 4-slot buckets + fill counters as bpKeyCountKernel.
+constexpr uint32_t KS_CHUNK = 32;
+
+__global__ __launch_bounds__(KT_EMIT_T) void bpEmitSpansKernel(const uint64_t *__restrict__ partR,
+                                                         const uint64_t *__restrict__ partREnd,
+                                                         const uint64_t *__restrict__ partS,
+                                                         const uint64_t *__restrict__ partSEnd, uint32_t P,
+                                                         uint32_t rc, uint32_t sc, const uint32_t *__restrict__ counts,
+                                                         const uint32_t *__restrict__ offsets, BPSpan *spans,
+                                                         uint32_t capacity) {
+  const uint32_t p = blockIdx.x * KT_EMIT_T + threadIdx.x;
+  if (p >= P) return;
+  const uint32_t c = counts[p];
+  if (c == 0) return;
+  const uint64_t r0 = partR[p], r1 = partREnd[p], s0 = partS[p], s1 = partSEnd[p];
+  const uint32_t nsChunks = (uint32_t)ceilDiv(s1 - s0, sc);
+  const uint32_t o = offsets[p];
+  for (uint32_t i = 0; i < c && o + i < capacity; ++i) {
+    const uint64_t rb = r0 + (uint64_t)(i / nsChunks) * rc, sb = s0 + (uint64_t)(i % nsChunks) * sc;
+    BPSpan sp;
+    sp.rb = rb;
+    sp.sb = sb;
+    sp.nr = (uint32_t)(min(r1, rb + rc) - rb);
+    sp.ns = (uint32_t)(min(s1, sb + sc) - sb);
+    sp.pad0 = sp.pad1 = 0;
+    spans[o + i] = sp;
+  }
+}
+
+void bpEmitSpans(const BPArgs &a, const uint32_t *counts, const uint32_t *offsets, BPSpan *spans, uint32_t capacity,
+                 hipStream_t s) {
+  if (a.P == 0) return;
+  hipLaunchKernelGGL(bpEmitSpansKernel, dim3(ceilDiv(a.P, KT_EMIT_T)), dim3(KT_EMIT_T), 0, s, a.partR,
+                     a.partREnd ? a.partREnd : a.partR + 1, a.partS, a.partSEnd ? a.partSEnd : a.partS + 1, a.P,
+                     a.rChunk, a.sChunk, counts, offsets, spans, capacity);
+  HIP_CHECK_LAUNCH();
+}
+
+// Bucket of a key-only word: fold the high half in with a 24-bit multiply
+// (full rate), one 32-bit multiplicative hash of the result.  Within a final
+// partition the word's low localBits bits are equal: they only offset the
+// product, whose top bits still come from the varying bits above them.
+__device__ __forceinline__ uint32_t ksBucket(uint64_t w, uint32_t bbits) {
+  const uint32_t x = (uint32_t)w ^ __umul24((uint32_t)(w >> 32), 0x2C1B3Cu);
+  return (x * 0x9E3779B1u) >> (32 - bbits);
+}
+
+// K words of a span per lane (indices clamped into the span: no predication).
+// Split layout (SplitLayout::loShift = localBits): the u32 low column and the
+// u16 high column compose the key fragment lo | hi << 32.
+template <int T, int K, bool SPLIT>
+struct KsSrc {
+  const void *lo;
+  const uint16_t *hi;
+  __device__ __forceinline__ void load(uint64_t base, uint32_t n, uint64_t (&v)[K]) const {
+    const uint32_t last = n ? n - 1 : 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint64_t i = base + min((uint32_t)(k * T) + threadIdx.x, last);
+      if constexpr (SPLIT)
+        v[k] = (uint64_t)__builtin_nontemporal_load(static_cast<const uint32_t *>(lo) + i) |
+               ((uint64_t)__builtin_nontemporal_load(hi + i) << 32);
+      else
+        v[k] = __builtin_nontemporal_load(static_cast<const uint64_t *>(lo) + i);
+    }
+  }
+};
+
+// The bucket table: 4 slots (32 B) per bucket, stored SoA: all first 16-byte
+// halves, then all second halves, so a random ds_read_b128 starts at one of
+// 16 bank quads instead of 8 (32-byte AoS buckets, round 3's variant 6):
+// half the expected lane collisions per 16-lane group.
+struct KsTable {
+  unsigned long long *t;
+  uint32_t maxBuckets;
+  __device__ __forceinline__ const ulonglong2 *half(uint32_t b, int h) const {
+    return reinterpret_cast<const ulonglong2 *>(t + (h ? 2 * maxBuckets : 0)) + b;
+  }
+  __device__ __forceinline__ unsigned long long &slot(uint32_t b, uint32_t p) const {
+    return t[(p >> 1) * 2 * maxBuckets + 2 * b + (p & 1)];
+  }
+};
+
+// One batch of T x K outer words (the first `valid` of them counted) against
+// the bucketized table; returns this lane's matches.
+template <int T, int K, int H>
+__device__ __forceinline__ uint32_t ksProbeBatch(const uint64_t (&sv)[K], uint32_t valid, const KsTable &table,
+                                                 const uint32_t *fill, uint32_t bbits, uint32_t bmask) {
+  uint32_t matches = 0;
+#pragma unroll
+  for (int h = 0; h < K / H; ++h) {
+    uint32_t bk[H], f[H];
+    ulonglong2 e0[H], e1[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      bk[j] = ksBucket(sv[h * H + j], bbits);
+      f[j] = fill[bk[j]];
+      e0[j] = *table.half(bk[j], 0);
+      e1[j] = *table.half(bk[j], 1);
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      const int k = h * H + j;
+      const uint64_t v = sv[k];
+      const uint32_t m = f[j];  // slots in use (> 4: passed through)
+      // Non-short-circuit tests: the whole 32-byte bucket is read up front.
+      uint32_t c = (uint32_t)((m > 0) & (e0[j].x == v)) + (uint32_t)((m > 1) & (e0[j].y == v)) +
+                   (uint32_t)((m > 2) & (e1[j].x == v)) + (uint32_t)((m > 3) & (e1[j].y == v));
+      // Elements passed through (~4 % of buckets at load 1/2, so most waves
+      // have a lane here): continue bucket by bucket, each step one round
+      // trip (counter and both halves of the bucket read together).
+      uint32_t b = bk[j], fb = m;
+      while (fb > BPK_SLOTS) {
+        b = (b + 1) & bmask;
+        fb = fill[b];
+        const ulonglong2 x0 = *table.half(b, 0), x1 = *table.half(b, 1);
+        c += (uint32_t)((fb > 0) & (x0.x == v)) + (uint32_t)((fb > 1) & (x0.y == v)) +
+             (uint32_t)((fb > 2) & (x1.x == v)) + (uint32_t)((fb > 3) & (x1.y == v));
+      }
+      matches += (uint32_t)(k * T) + threadIdx.x < valid ? c : 0u;
+    }
+  }
+  return matches;
+}
+
+template <int T, int K, int H, int MINW, bool SPLIT>
+__global__ __launch_bounds__(T, MINW) void bpKeySpanKernel(KsSrc<T, K, SPLIT> R, KsSrc<T, K, SPLIT> S,
+                                                           const BPSpan *__restrict__ spans,
+                                                           const uint32_t *__restrict__ nSpansPtr, uint32_t capacity,
+                                                           uint32_t *__restrict__ queue, uint32_t maxR,
+                                                           unsigned long long *__restrict__ result) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t maxSlots = 1u << ceilLog2(2ull * maxR);
+  const KsTable table{reinterpret_cast<unsigned long long *>(smem), maxSlots / BPK_SLOTS};
+  uint32_t *fill = reinterpret_cast<uint32_t *>(table.t + maxSlots);
+  BPSpan *desc = reinterpret_cast<BPSpan *>(fill + maxSlots / BPK_SLOTS);
+  unsigned long long *wsum = reinterpret_cast<unsigned long long *>(desc + KS_CHUNK);
+  uint32_t *qbase = reinterpret_cast<uint32_t *>(wsum + T / WAVE);
+  constexpr uint32_t BATCH = T * K;
+  const uint32_t t = threadIdx.x;
+  const uint32_t n = min(*nSpansPtr, capacity);
+  uint64_t matches = 0;
+  uint64_t rv[K], sv[K], nrv[K], nsv[K];
+  for (;;) {
+    if (t == 0) *qbase = atomicAdd(queue, KS_CHUNK);
+    __syncthreads();
+    const uint32_t base = __builtin_amdgcn_readfirstlane(*qbase);
+    if (base >= n) break;
+    const uint32_t cnt = min(KS_CHUNK, n - base);
+    if (t < cnt) desc[t] = spans[base + t];
+    __syncthreads();
+    {
+      const BPSpan d = desc[0];
+      R.load(d.rb, d.nr, rv);
+      S.load(d.sb, d.ns, sv);
+    }
+    for (uint32_t i = 0; i < cnt; ++i) {
+      const uint64_t rb = uniform64(desc[i].rb);
+      const uint64_t sb = uniform64(desc[i].sb);
+      const uint32_t nr = __builtin_amdgcn_readfirstlane(desc[i].nr);
+      const uint32_t ns = __builtin_amdgcn_readfirstlane(desc[i].ns);
+      uint32_t tbits = nr > 1 ? 32 - __clz(2 * nr - 1) : 1;
+      if (tbits < 6) tbits = 6;
+      const uint32_t bbits = tbits - 2, bmask = (1u << bbits) - 1;
+      for (uint32_t j = t; j <= bmask; j += T) fill[j] = 0;
+      __syncthreads();
+      // ---- build (nr <= maxR <= BATCH: one batch, from registers)
+      {
+        uint32_t bk[K], pos[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const bool valid = (uint32_t)(k * T) + t < nr;
+          bk[k] = ksBucket(rv[k], bbits);
+          pos[k] = atomicAdd(&fill[bk[k]], valid ? 1u : 0u);
+          pos[k] = valid ? pos[k] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          if (pos[k] == 0xFFFFFFFFu) continue;
+          uint32_t b = bk[k], p = pos[k];
+          while (p >= BPK_SLOTS) {  // home bucket full: the next one (its counter marks the pass)
+            b = (b + 1) & bmask;
+            p = atomicAdd(&fill[b], 1u);
+          }
+          table.slot(b, p) = rv[k];
+        }
+      }
+      __syncthreads();
+      // ---- the next span's words stream in while this one probes
+      if (i + 1 < cnt) {
+        const BPSpan d = desc[i + 1];
+        R.load(d.rb, d.nr, nrv);
+        S.load(d.sb, d.ns, nsv);
+      }
+      // ---- probe: the first batch from registers (no wait on the prefetch
+      // above: vmcnt is in order, so a load issued here would make the first
+      // use wait for the next span's words too), later batches loaded inline.
+      matches += ksProbeBatch<T, K, H>(sv, ns, table, fill, bbits, bmask);
+      for (uint32_t b0 = BATCH; b0 < ns; b0 += BATCH) {
+        uint64_t xv[K];
+        S.load(sb + b0, ns - b0, xv);
+        matches += ksProbeBatch<T, K, H>(xv, ns - b0, table, fill, bbits, bmask);
+      }
+      __syncthreads();  // the next span clears the counters
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        rv[k] = nrv[k];
+        sv[k] = nsv[k];
+      }
+    }
+  }
+  const unsigned long long total = blockReduceSum<T, unsigned long long>((unsigned long long)matches, wsum);
+  if (t == 0 && total) atomicAdd(result, total);
+}
+
+// ------------------------------------------- key-only spans, quotient table (v3)
+// KernelVariants::keyCount 8.  The v2 table above spends its LDS cycles on
+// 8-byte keys: a probe is a fill-counter read plus two random ds_read_b128
+// (33 LDS cycles per wave with the measured 3.0-3.6 conflict cycles per
+// instruction; PMC: the LDS pipe ~80 % busy, the kernel at 3.7 TB/s).  Here a
+// key fragment of f <= 32 + KQ_BITS bits (63-bit keys after 10 + 9 radix bits:
+// f = 44) is split into
+//   e = frag >> s (32 bits, s = f - 32)   and   lo = frag's low s bits;
+//   bucket b = (lo ^ h(e)) mod 2^KQ_BITS   (h: multiplicative hash of e),
+// and the bucket stores only v = e ^ salt(b): (b, v) determines the fragment
+// (lo = b ^ h(e) on its low s bits), so a slot is 4 bytes.  Buckets are two
+// u32 slots = one 8-byte ds_read_b64 per probe; 4096 buckets (32 KiB) hold
+// <= 2048 inner keys at load <= 1/4.
+//
+// Exactness: (b, v) names a key only in ITS OWN bucket b.  A key therefore
+// never leaves its home bucket in the quotient table: the third and later
+// keys of a bucket, and "escape" keys whose v equals the empty marker (one
+// fragment per bucket), go to a small overflow table of full 48-bit
+// fragments (KQ_OV entries, linear probing, compared whole).  Slots fill in
+// order (slot 0, slot 1, overflow), so a probe whose home bucket has an empty
+// slot 1 has seen every copy of its key; a full home bucket (~9 % of probes
+// at 2048 keys) adds one overflow lookup, the read that used to walk into
+// the next bucket.  (Round 3 let keys spill into the next bucket, where a
+// stored v of another home could equal the probe's: a 2^-32 false match per
+// foreign comparison.)  More than KQ_OV_CAP overflow keys in one span -- a
+// key with hundreds of copies in a light partition -- stops inserting and
+// sets KQF_COUNTED: the count is void and the join's build/probe re-runs on
+// counted tables.  The lanes that built a span reset their own slots after
+// its probe: no table clear.
+constexpr uint32_t KQ_BITS = 12;
+constexpr uint32_t KQ_BUCKETS = 1u << KQ_BITS;
+constexpr uint32_t KQ_EMPTY = 0xFFFFFFFFu;
+constexpr uint32_t KQ_OV_BITS = 9;
+constexpr uint32_t KQ_OV = 1u << KQ_OV_BITS;  // overflow entries (4 KiB)
+constexpr uint32_t KQ_OV_CAP = 3 * KQ_OV / 4;  // at most this many inserted: probes always find an empty entry
+constexpr unsigned long long KQ_OV_EMPTY = ~0ull;  // fragments are < 2^48
+constexpr uint32_t KQ_OV_FLAG = 0x80000000u;       // pos[]: overflow-table index
+constexpr uint32_t KQ_NONE = 0xFFFFFFFFu;
+// A placement that walked past this many overflow entries saw one key's
+// copies chained (unique keys at <= 25 % overflow load never do): KQF_CHAINS,
+// and later joins put every partition on counted spans (keyCount 9).
+constexpr uint32_t KQ_LONG_CHAIN = 64;
+// BPArgs::sideOverflow bits.
+constexpr unsigned long long KQF_CHAINS = 2;   // copies of a key chained (count exact)
+constexpr unsigned long long KQF_COUNTED = 8;  // quotient overflow table full: count void, re-run counted
+
+__device__ __forceinline__ uint32_t kqSalt(uint32_t b) { return (b + 1u) * 0x85EBCA77u; }
+
+// (bucket, stored value, tag) of a fragment of f <= 48 bits; s = f - 32
+// (0 when f <= 32).  The bucket absorbs the low KQ_BITS of lo, the tag holds
+// the rest of lo (f > 44 only: counted tables keep it next to the count).
+__device__ __forceinline__ void kqKey(uint64_t frag, uint32_t s, uint32_t &b, uint32_t &v, uint32_t &tag) {
+  const uint32_t e = (uint32_t)(frag >> s);
+  const uint32_t lo = (uint32_t)frag & ((1u << s) - 1u);
+  b = (lo ^ ((e * 0x9E3779B1u) >> (32 - KQ_BITS))) & (KQ_BUCKETS - 1);
+  tag = lo >> KQ_BITS;
+  v = e ^ kqSalt(b);
+}
+
+// Overflow-table home of a key from its (bucket, stored value): (b, v) is a
+// bijection of the fragment, so one 32-bit multiply spreads keys as well as
+// hashing the whole fragment would.
+__device__ __forceinline__ uint32_t kqOvHash(uint32_t b, uint32_t v) {
+  return ((v ^ (b << 20)) * 0x9E3779B1u) >> (32 - KQ_OV_BITS);
+}
+
+// Copies of `frag` (home h) in the overflow table (it holds < KQ_OV entries).
+__device__ __forceinline__ uint32_t kqOvCount(const unsigned long long *ov, uint32_t h, uint64_t frag) {
+  uint32_t c = 0;
+  for (uint32_t w = 0; w < KQ_OV; ++w) {
+    const unsigned long long y = ov[h];
+    if (y == KQ_OV_EMPTY) break;
+    c += y == frag;
+    h = (h + 1) & (KQ_OV - 1);
+  }
+  return c;
+}
+
+// Overflow placement: the entry index | KQ_OV_FLAG, or KQ_NONE when the table
+// is at its cap (full = true: the span's count is void).
+__device__ __forceinline__ uint32_t kqOvInsert(unsigned long long *ov, uint32_t *ovN, uint32_t h, uint64_t frag,
+                                               bool &chained, bool &full) {
+  if (atomicAdd(ovN, 1u) >= KQ_OV_CAP) {
+    full = true;
+    return KQ_NONE;
+  }
+  for (uint32_t w = 0;; ++w) {  // < KQ_OV_CAP entries taken: an empty one exists
+    if (atomicCAS(&ov[h], KQ_OV_EMPTY, (unsigned long long)frag) == KQ_OV_EMPTY) {
+      chained |= w > KQ_LONG_CHAIN;
+      return KQ_OV_FLAG | h;
+    }
+    h = (h + 1) & (KQ_OV - 1);
+  }
+}
+
+// One batch of T x K outer fragments (the first `valid` counted): all K
+// bucket reads in flight, then the overflow lookups of full home buckets.
+template <int T, int K>
+__device__ __forceinline__ uint32_t kqProbeBatch(const uint64_t (&pv)[K], uint32_t valid, uint32_t s,
+                                                 const uint2 *tab2, const unsigned long long *ov) {
+  uint32_t bk[K], v[K], tg[K];
+  uint2 x[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    kqKey(pv[k], s, bk[k], v[k], tg[k]);
+    x[k] = tab2[bk[k]];
+  }
+  uint32_t matches = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const bool esc = v[k] == KQ_EMPTY;  // only in the overflow table
+    uint32_t c = esc ? 0u : (uint32_t)(x[k].x == v[k]) + (uint32_t)(x[k].y == v[k]);
+    if (x[k].y != KQ_EMPTY || esc) c += kqOvCount(ov, kqOvHash(bk[k], v[k]), pv[k]);
+    matches += (uint32_t)(k * T) + threadIdx.x < valid ? c : 0u;
+  }
+  return matches;
+}
+
+// Counted table (bpKeyCountedSpansKernel): entry e = one distinct key,
+//   slot 0 = stored value, slot 1 = id << 16 | esc << 15 | (count - 1),
+//   id = dist << 4 | tag,  dist = e - home bucket (linear probing).
+// (stored value, id, esc) at entry e names exactly one fragment, so a probe
+// never matches a key of another home.  Escape keys (v = the empty marker)
+// are stored inline with esc = 1 and stored value 0: e = ~salt(b) is implied
+// by the home bucket, so (home, tag) names them.  Claimed by one 64-bit CAS
+// of (value, id, esc, 0) on an empty entry; a copy finding its own triple
+// adds 1 to slot 1 (counts <= 2048 per span stay below bit 15).
+__device__ __forceinline__ uint32_t kqCountedId(uint32_t dist, uint32_t tag) { return (dist << 4) | tag; }
+
+template <int T, int K>
+__device__ __forceinline__ uint32_t kqProbeCounted(const uint64_t (&pv)[K], uint32_t valid, uint32_t s,
+                                                   const uint2 *tab2) {
+  uint32_t bk[K], v[K], tg[K];
+  uint2 x[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    kqKey(pv[k], s, bk[k], v[k], tg[k]);
+    x[k] = tab2[bk[k]];
+  }
+  uint32_t matches = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const uint32_t esc = v[k] == KQ_EMPTY, vs = esc ? 0u : v[k];
+    uint32_t c = 0, e = bk[k];
+    uint2 y = x[k];
+    for (uint32_t dist = 0; dist < KQ_BUCKETS; ++dist) {
+      if (y.x == vs && (y.y >> 15) == ((kqCountedId(dist, tg[k]) << 1) | esc)) {
+        c = (y.y & 0x7FFFu) + 1;
+        break;
+      }
+      if (y.x == KQ_EMPTY) break;
+      e = (e + 1) & (KQ_BUCKETS - 1);
+      y = tab2[e];
+    }
+    matches += (uint32_t)(k * T) + threadIdx.x < valid ? c : 0u;
+  }
+  return matches;
+}
+
+size_t bpKeyQuotientLdsBytes() {
+  return KQ_BUCKETS * 8 + KQ_OV * 8 + 16 + KS_CHUNK * sizeof(BPSpan) + 16 * 8 + 16;
+}
+
+template <int T, int K, int MINW>
+__global__ __launch_bounds__(T, MINW) void bpKeyQuotientKernel(KsSrc<T, K, true> R, KsSrc<T, K, true> S,
+                                                               const BPSpan *__restrict__ spans,
+                                                               const uint32_t *__restrict__ nSpansPtr,
+                                                               uint32_t capacity, uint32_t *__restrict__ queue,
+                                                               uint32_t s, unsigned long long *__restrict__ result,
+                                                               unsigned long long *__restrict__ flags) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t *tab = reinterpret_cast<uint32_t *>(smem);  // [bucket][2]
+  const uint2 *tab2 = reinterpret_cast<const uint2 *>(smem);
+  unsigned long long *ov = reinterpret_cast<unsigned long long *>(tab + 2 * KQ_BUCKETS);
+  uint32_t *ovN = reinterpret_cast<uint32_t *>(ov + KQ_OV);
+  BPSpan *desc = reinterpret_cast<BPSpan *>(ovN + 4);
+  unsigned long long *wsum = reinterpret_cast<unsigned long long *>(desc + KS_CHUNK);
+  uint32_t *qbase = reinterpret_cast<uint32_t *>(wsum + T / WAVE);
+  constexpr uint32_t BATCH = T * K;
+  const uint32_t t = threadIdx.x;
+  const uint32_t n = min(*nSpansPtr, capacity);
+  {
+    uint4 *t4 = reinterpret_cast<uint4 *>(tab);  // main table and overflow table are adjacent
+    for (uint32_t i = t; i < (KQ_BUCKETS * 8 + KQ_OV * 8) / 16; i += T)
+      t4[i] = make_uint4(KQ_EMPTY, KQ_EMPTY, KQ_EMPTY, KQ_EMPTY);
+    if (t == 0) *ovN = 0;
+  }
+  uint64_t matches = 0;
+  bool full = false, chained = false;
+  uint64_t rv[K], sv[K], nrv[K], nsv[K];
+  for (;;) {
+    if (t == 0) *qbase = atomicAdd(queue, KS_CHUNK);
+    __syncthreads();  // (first round: also orders the table clear before any build)
+    const uint32_t base = __builtin_amdgcn_readfirstlane(*qbase);
+    if (base >= n) break;
+    const uint32_t cnt = min(KS_CHUNK, n - base);
+    if (t < cnt) desc[t] = spans[base + t];
+    __syncthreads();
+    {
+      const BPSpan d = desc[0];
+      R.load(d.rb, d.nr, rv);
+      S.load(d.sb, d.ns, sv);
+    }
+    for (uint32_t i = 0; i < cnt; ++i) {
+      const uint64_t sb = uniform64(desc[i].sb);
+      const uint32_t nr = __builtin_amdgcn_readfirstlane(desc[i].nr);
+      const uint32_t ns = __builtin_amdgcn_readfirstlane(desc[i].ns);
+      // ---- build (nr <= BATCH: one batch, from registers): slot 0, slot 1, overflow
+      uint32_t pos[K];
+      {
+        uint32_t bk[K], v[K], tg[K], old[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          kqKey(rv[k], s, bk[k], v[k], tg[k]);
+          const bool valid = (uint32_t)(k * T) + t < nr;
+          pos[k] = !valid ? KQ_NONE : (v[k] == KQ_EMPTY ? KQ_OV_FLAG : 2 * bk[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) old[k] = pos[k] < KQ_OV_FLAG ? atomicCAS(&tab[pos[k]], KQ_EMPTY, v[k]) : KQ_EMPTY;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          if (pos[k] >= KQ_OV_FLAG || old[k] == KQ_EMPTY) continue;  // placed in slot 0 (or not a main-table key)
+          pos[k] = atomicCAS(&tab[pos[k] + 1], KQ_EMPTY, v[k]) == KQ_EMPTY ? pos[k] + 1 : KQ_OV_FLAG;
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+          if (pos[k] == KQ_OV_FLAG) pos[k] = kqOvInsert(ov, ovN, kqOvHash(bk[k], v[k]), rv[k], chained, full);
+      }
+      __syncthreads();
+      // ---- the next span's words stream in while this one probes
+      if (i + 1 < cnt) {
+        const BPSpan d = desc[i + 1];
+        R.load(d.rb, d.nr, nrv);
+        S.load(d.sb, d.ns, nsv);
+      }
+      // ---- probe: first batch from registers, later batches loaded inline
+      matches += kqProbeBatch<T, K>(sv, ns, s, tab2, ov);
+      for (uint32_t b0 = BATCH; b0 < ns; b0 += BATCH) {
+        uint64_t xv[K];
+        S.load(sb + b0, ns - b0, xv);
+        matches += kqProbeBatch<T, K>(xv, ns - b0, s, tab2, ov);
+      }
+      __syncthreads();  // every probe of this span is done
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        if (pos[k] == KQ_NONE) continue;
+        if (pos[k] & KQ_OV_FLAG)
+          ov[pos[k] & ~KQ_OV_FLAG] = KQ_OV_EMPTY;
+        else
+          tab[pos[k]] = KQ_EMPTY;
+      }
+      if (t == 0) *ovN = 0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        rv[k] = nrv[k];
+        sv[k] = nsv[k];
+      }
+      __syncthreads();  // table empty again before the next build
+    }
+  }
+  const unsigned long long total = blockReduceSum<T, unsigned long long>((unsigned long long)matches, wsum);
+  if (t == 0 && total) atomicAdd(result, total);
+  if (__any(full) && (t & (WAVE - 1)) == 0) atomicOr(flags, KQF_COUNTED);
+  if (__any(chained) && (t & (WAVE - 1)) == 0) atomicOr(flags, KQF_CHAINS);
+}
+
+bool bpKeyQuotientFits(const BPArgs &a) {
+  return bpKeyCountedFits(a) && a.keyFragBits <= 32 + KQ_BITS;
+}
+
+bool bpKeyCountedFits(const BPArgs &a) {
+  return a.keyOnly && a.split && !a.materialize && !a.wide && a.keyFragBits >= 1 && a.keyFragBits <= 48 &&
+         a.rChunk <= 2048;
+}
+
+static void launchKeyQuotient(const BPArgs &a, const BPSpan *spans, const uint32_t *nSpans, uint32_t capacity,
+                              uint32_t *queue, hipStream_t st) {
+  constexpr int T = 512, K = 4;
+  HJ_CHECK(bpKeyQuotientFits(a), "buildProbeKeySpans: quotient table needs split key-only words of <= %u bits "
+           "(got %u) and rChunk <= 2048 (got %u)", 32 + KQ_BITS, a.keyFragBits, a.rChunk);
+  HJ_CHECK(a.sideOverflow, "buildProbeKeySpans: quotient table needs a flag word");
+  const uint32_t s = a.keyFragBits > 32 ? a.keyFragBits - 32 : 0;
+  const size_t lds = bpKeyQuotientLdsBytes();
+  const uint32_t perCu = (uint32_t)std::max<size_t>(1, std::min<size_t>(4, (160 * 1024) / lds));
+  const dim3 grid(std::min<uint32_t>(ceilDiv(capacity, KS_CHUNK), 256 * perCu));
+  HIP_CHECK(hipMemsetAsync(queue, 0, sizeof(uint32_t), st));
+  hipLaunchKernelGGL((bpKeyQuotientKernel<T, K, 8>), grid, dim3(T), lds, st, KsSrc<T, K, true>{a.R, a.Rhi},
+                     KsSrc<T, K, true>{a.S, a.Shi}, spans, nSpans, capacity, queue, s, a.result, a.sideOverflow);
+  HIP_CHECK_LAUNCH();
+}
+
+// ------------------------------------- key-only: partitions with repeated keys
+// Partitions with more than rChunk inner tuples (with unique keys a few in a
+// thousand, just above the mean; with repeated keys the hot ones) skip the
+// span work queue, whose one-slot-per-tuple quotient table holds every copy
+// of a key.  Their spans (bpPlanCounts -> heavySpans, same rChunk x sChunk
+// tiling) are counted here on a *counted* table over the same 32 KiB (see
+// kqProbeCounted): one entry per distinct key, so copies only add to a count.
+// A span's <= 2048 inner tuples fill at most half of the 4096 entries.  This
+// table also carries 45-48-bit fragments (the tag next to the count) and
+// escape keys inline, so it never needs a fallback: plans whose fragments the
+// quotient table cannot hold, and quotient spans that filled their overflow
+// table, count here.  A hot partition's spans spread over workgroups like any
+// others.
+template <int T, int K>
+__global__ __launch_bounds__(T) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R, KsSrc<T, K, true> S,
+                                                              const BPSpan *__restrict__ spans,
+                                                              const uint32_t *__restrict__ nSpansPtr, uint32_t capacity,
+                                                              uint32_t s, unsigned long long *__restrict__ result) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t *tab = reinterpret_cast<uint32_t *>(smem);  // [entry][value, id << 16 | esc << 15 | count - 1]
+  unsigned long long *tab64 = reinterpret_cast<unsigned long long *>(smem);
+  const uint2 *tab2 = reinterpret_cast<const uint2 *>(smem);
+  unsigned long long *wsum = reinterpret_cast<unsigned long long *>(tab + 2 * KQ_BUCKETS);
+  constexpr uint32_t BATCH = T * K;
+  const uint32_t t = threadIdx.x;
+  const uint32_t n = min(*nSpansPtr, capacity);
+  uint64_t matches = 0;
+  auto clear = [&]() {
+    uint4 *t4 = reinterpret_cast<uint4 *>(tab);
+    for (uint32_t i = t; i < KQ_BUCKETS / 2; i += T) t4[i] = make_uint4(KQ_EMPTY, KQ_EMPTY, KQ_EMPTY, KQ_EMPTY);
+  };
+  clear();
+  __syncthreads();
+  for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
+    const BPSpan sp = spans[w];
+    // ---- build: nr <= rChunk <= BATCH, one pass
+    uint64_t rv[K];
+    R.load(sp.rb, sp.nr, rv);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if ((uint32_t)(k * T) + t >= sp.nr) continue;
+      uint32_t e, v, tg;
+      kqKey(rv[k], s, e, v, tg);
+      const uint32_t esc = v == KQ_EMPTY, vs = esc ? 0u : v;
+      // <= 2048 distinct keys in 4096 entries: an empty entry is always reached
+      for (uint32_t dist = 0;; ++dist) {
+        const uint32_t hi = (kqCountedId(dist, tg) << 16) | (esc << 15);
+        const unsigned long long o = atomicCAS(&tab64[e], ~0ull, ((unsigned long long)hi << 32) | vs);
+        if (o == ~0ull) break;  // claimed with count - 1 = 0
+        if ((uint32_t)o == vs && ((uint32_t)(o >> 32) >> 15) == (hi >> 15)) {
+          atomicAdd(&tab[2 * e + 1], 1u);
+          break;
+        }
+        e = (e + 1) & (KQ_BUCKETS - 1);
+      }
+    }
+    __syncthreads();
+    // ---- probe the span's outer words
+    for (uint32_t b0 = 0; b0 < sp.ns; b0 += BATCH) {
+      const uint32_t ns = min(sp.ns - b0, BATCH);
+      uint64_t xv[K];
+      S.load(sp.sb + b0, ns, xv);
+      matches += kqProbeCounted<T, K>(xv, ns, s, tab2);
+    }
+    __syncthreads();
+    clear();
+    __syncthreads();
+  }
+  const unsigned long long total = blockReduceSum<T, unsigned long long>((unsigned long long)matches, wsum);
+  if (t == 0 && total) atomicAdd(result, total);
+}
+
+void bpKeyCountedSpans(const BPArgs &a, hipStream_t st) {
+  constexpr int T = 512, K = 4;
+  HJ_CHECK(bpKeyCountedFits(a) && a.rChunk <= (uint32_t)(T * K) && a.heavySpans && a.heavyCount,
+           "bpKeyCountedSpans: needs split key-only words of <= 48 fragment bits and the heavy span list");
+  const uint32_t s = a.keyFragBits > 32 ? a.keyFragBits - 32 : 0;
+  const size_t lds = KQ_BUCKETS * 8 + 16 * 8 + 16;
+  const dim3 grid(std::min<uint32_t>(std::max<uint32_t>(a.heavyCapacity, 1), 256 * 4));
+  hipLaunchKernelGGL((bpKeyCountedSpansKernel<T, K>), grid, dim3(T), lds, st, KsSrc<T, K, true>{a.R, a.Rhi},
+                     KsSrc<T, K, true>{a.S, a.Shi}, a.heavySpans, a.heavyCount, a.heavyCapacity, s, a.result);
+  HIP_CHECK_LAUNCH();
+}
+
+size_t bpKeySpanLdsBytes(uint32_t maxR) {
+  const uint64_t slots = uint64_t(1) << ceilLog2(2ull * maxR);
+  return slots * 8 + (slots / BPK_SLOTS) * 4 + KS_CHUNK * sizeof(BPSpan) + 16 * 8 + 16;
+}
+
+void buildProbeKeySpans(const BPArgs &a, const BPSpan *spans, const uint32_t *nSpans, uint32_t capacity,
+                        uint32_t *queue, hipStream_t s) {
+  if (capacity == 0) return;
+  constexpr int T = 512, K = 4, H = 2;
+  HJ_CHECK(a.keyOnly && !a.materialize && !a.wide, "buildProbeKeySpans: key-only counting joins only");
+  HJ_CHECK(!a.split || (a.Rhi && a.Shi), "buildProbeKeySpans: split layout without high columns");
+  HJ_CHECK(a.rChunk <= (uint32_t)(T * K), "buildProbeKeySpans: rChunk %u above one %d-word batch", a.rChunk, T * K);
+  if ((a.keyCount == 8 || a.keyCount == 9) && bpKeyQuotientFits(a)) {
+    launchKeyQuotient(a, spans, nSpans, capacity, queue, s);
+    return;
+  }
+  const size_t lds = bpKeySpanLdsBytes(a.rChunk);
+  HJ_CHECK(lds <= 160 * 1024, "buildProbeKeySpans: LDS %zu B exceeds 160 KiB (rChunk=%u)", lds, a.rChunk);
+  const uint32_t perCu = (uint32_t)std::max<size_t>(1, std::min<size_t>(4, (160 * 1024) / lds));
+  const dim3 grid(std::min<uint32_t>(ceilDiv(capacity, KS_CHUNK), 256 * perCu));
+  HIP_CHECK(hipMemsetAsync(queue, 0, sizeof(uint32_t), s));
+#define HJ_KS(SPLIT)                                                                                             \
+  hipLaunchKernelGGL((bpKeySpanKernel<T, K, H, 8, SPLIT>), grid, dim3(T), lds, s,                                 \
+                     KsSrc<T, K, SPLIT>{a.R, SPLIT ? a.Rhi : nullptr}, KsSrc<T, K, SPLIT>{a.S, SPLIT ? a.Shi : nullptr}, \
+                     spans, nSpans, capacity, queue, a.rChunk, a.result)
+  if (a.split)
+    HJ_KS(true);
+  else
+    HJ_KS(false);
+#undef HJ_KS
+  HIP_CHECK_LAUNCH();
+}
+
+// Loads this file's code object at engine start (kernels::preloadCodeObjects).
+void preloadKeyTables() {
+  hipFuncAttributes a;
+  HIP_CHECK(hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&bpEmitSpansKernel)));
+}
+
+}  // namespace kernels
+}  // namespace hpcjoin
