@@ -1213,7 +1213,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         need(b, rb, "b");
         need(oa, wa, "oa");
         need(ob, wb, "ob");
-        HJ_CHECK(n % 8 == 0, "stream_mix: n must be a multiple of 8");
+        HJ_CHECK(n % 512 == 0, "stream_mix: n must be a multiple of 512");
         kernels::streamMix(ra, rb, wa, wb, a.data_ptr(), b.data_ptr(), oa.data_ptr(), ob.data_ptr(), n,
                            reinterpret_cast<unsigned long long *>(sink.data_ptr()), nullptr);
       },

@@ -33,23 +33,27 @@ __global__ __launch_bounds__(256) void readKernelImpl(const ulonglong2 *__restri
 // so every stream is read / written with the widest access whatever its
 // element size; written words are XORs of read words (nothing folds away).
 using mixv = unsigned int __attribute__((ext_vector_type(4)));
+// A wave moves 512 elements per step: stream A's 512 x RA bytes are LA x 64
+// 16-byte vectors, vector k * 64 + lane of the wave's block -- every load and
+// store instruction is 64 consecutive 16-byte vectors (1 KiB, coalesced).
 template <int RA, int RB, int WA, int WB>
 __global__ __launch_bounds__(256) void streamMixKernel(const mixv *__restrict__ a, const mixv *__restrict__ b,
                                                        mixv *__restrict__ wa, mixv *__restrict__ wb, uint64_t steps,
                                                        unsigned long long *sink) {
-  constexpr int LA = RA / 2, LB = RB / 2, SA = WA / 2, SB = WB / 2;  // 16-byte vectors per 8 elements
-  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  constexpr int LA = RA / 2, LB = RB / 2, SA = WA / 2, SB = WB / 2;  // 16-byte vectors per lane and step
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint64_t waves = (uint64_t)gridDim.x * (256 / WAVE);
   mixv acc = {0, 0, 0, 0};
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < steps; i += stride) {
+  for (uint64_t w = (uint64_t)blockIdx.x * (256 / WAVE) + threadIdx.x / WAVE; w < steps; w += waves) {
     mixv x = {0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < LA; ++k) x ^= __builtin_nontemporal_load(a + i * LA + k);
+    for (int k = 0; k < LA; ++k) x ^= __builtin_nontemporal_load(a + (w * LA + k) * WAVE + lane);
 #pragma unroll
-    for (int k = 0; k < LB; ++k) x ^= __builtin_nontemporal_load(b + i * LB + k);
+    for (int k = 0; k < LB; ++k) x ^= __builtin_nontemporal_load(b + (w * LB + k) * WAVE + lane);
 #pragma unroll
-    for (int k = 0; k < SA; ++k) wa[i * SA + k] = x + (unsigned)k;
+    for (int k = 0; k < SA; ++k) wa[(w * SA + k) * WAVE + lane] = x + (unsigned)k;
 #pragma unroll
-    for (int k = 0; k < SB; ++k) wb[i * SB + k] = x - (unsigned)k;
+    for (int k = 0; k < SB; ++k) wb[(w * SB + k) * WAVE + lane] = x - (unsigned)k;
     acc ^= x;
   }
   if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9E3779B9u) *sink = acc.x;  // keeps read-only mixes live
@@ -57,8 +61,8 @@ __global__ __launch_bounds__(256) void streamMixKernel(const mixv *__restrict__ 
 
 void streamMix(int ra, int rb, int wa, int wb, const void *a, const void *b, void *oa, void *ob, uint64_t n,
                unsigned long long *sink, hipStream_t s) {
-  const uint64_t steps = n / 8;
-  const uint32_t grid = (uint32_t)std::min<uint64_t>(ceilDiv(steps, 256), 256 * 16);
+  const uint64_t steps = n / 512;  // wave steps of 512 elements
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(ceilDiv(steps, 256 / WAVE), 256 * 16);
 #define HJ_MIX(RA, RB, WA, WB)                                                                                    \
   if (ra == RA && rb == RB && wa == WA && wb == WB) {                                                             \
     hipLaunchKernelGGL((streamMixKernel<RA, RB, WA, WB>), dim3(grid), dim3(256), 0, s, (const mixv *)a,          \

@@ -48,7 +48,7 @@ def timed(fn, reps=5):
 def main():
     C = hpcjoin.require_native()
     n = int(float(sys.argv[1])) if len(sys.argv) > 1 else 1_000_000_000
-    n -= n % 8
+    n -= n % 512
     dev = torch.device("cuda", 0)
     buf = lambda b: torch.empty(max(n * b, 16), dtype=torch.uint8, device=dev) if b else torch.empty(16, dtype=torch.uint8, device=dev)
     sink = torch.zeros(1, dtype=torch.int64, device=dev)
