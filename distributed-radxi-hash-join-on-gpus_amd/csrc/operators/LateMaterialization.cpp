@@ -28,6 +28,26 @@ static uint32_t ownerOf(uint64_t rid, uint64_t ridsPerRank, uint32_t nodes) {
   return (uint32_t)std::min<uint64_t>(o, nodes - 1);
 }
 
+LateMaterialization::~LateMaterialization() {
+  for (auto &side : marks)
+    for (hipEvent_t &e : side)
+      if (e) (void)hipEventDestroy(e);
+}
+
+// After the final synchronisation: phase k of a side = mark k -> mark k + 1.
+void LateMaterialization::resolveMarks() {
+  double *acc[PHASES] = {&st.bucketMs, &st.requestMs, &st.gatherMs, &st.responseMs, &st.placeMs};
+  for (int side = 0; side < 2; ++side) {
+    if (!marked[side]) continue;
+    for (int k = 0; k < PHASES; ++k) {
+      float ms = 0;
+      HIP_CHECK(hipEventElapsedTime(&ms, marks[side][k], marks[side][k + 1]));
+      *acc[k] += ms;
+    }
+    marked[side] = false;
+  }
+}
+
 void LateMaterialization::materialize(const ulonglong2 *pairs, uint64_t n, uint64_t *out) {
   static_assert(OUT_WORDS == 2 + 2 * ROW_WORDS, "output row layout");
   if (ctx->onDevice() && ctx->comm()->size() == 1) {
@@ -47,6 +67,7 @@ void LateMaterialization::materialize(const ulonglong2 *pairs, uint64_t n, uint6
     if (n)
       HIP_CHECK(hipMemcpy2DAsync(out, OUT_WORDS * 8, pairs, 16, 16, n, hipMemcpyDeviceToDevice, ctx->stream()));
     HIP_CHECK(hipStreamSynchronize(ctx->stream()));
+    resolveMarks();
   } else {
     for (uint64_t i = 0; i < n; ++i) {
       out[i * OUT_WORDS] = pairs[i].x;
@@ -76,13 +97,12 @@ void LateMaterialization::fetchDevice(const ulonglong2 *pairs, uint64_t n, int s
     return;
   }
   // Bucket requests by owner with the LDS radix kernels (digit = owner).
-  uint64_t tp = performance::nowUs();
-  auto lap = [&](double &acc) {
-    HIP_CHECK(hipStreamSynchronize(s));
-    const uint64_t now = performance::nowUs();
-    acc += (now - tp) / 1000.0;
-    tp = now;
-  };
+  // Phase boundaries are timing events on the stream (resolveMarks).
+  for (hipEvent_t &e : marks[side])
+    if (!e) HIP_CHECK(hipEventCreate(&e));
+  int mark = 0;
+  auto lap = [&]() { HIP_CHECK(hipEventRecord(marks[side][mark++], s)); };
+  lap();
   const uint32_t bits = std::max<uint32_t>(1, ceilLog2(N)), F = 1u << bits;
   const kernels::PartitionGeometry g = kernels::partitionGeometry(n);
   uint32_t *blockHist = ws.getArray<uint32_t>((uint64_t)F * g.blocks);
@@ -117,9 +137,9 @@ void LateMaterialization::fetchDevice(const ulonglong2 *pairs, uint64_t n, int s
     if (r) sd[r] = sd[r - 1] + sendCounts[r - 1];
   }
   uint64_t *recvRids = ws.getArray<uint64_t>(std::max<uint64_t>(m, 1));
-  lap(st.bucketMs);
+  lap();
   c->allToAllV(rids, sendCounts.data(), sd.data(), recvRids, recvCounts.data(), rd.data(), Location::Device, s);
-  lap(st.requestMs);
+  lap();
   for (uint32_t r = 0; r < N; ++r)
     if (r != me) {
       st.requestBytes += sendCounts[r] * 8;
@@ -137,11 +157,12 @@ void LateMaterialization::fetchDevice(const ulonglong2 *pairs, uint64_t n, int s
     brd[r] = sd[r] * ROW_WORDS;
   }
   uint64_t *rowsBack = ws.getArray<uint64_t>(std::max<uint64_t>(n, 1) * ROW_WORDS);
-  lap(st.gatherMs);
+  lap();
   c->allToAllV(resp, bsc.data(), bsd.data(), rowsBack, brc.data(), brd.data(), Location::Device, s);
-  lap(st.responseMs);
+  lap();
   kernels::placeRows(rowsBack, idx, n, out, OUT_WORDS, col0, s);
-  lap(st.placeMs);
+  lap();
+  marked[side] = true;
 }
 
 void LateMaterialization::fetchHost(const ulonglong2 *pairs, uint64_t n, int side, const PayloadColumn &col,

@@ -27,8 +27,10 @@ struct PayloadColumn {
 class LateMaterialization {
  public:
   static constexpr uint32_t OUT_WORDS = 2 + 2 * 4;  // rid_inner, rid_outer, inner row, outer row
-  // Host-clock phase times (both sides summed; each phase ends at a stream
-  // synchronisation) and the bytes this rank put on its links.
+  // Device-timeline phase times (both sides summed; timing events recorded on
+  // the engine stream between the phases and resolved after materialize()'s
+  // final synchronisation -- no extra host syncs) and the bytes this rank put
+  // on its links.
   struct Stats {
     double bucketMs = 0;    // requests bucketed by owner rank (LDS radix kernels)
     double requestMs = 0;   // all-to-allv of the requested rids
@@ -42,6 +44,9 @@ class LateMaterialization {
   // matVariant: KernelVariants::matVariant of the single-rank gather kernel.
   LateMaterialization(core::ExecContext *ctx, const PayloadColumn &inner, const PayloadColumn &outer,
                       uint32_t matVariant = 1);
+  ~LateMaterialization();
+  LateMaterialization(const LateMaterialization &) = delete;
+  LateMaterialization &operator=(const LateMaterialization &) = delete;
   // out: [n][OUT_WORDS] u64 in the context's memory.  Collective: every rank calls it.
   void materialize(const ulonglong2 *pairs, uint64_t n, uint64_t *out);
 
@@ -52,6 +57,10 @@ class LateMaterialization {
   PayloadColumn cols[2];
   uint32_t matVariant = 1;
   Stats st;
+  static constexpr int PHASES = 5;             // bucket, request, gather, response, place
+  hipEvent_t marks[2][PHASES + 1] = {};        // per side: start + one per phase end (timing events)
+  bool marked[2] = {false, false};
+  void resolveMarks();
 };
 
 }  // namespace operators

@@ -522,3 +522,43 @@ def test_hot_partition_split(C, dev, n_ranks, chunks, opts):
     assert load[True] < load[False], load
     if opts == "mat":
         assert torch.equal(got[(True, "pairs")], got[(False, "pairs")])
+
+
+@pytest.mark.gpu
+def test_one_sided_in_process_distinct_devices(C):
+    """In-process one-sided windows on two GPUs: the scatter stores through
+    raw peer pointers after Window::enableOneSided enabled peer access between
+    the ranks' devices (data/Window.cpp).  Needs two visible devices: skipped
+    on the one-GPU test box, run wherever two are visible."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two visible GPUs")
+    group = C.InProcessGroup(2)
+    G_R, G_S = 300_007, 500_009
+    inner = C.GenSpec(seed=1234)
+    outer = C.GenSpec(distribution=C.KeyDistribution.UNIFORM, seed=4321, domain=G_R)
+    out, errs = [None, None], []
+
+    def rank_main(r):
+        try:
+            torch.cuda.set_device(r)
+            ctx = C.ExecContext("device", r, group.communicator(r))
+            R = C.Relation(C.Relation.local_size_for(G_R, r, 2), G_R, "device", r)
+            S = C.Relation(C.Relation.local_size_for(G_S, r, 2), G_S, "device", r)
+            R.generate(inner, C.Relation.local_offset_for(G_R, r, 2))
+            S.generate(outer, C.Relation.local_offset_for(G_S, r, 2))
+            cfg = C.JoinConfig()
+            cfg.exchange = C.ExchangeMode.ONE_SIDED
+            cfg.bitmap_join = False
+            j = C.HashJoin(R, S, ctx, cfg)
+            out[r] = (j.run(), j.plan)
+        except Exception as e:  # surface in the main thread
+            errs.append((r, repr(e)))
+
+    ts = [threading.Thread(target=rank_main, args=(r,)) for r in range(2)]
+    [t.start() for t in ts]
+    [t.join(timeout=600) for t in ts]
+    assert not errs, errs
+    exp = C.Relation.expected_matches(inner, G_R, outer, G_S)
+    for res, plan in out:
+        assert plan.one_sided and res["global_matches"] == exp
