@@ -392,8 +392,10 @@ void Window::stop() {
 
 void Window::flush() { stop(); }
 
-void Window::setPartitioned(void *p, const uint64_t *pb, uint32_t bits, const uint64_t *pe, uint16_t *hi) {
+void Window::setPartitioned(void *p, const uint64_t *pb, uint32_t bits, const uint64_t *pe, uint16_t *hi,
+                            uint64_t capacity) {
   partitionedHi = hi;
+  partitionedCapacity = capacity ? capacity : localWindowSize;
   partitioned = p;
   partBegin = pb;
   partEnd = pe;

@@ -108,8 +108,10 @@ class Window {
   // partEnd: null when partitions are contiguous (end of p = partBegin[p + 1]).
   // hi: the fragment column of the split layout (kernels.h, SplitLayout);
   // partitioned is then the u32 rid column.
+  // capacity: elements of the partitioned buffers (0 = the window size).
   void setPartitioned(void *partitioned, const uint64_t *partBegin, uint32_t localBits,
-                      const uint64_t *partEnd = nullptr, uint16_t *hi = nullptr);
+                      const uint64_t *partEnd = nullptr, uint16_t *hi = nullptr, uint64_t capacity = 0);
+  uint64_t getPartitionedCapacity() const { return partitionedCapacity; }
   const uint16_t *getPartitionedHi() const { return partitionedHi; }  // null unless split
   void *getPartitionedData() const { return partitioned; }
   const uint64_t *getPartitionBegin() const { return partBegin; }  // [owned * 2^localBits + 1] (ctx location)
@@ -149,6 +151,7 @@ class Window {
   const uint64_t *partEnd = nullptr;
   uint32_t localBits = 0;
   uint16_t *partitionedHi = nullptr;
+  uint64_t partitionedCapacity = 0;
   // One-sided state: peer p's window base (mapped), and the tuple offset of
   // this rank's chunk-c run in it: peerOffset[p * chunks + c].
   bool oneSided = false, oneSidedComplete = false;

@@ -75,6 +75,9 @@ __device__ __forceinline__ uint32_t hash64(uint64_t key, uint32_t tbits) {
   return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - tbits));
 }
 
+// dedupParts (optional, key-only words with repeated keys): partitions with
+// more than rChunk inner tuples are listed there (appended at *dedupCount)
+// for bpKeyDedup, which compacts them and emits their spans itself.
 // heavySpans (optional): partitions with more than heavyMin inner tuples
 // (rChunk: more than one table; 0 once repeated keys were seen) get no work
 // items here; their spans go to heavySpans instead (appended at *heavyCount,
@@ -85,11 +88,17 @@ __global__ __launch_bounds__(BPT) void bpPlanCountsKernel(const uint64_t *__rest
                                                           const uint64_t *__restrict__ partSEnd, uint32_t P, uint32_t rc,
                                                           uint32_t sc, uint32_t *counts, BPSpan *__restrict__ heavySpans,
                                                           uint32_t *__restrict__ heavyCount, uint32_t heavyCapacity,
-                                                          uint32_t heavyMin) {
+                                                          uint32_t heavyMin, uint32_t *__restrict__ dedupParts,
+                                                          uint32_t *__restrict__ dedupCount) {
   const uint32_t p = blockIdx.x * BPT + threadIdx.x;
   if (p >= P) return;
   const uint64_t nr = partREnd[p] - partR[p], ns = partSEnd[p] - partS[p];
   const uint32_t c = (nr == 0 || ns == 0) ? 0u : (uint32_t)(ceilDiv(nr, rc) * ceilDiv(ns, sc));
+  if (dedupParts && nr > rc && c) {  // more than one inner chunk: compacted first (bpKeyDedup), spans after
+    dedupParts[atomicAdd(dedupCount, 1u)] = p;
+    counts[p] = 0;
+    return;
+  }
   if (heavySpans && nr > heavyMin && c) {
     const uint32_t nsChunks = (uint32_t)ceilDiv(ns, sc);
     const uint32_t o = atomicAdd(heavyCount, c);
@@ -99,7 +108,7 @@ __global__ __launch_bounds__(BPT) void bpPlanCountsKernel(const uint64_t *__rest
       sp.sb = partS[p] + (uint64_t)(i % nsChunks) * sc;
       sp.nr = (uint32_t)(min(nr - (uint64_t)(i / nsChunks) * rc, (uint64_t)rc));
       sp.ns = (uint32_t)(min(ns - (uint64_t)(i % nsChunks) * sc, (uint64_t)sc));
-      sp.pad0 = sp.pad1 = 0;
+      sp.flags = sp.pad1 = 0;
       heavySpans[o + i] = sp;
     }
     counts[p] = 0;
@@ -114,7 +123,7 @@ void bpPlanCounts(const BPArgs &a, uint32_t *counts, hipStream_t s) {
   hipLaunchKernelGGL(bpPlanCountsKernel, dim3(ceilDiv(a.P, BPT)), dim3(BPT), 0, s, a.partR, a.partS,
                      a.partREnd ? a.partREnd : a.partR + 1, a.partSEnd ? a.partSEnd : a.partS + 1, a.P, a.rChunk,
                      a.sChunk, counts, a.heavySpans, a.heavyCount, a.heavyCapacity,
-                     a.heavyMin);
+                     a.heavyMin, a.dedupParts, a.dedupCount);
   HIP_CHECK_LAUNCH();
 }
 

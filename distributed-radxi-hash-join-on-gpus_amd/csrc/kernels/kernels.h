@@ -285,7 +285,8 @@ void claimOverflow(unsigned long long *gcur, const unsigned long long *gend, uin
 struct BPSpan {
   unsigned long long rb, sb;  // first inner / outer word of the span
   uint32_t nr, ns;            // inner (<= rChunk) / outer (<= sChunk) words
-  uint32_t pad0, pad1;
+  uint32_t flags;             // bit 0: the inner words are compacted (distinct words, counts in BPArgs::dedupCounts)
+  uint32_t pad1;
 };
 // --------------------------------------------------------------- build/probe
 struct BPItem {
@@ -356,6 +357,15 @@ struct BPArgs {
   uint32_t *heavyCount = nullptr;
   uint32_t heavyCapacity = 0;
   uint32_t heavyMin = 0xFFFFFFFFu;  // inner tuples above which a partition is heavy
+  // Optional (counted tables, repeated keys): partitions of more than rChunk
+  // inner tuples go to dedupParts (u32 count at dedupCount, zeroed by the
+  // caller); bpKeyDedup compacts each one's inner words in place to
+  // (distinct word, count) -- the count in dedupCounts, indexed like R -- and
+  // appends its spans, flagged as compacted, to heavySpans.
+  uint32_t *dedupParts = nullptr;
+  uint32_t *dedupCount = nullptr;
+  uint32_t *dedupCounts = nullptr;
+  uint64_t *dedupLen = nullptr;  // [P] compacted words per listed partition (kept for span re-emits)
   // Kernel variants (KernelVariants::keyCount / rowsLds).
   uint32_t keyCount = 8;
   uint32_t rowsLds = 1;
@@ -401,6 +411,9 @@ bool bpKeyCountedFits(const BPArgs &a);
 // keys): counted tables (build_probe.hip, bpKeyCountedSpansKernel); adds to
 // a.result.
 void bpKeyCountedSpans(const BPArgs &a, hipStream_t s);
+// Compacts the partitions bpPlanCounts listed in a.dedupParts (see BPArgs)
+// and appends their counted spans; run before bpKeyCountedSpans.
+void bpKeyDedup(const BPArgs &a, uint32_t maxParts, bool emitOnly, hipStream_t s);
 
 // Single-level counting join of unique inner keys (bitmap_join.hip): one
 // workgroup per network partition sets a 2^bits LDS bitmap from the inner

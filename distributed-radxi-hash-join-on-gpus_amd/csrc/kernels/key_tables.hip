@@ -60,7 +60,7 @@ __global__ __launch_bounds__(KT_EMIT_T) void bpEmitSpansKernel(const uint64_t *_
     sp.sb = sb;
     sp.nr = (uint32_t)(min(r1, rb + rc) - rb);
     sp.ns = (uint32_t)(min(s1, sb + sc) - sb);
-    sp.pad0 = sp.pad1 = 0;
+    sp.flags = sp.pad1 = 0;
     spans[o + i] = sp;
   }
 }
@@ -370,19 +370,19 @@ __device__ __forceinline__ uint32_t kqProbeBatch(const uint64_t (&pv)[K], uint32
 }
 
 // Counted table (bpKeyCountedSpansKernel): entry e = one distinct key,
-//   slot 0 = stored value, slot 1 = id << 16 | esc << 15 | (count - 1),
+//   slot 0 = stored value, slot 1 = id << 16 | esc << 15,  count[e] apart,
 //   id = dist << 4 | tag,  dist = e - home bucket (linear probing).
 // (stored value, id, esc) at entry e names exactly one fragment, so a probe
 // never matches a key of another home.  Escape keys (v = the empty marker)
 // are stored inline with esc = 1 and stored value 0: e = ~salt(b) is implied
 // by the home bucket, so (home, tag) names them.  Claimed by one 64-bit CAS
-// of (value, id, esc, 0) on an empty entry; a copy finding its own triple
-// adds 1 to slot 1 (counts <= 2048 per span stay below bit 15).
+// of (value, id, esc) on an empty entry; every copy (the claimer included)
+// adds its count to count[e], a separate u32 array read only on a match.
 __device__ __forceinline__ uint32_t kqCountedId(uint32_t dist, uint32_t tag) { return (dist << 4) | tag; }
 
 template <int T, int K>
-__device__ __forceinline__ uint32_t kqProbeCounted(const uint64_t (&pv)[K], uint32_t valid, uint32_t s,
-                                                   const uint2 *tab2) {
+__device__ __forceinline__ uint64_t kqProbeCounted(const uint64_t (&pv)[K], uint32_t valid, uint32_t s,
+                                                   const uint2 *tab2, const uint32_t *cnt) {
   uint32_t bk[K], v[K], tg[K];
   uint2 x[K];
 #pragma unroll
@@ -390,15 +390,15 @@ __device__ __forceinline__ uint32_t kqProbeCounted(const uint64_t (&pv)[K], uint
     kqKey(pv[k], s, bk[k], v[k], tg[k]);
     x[k] = tab2[bk[k]];
   }
-  uint32_t matches = 0;
+  uint64_t matches = 0;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const uint32_t esc = v[k] == KQ_EMPTY, vs = esc ? 0u : v[k];
     uint32_t c = 0, e = bk[k];
     uint2 y = x[k];
     for (uint32_t dist = 0; dist < KQ_BUCKETS; ++dist) {
-      if (y.x == vs && (y.y >> 15) == ((kqCountedId(dist, tg[k]) << 1) | esc)) {
-        c = (y.y & 0x7FFFu) + 1;
+      if (y.x == vs && y.y == ((kqCountedId(dist, tg[k]) << 16) | (esc << 15))) {
+        c = cnt[e];
         break;
       }
       if (y.x == KQ_EMPTY) break;
@@ -547,42 +547,50 @@ static void launchKeyQuotient(const BPArgs &a, const BPSpan *spans, const uint32
 // thousand, just above the mean; with repeated keys the hot ones) skip the
 // span work queue, whose one-slot-per-tuple quotient table holds every copy
 // of a key.  Their spans (bpPlanCounts -> heavySpans, same rChunk x sChunk
-// tiling) are counted here on a *counted* table over the same 32 KiB (see
-// kqProbeCounted): one entry per distinct key, so copies only add to a count.
-// A span's <= 2048 inner tuples fill at most half of the 4096 entries.  This
-// table also carries 45-48-bit fragments (the tag next to the count) and
-// escape keys inline, so it never needs a fallback: plans whose fragments the
-// quotient table cannot hold, and quotient spans that filled their overflow
-// table, count here.  A hot partition's spans spread over workgroups like any
-// others.
+// tiling) are counted here on a *counted* table (see kqProbeCounted): one
+// entry per distinct key, so copies only add to a count.  A span's <= 2048
+// inner words fill at most half of the 4096 entries.  The table also carries
+// 45-48-bit fragments (the tag in the entry) and escape keys inline, so it
+// never needs a fallback: plans whose fragments the quotient table cannot
+// hold, and quotient spans that filled their overflow table, count here.  A
+// hot partition's spans spread over workgroups like any others.
+//
+// Compacted spans (BPSpan::flags bit 0, from bpKeyDedup): the inner words are
+// distinct keys with a count each in BPArgs::dedupCounts, added whole.  A hot
+// key's million copies then cost one table entry instead of ~500 inner
+// chunks each re-reading the partition's outer side.
 template <int T, int K>
 __global__ __launch_bounds__(T) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R, KsSrc<T, K, true> S,
+                                                              const uint32_t *__restrict__ rCounts,
                                                               const BPSpan *__restrict__ spans,
                                                               const uint32_t *__restrict__ nSpansPtr, uint32_t capacity,
                                                               uint32_t s, unsigned long long *__restrict__ result) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint32_t *tab = reinterpret_cast<uint32_t *>(smem);  // [entry][value, id << 16 | esc << 15 | count - 1]
-  unsigned long long *tab64 = reinterpret_cast<unsigned long long *>(smem);
+  unsigned long long *tab64 = reinterpret_cast<unsigned long long *>(smem);  // [entry] value | id << 48 | esc << 47
   const uint2 *tab2 = reinterpret_cast<const uint2 *>(smem);
-  unsigned long long *wsum = reinterpret_cast<unsigned long long *>(tab + 2 * KQ_BUCKETS);
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(tab64 + KQ_BUCKETS);          // [entry] count
+  unsigned long long *wsum = reinterpret_cast<unsigned long long *>(cnt + KQ_BUCKETS);
   constexpr uint32_t BATCH = T * K;
   const uint32_t t = threadIdx.x;
   const uint32_t n = min(*nSpansPtr, capacity);
   uint64_t matches = 0;
   auto clear = [&]() {
-    uint4 *t4 = reinterpret_cast<uint4 *>(tab);
-    for (uint32_t i = t; i < KQ_BUCKETS / 2; i += T) t4[i] = make_uint4(KQ_EMPTY, KQ_EMPTY, KQ_EMPTY, KQ_EMPTY);
+    uint4 *t4 = reinterpret_cast<uint4 *>(smem);  // entries (all ones) then counts (zero)
+    for (uint32_t i = t; i < KQ_BUCKETS * 12 / 16; i += T)
+      t4[i] = i < KQ_BUCKETS / 2 ? make_uint4(KQ_EMPTY, KQ_EMPTY, KQ_EMPTY, KQ_EMPTY) : make_uint4(0, 0, 0, 0);
   };
   clear();
   __syncthreads();
   for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
     const BPSpan sp = spans[w];
+    const bool compacted = sp.flags & 1u;
     // ---- build: nr <= rChunk <= BATCH, one pass
     uint64_t rv[K];
     R.load(sp.rb, sp.nr, rv);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       if ((uint32_t)(k * T) + t >= sp.nr) continue;
+      const uint32_t add = compacted ? rCounts[sp.rb + (uint32_t)(k * T) + t] : 1u;
       uint32_t e, v, tg;
       kqKey(rv[k], s, e, v, tg);
       const uint32_t esc = v == KQ_EMPTY, vs = esc ? 0u : v;
@@ -590,9 +598,8 @@ __global__ __launch_bounds__(T) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R
       for (uint32_t dist = 0;; ++dist) {
         const uint32_t hi = (kqCountedId(dist, tg) << 16) | (esc << 15);
         const unsigned long long o = atomicCAS(&tab64[e], ~0ull, ((unsigned long long)hi << 32) | vs);
-        if (o == ~0ull) break;  // claimed with count - 1 = 0
-        if ((uint32_t)o == vs && ((uint32_t)(o >> 32) >> 15) == (hi >> 15)) {
-          atomicAdd(&tab[2 * e + 1], 1u);
+        if (o == ~0ull || ((uint32_t)o == vs && (uint32_t)(o >> 32) == hi)) {
+          atomicAdd(&cnt[e], add);
           break;
         }
         e = (e + 1) & (KQ_BUCKETS - 1);
@@ -604,7 +611,7 @@ __global__ __launch_bounds__(T) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R
       const uint32_t ns = min(sp.ns - b0, BATCH);
       uint64_t xv[K];
       S.load(sp.sb + b0, ns, xv);
-      matches += kqProbeCounted<T, K>(xv, ns, s, tab2);
+      matches += kqProbeCounted<T, K>(xv, ns, s, tab2, cnt);
     }
     __syncthreads();
     clear();
@@ -614,15 +621,146 @@ __global__ __launch_bounds__(T) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R
   if (t == 0 && total) atomicAdd(result, total);
 }
 
+size_t bpKeyCountedLdsBytes() { return KQ_BUCKETS * 12 + 16 * 8 + 16; }
+
 void bpKeyCountedSpans(const BPArgs &a, hipStream_t st) {
   constexpr int T = 512, K = 4;
   HJ_CHECK(bpKeyCountedFits(a) && a.rChunk <= (uint32_t)(T * K) && a.heavySpans && a.heavyCount,
            "bpKeyCountedSpans: needs split key-only words of <= 48 fragment bits and the heavy span list");
   const uint32_t s = a.keyFragBits > 32 ? a.keyFragBits - 32 : 0;
-  const size_t lds = KQ_BUCKETS * 8 + 16 * 8 + 16;
-  const dim3 grid(std::min<uint32_t>(std::max<uint32_t>(a.heavyCapacity, 1), 256 * 4));
+  const size_t lds = bpKeyCountedLdsBytes();
+  const dim3 grid(std::min<uint32_t>(std::max<uint32_t>(a.heavyCapacity, 1), 256 * 3));
   hipLaunchKernelGGL((bpKeyCountedSpansKernel<T, K>), grid, dim3(T), lds, st, KsSrc<T, K, true>{a.R, a.Rhi},
-                     KsSrc<T, K, true>{a.S, a.Shi}, a.heavySpans, a.heavyCount, a.heavyCapacity, s, a.result);
+                     KsSrc<T, K, true>{a.S, a.Shi}, a.dedupCounts, a.heavySpans, a.heavyCount, a.heavyCapacity, s,
+                     a.result);
+  HIP_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------ in-place inner compaction
+// bpKeyDedup: one workgroup per listed partition (more than rChunk inner
+// words, repeated keys known).  It streams the partition's inner words in
+// 2048-word batches into an LDS table of (full fragment, count) -- 4096
+// entries, 64-bit CAS claims, count adds -- and whenever more than 1024
+// distinct keys are held (so the next batch still fits at load <= 3/4),
+// flushes them back over the partition's own words: word i of the compacted
+// list overwrites inner word i, which was already read (a flush writes at most
+// as many entries as words consumed since the last one), with its count at
+// dedupCounts[i].  A key may appear in several flushes; counts then add up in
+// the counted table.  Finally the workgroup emits the partition's counted
+// spans over the compacted words (flags bit 0): ceil(distinct / rChunk) inner
+// chunks instead of ceil(words / rChunk).  The inner words are overwritten, so
+// the caller runs this once per join (not with per-chunk rebuilds); the
+// compacted lengths are kept per partition, and a re-run of the build/probe
+// (span list overflow) only re-emits the spans (emitOnly).
+constexpr uint32_t KD_ENTRIES = 4096;
+constexpr uint32_t KD_FLUSH = 1024;
+
+template <int T, int K>
+__global__ __launch_bounds__(T) void bpKeyDedupKernel(KsSrc<T, K, true> R, uint32_t *__restrict__ rlo,
+                                                       uint16_t *__restrict__ rhi, uint32_t *__restrict__ rCounts,
+                                                       const uint32_t *__restrict__ parts,
+                                                       const uint32_t *__restrict__ nPartsPtr, uint32_t maxParts,
+                                                       const uint64_t *__restrict__ partR,
+                                                       const uint64_t *__restrict__ partREnd,
+                                                       const uint64_t *__restrict__ partS,
+                                                       const uint64_t *__restrict__ partSEnd, uint32_t rc, uint32_t sc,
+                                                       BPSpan *__restrict__ spans, uint32_t *__restrict__ spanCount,
+                                                       uint32_t spanCapacity, uint64_t *__restrict__ lenByPart,
+                                                       bool emitOnly) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned long long *key = reinterpret_cast<unsigned long long *>(smem);  // [entry] fragment (~0 = empty)
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(key + KD_ENTRIES);         // [entry] count
+  uint32_t *ctl = cnt + KD_ENTRIES;                                       // [0] distinct held, [1] out, [2] span base
+  constexpr uint32_t BATCH = T * K;
+  const uint32_t t = threadIdx.x;
+  const uint32_t np = min(*nPartsPtr, maxParts);
+  for (uint32_t i = t; i < KD_ENTRIES; i += T) {
+    key[i] = ~0ull;
+    cnt[i] = 0;
+  }
+  for (uint32_t w = blockIdx.x; w < np; w += gridDim.x) {
+    const uint32_t p = parts[w];
+    const uint64_t rb = uniform64(partR[p]);
+    const uint64_t nr = uniform64(partREnd[p]) - rb;
+    if (t == 0) {
+      ctl[0] = 0;
+      ctl[1] = emitOnly ? (uint32_t)lenByPart[p] : 0u;
+    }
+    __syncthreads();
+    auto flush = [&]() {
+      for (uint32_t i = t; i < KD_ENTRIES; i += T) {
+        const unsigned long long f = key[i];
+        if (f == ~0ull) continue;
+        const uint64_t at = rb + atomicAdd(&ctl[1], 1u);
+        rlo[at] = (uint32_t)f;
+        rhi[at] = (uint16_t)(f >> 32);
+        rCounts[at] = cnt[i];
+        key[i] = ~0ull;
+        cnt[i] = 0;
+      }
+      __syncthreads();
+      if (t == 0) ctl[0] = 0;
+      __syncthreads();
+    };
+    for (uint64_t b0 = 0; b0 < (emitOnly ? 0 : nr); b0 += BATCH) {
+      const uint32_t nb = (uint32_t)min<uint64_t>(nr - b0, BATCH);
+      uint64_t v[K];
+      R.load(rb + b0, nb, v);  // used (so landed) before the barrier that precedes any flush over them
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        if ((uint32_t)(k * T) + t >= nb) continue;
+        const unsigned long long f = v[k];
+        uint32_t h = (uint32_t)((f * 0x9E3779B97F4A7C15ull) >> (64 - 12));
+        for (;;) {  // <= KD_FLUSH + BATCH distinct keys in 4096 entries: an empty entry is reached
+          const unsigned long long o = atomicCAS(&key[h], ~0ull, f);
+          if (o == ~0ull) atomicAdd(&ctl[0], 1u);
+          if (o == ~0ull || o == f) {
+            atomicAdd(&cnt[h], 1u);
+            break;
+          }
+          h = (h + 1) & (KD_ENTRIES - 1);
+        }
+      }
+      __syncthreads();
+      if (ctl[0] > KD_FLUSH || b0 + BATCH >= nr) flush();
+    }
+    // ---- the partition's counted spans over its compacted words
+    const uint64_t nd = ctl[1];
+    if (t == 0 && !emitOnly) lenByPart[p] = nd;
+    const uint64_t ns = uniform64(partSEnd[p]) - uniform64(partS[p]);
+    const uint32_t nsc = (uint32_t)ceilDiv(ns, sc);
+    const uint32_t c = (uint32_t)(ceilDiv(nd, rc) * nsc);
+    if (t == 0) ctl[2] = c ? atomicAdd(spanCount, c) : 0u;
+    __syncthreads();
+    const uint32_t o = ctl[2];
+    for (uint32_t i = t; i < c; i += T) {
+      if (o + i >= spanCapacity) break;
+      BPSpan sp;
+      sp.rb = rb + (uint64_t)(i / nsc) * rc;
+      sp.sb = partS[p] + (uint64_t)(i % nsc) * sc;
+      sp.nr = (uint32_t)min(nd - (uint64_t)(i / nsc) * rc, (uint64_t)rc);
+      sp.ns = (uint32_t)min(ns - (uint64_t)(i % nsc) * sc, (uint64_t)sc);
+      sp.flags = 1;
+      sp.pad1 = 0;
+      spans[o + i] = sp;
+    }
+    __syncthreads();
+  }
+}
+
+void bpKeyDedup(const BPArgs &a, uint32_t maxParts, bool emitOnly, hipStream_t st) {
+  constexpr int T = 512, K = 4;
+  if (maxParts == 0) return;
+  HJ_CHECK(a.split && a.dedupParts && a.dedupCount && a.dedupCounts && a.dedupLen && a.heavySpans && a.heavyCount &&
+               a.rChunk <= (uint32_t)(T * K),
+           "bpKeyDedup: needs split key-only words, the partition list, the count column and the span list");
+  const size_t lds = KD_ENTRIES * 12 + 16;
+  const dim3 grid(std::min<uint32_t>(maxParts, 256 * 3));
+  hipLaunchKernelGGL((bpKeyDedupKernel<T, K>), grid, dim3(T), lds, st, KsSrc<T, K, true>{a.R, a.Rhi},
+                     static_cast<uint32_t *>(const_cast<void *>(a.R)), const_cast<uint16_t *>(a.Rhi), a.dedupCounts,
+                     a.dedupParts, a.dedupCount, maxParts, a.partR, a.partREnd ? a.partREnd : a.partR + 1, a.partS,
+                     a.partSEnd ? a.partSEnd : a.partS + 1, a.rChunk, a.sChunk, a.heavySpans, a.heavyCount,
+                     a.heavyCapacity, a.dedupLen, emitOnly);
   HIP_CHECK_LAUNCH();
 }
 

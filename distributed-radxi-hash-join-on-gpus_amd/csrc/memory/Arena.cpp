@@ -23,6 +23,16 @@ static bool traceAlloc() {
   return on;
 }
 
+// HPCJOIN_POISON_ARENA=1: fill every raw allocation with 0xA5 bytes, so code
+// that silently relies on zeroed workspace memory fails loudly (debugging).
+static bool poisonAlloc() {
+  static const bool on = [] {
+    const char *e = std::getenv("HPCJOIN_POISON_ARENA");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 void *Arena::rawAlloc(Location loc, uint64_t bytes, int device) {
   if (bytes == 0) bytes = ALIGNMENT;
   void *p = nullptr;
@@ -41,12 +51,14 @@ void *Arena::rawAlloc(Location loc, uint64_t bytes, int device) {
   if (loc == Location::Device) {
     HIP_CHECK(hipSetDevice(device));
     HIP_CHECK(hipMalloc(&p, bytes));
+    if (poisonAlloc()) HIP_CHECK(hipMemset(p, 0xA5, bytes));
   } else if (loc == Location::Pinned) {
     HIP_CHECK(hipSetDevice(device));
     HIP_CHECK(hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable));
   } else {
     int r = posix_memalign(&p, ALIGNMENT, bytes);
     JOIN_ASSERT(r == 0 && p, "Arena", "posix_memalign(%lu) failed", (unsigned long)bytes);
+    if (poisonAlloc()) std::memset(p, 0xA5, bytes);
   }
   return p;
 }
@@ -91,10 +103,10 @@ void Arena::addChunk(uint64_t bytes, bool touch, void *stream) {
     if (loc_ == Location::Device) {
       HIP_CHECK(hipSetDevice(device_));
       const hipStream_t s = static_cast<hipStream_t>(stream);
-      HIP_CHECK(hipMemsetAsync(p, 0, bytes, s));
+      HIP_CHECK(hipMemsetAsync(p, poisonAlloc() ? 0xA5 : 0, bytes, s));
       HIP_CHECK(hipStreamSynchronize(s));
     } else {
-      std::memset(p, 0, bytes);
+      std::memset(p, poisonAlloc() ? 0xA5 : 0, bytes);
     }
   }
   chunks_.push_back(Chunk{p, bytes, 0});  // growth: existing allocations (and peers' mappings) stay valid

@@ -153,12 +153,27 @@ void BuildProbe::execute() {
   const bool keySpans = args.keyOnly;
   const bool counted = keySpans && args.keyCount >= 8 && kernels::bpKeyCountedFits(args);
   const bool quotient = counted && kernels::bpKeyQuotientFits(args);
+  // keyCount 9 (repeated inner keys): partitions of more than one inner chunk
+  // are first compacted to (distinct word, count) (kernels::bpKeyDedup), once
+  // per join -- not with per-chunk rebuilds of a pipelined outer side, which
+  // re-read the inner words.
+  const bool dedup = counted && args.keyCount == 9 && args.split && !plan.pipelineOuter;
   if (counted) {
     args.heavySpans = ws.getArray<kernels::BPSpan>(capacity);
     args.heavyCapacity = capacity;
     // keyCount 9 (repeated keys seen): every partition on counted tables.
     args.heavyMin = (args.keyCount == 9 || !quotient) ? 0 : args.rChunk;
     args.heavyCount = nItems + 1;  // high half of counters[2]: read back with the rest
+  }
+  if (dedup) {
+    if (!dedupCounts) {  // kept for the join: a re-run only re-emits the compacted spans
+      dedupCounts = ws.getArray<uint32_t>(std::max<uint64_t>(windows[0]->getPartitionedCapacity(), 1));
+      dedupLen = ws.getArray<uint64_t>(std::max<uint32_t>(args.P, 1));
+    }
+    args.dedupParts = ws.getArray<uint32_t>(std::max<uint32_t>(args.P, 1));
+    args.dedupCount = reinterpret_cast<uint32_t *>(counters + 1);  // the pair cursor is unused by a count
+    args.dedupCounts = dedupCounts;
+    args.dedupLen = dedupLen;
   }
   kernels::bpPlanCounts(args, counts, ctx->stream());
   kernels::scanExclusiveU32(counts, offsets, args.P, nItems, scanWs, ctx->stream());
@@ -169,6 +184,10 @@ void BuildProbe::execute() {
     kernels::bpEmitSpans(args, counts, offsets, spans, capacity, ctx->stream());
     args.sideOverflow = counters + 3;  // quotient table flags (kernels.h, BPArgs::sideOverflow)
     tl.beginSplit("BPKERNEL", "BPBUILD", wb, "BPPROBE", wp, ctx->stream());
+    if (dedup) {
+      kernels::bpKeyDedup(args, args.P, deduped, ctx->stream());
+      deduped = true;
+    }
     if (!counted || args.heavyMin != 0)  // otherwise every span is on the heavy list
       kernels::buildProbeKeySpans(args, spans, nItems, capacity, queue, ctx->stream());
     if (counted) kernels::bpKeyCountedSpans(args, ctx->stream());

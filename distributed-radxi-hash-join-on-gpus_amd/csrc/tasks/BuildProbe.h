@@ -79,6 +79,9 @@ class BuildProbe : public Task {
   bool reference = false, overflowOut = false, fused = false;
   bool duplicateChains = false;   // copies of a key chained in the quotient table
   bool countedAll = false;        // a quotient span overflowed: this task counts every partition on counted tables
+  bool deduped = false;           // heavy inner partitions compacted in place (kernels::bpKeyDedup)
+  uint32_t *dedupCounts = nullptr;
+  uint64_t *dedupLen = nullptr;
   const kernels::RowSink *sink = nullptr;
   uint64_t hostCursor = 0;
 };

@@ -155,7 +155,7 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
     if (!overflowBack) overflowBack = ctx->staging().getArray<unsigned int>(1);
     HIP_CHECK(hipMemcpyAsync(overflowBack, overflowFlag, sizeof(unsigned int), hipMemcpyDeviceToHost, ctx->stream()));
     // Final claim cursors are the partition ends (valid when no slot overflowed).
-    w->setPartitioned(sout, pbeg, bits, reinterpret_cast<const uint64_t *>(gcur), split.hi);
+    w->setPartitioned(sout, pbeg, bits, reinterpret_cast<const uint64_t *>(gcur), split.hi, std::max<uint64_t>(cap, 1));
     return;
   }
   void *out = alloc(std::max<uint64_t>(xp.recvTotal, 1) * ob);
@@ -204,7 +204,7 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
     host::localScatter(w->getData(), wide, it.data(), nItems, shift, bits, itemCursors, out);
     tl.end("LPPART");
   }
-  w->setPartitioned(out, partBegin, bits, nullptr, split.hi);
+  w->setPartitioned(out, partBegin, bits, nullptr, split.hi, std::max<uint64_t>(xp.recvTotal, 1));
 }
 
 }  // namespace tasks

@@ -145,9 +145,15 @@ def main():
     S.generate(spec, C.Relation.local_offset_for(G, info.rank, info.world))
     j = C.HashJoin(R, S, ctx, cfg2)
     assert j.plan.one_sided and ctx.workspace_capacity() == 0, (j.plan, ctx.workspace_capacity())
-    for _ in range(2):
+    exp = C.Relation.expected_matches(inner, G_R, spec, G)
+    for it in range(2):
         res = j.run()
-        assert res["global_matches"] == C.Relation.expected_matches(inner, G_R, spec, G), ("one-sided-fallback", res)
+        mine = [it, res["local_matches"], res["inner_received"], res["outer_received"], res["global_matches"]]
+        allv = comm.all_gather(mine) if hasattr(comm, "all_gather") else [mine]
+        if res["global_matches"] != exp:
+            print(f"one-sided-fallback mismatch rank {info.rank}: per-rank [run, local, inner_recv, outer_recv, "
+                  f"global] = {allv}, expected {exp}", flush=True)
+        assert res["global_matches"] == exp, ("one-sided-fallback", it, allv, exp)
     del j, S
     if info.rank == 0:
         print("one-sided with in-join fallback windows: exact", flush=True)

@@ -97,8 +97,8 @@ def oracle(C, info, R, S, domain):
     return total if out == 0 else None
 
 
-def run_config(C, info, ctx, comm, name, G_R, G_S, theta, cfg, steps, warmup):
-    domain = G_R
+def run_config(C, info, ctx, comm, name, G_R, G_S, theta, cfg, steps, warmup, domain=0):
+    domain = domain or G_R
     if name in ("zipf_both", "zipf_both_sparse"):
         inner = C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=1234, domain=domain, zipf_theta=theta)
         outer = C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=4321, domain=domain, zipf_theta=theta)
@@ -194,6 +194,8 @@ def main():
     ap.add_argument("--inner", type=float, default=1e9)
     ap.add_argument("--outer", type=float, default=4e9)
     ap.add_argument("--theta", type=float, default=0.75)
+    ap.add_argument("--domain", type=float, default=0, help="Zipf / uniform key domain (0 = |R|); a small domain "
+                    "puts more than a rank's fair share on one network partition")
     ap.add_argument("--configs", default="zipf_both,uniform_two,zipf_outer")
     ap.add_argument("--assign", default="lpt", help="comma list of lpt,round_robin (N > 1)")
     ap.add_argument("--split", default="on", help="comma list of on,off: hot-partition split (N > 1, LPT)")
@@ -213,7 +215,9 @@ def main():
                 if name == "uniform_two":
                     cfg.bitmap_join = False
                     cfg.replicate_bitmap = C.PlanChoice.OFF
-                out = run_config(C, info, ctx, comm, name, G_R, G_S, args.theta, cfg, args.steps, args.warmup)
+                out = run_config(C, info, ctx, comm, name, G_R, G_S, args.theta, cfg, args.steps, args.warmup,
+                                 int(args.domain))
+                out["domain"] = int(args.domain) or G_R
                 if info.rank == 0:
                     print(json.dumps(out), flush=True)
     del ctx

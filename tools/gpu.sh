@@ -12,6 +12,7 @@
 #   py=SCRIPT,ARGS      python SCRIPT ARGS
 #   stats=ARGS          rocprofv3 --kernel-trace --stats of bench.py ARGS
 #   pmc=CTRS/ARGS       rocprofv3 --pmc CTRS (comma-separated) of bench.py ARGS
+#   ebench=ENV/ARGS     bench.py ARGS with ENV (comma-separated K=V, e.g. HPCJOIN_NET_THREADS=512): A/B runs
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
 TAG=$1
@@ -33,6 +34,8 @@ for step in "$@"; do
     tests) timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$arg" > "$log" 2>&1 ;;
     smoke) timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > "$log" 2>&1 ;;
     bench) timeout -k 10 600 python -u bench.py $args > "$log" 2>&1 ;;
+    ebench) envs=${arg%%/*}; bargs=${arg#*/}
+            timeout -k 10 600 env ${envs//,/ } python -u bench.py ${bargs//,/ } > "$log" 2>&1 ;;
     skew) timeout -k 10 900 python -u tools/bench_skew.py $args > "$log" 2>&1 ;;
     py) timeout -k 10 900 python -u $args > "$log" 2>&1 ;;
     stats) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/stats$n" -o run --output-format csv \
