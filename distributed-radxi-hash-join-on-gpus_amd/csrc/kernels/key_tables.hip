@@ -393,17 +393,23 @@ __device__ __forceinline__ uint64_t kqProbeCounted(const uint64_t (&pv)[K], uint
   uint64_t matches = 0;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
+    // Home entry from the batched reads; the rare walk past occupied
+    // entries re-reads the table (x[] stays in registers, no indexing).
     const uint32_t esc = v[k] == KQ_EMPTY, vs = esc ? 0u : v[k];
     uint32_t c = 0, e = bk[k];
-    uint2 y = x[k];
-    for (uint32_t dist = 0; dist < KQ_BUCKETS; ++dist) {
+    bool walk = false;
+    if (x[k].x == vs && x[k].y == ((kqCountedId(0, tg[k]) << 16) | (esc << 15)))
+      c = cnt[e];
+    else
+      walk = x[k].x != KQ_EMPTY;
+    for (uint32_t dist = 1; walk && dist < KQ_BUCKETS; ++dist) {
+      e = (e + 1) & (KQ_BUCKETS - 1);
+      const uint2 y = tab2[e];
       if (y.x == vs && y.y == ((kqCountedId(dist, tg[k]) << 16) | (esc << 15))) {
         c = cnt[e];
         break;
       }
-      if (y.x == KQ_EMPTY) break;
-      e = (e + 1) & (KQ_BUCKETS - 1);
-      y = tab2[e];
+      walk = y.x != KQ_EMPTY;
     }
     matches += (uint32_t)(k * T) + threadIdx.x < valid ? c : 0u;
   }
@@ -595,7 +601,7 @@ __global__ __launch_bounds__(T) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R
       kqKey(rv[k], s, e, v, tg);
       const uint32_t esc = v == KQ_EMPTY, vs = esc ? 0u : v;
       // <= 2048 distinct keys in 4096 entries: an empty entry is always reached
-      for (uint32_t dist = 0;; ++dist) {
+      for (uint32_t dist = 0; dist < KQ_BUCKETS; ++dist) {
         const uint32_t hi = (kqCountedId(dist, tg) << 16) | (esc << 15);
         const unsigned long long o = atomicCAS(&tab64[e], ~0ull, ((unsigned long long)hi << 32) | vs);
         if (o == ~0ull || ((uint32_t)o == vs && (uint32_t)(o >> 32) == hi)) {
