@@ -255,7 +255,11 @@ uint64_t HashJoin::workspaceEstimate() const {
     if (plan.wireBits[r]) b += (n[r] + recv) * ((plan.wireBits[r] + 7) / 8) + (64ull << 10);  // wire buffers
     if (plan.twoLevel) {
       const uint64_t ob = plan.fragments ? 2 : plan.splitLocal ? kernels::SPLIT_BYTES : (plan.wide ? 16 : 8);
-      b += kernels::localSampledCapacityBound(recv, P, std::max<uint32_t>(1, plan.localSampleStride), 64) * ob;
+      const uint64_t slots = kernels::localSampledCapacityBound(recv, P, std::max<uint32_t>(1, plan.localSampleStride), 64);
+      b += slots * ob;
+      // Repeated keys on counted tables: the inner side's compaction counts
+      // (u32 per slot) and per-partition lengths / lists (BuildProbe, bpKeyDedup).
+      if (r == 0 && plan.keyOnly && plan.variants.keyCount == 9) b += slots * 4 + P * 12;
     }
   }
   // Build/probe work lists (items or spans, 32 B) and materialized pairs.

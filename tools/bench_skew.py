@@ -206,10 +206,10 @@ def main():
     info = init_distributed()
     ctx, comm = make_context(info, "device")
     G_R, G_S = int(args.inner), int(args.outer)
-    for name in args.configs.split(","):
-        for assign in args.assign.split(","):
-            for split in args.split.split(","):
-                if assign != "lpt" and split == "on" and len(args.split.split(",")) > 1:
+    for name in args.configs.replace("+", ",").split(","):
+        for assign in args.assign.replace("+", ",").split(","):
+            for split in args.split.replace("+", ",").split(","):
+                if assign != "lpt" and split == "on" and len(args.split.replace("+", ",").split(",")) > 1:
                     continue  # the split only exists under LPT
                 cfg = config_from_dict({"assignment": assign.upper(), "skew_split": split == "on", "chunks": 1 if info.world == 1 else 4})
                 if name == "uniform_two":
