@@ -714,14 +714,35 @@ __global__ __launch_bounds__(T) void bpKeyDedupKernel(KsSrc<T, K, true> R, uint3
       R.load(rb + b0, nb, v);  // used (so landed) before the barrier that precedes any flush over them
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        if ((uint32_t)(k * T) + t >= nb) continue;
+        const bool valid = (uint32_t)(k * T) + t < nb;
         const unsigned long long f = v[k];
+        // Hot partitions are mostly copies of one or two keys: a wave first
+        // folds the lanes that hold the key of its first (then second)
+        // pending lane into one insert of their popcount, so same-address
+        // LDS atomics do not serialise 64 deep.
+        uint32_t add = 1;
+        bool lead = valid, pending = valid;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          const uint64_t pm = __ballot(pending);
+          if (!pm) break;
+          const int l0 = __ffsll((unsigned long long)pm) - 1;
+          const unsigned long long fr = __shfl(f, l0);
+          const bool g = pending && f == fr;
+          const uint64_t gm = __ballot(g);
+          if (g) {
+            add = (uint32_t)__popcll(gm);
+            lead = (int)(t & (WAVE - 1)) == l0;
+            pending = false;
+          }
+        }
+        if (!lead) continue;
         uint32_t h = (uint32_t)((f * 0x9E3779B97F4A7C15ull) >> (64 - 12));
         for (;;) {  // <= KD_FLUSH + BATCH distinct keys in 4096 entries: an empty entry is reached
           const unsigned long long o = atomicCAS(&key[h], ~0ull, f);
           if (o == ~0ull) atomicAdd(&ctl[0], 1u);
           if (o == ~0ull || o == f) {
-            atomicAdd(&cnt[h], 1u);
+            atomicAdd(&cnt[h], add);
             break;
           }
           h = (h + 1) & (KD_ENTRIES - 1);

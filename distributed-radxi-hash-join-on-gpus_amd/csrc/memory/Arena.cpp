@@ -51,7 +51,17 @@ void *Arena::rawAlloc(Location loc, uint64_t bytes, int device) {
   if (loc == Location::Device) {
     HIP_CHECK(hipSetDevice(device));
     HIP_CHECK(hipMalloc(&p, bytes));
-    if (poisonAlloc()) HIP_CHECK(hipMemset(p, 0xA5, bytes));
+    if (poisonAlloc()) {
+      // On a private non-blocking stream: the synchronous hipMemset runs on
+      // the null stream, which waits for every blocking stream of the device
+      // -- with in-process ranks sharing one device, another rank's stream
+      // (and the barrier it is heading for) -- and deadlocked the ranks.
+      hipStream_t ps;
+      HIP_CHECK(hipStreamCreateWithFlags(&ps, hipStreamNonBlocking));
+      HIP_CHECK(hipMemsetAsync(p, 0xA5, bytes, ps));
+      HIP_CHECK(hipStreamSynchronize(ps));
+      HIP_CHECK(hipStreamDestroy(ps));
+    }
   } else if (loc == Location::Pinned) {
     HIP_CHECK(hipSetDevice(device));
     HIP_CHECK(hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable));
