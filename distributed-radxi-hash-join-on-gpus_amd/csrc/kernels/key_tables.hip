@@ -251,44 +251,45 @@ __global__ __launch_bounds__(T, MINW) void bpKeySpanKernel(KsSrc<T, K, SPLIT> R,
   if (t == 0 && total) atomicAdd(result, total);
 }
 
-// ------------------------------------------- key-only spans, quotient table (v3)
-// KernelVariants::keyCount 8.  The v2 table above spends its LDS cycles on
-// 8-byte keys: a probe is a fill-counter read plus two random ds_read_b128
-// (33 LDS cycles per wave with the measured 3.0-3.6 conflict cycles per
-// instruction; PMC: the LDS pipe ~80 % busy, the kernel at 3.7 TB/s).  Here a
-// key fragment of f <= 32 + KQ_BITS bits (63-bit keys after 10 + 9 radix bits:
-// f = 44) is split into
-//   e = frag >> s (32 bits, s = f - 32)   and   lo = frag's low s bits;
-//   bucket b = (lo ^ h(e)) mod 2^KQ_BITS   (h: multiplicative hash of e),
-// and the bucket stores only v = e ^ salt(b): (b, v) determines the fragment
-// (lo = b ^ h(e) on its low s bits), so a slot is 4 bytes.  Buckets are two
-// u32 slots = one 8-byte ds_read_b64 per probe; 4096 buckets (32 KiB) hold
-// <= 2048 inner keys at load <= 1/4.
+// ------------------------------------------- key-only spans, quotient table (v4)
+// KernelVariants::keyCount 8.  A key fragment of f <= 32 + KQ_BITS bits
+// (63-bit keys after 10 + 9 radix bits: f = 44) is split into
+//   v = frag >> s (32 bits, s = f - 32)   and   lo = frag's low s bits;
+//   home bucket b = (lo ^ h(v)) mod 2^KQ_BITS   (h: multiplicative hash of v),
+// and the bucket stores only v: (b, v) determines the fragment (lo = b ^ h(v)
+// on its low s bits), so a slot is 4 bytes.
 //
-// Exactness: (b, v) names a key only in ITS OWN bucket b.  A key therefore
-// never leaves its home bucket in the quotient table: the third and later
-// keys of a bucket, and "escape" keys whose v equals the empty marker (one
-// fragment per bucket), go to a small overflow table of full 48-bit
-// fragments (KQ_OV entries, linear probing, compared whole).  Slots fill in
-// order (slot 0, slot 1, overflow), so a probe whose home bucket has an empty
-// slot 1 has seen every copy of its key; a full home bucket (~9 % of probes
-// at 2048 keys) adds one overflow lookup, the read that used to walk into
-// the next bucket.  (Round 3 let keys spill into the next bucket, where a
-// stored v of another home could equal the probe's: a 2^-32 false match per
-// foreign comparison.)  More than KQ_OV_CAP overflow keys in one span -- a
-// key with hundreds of copies in a light partition -- stops inserting and
+// Layout (round 4): 4096 buckets x 4 u32 slots, stored as two 8-byte halves
+// (slots 0-1 of every bucket, then slots 2-3: a random ds_read_b64 starts at
+// one of 32 bank pairs), plus a u16 fill count per bucket.  A build is one
+// LDS atomic add on the bucket's count (its old value is the slot) and one
+// store; a probe reads the count and both halves (three LDS reads, no loop)
+// and compares the first `fill` slots.  Slots are never cleared -- the count
+// says which hold keys -- so there is no empty marker and no escape value:
+// every 32-bit v is a key.  (Round 3's two-slot buckets at ~1/2 load sent
+// ~37 % of probes, so nearly every wave, into an overflow walk: PMC showed the
+// kernel VALU-bound at 43 VALU instructions per word.)
+//
+// Exactness: (b, v) names a key only in its home bucket, and a key never
+// leaves it: the fifth and later keys of a bucket (~0.2 % of probes at 2048
+// keys per span) go to a small overflow table of full 48-bit fragments
+// (KQ_OV entries, linear probing, compared whole), read only when the home
+// bucket's count exceeds 4.  More than KQ_OV_CAP overflow keys in one span --
+// a key with hundreds of copies in a light partition -- stops inserting and
 // sets KQF_COUNTED: the count is void and the join's build/probe re-runs on
-// counted tables.  The lanes that built a span reset their own slots after
-// its probe: no table clear.
+// counted tables.  (Round 3 let keys spill into the next bucket, where a
+// stored v of another home could equal the probe's.)
+//
+// Counted tables (bpKeyCountedSpansKernel) keep a salted stored value with an
+// empty marker: kqSalt / kqKey below.
 constexpr uint32_t KQ_BITS = 12;
 constexpr uint32_t KQ_BUCKETS = 1u << KQ_BITS;
+constexpr uint32_t KQ_SLOTS = 4;
 constexpr uint32_t KQ_EMPTY = 0xFFFFFFFFu;
 constexpr uint32_t KQ_OV_BITS = 9;
 constexpr uint32_t KQ_OV = 1u << KQ_OV_BITS;  // overflow entries (4 KiB)
 constexpr uint32_t KQ_OV_CAP = 3 * KQ_OV / 4;  // at most this many inserted: probes always find an empty entry
 constexpr unsigned long long KQ_OV_EMPTY = ~0ull;  // fragments are < 2^48
-constexpr uint32_t KQ_OV_FLAG = 0x80000000u;       // pos[]: overflow-table index
-constexpr uint32_t KQ_NONE = 0xFFFFFFFFu;
 // A placement that walked past this many overflow entries saw one key's
 // copies chained (unique keys at <= 25 % overflow load never do): KQF_CHAINS,
 // and later joins put every partition on counted spans (keyCount 9).
@@ -296,6 +297,14 @@ constexpr uint32_t KQ_LONG_CHAIN = 64;
 // BPArgs::sideOverflow bits.
 constexpr unsigned long long KQF_CHAINS = 2;   // copies of a key chained (count exact)
 constexpr unsigned long long KQF_COUNTED = 8;  // quotient overflow table full: count void, re-run counted
+
+// Quotient-table key of a fragment: (home bucket, stored value).  v is bits
+// [s, s + 32) of the fragment: one v_alignbit of its two halves.
+__device__ __forceinline__ void kq4Key(uint64_t frag, uint32_t s, uint32_t &b, uint32_t &v) {
+  v = __builtin_amdgcn_alignbit((uint32_t)(frag >> 32), (uint32_t)frag, s);
+  const uint32_t lo = (uint32_t)frag & ((1u << s) - 1u);
+  b = (lo ^ ((v * 0x9E3779B1u) >> (32 - KQ_BITS))) & (KQ_BUCKETS - 1);
+}
 
 __device__ __forceinline__ uint32_t kqSalt(uint32_t b) { return (b + 1u) * 0x85EBCA77u; }
 
@@ -329,41 +338,44 @@ __device__ __forceinline__ uint32_t kqOvCount(const unsigned long long *ov, uint
   return c;
 }
 
-// Overflow placement: the entry index | KQ_OV_FLAG, or KQ_NONE when the table
-// is at its cap (full = true: the span's count is void).
-__device__ __forceinline__ uint32_t kqOvInsert(unsigned long long *ov, uint32_t *ovN, uint32_t h, uint64_t frag,
-                                               bool &chained, bool &full) {
+// Overflow placement; at the table's cap nothing is placed and full = true
+// (the span's count is void).
+__device__ __forceinline__ void kqOvInsert(unsigned long long *ov, uint32_t *ovN, uint32_t h, uint64_t frag,
+                                           bool &chained, bool &full) {
   if (atomicAdd(ovN, 1u) >= KQ_OV_CAP) {
     full = true;
-    return KQ_NONE;
+    return;
   }
   for (uint32_t w = 0;; ++w) {  // < KQ_OV_CAP entries taken: an empty one exists
     if (atomicCAS(&ov[h], KQ_OV_EMPTY, (unsigned long long)frag) == KQ_OV_EMPTY) {
       chained |= w > KQ_LONG_CHAIN;
-      return KQ_OV_FLAG | h;
+      return;
     }
     h = (h + 1) & (KQ_OV - 1);
   }
 }
 
-// One batch of T x K outer fragments (the first `valid` counted): all K
-// bucket reads in flight, then the overflow lookups of full home buckets.
+// One batch of T x K outer fragments (the first `valid` counted) against the
+// four-slot table: count, both halves, the overflow table past four keys.
 template <int T, int K>
-__device__ __forceinline__ uint32_t kqProbeBatch(const uint64_t (&pv)[K], uint32_t valid, uint32_t s,
-                                                 const uint2 *tab2, const unsigned long long *ov) {
-  uint32_t bk[K], v[K], tg[K];
-  uint2 x[K];
+__device__ __forceinline__ uint32_t kq4ProbeBatch(const uint64_t (&pv)[K], uint32_t valid, uint32_t s,
+                                                  const uint2 *h0, const uint2 *h1, const uint16_t *fill,
+                                                  const unsigned long long *ov) {
+  uint32_t bk[K], v[K], f[K];
+  uint2 x[K], y[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    kqKey(pv[k], s, bk[k], v[k], tg[k]);
-    x[k] = tab2[bk[k]];
+    kq4Key(pv[k], s, bk[k], v[k]);
+    f[k] = fill[bk[k]];
+    x[k] = h0[bk[k]];
+    y[k] = h1[bk[k]];
   }
   uint32_t matches = 0;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const bool esc = v[k] == KQ_EMPTY;  // only in the overflow table
-    uint32_t c = esc ? 0u : (uint32_t)(x[k].x == v[k]) + (uint32_t)(x[k].y == v[k]);
-    if (x[k].y != KQ_EMPTY || esc) c += kqOvCount(ov, kqOvHash(bk[k], v[k]), pv[k]);
+    uint32_t c = (uint32_t)(f[k] > 0 && x[k].x == v[k]) + (uint32_t)(f[k] > 1 && x[k].y == v[k]) +
+                 (uint32_t)(f[k] > 2 && y[k].x == v[k]) + (uint32_t)(f[k] > 3 && y[k].y == v[k]);
+    if (f[k] > KQ_SLOTS) c += kqOvCount(ov, kqOvHash(bk[k], v[k]), pv[k]);
     matches += (uint32_t)(k * T) + threadIdx.x < valid ? c : 0u;
   }
   return matches;
@@ -417,9 +429,12 @@ __device__ __forceinline__ uint64_t kqProbeCounted(const uint64_t (&pv)[K], uint
 }
 
 size_t bpKeyQuotientLdsBytes() {
-  return KQ_BUCKETS * 8 + KQ_OV * 8 + 16 + KS_CHUNK * sizeof(BPSpan) + 16 * 8 + 16;
+  return KQ_BUCKETS * KQ_SLOTS * 4 + KQ_BUCKETS * 2 + KQ_OV * 8 + 16 + KS_CHUNK * sizeof(BPSpan) + 16 * 8 + 16;
 }
 
+// T = 1024, K = 2: a span's <= 2048 inner words are one register batch.  The
+// ~77 KiB table admits two workgroups per CU: 32 waves, as the round-3
+// 512-thread kernel had at 4 workgroups.
 template <int T, int K, int MINW>
 __global__ __launch_bounds__(T, MINW) void bpKeyQuotientKernel(KsSrc<T, K, true> R, KsSrc<T, K, true> S,
                                                                const BPSpan *__restrict__ spans,
@@ -428,9 +443,12 @@ __global__ __launch_bounds__(T, MINW) void bpKeyQuotientKernel(KsSrc<T, K, true>
                                                                uint32_t s, unsigned long long *__restrict__ result,
                                                                unsigned long long *__restrict__ flags) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint32_t *tab = reinterpret_cast<uint32_t *>(smem);  // [bucket][2]
-  const uint2 *tab2 = reinterpret_cast<const uint2 *>(smem);
-  unsigned long long *ov = reinterpret_cast<unsigned long long *>(tab + 2 * KQ_BUCKETS);
+  uint32_t *slots = reinterpret_cast<uint32_t *>(smem);  // [half][bucket][2]
+  const uint2 *h0 = reinterpret_cast<const uint2 *>(smem);
+  const uint2 *h1 = h0 + KQ_BUCKETS;
+  uint16_t *fill = reinterpret_cast<uint16_t *>(slots + KQ_BUCKETS * KQ_SLOTS);
+  uint32_t *fill2 = reinterpret_cast<uint32_t *>(fill);  // two counts per word (atomics)
+  unsigned long long *ov = reinterpret_cast<unsigned long long *>(fill + KQ_BUCKETS);
   uint32_t *ovN = reinterpret_cast<uint32_t *>(ov + KQ_OV);
   BPSpan *desc = reinterpret_cast<BPSpan *>(ovN + 4);
   unsigned long long *wsum = reinterpret_cast<unsigned long long *>(desc + KS_CHUNK);
@@ -438,12 +456,12 @@ __global__ __launch_bounds__(T, MINW) void bpKeyQuotientKernel(KsSrc<T, K, true>
   constexpr uint32_t BATCH = T * K;
   const uint32_t t = threadIdx.x;
   const uint32_t n = min(*nSpansPtr, capacity);
-  {
-    uint4 *t4 = reinterpret_cast<uint4 *>(tab);  // main table and overflow table are adjacent
-    for (uint32_t i = t; i < (KQ_BUCKETS * 8 + KQ_OV * 8) / 16; i += T)
-      t4[i] = make_uint4(KQ_EMPTY, KQ_EMPTY, KQ_EMPTY, KQ_EMPTY);
-    if (t == 0) *ovN = 0;
-  }
+  auto clearFill = [&]() {
+    for (uint32_t i = t; i < KQ_BUCKETS / 4; i += T) reinterpret_cast<uint2 *>(fill2)[i] = make_uint2(0u, 0u);
+  };
+  clearFill();
+  for (uint32_t i = t; i < KQ_OV; i += T) ov[i] = KQ_OV_EMPTY;
+  if (t == 0) *ovN = 0;
   uint64_t matches = 0;
   bool full = false, chained = false;
   uint64_t rv[K], sv[K], nrv[K], nsv[K];
@@ -464,28 +482,21 @@ __global__ __launch_bounds__(T, MINW) void bpKeyQuotientKernel(KsSrc<T, K, true>
       const uint64_t sb = uniform64(desc[i].sb);
       const uint32_t nr = __builtin_amdgcn_readfirstlane(desc[i].nr);
       const uint32_t ns = __builtin_amdgcn_readfirstlane(desc[i].ns);
-      // ---- build (nr <= BATCH: one batch, from registers): slot 0, slot 1, overflow
-      uint32_t pos[K];
-      {
-        uint32_t bk[K], v[K], tg[K], old[K];
+      // ---- build (nr <= BATCH: one batch, from registers): the old count is the slot
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-          kqKey(rv[k], s, bk[k], v[k], tg[k]);
-          const bool valid = (uint32_t)(k * T) + t < nr;
-          pos[k] = !valid ? KQ_NONE : (v[k] == KQ_EMPTY ? KQ_OV_FLAG : 2 * bk[k]);
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k) old[k] = pos[k] < KQ_OV_FLAG ? atomicCAS(&tab[pos[k]], KQ_EMPTY, v[k]) : KQ_EMPTY;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          if (pos[k] >= KQ_OV_FLAG || old[k] == KQ_EMPTY) continue;  // placed in slot 0 (or not a main-table key)
-          pos[k] = atomicCAS(&tab[pos[k] + 1], KQ_EMPTY, v[k]) == KQ_EMPTY ? pos[k] + 1 : KQ_OV_FLAG;
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-          if (pos[k] == KQ_OV_FLAG) pos[k] = kqOvInsert(ov, ovN, kqOvHash(bk[k], v[k]), rv[k], chained, full);
+      for (int k = 0; k < K; ++k) {
+        uint32_t b, v;
+        kq4Key(rv[k], s, b, v);
+        if ((uint32_t)(k * T) + t >= nr) continue;
+        const uint32_t sh = (b & 1u) * 16u;
+        const uint32_t slot = (atomicAdd(&fill2[b >> 1], 1u << sh) >> sh) & 0xFFFFu;
+        if (slot < KQ_SLOTS)
+          slots[(slot >> 1) * (2 * KQ_BUCKETS) + 2 * b + (slot & 1u)] = v;
+        else
+          kqOvInsert(ov, ovN, kqOvHash(b, v), rv[k], chained, full);
       }
       __syncthreads();
+      const bool ovUsed = __builtin_amdgcn_readfirstlane(*ovN) != 0;  // no insert until the next build
       // ---- the next span's words stream in while this one probes
       if (i + 1 < cnt) {
         const BPSpan d = desc[i + 1];
@@ -493,22 +504,18 @@ __global__ __launch_bounds__(T, MINW) void bpKeyQuotientKernel(KsSrc<T, K, true>
         S.load(d.sb, d.ns, nsv);
       }
       // ---- probe: first batch from registers, later batches loaded inline
-      matches += kqProbeBatch<T, K>(sv, ns, s, tab2, ov);
+      matches += kq4ProbeBatch<T, K>(sv, ns, s, h0, h1, fill, ov);
       for (uint32_t b0 = BATCH; b0 < ns; b0 += BATCH) {
         uint64_t xv[K];
         S.load(sb + b0, ns - b0, xv);
-        matches += kqProbeBatch<T, K>(xv, ns - b0, s, tab2, ov);
+        matches += kq4ProbeBatch<T, K>(xv, ns - b0, s, h0, h1, fill, ov);
       }
       __syncthreads();  // every probe of this span is done
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        if (pos[k] == KQ_NONE) continue;
-        if (pos[k] & KQ_OV_FLAG)
-          ov[pos[k] & ~KQ_OV_FLAG] = KQ_OV_EMPTY;
-        else
-          tab[pos[k]] = KQ_EMPTY;
+      clearFill();      // (slots keep stale keys: the counts hide them)
+      if (ovUsed) {
+        for (uint32_t j = t; j < KQ_OV; j += T) ov[j] = KQ_OV_EMPTY;
+        if (t == 0) *ovN = 0;
       }
-      if (t == 0) *ovN = 0;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         rv[k] = nrv[k];
@@ -534,13 +541,13 @@ bool bpKeyCountedFits(const BPArgs &a) {
 
 static void launchKeyQuotient(const BPArgs &a, const BPSpan *spans, const uint32_t *nSpans, uint32_t capacity,
                               uint32_t *queue, hipStream_t st) {
-  constexpr int T = 512, K = 4;
+  constexpr int T = 1024, K = 2;
   HJ_CHECK(bpKeyQuotientFits(a), "buildProbeKeySpans: quotient table needs split key-only words of <= %u bits "
            "(got %u) and rChunk <= 2048 (got %u)", 32 + KQ_BITS, a.keyFragBits, a.rChunk);
   HJ_CHECK(a.sideOverflow, "buildProbeKeySpans: quotient table needs a flag word");
   const uint32_t s = a.keyFragBits > 32 ? a.keyFragBits - 32 : 0;
   const size_t lds = bpKeyQuotientLdsBytes();
-  const uint32_t perCu = (uint32_t)std::max<size_t>(1, std::min<size_t>(4, (160 * 1024) / lds));
+  const uint32_t perCu = (uint32_t)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / lds));
   const dim3 grid(std::min<uint32_t>(ceilDiv(capacity, KS_CHUNK), 256 * perCu));
   HIP_CHECK(hipMemsetAsync(queue, 0, sizeof(uint32_t), st));
   hipLaunchKernelGGL((bpKeyQuotientKernel<T, K, 8>), grid, dim3(T), lds, st, KsSrc<T, K, true>{a.R, a.Rhi},
@@ -809,7 +816,7 @@ void buildProbeKeySpans(const BPArgs &a, const BPSpan *spans, const uint32_t *nS
   }
   const size_t lds = bpKeySpanLdsBytes(a.rChunk);
   HJ_CHECK(lds <= 160 * 1024, "buildProbeKeySpans: LDS %zu B exceeds 160 KiB (rChunk=%u)", lds, a.rChunk);
-  const uint32_t perCu = (uint32_t)std::max<size_t>(1, std::min<size_t>(4, (160 * 1024) / lds));
+  const uint32_t perCu = (uint32_t)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / lds));
   const dim3 grid(std::min<uint32_t>(ceilDiv(capacity, KS_CHUNK), 256 * perCu));
   HIP_CHECK(hipMemsetAsync(queue, 0, sizeof(uint32_t), s));
 #define HJ_KS(SPLIT)                                                                                             \

@@ -393,38 +393,65 @@ def test_key_only_outer_past_2g_elements(C):
     ctx.reset_scratch()
 
 
+KQ_M = 0xFFFFFFFF
+
+
+def kq_salt(b):
+    return ((b + 1) * 0x85EBCA77) & KQ_M
+
+
+def kq_home(v, lo_bits=0):
+    return ((((v * 0x9E3779B1) & KQ_M) >> 20) ^ lo_bits) & 0xFFF
+
+
+def kq_fragment(b, e, s, tag=0):
+    """The fragment (f = 32 + s bits) whose counted-table key is (bucket b,
+    stored value e ^ salt(b), tag): key_tables.hip kqKey inverted."""
+    lo = kq_home(e, b) | (tag << 12)
+    return (e << s) | lo
+
+
+def kq4_fragment(b, v, s=12):
+    """The fragment whose quotient-table key is (home bucket b, stored value
+    v): key_tables.hip kq4Key inverted (s = 12: 44-bit fragments)."""
+    return (v << s) | kq_home(v, b)
+
+
 def quotient_escape_fragments(n, first_bucket=0):
-    """Fragments the quotient table (build_probe.hip, bpKeyQuotientKernel) can
-    only hold in its side list: 44-bit fragments f (63-bit keys above 10 + 9
-    radix bits) whose stored value e ^ salt(b) is the empty marker, one per
-    bucket b: e = ~salt(b), lo = b ^ h(e)."""
-    M = 0xFFFFFFFF
-    out = []
-    for b in range(first_bucket, first_bucket + n):
-        e = ~(((b + 1) * 0x85EBCA77) & M) & M
-        lo = (b ^ (((e * 0x9E3779B1) & M) >> 20)) & 0xFFF
-        out.append((e << 12) | lo)
-    return out
+    """Fragments whose counted-table value e ^ salt(b) is that table's empty
+    marker, one per bucket b (44-bit fragments: 63-bit keys above 10 + 9
+    radix bits): e = ~salt(b)."""
+    return [kq_fragment(b, ~kq_salt(b) & KQ_M, 12) for b in range(first_bucket, first_bucket + n)]
+
+
+def quotient_crowd_fragments(n, bucket=17):
+    """n distinct fragments with the same quotient-table home bucket: four
+    fill its slots, the rest go to the overflow table (cap 384 per span)."""
+    return [kq4_fragment(bucket, 0x9E370001 + 7919 * i) for i in range(n)]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n_escape,dup,key_count,reruns",
-                         [(20, 1, 8, 0), (40, 3, 8, 0), (100, 1, 8, 0), (400, 1, 8, 1), (20, 1, 9, 0), (300, 3, 9, 0)])
-def test_key_quotient_escapes(C, n_escape, dup, key_count, reruns):
-    """Quotient / counted build/probe with keys whose stored value is the
-    table's empty marker, all in one final partition.  The quotient table
-    (key_count 8) keeps them in its overflow table of full fragments (up to
-    384 per span); 400 fill it: the count is void and the build/probe re-runs
-    on counted tables (1 re-run), which hold escapes inline, as many as any
-    other key.  Repeated inner keys (dup 3) are seen at plan time: counted
-    tables from the first join.  Counts equal a torch oracle every time;
-    later joins of the same HashJoin start where the first ended (no
+@pytest.mark.parametrize("kind,n,dup,key_count,reruns",
+                         [("crowd", 20, 1, 8, 0), ("crowd", 40, 3, 8, 0), ("crowd", 100, 1, 8, 0),
+                          ("crowd", 400, 1, 8, 1), ("escape", 40, 1, 8, 0), ("escape", 20, 1, 9, 0),
+                          ("escape", 300, 3, 9, 0)])
+def test_key_quotient_escapes(C, kind, n, dup, key_count, reruns):
+    """Quotient / counted build/probe on adversarial keys, all in one final
+    partition.  crowd: n keys share one quotient-table home bucket -- 4 in its
+    slots, the rest in the overflow table of full fragments (up to 384 per
+    span); 400 fill it: the count is void and the build/probe re-runs on
+    counted tables (1 re-run).  escape: keys whose counted-table value is that
+    table's empty marker -- counted tables hold them inline, the quotient
+    table (no marker) as any other key.  Repeated inner keys (dup 3) are seen
+    at plan time or by the overflow chains.  Counts equal a torch oracle every
+    time; later joins of the same HashJoin start where the first ended (no
     re-run)."""
     import torch
     from helpers import ref_join_count
-    g = torch.Generator().manual_seed(n_escape * 7 + dup)
-    part = 0x2A5F3  # one (network, local) digit pair: the escapes share a span
-    esc = torch.tensor(quotient_escape_fragments(n_escape, first_bucket=17), dtype=torch.int64)
+    g = torch.Generator().manual_seed(n * 7 + dup + key_count)
+    part = 0x2A5F3  # one (network, local) digit pair: the keys share a span
+    frags = quotient_crowd_fragments(n) if kind == "crowd" else quotient_escape_fragments(n, first_bucket=17)
+    esc = torch.tensor(frags, dtype=torch.int64)
     esc_keys = (esc << 19) | part
     other = torch.randint(1 << 40, (1 << 62) - 1, (400_000,), generator=g, dtype=torch.int64).unique()
     rk = torch.cat([esc_keys.repeat(dup), other])
@@ -444,34 +471,21 @@ def test_key_quotient_escapes(C, n_escape, dup, key_count, reruns):
     assert j.plan.key_only and j.plan.split_local and j.plan.key_bits == 63, j.plan
     for i in range(2):
         res = j.run()
-        assert res["global_matches"] == exp, (n_escape, dup, res["global_matches"], exp)
+        assert res["global_matches"] == exp, (kind, n, dup, res["global_matches"], exp)
         assert res["reruns"] == (reruns if i == 0 else 0), (i, res["reruns"])
-
-
-KQ_M = 0xFFFFFFFF
-
-
-def kq_salt(b):
-    return ((b + 1) * 0x85EBCA77) & KQ_M
-
-
-def kq_fragment(b, e, s, tag=0):
-    """The fragment (f = 32 + s bits) whose quotient-table key is (bucket b,
-    stored value e ^ salt(b), tag): build_probe.hip kqKey inverted."""
-    lo = ((b ^ (((e * 0x9E3779B1) & KQ_M) >> 20)) & 0xFFF) | (tag << 12)
-    return (e << s) | lo
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("key_count,frag_bits", [(8, 44), (9, 44), (8, 48)])
 def test_key_tables_no_foreign_matches(C, key_count, frag_bits):
     """Quotient and counted tables store a key as (bucket, 32-bit value[, tag])
-    that names it only in its home bucket.  Three inner keys share home bucket
-    h (the third is displaced); every outer probe key B(X, d) has home h + d
-    and the SAME stored value and tag as inner key X: a table that compared a
-    displaced entry without its home would count B as X.  Exact counts
-    against a torch oracle on the quotient table (44-bit fragments), counted
-    tables (key_count 9) and the 48-bit counted path (8 + 7 radix bits)."""
+    that names it only in its home bucket.  Inner keys share home bucket h
+    (quotient table: six, so two sit in the overflow table; counted tables:
+    three, the third displaced); every outer probe key B(X, d) has home h + d
+    and the SAME stored value and tag as inner key X: a table that compared an
+    entry without its home would count B as X.  Exact counts against a torch
+    oracle on the quotient table (44-bit fragments), counted tables
+    (key_count 9) and the 48-bit counted path (8 + 7 radix bits)."""
     import torch
     from helpers import ref_join_count
     s = frag_bits - 32
@@ -480,21 +494,29 @@ def test_key_tables_no_foreign_matches(C, key_count, frag_bits):
     part = 0x2A5F3 & ((1 << bits) - 1)
     g = torch.Generator().manual_seed(frag_bits * 10 + key_count)
     h = 1000
-    tags = [0, 0, 0] if s <= 12 else [3, 3, 11]
-    es = [0x80000000 | int(x) for x in torch.randint(0, 1 << 31, (3,), generator=g)]
-    inner = [kq_fragment(h, e, s, t) for e, t in zip(es, tags)]
-    vs = [e ^ kq_salt(h) for e in es]
+    quotient = key_count == 8 and frag_bits == 44
+    n_in = 6 if quotient else 3
+    tags = [0] * n_in if s <= 12 else [3, 3, 11]
+    es = [0x80000000 | int(x) for x in torch.randint(0, 1 << 31, (n_in,), generator=g)]
     probes = []
-    for v, t in zip(vs, tags):
-        for d in (1, 2, 3, 4):
-            probes.append(kq_fragment(h + d, v ^ kq_salt(h + d), s, t))
+    if quotient:
+        inner = [kq4_fragment(h, e) for e in es]
+        for e in es:
+            for d in (1, 2, 3, 4):
+                probes.append(kq4_fragment(h + d, e))
+    else:
+        inner = [kq_fragment(h, e, s, t) for e, t in zip(es, tags)]
+        vs = [e ^ kq_salt(h) for e in es]
+        for v, t in zip(vs, tags):
+            for d in (1, 2, 3, 4):
+                probes.append(kq_fragment(h + d, v ^ kq_salt(h + d), s, t))
     assert not set(probes) & set(inner)
     key = lambda f: (torch.tensor(f, dtype=torch.int64) << bits) | part
     other = torch.randint(1 << 40, (1 << 62) - 1, (200_000,), generator=g, dtype=torch.int64).unique()
     rk = torch.cat([key(inner), other])
     sk = torch.cat([key(probes).repeat(7), key(inner).repeat(3), other[:50_000]])
     exp = ref_join_count(rk, sk)
-    assert exp == 9 + 50_000
+    assert exp == 3 * n_in + 50_000
     rows = lambda k: torch.stack([k, torch.arange(k.numel())], 1).contiguous().cuda()
     R, S = rows(rk), rows(sk)
     ctx = C.ExecContext("device", 0, C.LocalCommunicator())
