@@ -599,9 +599,11 @@ __global__ __launch_bounds__(T) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R
     const bool compacted = sp.flags & 1u;
     // ---- build: nr <= rChunk <= BATCH, one pass
     uint64_t rv[K];
+    uint32_t used[K];  // the entry each lane claimed or added to: cleared after the probe
     R.load(sp.rb, sp.nr, rv);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
+      used[k] = KQ_BUCKETS;
       if ((uint32_t)(k * T) + t >= sp.nr) continue;
       const uint32_t add = compacted ? rCounts[sp.rb + (uint32_t)(k * T) + t] : 1u;
       uint32_t e, v, tg;
@@ -613,6 +615,7 @@ __global__ __launch_bounds__(T) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R
         const unsigned long long o = atomicCAS(&tab64[e], ~0ull, ((unsigned long long)hi << 32) | vs);
         if (o == ~0ull || ((uint32_t)o == vs && (uint32_t)(o >> 32) == hi)) {
           atomicAdd(&cnt[e], add);
+          used[k] = e;
           break;
         }
         e = (e + 1) & (KQ_BUCKETS - 1);
@@ -627,7 +630,14 @@ __global__ __launch_bounds__(T) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R
       matches += kqProbeCounted<T, K>(xv, ns, s, tab2, cnt);
     }
     __syncthreads();
-    clear();
+    // Only the entries this span used (a few per lane instead of the whole
+    // 48 KiB table); copies of a key clear the same entry.
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (used[k] >= KQ_BUCKETS) continue;
+      tab64[used[k]] = ~0ull;
+      cnt[used[k]] = 0;
+    }
     __syncthreads();
   }
   const unsigned long long total = blockReduceSum<T, unsigned long long>((unsigned long long)matches, wsum);
