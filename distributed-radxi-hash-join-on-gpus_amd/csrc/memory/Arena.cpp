@@ -87,7 +87,7 @@ Arena::~Arena() { releaseAll(); }
 
 void Arena::releaseAll() {
   if (!fallbacks_.empty() || !chunks_.empty()) ++generation_;
-  for (auto &f : fallbacks_) rawFree(loc_, f.first);
+  for (auto &f : fallbacks_) rawFree(loc_, f.p);
   fallbacks_.clear();
   fallbackBytes_ = 0;
   for (auto &c : chunks_) rawFree(loc_, c.base);
@@ -169,7 +169,7 @@ void *Arena::get(uint64_t bytes) {
   }
   void *p = rawAlloc(loc_, sz, device_);
   const uint64_t accounted = sz + (align > ALIGNMENT ? align : 0);  // room for the padding once sub-allocated
-  fallbacks_.emplace_back(p, accounted);
+  fallbacks_.push_back(Fallback{p, sz, accounted});
   fallbackBytes_ += accounted;
   peakFallback_ = std::max(peakFallback_, fallbackBytes_);
   const uint64_t u = used() + fallbackBytes_;
@@ -178,16 +178,18 @@ void *Arena::get(uint64_t bytes) {
 }
 
 void Arena::reset() {
-  if (!fallbacks_.empty() || peakFallback_) {
-    for (auto &f : fallbacks_) rawFree(loc_, f.first);
-    if (!fallbacks_.empty()) ++generation_;
-    fallbacks_.clear();
-    fallbackBytes_ = 0;
-    // One new chunk holds every allocation that overflowed (+1/8 slack); the
-    // existing chunks keep their memory (and peers' mappings of it).
-    addChunk(peakFallback_ + peakFallback_ / 8, false);
-    peakFallback_ = 0;
-  }
+  // The last join's fallback allocations become chunks: a join that repeats
+  // the allocation sequence fits them again (first fit, in order), and
+  // nothing is freed, so generation() -- and every peer's IPC mapping of
+  // them -- stays valid.  (Freeing them and adding one consolidated chunk
+  // meant a peer re-imported a new allocation at the address range it had
+  // just unmapped; at 8 ranks on one GPU that second join's one-sided puts
+  // missed the windows.)  Consolidation happens where a join is planned:
+  // ensure() with nothing handed out re-lays everything out as one chunk.
+  for (auto &f : fallbacks_) chunks_.push_back(Chunk{static_cast<uint8_t *>(f.p), f.bytes, 0});
+  fallbacks_.clear();
+  fallbackBytes_ = 0;
+  peakFallback_ = 0;
   for (auto &c : chunks_) c.used = 0;
 }
 
@@ -203,17 +205,17 @@ void *Arena::allocationOf(const void *p) const {
   for (const auto &c : chunks_)
     if (q >= c.base && q < c.base + c.cap) return c.base;
   for (const auto &f : fallbacks_) {
-    const uint8_t *b = static_cast<const uint8_t *>(f.first);
-    if (q >= b && q < b + f.second) return f.first;
+    const uint8_t *b = static_cast<const uint8_t *>(f.p);
+    if (q >= b && q < b + f.bytes) return f.p;
   }
   return nullptr;
 }
 
 void Arena::freeFallback(void *p) {
   for (size_t i = 0; i < fallbacks_.size(); ++i)
-    if (fallbacks_[i].first == p) {
+    if (fallbacks_[i].p == p) {
       rawFree(loc_, p);
-      fallbackBytes_ -= fallbacks_[i].second;
+      fallbackBytes_ -= fallbacks_[i].accounted;
       fallbacks_.erase(fallbacks_.begin() + i);
       ++generation_;
       return;

@@ -10,15 +10,14 @@
 //
 // Growth never moves or frees memory a previous join used: when a join needs
 // more than the chunks hold, the overflow is served by individual
-// allocations and reset() adds ONE new chunk sized for that overflow, so the
-// next join with the same allocation sequence fits (first fit over the chunks
-// in order) and steady-state joins never allocate.  ensure() grows ahead of
+// allocations, which reset() keeps as chunks, so the next join with the same
+// allocation sequence fits (first fit over the chunks in order) and
+// steady-state joins never allocate.  ensure() grows ahead of
 // time (HashJoin reserves its plan's estimate at construction) and can touch
 // the new pages once, so a first join does not pay the first-touch cost;
 // between joins it re-lays the chunks out as one chunk of the request (the
 // total never ratchets to old chunks + request), and trim() gives memory back.
-// generation() counts FREES only (releaseAll, reset() dropping fallbacks,
-// freeFallback, trim): an address a peer mapped (one-sided windows) stays
+// generation() counts FREES only (releaseAll, freeFallback, trim): an address a peer mapped (one-sided windows) stays
 // valid until then, and frees happen only between joins, so a peer's
 // mappings of one join all carry one generation and an import never has to
 // close a mapping the same join still uses (core/ExecContext::ipcImport).
@@ -58,7 +57,7 @@ class Arena {
   void *get(uint64_t bytes);          // bump-allocate (fallback allocation when exhausted)
   template <typename T>
   T *getArray(uint64_t count) { return reinterpret_cast<T *>(get(count * sizeof(T))); }
-  void reset();                       // rewind; add a chunk for the last overflow, if any
+  void reset();                       // rewind; the last join's fallback allocations become chunks
   void releaseAll();
 
   Location location() const { return loc_; }
@@ -91,7 +90,12 @@ class Arena {
   uint64_t fallbackBytes_ = 0;
   uint64_t peakFallback_ = 0;  // largest fallbackBytes_ since the last reset
   uint64_t generation_ = 0;
-  std::vector<std::pair<void *, uint64_t>> fallbacks_;
+  struct Fallback {
+    void *p;
+    uint64_t bytes;      // allocated
+    uint64_t accounted;  // + the big-buffer alignment it would need inside a chunk
+  };
+  std::vector<Fallback> fallbacks_;
 };
 
 }  // namespace memory

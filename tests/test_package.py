@@ -120,9 +120,10 @@ def test_arena_growth_and_generation(C):
     """Workspace arena rules (memory/Arena.h): growth -- a fallback allocation
     or a chunk added mid-join -- keeps generation() (peers' IPC mappings of
     the same join stay open, core/ExecContext::ipcImport); only frees bump
-    it; ensure() with nothing handed out re-lays the chunks out as one chunk
-    of the request instead of adding the request on top; trim gives the
-    memory back."""
+    it; reset() keeps the fallback allocations as chunks, so a repeated
+    allocation sequence allocates nothing; ensure() with nothing handed out
+    re-lays the chunks out as one chunk of the request instead of adding the
+    request on top; trim gives the memory back."""
     MiB = 1 << 20
     ctx = C.ExecContext("host", -1, C.LocalCommunicator())
     g0 = ctx.workspace_generation()
@@ -132,11 +133,15 @@ def test_arena_growth_and_generation(C):
     ctx.workspace_scratch(8 * MiB)  # does not fit: a fallback allocation
     ctx.ensure_workspace(10 * MiB)  # in use: adds the 6 MiB shortfall, not 10
     assert ctx.workspace_capacity() == 10 * MiB and ctx.workspace_generation() == g0
-    ctx.reset_scratch()  # frees the fallback, adds a chunk for it
-    assert ctx.workspace_generation() == g0 + 1 and ctx.workspace_capacity() > 10 * MiB
-    assert ctx.trim_workspace(0) > 10 * MiB and ctx.workspace_capacity() == 0
-    assert ctx.workspace_generation() == g0 + 2
+    ctx.reset_scratch()  # the fallback becomes a chunk: nothing freed
+    assert ctx.workspace_generation() == g0 and ctx.workspace_capacity() == 18 * MiB
+    ctx.workspace_scratch(1 * MiB)
+    ctx.workspace_scratch(8 * MiB)  # the same sequence fits the chunks again: no allocation
+    assert ctx.workspace_capacity() == 18 * MiB and ctx.workspace_generation() == g0
+    ctx.reset_scratch()
+    assert ctx.trim_workspace(0) == 18 * MiB and ctx.workspace_capacity() == 0
+    assert ctx.workspace_generation() == g0 + 1
     ctx.ensure_workspace(4 * MiB)
-    assert ctx.workspace_generation() == g0 + 2
+    assert ctx.workspace_generation() == g0 + 1
     ctx.ensure_workspace(8 * MiB)  # nothing handed out: one chunk of 8 MiB, not 4 + 8
-    assert ctx.workspace_capacity() == 8 * MiB and ctx.workspace_generation() == g0 + 3
+    assert ctx.workspace_capacity() == 8 * MiB and ctx.workspace_generation() == g0 + 2
