@@ -464,7 +464,56 @@ __global__ __launch_bounds__(T, MINW) void bpKeyQuotientKernel(KsSrc<T, K, true>
   if (t == 0) *ovN = 0;
   uint64_t matches = 0;
   bool full = false, chained = false;
-  uint64_t rv[K], sv[K], nrv[K], nsv[K];
+  // Spans i + 1 and i + 2 are in flight while span i builds and probes (a
+  // span is ~2.6 us of a workgroup's time at two workgroups per CU; the loads
+  // of the next span alone, issued after the build, did not cover HBM latency
+  // under load).  Three register sets in fixed roles (the span loop unrolled
+  // by three): a copy between sets would make the compiler wait for the
+  // copied loads (vmcnt(0)) at the end of every span.  Every load is issued
+  // unconditionally -- past the chunk's end it re-reads its last span -- so
+  // the waits stay counted.
+  uint64_t ra[K], sa[K], rb[K], sb[K], rc[K], sc[K];
+  auto loadSpan = [&](const BPSpan &d, uint64_t (&rr)[K], uint64_t (&ss)[K]) {
+    R.load(d.rb, d.nr, rr);
+    S.load(d.sb, d.ns, ss);
+  };
+  // Span i from (rv, sv); span i + 2 loads into (rn, sn), the set span i - 1 used.
+  auto span = [&](uint32_t i, uint32_t cnt, const uint64_t (&rv)[K], const uint64_t (&sv)[K], uint64_t (&rn)[K],
+                  uint64_t (&sn)[K]) {
+    const uint64_t s0 = uniform64(desc[i].sb);
+    const uint32_t nr = __builtin_amdgcn_readfirstlane(desc[i].nr);
+    const uint32_t ns = __builtin_amdgcn_readfirstlane(desc[i].ns);
+    // ---- build (nr <= BATCH: one batch, from registers): the old count is the slot
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      uint32_t b, v;
+      kq4Key(rv[k], s, b, v);
+      if ((uint32_t)(k * T) + t >= nr) continue;
+      const uint32_t sh = (b & 1u) * 16u;
+      const uint32_t slot = (atomicAdd(&fill2[b >> 1], 1u << sh) >> sh) & 0xFFFFu;
+      if (slot < KQ_SLOTS)
+        slots[(slot >> 1) * (2 * KQ_BUCKETS) + 2 * b + (slot & 1u)] = v;
+      else
+        kqOvInsert(ov, ovN, kqOvHash(b, v), rv[k], chained, full);
+    }
+    __syncthreads();
+    const bool ovUsed = __builtin_amdgcn_readfirstlane(*ovN) != 0;  // no insert until the next build
+    loadSpan(desc[min(i + 2, cnt - 1)], rn, sn);
+    // ---- probe: first batch from registers, later batches loaded inline
+    matches += kq4ProbeBatch<T, K>(sv, ns, s, h0, h1, fill, ov);
+    for (uint32_t b0 = BATCH; b0 < ns; b0 += BATCH) {
+      uint64_t xv[K];
+      S.load(s0 + b0, ns - b0, xv);
+      matches += kq4ProbeBatch<T, K>(xv, ns - b0, s, h0, h1, fill, ov);
+    }
+    __syncthreads();  // every probe of this span is done
+    clearFill();      // (slots keep stale keys: the counts hide them)
+    if (ovUsed) {
+      for (uint32_t j = t; j < KQ_OV; j += T) ov[j] = KQ_OV_EMPTY;
+      if (t == 0) *ovN = 0;
+    }
+    __syncthreads();  // table empty again before the next build
+  };
   for (;;) {
     if (t == 0) *qbase = atomicAdd(queue, KS_CHUNK);
     __syncthreads();  // (first round: also orders the table clear before any build)
@@ -473,55 +522,12 @@ __global__ __launch_bounds__(T, MINW) void bpKeyQuotientKernel(KsSrc<T, K, true>
     const uint32_t cnt = min(KS_CHUNK, n - base);
     if (t < cnt) desc[t] = spans[base + t];
     __syncthreads();
-    {
-      const BPSpan d = desc[0];
-      R.load(d.rb, d.nr, rv);
-      S.load(d.sb, d.ns, sv);
-    }
-    for (uint32_t i = 0; i < cnt; ++i) {
-      const uint64_t sb = uniform64(desc[i].sb);
-      const uint32_t nr = __builtin_amdgcn_readfirstlane(desc[i].nr);
-      const uint32_t ns = __builtin_amdgcn_readfirstlane(desc[i].ns);
-      // ---- build (nr <= BATCH: one batch, from registers): the old count is the slot
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        uint32_t b, v;
-        kq4Key(rv[k], s, b, v);
-        if ((uint32_t)(k * T) + t >= nr) continue;
-        const uint32_t sh = (b & 1u) * 16u;
-        const uint32_t slot = (atomicAdd(&fill2[b >> 1], 1u << sh) >> sh) & 0xFFFFu;
-        if (slot < KQ_SLOTS)
-          slots[(slot >> 1) * (2 * KQ_BUCKETS) + 2 * b + (slot & 1u)] = v;
-        else
-          kqOvInsert(ov, ovN, kqOvHash(b, v), rv[k], chained, full);
-      }
-      __syncthreads();
-      const bool ovUsed = __builtin_amdgcn_readfirstlane(*ovN) != 0;  // no insert until the next build
-      // ---- the next span's words stream in while this one probes
-      if (i + 1 < cnt) {
-        const BPSpan d = desc[i + 1];
-        R.load(d.rb, d.nr, nrv);
-        S.load(d.sb, d.ns, nsv);
-      }
-      // ---- probe: first batch from registers, later batches loaded inline
-      matches += kq4ProbeBatch<T, K>(sv, ns, s, h0, h1, fill, ov);
-      for (uint32_t b0 = BATCH; b0 < ns; b0 += BATCH) {
-        uint64_t xv[K];
-        S.load(sb + b0, ns - b0, xv);
-        matches += kq4ProbeBatch<T, K>(xv, ns - b0, s, h0, h1, fill, ov);
-      }
-      __syncthreads();  // every probe of this span is done
-      clearFill();      // (slots keep stale keys: the counts hide them)
-      if (ovUsed) {
-        for (uint32_t j = t; j < KQ_OV; j += T) ov[j] = KQ_OV_EMPTY;
-        if (t == 0) *ovN = 0;
-      }
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        rv[k] = nrv[k];
-        sv[k] = nsv[k];
-      }
-      __syncthreads();  // table empty again before the next build
+    loadSpan(desc[0], ra, sa);
+    loadSpan(desc[min(1u, cnt - 1)], rb, sb);
+    for (uint32_t i = 0; i < cnt; i += 3) {
+      span(i, cnt, ra, sa, rc, sc);
+      if (i + 1 < cnt) span(i + 1, cnt, rb, sb, ra, sa);
+      if (i + 2 < cnt) span(i + 2, cnt, rc, sc, rb, sb);
     }
   }
   const unsigned long long total = blockReduceSum<T, unsigned long long>((unsigned long long)matches, wsum);
