@@ -410,7 +410,7 @@ bool bpKeyCountedFits(const BPArgs &a);
 // The spans bpPlanCounts wrote to a.heavySpans (partitions of repeated inner
 // keys): counted tables (build_probe.hip, bpKeyCountedSpansKernel); adds to
 // a.result.
-void bpKeyCountedSpans(const BPArgs &a, hipStream_t s);
+void bpKeyCountedSpans(const BPArgs &a, uint32_t *queue, hipStream_t s);
 // Compacts the partitions bpPlanCounts listed in a.dedupParts (see BPArgs)
 // and appends their counted spans; run before bpKeyCountedSpans.
 void bpKeyDedup(const BPArgs &a, uint32_t maxParts, bool emitOnly, hipStream_t s);

@@ -578,40 +578,52 @@ static void launchKeyQuotient(const BPArgs &a, const BPSpan *spans, const uint32
 // distinct keys with a count each in BPArgs::dedupCounts, added whole.  A hot
 // key's million copies then cost one table entry instead of ~500 inner
 // chunks each re-reading the partition's outer side.
-template <int T, int K>
-__global__ __launch_bounds__(T) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R, KsSrc<T, K, true> S,
-                                                              const uint32_t *__restrict__ rCounts,
-                                                              const BPSpan *__restrict__ spans,
-                                                              const uint32_t *__restrict__ nSpansPtr, uint32_t capacity,
-                                                              uint32_t s, unsigned long long *__restrict__ result) {
+// Structure as bpKeyQuotientKernel (T = 1024, K = 2): spans from a work queue
+// in chunks of KS_CHUNK, spans i + 1 and i + 2 in flight while span i builds
+// and probes, the span loop unrolled by three over fixed register sets.  The
+// table is 48 KiB; 1024-thread workgroups at <= 64 VGPRs put two on a CU.
+template <int T, int K, int MINW>
+__global__ __launch_bounds__(T, MINW) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R, KsSrc<T, K, true> S,
+                                                                    const uint32_t *__restrict__ rCounts,
+                                                                    const BPSpan *__restrict__ spans,
+                                                                    const uint32_t *__restrict__ nSpansPtr,
+                                                                    uint32_t capacity, uint32_t *__restrict__ queue,
+                                                                    uint32_t s, unsigned long long *__restrict__ result) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned long long *tab64 = reinterpret_cast<unsigned long long *>(smem);  // [entry] value | id << 48 | esc << 47
   const uint2 *tab2 = reinterpret_cast<const uint2 *>(smem);
   uint32_t *cnt = reinterpret_cast<uint32_t *>(tab64 + KQ_BUCKETS);          // [entry] count
-  unsigned long long *wsum = reinterpret_cast<unsigned long long *>(cnt + KQ_BUCKETS);
+  BPSpan *desc = reinterpret_cast<BPSpan *>(cnt + KQ_BUCKETS);
+  unsigned long long *wsum = reinterpret_cast<unsigned long long *>(desc + KS_CHUNK);
+  uint32_t *qbase = reinterpret_cast<uint32_t *>(wsum + T / WAVE);
   constexpr uint32_t BATCH = T * K;
   const uint32_t t = threadIdx.x;
   const uint32_t n = min(*nSpansPtr, capacity);
-  uint64_t matches = 0;
-  auto clear = [&]() {
+  {
     uint4 *t4 = reinterpret_cast<uint4 *>(smem);  // entries (all ones) then counts (zero)
     for (uint32_t i = t; i < KQ_BUCKETS * 12 / 16; i += T)
       t4[i] = i < KQ_BUCKETS / 2 ? make_uint4(KQ_EMPTY, KQ_EMPTY, KQ_EMPTY, KQ_EMPTY) : make_uint4(0, 0, 0, 0);
+  }
+  uint64_t matches = 0;
+  uint64_t ra[K], sa[K], rb[K], sb[K], rc[K], sc[K];
+  auto loadSpan = [&](const BPSpan &d, uint64_t (&rr)[K], uint64_t (&ss)[K]) {
+    R.load(d.rb, d.nr, rr);
+    S.load(d.sb, d.ns, ss);
   };
-  clear();
-  __syncthreads();
-  for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
-    const BPSpan sp = spans[w];
-    const bool compacted = sp.flags & 1u;
+  auto span = [&](uint32_t i, uint32_t nc, const uint64_t (&rv)[K], const uint64_t (&sv)[K], uint64_t (&rn)[K],
+                  uint64_t (&sn)[K]) {
+    const uint64_t r0 = uniform64(desc[i].rb), s0 = uniform64(desc[i].sb);
+    const uint32_t nr = __builtin_amdgcn_readfirstlane(desc[i].nr);
+    const uint32_t ns = __builtin_amdgcn_readfirstlane(desc[i].ns);
+    const bool compacted = __builtin_amdgcn_readfirstlane(desc[i].flags) & 1u;
     // ---- build: nr <= rChunk <= BATCH, one pass
-    uint64_t rv[K];
     uint32_t used[K];  // the entry each lane claimed or added to: cleared after the probe
-    R.load(sp.rb, sp.nr, rv);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       used[k] = KQ_BUCKETS;
-      if ((uint32_t)(k * T) + t >= sp.nr) continue;
-      const uint32_t add = compacted ? rCounts[sp.rb + (uint32_t)(k * T) + t] : 1u;
+      if ((uint32_t)(k * T) + t >= nr) continue;
+      uint32_t add = 1;
+      if (compacted) add = rCounts[r0 + (uint32_t)(k * T) + t];
       uint32_t e, v, tg;
       kqKey(rv[k], s, e, v, tg);
       const uint32_t esc = v == KQ_EMPTY, vs = esc ? 0u : v;
@@ -628,12 +640,13 @@ __global__ __launch_bounds__(T) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R
       }
     }
     __syncthreads();
-    // ---- probe the span's outer words
-    for (uint32_t b0 = 0; b0 < sp.ns; b0 += BATCH) {
-      const uint32_t ns = min(sp.ns - b0, BATCH);
+    loadSpan(desc[min(i + 2, nc - 1)], rn, sn);
+    // ---- probe: first batch from registers, later batches loaded inline
+    matches += kqProbeCounted<T, K>(sv, ns, s, tab2, cnt);
+    for (uint32_t b0 = BATCH; b0 < ns; b0 += BATCH) {
       uint64_t xv[K];
-      S.load(sp.sb + b0, ns, xv);
-      matches += kqProbeCounted<T, K>(xv, ns, s, tab2, cnt);
+      S.load(s0 + b0, ns - b0, xv);
+      matches += kqProbeCounted<T, K>(xv, ns - b0, s, tab2, cnt);
     }
     __syncthreads();
     // Only the entries this span used (a few per lane instead of the whole
@@ -645,23 +658,40 @@ __global__ __launch_bounds__(T) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R
       cnt[used[k]] = 0;
     }
     __syncthreads();
+  };
+  for (;;) {
+    if (t == 0) *qbase = atomicAdd(queue, KS_CHUNK);
+    __syncthreads();  // (first round: also orders the table clear before any build)
+    const uint32_t base = __builtin_amdgcn_readfirstlane(*qbase);
+    if (base >= n) break;
+    const uint32_t nc = min(KS_CHUNK, n - base);
+    if (t < nc) desc[t] = spans[base + t];
+    __syncthreads();
+    loadSpan(desc[0], ra, sa);
+    loadSpan(desc[min(1u, nc - 1)], rb, sb);
+    for (uint32_t i = 0; i < nc; i += 3) {
+      span(i, nc, ra, sa, rc, sc);
+      if (i + 1 < nc) span(i + 1, nc, rb, sb, ra, sa);
+      if (i + 2 < nc) span(i + 2, nc, rc, sc, rb, sb);
+    }
   }
   const unsigned long long total = blockReduceSum<T, unsigned long long>((unsigned long long)matches, wsum);
   if (t == 0 && total) atomicAdd(result, total);
 }
 
-size_t bpKeyCountedLdsBytes() { return KQ_BUCKETS * 12 + 16 * 8 + 16; }
+size_t bpKeyCountedLdsBytes() { return KQ_BUCKETS * 12 + KS_CHUNK * sizeof(BPSpan) + 16 * 8 + 16; }
 
-void bpKeyCountedSpans(const BPArgs &a, hipStream_t st) {
-  constexpr int T = 512, K = 4;
-  HJ_CHECK(bpKeyCountedFits(a) && a.rChunk <= (uint32_t)(T * K) && a.heavySpans && a.heavyCount,
-           "bpKeyCountedSpans: needs split key-only words of <= 48 fragment bits and the heavy span list");
+void bpKeyCountedSpans(const BPArgs &a, uint32_t *queue, hipStream_t st) {
+  constexpr int T = 1024, K = 2;
+  HJ_CHECK(bpKeyCountedFits(a) && a.rChunk <= (uint32_t)(T * K) && a.heavySpans && a.heavyCount && queue,
+           "bpKeyCountedSpans: needs split key-only words of <= 48 fragment bits, the heavy span list and a queue");
   const uint32_t s = a.keyFragBits > 32 ? a.keyFragBits - 32 : 0;
   const size_t lds = bpKeyCountedLdsBytes();
-  const dim3 grid(std::min<uint32_t>(std::max<uint32_t>(a.heavyCapacity, 1), 256 * 3));
-  hipLaunchKernelGGL((bpKeyCountedSpansKernel<T, K>), grid, dim3(T), lds, st, KsSrc<T, K, true>{a.R, a.Rhi},
-                     KsSrc<T, K, true>{a.S, a.Shi}, a.dedupCounts, a.heavySpans, a.heavyCount, a.heavyCapacity, s,
-                     a.result);
+  const dim3 grid(std::min<uint32_t>(std::max<uint32_t>(ceilDiv(a.heavyCapacity, KS_CHUNK), 1), 256 * 2));
+  HIP_CHECK(hipMemsetAsync(queue, 0, sizeof(uint32_t), st));
+  hipLaunchKernelGGL((bpKeyCountedSpansKernel<T, K, 8>), grid, dim3(T), lds, st, KsSrc<T, K, true>{a.R, a.Rhi},
+                     KsSrc<T, K, true>{a.S, a.Shi}, a.dedupCounts, a.heavySpans, a.heavyCount, a.heavyCapacity, queue,
+                     s, a.result);
   HIP_CHECK_LAUNCH();
 }
 

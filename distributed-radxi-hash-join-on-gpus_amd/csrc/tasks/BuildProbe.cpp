@@ -190,7 +190,7 @@ void BuildProbe::execute() {
     }
     if (!counted || args.heavyMin != 0)  // otherwise every span is on the heavy list
       kernels::buildProbeKeySpans(args, spans, nItems, capacity, queue, ctx->stream());
-    if (counted) kernels::bpKeyCountedSpans(args, ctx->stream());
+    if (counted) kernels::bpKeyCountedSpans(args, queue, ctx->stream());  // (the queue word is re-zeroed)
     hipEvent_t done = tl.mark(ctx->stream());
     tl.endAt("BPKERNEL", done);
     tl.endAt("BPTASKTIME", done);
