@@ -356,26 +356,31 @@ __device__ __forceinline__ void kqOvInsert(unsigned long long *ov, uint32_t *ovN
 }
 
 // One batch of T x K outer fragments (the first `valid` counted) against the
-// four-slot table: count, both halves, the overflow table past four keys.
+// four-slot table: the count and slots 0-1 for every probe; slots 2-3 only
+// in lanes whose bucket holds more than two keys (~8 % at 2048 keys per
+// span: an exec-masked read costs the LDS pipe a few lanes, not 64 -- the
+// kernel is LDS-pipe bound, PMC profiles/r4p); the overflow table past four.
 template <int T, int K>
 __device__ __forceinline__ uint32_t kq4ProbeBatch(const uint64_t (&pv)[K], uint32_t valid, uint32_t s,
                                                   const uint2 *h0, const uint2 *h1, const uint16_t *fill,
                                                   const unsigned long long *ov) {
   uint32_t bk[K], v[K], f[K];
-  uint2 x[K], y[K];
+  uint2 x[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     kq4Key(pv[k], s, bk[k], v[k]);
     f[k] = fill[bk[k]];
     x[k] = h0[bk[k]];
-    y[k] = h1[bk[k]];
   }
   uint32_t matches = 0;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    uint32_t c = (uint32_t)(f[k] > 0 && x[k].x == v[k]) + (uint32_t)(f[k] > 1 && x[k].y == v[k]) +
-                 (uint32_t)(f[k] > 2 && y[k].x == v[k]) + (uint32_t)(f[k] > 3 && y[k].y == v[k]);
-    if (f[k] > KQ_SLOTS) c += kqOvCount(ov, kqOvHash(bk[k], v[k]), pv[k]);
+    uint32_t c = (uint32_t)(f[k] > 0 && x[k].x == v[k]) + (uint32_t)(f[k] > 1 && x[k].y == v[k]);
+    if (f[k] > 2) {
+      const uint2 y = h1[bk[k]];
+      c += (uint32_t)(y.x == v[k]) + (uint32_t)(f[k] > 3 && y.y == v[k]);
+      if (f[k] > KQ_SLOTS) c += kqOvCount(ov, kqOvHash(bk[k], v[k]), pv[k]);
+    }
     matches += (uint32_t)(k * T) + threadIdx.x < valid ? c : 0u;
   }
   return matches;

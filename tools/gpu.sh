@@ -12,6 +12,7 @@
 #   py=SCRIPT,ARGS      python SCRIPT ARGS
 #   stats=ARGS          rocprofv3 --kernel-trace --stats of bench.py ARGS
 #   pstats=SCRIPT,ARGS  rocprofv3 --kernel-trace --stats of python SCRIPT ARGS
+#   ppmc=CTRS/SCRIPT,ARGS  rocprofv3 --pmc CTRS of python SCRIPT ARGS
 #   pmc=CTRS/ARGS       rocprofv3 --pmc CTRS (comma-separated) of bench.py ARGS
 #   ebench=ENV/ARGS     bench.py ARGS with ENV (comma-separated K=V, e.g. HPCJOIN_NET_THREADS=512): A/B runs
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -43,6 +44,8 @@ for step in "$@"; do
               -- python "$R/bench.py" $args) > "$log" 2>&1 ;;
     pstats) (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$OUT/stats$n" -o run --output-format csv \
               -- python "$R/"$args) > "$log" 2>&1 ;;
+    ppmc) ctrs=${arg%%/*}; sargs=${arg#*/}; (cd /tmp && timeout -s KILL 600 rocprofv3 --kernel-trace --pmc ${ctrs//,/ } \
+              -d "$OUT/pmc$n" -o run --output-format csv -- python "$R/"${sargs//,/ }) > "$log" 2>&1 ;;
     pmc) ctrs=${arg%%/*}; bargs=${arg#*/}; (cd /tmp && timeout -s KILL 300 rocprofv3 --kernel-trace --pmc ${ctrs//,/ } \
               -d "$OUT/pmc$n" -o run --output-format csv -- python "$R/bench.py" ${bargs//,/ }) > "$log" 2>&1 ;;
     *) echo "unknown step $step"; exit 2 ;;
