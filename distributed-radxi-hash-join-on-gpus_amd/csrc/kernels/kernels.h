@@ -366,10 +366,6 @@ struct BPArgs {
   uint32_t *dedupCount = nullptr;
   uint32_t *dedupCounts = nullptr;
   uint64_t *dedupLen = nullptr;  // [P] compacted words per listed partition (kept for span re-emits)
-  // Counted spans the four-slot counted table could not hold (bpKeyCountedSpans
-  // retries them on the linear table): heavyCapacity spans, u32 count.
-  BPSpan *retrySpans = nullptr;
-  uint32_t *retryCount = nullptr;
   // Kernel variants (KernelVariants::keyCount / rowsLds).
   uint32_t keyCount = 8;
   uint32_t rowsLds = 1;

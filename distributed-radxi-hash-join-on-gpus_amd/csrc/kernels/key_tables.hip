@@ -583,169 +583,32 @@ static void launchKeyQuotient(const BPArgs &a, const BPSpan *spans, const uint32
 // distinct keys with a count each in BPArgs::dedupCounts, added whole.  A hot
 // key's million copies then cost one table entry instead of ~500 inner
 // chunks each re-reading the partition's outer side.
-//
-// ------------------------------------------ counted four-slot table (kc4)
-// The counted spans' main kernel: the quotient kernel's table shape with a
-// count per slot.  2048 buckets x 4 slots; a key of f <= 48 fragment bits
-// (s = f - 32) is (home bucket b, stored value v, tag):
-//   v = bits [s, s + 32),  lo = the low s bits,
-//   b = (lo ^ h(v)) mod 2^11,  tag = lo >> 11 (<= 5 bits),
-// and a slot holds v (value arrays) and count << 5 | tag (count arrays):
-// (b, v, tag) names exactly one fragment, and a key never leaves its home
-// bucket.  A build is one fill-count atomic (the old count is the slot) and
-// two stores; copies of a key in one wave are folded into one insert first
-// (uncompacted spans).  A probe reads the count and slots 0-1, slots 2-3 only
-// past two keys, and the count word only on a value match; all matching
-// slots add (copies that landed in separate slots sum exactly).  Keys past a
-// bucket's fourth go to a small overflow table of (full fragment, count);
-// counts of 2^27 or more go to an eight-entry list the whole span checks.  A
-// span that fills either is void here: its workgroup appends it to the retry
-// list, counted afterwards on the linear table below (bpKeyCountedLinearKernel,
-// which holds any <= 2048 distinct keys).  Round 3-4's linear table alone:
-// 13.0 ms for the Zipf-both sparse 1e9 x 4e9 spans (profiles/r4s), a walk per
-// probe at ~1/2 load.
-constexpr uint32_t KC_BITS = 11;
-constexpr uint32_t KC_BUCKETS = 1u << KC_BITS;
-constexpr uint32_t KC_OV = 512;
-constexpr uint32_t KC_OV_CAP = 3 * KC_OV / 4;
-constexpr uint32_t KC_BIG = 8;
-constexpr uint32_t KC_COUNT_MAX = (1u << 27) - 1;
-
-__device__ __forceinline__ void kcKey(uint64_t frag, uint32_t s, uint32_t &b, uint32_t &v, uint32_t &tag) {
-  v = __builtin_amdgcn_alignbit((uint32_t)(frag >> 32), (uint32_t)frag, s);
-  const uint32_t lo = (uint32_t)frag & ((1u << s) - 1u);
-  b = (lo ^ ((v * 0x9E3779B1u) >> (32 - KC_BITS))) & (KC_BUCKETS - 1);
-  tag = lo >> KC_BITS;
-}
-
-__device__ __forceinline__ uint32_t kcOvHash(uint32_t b, uint32_t v) {
-  return ((v ^ (b << 20)) * 0x9E3779B1u) >> (32 - 9);
-}
-
-struct KcTable {
-  uint2 *val;        // [2][KC_BUCKETS]: slots 0-1, then slots 2-3
-  uint2 *cnt;        // [2][KC_BUCKETS]: count << 5 | tag per slot
-  uint16_t *fill;    // [KC_BUCKETS]
-  unsigned long long *ovKey;  // [KC_OV] full fragment, ~0 = empty
-  uint32_t *ovCnt;            // [KC_OV]
-  unsigned long long *bigKey;  // [KC_BIG]
-  unsigned long long *bigCnt;  // [KC_BIG]
-  uint32_t *ctl;               // [0] overflow inserts, [1] big keys
-};
-
-// Build one fragment with `add` copies.
-__device__ __forceinline__ void kcInsert(const KcTable &tb, uint64_t frag, uint32_t s, uint32_t add) {
-  uint32_t b, v, tg;
-  kcKey(frag, s, b, v, tg);
-  if (add > KC_COUNT_MAX) {
-    const uint32_t j = atomicAdd(&tb.ctl[1], 1u);
-    if (j < KC_BIG) {
-      tb.bigKey[j] = frag;
-      tb.bigCnt[j] = add;
-    }
-    return;
-  }
-  const uint32_t sh = (b & 1u) * 16u;
-  const uint32_t slot = (atomicAdd(reinterpret_cast<uint32_t *>(tb.fill) + (b >> 1), 1u << sh) >> sh) & 0xFFFFu;
-  if (slot < 4) {
-    const uint32_t i = (slot >> 1) * (2 * KC_BUCKETS) + 2 * b + (slot & 1u);
-    reinterpret_cast<uint32_t *>(tb.val)[i] = v;
-    reinterpret_cast<uint32_t *>(tb.cnt)[i] = (add << 5) | tg;
-    return;
-  }
-  if (atomicAdd(&tb.ctl[0], 1u) >= KC_OV_CAP) return;  // span void (ctl[0] > cap): retried
-  for (uint32_t h = kcOvHash(b, v);; h = (h + 1) & (KC_OV - 1))  // < cap entries taken: an empty one exists
-    if (atomicCAS(&tb.ovKey[h], ~0ull, (unsigned long long)frag) == ~0ull) {
-      tb.ovCnt[h] = add;
-      return;
-    }
-}
-
-template <int T, int K>
-__device__ __forceinline__ uint64_t kcProbeBatch(const uint64_t (&pv)[K], uint32_t valid, uint32_t s,
-                                                 const KcTable &tb, bool ovUsed, uint32_t nBig) {
-  uint32_t bk[K], v[K], tg[K], f[K];
-  uint2 x[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    kcKey(pv[k], s, bk[k], v[k], tg[k]);
-    f[k] = tb.fill[bk[k]];
-    x[k] = tb.val[bk[k]];
-  }
-  uint64_t matches = 0;
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    uint32_t c = 0;  // slot and overflow counts are < 2^27 each, their sum per key < 2^32
-    const uint32_t *c32 = reinterpret_cast<const uint32_t *>(tb.cnt);
-    const uint32_t i0 = 2 * bk[k];
-    if (f[k] > 0 && x[k].x == v[k]) {
-      const uint32_t w = c32[i0];
-      c += (w & 31u) == tg[k] ? (w >> 5) : 0u;
-    }
-    if (f[k] > 1 && x[k].y == v[k]) {
-      const uint32_t w = c32[i0 + 1];
-      c += (w & 31u) == tg[k] ? (w >> 5) : 0u;
-    }
-    if (f[k] > 2) {
-      const uint2 y = tb.val[KC_BUCKETS + bk[k]];
-      if (y.x == v[k]) {
-        const uint32_t w = c32[2 * KC_BUCKETS + i0];
-        c += (w & 31u) == tg[k] ? (w >> 5) : 0u;
-      }
-      if (f[k] > 3 && y.y == v[k]) {
-        const uint32_t w = c32[2 * KC_BUCKETS + i0 + 1];
-        c += (w & 31u) == tg[k] ? (w >> 5) : 0u;
-      }
-      if (f[k] > 4 && ovUsed)
-        for (uint32_t h = kcOvHash(bk[k], v[k]);; h = (h + 1) & (KC_OV - 1)) {
-          const unsigned long long y2 = tb.ovKey[h];
-          if (y2 == ~0ull) break;
-          if (y2 == pv[k]) c += tb.ovCnt[h];
-        }
-    }
-    uint64_t big = 0;
-    for (uint32_t j = 0; j < nBig; ++j) big += tb.bigKey[j] == pv[k] ? tb.bigCnt[j] : 0ull;
-    matches += (uint32_t)(k * T) + threadIdx.x < valid ? c + big : 0ull;
-  }
-  return matches;
-}
-
-size_t bpKeyCountedLdsBytes() {
-  return KC_BUCKETS * 8 * 2 * 2 + KC_BUCKETS * 2 + KC_OV * 12 + KC_BIG * 16 + 16 + KS_CHUNK * sizeof(BPSpan) +
-         16 * 8 + 16;
-}
-
+// Structure as bpKeyQuotientKernel (T = 1024, K = 2): spans from a work queue
+// in chunks of KS_CHUNK, spans i + 1 and i + 2 in flight while span i builds
+// and probes, the span loop unrolled by three over fixed register sets.  The
+// table is 48 KiB; 1024-thread workgroups at <= 64 VGPRs put two on a CU.
 template <int T, int K, int MINW>
 __global__ __launch_bounds__(T, MINW) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R, KsSrc<T, K, true> S,
                                                                     const uint32_t *__restrict__ rCounts,
                                                                     const BPSpan *__restrict__ spans,
                                                                     const uint32_t *__restrict__ nSpansPtr,
                                                                     uint32_t capacity, uint32_t *__restrict__ queue,
-                                                                    uint32_t s, unsigned long long *__restrict__ result,
-                                                                    BPSpan *__restrict__ retry,
-                                                                    uint32_t *__restrict__ retryCount) {
+                                                                    uint32_t s, unsigned long long *__restrict__ result) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  KcTable tb;
-  tb.val = reinterpret_cast<uint2 *>(smem);
-  tb.cnt = tb.val + 2 * KC_BUCKETS;
-  tb.ovKey = reinterpret_cast<unsigned long long *>(tb.cnt + 2 * KC_BUCKETS);
-  tb.bigKey = tb.ovKey + KC_OV;
-  tb.bigCnt = tb.bigKey + KC_BIG;
-  tb.ovCnt = reinterpret_cast<uint32_t *>(tb.bigCnt + KC_BIG);
-  tb.fill = reinterpret_cast<uint16_t *>(tb.ovCnt + KC_OV);
-  tb.ctl = reinterpret_cast<uint32_t *>(tb.fill + KC_BUCKETS);
-  BPSpan *desc = reinterpret_cast<BPSpan *>(tb.ctl + 4);
+  unsigned long long *tab64 = reinterpret_cast<unsigned long long *>(smem);  // [entry] value | id << 48 | esc << 47
+  const uint2 *tab2 = reinterpret_cast<const uint2 *>(smem);
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(tab64 + KQ_BUCKETS);          // [entry] count
+  BPSpan *desc = reinterpret_cast<BPSpan *>(cnt + KQ_BUCKETS);
   unsigned long long *wsum = reinterpret_cast<unsigned long long *>(desc + KS_CHUNK);
   uint32_t *qbase = reinterpret_cast<uint32_t *>(wsum + T / WAVE);
   constexpr uint32_t BATCH = T * K;
   const uint32_t t = threadIdx.x;
   const uint32_t n = min(*nSpansPtr, capacity);
-  auto clearFill = [&]() {
-    for (uint32_t i = t; i < KC_BUCKETS / 4; i += T) reinterpret_cast<uint2 *>(tb.fill)[i] = make_uint2(0u, 0u);
-  };
-  clearFill();
-  for (uint32_t i = t; i < KC_OV; i += T) tb.ovKey[i] = ~0ull;
-  if (t < 4) tb.ctl[t] = 0;
+  {
+    uint4 *t4 = reinterpret_cast<uint4 *>(smem);  // entries (all ones) then counts (zero)
+    for (uint32_t i = t; i < KQ_BUCKETS * 12 / 16; i += T)
+      t4[i] = i < KQ_BUCKETS / 2 ? make_uint4(KQ_EMPTY, KQ_EMPTY, KQ_EMPTY, KQ_EMPTY) : make_uint4(0, 0, 0, 0);
+  }
   uint64_t matches = 0;
   uint64_t ra[K], sa[K], rb[K], sb[K], rc[K], sc[K];
   auto loadSpan = [&](const BPSpan &d, uint64_t (&rr)[K], uint64_t (&ss)[K]) {
@@ -758,40 +621,47 @@ __global__ __launch_bounds__(T, MINW) void bpKeyCountedSpansKernel(KsSrc<T, K, t
     const uint32_t nr = __builtin_amdgcn_readfirstlane(desc[i].nr);
     const uint32_t ns = __builtin_amdgcn_readfirstlane(desc[i].ns);
     const bool compacted = __builtin_amdgcn_readfirstlane(desc[i].flags) & 1u;
-    // ---- build: compacted words carry their counts (copies of a key in an
-    // uncompacted span take a slot each; the probe sums every matching slot)
+    // ---- build: nr <= rChunk <= BATCH, one pass
+    uint32_t used[K];  // the entry each lane claimed or added to: cleared after the probe
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const bool lead = (uint32_t)(k * T) + t < nr;
+      used[k] = KQ_BUCKETS;
+      if ((uint32_t)(k * T) + t >= nr) continue;
       uint32_t add = 1;
-      if (compacted && lead) add = rCounts[r0 + (uint32_t)(k * T) + t];
-      if (lead) kcInsert(tb, rv[k], s, add);
+      if (compacted) add = rCounts[r0 + (uint32_t)(k * T) + t];
+      uint32_t e, v, tg;
+      kqKey(rv[k], s, e, v, tg);
+      const uint32_t esc = v == KQ_EMPTY, vs = esc ? 0u : v;
+      // <= 2048 distinct keys in 4096 entries: an empty entry is always reached
+      for (uint32_t dist = 0; dist < KQ_BUCKETS; ++dist) {
+        const uint32_t hi = (kqCountedId(dist, tg) << 16) | (esc << 15);
+        const unsigned long long o = atomicCAS(&tab64[e], ~0ull, ((unsigned long long)hi << 32) | vs);
+        if (o == ~0ull || ((uint32_t)o == vs && (uint32_t)(o >> 32) == hi)) {
+          atomicAdd(&cnt[e], add);
+          used[k] = e;
+          break;
+        }
+        e = (e + 1) & (KQ_BUCKETS - 1);
+      }
     }
     __syncthreads();
-    const uint32_t nOv = __builtin_amdgcn_readfirstlane(tb.ctl[0]);
-    const uint32_t nBig = __builtin_amdgcn_readfirstlane(tb.ctl[1]);
     loadSpan(desc[min(i + 2, nc - 1)], rn, sn);
-    if (nOv > KC_OV_CAP || nBig > KC_BIG) {
-      // Void here: the linear table counts this span afterwards.
-      if (t == 0) {
-        const uint32_t j = atomicAdd(retryCount, 1u);
-        if (j < capacity) retry[j] = desc[i];
-      }
-    } else {
-      // ---- probe: first batch from registers, later batches loaded inline
-      matches += kcProbeBatch<T, K>(sv, ns, s, tb, nOv != 0, nBig);
-      for (uint32_t b0 = BATCH; b0 < ns; b0 += BATCH) {
-        uint64_t xv[K];
-        S.load(s0 + b0, ns - b0, xv);
-        matches += kcProbeBatch<T, K>(xv, ns - b0, s, tb, nOv != 0, nBig);
-      }
+    // ---- probe: first batch from registers, later batches loaded inline
+    matches += kqProbeCounted<T, K>(sv, ns, s, tab2, cnt);
+    for (uint32_t b0 = BATCH; b0 < ns; b0 += BATCH) {
+      uint64_t xv[K];
+      S.load(s0 + b0, ns - b0, xv);
+      matches += kqProbeCounted<T, K>(xv, ns - b0, s, tab2, cnt);
     }
     __syncthreads();
-    clearFill();  // (slots keep stale keys: the counts hide them)
-    if (nOv) {
-      for (uint32_t j = t; j < KC_OV; j += T) tb.ovKey[j] = ~0ull;
+    // Only the entries this span used (a few per lane instead of the whole
+    // 48 KiB table); copies of a key clear the same entry.
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (used[k] >= KQ_BUCKETS) continue;
+      tab64[used[k]] = ~0ull;
+      cnt[used[k]] = 0;
     }
-    if (t < 2) tb.ctl[t] = 0;
     __syncthreads();
   };
   for (;;) {
@@ -814,97 +684,19 @@ __global__ __launch_bounds__(T, MINW) void bpKeyCountedSpansKernel(KsSrc<T, K, t
   if (t == 0 && total) atomicAdd(result, total);
 }
 
-// ----------------------------------------- counted linear table (retries)
-// Spans the four-slot kernel could not hold (a full overflow table or more
-// than eight counts of 2^27+): one entry per distinct key in 4096 entries,
-// linear probing, so any <= 2048 distinct keys fit.  Entry = (value, id, esc)
-// of the salted key above (kqKey, kqProbeCounted), count apart.
-template <int T, int K>
-__global__ __launch_bounds__(T) void bpKeyCountedLinearKernel(KsSrc<T, K, true> R, KsSrc<T, K, true> S,
-                                                               const uint32_t *__restrict__ rCounts,
-                                                               const BPSpan *__restrict__ spans,
-                                                               const uint32_t *__restrict__ nSpansPtr,
-                                                               uint32_t capacity, uint32_t s,
-                                                               unsigned long long *__restrict__ result) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned long long *tab64 = reinterpret_cast<unsigned long long *>(smem);  // [entry] value | id << 48 | esc << 47
-  const uint2 *tab2 = reinterpret_cast<const uint2 *>(smem);
-  uint32_t *cnt = reinterpret_cast<uint32_t *>(tab64 + KQ_BUCKETS);          // [entry] count
-  unsigned long long *wsum = reinterpret_cast<unsigned long long *>(cnt + KQ_BUCKETS);
-  constexpr uint32_t BATCH = T * K;
-  const uint32_t t = threadIdx.x;
-  const uint32_t n = min(*nSpansPtr, capacity);
-  uint64_t matches = 0;
-  if (blockIdx.x < n) {
-    uint4 *t4 = reinterpret_cast<uint4 *>(smem);  // entries (all ones) then counts (zero)
-    for (uint32_t i = t; i < KQ_BUCKETS * 12 / 16; i += T)
-      t4[i] = i < KQ_BUCKETS / 2 ? make_uint4(KQ_EMPTY, KQ_EMPTY, KQ_EMPTY, KQ_EMPTY) : make_uint4(0, 0, 0, 0);
-  }
-  __syncthreads();
-  for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
-    const BPSpan sp = spans[w];
-    const bool compacted = sp.flags & 1u;
-    uint64_t rv[K];
-    uint32_t used[K];
-    R.load(sp.rb, sp.nr, rv);
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      used[k] = KQ_BUCKETS;
-      if ((uint32_t)(k * T) + t >= sp.nr) continue;
-      const uint32_t add = compacted ? rCounts[sp.rb + (uint32_t)(k * T) + t] : 1u;
-      uint32_t e, v, tg;
-      kqKey(rv[k], s, e, v, tg);
-      const uint32_t esc = v == KQ_EMPTY, vs = esc ? 0u : v;
-      for (uint32_t dist = 0; dist < KQ_BUCKETS; ++dist) {  // <= 2048 distinct keys in 4096 entries
-        const uint32_t hi = (kqCountedId(dist, tg) << 16) | (esc << 15);
-        const unsigned long long o = atomicCAS(&tab64[e], ~0ull, ((unsigned long long)hi << 32) | vs);
-        if (o == ~0ull || ((uint32_t)o == vs && (uint32_t)(o >> 32) == hi)) {
-          atomicAdd(&cnt[e], add);
-          used[k] = e;
-          break;
-        }
-        e = (e + 1) & (KQ_BUCKETS - 1);
-      }
-    }
-    __syncthreads();
-    for (uint32_t b0 = 0; b0 < sp.ns; b0 += BATCH) {
-      const uint32_t ns = min(sp.ns - b0, BATCH);
-      uint64_t xv[K];
-      S.load(sp.sb + b0, ns, xv);
-      matches += kqProbeCounted<T, K>(xv, ns, s, tab2, cnt);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      if (used[k] >= KQ_BUCKETS) continue;
-      tab64[used[k]] = ~0ull;
-      cnt[used[k]] = 0;
-    }
-    __syncthreads();
-  }
-  const unsigned long long total = blockReduceSum<T, unsigned long long>((unsigned long long)matches, wsum);
-  if (t == 0 && total) atomicAdd(result, total);
-}
+size_t bpKeyCountedLdsBytes() { return KQ_BUCKETS * 12 + KS_CHUNK * sizeof(BPSpan) + 16 * 8 + 16; }
 
 void bpKeyCountedSpans(const BPArgs &a, uint32_t *queue, hipStream_t st) {
   constexpr int T = 1024, K = 2;
-  HJ_CHECK(bpKeyCountedFits(a) && a.rChunk <= (uint32_t)(T * K) && a.heavySpans && a.heavyCount && queue &&
-               a.retrySpans && a.retryCount,
-           "bpKeyCountedSpans: needs split key-only words of <= 48 fragment bits, the heavy span list, a queue and "
-           "a retry list");
+  HJ_CHECK(bpKeyCountedFits(a) && a.rChunk <= (uint32_t)(T * K) && a.heavySpans && a.heavyCount && queue,
+           "bpKeyCountedSpans: needs split key-only words of <= 48 fragment bits, the heavy span list and a queue");
   const uint32_t s = a.keyFragBits > 32 ? a.keyFragBits - 32 : 0;
   const size_t lds = bpKeyCountedLdsBytes();
   const dim3 grid(std::min<uint32_t>(std::max<uint32_t>(ceilDiv(a.heavyCapacity, KS_CHUNK), 1), 256 * 2));
   HIP_CHECK(hipMemsetAsync(queue, 0, sizeof(uint32_t), st));
-  HIP_CHECK(hipMemsetAsync(a.retryCount, 0, sizeof(uint32_t), st));
   hipLaunchKernelGGL((bpKeyCountedSpansKernel<T, K, 8>), grid, dim3(T), lds, st, KsSrc<T, K, true>{a.R, a.Rhi},
                      KsSrc<T, K, true>{a.S, a.Shi}, a.dedupCounts, a.heavySpans, a.heavyCount, a.heavyCapacity, queue,
-                     s, a.result, a.retrySpans, a.retryCount);
-  HIP_CHECK_LAUNCH();
-  constexpr int LT = 512, LK = 4;
-  hipLaunchKernelGGL((bpKeyCountedLinearKernel<LT, LK>), dim3(256 * 3), dim3(LT), KQ_BUCKETS * 12 + 16 * 8 + 16, st,
-                     KsSrc<LT, LK, true>{a.R, a.Rhi}, KsSrc<LT, LK, true>{a.S, a.Shi}, a.dedupCounts, a.retrySpans,
-                     a.retryCount, a.heavyCapacity, s, a.result);
+                     s, a.result);
   HIP_CHECK_LAUNCH();
 }
 

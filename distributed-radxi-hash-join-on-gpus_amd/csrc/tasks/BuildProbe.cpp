@@ -164,8 +164,6 @@ void BuildProbe::execute() {
     // keyCount 9 (repeated keys seen): every partition on counted tables.
     args.heavyMin = (args.keyCount == 9 || !quotient) ? 0 : args.rChunk;
     args.heavyCount = nItems + 1;  // high half of counters[2]: read back with the rest
-    args.retrySpans = ws.getArray<kernels::BPSpan>(capacity);
-    args.retryCount = ws.getArray<uint32_t>(1);  // zeroed by bpKeyCountedSpans
   }
   if (dedup) {
     if (!dedupCounts) {  // kept for the join: a re-run only re-emits the compacted spans

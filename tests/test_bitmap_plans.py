@@ -430,25 +430,11 @@ def quotient_crowd_fragments(n, bucket=17):
     return [kq4_fragment(bucket, 0x9E370001 + 7919 * i) for i in range(n)]
 
 
-def kc_fragment(b, v, s=12, tag=0):
-    """The fragment whose counted four-slot key is (home bucket b of 2048,
-    stored value v, tag): key_tables.hip kcKey inverted (s >= 11)."""
-    return (v << s) | ((b ^ (((v * 0x9E3779B1) & KQ_M) >> 21)) & 0x7FF) | (tag << 11)
-
-
-def counted_crowd_fragments(n, bucket=17):
-    """n distinct fragments with the same counted-table home bucket: past 4
-    slots and the 384-entry overflow table the span is retried on the linear
-    table."""
-    return [kc_fragment(bucket, 0x9E370001 + 7919 * i) for i in range(n)]
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,n,dup,key_count,reruns",
                          [("crowd", 20, 1, 8, 0), ("crowd", 40, 3, 8, 0), ("crowd", 100, 1, 8, 0),
                           ("crowd", 400, 1, 8, 1), ("escape", 40, 1, 8, 0), ("escape", 20, 1, 9, 0),
-                          ("escape", 300, 3, 9, 0), ("crowd", 20, 1, 9, 0), ("crowd", 300, 3, 9, 0),
-                          ("crowd", 450, 1, 9, 0)])
+                          ("escape", 300, 3, 9, 0)])
 def test_key_quotient_escapes(C, kind, n, dup, key_count, reruns):
     """Quotient / counted build/probe on adversarial keys, all in one final
     partition.  crowd: n keys share one quotient-table home bucket -- 4 in its
@@ -459,17 +445,12 @@ def test_key_quotient_escapes(C, kind, n, dup, key_count, reruns):
     table (no marker) as any other key.  Repeated inner keys (dup 3) are seen
     at plan time or by the overflow chains.  Counts equal a torch oracle every
     time; later joins of the same HashJoin start where the first ended (no
-    re-run).  key_count 9 crowds fill the counted four-slot table's bucket;
-    450 overflow it and the span is retried on the linear counted table in
-    the same join (no re-run)."""
+    re-run)."""
     import torch
     from helpers import ref_join_count
     g = torch.Generator().manual_seed(n * 7 + dup + key_count)
     part = 0x2A5F3  # one (network, local) digit pair: the keys share a span
-    if kind == "crowd":
-        frags = quotient_crowd_fragments(n) if key_count == 8 else counted_crowd_fragments(n)
-    else:
-        frags = quotient_escape_fragments(n, first_bucket=17)
+    frags = quotient_crowd_fragments(n) if kind == "crowd" else quotient_escape_fragments(n, first_bucket=17)
     esc = torch.tensor(frags, dtype=torch.int64)
     esc_keys = (esc << 19) | part
     other = torch.randint(1 << 40, (1 << 62) - 1, (400_000,), generator=g, dtype=torch.int64).unique()
@@ -498,10 +479,11 @@ def test_key_quotient_escapes(C, kind, n, dup, key_count, reruns):
 @pytest.mark.parametrize("key_count,frag_bits", [(8, 44), (9, 44), (8, 48)])
 def test_key_tables_no_foreign_matches(C, key_count, frag_bits):
     """Quotient and counted tables store a key as (bucket, 32-bit value[, tag])
-    that names it only in its home bucket.  Six inner keys share home bucket
-    h, so two sit in the overflow table; every outer probe key B(X, d) has
-    home h + d and the SAME stored value and tag as inner key X: a table that
-    compared an entry without its home would count B as X.  Exact counts against a torch
+    that names it only in its home bucket.  Inner keys share home bucket h
+    (quotient table: six, so two sit in the overflow table; counted tables:
+    three, the third displaced); every outer probe key B(X, d) has home h + d
+    and the SAME stored value and tag as inner key X: a table that compared an
+    entry without its home would count B as X.  Exact counts against a torch
     oracle on the quotient table (44-bit fragments), counted tables
     (key_count 9) and the 48-bit counted path (8 + 7 radix bits)."""
     import torch
@@ -513,12 +495,21 @@ def test_key_tables_no_foreign_matches(C, key_count, frag_bits):
     g = torch.Generator().manual_seed(frag_bits * 10 + key_count)
     h = 1000
     quotient = key_count == 8 and frag_bits == 44
-    n_in = 6
-    tags = [0] * n_in if s <= 12 else [3, 3, 11, 3, 30, 11]
+    n_in = 6 if quotient else 3
+    tags = [0] * n_in if s <= 12 else [3, 3, 11]
     es = [0x80000000 | int(x) for x in torch.randint(0, 1 << 31, (n_in,), generator=g)]
-    frag = (lambda b, e, t: kq4_fragment(b, e)) if quotient else (lambda b, e, t: kc_fragment(b, e, s, t & ((1 << (s - 11)) - 1)))
-    inner = [frag(h, e, t) for e, t in zip(es, tags)]
-    probes = [frag(h + d, e, t) for e, t in zip(es, tags) for d in (1, 2, 3, 4)]
+    probes = []
+    if quotient:
+        inner = [kq4_fragment(h, e) for e in es]
+        for e in es:
+            for d in (1, 2, 3, 4):
+                probes.append(kq4_fragment(h + d, e))
+    else:
+        inner = [kq_fragment(h, e, s, t) for e, t in zip(es, tags)]
+        vs = [e ^ kq_salt(h) for e in es]
+        for v, t in zip(vs, tags):
+            for d in (1, 2, 3, 4):
+                probes.append(kq_fragment(h + d, v ^ kq_salt(h + d), s, t))
     assert not set(probes) & set(inner)
     key = lambda f: (torch.tensor(f, dtype=torch.int64) << bits) | part
     other = torch.randint(1 << 40, (1 << 62) - 1, (200_000,), generator=g, dtype=torch.int64).unique()
