@@ -397,6 +397,15 @@ __device__ __forceinline__ uint32_t kq4ProbeBatch(const uint64_t (&pv)[K], uint3
 // adds its count to count[e], a separate u32 array read only on a match.
 __device__ __forceinline__ uint32_t kqCountedId(uint32_t dist, uint32_t tag) { return (dist << 4) | tag; }
 
+// 6144 entries (load <= 1/3 at 2048 keys per span, 72 KiB with the counts:
+// two 1024-thread workgroups per CU): home bucket b of 4096 sits at entry
+// b + b / 2, and linear probing wraps at 6144.  At 4096 entries (load 1/2)
+// most waves walked several entries per probe.  dist < 2048 (at most 2048
+// keys), so id = dist << 4 | tag stays within 15 bits.
+constexpr uint32_t KC_E = 6144;
+__device__ __forceinline__ uint32_t kcHome(uint32_t b) { return b + (b >> 1); }
+__device__ __forceinline__ uint32_t kcNext(uint32_t e) { return e + 1 == KC_E ? 0u : e + 1; }
+
 template <int T, int K>
 __device__ __forceinline__ uint64_t kqProbeCounted(const uint64_t (&pv)[K], uint32_t valid, uint32_t s,
                                                    const uint2 *tab2, const uint32_t *cnt) {
@@ -405,6 +414,7 @@ __device__ __forceinline__ uint64_t kqProbeCounted(const uint64_t (&pv)[K], uint
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     kqKey(pv[k], s, bk[k], v[k], tg[k]);
+    bk[k] = kcHome(bk[k]);
     x[k] = tab2[bk[k]];
   }
   uint64_t matches = 0;
@@ -419,8 +429,8 @@ __device__ __forceinline__ uint64_t kqProbeCounted(const uint64_t (&pv)[K], uint
       c = cnt[e];
     else
       walk = x[k].x != KQ_EMPTY;
-    for (uint32_t dist = 1; walk && dist < KQ_BUCKETS; ++dist) {
-      e = (e + 1) & (KQ_BUCKETS - 1);
+    for (uint32_t dist = 1; walk && dist < KC_E; ++dist) {
+      e = kcNext(e);
       const uint2 y = tab2[e];
       if (y.x == vs && y.y == ((kqCountedId(dist, tg[k]) << 16) | (esc << 15))) {
         c = cnt[e];
@@ -597,8 +607,8 @@ __global__ __launch_bounds__(T, MINW) void bpKeyCountedSpansKernel(KsSrc<T, K, t
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned long long *tab64 = reinterpret_cast<unsigned long long *>(smem);  // [entry] value | id << 48 | esc << 47
   const uint2 *tab2 = reinterpret_cast<const uint2 *>(smem);
-  uint32_t *cnt = reinterpret_cast<uint32_t *>(tab64 + KQ_BUCKETS);          // [entry] count
-  BPSpan *desc = reinterpret_cast<BPSpan *>(cnt + KQ_BUCKETS);
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(tab64 + KC_E);          // [entry] count
+  BPSpan *desc = reinterpret_cast<BPSpan *>(cnt + KC_E);
   unsigned long long *wsum = reinterpret_cast<unsigned long long *>(desc + KS_CHUNK);
   uint32_t *qbase = reinterpret_cast<uint32_t *>(wsum + T / WAVE);
   constexpr uint32_t BATCH = T * K;
@@ -606,8 +616,8 @@ __global__ __launch_bounds__(T, MINW) void bpKeyCountedSpansKernel(KsSrc<T, K, t
   const uint32_t n = min(*nSpansPtr, capacity);
   {
     uint4 *t4 = reinterpret_cast<uint4 *>(smem);  // entries (all ones) then counts (zero)
-    for (uint32_t i = t; i < KQ_BUCKETS * 12 / 16; i += T)
-      t4[i] = i < KQ_BUCKETS / 2 ? make_uint4(KQ_EMPTY, KQ_EMPTY, KQ_EMPTY, KQ_EMPTY) : make_uint4(0, 0, 0, 0);
+    for (uint32_t i = t; i < KC_E * 12 / 16; i += T)
+      t4[i] = i < KC_E / 2 ? make_uint4(KQ_EMPTY, KQ_EMPTY, KQ_EMPTY, KQ_EMPTY) : make_uint4(0, 0, 0, 0);
   }
   uint64_t matches = 0;
   uint64_t ra[K], sa[K], rb[K], sb[K], rc[K], sc[K];
@@ -625,15 +635,16 @@ __global__ __launch_bounds__(T, MINW) void bpKeyCountedSpansKernel(KsSrc<T, K, t
     uint32_t used[K];  // the entry each lane claimed or added to: cleared after the probe
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      used[k] = KQ_BUCKETS;
+      used[k] = KC_E;
       if ((uint32_t)(k * T) + t >= nr) continue;
       uint32_t add = 1;
       if (compacted) add = rCounts[r0 + (uint32_t)(k * T) + t];
       uint32_t e, v, tg;
       kqKey(rv[k], s, e, v, tg);
+      e = kcHome(e);
       const uint32_t esc = v == KQ_EMPTY, vs = esc ? 0u : v;
-      // <= 2048 distinct keys in 4096 entries: an empty entry is always reached
-      for (uint32_t dist = 0; dist < KQ_BUCKETS; ++dist) {
+      // <= 2048 distinct keys in 6144 entries: an empty entry is always reached
+      for (uint32_t dist = 0; dist < KC_E; ++dist) {
         const uint32_t hi = (kqCountedId(dist, tg) << 16) | (esc << 15);
         const unsigned long long o = atomicCAS(&tab64[e], ~0ull, ((unsigned long long)hi << 32) | vs);
         if (o == ~0ull || ((uint32_t)o == vs && (uint32_t)(o >> 32) == hi)) {
@@ -641,7 +652,7 @@ __global__ __launch_bounds__(T, MINW) void bpKeyCountedSpansKernel(KsSrc<T, K, t
           used[k] = e;
           break;
         }
-        e = (e + 1) & (KQ_BUCKETS - 1);
+        e = kcNext(e);
       }
     }
     __syncthreads();
@@ -658,7 +669,7 @@ __global__ __launch_bounds__(T, MINW) void bpKeyCountedSpansKernel(KsSrc<T, K, t
     // 48 KiB table); copies of a key clear the same entry.
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      if (used[k] >= KQ_BUCKETS) continue;
+      if (used[k] >= KC_E) continue;
       tab64[used[k]] = ~0ull;
       cnt[used[k]] = 0;
     }
@@ -684,7 +695,7 @@ __global__ __launch_bounds__(T, MINW) void bpKeyCountedSpansKernel(KsSrc<T, K, t
   if (t == 0 && total) atomicAdd(result, total);
 }
 
-size_t bpKeyCountedLdsBytes() { return KQ_BUCKETS * 12 + KS_CHUNK * sizeof(BPSpan) + 16 * 8 + 16; }
+size_t bpKeyCountedLdsBytes() { return KC_E * 12 + KS_CHUNK * sizeof(BPSpan) + 16 * 8 + 16; }
 
 void bpKeyCountedSpans(const BPArgs &a, uint32_t *queue, hipStream_t st) {
   constexpr int T = 1024, K = 2;
