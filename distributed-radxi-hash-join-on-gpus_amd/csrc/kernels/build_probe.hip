@@ -77,7 +77,9 @@ __device__ __forceinline__ uint32_t hash64(uint64_t key, uint32_t tbits) {
 
 // dedupParts (optional, key-only words with repeated keys): partitions with
 // more than rChunk inner tuples are listed there (appended at *dedupCount)
-// for bpKeyDedup, which compacts them and emits their spans itself.
+// for bpKeyDedup, which compacts them and emits their spans itself; those of
+// more than BP_DEDUP_SEG_MIN are also listed in dedupBig (their later
+// segments get workgroups of their own).
 // heavySpans (optional): partitions with more than heavyMin inner tuples
 // (rChunk: more than one table; 0 once repeated keys were seen) get no work
 // items here; their spans go to heavySpans instead (appended at *heavyCount,
@@ -89,13 +91,16 @@ __global__ __launch_bounds__(BPT) void bpPlanCountsKernel(const uint64_t *__rest
                                                           uint32_t sc, uint32_t *counts, BPSpan *__restrict__ heavySpans,
                                                           uint32_t *__restrict__ heavyCount, uint32_t heavyCapacity,
                                                           uint32_t heavyMin, uint32_t *__restrict__ dedupParts,
-                                                          uint32_t *__restrict__ dedupCount) {
+                                                          uint32_t *__restrict__ dedupCount,
+                                                          uint32_t *__restrict__ dedupBig,
+                                                          uint32_t *__restrict__ dedupBigCount) {
   const uint32_t p = blockIdx.x * BPT + threadIdx.x;
   if (p >= P) return;
   const uint64_t nr = partREnd[p] - partR[p], ns = partSEnd[p] - partS[p];
   const uint32_t c = (nr == 0 || ns == 0) ? 0u : (uint32_t)(ceilDiv(nr, rc) * ceilDiv(ns, sc));
   if (dedupParts && nr > rc && c) {  // more than one inner chunk: compacted first (bpKeyDedup), spans after
     dedupParts[atomicAdd(dedupCount, 1u)] = p;
+    if (nr > BP_DEDUP_SEG_MIN) dedupBig[atomicAdd(dedupBigCount, 1u)] = p;
     counts[p] = 0;
     return;
   }
@@ -120,10 +125,11 @@ __global__ __launch_bounds__(BPT) void bpPlanCountsKernel(const uint64_t *__rest
 void bpPlanCounts(const BPArgs &a, uint32_t *counts, hipStream_t s) {
   if (a.P == 0) return;
   HJ_CHECK(!a.heavySpans || a.heavyCount, "bpPlanCounts: heavy spans without their counter");
+  HJ_CHECK(!a.dedupParts || (a.dedupBig && a.dedupBigCount), "bpPlanCounts: compaction list without the big list");
   hipLaunchKernelGGL(bpPlanCountsKernel, dim3(ceilDiv(a.P, BPT)), dim3(BPT), 0, s, a.partR, a.partS,
                      a.partREnd ? a.partREnd : a.partR + 1, a.partSEnd ? a.partSEnd : a.partS + 1, a.P, a.rChunk,
                      a.sChunk, counts, a.heavySpans, a.heavyCount, a.heavyCapacity,
-                     a.heavyMin, a.dedupParts, a.dedupCount);
+                     a.heavyMin, a.dedupParts, a.dedupCount, a.dedupBig, a.dedupBigCount);
   HIP_CHECK_LAUNCH();
 }
 

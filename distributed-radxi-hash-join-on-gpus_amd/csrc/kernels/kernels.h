@@ -365,7 +365,9 @@ struct BPArgs {
   uint32_t *dedupParts = nullptr;
   uint32_t *dedupCount = nullptr;
   uint32_t *dedupCounts = nullptr;
-  uint64_t *dedupLen = nullptr;  // [P] compacted words per listed partition (kept for span re-emits)
+  uint64_t *dedupLen = nullptr;  // [P][BP_DEDUP_SEGS] compacted words per segment (kept for span re-emits)
+  uint32_t *dedupBig = nullptr;       // listed partitions of more than one segment (u32 count at dedupBigCount)
+  uint32_t *dedupBigCount = nullptr;
   // Kernel variants (KernelVariants::keyCount / rowsLds).
   uint32_t keyCount = 8;
   uint32_t rowsLds = 1;
@@ -414,6 +416,10 @@ void bpKeyCountedSpans(const BPArgs &a, uint32_t *queue, hipStream_t s);
 // Compacts the partitions bpPlanCounts listed in a.dedupParts (see BPArgs)
 // and appends their counted spans; run before bpKeyCountedSpans.
 void bpKeyDedup(const BPArgs &a, uint32_t maxParts, bool emitOnly, hipStream_t s);
+// Segments per compacted partition (bpKeyDedup): BPArgs::dedupLen has P of
+// them; a partition of n words has min(16, ceil(n / BP_DEDUP_SEG_MIN)).
+constexpr uint32_t BP_DEDUP_SEGS = 16;
+constexpr uint64_t BP_DEDUP_SEG_MIN = 32768;
 
 // Single-level counting join of unique inner keys (bitmap_join.hip): one
 // workgroup per network partition sets a 2^bits LDS bitmap from the inner

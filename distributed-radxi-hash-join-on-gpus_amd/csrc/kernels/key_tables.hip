@@ -712,35 +712,45 @@ void bpKeyCountedSpans(const BPArgs &a, uint32_t *queue, hipStream_t st) {
 }
 
 // ------------------------------------------------ in-place inner compaction
-// bpKeyDedup: one workgroup per listed partition (more than rChunk inner
-// words, repeated keys known).  It streams the partition's inner words in
+// bpKeyDedup: one workgroup per segment of a listed partition (more than
+// rChunk inner words, repeated keys known; a partition of n words has
+// min(BP_DEDUP_SEGS, ceil(n / 32K)) equal segments, so a hot key's million
+// copies are compacted by up to 16 workgroups instead of one: the largest
+// partition set the kernel's time).  Work items: segment 0 of every listed
+// partition, then segments 1-15 of the partitions bpPlanCounts also listed
+// as big (an item per possible segment of every partition cost ~0.6 ms of
+// empty items at 1e8 x 4e8).  It streams the segment's inner words in
 // 2048-word batches into an LDS table of (full fragment, count) -- 4096
 // entries, 64-bit CAS claims, count adds -- and whenever more than 1024
 // distinct keys are held (so the next batch still fits at load <= 3/4),
-// flushes them back over the partition's own words: word i of the compacted
+// flushes them back over the segment's own words: word i of the compacted
 // list overwrites inner word i, which was already read (a flush writes at most
 // as many entries as words consumed since the last one), with its count at
-// dedupCounts[i].  A key may appear in several flushes; counts then add up in
-// the counted table.  Finally the workgroup emits the partition's counted
-// spans over the compacted words (flags bit 0): ceil(distinct / rChunk) inner
-// chunks instead of ceil(words / rChunk).  The inner words are overwritten, so
-// the caller runs this once per join (not with per-chunk rebuilds); the
-// compacted lengths are kept per partition, and a re-run of the build/probe
-// (span list overflow) only re-emits the spans (emitOnly).
+// dedupCounts[i].  A key may appear in several flushes and segments; counts
+// then add up in the counted table.  Finally the workgroup emits the
+// segment's counted spans over its compacted words (flags bit 0):
+// ceil(distinct / rChunk) inner chunks, each against the partition's whole
+// outer side.  The inner words are overwritten, so the caller runs this once
+// per join (not with per-chunk rebuilds); the compacted lengths are kept per
+// segment, and a re-run of the build/probe (span list overflow) only re-emits
+// the spans (emitOnly).
 constexpr uint32_t KD_ENTRIES = 4096;
 constexpr uint32_t KD_FLUSH = 1024;
+constexpr uint64_t KD_SEG_MIN = BP_DEDUP_SEG_MIN;
 
 template <int T, int K>
 __global__ __launch_bounds__(T) void bpKeyDedupKernel(KsSrc<T, K, true> R, uint32_t *__restrict__ rlo,
                                                        uint16_t *__restrict__ rhi, uint32_t *__restrict__ rCounts,
                                                        const uint32_t *__restrict__ parts,
                                                        const uint32_t *__restrict__ nPartsPtr, uint32_t maxParts,
+                                                       const uint32_t *__restrict__ big,
+                                                       const uint32_t *__restrict__ nBigPtr,
                                                        const uint64_t *__restrict__ partR,
                                                        const uint64_t *__restrict__ partREnd,
                                                        const uint64_t *__restrict__ partS,
                                                        const uint64_t *__restrict__ partSEnd, uint32_t rc, uint32_t sc,
                                                        BPSpan *__restrict__ spans, uint32_t *__restrict__ spanCount,
-                                                       uint32_t spanCapacity, uint64_t *__restrict__ lenByPart,
+                                                       uint32_t spanCapacity, uint64_t *__restrict__ lenBySeg,
                                                        bool emitOnly) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned long long *key = reinterpret_cast<unsigned long long *>(smem);  // [entry] fragment (~0 = empty)
@@ -753,13 +763,23 @@ __global__ __launch_bounds__(T) void bpKeyDedupKernel(KsSrc<T, K, true> R, uint3
     key[i] = ~0ull;
     cnt[i] = 0;
   }
-  for (uint32_t w = blockIdx.x; w < np; w += gridDim.x) {
-    const uint32_t p = parts[w];
-    const uint64_t rb = uniform64(partR[p]);
-    const uint64_t nr = uniform64(partREnd[p]) - rb;
+  // Items: segment 0 of every listed partition, then segments 1-15 of the
+  // partitions listed as big (empty past a partition's segment count).
+  const uint32_t nb = min(*nBigPtr, maxParts);
+  for (uint32_t w = blockIdx.x; w < np + nb * (BP_DEDUP_SEGS - 1); w += gridDim.x) {
+    const uint32_t p = w < np ? parts[w] : big[(w - np) / (BP_DEDUP_SEGS - 1)];
+    const uint32_t sg = w < np ? 0u : 1u + (w - np) % (BP_DEDUP_SEGS - 1);
+    const uint64_t pb = uniform64(partR[p]);
+    const uint64_t pn = uniform64(partREnd[p]) - pb;
+    const uint64_t nseg = min<uint64_t>(BP_DEDUP_SEGS, ceilDiv(pn, KD_SEG_MIN));
+    if (sg >= nseg) continue;  // (uniform: no barrier skipped by part of the workgroup)
+    const uint64_t len = ceilDiv(pn, nseg);
+    const uint64_t rb = pb + sg * len;
+    const uint64_t nr = min<uint64_t>(len, pn - sg * len);
+    const size_t li = (size_t)p * BP_DEDUP_SEGS + sg;
     if (t == 0) {
       ctl[0] = 0;
-      ctl[1] = emitOnly ? (uint32_t)lenByPart[p] : 0u;
+      ctl[1] = emitOnly ? (uint32_t)lenBySeg[li] : 0u;
     }
     __syncthreads();
     auto flush = [&]() {
@@ -820,9 +840,9 @@ __global__ __launch_bounds__(T) void bpKeyDedupKernel(KsSrc<T, K, true> R, uint3
       __syncthreads();
       if (ctl[0] > KD_FLUSH || b0 + BATCH >= nr) flush();
     }
-    // ---- the partition's counted spans over its compacted words
+    // ---- the segment's counted spans over its compacted words
     const uint64_t nd = ctl[1];
-    if (t == 0 && !emitOnly) lenByPart[p] = nd;
+    if (t == 0 && !emitOnly) lenBySeg[li] = nd;
     const uint64_t ns = uniform64(partSEnd[p]) - uniform64(partS[p]);
     const uint32_t nsc = (uint32_t)ceilDiv(ns, sc);
     const uint32_t c = (uint32_t)(ceilDiv(nd, rc) * nsc);
@@ -851,10 +871,11 @@ void bpKeyDedup(const BPArgs &a, uint32_t maxParts, bool emitOnly, hipStream_t s
                a.rChunk <= (uint32_t)(T * K),
            "bpKeyDedup: needs split key-only words, the partition list, the count column and the span list");
   const size_t lds = KD_ENTRIES * 12 + 16;
+  HJ_CHECK(a.dedupBig && a.dedupBigCount, "bpKeyDedup: needs the big-partition list");
   const dim3 grid(std::min<uint32_t>(maxParts, 256 * 3));
   hipLaunchKernelGGL((bpKeyDedupKernel<T, K>), grid, dim3(T), lds, st, KsSrc<T, K, true>{a.R, a.Rhi},
                      static_cast<uint32_t *>(const_cast<void *>(a.R)), const_cast<uint16_t *>(a.Rhi), a.dedupCounts,
-                     a.dedupParts, a.dedupCount, maxParts, a.partR, a.partREnd ? a.partREnd : a.partR + 1, a.partS,
+                     a.dedupParts, a.dedupCount, maxParts, a.dedupBig, a.dedupBigCount, a.partR, a.partREnd ? a.partREnd : a.partR + 1, a.partS,
                      a.partSEnd ? a.partSEnd : a.partS + 1, a.rChunk, a.sChunk, a.heavySpans, a.heavyCount,
                      a.heavyCapacity, a.dedupLen, emitOnly);
   HIP_CHECK_LAUNCH();

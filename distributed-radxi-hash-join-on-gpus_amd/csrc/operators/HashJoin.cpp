@@ -259,7 +259,7 @@ uint64_t HashJoin::workspaceEstimate() const {
       b += slots * ob;
       // Repeated keys on counted tables: the inner side's compaction counts
       // (u32 per slot) and per-partition lengths / lists (BuildProbe, bpKeyDedup).
-      if (r == 0 && plan.keyOnly && plan.variants.keyCount == 9) b += slots * 4 + P * 12;
+      if (r == 0 && plan.keyOnly && plan.variants.keyCount == 9) b += slots * 4 + P * (8 + 8 * kernels::BP_DEDUP_SEGS);
     }
   }
   // Build/probe work lists (items or spans, 32 B) and materialized pairs.

@@ -168,10 +168,12 @@ void BuildProbe::execute() {
   if (dedup) {
     if (!dedupCounts) {  // kept for the join: a re-run only re-emits the compacted spans
       dedupCounts = ws.getArray<uint32_t>(std::max<uint64_t>(windows[0]->getPartitionedCapacity(), 1));
-      dedupLen = ws.getArray<uint64_t>(std::max<uint32_t>(args.P, 1));
+      dedupLen = ws.getArray<uint64_t>((uint64_t)std::max<uint32_t>(args.P, 1) * kernels::BP_DEDUP_SEGS);
     }
     args.dedupParts = ws.getArray<uint32_t>(std::max<uint32_t>(args.P, 1));
     args.dedupCount = reinterpret_cast<uint32_t *>(counters + 1);  // the pair cursor is unused by a count
+    args.dedupBig = ws.getArray<uint32_t>(std::max<uint32_t>(args.P, 1));
+    args.dedupBigCount = reinterpret_cast<uint32_t *>(counters + 1) + 1;  // (zeroed with the counters)
     args.dedupCounts = dedupCounts;
     args.dedupLen = dedupLen;
   }
