@@ -23,6 +23,16 @@ static bool traceAlloc() {
   return on;
 }
 
+// HPCJOIN_ARENA_SKIP_MB=n (experiments): every rewind leaves the first n MiB
+// of the first chunk unused, shifting where a join's buffers land.
+static uint64_t skipBytes() {
+  static const uint64_t b = [] {
+    const char *e = std::getenv("HPCJOIN_ARENA_SKIP_MB");
+    return e && e[0] ? (uint64_t)std::atoll(e) << 20 : 0ull;
+  }();
+  return b;
+}
+
 // HPCJOIN_POISON_ARENA=1: fill every raw allocation with 0xA5 bytes, so code
 // that silently relies on zeroed workspace memory fails loudly (debugging).
 static bool poisonAlloc() {
@@ -128,9 +138,10 @@ void Arena::reserve(uint64_t bytes) {
 }
 
 uint64_t Arena::ensure(uint64_t bytes, bool touch, void *stream) {
+  bytes += skipBytes();
   const uint64_t have = capacity();
   if (have >= bytes) return 0;
-  if (used() == 0 && fallbacks_.empty()) {
+  if (used() <= skipBytes() && fallbacks_.empty()) {
     // Between joins nothing lives in the chunks: re-lay them out as ONE chunk
     // of the request (first fit over several smaller chunks could leave a big
     // buffer without a chunk that holds it), so the total is the request,
@@ -191,6 +202,7 @@ void Arena::reset() {
   fallbackBytes_ = 0;
   peakFallback_ = 0;
   for (auto &c : chunks_) c.used = 0;
+  if (!chunks_.empty() && skipBytes() < chunks_[0].cap) chunks_[0].used = skipBytes();
 }
 
 bool Arena::owns(const void *p) const {
