@@ -154,6 +154,20 @@ uint64_t Arena::ensure(uint64_t bytes, bool touch, void *stream) {
   return capacity() - have;
 }
 
+uint64_t Arena::ensureParts(const std::vector<uint64_t> &parts, bool touch, void *stream) {
+  uint64_t want = skipBytes();
+  for (uint64_t p : parts) want += p;
+  const uint64_t have = capacity();
+  if (have >= want) return 0;
+  if (used() <= skipBytes() && fallbacks_.empty()) {
+    releaseAll();
+    for (size_t i = 0; i < parts.size(); ++i) addChunk(parts[i] + (i == 0 ? skipBytes() : 0), touch, stream);
+    return capacity() > have ? capacity() - have : 0;
+  }
+  addChunk(want - have, touch, stream);  // mid-join: the shortfall
+  return capacity() - have;
+}
+
 uint64_t Arena::trim(uint64_t keep) {
   const uint64_t have = capacity() + fallbackBytes_;
   if (have <= keep && fallbacks_.empty()) return 0;

@@ -50,6 +50,10 @@ class Arena {
   // memset could land after a join's first writes) so its pages are mapped
   // before the first join uses them.  Returns the bytes added.
   uint64_t ensure(uint64_t bytes, bool touch = false, void *stream = nullptr);
+  // As ensure(sum of parts), laid out as one chunk per part (in order) when
+  // the arena must be re-laid out: a join's big buffers then each start at an
+  // allocation of their own.  Returns the bytes added.
+  uint64_t ensureParts(const std::vector<uint64_t> &parts, bool touch = false, void *stream = nullptr);
   // Between joins: drop everything handed out (previous joins' outputs
   // included) and shrink to one chunk of `keep` bytes (0 = none) if the
   // arena holds more.  Returns the bytes freed.

@@ -187,13 +187,17 @@ void HashJoin::makeJoinPlan() {
     // only means the first join falls back to hipMalloc, as without it.
     size_t freeB = 0, totalB = 0;
     HIP_CHECK(hipMemGetInfo(&freeB, &totalB));
-    uint64_t want = std::min<uint64_t>(workspaceEstimate(), (uint64_t)(freeB * 0.85));
+    const std::vector<uint64_t> parts = workspaceParts();
+    const uint64_t est = workspaceEstimate();
+    uint64_t want = std::min<uint64_t>(est, (uint64_t)(freeB * 0.85));
     if (config.workspaceBudget) want = std::min<uint64_t>(want, config.workspaceBudget);
     // Rewound first: a previous join's buffers are dead once a new join is
-    // planned on this context, so ensure() re-lays the chunks out as one
-    // chunk of `want` instead of adding `want` on top of them.
+    // planned on this context, so the chunks are re-laid out instead of
+    // growing on top of them.  The whole estimate: one chunk per part; capped:
+    // one chunk of what the cap allows.
     ctx->workspace().reset();
-    reserved = ctx->workspace().ensure(want, true, ctx->stream());
+    reserved = want == est ? ctx->workspace().ensureParts(parts, true, ctx->stream())
+                           : ctx->workspace().ensure(want, true, ctx->stream());
     JOIN_DEBUG("HashJoin", "workspace: estimate %.2f GB, added %.2f GB", want / 1e9, reserved / 1e9);
   }
   reserveMs = (nowUs() - tReserve) / 1000.0;
@@ -227,46 +231,61 @@ int HashJoin::innerKeyRepeats() {
 }
 
 uint64_t HashJoin::workspaceEstimate() const {
+  uint64_t b = 0;
+  for (uint64_t x : workspaceParts()) b += x;
+  return b;
+}
+
+// The estimate as the join's big buffers in allocation order, after one part
+// for everything small (plans, histograms, cursors, counters, scan scratch,
+// build/probe work lists).  Reserved as one chunk per part: a buffer then
+// starts at an allocation of its own, as a fallback hipMalloc would put it.
+// Sub-allocated from one 40 GiB chunk the same scatters ran 0.3-0.4 ms
+// slower each (1B x 1B general path 20.59 vs 19.28 ms same box; which
+// kernels were slow moved with the buffers' offsets, profiles/r4sk).
+std::vector<uint64_t> HashJoin::workspaceParts() const {
   const uint32_t N = numberOfNodes, F = 1u << plan.networkBits;
   const uint64_t n[2] = {innerRelation->getLocalSize(), outerRelation->getLocalSize()};
   const uint64_t g[2] = {innerRelation->getGlobalSize(), outerRelation->getGlobalSize()};
-  uint64_t b = 64ull << 20;  // plans, histograms, cursors, counters, scan scratch
+  std::vector<uint64_t> parts(1, 64ull << 20);
   auto sampledCap = [&](uint64_t m) {
     const kernels::PartitionGeometry geom = kernels::partitionGeometry(m, config.maxPartitionBlocks);
     const uint32_t stride = kernels::sampleStrideFor(geom, m, F, std::max<uint32_t>(1, config.sampleStride));
     return kernels::sampledLayoutCapacityBound(kernels::sampleScale(geom, m, stride, false), F);
   };
   if (plan.bitmapJoin) {
-    for (int r = 0; r < 2; ++r) b += (sampledCap(n[r]) + 64) * 4;  // u32 fragments in claim slices
-    if (plan.bitmapReplicated) b += 2ull * F * kernels::bitmapWords(plan.bitmapBits) * 4;
-    return b;
+    for (int r = 0; r < 2; ++r) parts.push_back((sampledCap(n[r]) + 64) * 4);  // u32 fragments in claim slices
+    if (plan.bitmapReplicated) parts.push_back(2ull * F * kernels::bitmapWords(plan.bitmapBits) * 4);
+    return parts;
   }
   const uint64_t wordB = plan.fragments ? 4 : plan.wide ? 16 : 8;
   const uint64_t owned = N == 1 ? F : ceilDiv(F, N) + 1;
   const uint64_t P = plan.twoLevel ? owned << plan.localBits : owned;
-  uint64_t recvTotal[2];
+  uint64_t recvTotal[2], local[2] = {0, 0};
   for (int r = 0; r < 2; ++r) {
     // N > 1: the fair share plus a quarter (LPT balances partitions; skew
     // beyond that falls back to allocation inside the first join).
     const uint64_t recv = N == 1 ? (plan.sampledNetwork ? sampledCap(n[r]) : n[r]) : g[r] / N + g[r] / (4 * N) + (1 << 20);
     recvTotal[r] = recv;
-    b += recv * wordB;
-    if (N > 1 && !plan.oneSided) b += (plan.sampledNetwork ? n[r] + n[r] / 8 : n[r]) * wordB;  // send buffer
-    if (plan.wireBits[r]) b += (n[r] + recv) * ((plan.wireBits[r] + 7) / 8) + (64ull << 10);  // wire buffers
+    if (N > 1 && !plan.oneSided) parts.push_back((plan.sampledNetwork ? n[r] + n[r] / 8 : n[r]) * wordB);  // send buffer
+    if (plan.wireBits[r]) parts.push_back((n[r] + recv) * ((plan.wireBits[r] + 7) / 8) + (64ull << 10));  // wire buffers
+    parts.push_back(recv * wordB);  // window
     if (plan.twoLevel) {
       const uint64_t ob = plan.fragments ? 2 : plan.splitLocal ? kernels::SPLIT_BYTES : (plan.wide ? 16 : 8);
       const uint64_t slots = kernels::localSampledCapacityBound(recv, P, std::max<uint32_t>(1, plan.localSampleStride), 64);
-      b += slots * ob;
+      local[r] = slots * ob;
       // Repeated keys on counted tables: the inner side's compaction counts
-      // (u32 per slot) and per-partition lengths / lists (BuildProbe, bpKeyDedup).
-      if (r == 0 && plan.keyOnly && plan.variants.keyCount == 9) b += slots * 4 + P * (8 + 8 * kernels::BP_DEDUP_SEGS);
+      // (u32 per slot) and per-segment lengths / lists (BuildProbe, bpKeyDedup).
+      if (r == 0 && plan.keyOnly && plan.variants.keyCount == 9) local[r] += slots * 4 + P * (8 + 8 * kernels::BP_DEDUP_SEGS);
     }
   }
+  for (int r = 0; r < 2; ++r)
+    if (local[r]) parts.push_back(local[r]);
   // Build/probe work lists (items or spans, 32 B) and materialized pairs.
-  b += (2 * P + recvTotal[1] / std::max<uint32_t>(plan.sChunk, 1) + recvTotal[0] / std::max<uint32_t>(plan.rChunk, 1) +
-        2048) * 48;
-  if (plan.materialize) b += (config.outputCapacity ? config.outputCapacity : recvTotal[1] + 1024) * 16;
-  return b;
+  parts[0] += (2 * P + recvTotal[1] / std::max<uint32_t>(plan.sChunk, 1) +
+               recvTotal[0] / std::max<uint32_t>(plan.rChunk, 1) + 2048) * 48;
+  if (plan.materialize) parts.push_back((config.outputCapacity ? config.outputCapacity : recvTotal[1] + 1024) * 16);
+  return parts;
 }
 
 // Count-only single-level bitmap plans (tasks/BitmapJoin) and the N > 1 cost

@@ -113,6 +113,7 @@ class HashJoin {
   // Upper estimate of the workspace bytes one run() of this plan carves from
   // the arena (windows, send/wire buffers, local pass output, work lists).
   uint64_t workspaceEstimate() const;
+  std::vector<uint64_t> workspaceParts() const;  // the estimate as one chunk per big buffer
   // Bytes the constructor added to the arena (0 if it already held the estimate).
   uint64_t reservedBytes() const { return reserved; }
   // Construction cost: planning (key / rid bounds, repeated-key and low-bit
