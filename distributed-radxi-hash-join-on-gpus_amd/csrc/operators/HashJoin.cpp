@@ -261,7 +261,7 @@ std::vector<uint64_t> HashJoin::workspaceParts() const {
   const uint64_t wordB = plan.fragments ? 4 : plan.wide ? 16 : 8;
   const uint64_t owned = N == 1 ? F : ceilDiv(F, N) + 1;
   const uint64_t P = plan.twoLevel ? owned << plan.localBits : owned;
-  uint64_t recvTotal[2], local[2] = {0, 0};
+  uint64_t recvTotal[2], local[2][2] = {{0, 0}, {0, 0}}, dedup = 0;
   for (int r = 0; r < 2; ++r) {
     // N > 1: the fair share plus a quarter (LPT balances partitions; skew
     // beyond that falls back to allocation inside the first join).
@@ -273,14 +273,19 @@ std::vector<uint64_t> HashJoin::workspaceParts() const {
     if (plan.twoLevel) {
       const uint64_t ob = plan.fragments ? 2 : plan.splitLocal ? kernels::SPLIT_BYTES : (plan.wide ? 16 : 8);
       const uint64_t slots = kernels::localSampledCapacityBound(recv, P, std::max<uint32_t>(1, plan.localSampleStride), 64);
-      local[r] = slots * ob;
+      // Split columns are two allocations (u32, then u16): a part each.
+      const bool split = plan.splitLocal && !plan.fragments && !plan.wide;
+      local[r][0] = slots * (split ? ob - 2 : ob);
+      local[r][1] = split ? slots * 2 : 0;
       // Repeated keys on counted tables: the inner side's compaction counts
       // (u32 per slot) and per-segment lengths / lists (BuildProbe, bpKeyDedup).
-      if (r == 0 && plan.keyOnly && plan.variants.keyCount == 9) local[r] += slots * 4 + P * (8 + 8 * kernels::BP_DEDUP_SEGS);
+      if (r == 0 && plan.keyOnly && plan.variants.keyCount == 9) dedup = slots * 4 + P * (8 + 8 * kernels::BP_DEDUP_SEGS);
     }
   }
   for (int r = 0; r < 2; ++r)
-    if (local[r]) parts.push_back(local[r]);
+    for (int c = 0; c < 2; ++c)
+      if (local[r][c]) parts.push_back(local[r][c]);
+  if (dedup) parts.push_back(dedup);
   // Build/probe work lists (items or spans, 32 B) and materialized pairs.
   parts[0] += (2 * P + recvTotal[1] / std::max<uint32_t>(plan.sChunk, 1) +
                recvTotal[0] / std::max<uint32_t>(plan.rChunk, 1) + 2048) * 48;
