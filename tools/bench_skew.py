@@ -181,6 +181,11 @@ def run_config(C, info, ctx, comm, name, G_R, G_S, theta, cfg, steps, warmup, do
         "local_fallbacks": sum(r["local_fallbacks"] for r in res), "network_fallbacks": sum(r["network_fallbacks"] for r in res),
         "reruns": res[-1]["reruns"],
         "phases_ms": {k: round(res[-1][k], 3) for k in ("dev_network_ms", "dev_local_partition_ms", "dev_build_probe_ms")},
+        "first_phases_ms": {k: round(first[k], 3) for k in ("histogram_ms", "network_ms", "local_ms", "join_ms",
+                                                             "dev_network_ms", "dev_local_partition_ms",
+                                                             "dev_build_probe_ms") if k in first},
+        "steady_phases_ms": {k: round(res[-1][k], 3) for k in ("histogram_ms", "network_ms", "local_ms", "join_ms")
+                             if k in res[-1]},
     }
     del join, R, S
     ctx.reset_scratch()
