@@ -2,7 +2,6 @@
 
 #include <cstring>
 #include <mutex>
-#include <map>
 #include <set>
 
 #include "../comm/Communicator.h"
@@ -45,34 +44,18 @@ ExecContext::ExecContext(Location loc, int device, comm::Communicator *comm)
     HIP_CHECK(hipStreamCreateWithPriority(&commStream_, hipStreamNonBlocking, greatestPrio));
     HIP_CHECK(hipStreamCreateWithFlags(&decodeStream_, hipStreamNonBlocking));
     // One small copy each way between the device and pinned memory (the
-    // staging arena's kind) and pageable memory on the engine stream: the
-    // process's first such
+    // staging arena's kind) on the engine stream: the process's first such
     // copy paid ~17 ms of copy-path setup inside the first join's network
     // phase (its claim-cursor read-back; 1e8 x 4e8 first join 23.3 vs 6.3 ms
     // steady, only in the first join of a process, gpurun_out/r4fj3).
-    // The two 256-byte buffers live for the process (one pair per device):
-    // freeing them here would synchronise the whole device, which waits on
-    // other ranks' collectives in a multi-process rehearsal.
-    static std::mutex wm;
-    static std::map<int, std::pair<void *, void *>> warm;
-    std::pair<void *, void *> b;
-    {
-      std::lock_guard<std::mutex> g(wm);
-      auto it = warm.find(device_);
-      if (it == warm.end()) {
-        void *d = nullptr, *h = nullptr;
-        HIP_CHECK(hipMalloc(&d, 256));
-        HIP_CHECK(hipHostMalloc(&h, 256, hipHostMallocMapped | hipHostMallocPortable));
-        it = warm.emplace(device_, std::make_pair(d, h)).first;
-      }
-      b = it->second;
-    }
-    unsigned char pageable[256] = {};  // (the runtime's staged path for pageable host memory, too)
-    HIP_CHECK(hipMemcpyAsync(b.second, b.first, 256, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipMemcpyAsync(b.first, b.second, 256, hipMemcpyHostToDevice, stream_));
-    HIP_CHECK(hipMemcpyAsync(pageable, b.first, 256, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipMemcpyAsync(b.first, pageable, 256, hipMemcpyHostToDevice, stream_));
+    void *d = nullptr, *h = nullptr;
+    HIP_CHECK(hipMalloc(&d, 256));
+    HIP_CHECK(hipHostMalloc(&h, 256, hipHostMallocMapped | hipHostMallocPortable));
+    HIP_CHECK(hipMemcpyAsync(h, d, 256, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(d, h, 256, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
+    HIP_CHECK(hipHostFree(h));
+    HIP_CHECK(hipFree(d));
   }
 }
 
