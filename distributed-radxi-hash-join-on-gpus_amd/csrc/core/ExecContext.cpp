@@ -43,19 +43,6 @@ ExecContext::ExecContext(Location loc, int device, comm::Communicator *comm)
     HIP_CHECK(hipDeviceGetStreamPriorityRange(&leastPrio, &greatestPrio));
     HIP_CHECK(hipStreamCreateWithPriority(&commStream_, hipStreamNonBlocking, greatestPrio));
     HIP_CHECK(hipStreamCreateWithFlags(&decodeStream_, hipStreamNonBlocking));
-    // One small copy each way between the device and pinned memory (the
-    // staging arena's kind) on the engine stream: the process's first such
-    // copy paid ~17 ms of copy-path setup inside the first join's network
-    // phase (its claim-cursor read-back; 1e8 x 4e8 first join 23.3 vs 6.3 ms
-    // steady, only in the first join of a process, gpurun_out/r4fj3).
-    void *d = nullptr, *h = nullptr;
-    HIP_CHECK(hipMalloc(&d, 256));
-    HIP_CHECK(hipHostMalloc(&h, 256, hipHostMallocMapped | hipHostMallocPortable));
-    HIP_CHECK(hipMemcpyAsync(h, d, 256, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipMemcpyAsync(d, h, 256, hipMemcpyHostToDevice, stream_));
-    HIP_CHECK(hipStreamSynchronize(stream_));
-    HIP_CHECK(hipHostFree(h));
-    HIP_CHECK(hipFree(d));
   }
 }
 
