@@ -83,6 +83,7 @@ def main():
         del j
     del Rs, Ss
     for name, spec, G, opts in cases:
+        print(f"[rank {info.rank}] {name}", flush=True)  # progress (shown only when a run times out)
         S = C.Relation(C.Relation.local_size_for(G, info.rank, info.world), G, "device", info.local_rank)
         S.generate(spec, C.Relation.local_offset_for(G, info.rank, info.world))
         cfg = C.JoinConfig()

@@ -10,6 +10,7 @@ import socket
 import subprocess
 import sys
 import threading
+import time
 
 import pytest
 
@@ -424,8 +425,21 @@ def test_rccl_multiprocess_shared_gpu(world):
     script = os.path.join(ROOT, "tests", "rccl_worker.py")
     procs = [subprocess.Popen([sys.executable, "-u", script], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(world)]
+    # RCCL's socket transport between processes sharing one GPU: usually
+    # 10-40 s for all cases.  On a timeout the ranks' last output says which
+    # case they were in.
+    outs = [None] * world
+    deadline = time.time() + 240
     try:
-        outs = [p.communicate(timeout=110)[0] for p in procs]
+        for i, p in enumerate(procs):
+            outs[i] = p.communicate(timeout=max(1.0, deadline - time.time()))[0]
+    except subprocess.TimeoutExpired:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        tails = [f"rank {i}: " + ((outs[i] if outs[i] is not None else p.communicate()[0]) or "")[-1500:]
+                 for i, p in enumerate(procs)]
+        pytest.fail("rccl_worker timed out after 240 s; last output per rank:\n" + "\n".join(tails))
     finally:
         for p in procs:
             if p.poll() is None:
