@@ -193,11 +193,14 @@ void HashJoin::makeJoinPlan() {
     if (config.workspaceBudget) want = std::min<uint64_t>(want, config.workspaceBudget);
     // Rewound first: a previous join's buffers are dead once a new join is
     // planned on this context, so the chunks are re-laid out instead of
-    // growing on top of them.  The whole estimate: one chunk per part; capped:
-    // one chunk of what the cap allows.
+    // growing on top of them.  One rank with the whole estimate: one chunk per
+    // part; otherwise one chunk (capped: of what the cap allows).  N > 1 keeps
+    // the single chunk: with a chunk per part the 4- and 8-process RCCL test
+    // (IPC-mapped one-sided windows, workspaces re-laid out between joins)
+    // hung in 4 of 5 runs (gpurun_out/r4final3, rccl_repeat1), never before.
     ctx->workspace().reset();
-    reserved = want == est ? ctx->workspace().ensureParts(parts, true, ctx->stream())
-                           : ctx->workspace().ensure(want, true, ctx->stream());
+    reserved = (want == est && numberOfNodes == 1) ? ctx->workspace().ensureParts(parts, true, ctx->stream())
+                                                   : ctx->workspace().ensure(want, true, ctx->stream());
     JOIN_DEBUG("HashJoin", "workspace: estimate %.2f GB, added %.2f GB", want / 1e9, reserved / 1e9);
   }
   reserveMs = (nowUs() - tReserve) / 1000.0;

@@ -429,7 +429,7 @@ def test_rccl_multiprocess_shared_gpu(world):
     # 10-40 s for all cases.  On a timeout the ranks' last output says which
     # case they were in.
     outs = [None] * world
-    deadline = time.time() + 240
+    deadline = time.time() + 150
     try:
         for i, p in enumerate(procs):
             outs[i] = p.communicate(timeout=max(1.0, deadline - time.time()))[0]
@@ -439,7 +439,7 @@ def test_rccl_multiprocess_shared_gpu(world):
                 p.kill()
         tails = [f"rank {i}: " + ((outs[i] if outs[i] is not None else p.communicate()[0]) or "")[-1500:]
                  for i, p in enumerate(procs)]
-        pytest.fail("rccl_worker timed out after 240 s; last output per rank:\n" + "\n".join(tails))
+        pytest.fail("rccl_worker timed out after 150 s; last output per rank:\n" + "\n".join(tails))
     finally:
         for p in procs:
             if p.poll() is None:
