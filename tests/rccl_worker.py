@@ -135,7 +135,10 @@ def main():
     # hipMalloc and the peers import a rank's second window while its first
     # one is in use.  Growth keeps the arena generation, so that first mapping
     # stays open (it used to be closed at the second import).
+    step = lambda m: print(f"[rank {info.rank}] fallback case: {m}", flush=True)
+    step("trim")
     ctx.trim_workspace(0)
+    step("barrier")
     comm.barrier()
     cfg2 = C.JoinConfig()
     cfg2.bitmap_join = False
@@ -144,10 +147,12 @@ def main():
     G = 4 * G_S
     S = C.Relation(C.Relation.local_size_for(G, info.rank, info.world), G, "device", info.local_rank)
     S.generate(spec, C.Relation.local_offset_for(G, info.rank, info.world))
+    step("construct")
     j = C.HashJoin(R, S, ctx, cfg2)
     assert j.plan.one_sided and ctx.workspace_capacity() == 0, (j.plan, ctx.workspace_capacity())
     exp = C.Relation.expected_matches(inner, G_R, spec, G)
     for it in range(2):
+        step(f"run {it}")
         res = j.run()
         mine = [it, res["local_matches"], res["inner_received"], res["outer_received"], res["global_matches"]]
         allv = comm.all_gather(mine) if hasattr(comm, "all_gather") else [mine]
