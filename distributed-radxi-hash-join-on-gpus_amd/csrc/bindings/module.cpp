@@ -827,6 +827,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("reserve_workspace", [](core::ExecContext &c, uint64_t b) { c.workspace().reserve(b); })
       .def("trim_workspace", [](core::ExecContext &c, uint64_t keep) {
              c.synchronize();
+             c.releaseImports();  // before this rank frees memory peers may still map
              return c.workspace().trim(keep);
            },
            py::arg("keep") = 0,

@@ -137,6 +137,11 @@ void *ExecContext::ipcImport(uint32_t peer, const uint64_t handle[8], uint64_t g
   return ptr;
 }
 
+void ExecContext::releaseImports() {
+  for (auto &m : ipcImported_) HIP_CHECK(hipIpcCloseMemHandle(m.base));
+  ipcImported_.clear();
+}
+
 hipEvent_t ExecContext::acquireEvent() {
   if (eventsUsed_ == events_.size()) {
     hipEvent_t e;

@@ -62,6 +62,12 @@ class ExecContext {
   void ipcExport(const void *p, uint64_t handle[8], uint64_t *offset, uint64_t *generation);
   void *ipcImport(uint32_t peer, const uint64_t handle[8], uint64_t generation);
   size_t ipcMappings() const { return ipcImported_.size(); }
+  // Between joins, before this rank frees workspace memory: close every
+  // mapping of peers' memory first.  Every rank closes its imports before it
+  // frees its own chunks, so no rank's free can wait on a peer that is itself
+  // waiting in a free (the multi-process one-sided test hung intermittently
+  // around a workspace trim).  Imports are re-opened at the next join.
+  void releaseImports();
 
  private:
   Location loc_;
