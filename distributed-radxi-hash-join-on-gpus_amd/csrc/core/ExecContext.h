@@ -62,11 +62,14 @@ class ExecContext {
   void ipcExport(const void *p, uint64_t handle[8], uint64_t *offset, uint64_t *generation);
   void *ipcImport(uint32_t peer, const uint64_t handle[8], uint64_t generation);
   size_t ipcMappings() const { return ipcImported_.size(); }
-  // Between joins, before this rank frees workspace memory: close every
-  // mapping of peers' memory first.  Every rank closes its imports before it
-  // frees its own chunks, so no rank's free can wait on a peer that is itself
-  // waiting in a free (the multi-process one-sided test hung intermittently
-  // around a workspace trim).  Imports are re-opened at the next join.
+  // Between joins, before an explicit workspace trim frees this rank's
+  // memory: close every mapping of peers' memory first, so no rank's free can
+  // wait on a peer that is itself waiting in a free (the multi-process
+  // one-sided test hung intermittently around `trim_workspace(0)`; 3 of 3
+  // clean runs at 2/4/8 ranks since, gpurun_out/rccl_repeat6-8).  Imports are
+  // re-opened at the next join.  Not called when a plan re-lays the workspace
+  // out: closing there made the next one-sided join at 4 ranks inexact
+  // (rccl_repeat4); that path keeps closing stale mappings in ipcImport.
   void releaseImports();
 
  private:

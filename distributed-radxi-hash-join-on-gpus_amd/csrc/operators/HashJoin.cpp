@@ -199,7 +199,6 @@ void HashJoin::makeJoinPlan() {
     // (IPC-mapped one-sided windows, workspaces re-laid out between joins)
     // hung in 4 of 5 runs (gpurun_out/r4final3, rccl_repeat1), never before.
     ctx->workspace().reset();
-    if (numberOfNodes > 1 && ctx->workspace().capacity() < want) ctx->releaseImports();  // a re-layout frees chunks
     reserved = (want == est && numberOfNodes == 1) ? ctx->workspace().ensureParts(parts, true, ctx->stream())
                                                    : ctx->workspace().ensure(want, true, ctx->stream());
     JOIN_DEBUG("HashJoin", "workspace: estimate %.2f GB, added %.2f GB", want / 1e9, reserved / 1e9);
