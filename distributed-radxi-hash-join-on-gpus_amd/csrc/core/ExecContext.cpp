@@ -1,5 +1,6 @@
 #include "ExecContext.h"
 
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <set>
@@ -105,9 +106,21 @@ void ExecContext::ipcExport(const void *p, uint64_t handle[8], uint64_t *offset,
   JOIN_ASSERT(onDevice(), "ExecContext", "IPC export of host memory");
   void *base = workspace_->allocationOf(p);
   JOIN_ASSERT(base != nullptr, "ExecContext", "IPC export: %p is not in the workspace", p);
-  hipIpcMemHandle_t h;
-  HIP_CHECK(hipIpcGetMemHandle(&h, base));
-  std::memcpy(handle, &h, sizeof(h));
+  const uint64_t gen = workspace_->generation();
+  // Entries of older generations name freed allocations: drop them.
+  ipcExported_.erase(std::remove_if(ipcExported_.begin(), ipcExported_.end(),
+                                    [&](const IpcExport &x) { return x.generation != gen; }),
+                     ipcExported_.end());
+  const IpcExport *hit = nullptr;
+  for (const auto &x : ipcExported_)
+    if (x.base == base) hit = &x;
+  if (!hit) {
+    IpcExport x{base, gen, {}};
+    HIP_CHECK(hipIpcGetMemHandle(&x.handle, base));
+    ipcExported_.push_back(x);
+    hit = &ipcExported_.back();
+  }
+  std::memcpy(handle, &hit->handle, sizeof(hit->handle));
   *offset = (uint64_t)(static_cast<const uint8_t *>(p) - static_cast<const uint8_t *>(base));
   *generation = workspace_->generation();
 }

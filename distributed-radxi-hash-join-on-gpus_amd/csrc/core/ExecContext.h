@@ -91,6 +91,17 @@ class ExecContext {
     void *base;
   };
   std::vector<IpcMapping> ipcImported_;
+  // One export per allocation and arena generation: a second
+  // hipIpcGetMemHandle of the same allocation (the join's second window in
+  // the same chunk) while a peer is still opening the first handle was the
+  // suspected cause of intermittent open failures ("invalid device pointer")
+  // and one inexact one-sided join at 4 ranks.
+  struct IpcExport {
+    void *base;
+    uint64_t generation;
+    hipIpcMemHandle_t handle;
+  };
+  std::vector<IpcExport> ipcExported_;
 };
 
 }  // namespace core

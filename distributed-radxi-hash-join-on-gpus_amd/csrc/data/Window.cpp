@@ -262,6 +262,10 @@ void Window::enableOneSided() {
     }
     for (uint32_t c = 0; c < C; ++c) peerOffset[(size_t)p * C + c] = r[H + (size_t)c * N + me];
   }
+  // Every rank has opened its peers' handles before any rank goes on to
+  // export, free or re-lay out memory (an exporter's later runtime calls must
+  // not race a peer's open of the handle it just sent).
+  if (!shared) ctx->comm()->barrier();
   oneSided = true;
   oneSidedComplete = false;
 }
