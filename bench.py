@@ -13,6 +13,7 @@ checked against the exact oracle (|R| for unique keys).
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 import argparse
+import gc
 import json
 import os
 import signal
@@ -320,11 +321,16 @@ def measure(C, info, ctx, comm, on_gpu, G_R, G_S, inner, outer, cfg, rel_loc, st
     ctx.reset_scratch()
     barrier()
     results = []
+    # No Python garbage collection inside the timed joins (host noise only:
+    # the joins allocate nothing the collector tracks beyond their result dicts).
+    gc.collect()
+    gc.disable()
     t0 = time.perf_counter()
     for _ in range(steps):
         results.append(join.run())
     barrier()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     mine = [int(elapsed * 1e9), int(first_ms * 1e6), int(setup_ms * 1e6), int(join.plan_ms * 1e6)]
     plan_ms = join.plan_ms
     if info.world > 1:
@@ -418,6 +424,15 @@ def main():
               "local_items": results[-1]["local_items"], "workspace_GB": round(ctx.workspace_capacity() / 1e9, 2),
               "workspace_peak_GB": round(ctx.workspace_peak() / 1e9, 2),
               "step_ms": [round(r["join_ms"], 2) for r in results],
+              # Per step: device span (first -> last event of the join) and
+              # what the host added around it (join_ms - dev_span_ms), split
+              # into enqueue (start -> last kernel enqueued) and the wait for
+              # the result after it.  A stall shows as a large host gap with
+              # an unchanged device span.
+              "step_dev_span_ms": [round(r["dev_span_ms"], 3) for r in results],
+              "step_host_gap_ms": [round(r["join_ms"] - r["dev_span_ms"], 3) for r in results],
+              "step_enqueue_ms": [round(r["enqueue_ms"], 3) for r in results],
+              "step_host_wait_ms": [round(r["host_wait_ms"], 3) for r in results],
               "step_phases_ms": [[round(r[k], 2) for k in PHASES] for r in results]}
     links = link_prediction(info, plan, results)
     if links is not None:

@@ -536,6 +536,10 @@ py::dict resultToDict(const operators::JoinResult &r) {
   d["dev_build_probe_ms"] = r.devBuildProbeMs;
   d["setup_ms"] = r.setupMs;
   d["teardown_ms"] = r.teardownMs;
+  d["enqueue_ms"] = r.enqueueMs;
+  d["host_wait_ms"] = r.hostWaitMs;
+  d["dev_span_ms"] = r.devSpanMs;
+  d["exchange_checked"] = r.exchangeChecked;
   d["inner_received"] = r.innerReceived;
   d["wire_bytes"] = r.wireBytes;
   d["outer_received"] = r.outerReceived;
@@ -640,6 +644,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("direct_count", &core::JoinConfig::directCount)
       .def_readwrite("bitmap_join", &core::JoinConfig::bitmapJoin)
       .def_readwrite("replicate_bitmap", &core::JoinConfig::replicateBitmap)
+      .def_readwrite("verify_exchange", &core::JoinConfig::verifyExchange)
       .def_readwrite("exchange", &core::JoinConfig::exchange)
       .def_readwrite("split_histogram", &core::JoinConfig::splitHistogram)
       .def_readwrite("pipeline_outer", &core::JoinConfig::pipelineOuter)
@@ -826,12 +831,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            "the observed peak now (so the next join does not pay for it)")
       .def("reserve_workspace", [](core::ExecContext &c, uint64_t b) { c.workspace().reserve(b); })
       .def("trim_workspace", [](core::ExecContext &c, uint64_t keep) {
+             // Collective when the communicator has several ranks (every rank
+             // calls it together): all ranks close their mappings of peers'
+             // memory before any rank frees, and no rank starts a join
+             // before every free is done.
              c.synchronize();
-             c.releaseImports();  // before this rank frees memory peers may still map
-             return c.workspace().trim(keep);
+             c.releaseImports();
+             const bool multi = c.comm()->size() > 1;
+             if (multi) c.comm()->barrier();
+             const uint64_t freed = c.workspace().trim(keep);
+             if (multi) c.comm()->barrier();
+             return freed;
            },
            py::arg("keep") = 0,
-           "Between joins: shrink the workspace to one chunk of `keep` bytes; returns the bytes freed")
+           "Between joins, on every rank together: shrink the workspace to one chunk of `keep` bytes; returns the "
+           "bytes freed")
       .def("workspace_generation", [](core::ExecContext &c) { return c.workspace().generation(); })
       .def("ensure_workspace", [](core::ExecContext &c, uint64_t b) { return c.workspace().ensure(b); })
       .def("workspace_scratch", [](core::ExecContext &c, uint64_t b) {
@@ -1072,17 +1086,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("outer_rows"), py::arg("outer_rid_offset"), py::arg("outer_global_rows"))
       .def("output", [](operators::HashJoin &j) {
         const auto &r = j.lastResult();
-        const uint64_t n = std::min<uint64_t>(r.outputPairs, r.outputPairs);
+        const uint64_t n = r.outputPairs;
         at::Tensor out = at::empty({(int64_t)n, 2}, at::kLong);
         if (n && j.getOutput()) {
-          hipPointerAttribute_t attr;
-          bool dev = hipPointerGetAttributes(&attr, j.getOutput()) == hipSuccess && attr.type == hipMemoryTypeDevice;
-          if (dev)
+          HJ_CHECK(j.outputValid(),
+                   "HashJoin.output(): the pairs of the last run were in the engine workspace, which a later join, "
+                   "plan or trim_workspace on the same context has since reused; read output() right after run()");
+          if (j.context()->onDevice())
             HIP_CHECK(hipMemcpy(out.data_ptr(), j.getOutput(), n * 16, hipMemcpyDeviceToHost));
           else
             std::memcpy(out.data_ptr(), j.getOutput(), n * 16);
         }
-        (void)hipGetLastError();
         return out;
       });
   m.def("result_counter", []() { return operators::HashJoin::RESULT_COUNTER; });

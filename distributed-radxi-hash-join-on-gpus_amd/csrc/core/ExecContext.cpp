@@ -1,9 +1,13 @@
 #include "ExecContext.h"
 
 #include <algorithm>
+#include <chrono>
+#include <cstddef>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <set>
+#include <immintrin.h>
 
 #include "../comm/Communicator.h"
 #include "../kernels/kernels.h"
@@ -44,11 +48,70 @@ ExecContext::ExecContext(Location loc, int device, comm::Communicator *comm)
     HIP_CHECK(hipDeviceGetStreamPriorityRange(&leastPrio, &greatestPrio));
     HIP_CHECK(hipStreamCreateWithPriority(&commStream_, hipStreamNonBlocking, greatestPrio));
     HIP_CHECK(hipStreamCreateWithFlags(&decodeStream_, hipStreamNonBlocking));
+    HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&control_), sizeof(kernels::DeviceControl)));
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&mailboxHost_), sizeof(kernels::ResultMailbox),
+                            hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(mailboxHost_, 0, sizeof(kernels::ResultMailbox));
+    HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void **>(&mailboxDev_), mailboxHost_, 0));
+    warmRuntimeCopies();
+  }
+}
+
+// The runtime loads its copy / fill kernels on first use: the first join of
+// a process paid ~17 ms in its network phase for it (docs/ROUND4.md, 1e8 x
+// 4e8 sparse keys; nothing of it under rocprofv3, whose copies are kernels
+// it loads itself).  One tiny fill and one copy of each direction on the
+// engine's compute stream move that cost here, and the fill zeroes the
+// control block.
+void ExecContext::warmRuntimeCopies() {
+  // Pinned scratch for a join's small read-backs (claim cursors, counters:
+  // tens of KiB): reserved now, so a first join does not pay a pinned
+  // allocation (~ms) in the middle of its network phase.
+  staging_->ensure(kStagingReserve);
+  kernels::zeroWords(control_, sizeof(kernels::DeviceControl) / 8, stream_);
+  const char *w = std::getenv("HPCJOIN_WARM_COPIES");
+  if (w && w[0] == '0') {
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    return;
+  }
+  HIP_CHECK(hipMemsetAsync(reinterpret_cast<uint8_t *>(control_) + offsetof(kernels::DeviceControl, pad), 0, 16,
+                           stream_));
+  void *pinned = staging_->get(256);
+  std::memset(pinned, 0, 256);
+  uint8_t *dev = reinterpret_cast<uint8_t *>(control_) + offsetof(kernels::DeviceControl, pad);
+  HIP_CHECK(hipMemcpyAsync(dev, pinned, 32, hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(static_cast<uint8_t *>(pinned) + 64, dev, 32, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipMemcpyAsync(dev + 32, dev, 16, hipMemcpyDeviceToDevice, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  staging_->reset();
+}
+
+void ExecContext::beginControl() {
+  if (controlDirty_) kernels::zeroWords(control_, sizeof(kernels::DeviceControl) / 8, stream_);
+  controlDirty_ = true;
+}
+
+bool ExecContext::waitMailbox(uint64_t seq) const {
+  using clk = std::chrono::steady_clock;
+  const auto deadline = clk::now() + std::chrono::milliseconds(utils::commTimeoutMs());
+  const volatile unsigned long long *p = &mailboxHost_->seq;
+  for (uint32_t spin = 1;; ++spin) {
+    if (__atomic_load_n(p, __ATOMIC_ACQUIRE) >= seq) return true;
+    _mm_pause();
+    if ((spin & 4095) == 0) {
+      // A faulted kernel never publishes: poll the stream for its error.
+      const hipError_t e = hipStreamQuery(stream_);
+      if (e != hipSuccess && e != hipErrorNotReady) HIP_CHECK(e);
+      if (e == hipSuccess && __atomic_load_n(p, __ATOMIC_ACQUIRE) < seq) return false;
+      if (clk::now() > deadline) return false;
+    }
   }
 }
 
 ExecContext::~ExecContext() {
   for (auto &m : ipcImported_) (void)hipIpcCloseMemHandle(m.base);
+  if (control_) (void)hipFree(control_);
+  if (mailboxHost_) (void)hipHostFree(mailboxHost_);
   for (hipEvent_t e : events_) (void)hipEventDestroy(e);
   timeline_.reset();
   workspace_.reset();
@@ -61,17 +124,14 @@ ExecContext::~ExecContext() {
 uint32_t ExecContext::nodeId() const { return comm_->rank(); }
 uint32_t ExecContext::numberOfNodes() const { return comm_->size(); }
 
+// Polled waits (utils::waitStream): a lost peer cannot hang this rank
+// forever, and the host sees the end of the join's last kernel within
+// microseconds instead of after a runtime sleep on an interrupt.
 void ExecContext::synchronize() const {
   if (!onDevice()) return;
-  if (comm_->size() > 1) {  // a lost peer must not hang this rank forever
-    utils::waitStream(commStream_, comm_, "exchange stream");
-    utils::waitStream(decodeStream_, comm_, "decode stream");
-    utils::waitStream(stream_, comm_, "compute stream");
-    return;
-  }
-  HIP_CHECK(hipStreamSynchronize(commStream_));
-  HIP_CHECK(hipStreamSynchronize(decodeStream_));
-  HIP_CHECK(hipStreamSynchronize(stream_));
+  utils::waitStream(commStream_, comm_, "exchange stream");
+  utils::waitStream(decodeStream_, comm_, "decode stream");
+  utils::waitStream(stream_, comm_, "compute stream");
 }
 
 void ExecContext::copy(void *dst, const void *src, uint64_t bytes, bool toDevice, bool fromDevice) const {

@@ -21,6 +21,10 @@ class Arena;
 namespace performance {
 class Timeline;
 }
+namespace kernels {
+struct DeviceControl;
+struct ResultMailbox;
+}
 
 namespace core {
 
@@ -72,7 +76,32 @@ class ExecContext {
   // (rccl_repeat4); that path keeps closing stale mappings in ipcImport.
   void releaseImports();
 
+  // Persistent join scratch of a device engine (kernels::DeviceControl):
+  // zeroed once here; the kernels that consume it return it to zero, so the
+  // bitmap join issues no memset.  A join that ends in an exception may leave
+  // it dirty: beginControl() re-zeroes it before the next use then.
+  kernels::DeviceControl *control() const { return control_; }
+  void beginControl();
+  void endControl() { controlDirty_ = false; }
+  // Host-mapped result mailbox (kernels::ResultMailbox): the device alias for
+  // kernels, the next sequence number, and a spin wait for it (no runtime
+  // call, no interrupt wake-up).  waitMailbox returns false when seq did not
+  // arrive within the communicator timeout (the caller then synchronises the
+  // streams, which reports a device fault).
+  kernels::ResultMailbox *mailboxDevice() const { return mailboxDev_; }
+  const kernels::ResultMailbox &mailbox() const { return *mailboxHost_; }
+  uint64_t nextMailboxSeq() { return ++mailboxSeq_; }
+  bool waitMailbox(uint64_t seq) const;
+
  private:
+  kernels::DeviceControl *control_ = nullptr;
+  bool controlDirty_ = false;
+  kernels::ResultMailbox *mailboxHost_ = nullptr;
+  kernels::ResultMailbox *mailboxDev_ = nullptr;
+  uint64_t mailboxSeq_ = 0;
+  void warmRuntimeCopies();
+  static constexpr uint64_t kStagingReserve = 4ull << 20;
+
   Location loc_;
   std::vector<hipEvent_t> events_;
   size_t eventsUsed_ = 0;

@@ -106,6 +106,12 @@ struct JoinConfig {
   // range fits (host path and N == 1 included); Off: never.
   PlanChoice replicateBitmap = PlanChoice::Auto;
   ExchangeMode exchange = ExchangeMode::Rccl;
+  // N > 1: check the exchanged data, not only the counts -- content hashes
+  // of every (source, chunk, partition) run on the sender vs what arrived
+  // (operators/ExchangeVerify.h).  One extra read of the input and of the
+  // windows per join.  Auto: on for one-sided windows (IPC puts, where a lost
+  // or misdirected put would otherwise be silent), off for RCCL all-to-allv.
+  PlanChoice verifyExchange = PlanChoice::Auto;
   uint32_t localItemTiles = 64; // local pass work item: up to this many 4096-tuple tiles of one segment
   uint32_t localGeometry = 0;   // local scatter workgroup geometry (0 = 1024 x 8; 1-4: sweep alternatives)
   KernelVariants variants;      // kernel-shape variants (sweeps; core/Types.h)

@@ -41,11 +41,31 @@ __device__ __forceinline__ T waveReduceSum(T x) {
   return x;
 }
 
+// Workgroup barrier that orders LDS accesses only.  __syncthreads() is a
+// workgroup-scope release/acquire for every address space, so the compiler
+// puts s_waitcnt vmcnt(0) in front of it: all of the wave's global loads in
+// flight (a prefetched tile) must land first.  Kernels whose waves hand each
+// other data through LDS alone use this one and keep their loads in flight.
+__device__ __forceinline__ void ldsBarrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+template <bool LDS_ONLY>
+__device__ __forceinline__ void blockBarrier() {
+  if constexpr (LDS_ONLY)
+    ldsBarrier();
+  else
+    __syncthreads();
+}
+
 // Exclusive scan of an LDS array data[0..n) into out[0..n) (may alias) by a
 // workgroup of NT threads; each thread owns a contiguous run of entries.
 // waveTot must hold NT/64 entries of T.  Contains the barriers it needs; all
-// threads of the block must call it.
-template <int NT, typename T, typename U>
+// threads of the block must call it.  LDS_ONLY: its barriers order LDS only
+// (ldsBarrier), for callers with global loads in flight across the scan.
+template <int NT, typename T, typename U, bool LDS_ONLY = false>
 __device__ __forceinline__ T blockExclusiveScanLds(const U *data, T *out, int n, T *waveTot) {
   const int t = threadIdx.x, lane = t & (WAVE - 1), wid = t / WAVE;
   const int per = (n + NT - 1) / NT;
@@ -55,7 +75,7 @@ __device__ __forceinline__ T blockExclusiveScanLds(const U *data, T *out, int n,
     if (b + i < n) local += T(data[b + i]);
   T incl = waveInclusiveScan<T>(local);
   if (lane == WAVE - 1) waveTot[wid] = incl;
-  __syncthreads();
+  blockBarrier<LDS_ONLY>();
   T prefix = 0, total = 0;
 #pragma unroll
   for (int w = 0; w < NT / WAVE; ++w) {
@@ -70,7 +90,7 @@ __device__ __forceinline__ T blockExclusiveScanLds(const U *data, T *out, int n,
       out[b + i] = run;
       run += v;
     }
-  __syncthreads();
+  blockBarrier<LDS_ONLY>();
   return total;
 }
 

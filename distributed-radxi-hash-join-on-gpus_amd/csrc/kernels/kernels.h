@@ -122,7 +122,9 @@ struct SampledInput {
   uint32_t stride;
   uint64_t *totals;  // [NGROUPS][F]
 };
-void netSampledTotals(const SampledInput *sides, uint32_t count, uint32_t bits, hipStream_t s, KeyMix mix);
+// preZeroed: the totals are already zero (DeviceControl), no clear is issued.
+void netSampledTotals(const SampledInput *sides, uint32_t count, uint32_t bits, hipStream_t s, KeyMix mix,
+                      bool preZeroed = false);
 // totals[c][g][d] (u64) = sum of blockHist[d][b] over the blocks b of chunk c
 // (blocksPerChunk each) with (b - first block of c) % NGROUPS == g: the claim
 // groups of chunk c's scatter launch (sampled N > 1 network pass).
@@ -186,6 +188,7 @@ struct LayoutInput {
   SampleScale sc;
   void *gstart, *gcur, *gend;
   unsigned long long *capacityUsed;
+  bool clearSampled = false;  // zero `sampled` after reading it (DeviceControl totals)
 };
 void netSampledLayout(const LayoutInput *sides, uint32_t count, uint32_t F, bool narrow, hipStream_t s);
 // gend (optional, same layout and width as gcur): end of every group slice.
@@ -443,6 +446,69 @@ struct BitmapCounters {
   unsigned long long dup;       // BM_FLAG_DUP raised
   unsigned long long overflow;  // BM_FLAG_OVERFLOW raised
 };
+// Result delivery without a device->host copy.  A ResultMailbox lives in
+// host-mapped pinned memory; the last wave of a join's final kernel writes the
+// join's counters into it with system-scope stores and then publishes `seq`
+// (release), so the host spins on one word instead of waiting for a copy
+// engine or a blit kernel (BENCH_r04: two joins stalled 6-8 ms after their
+// last kernel, in the D2H copy + stream synchronisation).
+struct ResultMailbox {
+  unsigned long long seq;  // written last
+  unsigned long long matches, popcount, dup, overflow;
+  unsigned long long pad[3];
+};
+// Per-engine persistent device scratch that the kernels consuming it restore
+// to zero, so a join issues no memset (no runtime fill kernel, no first-use
+// load of the runtime's blit code): sampled totals of both sides (cleared by
+// netSampledLayout after it reads them) and the bitmap join's counters plus
+// the arrival count of its final kernel (cleared by that kernel's last wave).
+struct DeviceControl {
+  unsigned long long totals[2 * CLAIM_GROUPS * (1u << MAX_PART_BITS)];
+  BitmapCounters counters;
+  unsigned int arrivals;
+  unsigned int pad[15];
+};
+// Passed to the final kernel of a mailbox join (box == nullptr: plain counters).
+struct MailboxArgs {
+  ResultMailbox *box = nullptr;  // device alias of the host-mapped mailbox
+  unsigned int *arrivals = nullptr;
+  unsigned long long seq = 0;
+};
+// ------------------------------------------------- exchange verification
+// Content checksum of exchanged tuples (JoinConfig::verifyExchange,
+// kernels/verify.hip): each tuple adds exchangeHash(mixed key, rid) to the sum
+// of its (source, chunk, partition) run, on the sender from its input and on
+// the receiver from its window; the sums must agree.
+HJ_HD uint64_t exchangeHash(uint64_t mk, uint64_t rid) {
+  uint64_t x = mk * 0x9E3779B97F4A7C15ull ^ (rid + 0x632BE59BD9B4E019ull) * 0xC2B2AE3D27D4EB4Full;
+  x ^= x >> 31;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 29;
+  return x;
+}
+// How a window word holds (mixed key, rid): Compressed value = rid |
+// (mk >> bits) << keyShift (keyShift 0: key-only words, no rid); Wide 16-B
+// tuples (mk, rid).  withRid = 0 when the rid did not travel (count-only wire).
+struct ChecksumFormat {
+  enum Kind : uint32_t { Compressed = 0, Wide = 1 };
+  uint32_t kind = Compressed;
+  uint32_t bits = 0, keyShift = 0, withRid = 0;
+};
+struct ChecksumSeg {
+  uint64_t begin, len;  // window tuple range
+  uint32_t partition;   // global partition id (the digit the window word omits)
+  uint32_t slot;        // index of the (source, chunk, partition) sum
+};
+// sums[d] += hashes of in[begin, end) by digit (mk & (2^bits - 1)); sums zeroed by the caller.
+void exchangeChecksumSend(const data::Tuple *in, uint64_t begin, uint64_t end, uint32_t bits, KeyMix mix,
+                          bool withRid, unsigned long long *sums, hipStream_t s);
+// sums[seg.slot] += hashes of the window run of every segment (segs: device array).
+void exchangeChecksumRecv(const void *window, const ChecksumFormat &fmt, const ChecksumSeg *segs, uint32_t nSegs,
+                          unsigned long long *sums, hipStream_t s);
+void flipWindowWord(void *window, uint64_t word, hipStream_t s);
+
+// p[0, words) = 0 (u64 words) with the engine's own kernel.
+void zeroWords(void *p, uint64_t words, hipStream_t s);
 struct BitmapSlices {
   enum Kind : int { Claim = 0, Table = 1 };
   int kind = Claim;
@@ -464,8 +530,11 @@ struct BitmapSlices {
 uint32_t bitmapWords(uint32_t bits);
 // bits may exceed BITMAP_MAX_BITS by up to BITMAP_MAX_SPLIT: each partition
 // is then joined by 2^(bits - BITMAP_MAX_BITS) workgroups.
+// mb.box != nullptr: the kernel's last wave publishes *out into the mailbox
+// (seq mb.seq) and resets *out and *mb.arrivals to zero.
 void bitmapJoin(uint32_t elemBytes, const void *r, const void *s, const BitmapSlices &rs, const BitmapSlices &ss,
-                uint32_t partitions, uint32_t keyShift, uint32_t bits, BitmapCounters *out, hipStream_t st);
+                uint32_t partitions, uint32_t keyShift, uint32_t bits, BitmapCounters *out, hipStream_t st,
+                const MailboxArgs &mb = MailboxArgs());
 // bitmaps[d * bitmapWords(bits) ...] = partition d's bitmap of r.
 // Partitions [first, first + count) only (count = UINT32_MAX: to the end).
 void bitmapBuild(uint32_t elemBytes, const void *r, const BitmapSlices &rs, uint32_t partitions, uint32_t keyShift,

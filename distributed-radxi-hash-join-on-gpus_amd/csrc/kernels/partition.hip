@@ -69,6 +69,25 @@ struct Loader<uint32_t> {
   static __device__ __forceinline__ uint32_t load(const uint32_t *p) { return __builtin_nontemporal_load(p); }
 };
 
+// What a scatter policy loads per element.  PlainLoad: the whole input
+// element.  KeyLoad: only the key of a 16-byte tuple, for policies whose
+// output never carries the rid (count-only fragments, key-only words): half
+// the VGPRs per element in flight.  With whole tuples the frag scatter sat at
+// 121 VGPRs and the compiler reused the dead rid halves of pending loads for
+// address arithmetic, which put an s_waitcnt vmcnt(0) after every second
+// load of the next tile's prefetch (three serial HBM round trips per tile).
+template <typename In>
+struct PlainLoad {
+  using LoadT = In;
+  static __device__ __forceinline__ LoadT load(const In *p) { return Loader<In>::load(p); }
+};
+struct KeyLoad {
+  using LoadT = uint64_t;
+  static __device__ __forceinline__ LoadT load(const ulonglong2 *p) {
+    return __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(p));
+  }
+};
+
 // ------------------------------------------------------- histogram (pass 1)
 __device__ __forceinline__ void netHistogramBody(const ulonglong2 *__restrict__ in, uint64_t n, uint32_t tpb,
                                                  uint32_t bits, uint32_t *__restrict__ blockHist, KeyMix mix,
@@ -225,13 +244,16 @@ static SampledSideArgs sampledSide(const SampledInput &x) {
                          x.stride, reinterpret_cast<unsigned long long *>(x.totals)};
 }
 
-void netSampledTotals(const SampledInput *sides, uint32_t count, uint32_t bits, hipStream_t s, KeyMix mix) {
+void netSampledTotals(const SampledInput *sides, uint32_t count, uint32_t bits, hipStream_t s, KeyMix mix,
+                      bool preZeroed) {
   HJ_CHECK(bits >= 1 && bits <= MAX_PART_BITS, "netSampledTotals: bits=%u out of range", bits);
   HJ_CHECK(count == 1 || count == 2, "netSampledTotals: %u sides", count);
   const uint32_t F = 1u << bits;
   const size_t bytes = (size_t)NGROUPS * F * sizeof(uint64_t);
   // Both sides' totals adjacent: one clear.
-  if (count == 2 && sides[1].totals == sides[0].totals + (size_t)NGROUPS * F) {
+  if (preZeroed) {
+    // DeviceControl totals: the layout kernel that read them last cleared them.
+  } else if (count == 2 && sides[1].totals == sides[0].totals + (size_t)NGROUPS * F) {
     HIP_CHECK(hipMemsetAsync(sides[0].totals, 0, 2 * bytes, s));
   } else {
     for (uint32_t i = 0; i < count; ++i) HIP_CHECK(hipMemsetAsync(sides[i].totals, 0, bytes, s));
@@ -407,7 +429,7 @@ void netGroupTotals(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint
 // array: the local pass and wide tuples recompute the digit from the staged
 // word, and compressed words carry it in their top bits whenever the key
 // range leaves `bits` spare bits (JoinPlan knows; the 1B config does).
-struct NetCompressedPol {  // 16 B tuple -> 8 B CompressedTuple, digit in the top bits
+struct NetCompressedPol : PlainLoad<ulonglong2> {  // 16 B tuple -> 8 B CompressedTuple, digit in the top bits
   using InT = ulonglong2;
   using StageT = uint64_t;
   using OutT = uint64_t;
@@ -434,13 +456,42 @@ struct NetCompressedDigPol : NetCompressedPol {  // no spare bits: digits staged
   __device__ __forceinline__ OutT out(const StageT &v) const { return v; }
   __device__ __forceinline__ void store(OutT *o, uint64_t pos, const StageT &v) const { o[pos] = out(v); }
 };
+// Key-only words (count-only joins of keys too wide for a CompressedTuple,
+// JoinPlan::keyOnly): value = mixed key >> bits, digit in the top bits (the
+// word has `bits` spare bits by construction); only keys are loaded.  MIX is
+// the plan's key mixing as a compile-time choice (no branch per element).
+template <bool MIX>
+__device__ __forceinline__ uint64_t mixKey(const KeyMix &m, uint64_t k) {
+  if constexpr (MIX)
+    return KeyMix{1u, m.bits}.apply(k);
+  else
+    return k;
+}
+template <bool MIX>
+struct NetKeyPol : KeyLoad {
+  using InT = ulonglong2;
+  using StageT = uint64_t;
+  using OutT = uint64_t;
+  static constexpr bool kDigArray = false;
+  uint64_t mask;
+  uint32_t bits;
+  KeyMix mix;
+  __device__ __forceinline__ uint32_t digit(const LoadT &k) const { return (uint32_t)(mixKey<MIX>(mix, k) & mask); }
+  __device__ __forceinline__ StageT stage(const LoadT &k, uint32_t d) const {
+    return (mixKey<MIX>(mix, k) >> bits) | ((uint64_t)d << (64 - bits));
+  }
+  __device__ __forceinline__ uint32_t stagedDigit(const StageT &v) const { return (uint32_t)(v >> (64 - bits)); }
+  __device__ __forceinline__ OutT out(const StageT &v) const { return v & (~0ull >> bits); }
+  __device__ __forceinline__ void store(OutT *o, uint64_t pos, const StageT &v) const { o[pos] = out(v); }
+};
 // Count-only projection: a counting join never reads a rid, so the network
 // pass keeps only the key fragment above the network digit (4 bytes instead
 // of the 8-byte CompressedTuple; the reference compares key bits only,
 // tasks/BuildProbe.cpp:101-102, and reports only the count, :115).  The
 // digit rides in the staged word's top bits (fragBits + bits <= 32, checked
 // by the launcher).
-struct NetFragPol {
+template <bool MIX>
+struct NetFragPolT : KeyLoad {
   using InT = ulonglong2;
   using StageT = uint32_t;
   using OutT = uint32_t;
@@ -448,15 +499,16 @@ struct NetFragPol {
   uint64_t mask;
   uint32_t bits;
   KeyMix mix;
-  __device__ __forceinline__ uint32_t digit(const InT &x) const { return (uint32_t)(mix.apply(x.x) & mask); }
-  __device__ __forceinline__ StageT stage(const InT &x, uint32_t d) const {
-    return (uint32_t)(mix.apply(x.x) >> bits) | (d << (32 - bits));
+  __device__ __forceinline__ uint32_t digit(const LoadT &k) const { return (uint32_t)(mixKey<MIX>(mix, k) & mask); }
+  __device__ __forceinline__ StageT stage(const LoadT &k, uint32_t d) const {
+    return (uint32_t)(mixKey<MIX>(mix, k) >> bits) | (d << (32 - bits));
   }
   __device__ __forceinline__ uint32_t stagedDigit(const StageT &v) const { return v >> (32 - bits); }
   __device__ __forceinline__ OutT out(const StageT &v) const { return v & (0xFFFFFFFFu >> bits); }
   __device__ __forceinline__ void store(OutT *o, uint64_t pos, const StageT &v) const { o[pos] = out(v); }
 };
-struct NetWidePol {  // 16 B tuple -> 16 B tuple (full-range keys)
+using NetFragPol = NetFragPolT<false>;  // ablation entry (no key mixing)
+struct NetWidePol : PlainLoad<ulonglong2> {  // 16 B tuple -> 16 B tuple (full-range keys)
   using InT = ulonglong2;
   using StageT = ulonglong2;
   using OutT = ulonglong2;
@@ -471,7 +523,7 @@ struct NetWidePol {  // 16 B tuple -> 16 B tuple (full-range keys)
   __device__ __forceinline__ OutT out(const StageT &v) const { return v; }
   __device__ __forceinline__ void store(OutT *o, uint64_t pos, const StageT &v) const { o[pos] = out(v); }
 };
-struct LocalCompressedPol {  // 8 B -> 8 B, digit = (value >> shift) & mask
+struct LocalCompressedPol : PlainLoad<uint64_t> {  // 8 B -> 8 B, digit = (value >> shift) & mask
   using InT = uint64_t;
   using StageT = uint64_t;
   using OutT = uint64_t;
@@ -484,7 +536,7 @@ struct LocalCompressedPol {  // 8 B -> 8 B, digit = (value >> shift) & mask
   __device__ __forceinline__ OutT out(const StageT &v) const { return v; }
   __device__ __forceinline__ void store(OutT *o, uint64_t pos, const StageT &v) const { o[pos] = out(v); }
 };
-struct LocalWidePol {  // 16 B -> 16 B, digit = (key >> shift) & mask
+struct LocalWidePol : PlainLoad<ulonglong2> {  // 16 B -> 16 B, digit = (key >> shift) & mask
   using InT = ulonglong2;
   using StageT = ulonglong2;
   using OutT = ulonglong2;
@@ -499,7 +551,7 @@ struct LocalWidePol {  // 16 B -> 16 B, digit = (key >> shift) & mask
 };
 // u32 key fragment -> u16 of the bits above the local digit (count-only
 // two-level pass, JoinPlan::fragments): 2 bytes written per tuple.
-struct LocalFragPol {
+struct LocalFragPol : PlainLoad<uint32_t> {
   using InT = uint32_t;
   using StageT = uint32_t;
   using OutT = uint16_t;
@@ -524,15 +576,18 @@ struct LocalSplitPol : LocalCompressedPol {  // 8 B -> u32 rid / key low word + 
   }
 };
 
-// LDS per workgroup: cursor and wbase (F x CurT), cnt and off (F x u32), scan
-// scratch, the reordered tile (TILE x StageT) and, only for
-// NetCompressedDigPol, the tile's digits (TILE x u16).  At F = 1024 with
-// 32-bit cursors and 8-byte words: 16 KiB + 32 KiB -> three 256-thread
-// workgroups (12 wave64s) per CU.
+// Digit arrays in LDS are padded to at least 1024 entries (the widest
+// workgroup): every thread of the claim loop then owns whole, existing
+// entries, and the loop needs no per-thread bound check (see scatterTile).
+HJ_HD uint32_t padDigits(uint32_t F) { return F > 1024u ? F : 1024u; }
+
+// LDS per workgroup: cursor and wbase (FP x CurT), cnt and off (FP x u32)
+// with FP = padDigits(F), scan scratch, the reordered tile (TILE x StageT)
+// and, only for NetCompressedDigPol, the tile's digits (TILE x u16).
 template <class Pol, typename CurT, int TILE>
 struct ScatterLayout {
   static __host__ __device__ constexpr size_t valOffset(uint32_t F) {
-    return ((size_t)F * (2 * sizeof(CurT) + 8) + 64 + 15) & ~size_t(15);
+    return ((size_t)padDigits(F) * (2 * sizeof(CurT) + 8) + 64 + 15) & ~size_t(15);
   }
   static __host__ __device__ constexpr size_t bytes(uint32_t F) {
     return valOffset(F) + (size_t)TILE * sizeof(typename Pol::StageT) + (Pol::kDigArray ? (size_t)TILE * 2 : 0);
@@ -547,37 +602,83 @@ struct ScatterSmem {
   typename Pol::StageT *val;
   uint16_t *dig;
   __device__ __forceinline__ ScatterSmem(unsigned char *smem, uint32_t F) {
+    const uint32_t FP = padDigits(F);
     cursor = reinterpret_cast<CurT *>(smem);
-    wbase = cursor + F;
-    cnt = reinterpret_cast<uint32_t *>(wbase + F);
-    off = cnt + F;
-    wave = off + F;
+    wbase = cursor + FP;
+    cnt = reinterpret_cast<uint32_t *>(wbase + FP);
+    off = cnt + FP;
+    wave = off + FP;
     val = reinterpret_cast<typename Pol::StageT *>(smem + ScatterLayout<Pol, CurT, TILE>::valOffset(F));
     dig = reinterpret_cast<uint16_t *>(val + TILE);
   }
 };
 
-template <class Pol, int NTH, int IPT, bool FULL>
-__device__ __forceinline__ void loadTile(const typename Pol::InT *__restrict__ src, uint32_t count,
-                                         typename Pol::InT (&v)[IPT]) {
-#pragma unroll
-  for (int i = 0; i < IPT; ++i) {
-    const uint32_t idx = i * NTH + threadIdx.x;
-    if (FULL || idx < count) v[i] = Loader<typename Pol::InT>::load(src + idx);
+// Where the branch-free scatter sends what must not land in the output:
+// stores of lanes without an element (a range's tail tile) or past a bounded
+// slice, and the claim atomics of padding digits (adding 0).  Writing these
+// to scratch instead of branching around them keeps the tile loop free of
+// divergent control flow: after a store or atomic under an exec mask the
+// compiler's wait-count pass can no longer count the wave's memory operations
+// and falls back to vmcnt(0) -- every load and store of the wave in flight
+// must land -- and it serialises the write-out's LDS reads element by element.
+__device__ ulonglong2 g_scatterTrash[1024];
+
+template <class P, class = void>
+struct TwoArrayStore : std::false_type {};
+template <class P>
+struct TwoArrayStore<P, std::void_t<decltype(&P::hi)>> : std::true_type {};
+
+// Stores x at out[pos] when ok, else into the trash line of thread t.
+template <class Pol>
+__device__ __forceinline__ void storeSel(const Pol &pol, typename Pol::OutT *out, uint64_t pos,
+                                         const typename Pol::StageT &x, bool ok, uint32_t t) {
+  using OutT = typename Pol::OutT;
+  OutT *trash = reinterpret_cast<OutT *>(g_scatterTrash);
+  if constexpr (TwoArrayStore<Pol>::value) {
+    uint16_t *hi = ok ? pol.hi + pos : reinterpret_cast<uint16_t *>(g_scatterTrash + 512) + t;
+    OutT *lo = ok ? out + pos : trash + t;
+    *lo = (OutT)(x >> pol.loShift);
+    *hi = (uint16_t)(x >> pol.fragShift);
+  } else {
+    OutT *p = ok ? out + pos : trash + t;
+    *p = pol.out(x);
   }
 }
 
-// One tile.  FULL tiles (every tile but a range's tail) are branch-free so
-// hipcc can keep all IPT LDS atomics, loads and stores in flight with counted
-// waits; the predicated tail path is only taken once per range.
+template <class Pol, int NTH, int IPT, bool FULL>
+__device__ __forceinline__ void loadTile(const typename Pol::InT *__restrict__ src, uint32_t count,
+                                         typename Pol::LoadT (&v)[IPT]) {
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    const uint32_t idx = i * NTH + threadIdx.x;
+    if (FULL || idx < count) v[i] = Pol::load(src + idx);
+  }
+}
+
+// Next tile into registers, branch-free: indices past the range end read its
+// last element (loaded, never ranked), so every tile issues exactly IPT loads.
+template <class Pol, int NTH, int IPT>
+__device__ __forceinline__ void prefetchTile(const typename Pol::InT *__restrict__ in, uint64_t nbase, uint64_t last,
+                                             typename Pol::LoadT (&v)[IPT]) {
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    const uint64_t idx = nbase + (uint64_t)(i * NTH + threadIdx.x);
+    v[i] = Pol::load(in + (idx < last ? idx : last));
+  }
+}
+
+// One tile.  FULL tiles (every tile but a range's tail) have no divergent
+// control flow at all, so hipcc keeps the IPT LDS atomics, loads and stores
+// in flight with counted waits; the tail tile predicates its LDS work only.
 // BOUNDED (claim mode with estimated slices): l.cursor[d] holds the end of the
 // group's slice of digit d; claimed positions past it are not written (the
 // caller detects the overflow from the final claim cursors and re-runs).
-template <class Pol, typename CurT, int NTH, int IPT, int MODE, bool FULL, bool CLAIM, bool BOUNDED = false>
+// MAXD = padDigits(F) / NTH claim entries per thread.
+template <class Pol, typename CurT, int NTH, int IPT, int MODE, bool FULL, bool CLAIM, bool BOUNDED, int MAXD>
 __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict__ in, uint64_t base, uint64_t end,
                                             uint32_t count, uint32_t F, const ScatterSmem<Pol, CurT, NTH * IPT> &l,
                                             const Pol &pol, typename Pol::OutT *__restrict__ out,
-                                            typename Pol::InT (&v)[IPT], CurT *__restrict__ gcur) {
+                                            typename Pol::LoadT (&v)[IPT], CurT *__restrict__ gcur) {
   constexpr uint32_t TILE = NTH * IPT;
   const uint32_t t = threadIdx.x;
   uint32_t dr[IPT];
@@ -589,18 +690,28 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
       dr[i] = (d << 16) | atomicAdd(&l.cnt[d], 1u);
     }
   }
-  __syncthreads();  // A: counts final; previous tile's write-out done
-  blockExclusiveScanLds<NTH, uint32_t, uint32_t>(l.cnt, l.off, (int)F, l.wave);
-  constexpr int MAXD = (1 << MAX_PART_BITS) / NTH > 0 ? (1 << MAX_PART_BITS) / NTH : 1;
+  // Barriers of the tile loop order LDS only (ldsBarrier): the waves share
+  // nothing through global memory here, and a full __syncthreads() would make
+  // every wave wait for its prefetch of the next tile (vmcnt(0)) before the
+  // write-out, so loads and stores of a workgroup would never overlap.
+  ldsBarrier();  // A: counts final; previous tile's write-out done
   CurT claim[MAXD];
   if constexpr (CLAIM) {
-    // One device atomic per digit claims this tile's run in the group's slice.
+    // One device atomic per digit claims this tile's run in the group's slice,
+    // issued before the scan so its round trip overlaps the scan.  Waves whose
+    // digits are all padding (d >= F: F < NTH) skip it on a scalar branch (no
+    // exec mask); a wave straddling F (only F < 64) sends its padding lanes'
+    // zero adds to the trash.
+    CurT *trash = reinterpret_cast<CurT *>(g_scatterTrash);
+    const uint32_t wave0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(t & ~(uint32_t)(WAVE - 1)));
 #pragma unroll
     for (int k = 0; k < MAXD; ++k) {
       const uint32_t d = t + k * NTH;
-      if (d < F) claim[k] = atomicAdd(&gcur[d], (CurT)l.cnt[d]);
+      if (wave0 + k * NTH < F) claim[k] = atomicAdd(d < F ? gcur + d : trash + t, (CurT)l.cnt[d]);
     }
-  } else {
+  }
+  blockExclusiveScanLds<NTH, uint32_t, uint32_t, true>(l.cnt, l.off, (int)F, l.wave);
+  if constexpr (!CLAIM) {
     for (uint32_t d = t; d < F; d += NTH) {
       const CurT c = l.cursor[d];
       l.wbase[d] = c - (CurT)l.off[d];  // wraps; wbase + idx lands back in range
@@ -608,83 +719,81 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
       l.cnt[d] = 0;
     }
   }
+  // Staging: every position first, then every write (one batch of LDS reads
+  // and one of writes; interleaved, each write waited for its own read).
+  uint32_t pos[IPT];
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    const uint32_t idx = i * NTH + t;
+    if (FULL || idx < count) pos[i] = l.off[dr[i] >> 16] + (dr[i] & 0xFFFFu);
+  }
 #pragma unroll
   for (int i = 0; i < IPT; ++i) {
     const uint32_t idx = i * NTH + t;
     if (FULL || idx < count) {
       const uint32_t d = dr[i] >> 16;
-      const uint32_t pos = l.off[d] + (dr[i] & 0xFFFFu);
-      l.val[pos] = pol.stage(v[i], d);
-      if constexpr (Pol::kDigArray) l.dig[pos] = (uint16_t)d;
+      l.val[pos[i]] = pol.stage(v[i], d);
+      if constexpr (Pol::kDigArray) l.dig[pos[i]] = (uint16_t)d;
     }
   }
   // Prefetch the next tile while this one is streamed out.
-  const uint64_t nbase = base + TILE;
-  if (nbase + TILE <= end)
-    loadTile<Pol, NTH, IPT, true>(in + nbase, TILE, v);
-  else if (nbase < end)
-    loadTile<Pol, NTH, IPT, false>(in + nbase, (uint32_t)(end - nbase), v);
+  prefetchTile<Pol, NTH, IPT>(in, base + TILE, end - 1, v);
   if constexpr (CLAIM) {
 #pragma unroll
-    for (int k = 0; k < MAXD; ++k) {
+    for (int k = 0; k < MAXD; ++k) {  // padding entries get garbage bases nobody reads
       const uint32_t d = t + k * NTH;
-      if (d < F) {
-        l.wbase[d] = claim[k] - (CurT)l.off[d];
-        l.cnt[d] = 0;
-      }
+      l.wbase[d] = claim[k] - (CurT)l.off[d];
+      l.cnt[d] = 0;
     }
   }
-  __syncthreads();  // B: staged tile and write bases visible
+  ldsBarrier();  // B: staged tile and write bases visible
 #pragma unroll
   for (int i = 0; i < IPT; ++i) {
     const uint32_t idx = i * NTH + t;
-    if (FULL || idx < count) {
-      const typename Pol::StageT x = l.val[idx];
-      uint32_t d;
-      if constexpr (Pol::kDigArray)
-        d = l.dig[idx];
-      else
-        d = pol.stagedDigit(x);
-      if constexpr (MODE == 0) {
-        const CurT pos = (CurT)(l.wbase[d] + (CurT)idx);
-        if constexpr (BOUNDED) {
-          if (pos < l.cursor[d]) pol.store(out, (uint64_t)pos, x);
-        } else {
-          pol.store(out, (uint64_t)pos, x);
-        }
-      } else if constexpr (MODE == 1) {
-        out[base + idx] = pol.out(x);
-        asm volatile("" ::"v"(l.wbase[d]));
-      } else {
-        const auto y = pol.out(x);
-        asm volatile("" ::"v"(y), "v"(l.wbase[d]));
-      }
+    const bool have = FULL || idx < count;
+    const uint32_t at = have ? idx : 0;  // the tail tile's element 0 exists
+    const typename Pol::StageT x = l.val[at];
+    uint32_t d;
+    if constexpr (Pol::kDigArray)
+      d = l.dig[at];
+    else
+      d = pol.stagedDigit(x);
+    if constexpr (MODE == 0) {
+      const CurT pos = (CurT)(l.wbase[d] + (CurT)idx);
+      bool ok = have;
+      if constexpr (BOUNDED) ok = ok && pos < l.cursor[d];
+      storeSel(pol, out, (uint64_t)pos, x, ok, t);
+    } else if constexpr (MODE == 1) {
+      if (have) out[base + idx] = pol.out(x);
+      asm volatile("" ::"v"(l.wbase[d]));
+    } else {
+      const auto y = pol.out(x);
+      asm volatile("" ::"v"(y), "v"(l.wbase[d]));
     }
   }
 }
 
 // Scatter [begin, end) of `in` into `out` at the cursors held in LDS
 // (initialised by the caller, advanced here).  Per tile:
-//   rank (LDS atomics) | A | scan + per-digit write base | stage into LDS,
-//   prefetch next tile into registers | B | stream the reordered tile out.
+//   rank (LDS atomics) | A | claim + scan + per-digit write base | stage into
+//   LDS, prefetch next tile into registers | B | stream the reordered tile out.
 // MODE (ablation only): 0 = real scatter, 1 = coalesced write-out, 2 = none.
-template <class Pol, typename CurT, int NTH, int IPT, int MODE, bool CLAIM = false, bool BOUNDED = false>
+template <class Pol, typename CurT, int NTH, int IPT, int MODE, bool CLAIM = false, bool BOUNDED = false,
+          int MAXD = 1>
 __device__ __forceinline__ void scatterRange(const typename Pol::InT *__restrict__ in, uint64_t begin, uint64_t end,
                                              uint32_t F, unsigned char *smem, const Pol &pol,
                                              typename Pol::OutT *__restrict__ out, CurT *gcur = nullptr) {
   constexpr uint32_t TILE = NTH * IPT;
   const ScatterSmem<Pol, CurT, TILE> l(smem, F);
-  typename Pol::InT v[IPT];
-  if (begin + TILE <= end)
-    loadTile<Pol, NTH, IPT, true>(in + begin, TILE, v);
-  else if (begin < end)
-    loadTile<Pol, NTH, IPT, false>(in + begin, (uint32_t)(end - begin), v);
+  typename Pol::LoadT v[IPT];
+  if (begin < end) prefetchTile<Pol, NTH, IPT>(in, begin, end - 1, v);
   for (uint64_t base = begin; base < end; base += TILE) {
     if (base + TILE <= end)
-      scatterTile<Pol, CurT, NTH, IPT, MODE, true, CLAIM, BOUNDED>(in, base, end, TILE, F, l, pol, out, v, gcur);
+      scatterTile<Pol, CurT, NTH, IPT, MODE, true, CLAIM, BOUNDED, MAXD>(in, base, end, TILE, F, l, pol, out, v,
+                                                                         gcur);
     else
-      scatterTile<Pol, CurT, NTH, IPT, MODE, false, CLAIM, BOUNDED>(in, base, end, (uint32_t)(end - base), F, l, pol,
-                                                                    out, v, gcur);
+      scatterTile<Pol, CurT, NTH, IPT, MODE, false, CLAIM, BOUNDED, MAXD>(in, base, end, (uint32_t)(end - base), F, l,
+                                                                          pol, out, v, gcur);
   }
   __syncthreads();
 }
@@ -696,45 +805,60 @@ struct ScatterOcc {
   static constexpr int value = NTH == 256 ? 3 : (NTH == 512 ? 4 : 4);
 };
 
+// Per-workgroup cursors (ablation baseline): F <= NTH * MAXD digits, no claims.
 template <class Pol, typename CurT, int NTH, int IPT, int MODE>
 __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void netScatterKernel(
     const typename Pol::InT *__restrict__ in, uint64_t n, uint32_t tpb, uint32_t F, Pol pol, uint32_t totalBlocks,
     uint32_t blockBegin, const uint64_t *__restrict__ cursors, typename Pol::OutT *out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr uint32_t TILE = NTH * IPT;
   const uint32_t blk = blockBegin + blockIdx.x;
+  const uint32_t FP = padDigits(F);
   CurT *cursor = reinterpret_cast<CurT *>(smem);
-  uint32_t *cnt = reinterpret_cast<uint32_t *>(cursor + 2 * F);
-  for (uint32_t d = threadIdx.x; d < F; d += NTH) {
-    cursor[d] = (CurT)cursors[(uint64_t)d * totalBlocks + blk];
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(cursor + 2 * FP);
+  for (uint32_t d = threadIdx.x; d < FP; d += NTH) {
+    if (d < F) cursor[d] = (CurT)cursors[(uint64_t)d * totalBlocks + blk];
     cnt[d] = 0;
   }
   __syncthreads();
   const uint64_t begin = (uint64_t)blk * tpb * PART_TILE;  // geometry is in PART_TILE units
   const uint64_t end = min(n, begin + (uint64_t)tpb * PART_TILE);
-  (void)TILE;
   scatterRange<Pol, CurT, NTH, IPT, MODE>(in, begin, end, F, smem, pol, out);
 }
 
 // Claim-mode network scatter: cursors come from the group slices (gcur is
 // [NGROUPS][F] for this chunk), so no per-workgroup cursor array is loaded.
-template <class Pol, typename CurT, int NTH, int IPT, int MODE, bool BOUNDED = false>
+// MAXD = padDigits(F) / NTH (scatterLaunchMaxd).
+template <class Pol, typename CurT, int NTH, int IPT, int MODE, bool BOUNDED, int MAXD>
 __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void netScatterClaimKernel(
     const typename Pol::InT *__restrict__ in, uint64_t n, uint32_t tpb, uint32_t F, Pol pol, uint32_t blockBegin,
     CurT *__restrict__ gcur, typename Pol::OutT *out, const CurT *__restrict__ gend = nullptr) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t blk = blockBegin + blockIdx.x;
+  const uint32_t FP = padDigits(F);
   CurT *sliceEnd = reinterpret_cast<CurT *>(smem);  // the per-workgroup cursor array is unused in claim mode
-  uint32_t *cnt = reinterpret_cast<uint32_t *>(reinterpret_cast<CurT *>(smem) + 2 * F);
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(reinterpret_cast<CurT *>(smem) + 2 * FP);
   const size_t grp = (size_t)(blockIdx.x % NGROUPS) * F;
-  for (uint32_t d = threadIdx.x; d < F; d += NTH) {
+  for (uint32_t d = threadIdx.x; d < FP; d += NTH) {
     cnt[d] = 0;
-    if constexpr (BOUNDED) sliceEnd[d] = gend[grp + d];
+    if constexpr (BOUNDED)
+      if (d < F) sliceEnd[d] = gend[grp + d];
   }
   __syncthreads();
   const uint64_t begin = (uint64_t)blk * tpb * PART_TILE;
   const uint64_t end = min(n, begin + (uint64_t)tpb * PART_TILE);
-  scatterRange<Pol, CurT, NTH, IPT, MODE, true, BOUNDED>(in, begin, end, F, smem, pol, out, gcur + grp);
+  scatterRange<Pol, CurT, NTH, IPT, MODE, true, BOUNDED, MAXD>(in, begin, end, F, smem, pol, out, gcur + grp);
+}
+
+// Calls fn(std::integral_constant<int, MAXD>) with MAXD = padDigits(F) / NTH:
+// one of two values per workgroup width (F <= 1024 or F = 2048).
+template <int NTH, class Fn>
+static void withMaxd(uint32_t F, Fn &&fn) {
+  constexpr int LO = 1024 / NTH, HI = (1 << MAX_PART_BITS) / NTH;
+  static_assert(HI == 2 * LO, "withMaxd: two digit-array sizes");
+  if (padDigits(F) / NTH == (uint32_t)LO)
+    fn(std::integral_constant<int, LO>());
+  else
+    fn(std::integral_constant<int, HI>());
 }
 
 // Default geometry (measured on MI355X, tools/microbench.py ablation).
@@ -774,29 +898,25 @@ static void launchNetClaimIpt(const Pol &pol, const data::Tuple *in, uint64_t n,
   const auto *src = reinterpret_cast<const typename Pol::InT *>(in);
   auto *dst = reinterpret_cast<typename Pol::OutT *>(out);
   const dim3 grid(blockEnd - blockBegin);
-  if (narrow) {
-    const size_t lds = ScatterLayout<Pol, uint32_t, CL_NTH * CL_IPT>::bytes(F);
+  auto go = [&](auto cur, auto maxd) {
+    using C = decltype(cur);
+    constexpr int M = decltype(maxd)::value;
+    const size_t lds = ScatterLayout<Pol, C, CL_NTH * CL_IPT>::bytes(F);
     HJ_CHECK(lds <= 160 * 1024, "scatter LDS %zu too large", lds);
-    auto *gc = reinterpret_cast<uint32_t *>(gcur);
+    auto *gc = reinterpret_cast<C *>(gcur);
     if (gend)
-      hipLaunchKernelGGL((netScatterClaimKernel<Pol, uint32_t, CL_NTH, CL_IPT, 0, true>), grid, dim3(CL_NTH), lds,
-                         s, src, n, g.tilesPerBlock, F, pol, blockBegin, gc, dst,
-                         reinterpret_cast<const uint32_t *>(gend));
+      hipLaunchKernelGGL((netScatterClaimKernel<Pol, C, CL_NTH, CL_IPT, 0, true, M>), grid, dim3(CL_NTH), lds, s, src,
+                         n, g.tilesPerBlock, F, pol, blockBegin, gc, dst, reinterpret_cast<const C *>(gend));
     else
-      hipLaunchKernelGGL((netScatterClaimKernel<Pol, uint32_t, CL_NTH, CL_IPT, 0>), grid, dim3(CL_NTH), lds, s, src,
-                         n, g.tilesPerBlock, F, pol, blockBegin, gc, dst, nullptr);
-  } else {
-    const size_t lds = ScatterLayout<Pol, unsigned long long, CL_NTH * CL_IPT>::bytes(F);
-    HJ_CHECK(lds <= 160 * 1024, "scatter LDS %zu too large", lds);
-    auto *gc = reinterpret_cast<unsigned long long *>(gcur);
-    if (gend)
-      hipLaunchKernelGGL((netScatterClaimKernel<Pol, unsigned long long, CL_NTH, CL_IPT, 0, true>), grid,
-                         dim3(CL_NTH), lds, s, src, n, g.tilesPerBlock, F, pol, blockBegin, gc, dst,
-                         reinterpret_cast<const unsigned long long *>(gend));
+      hipLaunchKernelGGL((netScatterClaimKernel<Pol, C, CL_NTH, CL_IPT, 0, false, M>), grid, dim3(CL_NTH), lds, s,
+                         src, n, g.tilesPerBlock, F, pol, blockBegin, gc, dst, nullptr);
+  };
+  withMaxd<CL_NTH>(F, [&](auto maxd) {
+    if (narrow)
+      go(uint32_t(), maxd);
     else
-      hipLaunchKernelGGL((netScatterClaimKernel<Pol, unsigned long long, CL_NTH, CL_IPT, 0>), grid, dim3(CL_NTH),
-                         lds, s, src, n, g.tilesPerBlock, F, pol, blockBegin, gc, dst, nullptr);
-  }
+      go((unsigned long long)0, maxd);
+  });
   HIP_CHECK_LAUNCH();
 }
 
@@ -843,13 +963,25 @@ void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keySh
   HJ_CHECK(blockBegin <= blockEnd && blockEnd <= g.blocks, "netScatter: block range [%u,%u) of %u", blockBegin,
            blockEnd, g.blocks);
   if (n == 0 || blockEnd == blockBegin) return;
+  HJ_CHECK(withRids || keyShift == 0, "netScatter: key-only words need keyShift 0 (got %u)", keyShift);
+  if (!withRids) {  // key >> bits always leaves `bits` spare top bits
+    auto go = [&](auto kpol) {
+      kpol.mask = (1ull << bits) - 1;
+      kpol.bits = bits;
+      kpol.mix = mix;
+      launchNetClaim(kpol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
+    };
+    if (mix.on)
+      go(NetKeyPol<true>());
+    else
+      go(NetKeyPol<false>());
+    return;
+  }
   NetCompressedPol pol;
   pol.mask = (1ull << bits) - 1;
   pol.bits = bits;
   pol.keyShift = keyShift;
   pol.mix = mix;
-  pol.ridMask = withRids ? ~0ull : 0ull;
-  HJ_CHECK(withRids || keyShift == 0, "netScatter: key-only words need keyShift 0 (got %u)", keyShift);
   if (digitFitsOnTop(bits, keyShift, mix.on ? std::max(keyBits, mix.bits) : keyBits)) {
     launchNetClaim(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
   } else {
@@ -884,11 +1016,16 @@ void netScatterFrag(const data::Tuple *in, uint64_t n, uint32_t bits, const Part
   HJ_CHECK(blockBegin <= blockEnd && blockEnd <= g.blocks, "netScatterFrag: block range [%u,%u) of %u", blockBegin,
            blockEnd, g.blocks);
   if (n == 0 || blockEnd == blockBegin) return;
-  NetFragPol pol;
-  pol.mask = (1ull << bits) - 1;
-  pol.bits = bits;
-  pol.mix = mix;
-  launchNetClaim(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
+  auto go = [&](auto pol) {
+    pol.mask = (1ull << bits) - 1;
+    pol.bits = bits;
+    pol.mix = mix;
+    launchNetClaim(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
+  };
+  if (mix.on)
+    go(NetFragPolT<true>());
+  else
+    go(NetFragPolT<false>());
 }
 
 // ------------------------------------------------ device-side sampled layout
@@ -908,6 +1045,7 @@ struct LayoutSideArgs {
   SampleScale sc;
   CurT *gstart, *gcur, *gend;
   unsigned long long *capacityUsed;
+  unsigned long long *clear;  // = sampled when it is DeviceControl scratch, else nullptr
 };
 
 // Workgroup i lays out side i (one or two sides per launch).
@@ -945,6 +1083,7 @@ __global__ __launch_bounds__(LAY_NT) void netSampledLayoutKernel(LayoutSideArgs<
         const double margin = sc.sigmas * sqrt(fmax(est, scale) * scale) + sc.frac * est + sc.floor;
         c = fmin(ceil(est + margin), total);
       }
+      if (ls.clear) ls.clear[(size_t)g * F + d] = 0;  // read once (above), by this thread
       cap[k] = ((unsigned long long)c + 15ull) & ~15ull;
       local += cap[k];
     }
@@ -971,9 +1110,11 @@ __global__ __launch_bounds__(LAY_NT) void netSampledLayoutKernel(LayoutSideArgs<
 
 template <typename CurT>
 static LayoutSideArgs<CurT> layoutSide(const LayoutInput &x) {
-  return LayoutSideArgs<CurT>{reinterpret_cast<const unsigned long long *>(x.sampled), x.sc,
+  auto *sampled = reinterpret_cast<const unsigned long long *>(x.sampled);
+  return LayoutSideArgs<CurT>{sampled, x.sc,
                               static_cast<CurT *>(x.gstart), static_cast<CurT *>(x.gcur), static_cast<CurT *>(x.gend),
-                              x.capacityUsed};
+                              x.capacityUsed,
+                              x.clearSampled ? const_cast<unsigned long long *>(sampled) : nullptr};
 }
 
 void netSampledLayout(const LayoutInput *sides, uint32_t count, uint32_t F, bool narrow, hipStream_t s) {
@@ -1043,18 +1184,19 @@ void scatterAblation(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t 
   NetCompressedDigPol dpol;
   static_cast<NetCompressedPol &>(dpol) = pol;
 #define HJ_CLAIM(NTH, IPT)                                                                                        \
-  do {                                                                                                            \
+  withMaxd<NTH>(1u << bits, [&](auto maxd) {                                                                      \
+    constexpr int M = decltype(maxd)::value;                                                                      \
     const size_t lds = ScatterLayout<NetCompressedPol, uint32_t, NTH * IPT>::bytes(1u << bits);                  \
     auto *gc = reinterpret_cast<uint32_t *>(gcur);                                                                \
     if (mode == 1)                                                                                                \
-      hipLaunchKernelGGL((netScatterClaimKernel<NetCompressedPol, uint32_t, NTH, IPT, 1>), dim3(g.blocks),        \
+      hipLaunchKernelGGL((netScatterClaimKernel<NetCompressedPol, uint32_t, NTH, IPT, 1, false, M>), dim3(g.blocks), \
                          dim3(NTH), lds, s, reinterpret_cast<const ulonglong2 *>(in), n, g.tilesPerBlock,         \
                          1u << bits, pol, 0u, gc, out);                                                           \
     else                                                                                                          \
-      hipLaunchKernelGGL((netScatterClaimKernel<NetCompressedPol, uint32_t, NTH, IPT, 0>), dim3(g.blocks),        \
+      hipLaunchKernelGGL((netScatterClaimKernel<NetCompressedPol, uint32_t, NTH, IPT, 0, false, M>), dim3(g.blocks), \
                          dim3(NTH), lds, s, reinterpret_cast<const ulonglong2 *>(in), n, g.tilesPerBlock,         \
                          1u << bits, pol, 0u, gc, out);                                                           \
-  } while (0)
+  })
 #define HJ_ABL(P, p, NTH, IPT)                                                                                    \
   do {                                                                                                            \
     if (mode == 1) launchNet<P, uint32_t, NTH, IPT, 1>(p, in, n, bits, g, 0, g.blocks, cursors, out, s);          \
@@ -1078,9 +1220,12 @@ void scatterAblation(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t 
   using FragLayout = ScatterLayout<NetFragPol, uint32_t, 1024 * 16>;
   const size_t fragLds = FragLayout::bytes(1u << bits);
 #define HJ_FRAG(M)                                                                                                \
-  hipLaunchKernelGGL((netScatterClaimKernel<NetFragPol, uint32_t, 1024, 16, M>), dim3(g.blocks), dim3(1024),      \
-                     fragLds, s, reinterpret_cast<const ulonglong2 *>(in), n, g.tilesPerBlock, 1u << bits, fpol,  \
-                     0u, reinterpret_cast<uint32_t *>(gcur), reinterpret_cast<uint32_t *>(out))
+  withMaxd<1024>(1u << bits, [&](auto maxd) {                                                                     \
+    hipLaunchKernelGGL((netScatterClaimKernel<NetFragPol, uint32_t, 1024, 16, M, false, decltype(maxd)::value>),  \
+                       dim3(g.blocks), dim3(1024), fragLds, s, reinterpret_cast<const ulonglong2 *>(in), n,      \
+                       g.tilesPerBlock, 1u << bits, fpol, 0u, reinterpret_cast<uint32_t *>(gcur),                 \
+                       reinterpret_cast<uint32_t *>(out));                                                        \
+  })
   if (geometry == 10) {
     if (mode == 1) HJ_FRAG(1);
     else if (mode == 2) HJ_FRAG(2);
@@ -1380,7 +1525,7 @@ void claimOverflow(unsigned long long *gcur, const unsigned long long *gend, uin
   HIP_CHECK_LAUNCH();
 }
 
-template <class Pol, typename CurT, int NTH, int IPT, bool BOUNDED = false>
+template <class Pol, typename CurT, int NTH, int IPT, bool BOUNDED, int MAXD>
 __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void localScatterClaimKernel(
     const typename Pol::InT *__restrict__ in, const LocalItem *__restrict__ items, uint32_t nItems, uint32_t F,
     Pol pol, CurT *__restrict__ gcur, typename Pol::OutT *out, const CurT *__restrict__ gend) {
@@ -1388,16 +1533,39 @@ __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void localScatterClaim
   const uint32_t q = (nItems + NGROUPS - 1) / NGROUPS;
   const uint32_t item = (blockIdx.x % NGROUPS) * q + blockIdx.x / NGROUPS;  // XCD-contiguous items
   if (item >= nItems) return;  // uniform per workgroup
+  const uint32_t FP = padDigits(F);
   CurT *sliceEnd = reinterpret_cast<CurT *>(smem);
-  uint32_t *cnt = reinterpret_cast<uint32_t *>(reinterpret_cast<CurT *>(smem) + 2 * F);
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(reinterpret_cast<CurT *>(smem) + 2 * FP);
   const LocalItem it = items[item];
-  for (uint32_t d = threadIdx.x; d < F; d += NTH) {
+  for (uint32_t d = threadIdx.x; d < FP; d += NTH) {
     cnt[d] = 0;
-    if constexpr (BOUNDED) sliceEnd[d] = gend[(uint64_t)it.stream * F + d];
+    if constexpr (BOUNDED)
+      if (d < F) sliceEnd[d] = gend[(uint64_t)it.stream * F + d];
   }
   __syncthreads();
-  scatterRange<Pol, CurT, NTH, IPT, 0, true, BOUNDED>(in, it.begin, it.begin + it.len, F, smem, pol, out,
-                                                      gcur + (uint64_t)it.stream * F);
+  scatterRange<Pol, CurT, NTH, IPT, 0, true, BOUNDED, MAXD>(in, it.begin, it.begin + it.len, F, smem, pol, out,
+                                                            gcur + (uint64_t)it.stream * F);
+}
+
+// One local claim-scatter launch (MAXD from F, bounded when gend is given).
+template <class P, typename C, int NTH, int IPT>
+static void launchLocalClaim(const void *in, const LocalItem *items, uint32_t nItems, uint32_t F, const P &pol,
+                             void *gcur, void *out, const void *gend, hipStream_t s) {
+  const size_t lds = ScatterLayout<P, C, NTH * IPT>::bytes(F);
+  HJ_CHECK(lds <= 160 * 1024, "local scatter LDS %zu too large", lds);
+  const uint32_t grid = ((nItems + NGROUPS - 1) / NGROUPS) * NGROUPS;
+  withMaxd<NTH>(F, [&](auto maxd) {
+    constexpr int M = decltype(maxd)::value;
+    if (gend)
+      hipLaunchKernelGGL((localScatterClaimKernel<P, C, NTH, IPT, true, M>), dim3(grid), dim3(NTH), lds, s,
+                         reinterpret_cast<const typename P::InT *>(in), items, nItems, F, pol,
+                         reinterpret_cast<C *>(gcur), reinterpret_cast<typename P::OutT *>(out),
+                         reinterpret_cast<const C *>(gend));
+    else
+      hipLaunchKernelGGL((localScatterClaimKernel<P, C, NTH, IPT, false, M>), dim3(grid), dim3(NTH), lds, s,
+                         reinterpret_cast<const typename P::InT *>(in), items, nItems, F, pol,
+                         reinterpret_cast<C *>(gcur), reinterpret_cast<typename P::OutT *>(out), nullptr);
+  });
 }
 
 template <class P>
@@ -1414,13 +1582,7 @@ static void setSplit(LocalSplitPol &p, const SplitLayout &sl) {
 template <int NTH, int IPT>
 static void launchLocalSplitGeom(const void *in, const LocalItem *items, uint32_t nItems, uint32_t F,
                                  const LocalSplitPol &pol, void *gcur, void *out, const void *gend, hipStream_t s) {
-  const size_t lds = ScatterLayout<LocalSplitPol, unsigned long long, NTH * IPT>::bytes(F);
-  HJ_CHECK(lds <= 160 * 1024, "local scatter LDS %zu too large", lds);
-  const uint32_t grid = ((nItems + NGROUPS - 1) / NGROUPS) * NGROUPS;
-  hipLaunchKernelGGL((localScatterClaimKernel<LocalSplitPol, unsigned long long, NTH, IPT, true>), dim3(grid),
-                     dim3(NTH), lds, s, reinterpret_cast<const uint64_t *>(in), items, nItems, F, pol,
-                     reinterpret_cast<unsigned long long *>(gcur), reinterpret_cast<uint32_t *>(out),
-                     reinterpret_cast<const unsigned long long *>(gend));
+  launchLocalClaim<LocalSplitPol, unsigned long long, NTH, IPT>(in, items, nItems, F, pol, gcur, out, gend, s);
 }
 
 void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift, uint32_t bits,
@@ -1448,22 +1610,13 @@ void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nI
     HIP_CHECK_LAUNCH();
     return;
   }
-#define HJ_LOCAL(P, C)                                                                                        \
-  do {                                                                                                        \
-    P pol;                                                                                                    \
-    pol.mask = mask;                                                                                          \
-    pol.shift = shift;                                                                                        \
-    setSplit(pol, split);                                                                                     \
-    const size_t lds = ScatterLayout<P, C, CL_NTH * CL_IPT>::bytes(F);                                         \
-    if (gend)                                                                                                 \
-      hipLaunchKernelGGL((localScatterClaimKernel<P, C, CL_NTH, CL_IPT, true>), dim3(grid), dim3(CL_NTH), lds, \
-                         s, reinterpret_cast<const typename P::InT *>(in), items, nItems, F, pol,              \
-                         reinterpret_cast<C *>(gcur), reinterpret_cast<typename P::OutT *>(out),               \
-                         reinterpret_cast<const C *>(gend));                                                   \
-    else                                                                                                      \
-      hipLaunchKernelGGL((localScatterClaimKernel<P, C, CL_NTH, CL_IPT>), dim3(grid), dim3(CL_NTH), lds, s,    \
-                         reinterpret_cast<const typename P::InT *>(in), items, nItems, F, pol,                 \
-                         reinterpret_cast<C *>(gcur), reinterpret_cast<typename P::OutT *>(out), nullptr);     \
+#define HJ_LOCAL(P, C)                                                                                      \
+  do {                                                                                                      \
+    P pol;                                                                                                  \
+    pol.mask = mask;                                                                                        \
+    pol.shift = shift;                                                                                      \
+    setSplit(pol, split);                                                                                   \
+    launchLocalClaim<P, C, CL_NTH, CL_IPT>(in, items, nItems, F, pol, gcur, out, gend, s);                  \
   } while (0)
   if (frag && narrow) HJ_LOCAL(LocalFragPol, uint32_t);
   else if (frag) HJ_LOCAL(LocalFragPol, unsigned long long);

@@ -3,6 +3,8 @@
 // (/root/reference/operators/gpu/small_data.cu:95-155).  Three launches:
 // per-block reduce -> single-block scan of block sums -> per-block downsweep.
 #include "kernels.h"
+
+#include <algorithm>
 #include "device_common.h"
 
 namespace hpcjoin {
@@ -77,6 +79,20 @@ void scanExclusiveU32to64(const uint32_t *in, unsigned long long *out, uint64_t 
 }
 
 // Loads this file's code object at engine start (kernels::preloadCodeObjects).
+// Zero fill with the engine's own kernel (no runtime fill kernel: those are
+// loaded lazily by the runtime on first use).
+__global__ __launch_bounds__(SCAN_T) void zeroWordsKernel(unsigned long long *p, uint64_t words) {
+  for (uint64_t i = (uint64_t)blockIdx.x * SCAN_T + threadIdx.x; i < words; i += (uint64_t)gridDim.x * SCAN_T)
+    p[i] = 0;
+}
+
+void zeroWords(void *p, uint64_t words, hipStream_t s) {
+  if (words == 0) return;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(1024, (words + SCAN_T - 1) / SCAN_T);
+  hipLaunchKernelGGL(zeroWordsKernel, dim3(grid), dim3(SCAN_T), 0, s, static_cast<unsigned long long *>(p), words);
+  HIP_CHECK_LAUNCH();
+}
+
 void preloadScan() {
   hipFuncAttributes a;
   HIP_CHECK(hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&scanSumsKernel<uint32_t>)));

@@ -96,6 +96,7 @@ void Arena::rawFree(Location loc, void *p) {
 Arena::~Arena() { releaseAll(); }
 
 void Arena::releaseAll() {
+  ++epoch_;
   if (!fallbacks_.empty() || !chunks_.empty()) ++generation_;
   for (auto &f : fallbacks_) rawFree(loc_, f.p);
   fallbacks_.clear();
@@ -211,6 +212,7 @@ void Arena::reset() {
   // just unmapped; at 8 ranks on one GPU that second join's one-sided puts
   // missed the windows.)  Consolidation happens where a join is planned:
   // ensure() with nothing handed out re-lays everything out as one chunk.
+  ++epoch_;
   for (auto &f : fallbacks_) chunks_.push_back(Chunk{static_cast<uint8_t *>(f.p), f.bytes, 0});
   fallbacks_.clear();
   fallbackBytes_ = 0;
@@ -244,6 +246,7 @@ void Arena::freeFallback(void *p) {
       fallbackBytes_ -= fallbacks_[i].accounted;
       fallbacks_.erase(fallbacks_.begin() + i);
       ++generation_;
+      ++epoch_;
       return;
     }
 }

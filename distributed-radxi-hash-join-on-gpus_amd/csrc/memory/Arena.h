@@ -72,6 +72,10 @@ class Arena {
   uint64_t fallbackBytes() const { return fallbackBytes_; }
   size_t chunkCount() const { return chunks_.size(); }
   uint64_t generation() const { return generation_; }
+  // Counts rewinds and frees: memory handed out before an epoch change may
+  // be handed out again (or be gone), so a result left in the workspace
+  // (HashJoin::getOutput) is valid only while the epoch is unchanged.
+  uint64_t epoch() const { return epoch_; }
   bool owns(const void *p) const;
   // Start of the raw allocation (chunk or fallback) holding p; null if none.
   void *allocationOf(const void *p) const;
@@ -94,6 +98,7 @@ class Arena {
   uint64_t fallbackBytes_ = 0;
   uint64_t peakFallback_ = 0;  // largest fallbackBytes_ since the last reset
   uint64_t generation_ = 0;
+  uint64_t epoch_ = 0;
   struct Fallback {
     void *p;
     uint64_t bytes;      // allocated

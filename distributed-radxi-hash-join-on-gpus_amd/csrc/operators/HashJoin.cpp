@@ -15,6 +15,7 @@
 #include "../performance/Timeline.h"
 #include "../performance/Trace.h"
 #include "../tasks/BitmapJoin.h"
+#include "ExchangeVerify.h"
 #include "JoinStrategies.h"
 #include "../utils/Fault.h"
 #include "../utils/Hip.h"
@@ -193,14 +194,22 @@ void HashJoin::makeJoinPlan() {
     if (config.workspaceBudget) want = std::min<uint64_t>(want, config.workspaceBudget);
     // Rewound first: a previous join's buffers are dead once a new join is
     // planned on this context, so the chunks are re-laid out instead of
-    // growing on top of them.  One rank with the whole estimate: one chunk per
-    // part; otherwise one chunk (capped: of what the cap allows).  N > 1 keeps
-    // the single chunk: with a chunk per part the 4- and 8-process RCCL test
-    // (IPC-mapped one-sided windows, workspaces re-laid out between joins)
-    // hung in 4 of 5 runs (gpurun_out/r4final3, rccl_repeat1), never before.
+    // growing on top of them.  With the whole estimate: one chunk per part;
+    // otherwise one chunk (capped: of what the cap allows).
+    // N > 1: re-laying out frees chunks that peers may still have IPC-mapped
+    // (one-sided windows of an earlier join).  The free is made a collective
+    // step: every rank finishes its device work, closes its mappings of peers'
+    // memory, and waits until all peers have closed theirs before any rank
+    // frees (the uncoordinated free was a suspected cause of the
+    // hangs and failed IPC opens of the 4/8-process test).
+    if (numberOfNodes > 1) {
+      ctx->synchronize();
+      ctx->releaseImports();
+      ctx->comm()->barrier();
+    }
     ctx->workspace().reset();
-    reserved = (want == est && numberOfNodes == 1) ? ctx->workspace().ensureParts(parts, true, ctx->stream())
-                                                   : ctx->workspace().ensure(want, true, ctx->stream());
+    reserved = want == est ? ctx->workspace().ensureParts(parts, true, ctx->stream())
+                           : ctx->workspace().ensure(want, true, ctx->stream());
     JOIN_DEBUG("HashJoin", "workspace: estimate %.2f GB, added %.2f GB", want / 1e9, reserved / 1e9);
   }
   reserveMs = (nowUs() - tReserve) / 1000.0;
@@ -434,6 +443,8 @@ bool HashJoin::lowKeyBitsSkewed() {
   return skewed;
 }
 
+bool HashJoin::outputValid() const { return output && ctx->workspace().epoch() == outputEpoch; }
+
 void HashJoin::join() {
   run();
   RESULT_COUNTER = result.localMatches;
@@ -522,6 +533,13 @@ JoinResult HashJoin::runImpl() {
     run.inner->assertAllTuplesWritten();
     run.outer->assertAllTuplesWritten();
   }
+  const bool verify = numberOfNodes > 1 && run.hc &&
+                      (config.verifyExchange == core::PlanChoice::On ||
+                       (config.verifyExchange == core::PlanChoice::Auto && plan.oneSided));
+  if (verify) {  // both windows complete first (the outer one may still be on the links)
+    run.outer->stop();
+    result.exchangeChecked = verifyExchange(env, run).cells;
+  }
   if (dev && !run.networkEventRecorded) HIP_CHECK(hipEventRecord(ev[2], ctx->stream()));
   Measurements::stopWaitingForNetworkCompletion();
   run.t3 = nowUs();
@@ -532,6 +550,7 @@ JoinResult HashJoin::runImpl() {
   const uint64_t t4 = nowUs();
   ctx->timeline().resolve();  // every stream was synchronised above
   output = local.buildProbes().empty() ? nullptr : local.buildProbes().front()->getOutput();
+  outputEpoch = ctx->workspace().epoch();
   local.release();
   result.wireBytes = run.inner->wireBytesSent() + run.outer->wireBytesSent();
   result.innerReceived = run.inner->computeLocalWindowSize();
@@ -569,6 +588,8 @@ void HashJoin::recordTimes(const JoinRun &run, uint64_t t4) {
   result.devLocalPartitionMs = ms;
   HIP_CHECK(hipEventElapsedTime(&ms, ev[3], ev[4]));
   result.devBuildProbeMs = ms;
+  HIP_CHECK(hipEventElapsedTime(&ms, ev[0], ev[4]));
+  result.devSpanMs = ms;
   Measurements::storeDevicePhase("DHIST", result.devHistogramMs);
   Measurements::storeDevicePhase("DNET", result.devNetworkMs);
   Measurements::storeDevicePhase("DLOCPART", result.devLocalPartitionMs);

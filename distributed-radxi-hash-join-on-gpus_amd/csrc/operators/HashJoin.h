@@ -40,6 +40,11 @@ struct JoinResult {
   double histogramMs = 0, windowMs = 0, networkMs = 0, localMs = 0;  // host phases
   double devHistogramMs = 0, devNetworkMs = 0, devLocalPartitionMs = 0, devBuildProbeMs = 0;  // hipEvents
   double setupMs = 0, teardownMs = 0;  // outside the join span: scratch reset / result reduction
+  // Host side of the join span: enqueue (join start -> last kernel enqueued)
+  // and the wait for the result after it; devSpanMs = first -> last event.
+  // joinMs - devSpanMs is what the host added around the device work.
+  double enqueueMs = 0, hostWaitMs = 0, devSpanMs = 0;
+  uint64_t exchangeChecked = 0;    // (source, chunk, partition) runs whose content was verified (verifyExchange)
   uint64_t innerReceived = 0, outerReceived = 0;
   uint64_t wireBytes = 0;          // bytes this rank sent to peers (after the wire codec)
   uint64_t localItems = 0, buildProbeItems = 0;
@@ -76,9 +81,13 @@ class HashJoin {
   const JoinResult &lastResult() const { return result; }
   const core::JoinPlan &getPlan() const { return plan; }
   const core::JoinConfig &getConfig() const { return config; }
-  // Materialized (rid_inner, rid_outer) pairs of the last run, in ctx memory
-  // (valid until the next run on this context).
+  core::ExecContext *context() const { return ctx; }
+  // Materialized (rid_inner, rid_outer) pairs of the last run(), in the engine's workspace: valid
+  // until the workspace is rewound or freed (the next join on the context,
+  // a new HashJoin planned on it, trim_workspace).  outputValid() says whether
+  // it still is.
   const ulonglong2 *getOutput() const { return output; }
+  bool outputValid() const;
   // Fused materialization: while a sink is set, a device join at N = 1 over
   // the split layout writes whole output rows (LateMaterialization's layout)
   // from its materialize pass instead of pairs.  canFuseRows() says whether
@@ -138,6 +147,7 @@ class HashJoin {
   core::JoinPlan basePlan;         // two-level plan (what a bitmap plan falls back to)
   bool bitmapExact = false;        // bitmap plan: exact histograms (small inputs, or after an overflow)
   const ulonglong2 *output = nullptr;
+  uint64_t outputEpoch = 0;  // workspace epoch when `output` was written
   kernels::RowSink sink;
   bool hasSink = false;
   uint64_t ridLo[2] = {~0ull, ~0ull}, ridHi[2] = {0, 0};

@@ -325,6 +325,13 @@ bool BitmapPlan::run(uint64_t t0, JoinResult &r) {
   r.networkMs = r.joinMs;
   r.devNetworkMs = o.devSampleMs + o.devScatterMs;
   r.devBuildProbeMs = o.devJoinMs;
+  r.enqueueMs = o.enqueueUs > t0 ? (o.enqueueUs - t0) / 1000.0 : 0.0;
+  r.hostWaitMs = o.hostWaitMs;
+  if (ctx->onDevice()) {
+    float ms = 0;
+    HIP_CHECK(hipEventElapsedTime(&ms, env.ev[0], env.ev[4]));
+    r.devSpanMs = ms;
+  }
   Measurements::storeNetworkDetails(env.inner->getLocalSize(), env.outer->getLocalSize(), 1);
   Measurements::storeBuildProbeDetails(r.innerReceived, r.outerReceived, r.buildProbeItems);
   Measurements::storeResultTuples(r.localMatches);

@@ -8,6 +8,7 @@
 
 #include "../comm/Communicator.h"
 #include "../memory/Arena.h"
+#include "../performance/Clock.h"
 #include "../performance/Measurements.h"
 #include "../performance/Timeline.h"
 #include "../performance/Trace.h"
@@ -79,7 +80,10 @@ void BitmapJoin::layoutSides(Side *sides, uint32_t count, bool exact, bool narro
   memory::Arena &ws = ctx->workspace();
   const hipStream_t st = ctx->stream();
   const kernels::KeyMix mix{plan.keyMix ? 1u : 0u, plan.keyBits};
-  uint64_t *totals = ws.getArray<uint64_t>((uint64_t)count * G * F);  // adjacent: one clear
+  // Adjacent: one clear -- or none, in the engine's control block (N = 1),
+  // which the layout kernel returns to zero after reading.
+  uint64_t *totals = useControl ? reinterpret_cast<uint64_t *>(ctx->control()->totals)
+                                : ws.getArray<uint64_t>((uint64_t)count * G * F);
   kernels::SampledInput in[2];
   kernels::LayoutInput lay[2];
   bool sampled = !exact;
@@ -98,9 +102,10 @@ void BitmapJoin::layoutSides(Side *sides, uint32_t count, bool exact, bool narro
     narrow = narrow && kernels::cursorsNarrow(s.cap + n);
     lay[i].sampled = in[i].totals;
     lay[i].sc = sc;
+    lay[i].clearSampled = useControl;
   }
   if (sampled) {
-    kernels::netSampledTotals(in, count, bits, st, mix);
+    kernels::netSampledTotals(in, count, bits, st, mix, useControl);
   } else {  // exact histograms (or an input too small to sample): every tile, per block
     for (uint32_t i = 0; i < count; ++i) {
       uint32_t *blockHist = ws.getArray<uint32_t>((uint64_t)F * in[i].geom.blocks);
@@ -156,8 +161,18 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
   const uint32_t F = 1u << plan.networkBits, N = ctx->numberOfNodes(), bits = plan.bitmapBits;
   const hipStream_t st = ctx->stream();
   memory::Arena &ws = ctx->workspace();
-  BitmapCounters *cnt = ws.getArray<BitmapCounters>(1);
-  HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(BitmapCounters), st));
+  // One rank: counters and sampled totals in the engine's control block
+  // (no memset) and the result delivered through the host-mapped mailbox (no
+  // copy): the join is its kernels plus one spin on a host word.
+  useControl = N == 1 && ctx->control() != nullptr;
+  BitmapCounters *cnt;
+  if (useControl) {
+    ctx->beginControl();
+    cnt = &ctx->control()->counters;
+  } else {
+    cnt = ws.getArray<BitmapCounters>(1);
+    HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(BitmapCounters), st));
+  }
   Outcome o;
   // One cursor width for both sides (the fused N = 1 kernel reads both with
   // one slice type; e.g. 1B inner x 4B outer needs 8-byte cursors on both).
@@ -195,7 +210,12 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
     tl.beginAt("BPTASKTIME", ev[2]);
     tl.beginSplitAt("BPKERNEL", "BPBUILD", (double)inner->getLocalSize(), "BPPROBE", (double)outer->getLocalSize(),
                     ev[2]);
-    kernels::bitmapJoin(4, ri.frags, ro.frags, ri.slices, ro.slices, F, 0, bits, cnt, st);
+    kernels::MailboxArgs mb;
+    mb.box = ctx->mailboxDevice();
+    mb.arrivals = &ctx->control()->arrivals;
+    mb.seq = ctx->nextMailboxSeq();
+    mailboxSeq = mb.seq;
+    kernels::bitmapJoin(4, ri.frags, ro.frags, ri.slices, ro.slices, F, 0, bits, cnt, st, mb);
     HIP_CHECK(hipEventRecord(ev[4], st));
     tl.endAt("BPKERNEL", ev[4]);
     tl.endAt("BPTASKTIME", ev[4]);
@@ -262,13 +282,32 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
   // back[0]: this rank's counters; back[1] (N > 1): all ranks' sums, combined
   // on the device behind the probe (one synchronisation per join).
   BitmapCounters *back = ctx->staging().getArray<BitmapCounters>(2);
-  HIP_CHECK(hipMemcpyAsync(back, cnt, sizeof(BitmapCounters), hipMemcpyDeviceToHost, st));
-  if (N > 1) {
-    static_assert(sizeof(BitmapCounters) == 4 * sizeof(uint64_t), "BitmapCounters: four u64 sums");
-    ctx->comm()->allReduceSumDevice(reinterpret_cast<uint64_t *>(cnt), 4, st);
-    HIP_CHECK(hipMemcpyAsync(back + 1, cnt, sizeof(BitmapCounters), hipMemcpyDeviceToHost, st));
+  const uint64_t tEnqueued = performance::nowUs();
+  if (useControl) {
+    // The kernel's last wave published the counters: spin on the mailbox,
+    // then the streams (their last kernel ends microseconds later).
+    const bool arrived = ctx->waitMailbox(mailboxSeq);
+    // Polls the end event's signal (no blocking wait on an interrupt).
+    if (arrived) utils::waitEvent(ev[4], nullptr, "bitmap join");
+    o.hostWaitMs = (performance::nowUs() - tEnqueued) / 1000.0;
+    ctx->synchronize();
+    JOIN_ASSERT(arrived || ctx->mailbox().seq >= mailboxSeq, "BitmapJoin",
+                "the join's final kernel completed without publishing its result (mailbox seq %llu < %llu)",
+                (unsigned long long)ctx->mailbox().seq, (unsigned long long)mailboxSeq);
+    const kernels::ResultMailbox &m = ctx->mailbox();
+    back[0] = BitmapCounters{m.matches, m.popcount, m.dup, m.overflow};
+    ctx->endControl();
+  } else {
+    HIP_CHECK(hipMemcpyAsync(back, cnt, sizeof(BitmapCounters), hipMemcpyDeviceToHost, st));
+    if (N > 1) {
+      static_assert(sizeof(BitmapCounters) == 4 * sizeof(uint64_t), "BitmapCounters: four u64 sums");
+      ctx->comm()->allReduceSumDevice(reinterpret_cast<uint64_t *>(cnt), 4, st);
+      HIP_CHECK(hipMemcpyAsync(back + 1, cnt, sizeof(BitmapCounters), hipMemcpyDeviceToHost, st));
+    }
+    ctx->synchronize();
+    o.hostWaitMs = (performance::nowUs() - tEnqueued) / 1000.0;
   }
-  ctx->synchronize();
+  o.enqueueUs = tEnqueued;
   float ms = 0;
   HIP_CHECK(hipEventElapsedTime(&ms, ev[0], ev[1]));
   o.devSampleMs = ms;

@@ -54,6 +54,8 @@ class BitmapJoin {
     bool overflow = false;     // some rank's sampled slice overflowed
     uint64_t linkBytes = 0;    // this rank's share of the all-reduce traffic (ring estimate)
     double devSampleMs = 0, devScatterMs = 0, devJoinMs = 0;  // hipEvents (device engine)
+    uint64_t enqueueUs = 0;    // host clock when the last kernel of the join was enqueued
+    double hostWaitMs = 0;     // host wait from there to the result (mailbox spin + stream sync)
   };
 
   // ev: 5 timing events of the caller (ev[0] already recorded at join start).
@@ -91,6 +93,8 @@ class BitmapJoin {
   const core::JoinPlan &plan;
   uint32_t maxBlocks, sampleStride;
   hipEvent_t *ev;
+  bool useControl = false;   // N = 1 device engine: control-block scratch + mailbox result
+  uint64_t mailboxSeq = 0;
 };
 
 }  // namespace tasks

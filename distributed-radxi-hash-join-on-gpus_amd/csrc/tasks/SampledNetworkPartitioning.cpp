@@ -8,6 +8,7 @@
 
 #include "../memory/Arena.h"
 #include "../performance/Timeline.h"
+#include "../utils/Fault.h"
 #include "../utils/Hip.h"
 
 namespace hpcjoin {
@@ -171,7 +172,7 @@ void SampledNetworkPartitioning::scatterSide(int k) {
 bool SampledNetworkPartitioning::finishSide(int k) {
   const uint32_t F = 1u << plan.networkBits, G = CLAIM_GROUPS;
   Side &s = sides[k];
-  HIP_CHECK(hipEventSynchronize(s.cursorsReady));
+  utils::waitEvent(s.cursorsReady, ctx->comm(), "sampled network cursors");  // polls: no interrupt wake-up
   const size_t m = (size_t)G * F;
   s.start.resize(m);
   s.fill.assign(m, 0);

@@ -251,7 +251,13 @@ bool SampledShuffle::exchangeSide(int k) {
   const char *kFlush = k == 0 ? "MIFLUSHPART" : "MOFLUSHPART";
   ctx->timeline().begin(kFlush, ctx->stream());
   utils::waitEvent(s.scattered[C - 1], ctx->comm(), "sampled network scatter");  // one stream: all chunks done
+  // Checks raise flags that travel in the fill all-gather instead of throwing
+  // here: a rank that threw before the collective would leave its peers
+  // blocked in it.  A cell past u32 is an overflow (exact re-run);
+  // claims that do not add up to the chunk are an engine fault, raised on
+  // every rank after the gather.
   bool over = false;
+  uint64_t brokenChunk = 0;  // 1 + the first chunk whose claims do not add up
   {
     const uint32_t *c32 = static_cast<const uint32_t *>(s.cursorsBack);
     const uint64_t *c64 = static_cast<const uint64_t *>(s.cursorsBack);
@@ -262,22 +268,24 @@ bool SampledShuffle::exchangeSide(int k) {
       for (size_t i = 0; i < GF; ++i) {
         const size_t at = (size_t)c * GF + i;
         const uint64_t fill = (s.narrow ? c32[at] : c64[at]) - s.start[at];
-        over = over || fill > s.cap[at];
-        HJ_CHECK(fill <= 0xffffffffull, "sampled network pass: cell %zu holds %lu tuples (the fill all-gather packs u32)",
-                 at, (unsigned long)fill);
+        over = over || fill > s.cap[at] || fill > 0xffffffffull;  // the fill all-gather packs u32
         sum += fill;
         mine[at / 2] |= std::min<uint64_t>(fill, 0xffffffffull) << (32 * (at & 1));
       }
       const uint64_t b = std::min<uint64_t>(n, (uint64_t)c * bpc * span);
       const uint64_t e = std::min<uint64_t>(n, (uint64_t)std::min<uint32_t>(blocks, (c + 1) * bpc) * span);
-      HJ_CHECK(sum == e - b, "sampled network pass: chunk %u claimed %lu of %lu tuples", c, (unsigned long)sum,
-               (unsigned long)(e - b));
+      if (sum != e - b && !brokenChunk) brokenChunk = 1 + c;
     }
   }
-  mine[W - 1] = over ? 1 : 0;
+  mine[W - 1] = (over ? 1 : 0) | (brokenChunk << 1);
   ctx->comm()->allGatherHost(mine.data(), all.data(), W);
   bool anyOver = false;
-  for (uint32_t r = 0; r < N; ++r) anyOver = anyOver || all[(size_t)r * W + W - 1] != 0;
+  for (uint32_t r = 0; r < N; ++r) {
+    const uint64_t flags = all[(size_t)r * W + W - 1];
+    HJ_CHECK((flags >> 1) == 0, "sampled network pass: rank %u's chunk %lu claims do not add up to its tuples", r,
+             (unsigned long)((flags >> 1) - 1));
+    anyOver = anyOver || (flags & 1) != 0;
+  }
   // Receive totals of every rank vs its window capacity (same verdict everywhere).
   for (uint32_t r = 0; r < N && !anyOver; ++r) {
     uint64_t got = 0;

@@ -34,12 +34,15 @@ void armFault(const std::string &phase, int rank) {
   t_armed = !phase.empty();
 }
 
-void faultPoint(const char *phase) {
+bool faultHit(const char *phase) {
   const bool hit = (t_armed && t_phase == phase && (t_rank < 0 || t_rank == debugRank())) || envFault(phase);
-  if (hit) {
-    t_armed = false;  // one shot
+  if (hit) t_armed = false;  // one shot
+  return hit;
+}
+
+void faultPoint(const char *phase) {
+  if (faultHit(phase))
     throw InjectedFault(format("[FAULT][rank %d] injected fault at phase '%s'", debugRank(), phase));
-  }
 }
 
 uint64_t commTimeoutMs() {
@@ -68,9 +71,11 @@ static void waitUntil(Query query, comm::Communicator *comm, const char *what) {
       if (comm) comm->abort(why);
       fail("WATCHDOG", __FILE__, __LINE__, why);
     }
-    // Short spin first (most waits end within microseconds of the last
-    // kernel), then back off so a stuck collective does not burn a core.
-    if (spin < 2000) std::this_thread::yield();
+    // Yield-spin for the first 100 ms (a join's waits end within
+    // microseconds of its last kernel; a sleep would add its granularity to
+    // every join), then back off so a stuck collective does not burn a core.
+    (void)spin;
+    if (now - t0 < std::chrono::milliseconds(100)) std::this_thread::yield();
     else std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
 }

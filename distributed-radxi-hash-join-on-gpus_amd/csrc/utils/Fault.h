@@ -31,6 +31,9 @@ struct InjectedFault : std::runtime_error {
 // Arm a fault for the calling thread (rank < 0: any rank). Empty phase disarms.
 void armFault(const std::string &phase, int rank = -1);
 void faultPoint(const char *phase);
+// Non-throwing variant: true (once) when a fault is armed for this phase --
+// the caller injects it (e.g. "corrupt_window": flip a word of a window).
+bool faultHit(const char *phase);
 
 uint64_t commTimeoutMs();
 void setCommTimeoutMs(uint64_t ms);  // process-wide override (tests)

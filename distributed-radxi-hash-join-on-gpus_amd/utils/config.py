@@ -35,7 +35,7 @@ def config_from_dict(d: dict | None = None, env_prefix: str = "HPCJOIN_"):
     cfg = C.JoinConfig()
     merged = dict(d or {})
     for f in _FIELDS + ["assignment", "format", "key_hashing", "network_histogram", "local_histogram", "wire_codec",
-                        "replicate_bitmap", "exchange"]:
+                        "replicate_bitmap", "exchange", "verify_exchange"]:
         v = os.environ.get(env_prefix + f.upper())
         if v is not None:
             merged[f] = v
@@ -52,8 +52,8 @@ def config_from_dict(d: dict | None = None, env_prefix: str = "HPCJOIN_"):
             setattr(cfg, k, v if isinstance(v, bool) else str(v).lower() in ("1", "true", "yes"))
         elif k == "wire_codec":
             cfg.wire_codec = getattr(C.WireCodecMode, str(v).upper())
-        elif k == "replicate_bitmap":
-            cfg.replicate_bitmap = getattr(C.PlanChoice, str(v).upper())
+        elif k in ("replicate_bitmap", "verify_exchange"):
+            setattr(cfg, k, getattr(C.PlanChoice, str(v).upper()))
         elif k == "exchange":
             cfg.exchange = getattr(C.ExchangeMode, str(v).upper())
         elif k in _FIELDS:

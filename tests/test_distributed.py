@@ -411,6 +411,7 @@ def test_tpch_late_materialization(C, dev, n_ranks):
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(420)  # above the per-rank deadline below, so a hang reports every rank's last output
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_rccl_multiprocess_shared_gpu(world):
     """One process per rank over the real RCCL library, as torchrun launches
@@ -429,7 +430,7 @@ def test_rccl_multiprocess_shared_gpu(world):
     # 10-40 s for all cases.  On a timeout the ranks' last output says which
     # case they were in.
     outs = [None] * world
-    deadline = time.time() + 150
+    deadline = time.time() + 300
     try:
         for i, p in enumerate(procs):
             outs[i] = p.communicate(timeout=max(1.0, deadline - time.time()))[0]
@@ -439,7 +440,7 @@ def test_rccl_multiprocess_shared_gpu(world):
                 p.kill()
         tails = [f"rank {i}: " + ((outs[i] if outs[i] is not None else p.communicate()[0]) or "")[-1500:]
                  for i, p in enumerate(procs)]
-        pytest.fail("rccl_worker timed out after 150 s; last output per rank:\n" + "\n".join(tails))
+        pytest.fail("rccl_worker timed out after 300 s; last output per rank:\n" + "\n".join(tails))
     finally:
         for p in procs:
             if p.poll() is None:
@@ -576,3 +577,79 @@ def test_one_sided_in_process_distinct_devices(C):
     exp = C.Relation.expected_matches(inner, G_R, outer, G_S)
     for res, plan in out:
         assert plan.one_sided and res["global_matches"] == exp
+
+
+@pytest.mark.parametrize("dev", devices())
+@pytest.mark.parametrize("n_ranks,chunks,opts", [(2, 1, "one-sided"), (4, 2, "rccl"), (3, 3, "wide"),
+                                                  (4, 2, "mat-one-sided"), (4, 2, "hot-split"), (2, 2, "key-only")])
+def test_exchange_verification(C, dev, n_ranks, chunks, opts):
+    """verify_exchange: every (source, chunk, partition) run is hashed on the
+    sender (from its input) and on the receiver (from its window); runs of a
+    split hot partition's replicated side count once per receiving helper.
+    Clean exchanges verify on every path (two-sided, one-sided, wide tuples,
+    materializing, hot-partition split, key-only words)."""
+    hot = opts == "hot-split"
+    sparse = opts == "key-only"
+    inner = C.GenSpec(seed=1234)
+    outer = (C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=77, domain=5, zipf_theta=0.99) if hot
+             else C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=4321, domain=200_003, zipf_theta=0.8))
+    if sparse:
+        inner.sparse64 = True
+        outer = C.GenSpec(seed=99)
+        outer.sparse64 = True
+
+    def cfg_fn(c):
+        c.verify_exchange = C.PlanChoice.ON
+        c.bitmap_join = False
+        c.chunks = chunks
+        c.materialize = opts.startswith("mat")
+        if "one-sided" in opts:
+            c.exchange = C.ExchangeMode.ONE_SIDED
+        if opts == "wide":
+            c.format = C.TupleFormat.WIDE
+        if hot:
+            c.key_hashing = C.KeyHashing.OFF
+    results, exp = run_ranks(C, n_ranks, "device" if dev == "cuda" else "host", 200_003, 300_007, cfg_fn=cfg_fn,
+                             inner=inner, outer=outer)
+    for res, plan in results:
+        assert res["global_matches"] == exp
+        assert res["exchange_checked"] > 0
+        if sparse:
+            assert plan.key_only
+
+
+@pytest.mark.parametrize("dev", devices())
+@pytest.mark.parametrize("mode", ["ONE_SIDED", "RCCL"])
+def test_exchange_verification_catches_corruption(C, dev, mode):
+    """A word of one rank's window flipped after it arrived (fault injection
+    "corrupt_window") makes the join fail on EVERY rank with the exchange
+    verification's message -- instead of returning a wrong count."""
+    n_ranks = 3
+    group = C.InProcessGroup(n_ranks)
+    loc = "device" if dev == "cuda" else "host"
+    errors = [None] * n_ranks
+
+    def rank_main(r):
+        try:
+            ctx = C.ExecContext(loc, 0 if loc == "device" else -1, group.communicator(r))
+            G = 100_003
+            R = C.Relation(C.Relation.local_size_for(G, r, n_ranks), G, loc, 0)
+            S = C.Relation(C.Relation.local_size_for(G, r, n_ranks), G, loc, 0)
+            R.generate(C.GenSpec(seed=1234), C.Relation.local_offset_for(G, r, n_ranks))
+            S.generate(C.GenSpec(seed=4321), C.Relation.local_offset_for(G, r, n_ranks))
+            cfg = C.JoinConfig()
+            cfg.verify_exchange = C.PlanChoice.ON
+            cfg.bitmap_join = False
+            cfg.exchange = getattr(C.ExchangeMode, mode)
+            j = C.HashJoin(R, S, ctx, cfg)
+            assert j.run()["global_matches"] == G  # clean first
+            if r == 1:
+                C.fault.arm("corrupt_window", r)
+            j.run()
+        except Exception as e:  # noqa: BLE001
+            errors[r] = str(e)
+
+    ts = [threading.Thread(target=rank_main, args=(r,)) for r in range(n_ranks)]
+    [t.start() for t in ts]
+    [t.join(timeout=300) for t in ts]
+    assert all(e is not None and "exchange verification" in e and "did not arrive intact" in e for e in errors), errors

@@ -79,6 +79,30 @@ def test_join_wide_and_materialize(C, dev):
 
 
 @pytest.mark.parametrize("dev", devices())
+def test_output_invalid_after_workspace_reuse(C, dev):
+    """output() reads the pairs from the engine's workspace: once a later join
+    on the same context has rewound it, the call raises instead of returning
+    (or, on a freed device buffer, crashing on) whatever the memory holds now."""
+    loc = "device" if dev == "cuda" else "host"
+    ctx = C.ExecContext(loc, 0 if loc == "device" else -1, C.LocalCommunicator())
+    G = 50_000
+    R = C.Relation(G, G, loc, 0)
+    S = C.Relation(G, G, loc, 0)
+    R.generate(C.GenSpec(seed=1234), 0)
+    S.generate(C.GenSpec(seed=4321), 0)
+    cfg = C.JoinConfig()
+    cfg.materialize = True
+    j = C.HashJoin(R, S, ctx, cfg)
+    assert j.run()["output_pairs"] == G
+    assert j.output().shape == (G, 2)
+    j.run()
+    assert j.output().shape == (G, 2)  # still the last run of this join
+    ctx.reset_scratch()  # what the next join on the context does first
+    with pytest.raises(RuntimeError, match="reused"):
+        j.output()
+
+
+@pytest.mark.parametrize("dev", devices())
 def test_join_repeatable(C, dev):
     res, exp, j = run_join(C, dev, 200_000, 200_000)
     for _ in range(3):

@@ -15,6 +15,8 @@
 #   ppmc=CTRS/SCRIPT,ARGS  rocprofv3 --pmc CTRS of python SCRIPT ARGS
 #   pmc=CTRS/ARGS       rocprofv3 --pmc CTRS (comma-separated) of bench.py ARGS
 #   ebench=ENV/ARGS     bench.py ARGS with ENV (comma-separated K=V, e.g. HPCJOIN_NET_THREADS=512): A/B runs
+#   abbench=ARGS        same-box A/B: bench.py ARGS of ab/base (a built copy of an older tree) and of this
+#                       tree, alternating base/new twice
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
 TAG=$1
@@ -39,6 +41,12 @@ for step in "$@"; do
     ebench) envs=${arg%%/*}; bargs=${arg#*/}
             timeout -k 10 600 env ${envs//,/ } python -u bench.py ${bargs//,/ } > "$log" 2>&1 ;;
     skew) timeout -k 10 900 python -u tools/bench_skew.py $args > "$log" 2>&1 ;;
+    abbench) rc=0
+             for i in 1 2; do
+               (cd "$R/ab/base" && timeout -k 10 300 python -u bench.py $args > "$OUT/$n.base$i.log" 2>&1) || { rc=$?; break; }
+               timeout -k 10 300 python -u bench.py $args > "$OUT/$n.new$i.log" 2>&1 || { rc=$?; break; }
+             done
+             echo "abbench rc=$rc" > "$log"; (exit $rc) ;;
     py) timeout -k 10 900 python -u $args > "$log" 2>&1 ;;
     stats) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/stats$n" -o run --output-format csv \
               -- python "$R/bench.py" $args) > "$log" 2>&1 ;;
