@@ -540,6 +540,8 @@ py::dict resultToDict(const operators::JoinResult &r) {
   d["host_wait_ms"] = r.hostWaitMs;
   d["dev_span_ms"] = r.devSpanMs;
   d["exchange_checked"] = r.exchangeChecked;
+  d["passes"] = r.passes;
+  d["compact_ms"] = r.compactMs;
   d["inner_received"] = r.innerReceived;
   d["wire_bytes"] = r.wireBytes;
   d["outer_received"] = r.outerReceived;
@@ -645,6 +647,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("bitmap_join", &core::JoinConfig::bitmapJoin)
       .def_readwrite("replicate_bitmap", &core::JoinConfig::replicateBitmap)
       .def_readwrite("verify_exchange", &core::JoinConfig::verifyExchange)
+      .def_readwrite("passes", &core::JoinConfig::passes)
       .def_readwrite("exchange", &core::JoinConfig::exchange)
       .def_readwrite("split_histogram", &core::JoinConfig::splitHistogram)
       .def_readwrite("pipeline_outer", &core::JoinConfig::pipelineOuter)
@@ -981,6 +984,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("plan", &operators::HashJoin::getPlan)
       .def("workspace_estimate", &operators::HashJoin::workspaceEstimate)
       .def_property_readonly("reserved_bytes", &operators::HashJoin::reservedBytes)
+      .def_property_readonly("spill_passes", &operators::HashJoin::spillPasses)
+      .def_property_readonly("spill_info", [](const operators::HashJoin &j) {
+        py::dict d;
+        d["passes"] = j.spillPasses();
+        d["estimate_bytes"] = j.spill.estimate;
+        d["available_bytes"] = j.spill.available;
+        d["pass_buffer_bytes"] = j.spill.passBuffers;
+        d["pass_estimate_bytes"] = j.spill.passEstimate;
+        d["pass_workspace_bytes"] = j.spill.passReserved;
+        return d;
+      })
       .def_property_readonly("plan_ms", &operators::HashJoin::planMilliseconds)
       .def_property_readonly("reserve_ms", &operators::HashJoin::reserveMilliseconds)
       .def(

@@ -62,12 +62,17 @@ void RcclCommunicator::abort(const std::string &why) {
 RcclCommunicator::~RcclCommunicator() {
   if (comm_) ncclCommDestroy(static_cast<ncclComm_t>(comm_));
   if (scratch_) (void)hipFree(scratch_);
+  for (uint64_t *p : retired_) (void)hipFree(p);
   if (stream_) (void)hipStreamDestroy(stream_);
 }
 
 uint64_t *RcclCommunicator::scratch(size_t words) {
   if (words > scratchWords_) {
-    if (scratch_) HIP_CHECK(hipFree(scratch_));
+    // The outgrown buffer is kept until the communicator goes: hipFree
+    // synchronises the whole device, and between ranks that would wait on
+    // this process's in-flight collectives (e.g. an exchange still on the
+    // links while a host collective grows the scratch).
+    if (scratch_) retired_.push_back(scratch_);
     scratchWords_ = words < 4096 ? 4096 : words;
     HIP_CHECK(hipMalloc(&scratch_, scratchWords_ * 8));
   }

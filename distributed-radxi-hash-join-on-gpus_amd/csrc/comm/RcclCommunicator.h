@@ -44,6 +44,7 @@ class RcclCommunicator : public Communicator {
   int device_;
   hipStream_t stream_ = nullptr;  // for the small blocking collectives
   uint64_t *scratch_ = nullptr;
+  std::vector<uint64_t *> retired_;  // outgrown scratch buffers (freed with the communicator)
   size_t scratchWords_ = 0;
   std::string abortReason_;
 };

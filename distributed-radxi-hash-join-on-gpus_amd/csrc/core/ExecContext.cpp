@@ -152,7 +152,40 @@ void ExecContext::copy(void *dst, const void *src, uint64_t bytes, bool toDevice
     std::memcpy(p, src, bytes);
     src = p;
   }
+  // Uploads out of the staging arena are read by one of the engine's own
+  // kernels over the host link (no copy engine: bench_skew's first join paid
+  // ~5-10 ms in its local pass for the first SDMA upload of a process).
+  if (toDevice && !fromDevice && staging_->owns(src)) {
+    kernels::copyFromHost(dst, src, bytes, stream_);
+    return;
+  }
   HIP_CHECK(hipMemcpyAsync(dst, src, bytes, k, stream_));
+}
+
+void ExecContext::readBack(void *dst, const void *src, uint64_t bytes, hipStream_t s) const {
+  if (bytes == 0) return;
+  if (!onDevice()) {
+    std::memcpy(dst, src, bytes);
+    return;
+  }
+  if (!s) s = stream_;
+  if (staging_->owns(dst))
+    kernels::copyToHost(dst, src, bytes, s);
+  else
+    HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+}
+
+void ExecContext::zero(void *dev, uint64_t bytes, hipStream_t s) const {
+  if (bytes == 0) return;
+  if (!onDevice()) {
+    std::memset(dev, 0, bytes);
+    return;
+  }
+  if (!s) s = stream_;
+  if (((reinterpret_cast<uintptr_t>(dev) | bytes) & 7) == 0)
+    kernels::zeroWords(dev, bytes / 8, s);
+  else
+    HIP_CHECK(hipMemsetAsync(dev, 0, bytes, s));
 }
 
 void ExecContext::resetScratch() {

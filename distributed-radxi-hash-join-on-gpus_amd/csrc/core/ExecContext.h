@@ -51,6 +51,14 @@ class ExecContext {
 
   void synchronize() const;                 // compute + comm streams
   void copy(void *dst, const void *src, uint64_t bytes, bool toDevice, bool fromDevice) const;  // async on stream()
+  // Device -> host read-back on stream s (default: stream()).  Into the
+  // pinned staging arena it is one of the engine's own kernels writing the
+  // mapped host memory (no copy engine, no runtime blit kernel); elsewhere a
+  // runtime copy.  The host reads dst after an event recorded behind it.
+  void readBack(void *dst, const void *src, uint64_t bytes, hipStream_t s = nullptr) const;
+  // Zero device memory on stream s (default: stream()) with the engine's own
+  // kernel when 8-byte aligned, else a runtime fill.
+  void zero(void *dev, uint64_t bytes, hipStream_t s = nullptr) const;
   void resetScratch();
   // Synchronisation event (timing disabled) from a per-context pool, valid
   // until the next resetScratch(): joins reuse the same events instead of

@@ -112,6 +112,11 @@ struct JoinConfig {
   // windows per join.  Auto: on for one-sided windows (IPC puts, where a lost
   // or misdirected put would otherwise be silent), off for RCCL all-to-allv.
   PlanChoice verifyExchange = PlanChoice::Auto;
+  // Capacity spill (kernels/spill.hip): run the join in this many passes,
+  // each over the tuples whose key hashes to it (counting joins).  0 = auto:
+  // on a device engine, as many as it takes for one pass's buffers and
+  // workspace to fit what HBM has free (capped by workspaceBudget).
+  uint32_t passes = 0;
   uint32_t localItemTiles = 64; // local pass work item: up to this many 4096-tuple tiles of one segment
   uint32_t localGeometry = 0;   // local scatter workgroup geometry (0 = 1024 x 8; 1-4: sweep alternatives)
   KernelVariants variants;      // kernel-shape variants (sweeps; core/Types.h)

@@ -120,6 +120,16 @@ void Relation::generate(const GenSpec &spec, uint64_t globalOffset) {
   }
 }
 
+void Relation::inheritBounds(const Relation &parent, uint64_t maxKey, uint64_t ridMax) {
+  keyBoundKnown_ = true;
+  maxKey_ = maxKey;
+  ridsPositional_ = false;
+  ridBoundKnown_ = true;
+  ridMax_ = ridMax;
+  lowBitsUniform_ = parent.lowBitsUniform_;
+  keyRepeats_ = parent.keyRepeats_;
+}
+
 void Relation::setGenerated(uint64_t ridBase, bool lowBitsUniform) {
   keyBoundKnown_ = true;
   ridsPositional_ = true;

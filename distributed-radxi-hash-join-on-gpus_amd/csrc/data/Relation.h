@@ -82,6 +82,13 @@ class Relation {
   // planner decides bitmap vs two-level and the key-only table kind from it
   // before the first join (HashJoin::makeJoinPlan samples when 0).
   int keyRepeats() const { return keyRepeats_; }
+  // A pass view of a subset of `parent`'s tuples (capacity spill,
+  // operators/HashJoin::runPasses): the parent's key bound (maxKey), its
+  // repeated-key knowledge and low-bit uniformity carry over; rids are
+  // bounded by ridMax but no longer positional.
+  void inheritBounds(const Relation &parent, uint64_t maxKey, uint64_t ridMax);
+  bool ridBoundKnown() const { return ridBoundKnown_; }
+  uint64_t ridMax() const { return ridMax_; }
 
  protected:
   void randomOrder();
@@ -104,6 +111,8 @@ class Relation {
   uint64_t ridBase_ = 0;
   bool lowBitsUniform_ = false;
   int keyRepeats_ = 0;
+  bool ridBoundKnown_ = false;
+  uint64_t ridMax_ = 0;
 };
 
 }  // namespace data

@@ -507,8 +507,32 @@ void exchangeChecksumRecv(const void *window, const ChecksumFormat &fmt, const C
                           unsigned long long *sums, hipStream_t s);
 void flipWindowWord(void *window, uint64_t word, hipStream_t s);
 
+// ------------------------------------------------------- capacity spill
+// Pass of a key when a join runs in K passes (kernels/spill.hip): a hash of
+// the whole key, independent of the radix digits (its low bits), so every
+// pass spreads over all partitions.
+constexpr uint32_t MAX_SPILL_PASSES = 256;
+HJ_HD uint32_t passOf(uint64_t key, uint32_t K) {
+  uint64_t x = key ^ 0x5851F42D4C957F2Dull;
+  x ^= x >> 33;
+  x *= 0xFF51AFD7ED558CCDull;
+  x ^= x >> 33;
+  x *= 0xC4CEB9FE1A85EC53ull;
+  x ^= x >> 33;
+  return (uint32_t)(((x >> 32) * (uint64_t)K) >> 32);
+}
+// counts[p] += tuples of pass p (counts zeroed by the caller).
+void passCounts(const data::Tuple *in, uint64_t n, uint32_t K, unsigned long long *counts, hipStream_t s);
+// out = the tuples of pass k (any order); *cursor (zeroed by the caller) ends at their count.
+void passCompact(const data::Tuple *in, uint64_t n, uint32_t K, uint32_t k, data::Tuple *out,
+                 unsigned long long *cursor, hipStream_t s);
+
 // p[0, words) = 0 (u64 words) with the engine's own kernel.
 void zeroWords(void *p, uint64_t words, hipStream_t s);
+// dst (pinned, device-mapped host memory) = src (device), by the engine's own kernel.
+void copyToHost(void *dst, const void *src, uint64_t bytes, hipStream_t s);
+// dst (device) = src (pinned, device-mapped host memory): the same kernel the other way round.
+void copyFromHost(void *dst, const void *src, uint64_t bytes, hipStream_t s);
 struct BitmapSlices {
   enum Kind : int { Claim = 0, Table = 1 };
   int kind = Claim;

@@ -93,6 +93,38 @@ void zeroWords(void *p, uint64_t words, hipStream_t s) {
   HIP_CHECK_LAUNCH();
 }
 
+// dst (pinned, device-mapped host memory) = src, by the engine's own kernel:
+// a join's small read-backs need no copy engine (SDMA: the first copy of a
+// process stalled its join by ~12-17 ms, profiles/r1_sdma_outlier.md) and no
+// runtime blit kernel.  System-scope stores: visible to the host once the
+// kernel (and the event behind it) completes.
+template <typename W>
+__global__ __launch_bounds__(SCAN_T) void copyToHostKernel(W *dst, const W *__restrict__ src, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * SCAN_T + threadIdx.x; i < n; i += (uint64_t)gridDim.x * SCAN_T)
+    __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void copyFromHost(void *dst, const void *src, uint64_t bytes, hipStream_t s) { copyToHost(dst, src, bytes, s); }
+
+void copyToHost(void *dst, const void *src, uint64_t bytes, hipStream_t s) {
+  if (bytes == 0) return;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | bytes;
+  auto go = [&](auto w) {
+    using W = decltype(w);
+    const uint64_t n = bytes / sizeof(W);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(256, (n + SCAN_T - 1) / SCAN_T);
+    hipLaunchKernelGGL(copyToHostKernel<W>, dim3(grid), dim3(SCAN_T), 0, s, static_cast<W *>(dst),
+                       static_cast<const W *>(src), n);
+  };
+  if ((a & 7) == 0)
+    go((unsigned long long)0);
+  else if ((a & 3) == 0)
+    go(0u);
+  else
+    go((unsigned char)0);
+  HIP_CHECK_LAUNCH();
+}
+
 void preloadScan() {
   hipFuncAttributes a;
   HIP_CHECK(hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&scanSumsKernel<uint32_t>)));

@@ -51,6 +51,145 @@ HashJoin::HashJoin(data::Relation *innerRelation, data::Relation *outerRelation,
 HashJoin::~HashJoin() {
   for (auto &e : ev)
     if (e) (void)hipEventDestroy(e);
+  for (data::Tuple *&b : passBuf) {
+    memory::Arena::rawFree(ctx->location(), b);
+    b = nullptr;
+  }
+}
+
+// Capacity spill.  A join whose workspace estimate exceeds what HBM has free
+// (or config.workspaceBudget) runs in K passes over the key-hash classes
+// kernels::passOf: pass k holds ~1/K of both relations (compacted into pass
+// buffers) and needs ~1/K of the workspace.  K is the smallest count for
+// which one pass's buffers and workspace fit, agreed by all ranks (max).
+// The pass sizes are counted once here (one read of each relation), the
+// pass buffers allocated once for the largest pass.
+void HashJoin::planPasses() {
+  uint32_t K = config.passes;
+  const uint64_t n[2] = {innerRelation->getLocalSize(), outerRelation->getLocalSize()};
+  if (K == 0) {
+    K = 1;
+    if (ctx->onDevice() && config.reserveWorkspace && !plan.materialize) {
+      // One pass holds its pass buffers (~1/K of both relations) and its
+      // join's workspace (~1/K of the estimate, with a margin for the smaller
+      // joins' fixed parts and for pass-size spread).  workspaceBudget caps
+      // both together.
+      size_t freeB = 0, totalB = 0;
+      HIP_CHECK(hipMemGetInfo(&freeB, &totalB));
+      uint64_t avail = (uint64_t)(freeB * 0.85);
+      if (config.workspaceBudget) avail = std::min<uint64_t>(avail, config.workspaceBudget);
+      const uint64_t est = workspaceEstimate(), tuplesB = (n[0] + n[1]) * sizeof(data::Tuple);
+      spill.estimate = est;
+      spill.available = avail;
+      if (est > avail) {
+        K = 2;
+        while (K < kernels::MAX_SPILL_PASSES &&
+               (double)est / K * 1.3 + (double)tuplesB / K * 1.05 + (256u << 20) > (double)avail)
+          ++K;
+      }
+    }
+  }
+  K = std::max<uint32_t>(1, std::min<uint32_t>(K, kernels::MAX_SPILL_PASSES));
+  {  // every rank runs the same number of passes
+    std::vector<uint64_t> all(numberOfNodes);
+    const uint64_t mine = K;
+    ctx->comm()->allGatherHost(&mine, all.data(), 1);
+    for (uint64_t k : all) K = std::max<uint32_t>(K, (uint32_t)k);
+  }
+  passes = K;
+  if (K == 1) return;
+  JOIN_ASSERT(!plan.materialize, "HashJoin", "capacity spill (%u passes) runs counting joins only", K);
+  data::Relation *rel[2] = {innerRelation, outerRelation};
+  std::vector<uint64_t> counts(2 * (size_t)K, 0);
+  if (ctx->onDevice()) {
+    auto *d = ctx->workspace().getArray<unsigned long long>(2 * (size_t)K);
+    ctx->zero(d, 2 * (size_t)K * 8);
+    for (int r = 0; r < 2; ++r) kernels::passCounts(rel[r]->getData(), n[r], K, d + (size_t)r * K, ctx->stream());
+    HIP_CHECK(hipMemcpyAsync(counts.data(), d, 2 * (size_t)K * 8, hipMemcpyDeviceToHost, ctx->stream()));
+    utils::waitStream(ctx->stream(), ctx->comm(), "pass counts");
+    ctx->workspace().reset();
+  } else {
+    for (int r = 0; r < 2; ++r) {
+      const data::Tuple *t = rel[r]->getData();
+      for (uint64_t i = 0; i < n[r]; ++i) ++counts[(size_t)r * K + kernels::passOf(t[i].key, K)];
+    }
+  }
+  std::vector<uint64_t> global(counts);
+  ctx->comm()->allReduceSumHost(global.data(), global.size());
+  for (int r = 0; r < 2; ++r) {
+    passCount[r].assign(counts.begin() + (size_t)r * K, counts.begin() + (size_t)(r + 1) * K);
+    passGlobal[r].assign(global.begin() + (size_t)r * K, global.begin() + (size_t)(r + 1) * K);
+    const uint64_t cap = *std::max_element(passCount[r].begin(), passCount[r].end());
+    if (passBuf[r]) memory::Arena::rawFree(ctx->location(), passBuf[r]);
+    passBuf[r] = static_cast<data::Tuple *>(
+        memory::Arena::rawAlloc(ctx->location(), std::max<uint64_t>(cap, 1) * sizeof(data::Tuple), ctx->device()));
+    spill.passBuffers += std::max<uint64_t>(cap, 1) * sizeof(data::Tuple);
+  }
+  JOIN_DEBUG("HashJoin", "capacity spill: %u passes", K);
+}
+
+// One pass per key-hash class: compact both relations' tuples of the class
+// into the pass buffers, join them with a plan of their own (bounds
+// inherited, no re-scan), add the counts.
+JoinResult HashJoin::runPasses() {
+  performance::TraceRange traceJoin("hpcjoin::join_passes");
+  const uint64_t t0 = nowUs();
+  JoinResult total;
+  total.innerLocal = innerRelation->getLocalSize();
+  total.outerLocal = outerRelation->getLocalSize();
+  total.passes = passes;
+  data::Relation *rel[2] = {innerRelation, outerRelation};
+  core::JoinConfig sub = config;
+  sub.passes = 1;
+  sub.keyHashing = plan.keyMix ? core::KeyHashing::On : core::KeyHashing::Off;
+  for (uint32_t k = 0; k < passes; ++k) {
+    const uint64_t tc = nowUs();
+    if (ctx->onDevice()) {
+      ctx->resetScratch();
+      auto *cur = ctx->workspace().getArray<unsigned long long>(2);
+      ctx->zero(cur, 16);
+      for (int r = 0; r < 2; ++r)
+        kernels::passCompact(rel[r]->getData(), rel[r]->getLocalSize(), passes, k, passBuf[r], cur + r, ctx->stream());
+      utils::waitStream(ctx->stream(), ctx->comm(), "pass compaction");
+    } else {
+      for (int r = 0; r < 2; ++r) {
+        const data::Tuple *t = rel[r]->getData();
+        uint64_t at = 0;
+        for (uint64_t i = 0; i < rel[r]->getLocalSize(); ++i)
+          if (kernels::passOf(t[i].key, passes) == k) passBuf[r][at++] = t[i];
+      }
+    }
+    total.compactMs += (nowUs() - tc) / 1000.0;
+    data::Relation Rk(passBuf[0], passCount[0][k], passGlobal[0][k], ctx->location(), ctx->device());
+    data::Relation Sk(passBuf[1], passCount[1][k], passGlobal[1][k], ctx->location(), ctx->device());
+    Rk.inheritBounds(*innerRelation, planMaxKey, planMaxRid);
+    Sk.inheritBounds(*outerRelation, planMaxKey, planMaxRid);
+    HashJoin pass(&Rk, &Sk, ctx, sub);
+    spill.passEstimate = std::max<uint64_t>(spill.passEstimate, pass.workspaceEstimate());
+    spill.passReserved = std::max<uint64_t>(spill.passReserved, ctx->workspace().capacity());
+    const JoinResult r = pass.run();
+    total.localMatches += r.localMatches;
+    total.globalMatches += r.globalMatches;
+    total.innerReceived += r.innerReceived;
+    total.outerReceived += r.outerReceived;
+    total.wireBytes += r.wireBytes;
+    total.localItems += r.localItems;
+    total.buildProbeItems += r.buildProbeItems;
+    total.networkFallbacks += r.networkFallbacks;
+    total.localFallbacks += r.localFallbacks;
+    total.reruns += r.reruns;
+    total.devNetworkMs += r.devNetworkMs;
+    total.devLocalPartitionMs += r.devLocalPartitionMs;
+    total.devBuildProbeMs += r.devBuildProbeMs;
+    total.devSpanMs += r.devSpanMs;
+    total.bitmapJoin = r.bitmapJoin;
+    total.sampledNetwork = r.sampledNetwork;
+  }
+  total.joinMs = (nowUs() - t0) / 1000.0;
+  total.networkMs = total.joinMs;
+  result = total;
+  RESULT_COUNTER = result.localMatches;
+  return result;
 }
 
 void HashJoin::makeJoinPlan() {
@@ -86,6 +225,12 @@ void HashJoin::makeJoinPlan() {
         if (e > b) {
           h[1] = r->ridBase() + e - 1;
           h[2] = r->ridBase() + b;
+        }
+      } else if (r->keyBoundKnown() && r->ridBoundKnown()) {  // a pass view: the parent join's bounds
+        h[0] = r->maxKey();
+        if (e > b) {
+          h[1] = r->ridMax();
+          h[2] = 0;
         }
       } else if (ctx->onDevice() && e > b) {
         unsigned long long *d = ctx->workspace().getArray<unsigned long long>(3);
@@ -127,6 +272,8 @@ void HashJoin::makeJoinPlan() {
   }
   plan = core::makePlan(config, numberOfNodes, innerRelation->getGlobalSize(), outerRelation->getGlobalSize(), mx[0],
                         mx[1]);
+  planMaxKey = mx[0];
+  planMaxRid = mx[1];
   // Repeated inner keys are known before the first join (generator metadata
   // or the sample above): no bitmap plan to attempt and throw away, and
   // key-only words go on counted tables from the first join instead of
@@ -182,7 +329,8 @@ void HashJoin::makeJoinPlan() {
   if (ctx->onDevice())
     for (auto &e : ev)
       if (!e) HIP_CHECK(hipEventCreate(&e));
-  if (ctx->onDevice() && config.reserveWorkspace) {
+  planPasses();
+  if (ctx->onDevice() && config.reserveWorkspace && passes == 1) {
     // Capped by what HBM has free (the estimate is generous for N > 1, where
     // received sizes are only known after the histogram): a short estimate
     // only means the first join falls back to hipMalloc, as without it.
@@ -467,6 +615,7 @@ bool HashJoin::canFuseRows() const {
 
 JoinResult HashJoin::run() {
   try {
+    if (passes > 1) return runPasses();
     return runImpl();
   } catch (const std::exception &e) {
     while (!TASK_QUEUE.empty()) TASK_QUEUE.pop();  // tasks are owned (and freed) by runImpl

@@ -45,6 +45,8 @@ struct JoinResult {
   // joinMs - devSpanMs is what the host added around the device work.
   double enqueueMs = 0, hostWaitMs = 0, devSpanMs = 0;
   uint64_t exchangeChecked = 0;    // (source, chunk, partition) runs whose content was verified (verifyExchange)
+  uint32_t passes = 1;             // capacity spill: key-hash passes the join ran in (JoinConfig::passes)
+  double compactMs = 0;            // capacity spill: host wall of the per-pass compaction (in joinMs)
   uint64_t innerReceived = 0, outerReceived = 0;
   uint64_t wireBytes = 0;          // bytes this rank sent to peers (after the wire codec)
   uint64_t localItems = 0, buildProbeItems = 0;
@@ -115,6 +117,8 @@ class HashJoin {
 
  private:
   void makeJoinPlan();
+  void planPasses();
+  JoinResult runPasses();
   void planBitmap();
   void recordTimes(const JoinRun &run, uint64_t t4);
   bool lowKeyBitsSkewed();
@@ -125,6 +129,7 @@ class HashJoin {
   std::vector<uint64_t> workspaceParts() const;  // the estimate as one chunk per big buffer
   // Bytes the constructor added to the arena (0 if it already held the estimate).
   uint64_t reservedBytes() const { return reserved; }
+  uint32_t spillPasses() const { return passes; }
   // Construction cost: planning (key / rid bounds, repeated-key and low-bit
   // scans when the generator did not record them, the all-gather) and the
   // workspace reservation (allocation + first touch).  Host wall time, ms.
@@ -147,6 +152,22 @@ class HashJoin {
   core::JoinPlan basePlan;         // two-level plan (what a bitmap plan falls back to)
   bool bitmapExact = false;        // bitmap plan: exact histograms (small inputs, or after an overflow)
   const ulonglong2 *output = nullptr;
+  // Capacity spill (planPasses / runPasses): pass count, this rank's and the
+  // global tuple counts per pass, the pass buffers (one inner and one outer
+  // pass at a time) and the plan's global key / rid bounds.
+  uint32_t passes = 1;
+  std::vector<uint64_t> passCount[2], passGlobal[2];
+  data::Tuple *passBuf[2] = {nullptr, nullptr};
+  uint64_t planMaxKey = 0, planMaxRid = 0;
+ public:
+  // The capacity planner's inputs and outcome (bytes): single-pass workspace
+  // estimate, memory available to one pass (free HBM x 0.85, capped by
+  // workspaceBudget), the pass buffers, and the largest pass join's estimate
+  // and reservation (filled in by runPasses).
+  struct SpillInfo {
+    uint64_t estimate = 0, available = 0, passBuffers = 0, passEstimate = 0, passReserved = 0;
+  } spill;
+ private:
   uint64_t outputEpoch = 0;  // workspace epoch when `output` was written
   kernels::RowSink sink;
   bool hasSink = false;

@@ -171,7 +171,7 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
     cnt = &ctx->control()->counters;
   } else {
     cnt = ws.getArray<BitmapCounters>(1);
-    HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(BitmapCounters), st));
+    ctx->zero(cnt, sizeof(BitmapCounters));
   }
   Outcome o;
   // One cursor width for both sides (the fused N = 1 kernel reads both with
@@ -298,11 +298,11 @@ BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
     back[0] = BitmapCounters{m.matches, m.popcount, m.dup, m.overflow};
     ctx->endControl();
   } else {
-    HIP_CHECK(hipMemcpyAsync(back, cnt, sizeof(BitmapCounters), hipMemcpyDeviceToHost, st));
+    ctx->readBack(back, cnt, sizeof(BitmapCounters));
     if (N > 1) {
       static_assert(sizeof(BitmapCounters) == 4 * sizeof(uint64_t), "BitmapCounters: four u64 sums");
       ctx->comm()->allReduceSumDevice(reinterpret_cast<uint64_t *>(cnt), 4, st);
-      HIP_CHECK(hipMemcpyAsync(back + 1, cnt, sizeof(BitmapCounters), hipMemcpyDeviceToHost, st));
+      ctx->readBack(back + 1, cnt, sizeof(BitmapCounters));
     }
     ctx->synchronize();
     o.hostWaitMs = (performance::nowUs() - tEnqueued) / 1000.0;

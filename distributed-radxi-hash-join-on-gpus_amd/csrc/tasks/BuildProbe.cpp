@@ -133,7 +133,7 @@ void BuildProbe::execute() {
   tl.begin("BPTASKTIME", ctx->stream());
   const uint64_t tAlloc = performance::nowUs();
   counters = ws.getArray<unsigned long long>(4);
-  HIP_CHECK(hipMemsetAsync(counters, 0, 4 * sizeof(unsigned long long), ctx->stream()));
+  ctx->zero(counters, 4 * sizeof(unsigned long long));
   args.result = counters;
   args.outCursor = counters + 1;
   uint32_t *nItems = reinterpret_cast<uint32_t *>(counters + 2);
@@ -216,7 +216,7 @@ void BuildProbe::execute() {
   uint32_t *itemCounts = ws.getArray<uint32_t>(capacity);
   unsigned long long *itemOffsets = ws.getArray<unsigned long long>(capacity);
   void *scanWs64 = ws.get(kernels::scanWorkspaceBytes(capacity));
-  HIP_CHECK(hipMemsetAsync(itemCounts, 0, (size_t)capacity * sizeof(uint32_t), ctx->stream()));
+  ctx->zero(itemCounts, (size_t)capacity * sizeof(uint32_t));
   kernels::BPArgs countArgs = args;
   countArgs.materialize = false;
   countArgs.itemCounts = itemCounts;
@@ -236,8 +236,7 @@ void BuildProbe::execute() {
 // completes the read-back (no separate blocking copy afterwards).
 void BuildProbe::readBackCounters() {
   countersBack = ctx->staging().getArray<unsigned long long>(4);
-  HIP_CHECK(hipMemcpyAsync(countersBack, counters, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                           ctx->stream()));
+  ctx->readBack(countersBack, counters, 4 * sizeof(unsigned long long));
 }
 
 bool BuildProbe::collect() {

@@ -98,8 +98,7 @@ void HistogramComputation::launchOuter(hipStream_t exchangeStream) {
   ctx->timeline().begin("HOGLOBAL", exchangeStream);
   ctx->comm()->allGatherDevice(h->chunkTotalsDevice(), gatherDev, per, exchangeStream);
   ctx->timeline().end("HOGLOBAL", exchangeStream);
-  HIP_CHECK(hipMemcpyAsync(outerGatherHost, gatherDev, per * numberOfNodes * 8, hipMemcpyDeviceToHost,
-                           exchangeStream));
+  ctx->readBack(outerGatherHost, gatherDev, per * numberOfNodes * 8, exchangeStream);
   HIP_CHECK(hipEventRecord(outerGatherDone, exchangeStream));
   outerLaunched = true;
 }

@@ -131,7 +131,7 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
     ctx->copy(dLb, lb.data(), (owned + 1) * 4ull, true, false);
     if (!overflowFlag) {
       overflowFlag = ctx->workspace().getArray<unsigned int>(1);
-      HIP_CHECK(hipMemsetAsync(overflowFlag, 0, sizeof(unsigned int), ctx->stream()));
+      ctx->zero(overflowFlag, sizeof(unsigned int));
     }
     performance::Measurements::add("LPHISTELEM", (double)(xp.recvTotal / S), "tuples");
     // Back-to-back spans on one stream share their boundary events.
@@ -153,7 +153,7 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
     // Read back with the join's final synchronisation (the flag accumulates
     // over sides; the last copy enqueued sees them all).
     if (!overflowBack) overflowBack = ctx->staging().getArray<unsigned int>(1);
-    HIP_CHECK(hipMemcpyAsync(overflowBack, overflowFlag, sizeof(unsigned int), hipMemcpyDeviceToHost, ctx->stream()));
+    ctx->readBack(overflowBack, overflowFlag, sizeof(unsigned int));
     // Final claim cursors are the partition ends (valid when no slot overflowed).
     w->setPartitioned(sout, pbeg, bits, reinterpret_cast<const uint64_t *>(gcur), split.hi, std::max<uint64_t>(cap, 1));
     return;

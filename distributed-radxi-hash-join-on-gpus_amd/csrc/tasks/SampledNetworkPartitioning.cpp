@@ -164,7 +164,7 @@ void SampledNetworkPartitioning::scatterSide(int k) {
   ctx->timeline().end(key, ctx->stream());
   const size_t bytes = 3 * (size_t)G * F * (s.narrow ? 4 : 8);  // starts, final cursors, ends
   s.cursorsBack = ctx->staging().get(bytes);
-  HIP_CHECK(hipMemcpyAsync(s.cursorsBack, s.gstart, bytes, hipMemcpyDeviceToHost, ctx->stream()));
+  ctx->readBack(s.cursorsBack, s.gstart, bytes);
   if (!s.cursorsReady) s.cursorsReady = ctx->acquireEvent();
   HIP_CHECK(hipEventRecord(s.cursorsReady, ctx->stream()));
 }

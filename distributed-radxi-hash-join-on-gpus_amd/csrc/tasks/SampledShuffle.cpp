@@ -75,12 +75,11 @@ void SampledShuffle::sampleAndAssign() {
       kernels::netChunkGroupTotals(blockHist, F, g.blocks, s.local->blocksPerChunk(), s.chunks, groupDev,
                                    ctx->stream());
     } else {
-      HIP_CHECK(hipMemsetAsync(groupDev, 0, (size_t)s.chunks * G * F * 8, ctx->stream()));
+      ctx->zero(groupDev, (size_t)s.chunks * G * F * 8);
     }
     ctx->timeline().end(key, ctx->stream());
     s.sampled = ctx->staging().getArray<uint64_t>((uint64_t)s.chunks * G * F);
-    HIP_CHECK(hipMemcpyAsync(s.sampled, groupDev, (size_t)s.chunks * G * F * 8, hipMemcpyDeviceToHost,
-                             ctx->stream()));
+    ctx->readBack(s.sampled, groupDev, (size_t)s.chunks * G * F * 8);
   }
   utils::waitStream(ctx->stream(), ctx->comm(), "sampled network histograms");
   for (Side &s : sides) {
@@ -214,8 +213,7 @@ void SampledShuffle::scatterSide(int k) {
     if (b1 > b0)
       kernels::netScatter(s.relation->getData(), n, plan.networkBits, plan.keyShift, g, b0, b1, gc, s.send,
                           ctx->stream(), plan.keyBits, mix, ge, s.narrow ? 1 : 0, !plan.keyOnly);
-    HIP_CHECK(hipMemcpyAsync(static_cast<uint8_t *>(s.cursorsBack) + c * perChunk, gc, perChunk,
-                             hipMemcpyDeviceToHost, ctx->stream()));
+    ctx->readBack(static_cast<uint8_t *>(s.cursorsBack) + c * perChunk, gc, perChunk);
     s.scattered[c] = ctx->acquireEvent();
     HIP_CHECK(hipEventRecord(s.scattered[c], ctx->stream()));
   }

@@ -5,7 +5,9 @@ end -- torch.distributed bootstrap, ncclUniqueId broadcast, RCCL all-gather of
 histograms, chunked all-to-allv, all-reduce of the result -- on unique, Zipf
 and materialising joins, and checks every count against the oracle.
 """
+import faulthandler
 import os
+import signal
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -17,7 +19,14 @@ from hpcjoin.parallel import init_distributed, make_context  # noqa: E402
 
 
 def main():
+    # SIGUSR1 dumps every thread's Python stack (the test sends it to all
+    # ranks when a run times out, so a hang says where each rank was).
+    faulthandler.register(signal.SIGUSR1, all_threads=True)
     C = hpcjoin.require_native()
+    # A rank that fails makes its peers fail too (within the test's deadline)
+    # instead of leaving them in a collective: the engine's waits give up
+    # after this long.
+    C.fault.set_comm_timeout_ms(90_000)
     info = init_distributed()
     ctx, comm = make_context(info, "device")
     assert comm.name() == "rccl", comm.name()

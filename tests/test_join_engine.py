@@ -578,3 +578,60 @@ def test_repeated_inner_keys_planned_before_first_join(C, dev):
         assert j.plan.inner_repeats == rep, (rep, j.plan)
         from helpers import ref_join_count
         assert j.run()["global_matches"] == ref_join_count(keys, i)
+
+
+@pytest.mark.parametrize("dev", devices())
+@pytest.mark.parametrize("passes,outer_dist,sparse", [(3, "UNIQUE", False), (4, "ZIPF", False), (2, "UNIFORM", True)])
+def test_capacity_spill_passes(C, dev, passes, outer_dist, sparse):
+    """Capacity spill: the join runs in `passes` key-hash passes (pass k joins
+    the tuples of both sides whose key hashes to k), each a complete join with
+    ~1/passes of the workspace; the counts add up to the oracle and equal the
+    single-pass join."""
+    loc = "device" if dev == "cuda" else "host"
+    ctx = C.ExecContext(loc, 0 if loc == "device" else -1, C.LocalCommunicator())
+    G_R, G_S = 150_001, 400_003
+    inner = C.GenSpec(seed=1234)
+    outer = C.GenSpec(distribution=getattr(C.KeyDistribution, outer_dist), seed=4321,
+                      domain=0 if outer_dist == "UNIQUE" else G_R, zipf_theta=0.9)
+    inner.sparse64 = outer.sparse64 = sparse
+    if outer_dist == "UNIQUE":
+        G_S = G_R
+    R = C.Relation(G_R, G_R, loc, 0)
+    S = C.Relation(G_S, G_S, loc, 0)
+    R.generate(inner, 0)
+    S.generate(outer, 0)
+    exp = C.Relation.expected_matches(inner, G_R, outer, G_S)
+    got = {}
+    for k in (1, passes):
+        cfg = C.JoinConfig()
+        cfg.passes = k
+        j = C.HashJoin(R, S, ctx, cfg)
+        assert j.spill_passes == k
+        for _ in range(2):
+            res = j.run()
+            assert res["global_matches"] == exp, (k, res["global_matches"], exp)
+            assert res["passes"] == k
+        got[k] = res["local_matches"]
+        del j
+    assert got[1] == got[passes]
+
+
+@pytest.mark.gpu
+def test_capacity_spill_auto_budget(C, cuda):
+    """workspace_budget below the plan's estimate: the planner picks K > 1
+    passes by itself and the join stays exact."""
+    ctx = C.ExecContext("device", 0, C.LocalCommunicator())
+    G = 1 << 24
+    R = C.Relation(G, G, "device", 0)
+    S = C.Relation(G, G, "device", 0)
+    R.generate(C.GenSpec(seed=1234), 0)
+    S.generate(C.GenSpec(seed=4321), 0)
+    full = C.HashJoin(R, S, ctx, C.JoinConfig())
+    est = full.workspace_estimate()
+    del full
+    cfg = C.JoinConfig()
+    cfg.workspace_budget = est // 4
+    j = C.HashJoin(R, S, ctx, cfg)
+    assert j.spill_passes >= 4, (j.spill_passes, est)
+    res = j.run()
+    assert res["global_matches"] == G and res["passes"] == j.spill_passes

@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""Capacity spill benchmark: a join whose relations plus workspace exceed
+what HBM holds (or a forced workspace budget) runs in K key-hash passes
+(JoinConfig.passes, kernels/spill.hip).  One JSON line per configuration.
+
+    python tools/bench_spill.py --size 1e9 --budget-frac 0.25      # 1B x 1B, workspace budget = estimate / 4
+    python tools/bench_spill.py --size 6e9                          # 6B x 6B in HBM: 192 GB of relations
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("HSA_ENABLE_SDMA", "0")
+
+import torch  # noqa: E402
+
+import hpcjoin  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=float, default=1e9, help="tuples per relation")
+    ap.add_argument("--budget-frac", type=float, default=0.0,
+                    help="memory budget of one pass (its pass buffers + its workspace) as a fraction of the "
+                         "single-pass workspace estimate; 0: what HBM has free")
+    ap.add_argument("--passes", type=int, default=0, help="force the pass count (0: planner)")
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--input", default="device", choices=["device", "pinned"])
+    ap.add_argument("--reference", default="auto", choices=["auto", "on", "off"],
+                    help="also time the single-pass join when it fits (auto: when no budget is forced)")
+    args = ap.parse_args()
+    C = hpcjoin.require_native()
+    ctx = C.ExecContext("device", 0, C.LocalCommunicator())
+    G = int(args.size)
+    R = C.Relation(G, G, args.input, 0)
+    S = C.Relation(G, G, args.input, 0)
+    R.generate(C.GenSpec(seed=1234), 0)
+    S.generate(C.GenSpec(seed=4321), 0)
+    torch.cuda.synchronize()
+    free0, total = torch.cuda.mem_get_info()
+    probe = C.JoinConfig()
+    probe.reserve_workspace = False
+    probe.passes = 1
+    est = C.HashJoin(R, S, ctx, probe).workspace_estimate()
+    cfg = C.JoinConfig()
+    cfg.passes = args.passes
+    if args.budget_frac > 0:
+        cfg.workspace_budget = int(est * args.budget_frac)
+    t0 = time.perf_counter()
+    j = C.HashJoin(R, S, ctx, cfg)
+    setup_ms = (time.perf_counter() - t0) * 1e3
+    try:
+        first = j.run()
+    except Exception as e:  # noqa: BLE001 -- report what the planner decided
+        print(json.dumps({"bench": "capacity_spill", "size": G, "error": str(e)[:300],
+                          "spill": {k: (round(v / 1e9, 2) if k.endswith("bytes") else v)
+                                    for k, v in j.spill_info.items()},
+                          "single_pass_workspace_estimate_GB": round(est / 1e9, 1),
+                          "hbm_free_after_relations_GB": round(free0 / 1e9, 1)}), flush=True)
+        raise
+    times, res = [], None
+    for _ in range(args.steps):
+        t0 = time.perf_counter()
+        res = j.run()
+        times.append((time.perf_counter() - t0) * 1e3)
+    out = {"bench": "capacity_spill", "size": G, "input": args.input, "relations_GB": round(2 * G * 16 / 1e9, 1),
+           "hbm_total_GB": round(total / 1e9, 1), "hbm_free_after_relations_GB": round(free0 / 1e9, 1),
+           "single_pass_workspace_estimate_GB": round(est / 1e9, 1),
+           "workspace_budget_GB": round(cfg.workspace_budget / 1e9, 1) if cfg.workspace_budget else None,
+           "passes": j.spill_passes, "setup_ms": round(setup_ms, 1), "first_join_ms": round(first["join_ms"], 2),
+           "ms_per_join": round(sum(times) / len(times), 2), "join_ms": [round(t, 2) for t in times],
+           "compact_ms": round(res["compact_ms"], 2), "value_Gtuples_per_s": round(2 * G / (sum(times) / len(times)) / 1e6, 2),
+           "matches": res["global_matches"], "expected_matches": G, "correct": res["global_matches"] == G,
+           "spill": {k: (round(v / 1e9, 2) if k.endswith("bytes") else v) for k, v in j.spill_info.items()},
+           "plan": repr(j.plan)}
+    del j
+    if args.reference == "on" or (args.reference == "auto" and args.budget_frac > 0):
+        one = C.JoinConfig()
+        one.passes = 1
+        jr = C.HashJoin(R, S, ctx, one)
+        jr.run()
+        t = []
+        for _ in range(args.steps):
+            t0 = time.perf_counter()
+            r1 = jr.run()
+            t.append((time.perf_counter() - t0) * 1e3)
+        out["single_pass_ms"] = round(sum(t) / len(t), 2)
+        out["single_pass_correct"] = r1["global_matches"] == G
+        del jr
+    print(json.dumps(out), flush=True)
+    del ctx
+
+
+if __name__ == "__main__":
+    main()
