@@ -17,6 +17,12 @@
 #   ebench=ENV/ARGS     bench.py ARGS with ENV (comma-separated K=V, e.g. HPCJOIN_NET_THREADS=512): A/B runs
 #   abbench=ARGS        same-box A/B: bench.py ARGS of ab/base (a built copy of an older tree) and of this
 #                       tree, alternating base/new twice
+#   sweep=FIELD/V1:V2/ARGS  bench.py ARGS once per value of the HPCJOIN_<FIELD> override (parameter sweeps)
+#   pmcset=GROUP/ARGS   a named PMC group of bench.py ARGS: fetch (FETCH_SIZE), write (WRITE_SIZE),
+#                       sq (waves, busy/wait cycles, LDS instructions and bank conflicts, VMEM rd/wr)
+#   rccl=N/ARGS         bench.py ARGS as N RCCL processes sharing this GPU (HPCJOIN_SHARE_GPU=1: socket
+#                       transport -- the multi-process path end to end, not xGMI speed)
+#   prccl=N/ARGS        the same under rocprofv3 --kernel-trace (stream overlap across ranks)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
 TAG=$1
@@ -41,6 +47,26 @@ for step in "$@"; do
     ebench) envs=${arg%%/*}; bargs=${arg#*/}
             timeout -k 10 600 env ${envs//,/ } python -u bench.py ${bargs//,/ } > "$log" 2>&1 ;;
     skew) timeout -k 10 900 python -u tools/bench_skew.py $args > "$log" 2>&1 ;;
+    sweep) f=${arg%%/*}; rest=${arg#*/}; vals=${rest%%/*}; bargs=${rest#*/}; [ "$bargs" = "$rest" ] && bargs=""
+           rc=0
+           for v in ${vals//:/ }; do
+             env HPCJOIN_$f=$v timeout -k 10 300 python -u bench.py ${bargs//,/ } > "$OUT/$n.$f=$v.log" 2>&1 || { rc=$?; break; }
+           done
+           echo "sweep $f rc=$rc" > "$log"; (exit $rc) ;;
+    pmcset) grp=${arg%%/*}; bargs=${arg#*/}; [ "$bargs" = "$arg" ] && bargs=""
+            case $grp in
+              fetch) ctrs="FETCH_SIZE" ;;
+              write) ctrs="WRITE_SIZE" ;;
+              sq) ctrs="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD" ;;
+              *) echo "unknown pmc group $grp"; exit 2 ;;
+            esac
+            (cd /tmp && timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $ctrs -d "$OUT/pmc$n" -o run \
+               --output-format csv -- python "$R/bench.py" ${bargs//,/ }) > "$log" 2>&1 ;;
+    rccl) np=${arg%%/*}; bargs=${arg#*/}; [ "$bargs" = "$arg" ] && bargs=""
+          HPCJOIN_SHARE_GPU=1 timeout -k 10 900 python -u bench.py --gpus $np ${bargs//,/ } > "$log" 2>&1 ;;
+    prccl) np=${arg%%/*}; bargs=${arg#*/}; [ "$bargs" = "$arg" ] && bargs=""
+           (cd /tmp && HPCJOIN_SHARE_GPU=1 timeout -k 10 600 rocprofv3 --kernel-trace -d "$OUT/trace$n" -o run \
+              --output-format csv -- python "$R/bench.py" --gpus $np ${bargs//,/ }) > "$log" 2>&1 ;;
     abbench) rc=0
              for i in 1 2; do
                (cd "$R/ab/base" && timeout -k 10 300 python -u bench.py $args > "$OUT/$n.base$i.log" 2>&1) || { rc=$?; break; }
