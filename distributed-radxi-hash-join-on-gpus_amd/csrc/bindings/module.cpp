@@ -993,6 +993,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         d["pass_buffer_bytes"] = j.spill.passBuffers;
         d["pass_estimate_bytes"] = j.spill.passEstimate;
         d["pass_workspace_bytes"] = j.spill.passReserved;
+        d["pass_peak_bytes"] = j.spill.passPeak;
         return d;
       })
       .def_property_readonly("plan_ms", &operators::HashJoin::planMilliseconds)

@@ -71,9 +71,10 @@ void HashJoin::planPasses() {
     K = 1;
     if (ctx->onDevice() && config.reserveWorkspace && !plan.materialize) {
       // One pass holds its pass buffers (~1/K of both relations) and its
-      // join's workspace (~1/K of the estimate, with a margin for the smaller
-      // joins' fixed parts and for pass-size spread).  workspaceBudget caps
-      // both together.
+      // join's workspace (~1/K of the estimate, with a margin: a pass join's
+      // sampled local pass that overflows re-runs exactly beside its sampled
+      // buffers -- 6B x 6B in 6 passes peaked at 1.55x its estimate and ran
+      // out of HBM).  workspaceBudget caps both together.
       size_t freeB = 0, totalB = 0;
       HIP_CHECK(hipMemGetInfo(&freeB, &totalB));
       uint64_t avail = (uint64_t)(freeB * 0.85);
@@ -84,7 +85,7 @@ void HashJoin::planPasses() {
       if (est > avail) {
         K = 2;
         while (K < kernels::MAX_SPILL_PASSES &&
-               (double)est / K * 1.3 + (double)tuplesB / K * 1.05 + (256u << 20) > (double)avail)
+               (double)est / K * 1.6 + (double)tuplesB / K * 1.05 + (256u << 20) > (double)avail)
           ++K;
       }
     }
@@ -168,6 +169,7 @@ JoinResult HashJoin::runPasses() {
     spill.passEstimate = std::max<uint64_t>(spill.passEstimate, pass.workspaceEstimate());
     spill.passReserved = std::max<uint64_t>(spill.passReserved, ctx->workspace().capacity());
     const JoinResult r = pass.run();
+    spill.passPeak = std::max<uint64_t>(spill.passPeak, ctx->workspace().peak());
     total.localMatches += r.localMatches;
     total.globalMatches += r.globalMatches;
     total.innerReceived += r.innerReceived;

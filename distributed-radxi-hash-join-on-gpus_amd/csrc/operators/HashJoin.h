@@ -165,7 +165,7 @@ class HashJoin {
   // workspaceBudget), the pass buffers, and the largest pass join's estimate
   // and reservation (filled in by runPasses).
   struct SpillInfo {
-    uint64_t estimate = 0, available = 0, passBuffers = 0, passEstimate = 0, passReserved = 0;
+    uint64_t estimate = 0, available = 0, passBuffers = 0, passEstimate = 0, passReserved = 0, passPeak = 0;
   } spill;
  private:
   uint64_t outputEpoch = 0;  // workspace epoch when `output` was written

@@ -9,7 +9,7 @@ from .._native import require_native
 _FIELDS = ["network_bits", "local_bits", "two_level", "key_shift", "materialize", "output_capacity", "build_target",
            "r_chunk", "s_chunk", "chunks", "checks", "max_partition_blocks", "sample_stride", "local_sample_stride", "local_item_tiles", "local_geometry",
            "split_local", "direct_count", "split_histogram", "pipeline_outer", "bitmap_join", "skew_split",
-           "reserve_workspace",
+           "reserve_workspace", "passes", "workspace_budget",
            # kernel-shape variants (sweeps / A-B tests; JoinConfig.variants in C++)
            "net_ipt", "net_threads", "bm_threads", "bm_flat", "reduce_chunks", "key_count", "rows_lds", "mat_variant"]
 _BOOLS = ("two_level", "materialize", "checks", "split_local", "direct_count", "split_histogram", "pipeline_outer",

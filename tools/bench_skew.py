@@ -204,6 +204,9 @@ def main():
     ap.add_argument("--configs", default="zipf_both,uniform_two,zipf_outer")
     ap.add_argument("--assign", default="lpt", help="comma list of lpt,round_robin (N > 1)")
     ap.add_argument("--split", default="on", help="comma list of on,off: hot-partition split (N > 1, LPT)")
+    ap.add_argument("--shuffle", action="store_true",
+                    help="N > 1: force the hash-partition shuffle (no replicated bitmaps), so the assignment decides "
+                         "what every rank receives")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     args = ap.parse_args()
@@ -217,8 +220,9 @@ def main():
                 if assign != "lpt" and split == "on" and len(args.split.replace("+", ",").split(",")) > 1:
                     continue  # the split only exists under LPT
                 cfg = config_from_dict({"assignment": assign.upper(), "skew_split": split == "on", "chunks": 1 if info.world == 1 else 4})
-                if name == "uniform_two":
-                    cfg.bitmap_join = False
+                if name == "uniform_two" or args.shuffle:
+                    if name == "uniform_two":
+                        cfg.bitmap_join = False
                     cfg.replicate_bitmap = C.PlanChoice.OFF
                 out = run_config(C, info, ctx, comm, name, G_R, G_S, args.theta, cfg, args.steps, args.warmup,
                                  int(args.domain))
