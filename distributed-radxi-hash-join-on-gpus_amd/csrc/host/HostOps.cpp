@@ -20,8 +20,6 @@ static double zeta(uint64_t n, double theta) {
   for (uint64_t i = 1; i <= m; ++i) s += std::pow((double)i, -theta);
   if (n > m) {
     const double a = (double)m, b = (double)n;
-    const double f = [&] { return 0.0; }();
-    (void)f;
     // integral_a^b x^-t dx + (f(b) - f(a))/2 - (f'(b) - f'(a))/12
     s += (std::pow(b, 1 - theta) - std::pow(a, 1 - theta)) / (1 - theta);
     s += (std::pow(b, -theta) - std::pow(a, -theta)) / 2;
@@ -32,7 +30,12 @@ static double zeta(uint64_t n, double theta) {
 
 kernels::ZipfParams makeZipf(uint64_t n, double theta) {
   JOIN_ASSERT(n >= 2, "Zipf", "domain must be >= 2");
-  JOIN_ASSERT(theta > 0 && theta < 1, "Zipf", "theta must be in (0,1), got %f", theta);
+  // Gray et al.'s closed-form inverse is the continuous approximation of
+  // sum_{i<=r} i^-theta, valid on both sides of 1 (alpha = 1/(1-theta) < 0
+  // above it): ranks 0 and 1 are exact, the rest within ~1% of the mass
+  // (tests/test_package.py checks theta 0.99 and 1.1).  theta = 1 has no alpha.
+  JOIN_ASSERT(theta > 0 && theta <= 4 && std::fabs(theta - 1.0) >= 1e-3, "Zipf",
+              "theta must be in (0,4] and not 1, got %f", theta);
   kernels::ZipfParams z;
   z.n = n;
   z.theta = theta;

@@ -39,6 +39,22 @@ def test_ops_pipeline_and_join(dev):
     assert torch.equal(got, ref)
 
 
+@pytest.mark.parametrize("dev", devices())
+@pytest.mark.parametrize("theta,domain", [(0.99, 20), (1.1, 100), (1.5, 100)])
+def test_zipf_frequencies(dev, theta, domain):
+    """Zipf draws (theta on both sides of 1) against the exact law: the two
+    hottest keys are exact in Gray et al.'s inverse, the rest within ~1.5%."""
+    from hpcjoin import ops
+    n = 400_000
+    S = ops.generate(n, "ZIPF", seed=9, domain=domain, zipf_theta=theta, device=dev).cpu()
+    freq = torch.sort(torch.unique(S[:, 0], return_counts=True)[1].double() / n, descending=True).values
+    law = torch.arange(1, domain + 1, dtype=torch.float64) ** -theta
+    law /= law.sum()
+    assert freq.numel() <= domain
+    assert abs(freq[0] - law[0]) < 0.004 and abs(freq[1] - law[1]) < 0.004
+    assert (freq - law[:freq.numel()]).abs().max() < 0.015
+
+
 def test_config_roundtrip(C, monkeypatch):
     from hpcjoin.utils import config_from_dict, config_to_dict
     cfg = config_from_dict({"network_bits": 7, "assignment": "round_robin", "materialize": True, "format": "wide"})
