@@ -854,7 +854,35 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("workspace_scratch", [](core::ExecContext &c, uint64_t b) {
              return reinterpret_cast<uintptr_t>(c.workspace().get(b));
            }, "Hand out b bytes of the workspace (tests of the arena's growth rules)")
-      .def("synchronize", &core::ExecContext::synchronize);
+      .def("synchronize", &core::ExecContext::synchronize)
+      // One-sided window plumbing, for the IPC ordering tests (tests/ipc_order_worker.py)
+      .def("ipc_export", [](core::ExecContext &c, uintptr_t p) {
+             uint64_t h[8], off = 0, gen = 0, tagOff = 0, nonce = 0;
+             c.ipcExport(reinterpret_cast<const void *>(p), h, &off, &gen, &tagOff, &nonce);
+             return py::make_tuple(py::bytes(reinterpret_cast<const char *>(h), sizeof(h)), off, gen, tagOff, nonce);
+           }, py::arg("ptr"),
+           "(handle bytes, offset in its allocation, workspace generation, tag offset, tag nonce) of a workspace "
+           "address")
+      .def("ipc_import", [](core::ExecContext &c, uint32_t peer, const py::bytes &handle, uint64_t gen,
+                            uint64_t tagOff, uint64_t nonce) {
+             const std::string s = handle;
+             TORCH_CHECK(s.size() == 64, "an IPC handle is 64 bytes");
+             uint64_t h[8];
+             std::memcpy(h, s.data(), 64);
+             return reinterpret_cast<uintptr_t>(c.ipcImport(peer, h, gen, tagOff, nonce));
+           }, py::arg("peer"), py::arg("handle"), py::arg("generation"), py::arg("tag_offset"), py::arg("nonce"),
+           "Base address of the mapping of a peer's exported allocation (cached per handle and generation; a "
+           "fresh open checks the allocation's tag and throws on a stale mapping)")
+      .def("release_imports", &core::ExecContext::releaseImports)
+      .def("ipc_mappings", &core::ExecContext::ipcMappings)
+      .def("ipc_log", [](const core::ExecContext &c) {
+             py::list out;
+             for (const auto &e : c.ipcLog())
+               out.append(py::make_tuple(std::string(1, e.op), e.cached, e.peer, e.generation, e.handleHash,
+                                         reinterpret_cast<uintptr_t>(e.ptr)));
+             return out;
+           }, "(op, cached, peer, generation, handle hash, address) per export 'E' / open 'O' / stale close 'C' / "
+              "releaseImports 'R', in order");
 
   py::class_<data::GenSpec>(m, "GenSpec")
       .def(py::init<>())
@@ -1123,6 +1151,40 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
             "(rank -1: any rank).  An empty phase disarms.");
   fault.def("set_comm_timeout_ms", &utils::setCommTimeoutMs, py::arg("ms"));
   fault.def("comm_timeout_ms", &utils::commTimeoutMs);
+
+  auto ipc = m.def_submodule("ipc", "raw HIP IPC calls and host copies, for the IPC ordering tests");
+  ipc.def("get_handle", [](uintptr_t p) {
+    hipIpcMemHandle_t h;
+    HIP_CHECK(hipIpcGetMemHandle(&h, reinterpret_cast<void *>(p)));
+    return py::bytes(reinterpret_cast<const char *>(&h), sizeof(h));
+  });
+  ipc.def("open", [](const py::bytes &handle) {
+    const std::string s = handle;
+    TORCH_CHECK(s.size() == sizeof(hipIpcMemHandle_t), "an IPC handle is 64 bytes");
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, s.data(), sizeof(h));
+    void *p = nullptr;
+    HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+    return reinterpret_cast<uintptr_t>(p);
+  });
+  ipc.def("close", [](uintptr_t p) { HIP_CHECK(hipIpcCloseMemHandle(reinterpret_cast<void *>(p))); });
+  ipc.def("is_device_pointer", [](uintptr_t p) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, reinterpret_cast<void *>(p)) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return a.type == hipMemoryTypeDevice;
+  });
+  ipc.def("write", [](uintptr_t p, const py::bytes &b) {
+    const std::string s = b;
+    HIP_CHECK(hipMemcpy(reinterpret_cast<void *>(p), s.data(), s.size(), hipMemcpyHostToDevice));
+  });
+  ipc.def("read", [](uintptr_t p, size_t n) {
+    std::string s(n, '\0');
+    HIP_CHECK(hipMemcpy(s.data(), reinterpret_cast<const void *>(p), n, hipMemcpyDeviceToHost));
+    return py::bytes(s);
+  });
 
   auto meas = m.def_submodule("measurements");
   meas.def("init", &performance::Measurements::init, py::arg("node_id"), py::arg("number_of_nodes"),

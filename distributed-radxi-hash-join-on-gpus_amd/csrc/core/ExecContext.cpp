@@ -5,6 +5,7 @@
 #include <cstddef>
 #include <cstdlib>
 #include <cstring>
+#include <unistd.h>
 #include <mutex>
 #include <set>
 #include <immintrin.h>
@@ -194,7 +195,17 @@ void ExecContext::resetScratch() {
   eventsUsed_ = 0;
 }
 
-void ExecContext::ipcExport(const void *p, uint64_t handle[8], uint64_t *offset, uint64_t *generation) {
+void ExecContext::logIpc(char op, bool cached, uint32_t peer, uint64_t generation, const void *handle,
+                         const void *ptr) {
+  uint64_t h = 1469598103934665603ull;
+  if (handle)
+    for (size_t i = 0; i < sizeof(hipIpcMemHandle_t); ++i) h = (h ^ static_cast<const uint8_t *>(handle)[i]) * 1099511628211ull;
+  if (ipcLog_.size() >= 4096) ipcLog_.erase(ipcLog_.begin(), ipcLog_.begin() + 1024);
+  ipcLog_.push_back(IpcEvent{op, cached, peer, generation, handle ? h : 0, ptr});
+}
+
+void ExecContext::ipcExport(const void *p, uint64_t handle[8], uint64_t *offset, uint64_t *generation,
+                            uint64_t *tagOffset, uint64_t *nonce) {
   static_assert(sizeof(hipIpcMemHandle_t) == 64, "unexpected hipIpcMemHandle_t size");
   JOIN_ASSERT(onDevice(), "ExecContext", "IPC export of host memory");
   void *base = workspace_->allocationOf(p);
@@ -207,18 +218,32 @@ void ExecContext::ipcExport(const void *p, uint64_t handle[8], uint64_t *offset,
   const IpcExport *hit = nullptr;
   for (const auto &x : ipcExported_)
     if (x.base == base) hit = &x;
+  const bool cached = hit != nullptr;
   if (!hit) {
-    IpcExport x{base, gen, {}};
+    IpcExport x{base, gen, {}, 0, 0};
     HIP_CHECK(hipIpcGetMemHandle(&x.handle, base));
+    uint8_t *tag = static_cast<uint8_t *>(workspace_->tagOf(base));
+    JOIN_ASSERT(tag != nullptr, "ExecContext", "IPC export: allocation %p has no tag", base);
+    x.tagOffset = (uint64_t)(tag - static_cast<uint8_t *>(base));
+    // Unique per process and export: pid, a serial, and the clock.
+    x.nonce = ((uint64_t)getpid() << 40) ^ (++exportSerial_ << 20) ^
+              (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+    const uint64_t stamp[2] = {x.nonce, gen};
+    HIP_CHECK(hipSetDevice(device_));
+    HIP_CHECK(hipMemcpy(tag, stamp, sizeof(stamp), hipMemcpyHostToDevice));
     ipcExported_.push_back(x);
     hit = &ipcExported_.back();
   }
+  logIpc('E', cached, comm_ ? comm_->rank() : 0, gen, &hit->handle, base);
   std::memcpy(handle, &hit->handle, sizeof(hit->handle));
   *offset = (uint64_t)(static_cast<const uint8_t *>(p) - static_cast<const uint8_t *>(base));
   *generation = workspace_->generation();
+  *tagOffset = hit->tagOffset;
+  *nonce = hit->nonce;
 }
 
-void *ExecContext::ipcImport(uint32_t peer, const uint64_t handle[8], uint64_t generation) {
+void *ExecContext::ipcImport(uint32_t peer, const uint64_t handle[8], uint64_t generation, uint64_t tagOffset,
+                             uint64_t nonce) {
   std::vector<uint64_t> key(handle, handle + 8);
   for (size_t i = 0; i < ipcImported_.size();) {
     IpcMapping &m = ipcImported_[i];
@@ -228,22 +253,41 @@ void *ExecContext::ipcImport(uint32_t peer, const uint64_t handle[8], uint64_t g
     // fallback allocation behind the peer's second window) keeps the
     // generation: the first window's mapping stays open.
     if (m.peer == peer && m.generation != generation) {
+      logIpc('C', false, peer, m.generation, m.handle.data(), m.base);
       HIP_CHECK(hipIpcCloseMemHandle(m.base));
       ipcImported_.erase(ipcImported_.begin() + i);
       continue;
     }
-    if (m.peer == peer && m.handle == key) return m.base;
+    if (m.peer == peer && m.handle == key) {
+      JOIN_ASSERT(m.nonce == nonce, "ExecContext",
+                  "IPC import from rank %u: a cached mapping of generation %lu carries another export's tag", peer,
+                  (unsigned long)generation);
+      return m.base;
+    }
     ++i;
   }
   hipIpcMemHandle_t h;
   std::memcpy(&h, handle, sizeof(h));
   void *ptr = nullptr;
   HIP_CHECK(hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess));
-  ipcImported_.push_back(IpcMapping{peer, std::move(key), generation, ptr});
+  logIpc('O', false, peer, generation, &h, ptr);
+  uint64_t stamp[2] = {0, 0};
+  HIP_CHECK(hipSetDevice(device_));
+  HIP_CHECK(hipMemcpy(stamp, static_cast<uint8_t *>(ptr) + tagOffset, sizeof(stamp), hipMemcpyDeviceToHost));
+  if (stamp[0] != nonce || stamp[1] != generation) {
+    (void)hipIpcCloseMemHandle(ptr);
+    JOIN_ASSERT(false, "ExecContext",
+                "stale IPC mapping: rank %u's handle (generation %lu) opened memory tagged by another export "
+                "(generation %lu) -- a mapping of a freed allocation at the same address is still open in this "
+                "process, so puts through it would be lost",
+                peer, (unsigned long)generation, (unsigned long)stamp[1]);
+  }
+  ipcImported_.push_back(IpcMapping{peer, std::move(key), generation, ptr, nonce});
   return ptr;
 }
 
 void ExecContext::releaseImports() {
+  if (!ipcImported_.empty()) logIpc('R', false, 0, 0, nullptr, nullptr);
   for (auto &m : ipcImported_) HIP_CHECK(hipIpcCloseMemHandle(m.base));
   ipcImported_.clear();
 }

@@ -65,24 +65,44 @@ class ExecContext {
   // creating and destroying several per join.
   hipEvent_t acquireEvent();
   // One-sided exchange (JoinConfig::exchange = OneSided): the IPC handle of
-  // the device allocation holding `p` (8 words), p's offset in it and the
-  // workspace generation (memory::Arena::generation); and the mapping of a
-  // peer's exported allocation, cached per (peer, handle) while the peer's
-  // generation is unchanged.  A peer whose generation moved may have freed
-  // what we mapped (and ROCm may reuse handle bytes): its mappings are closed
-  // and re-opened.
-  void ipcExport(const void *p, uint64_t handle[8], uint64_t *offset, uint64_t *generation);
-  void *ipcImport(uint32_t peer, const uint64_t handle[8], uint64_t generation);
+  // the device allocation holding `p` (8 words), p's offset in it, the
+  // workspace generation (memory::Arena::generation), and the allocation's
+  // tag (offset of its Arena::TAG_BYTES tail, and the nonce this export
+  // wrote there); and the mapping of a peer's exported allocation, cached per
+  // (peer, handle) while the peer's generation is unchanged.
+  //
+  // ROCm's handle is derived from the allocation's address: a new allocation
+  // at a freed one's address exports the SAME handle bytes, and while this
+  // process still holds any open mapping of the old handle, opening the new
+  // one returns that mapping of the FREED memory -- puts through it are lost
+  // (tests/ipc_order_worker.py; round 4's inexact one-sided join).  So a
+  // peer whose generation moved has its mappings closed before the open, and
+  // every fresh open reads the tag back: a nonce other than the one the
+  // exporter sent means a stale mapping, and the import throws.
+  void ipcExport(const void *p, uint64_t handle[8], uint64_t *offset, uint64_t *generation, uint64_t *tagOffset,
+                 uint64_t *nonce);
+  void *ipcImport(uint32_t peer, const uint64_t handle[8], uint64_t generation, uint64_t tagOffset, uint64_t nonce);
   size_t ipcMappings() const { return ipcImported_.size(); }
-  // Between joins, before an explicit workspace trim frees this rank's
-  // memory: close every mapping of peers' memory first, so no rank's free can
-  // wait on a peer that is itself waiting in a free (the multi-process
-  // one-sided test hung intermittently around `trim_workspace(0)`; 3 of 3
-  // clean runs at 2/4/8 ranks since, gpurun_out/rccl_repeat6-8).  Imports are
-  // re-opened at the next join.  Not called when a plan re-lays the workspace
-  // out: closing there made the next one-sided join at 4 ranks inexact
-  // (rccl_repeat4); that path keeps closing stale mappings in ipcImport.
+  // Between joins, before any rank frees workspace memory (trim_workspace,
+  // a plan that re-lays the workspace out at N > 1): every rank closes its
+  // mappings of peers' memory, then a barrier, then the frees -- so no
+  // mapping outlives the allocation it names and no handle is opened after
+  // its allocation is gone (HashJoin::makeJoinPlan, module.cpp trim_workspace).
+  // Imports are re-opened at the next join.
   void releaseImports();
+  // Every export / open / close of this context, in order (the last 4096):
+  // op 'E' export (cached = true: the allocation's handle of this
+  // generation was handed out again), 'O' open, 'C' close of a stale
+  // mapping, 'R' releaseImports.  handleHash = FNV-1a of the 64 handle bytes.
+  struct IpcEvent {
+    char op;
+    bool cached;
+    uint32_t peer;
+    uint64_t generation;
+    uint64_t handleHash;
+    const void *ptr;
+  };
+  const std::vector<IpcEvent> &ipcLog() const { return ipcLog_; }
 
   // Persistent join scratch of a device engine (kernels::DeviceControl):
   // zeroed once here; the kernels that consume it return it to zero, so the
@@ -126,6 +146,7 @@ class ExecContext {
     std::vector<uint64_t> handle;
     uint64_t generation;
     void *base;
+    uint64_t nonce;
   };
   std::vector<IpcMapping> ipcImported_;
   // One export per allocation and arena generation: a second
@@ -137,8 +158,12 @@ class ExecContext {
     void *base;
     uint64_t generation;
     hipIpcMemHandle_t handle;
+    uint64_t tagOffset, nonce;
   };
+  uint64_t exportSerial_ = 0;
   std::vector<IpcExport> ipcExported_;
+  std::vector<IpcEvent> ipcLog_;
+  void logIpc(char op, bool cached, uint32_t peer, uint64_t generation, const void *handle, const void *ptr);
 };
 
 }  // namespace core

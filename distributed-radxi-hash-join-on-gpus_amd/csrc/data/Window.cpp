@@ -226,12 +226,12 @@ void Window::enableOneSided() {
   const bool shared = ctx->comm()->sharesAddressSpace();
   JOIN_ASSERT(shared || ctx->onDevice(), "Window", "one-sided host windows need in-process ranks");
   // Per rank: {pid, raw pointer, IPC handle (8 words), offset, workspace
-  // generation, device, recvDispls[C][N]}.
-  const size_t H = 13, R = H + (size_t)C * N;
+  // generation, device, tag offset, tag nonce, recvDispls[C][N]}.
+  const size_t H = 15, R = H + (size_t)C * N;
   std::vector<uint64_t> mine(R, 0), all(R * N);
   mine[0] = (uint64_t)getpid();
   mine[1] = (uint64_t)(uintptr_t)data;
-  if (!shared) ctx->ipcExport(data, &mine[2], &mine[10], &mine[11]);
+  if (!shared) ctx->ipcExport(data, &mine[2], &mine[10], &mine[11], &mine[13], &mine[14]);
   mine[12] = ctx->onDevice() ? (uint64_t)ctx->device() : ~0ull;
   for (size_t i = 0; i < (size_t)C * N; ++i) mine[H + i] = plan.recvDispls[i];
   ctx->comm()->allGatherHost(mine.data(), all.data(), R);
@@ -258,7 +258,7 @@ void Window::enableOneSided() {
       }
       peerBase[p] = reinterpret_cast<uint8_t *>((uintptr_t)r[1]);
     } else {
-      peerBase[p] = static_cast<uint8_t *>(ctx->ipcImport(p, &r[2], r[11])) + r[10];
+      peerBase[p] = static_cast<uint8_t *>(ctx->ipcImport(p, &r[2], r[11], r[13], r[14])) + r[10];
     }
     for (uint32_t c = 0; c < C; ++c) peerOffset[(size_t)p * C + c] = r[H + (size_t)c * N + me];
   }

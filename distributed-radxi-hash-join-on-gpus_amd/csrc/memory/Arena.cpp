@@ -119,7 +119,7 @@ uint64_t Arena::used() const {
 
 void Arena::addChunk(uint64_t bytes, bool touch, void *stream) {
   bytes = ceilDiv(std::max<uint64_t>(bytes, ALIGNMENT), BIG_ALIGNMENT) * BIG_ALIGNMENT;
-  uint8_t *p = static_cast<uint8_t *>(rawAlloc(loc_, bytes, device_));
+  uint8_t *p = static_cast<uint8_t *>(rawAlloc(loc_, bytes + TAG_BYTES, device_));  // + the allocation's tag
   if (touch) {
     if (loc_ == Location::Device) {
       HIP_CHECK(hipSetDevice(device_));
@@ -193,7 +193,7 @@ void *Arena::get(uint64_t bytes) {
       return c.base + start;
     }
   }
-  void *p = rawAlloc(loc_, sz, device_);
+  void *p = rawAlloc(loc_, sz + TAG_BYTES, device_);
   const uint64_t accounted = sz + (align > ALIGNMENT ? align : 0);  // room for the padding once sub-allocated
   fallbacks_.push_back(Fallback{p, sz, accounted});
   fallbackBytes_ += accounted;
@@ -236,6 +236,14 @@ void *Arena::allocationOf(const void *p) const {
     const uint8_t *b = static_cast<const uint8_t *>(f.p);
     if (q >= b && q < b + f.bytes) return f.p;
   }
+  return nullptr;
+}
+
+void *Arena::tagOf(const void *base) const {
+  for (const auto &c : chunks_)
+    if (c.base == base) return c.base + c.cap;
+  for (const auto &f : fallbacks_)
+    if (f.p == base) return static_cast<uint8_t *>(f.p) + f.bytes;
   return nullptr;
 }
 

@@ -36,6 +36,11 @@ class Arena {
   static constexpr uint64_t ALIGNMENT = 256;  // >= a 128-B L2 line, 16-B LDS-DMA friendly
   static constexpr uint64_t BIG_BYTES = 4ull << 20;
   static constexpr uint64_t BIG_ALIGNMENT = 2ull << 20;
+  // Every raw allocation (chunk or fallback) ends in TAG_BYTES the arena
+  // never hands out: the one-sided exchange stamps an exported allocation
+  // there, so a peer can prove its IPC mapping names that allocation and not
+  // a freed one at the same address (core/ExecContext::ipcImport).
+  static constexpr uint64_t TAG_BYTES = 256;
 
   Arena(Location loc, int device = 0) : loc_(loc), device_(device) {}
   ~Arena();
@@ -79,6 +84,8 @@ class Arena {
   bool owns(const void *p) const;
   // Start of the raw allocation (chunk or fallback) holding p; null if none.
   void *allocationOf(const void *p) const;
+  // The TAG_BYTES tail of the allocation starting at `base`; null if none.
+  void *tagOf(const void *base) const;
   void freeFallback(void *p);         // frees one fallback allocation (no-op for arena memory)
 
   static void *rawAlloc(Location loc, uint64_t bytes, int device);

@@ -697,3 +697,38 @@ def test_capacity_spill_multirank(C, dev, n_ranks, passes, opts):
                              outer_dist="ZIPF", theta=0.8)
     for res, plan in results:
         assert res["global_matches"] == exp and res["passes"] == passes
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(120)
+def test_ipc_ordering():
+    """Round 4's one-sided failures replayed in a fixed order by two processes
+    on one GPU (tests/ipc_order_worker.py): two windows in one allocation,
+    the exporter's re-layout while the importer holds mappings, a handle
+    opened after its allocation was freed.  The engine's export cache,
+    generation checks and coordinated release must give exact contents in
+    every case; what raw HIP IPC did in the same orders (round 4's calls) is
+    written to gpurun_out/ipc_order.json."""
+    port = _free_port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2", LOCAL_WORLD_SIZE="2",
+               HPCJOIN_SHARE_GPU="1")
+    script = os.path.join(ROOT, "tests", "ipc_order_worker.py")
+    procs = [subprocess.Popen([sys.executable, "-u", script], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(2)]
+    try:
+        outs = [p.communicate(timeout=90)[0] for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    gout = os.path.join(ROOT, "gpurun_out")
+    obs = next((ln[len("IPC_ORDER "):] for ln in outs[1].splitlines() if ln.startswith("IPC_ORDER ")), None)
+    if os.path.isdir(gout):
+        with open(os.path.join(gout, "ipc_order.json"), "w") as f:
+            f.write(obs or "null")
+            f.write("\n")
+            for i, o in enumerate(outs):
+                f.write(f"===== rank {i} =====\n{o}\n")
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o[-4000:]
+    assert obs is not None, outs[1][-4000:]
