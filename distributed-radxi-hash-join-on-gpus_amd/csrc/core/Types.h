@@ -42,7 +42,7 @@ HJ_HD uint64_t ceilDiv(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 // launcher reads the environment (Python: HPCJOIN_<FIELD> is resolved once by
 // utils.config.config_from_dict).
 struct KernelVariants {
-  uint32_t netIpt = 0;        // claim-scatter tile: 0 = auto (16 x 1024 for u32 words, 8 x 1024 else), 15 = 15K tiles at 2048-way
+  uint32_t netIpt = 0;        // claim-scatter tile: 0 = 8 x 1024, 16 = 16 x 1024 (u32 words only), 15 = 15K tiles at 2048-way
   uint32_t netThreads = 0;    // claim-scatter workgroup width: 0 = 1024, 512 = half-width (2-3 per CU)
   uint32_t bmThreads = 0;     // bitmap kernels' workgroup size: 0 = auto (256 for <= 32 KiB bitmaps, else 1024)
   int32_t bmFlat = -1;        // bitmap slice walk: -1 = auto, 0 = per claim slice, 1 = one flat walk per partition

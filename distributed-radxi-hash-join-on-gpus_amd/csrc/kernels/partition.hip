@@ -496,6 +496,7 @@ struct NetFragPolT : KeyLoad {
   using StageT = uint32_t;
   using OutT = uint32_t;
   static constexpr bool kDigArray = false;
+  static constexpr bool kEarly = true;  // earlyPrefetch
   uint64_t mask;
   uint32_t bits;
   KeyMix mix;
@@ -667,6 +668,29 @@ __device__ __forceinline__ void prefetchTile(const typename Pol::InT *__restrict
   }
 }
 
+// Early prefetch: when the staged word is no wider than the loaded one and
+// carries its digit (no separate digit array), the rank phase turns every
+// loaded element into its staged word right away, so the registers of the
+// loaded tile are free again before the scan -- the next tile's loads are
+// issued after the claims (so the claim atomics, issued first, can be waited
+// for without waiting for the loads) and overlap the scan, the staging and
+// the write-out instead of only the write-out.  Only where the tile's loads
+// take at most 16 VGPRs per thread: with wider tiles the staged words, ranks
+// and next tile no longer fit 128 VGPRs (1024-thread groups) and spill.  And
+// only for policies that opt in (kEarly): measured on MI355X, same box, the
+// count-only fragment scatter gains (1.90 -> 1.80 ms per call, 1B x 1B join
+// 10.16 -> 9.62 ms) while the key-only scatter is unchanged (2.28 / 2.31) and
+// the local split scatter loses (1.45 -> 1.54).
+template <class P, class = void>
+struct EarlyOptIn : std::false_type {};
+template <class P>
+struct EarlyOptIn<P, std::void_t<decltype(P::kEarly)>> : std::integral_constant<bool, P::kEarly> {};
+template <class Pol, int IPT>
+constexpr bool earlyPrefetch() {
+  return EarlyOptIn<Pol>::value && !Pol::kDigArray && sizeof(typename Pol::StageT) <= sizeof(typename Pol::LoadT) &&
+         IPT * sizeof(typename Pol::LoadT) <= 64;
+}
+
 // One tile.  FULL tiles (every tile but a range's tail) have no divergent
 // control flow at all, so hipcc keeps the IPT LDS atomics, loads and stores
 // in flight with counted waits; the tail tile predicates its LDS work only.
@@ -680,14 +704,22 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
                                             const Pol &pol, typename Pol::OutT *__restrict__ out,
                                             typename Pol::LoadT (&v)[IPT], CurT *__restrict__ gcur) {
   constexpr uint32_t TILE = NTH * IPT;
+  constexpr bool EARLY = earlyPrefetch<Pol, IPT>();
   const uint32_t t = threadIdx.x;
+  // EARLY: sw = staged words, dr = ranks (then positions); else dr = digit << 16 | rank.
   uint32_t dr[IPT];
+  typename Pol::StageT sw[EARLY ? IPT : 1];
 #pragma unroll
   for (int i = 0; i < IPT; ++i) {
     const uint32_t idx = i * NTH + t;
     if (FULL || idx < count) {
       const uint32_t d = pol.digit(v[i]);
-      dr[i] = (d << 16) | atomicAdd(&l.cnt[d], 1u);
+      if constexpr (EARLY) {
+        dr[i] = atomicAdd(&l.cnt[d], 1u);
+        sw[i] = pol.stage(v[i], d);
+      } else {
+        dr[i] = (d << 16) | atomicAdd(&l.cnt[d], 1u);
+      }
     }
   }
   // Barriers of the tile loop order LDS only (ldsBarrier): the waves share
@@ -710,6 +742,7 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
       if (wave0 + k * NTH < F) claim[k] = atomicAdd(d < F ? gcur + d : trash + t, (CurT)l.cnt[d]);
     }
   }
+  if constexpr (EARLY) prefetchTile<Pol, NTH, IPT>(in, base + TILE, end - 1, v);
   blockExclusiveScanLds<NTH, uint32_t, uint32_t, true>(l.cnt, l.off, (int)F, l.wave);
   if constexpr (!CLAIM) {
     for (uint32_t d = t; d < F; d += NTH) {
@@ -721,23 +754,36 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
   }
   // Staging: every position first, then every write (one batch of LDS reads
   // and one of writes; interleaved, each write waited for its own read).
-  uint32_t pos[IPT];
+  if constexpr (EARLY) {
 #pragma unroll
-  for (int i = 0; i < IPT; ++i) {
-    const uint32_t idx = i * NTH + t;
-    if (FULL || idx < count) pos[i] = l.off[dr[i] >> 16] + (dr[i] & 0xFFFFu);
-  }
-#pragma unroll
-  for (int i = 0; i < IPT; ++i) {
-    const uint32_t idx = i * NTH + t;
-    if (FULL || idx < count) {
-      const uint32_t d = dr[i] >> 16;
-      l.val[pos[i]] = pol.stage(v[i], d);
-      if constexpr (Pol::kDigArray) l.dig[pos[i]] = (uint16_t)d;
+    for (int i = 0; i < IPT; ++i) {
+      const uint32_t idx = i * NTH + t;
+      if (FULL || idx < count) dr[i] += l.off[pol.stagedDigit(sw[i])];
     }
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const uint32_t idx = i * NTH + t;
+      if (FULL || idx < count) l.val[dr[i]] = sw[i];
+    }
+  } else {
+    uint32_t pos[IPT];
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const uint32_t idx = i * NTH + t;
+      if (FULL || idx < count) pos[i] = l.off[dr[i] >> 16] + (dr[i] & 0xFFFFu);
+    }
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const uint32_t idx = i * NTH + t;
+      if (FULL || idx < count) {
+        const uint32_t d = dr[i] >> 16;
+        l.val[pos[i]] = pol.stage(v[i], d);
+        if constexpr (Pol::kDigArray) l.dig[pos[i]] = (uint16_t)d;
+      }
+    }
+    // Prefetch the next tile while this one is streamed out.
+    prefetchTile<Pol, NTH, IPT>(in, base + TILE, end - 1, v);
   }
-  // Prefetch the next tile while this one is streamed out.
-  prefetchTile<Pol, NTH, IPT>(in, base + TILE, end - 1, v);
   if constexpr (CLAIM) {
 #pragma unroll
     for (int k = 0; k < MAXD; ++k) {  // padding entries get garbage bases nobody reads
@@ -921,10 +967,12 @@ static void launchNetClaimIpt(const Pol &pol, const data::Tuple *in, uint64_t n,
 }
 
 // Tile of the claim scatter (PartitionGeometry::ipt = KernelVariants::netIpt):
-// 8192 tuples by default; 16384 for 4-byte staged words (count-only
-// fragments leave LDS room for twice the run length per partition and tile;
-// measured on MI355X, 1B x 1B: 10.58 vs 10.78 ms per join); 15360 at 2048-way
-// (ipt 15): longer runs per partition and tile, one workgroup per CU.
+// 8192 tuples by default, with the early prefetch (earlyPrefetch: the next
+// tile's loads overlap the scan and staging).  ipt 16 = 16384-tuple tiles of
+// 4-byte staged words (longer runs per partition and tile, but too many
+// registers for the early prefetch: 1B x 1B 10.08 ms vs 9.56 with 8192 +
+// early prefetch, same box, profiles/r5/README.md); ipt 15 = 15360 at
+// 2048-way.
 template <class Pol>
 static void launchNetClaim(const Pol &pol, const data::Tuple *in, uint64_t n, uint32_t bits,
                            const PartitionGeometry &g, uint32_t blockBegin, uint32_t blockEnd, void *gcur,
@@ -934,7 +982,7 @@ static void launchNetClaim(const Pol &pol, const data::Tuple *in, uint64_t n, ui
   // one's rank/scan/claim phases overlap another's loads and stores.
   if (g.nth == 512) {
     if constexpr (sizeof(typename Pol::StageT) == 4) {
-      if (g.ipt == 0 || g.ipt == 16) {
+      if (g.ipt == 16) {
         launchNetClaimIpt<Pol, 16, 512>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
         return;
       }
@@ -944,7 +992,7 @@ static void launchNetClaim(const Pol &pol, const data::Tuple *in, uint64_t n, ui
     return;
   }
   if constexpr (sizeof(typename Pol::StageT) == 4) {
-    if (g.ipt == 0 || g.ipt == 16) {
+    if (g.ipt == 16) {
       launchNetClaimIpt<Pol, 16>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
       return;
     }
