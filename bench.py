@@ -457,7 +457,8 @@ def main():
             sh["wire_bytes_rank0"] = sres[-1]["wire_bytes"]
             sh["received_tuples_rank0"] = [sres[-1]["inner_received"], sres[-1]["outer_received"]]
             del sj
-            shuffle = {"data": "same relations as the headline, plan forced to the hash-partition shuffle", **sh}
+            shuffle = {"data": "same relations as the headline, plan forced to the hash-partition shuffle (the "
+                               "reference's N > 1 algorithm: the radix-join scaling curve)", **sh}
             ctx.reset_scratch()
         except Exception as e:  # noqa: BLE001
             shuffle = {"error": f"{type(e).__name__}: {e}"[:500], "correct": False}
@@ -522,6 +523,14 @@ def main():
                 "chunks": cfg.chunks,
                 "input": rel_loc,
             },
+            "value_note": ("N > 1: `value` is the planner's choice for this workload, replicated LDS bitmaps (one "
+                           "all-reduce of the inner key bitmap, each rank probes its own outer slice) -- not the "
+                           "reference's radix shuffle; `shuffle_path` is the same join through the hash-partition "
+                           "shuffle (the radix-join scaling curve) and `general_path` the random 63-bit key join"
+                           if info.world > 1 and plan.bitmap_replicated else
+                           "N = 1: single-level LDS bitmap join over the claim-scatter partitions (no exchange); "
+                           "`general_path` is the two-level radix hash join on random 63-bit keys"
+                           if plan.bitmap_join else "two-level radix hash join"),
             "first_join_ms": head["first_join_ms"],
             "setup_ms": head["setup_ms"],
             "plan_ms": head["plan_ms"],
