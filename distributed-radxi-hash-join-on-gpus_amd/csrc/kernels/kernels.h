@@ -419,6 +419,12 @@ void bpKeyCountedSpans(const BPArgs &a, uint32_t *queue, hipStream_t s);
 // Compacts the partitions bpPlanCounts listed in a.dedupParts (see BPArgs)
 // and appends their counted spans; run before bpKeyCountedSpans.
 void bpKeyDedup(const BPArgs &a, uint32_t maxParts, bool emitOnly, hipStream_t s);
+// After bpKeyDedup (not on an emitOnly re-run): one workgroup per partition
+// of several segments moves the segments' compacted lists together (in
+// place, in segment order) and emits the partition's counted spans over the
+// merged list -- ceil(distinct / rChunk) passes over its outer side instead
+// of one per segment.
+void bpKeyDedupMerge(const BPArgs &a, uint32_t maxParts, hipStream_t s);
 // Segments per compacted partition (bpKeyDedup): BPArgs::dedupLen has P of
 // them; a partition of n words has min(16, ceil(n / BP_DEDUP_SEG_MIN)).
 constexpr uint32_t BP_DEDUP_SEGS = 16;

@@ -840,12 +840,14 @@ __global__ __launch_bounds__(T) void bpKeyDedupKernel(KsSrc<T, K, true> R, uint3
       __syncthreads();
       if (ctl[0] > KD_FLUSH || b0 + BATCH >= nr) flush();
     }
-    // ---- the segment's counted spans over its compacted words
+    // ---- the segment's counted spans over its compacted words (a partition
+    // of several segments: bpKeyDedupMergeKernel merges the lists and emits;
+    // on a re-emit its merged list is segment 0's, the others are empty)
     const uint64_t nd = ctl[1];
     if (t == 0 && !emitOnly) lenBySeg[li] = nd;
     const uint64_t ns = uniform64(partSEnd[p]) - uniform64(partS[p]);
     const uint32_t nsc = (uint32_t)ceilDiv(ns, sc);
-    const uint32_t c = (uint32_t)(ceilDiv(nd, rc) * nsc);
+    const uint32_t c = (nseg > 1 && !emitOnly) ? 0u : (uint32_t)(ceilDiv(nd, rc) * nsc);
     if (t == 0) ctl[2] = c ? atomicAdd(spanCount, c) : 0u;
     __syncthreads();
     const uint32_t o = ctl[2];
@@ -878,6 +880,98 @@ void bpKeyDedup(const BPArgs &a, uint32_t maxParts, bool emitOnly, hipStream_t s
                      a.dedupParts, a.dedupCount, maxParts, a.dedupBig, a.dedupBigCount, a.partR, a.partREnd ? a.partREnd : a.partR + 1, a.partS,
                      a.partSEnd ? a.partSEnd : a.partS + 1, a.rChunk, a.sChunk, a.heavySpans, a.heavyCount,
                      a.heavyCapacity, a.dedupLen, emitOnly);
+  HIP_CHECK_LAUNCH();
+}
+
+// Merge of a multi-segment partition's compacted lists (see bpKeyDedupMerge
+// in kernels.h).  Segment g's list (lenBySeg words at the segment's start)
+// moves to the end of the lists before it; a destination never reaches past
+// its own source (a list is no longer than its segment), so copying the
+// segments in order, each in register-staged batches with a barrier between
+// the batch's loads and stores, never overwrites a word still to be read.
+template <int T, int K>
+__global__ __launch_bounds__(T) void bpKeyDedupMergeKernel(
+    uint32_t *__restrict__ rlo, uint16_t *__restrict__ rhi, uint32_t *__restrict__ rCounts,
+    const uint32_t *__restrict__ big, const uint32_t *__restrict__ nBigPtr, uint32_t maxParts,
+    const uint64_t *__restrict__ partR, const uint64_t *__restrict__ partREnd, const uint64_t *__restrict__ partS,
+    const uint64_t *__restrict__ partSEnd, uint32_t rc, uint32_t sc, BPSpan *__restrict__ spans,
+    uint32_t *__restrict__ spanCount, uint32_t spanCapacity, uint64_t *__restrict__ lenBySeg) {
+  __shared__ uint32_t spanBase;
+  constexpr uint32_t BATCH = T * K;
+  const uint32_t t = threadIdx.x;
+  const uint32_t nb = min(*nBigPtr, maxParts);
+  for (uint32_t w = blockIdx.x; w < nb; w += gridDim.x) {
+    const uint32_t p = big[w];
+    const uint64_t pb = uniform64(partR[p]);
+    const uint64_t pn = uniform64(partREnd[p]) - pb;
+    const uint64_t nseg = min<uint64_t>(BP_DEDUP_SEGS, ceilDiv(pn, KD_SEG_MIN));
+    const uint64_t len = ceilDiv(pn, nseg);
+    uint64_t out = uniform64(lenBySeg[(size_t)p * BP_DEDUP_SEGS]);  // segment 0 stays where it is
+    for (uint32_t g = 1; g < nseg; ++g) {
+      const uint64_t L = uniform64(lenBySeg[(size_t)p * BP_DEDUP_SEGS + g]);
+      const uint64_t src = pb + g * len, dst = pb + out;
+      for (uint64_t i0 = 0; i0 < L; i0 += BATCH) {
+        uint32_t lo[K], ct[K];
+        uint16_t hi[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const uint64_t i = i0 + (uint64_t)(k * T + t);
+          if (i < L) {
+            lo[k] = rlo[src + i];
+            hi[k] = rhi[src + i];
+            ct[k] = rCounts[src + i];
+          }
+        }
+        __syncthreads();  // the batch is read before any of it is overwritten
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const uint64_t i = i0 + (uint64_t)(k * T + t);
+          if (i < L) {
+            rlo[dst + i] = lo[k];
+            rhi[dst + i] = hi[k];
+            rCounts[dst + i] = ct[k];
+          }
+        }
+        __syncthreads();
+      }
+      out += L;
+    }
+    if (t == 0) {  // a re-emit (bpKeyDedup emitOnly) then emits the merged list as segment 0's
+      lenBySeg[(size_t)p * BP_DEDUP_SEGS] = out;
+      for (uint32_t g = 1; g < BP_DEDUP_SEGS; ++g) lenBySeg[(size_t)p * BP_DEDUP_SEGS + g] = 0;
+    }
+    const uint64_t ns = uniform64(partSEnd[p]) - uniform64(partS[p]);
+    const uint32_t nsc = (uint32_t)ceilDiv(ns, sc);
+    const uint32_t c = (uint32_t)(ceilDiv(out, rc) * nsc);
+    if (t == 0) spanBase = c ? atomicAdd(spanCount, c) : 0u;
+    __syncthreads();
+    const uint32_t o = spanBase;
+    for (uint32_t i = t; i < c; i += T) {
+      if (o + i >= spanCapacity) break;
+      BPSpan sp;
+      sp.rb = pb + (uint64_t)(i / nsc) * rc;
+      sp.sb = partS[p] + (uint64_t)(i % nsc) * sc;
+      sp.nr = (uint32_t)min(out - (uint64_t)(i / nsc) * rc, (uint64_t)rc);
+      sp.ns = (uint32_t)min(ns - (uint64_t)(i % nsc) * sc, (uint64_t)sc);
+      sp.flags = 1;
+      sp.pad1 = 0;
+      spans[o + i] = sp;
+    }
+    __syncthreads();
+  }
+}
+
+void bpKeyDedupMerge(const BPArgs &a, uint32_t maxParts, hipStream_t st) {
+  constexpr int T = 512, K = 4;
+  if (maxParts == 0) return;
+  HJ_CHECK(a.split && a.dedupCounts && a.dedupLen && a.dedupBig && a.dedupBigCount && a.heavySpans && a.heavyCount,
+           "bpKeyDedupMerge: needs split key-only words, the big-partition list, the count column and the span list");
+  const dim3 grid(std::min<uint32_t>(maxParts, 256 * 4));
+  hipLaunchKernelGGL((bpKeyDedupMergeKernel<T, K>), grid, dim3(T), 0, st,
+                     static_cast<uint32_t *>(const_cast<void *>(a.R)), const_cast<uint16_t *>(a.Rhi), a.dedupCounts,
+                     a.dedupBig, a.dedupBigCount, maxParts, a.partR, a.partREnd ? a.partREnd : a.partR + 1, a.partS,
+                     a.partSEnd ? a.partSEnd : a.partS + 1, a.rChunk, a.sChunk, a.heavySpans, a.heavyCount,
+                     a.heavyCapacity, a.dedupLen);
   HIP_CHECK_LAUNCH();
 }
 

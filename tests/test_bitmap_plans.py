@@ -316,7 +316,7 @@ def test_key_only_count_variants(C, variant):
         R.generate(inner, 0)
         S.generate(outer, 0)
         cfg = C.JoinConfig()
-        cfg.key_count = int(variant[0])
+        cfg.key_count = int(variant.rstrip("sw"))
         # 7: v2 span kernel; 8: quotient table (44-bit fragments: 63-bit keys
         # above 10 + 9 radix bits; unsplit words: v2); 9: counted tables
         # throughout; "s": over the split (u32 + u16) local output; "8w": 48-bit
@@ -332,6 +332,35 @@ def test_key_only_count_variants(C, variant):
         exp = ref_join_count(R.to_tensor()[:, 0].cpu(), S.to_tensor()[:, 0].cpu())
         for _ in range(2):
             assert j.run()["global_matches"] == exp, (variant, G_R, theta)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key_count", [8, 9])
+def test_key_only_multi_segment_compaction(C, key_count):
+    """Hot keys with hundreds of thousands of inner copies: their partitions
+    hold more than BP_DEDUP_SEG_MIN (32K) inner words, so bpKeyDedup compacts
+    them in several segments and bpKeyDedupMerge moves the segment lists
+    together before the counted spans; exact against a torch reference."""
+    from helpers import ref_join_count
+    ctx = C.ExecContext("device", 0, C.LocalCommunicator())
+    G_R, G_S = 3_000_017, 2_000_003
+    inner = C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=41, domain=20_000, zipf_theta=0.99)
+    inner.sparse64 = True
+    outer = C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=42, domain=20_000, zipf_theta=0.9)
+    outer.sparse64 = True
+    R = C.Relation(G_R, G_R, "device", 0)
+    S = C.Relation(G_S, G_S, "device", 0)
+    R.generate(inner, 0)
+    S.generate(outer, 0)
+    cfg = C.JoinConfig()
+    cfg.key_count = key_count
+    cfg.split_local = True
+    cfg.network_bits, cfg.local_bits = 10, 9  # 63-bit keys: 44-bit fragments (split words, quotient-eligible)
+    j = C.HashJoin(R, S, ctx, cfg)
+    assert j.plan.key_only and j.plan.split_local, j.plan
+    exp = ref_join_count(R.to_tensor()[:, 0].cpu(), S.to_tensor()[:, 0].cpu())
+    for _ in range(3):
+        assert j.run()["global_matches"] == exp, key_count
 
 
 @pytest.mark.gpu

@@ -9,6 +9,7 @@
 #   smoke               __graft_entry__.smoke()
 #   bench=ARGS          python bench.py ARGS        (ARGS: comma-separated, e.g. --general,only,--steps,10)
 #   skew=ARGS           python tools/bench_skew.py ARGS
+#   eskew=ENV/ARGS      tools/bench_skew.py ARGS with ENV (comma-separated K=V)
 #   sskew=ARGS          tools/bench_skew.py ARGS with HPCJOIN_SHARE_GPU=1 (--gpus N: N RCCL ranks on this GPU)
 #   py=SCRIPT,ARGS      python SCRIPT ARGS
 #   stats=ARGS          rocprofv3 --kernel-trace --stats of bench.py ARGS
@@ -48,6 +49,8 @@ for step in "$@"; do
     ebench) envs=${arg%%/*}; bargs=${arg#*/}
             timeout -k 10 600 env ${envs//,/ } python -u bench.py ${bargs//,/ } > "$log" 2>&1 ;;
     skew) timeout -k 10 900 python -u tools/bench_skew.py $args > "$log" 2>&1 ;;
+    eskew) envs=${arg%%/*}; sargs=${arg#*/}
+           timeout -k 10 900 env ${envs//,/ } python -u tools/bench_skew.py ${sargs//,/ } > "$log" 2>&1 ;;
     sskew) HPCJOIN_SHARE_GPU=1 timeout -k 10 900 python -u tools/bench_skew.py $args > "$log" 2>&1 ;;
     sweep) f=${arg%%/*}; rest=${arg#*/}; vals=${rest%%/*}; bargs=${rest#*/}; [ "$bargs" = "$rest" ] && bargs=""
            rc=0
