@@ -387,8 +387,13 @@ __device__ __forceinline__ uint32_t kq4ProbeBatch(const uint64_t (&pv)[K], uint3
 }
 
 // Counted table (bpKeyCountedSpansKernel): entry e = one distinct key,
-//   slot 0 = stored value, slot 1 = id << 16 | esc << 15,  count[e] apart,
-//   id = dist << 4 | tag,  dist = e - home bucket (linear probing).
+//   slot 0 = stored value, slot 1 = id << 16 | esc << 15 | displaced,  count[e] apart,
+//   id = dist << 4 | tag,  dist = e - home bucket (linear probing),
+//   displaced (bit 0, home entries only) = some key of this home sits further on.
+// A probe whose home entry holds another key walks only when that entry's
+// displaced bit is set: a key absent from the span (most probes of a sparse
+// outer side) stops at its home instead of walking to the next empty entry,
+// so few waves run the divergent walk loop.
 // (stored value, id, esc) at entry e names exactly one fragment, so a probe
 // never matches a key of another home.  Escape keys (v = the empty marker)
 // are stored inline with esc = 1 and stored value 0: e = ~salt(b) is implied
@@ -425,14 +430,15 @@ __device__ __forceinline__ uint64_t kqProbeCounted(const uint64_t (&pv)[K], uint
     const uint32_t esc = v[k] == KQ_EMPTY, vs = esc ? 0u : v[k];
     uint32_t c = 0, e = bk[k];
     bool walk = false;
-    if (x[k].x == vs && x[k].y == ((kqCountedId(0, tg[k]) << 16) | (esc << 15)))
+    if (x[k].x == vs && (x[k].y & ~1u) == ((kqCountedId(0, tg[k]) << 16) | (esc << 15)))
       c = cnt[e];
     else
-      walk = x[k].x != KQ_EMPTY;
+      walk = (x[k].y & 1u) != 0;  // (an empty entry has the bit set too: ~0)
+    walk = walk && x[k].x != KQ_EMPTY;
     for (uint32_t dist = 1; walk && dist < KC_E; ++dist) {
       e = kcNext(e);
       const uint2 y = tab2[e];
-      if (y.x == vs && y.y == ((kqCountedId(dist, tg[k]) << 16) | (esc << 15))) {
+      if (y.x == vs && (y.y & ~1u) == ((kqCountedId(dist, tg[k]) << 16) | (esc << 15))) {
         c = cnt[e];
         break;
       }
@@ -644,12 +650,15 @@ __global__ __launch_bounds__(T, MINW) void bpKeyCountedSpansKernel(KsSrc<T, K, t
       e = kcHome(e);
       const uint32_t esc = v == KQ_EMPTY, vs = esc ? 0u : v;
       // <= 2048 distinct keys in 6144 entries: an empty entry is always reached
+      const uint32_t home = e;
       for (uint32_t dist = 0; dist < KC_E; ++dist) {
         const uint32_t hi = (kqCountedId(dist, tg) << 16) | (esc << 15);
         const unsigned long long o = atomicCAS(&tab64[e], ~0ull, ((unsigned long long)hi << 32) | vs);
-        if (o == ~0ull || ((uint32_t)o == vs && (uint32_t)(o >> 32) == hi)) {
+        if (o == ~0ull || ((uint32_t)o == vs && ((uint32_t)(o >> 32) & ~1u) == hi)) {
           atomicAdd(&cnt[e], add);
           used[k] = e;
+          // the home is occupied (by another key) from here on: mark it
+          if (dist) atomicOr(&tab64[home], 1ull << 32);
           break;
         }
         e = kcNext(e);
