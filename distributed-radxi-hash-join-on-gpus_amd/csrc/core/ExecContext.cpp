@@ -219,6 +219,19 @@ void ExecContext::ipcExport(const void *p, uint64_t handle[8], uint64_t *offset,
   for (const auto &x : ipcExported_)
     if (x.base == base) hit = &x;
   const bool cached = hit != nullptr;
+  if (hit) {
+    // The tag must still be this export's: anything else is a write past
+    // the end of a workspace buffer (the tag is the allocation's tail).
+    uint64_t stamp[2] = {0, 0};
+    HIP_CHECK(hipSetDevice(device_));
+    HIP_CHECK(hipMemcpy(stamp, static_cast<const uint8_t *>(hit->base) + hit->tagOffset, sizeof(stamp),
+                        hipMemcpyDeviceToHost));
+    JOIN_ASSERT(stamp[0] == hit->nonce && stamp[1] == gen, "ExecContext",
+                "IPC export: the tag of allocation %p (generation %lu) was overwritten: nonce %016lx gen %lu, "
+                "expected %016lx gen %lu -- a write past the end of a workspace buffer",
+                hit->base, (unsigned long)gen, (unsigned long)stamp[0], (unsigned long)stamp[1],
+                (unsigned long)hit->nonce, (unsigned long)gen);
+  }
   if (!hit) {
     IpcExport x{base, gen, {}, 0, 0};
     HIP_CHECK(hipIpcGetMemHandle(&x.handle, base));
@@ -230,7 +243,11 @@ void ExecContext::ipcExport(const void *p, uint64_t handle[8], uint64_t *offset,
               (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
     const uint64_t stamp[2] = {x.nonce, gen};
     HIP_CHECK(hipSetDevice(device_));
-    HIP_CHECK(hipMemcpy(tag, stamp, sizeof(stamp), hipMemcpyHostToDevice));
+    // Complete before the handle is published: a synchronous hipMemcpy from
+    // pageable memory may return once the source is staged, before the DMA
+    // lands (importers then read the previous tag: seen at 8 ranks).
+    HIP_CHECK(hipMemcpyAsync(tag, stamp, sizeof(stamp), hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
     ipcExported_.push_back(x);
     hit = &ipcExported_.back();
   }
@@ -277,10 +294,11 @@ void *ExecContext::ipcImport(uint32_t peer, const uint64_t handle[8], uint64_t g
   if (stamp[0] != nonce || stamp[1] != generation) {
     (void)hipIpcCloseMemHandle(ptr);
     JOIN_ASSERT(false, "ExecContext",
-                "stale IPC mapping: rank %u's handle (generation %lu) opened memory tagged by another export "
-                "(generation %lu) -- a mapping of a freed allocation at the same address is still open in this "
-                "process, so puts through it would be lost",
-                peer, (unsigned long)generation, (unsigned long)stamp[1]);
+                "stale IPC mapping: rank %u's handle (generation %lu, nonce %016lx) opened memory tagged by "
+                "another export (generation %lu, nonce %016lx) -- a mapping of a freed allocation at the same "
+                "address is still open in this process, so puts through it would be lost",
+                peer, (unsigned long)generation, (unsigned long)nonce, (unsigned long)stamp[1],
+                (unsigned long)stamp[0]);
   }
   ipcImported_.push_back(IpcMapping{peer, std::move(key), generation, ptr, nonce});
   return ptr;
