@@ -27,6 +27,7 @@ ExecContext::ExecContext(Location loc, int device, comm::Communicator *comm)
               comm_->name().c_str(), locationName(loc));
   utils::setDebugRank((int)comm_->rank());
   workspace_.reset(new memory::Arena(loc, device_));
+  windows_.reset(new memory::Arena(loc, device_));
   // Pinned on a device engine: host->device uploads and device->host result
   // copies through it are true DMA transfers that never block the host.
   staging_.reset(new memory::Arena(onDevice() ? Location::Pinned : Location::Host, device_));
@@ -117,6 +118,7 @@ ExecContext::~ExecContext() {
   timeline_.reset();
   workspace_.reset();
   staging_.reset();
+  windows_.reset();
   if (stream_) (void)hipStreamDestroy(stream_);
   if (commStream_) (void)hipStreamDestroy(commStream_);
   if (decodeStream_) (void)hipStreamDestroy(decodeStream_);
@@ -192,6 +194,7 @@ void ExecContext::zero(void *dev, uint64_t bytes, hipStream_t s) const {
 void ExecContext::resetScratch() {
   workspace_->reset();
   staging_->reset();
+  windows_->reset();
   eventsUsed_ = 0;
 }
 
@@ -208,12 +211,13 @@ void ExecContext::ipcExport(const void *p, uint64_t handle[8], uint64_t *offset,
                             uint64_t *tagOffset, uint64_t *nonce) {
   static_assert(sizeof(hipIpcMemHandle_t) == 64, "unexpected hipIpcMemHandle_t size");
   JOIN_ASSERT(onDevice(), "ExecContext", "IPC export of host memory");
-  void *base = workspace_->allocationOf(p);
+  memory::Arena *arena = windows_->allocationOf(p) ? windows_.get() : workspace_.get();
+  void *base = arena->allocationOf(p);
   JOIN_ASSERT(base != nullptr, "ExecContext", "IPC export: %p is not in the workspace", p);
-  const uint64_t gen = workspace_->generation();
+  const uint64_t gen = arena->generation();
   // Entries of older generations name freed allocations: drop them.
   ipcExported_.erase(std::remove_if(ipcExported_.begin(), ipcExported_.end(),
-                                    [&](const IpcExport &x) { return x.generation != gen; }),
+                                    [&](const IpcExport &x) { return x.arena == arena && x.generation != gen; }),
                      ipcExported_.end());
   const IpcExport *hit = nullptr;
   for (const auto &x : ipcExported_)
@@ -233,9 +237,9 @@ void ExecContext::ipcExport(const void *p, uint64_t handle[8], uint64_t *offset,
                 (unsigned long)hit->nonce, (unsigned long)gen);
   }
   if (!hit) {
-    IpcExport x{base, gen, {}, 0, 0};
+    IpcExport x{arena, base, gen, {}, 0, 0};
     HIP_CHECK(hipIpcGetMemHandle(&x.handle, base));
-    uint8_t *tag = static_cast<uint8_t *>(workspace_->tagOf(base));
+    uint8_t *tag = static_cast<uint8_t *>(arena->tagOf(base));
     JOIN_ASSERT(tag != nullptr, "ExecContext", "IPC export: allocation %p has no tag", base);
     x.tagOffset = (uint64_t)(tag - static_cast<uint8_t *>(base));
     // Unique per process and export: pid, a serial, and the clock.
@@ -254,7 +258,7 @@ void ExecContext::ipcExport(const void *p, uint64_t handle[8], uint64_t *offset,
   logIpc('E', cached, comm_ ? comm_->rank() : 0, gen, &hit->handle, base);
   std::memcpy(handle, &hit->handle, sizeof(hit->handle));
   *offset = (uint64_t)(static_cast<const uint8_t *>(p) - static_cast<const uint8_t *>(base));
-  *generation = workspace_->generation();
+  *generation = gen;
   *tagOffset = hit->tagOffset;
   *nonce = hit->nonce;
 }

@@ -47,6 +47,13 @@ class ExecContext {
   uint32_t numberOfNodes() const;
   memory::Arena &workspace() { return *workspace_; }  // data-side scratch (HBM or host), reset per join
   memory::Arena &staging() { return *staging_; }      // pinned host scratch for plans/results, reset per join
+  // Receive windows of one-sided exchanges (peers IPC-map them): rewound per
+  // join like the workspace but never freed before the context is -- a
+  // freed allocation's address can come back with the same IPC handle bytes,
+  // and the runtime then hands a peer's re-open its still-referenced mapping
+  // of the freed memory (see ipcExport).  Growth adds allocations at new
+  // addresses, so an exported handle always names live memory.
+  memory::Arena &windows() { return *windows_; }
   performance::Timeline &timeline() { return *timeline_; }  // sub-phase spans of the current join (.perf keys)
 
   void synchronize() const;                 // compute + comm streams
@@ -140,6 +147,7 @@ class ExecContext {
   hipStream_t decodeStream_ = nullptr;
   std::unique_ptr<memory::Arena> workspace_;
   std::unique_ptr<memory::Arena> staging_;
+  std::unique_ptr<memory::Arena> windows_;
   std::unique_ptr<performance::Timeline> timeline_;
   struct IpcMapping {
     uint32_t peer;
@@ -155,6 +163,7 @@ class ExecContext {
   // suspected cause of intermittent open failures ("invalid device pointer")
   // and one inexact one-sided join at 4 ranks.
   struct IpcExport {
+    const memory::Arena *arena;
     void *base;
     uint64_t generation;
     hipIpcMemHandle_t handle;

@@ -17,10 +17,10 @@ namespace hpcjoin {
 namespace data {
 
 Window::Window(const histograms::ExchangePlan &plan, histograms::GlobalHistogram *globalHistogram,
-               histograms::AssignmentMap *assignment, core::ExecContext *ctx, bool wide)
+               histograms::AssignmentMap *assignment, core::ExecContext *ctx, bool wide, bool ipcWindow)
     : plan(plan), globalHistogram(globalHistogram), assignment(assignment), ctx(ctx), wide(wide) {
   localWindowSize = plan.recvTotal;
-  data = ctx->workspace().get(localWindowSize * tupleBytes());
+  data = (ipcWindow ? ctx->windows() : ctx->workspace()).get(localWindowSize * tupleBytes());
   exchanged.assign(plan.chunks, false);
   createExchangeEvents();
 }

@@ -29,8 +29,10 @@ namespace data {
 
 class Window {
  public:
+  // ipcWindow: the receive buffer comes from ExecContext::windows() (a
+  // one-sided window that peers IPC-map) instead of the workspace.
   Window(const histograms::ExchangePlan &plan, histograms::GlobalHistogram *globalHistogram,
-         histograms::AssignmentMap *assignment, core::ExecContext *ctx, bool wide);
+         histograms::AssignmentMap *assignment, core::ExecContext *ctx, bool wide, bool ipcWindow = false);
   // Window of `capacityTuples` whose plan is filled in after the scatter
   // (sampled network passes: single-rank, no exchange; or N > 1, exchanged
   // with exchangeSegmented as the plan's chunks become known).

@@ -24,7 +24,8 @@ std::unique_ptr<data::Window> ExchangeStrategy::makeWindow(tasks::HistogramCompu
   const core::JoinPlan &plan = env.plan;
   std::unique_ptr<data::Window> w(new data::Window(
       (side == 0 ? hc.innerOffsetMap() : hc.outerOffsetMap())->getExchangePlan(),
-      side == 0 ? hc.innerGlobal() : hc.outerGlobal(), hc.assignmentMap(), env.ctx, plan.wide));
+      side == 0 ? hc.innerGlobal() : hc.outerGlobal(), hc.assignmentMap(), env.ctx, plan.wide,
+      plan.oneSided && env.ctx->onDevice() && !env.ctx->comm()->sharesAddressSpace()));
   if (plan.oneSided) w->enableOneSided();
   if (plan.wireBits[side]) {
     kernels::WireCodec c;
