@@ -1,6 +1,7 @@
 #include "JoinStrategies.h"
 
 #include "HashJoin.h"
+#include "../comm/Communicator.h"
 #include "../performance/Clock.h"
 #include "../performance/Measurements.h"
 #include "../performance/Timeline.h"
