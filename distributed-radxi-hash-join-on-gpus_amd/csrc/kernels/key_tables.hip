@@ -414,37 +414,48 @@ __device__ __forceinline__ uint32_t kcNext(uint32_t e) { return e + 1 == KC_E ? 
 template <int T, int K>
 __device__ __forceinline__ uint64_t kqProbeCounted(const uint64_t (&pv)[K], uint32_t valid, uint32_t s,
                                                    const uint2 *tab2, const uint32_t *cnt) {
-  uint32_t bk[K], v[K], tg[K];
+  // The home entry and its count are read together for every probe (the
+  // count is needed only on a hit, but reading it unconditionally keeps the
+  // probe branch-free and takes the dependent second LDS round trip off the
+  // common path); only lanes whose home is marked displaced walk, and a wave
+  // with none skips the walk on a scalar branch.
+  uint32_t bk[K], v[K], tg[K], cv[K];
   uint2 x[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     kqKey(pv[k], s, bk[k], v[k], tg[k]);
     bk[k] = kcHome(bk[k]);
     x[k] = tab2[bk[k]];
+    cv[k] = cnt[bk[k]];
   }
   uint64_t matches = 0;
+  bool walk[K];
+  bool any = false;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    // Home entry from the batched reads; the rare walk past occupied
-    // entries re-reads the table (x[] stays in registers, no indexing).
     const uint32_t esc = v[k] == KQ_EMPTY, vs = esc ? 0u : v[k];
-    uint32_t c = 0, e = bk[k];
-    bool walk = false;
-    if (x[k].x == vs && (x[k].y & ~1u) == ((kqCountedId(0, tg[k]) << 16) | (esc << 15)))
-      c = cnt[e];
-    else
-      walk = (x[k].y & 1u) != 0;  // (an empty entry has the bit set too: ~0)
-    walk = walk && x[k].x != KQ_EMPTY;
-    for (uint32_t dist = 1; walk && dist < KC_E; ++dist) {
-      e = kcNext(e);
-      const uint2 y = tab2[e];
-      if (y.x == vs && (y.y & ~1u) == ((kqCountedId(dist, tg[k]) << 16) | (esc << 15))) {
-        c = cnt[e];
-        break;
+    const bool hit = x[k].x == vs && (x[k].y & ~1u) == ((kqCountedId(0, tg[k]) << 16) | (esc << 15));
+    const bool counted = (uint32_t)(k * T) + threadIdx.x < valid;
+    matches += hit && counted ? cv[k] : 0u;
+    walk[k] = !hit && counted && (x[k].y & 1u) != 0 && x[k].x != KQ_EMPTY;  // (an empty entry has the bit set: ~0)
+    any |= walk[k];
+  }
+  if (__any(any)) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint32_t esc = v[k] == KQ_EMPTY, vs = esc ? 0u : v[k];
+      uint32_t e = bk[k];
+      bool w = walk[k];
+      for (uint32_t dist = 1; w && dist < KC_E; ++dist) {
+        e = kcNext(e);
+        const uint2 y = tab2[e];
+        if (y.x == vs && (y.y & ~1u) == ((kqCountedId(dist, tg[k]) << 16) | (esc << 15))) {
+          matches += cnt[e];
+          break;
+        }
+        w = y.x != KQ_EMPTY;
       }
-      walk = y.x != KQ_EMPTY;
     }
-    matches += (uint32_t)(k * T) + threadIdx.x < valid ? c : 0u;
   }
   return matches;
 }
