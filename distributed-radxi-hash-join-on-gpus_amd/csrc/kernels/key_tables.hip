@@ -660,19 +660,27 @@ __global__ __launch_bounds__(T, MINW) void bpKeyCountedSpansKernel(KsSrc<T, K, t
       kqKey(rv[k], s, e, v, tg);
       e = kcHome(e);
       const uint32_t esc = v == KQ_EMPTY, vs = esc ? 0u : v;
-      // <= 2048 distinct keys in 6144 entries: an empty entry is always reached
+      // <= 2048 distinct keys in 6144 entries: an empty entry is always reached.
+      // The home entry first, straight-line (most keys end there); a lane
+      // whose home holds another key walks on.
       const uint32_t home = e;
-      for (uint32_t dist = 0; dist < KC_E; ++dist) {
+      const uint32_t hi0 = (kqCountedId(0, tg) << 16) | (esc << 15);
+      const unsigned long long o0 = atomicCAS(&tab64[e], ~0ull, ((unsigned long long)hi0 << 32) | vs);
+      if (o0 == ~0ull || ((uint32_t)o0 == vs && ((uint32_t)(o0 >> 32) & ~1u) == hi0)) {
+        atomicAdd(&cnt[e], add);
+        used[k] = e;
+        continue;
+      }
+      for (uint32_t dist = 1; dist < KC_E; ++dist) {
+        e = kcNext(e);
         const uint32_t hi = (kqCountedId(dist, tg) << 16) | (esc << 15);
         const unsigned long long o = atomicCAS(&tab64[e], ~0ull, ((unsigned long long)hi << 32) | vs);
         if (o == ~0ull || ((uint32_t)o == vs && ((uint32_t)(o >> 32) & ~1u) == hi)) {
           atomicAdd(&cnt[e], add);
           used[k] = e;
-          // the home is occupied (by another key) from here on: mark it
-          if (dist) atomicOr(&tab64[home], 1ull << 32);
+          atomicOr(&tab64[home], 1ull << 32);  // the home holds another key: mark it displaced
           break;
         }
-        e = kcNext(e);
       }
     }
     __syncthreads();
