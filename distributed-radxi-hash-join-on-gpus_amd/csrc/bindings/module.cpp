@@ -288,6 +288,41 @@ uint64_t opNpjCount(const at::Tensor &R, const at::Tensor &S) {
   return (uint64_t)res.cpu()[0].item<int64_t>();
 }
 
+// (inner rid, outer rid) pairs of the no-partitioning join, [matches, 2] int64
+// on the inputs' device: count pass, exact allocation, materializing pass.
+at::Tensor opNpjJoin(const at::Tensor &R, const at::Tensor &S) {
+  checkTuples(R, "R");
+  checkTuples(S, "S");
+  setDevice(R);
+  if (!R.is_cuda()) {
+    const auto v = host::npjPairs(ptr<data::Tuple>(R), R.size(0), ptr<data::Tuple>(S), S.size(0));
+    at::Tensor out = at::empty({(int64_t)v.size(), 2}, like(R));
+    int64_t *o = out.data_ptr<int64_t>();
+    for (size_t i = 0; i < v.size(); ++i) {
+      o[2 * i] = (int64_t)v[i].first;
+      o[2 * i + 1] = (int64_t)v[i].second;
+    }
+    return out;
+  }
+  const uint64_t slots = kernels::npjTableSlots(R.size(0));
+  at::Tensor table = at::empty({(int64_t)slots}, like(R));
+  at::Tensor rids = at::empty({(int64_t)slots}, like(R));
+  at::Tensor res = at::zeros({2}, like(R));
+  kernels::npjBuildRids(ptr<data::Tuple>(R), R.size(0), ptr<unsigned long long>(table), ptr<unsigned long long>(rids),
+                        slots, nullptr);
+  kernels::npjProbe(ptr<data::Tuple>(S), S.size(0), ptr<unsigned long long>(table), slots,
+                    ptr<unsigned long long>(res), nullptr);
+  HIP_CHECK(hipDeviceSynchronize());
+  const int64_t m = res.cpu()[0].item<int64_t>();
+  at::Tensor out = at::empty({m, 2}, like(R));
+  kernels::npjProbePairs(ptr<data::Tuple>(S), S.size(0), ptr<unsigned long long>(table),
+                         ptr<unsigned long long>(rids), slots, reinterpret_cast<ulonglong2 *>(out.data_ptr()),
+                         (uint64_t)m, ptr<unsigned long long>(res) + 1, nullptr);
+  HIP_CHECK(hipDeviceSynchronize());
+  TORCH_CHECK(res.cpu()[1].item<int64_t>() == m, "npj_join: the materializing pass found another match count");
+  return out;
+}
+
 at::Tensor opNetScatterGlobalAtomic(const at::Tensor &tuples, int64_t bits, int64_t keyShift,
                                     const at::Tensor &partBegin) {
   checkTuples(tuples, "tuples");
@@ -1232,6 +1267,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       },
       py::arg("n"), py::arg("rid_offset"), py::arg("seed"), py::arg("device") = "cpu");
   ops.def("npj_count", &opNpjCount);
+  ops.def("npj_join", &opNpjJoin, py::arg("R"), py::arg("S"),
+          "(inner rid, outer rid) pairs of the no-partitioning hash join, [matches, 2] int64");
   ops.def("wire_pack", &opWirePack, py::arg("raw"), py::arg("w"), py::arg("rid_bits"), py::arg("key_shift"),
           py::arg("segments"));
   ops.def("wire_unpack", &opWireUnpack, py::arg("wire"), py::arg("raw"), py::arg("w"), py::arg("rid_bits"),

@@ -255,6 +255,20 @@ uint64_t npjJoin(const data::Tuple *R, uint64_t nR, const data::Tuple *S, uint64
   return m;
 }
 
+std::vector<std::pair<uint64_t, uint64_t>> npjPairs(const data::Tuple *R, uint64_t nR, const data::Tuple *S,
+                                                    uint64_t nS) {
+  std::unordered_map<uint64_t, std::vector<uint64_t>> rids;
+  rids.reserve(nR * 2);
+  for (uint64_t i = 0; i < nR; ++i) rids[R[i].key].push_back(R[i].rid);
+  std::vector<std::pair<uint64_t, uint64_t>> out;
+  for (uint64_t i = 0; i < nS; ++i) {
+    auto it = rids.find(S[i].key);
+    if (it == rids.end()) continue;
+    for (uint64_t r : it->second) out.emplace_back(r, S[i].rid);
+  }
+  return out;
+}
+
 // Wire codec twins: a plain bit-stream writer/reader over each segment's
 // groups of 64 (independent of the device's per-lane word assembly).
 void wirePack(const uint64_t *raw, uint64_t *wire, const kernels::WireSeg *segs, uint32_t nSegs,

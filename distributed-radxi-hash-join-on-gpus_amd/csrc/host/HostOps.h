@@ -8,6 +8,7 @@
 #pragma once
 
 #include <cstdint>
+#include <utility>
 #include <vector>
 
 #include "../kernels/kernels.h"
@@ -47,6 +48,9 @@ void wireUnpack(const uint64_t *wire, uint64_t *raw, const kernels::WireSeg *seg
                 const kernels::WireCodec &c);
 
 uint64_t npjJoin(const data::Tuple *R, uint64_t nR, const data::Tuple *S, uint64_t nS);
+// (inner rid, outer rid) of every match, outer order, inner copies in input order.
+std::vector<std::pair<uint64_t, uint64_t>> npjPairs(const data::Tuple *R, uint64_t nR, const data::Tuple *S,
+                                                    uint64_t nS);
 
 }  // namespace host
 }  // namespace hpcjoin

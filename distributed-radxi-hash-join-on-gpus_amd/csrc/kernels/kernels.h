@@ -635,6 +635,18 @@ uint64_t npjTableSlots(uint64_t innerSize);
 void npjBuild(const data::Tuple *R, uint64_t nR, unsigned long long *table, uint64_t slots, hipStream_t s);
 void npjProbe(const data::Tuple *S, uint64_t nS, const unsigned long long *table, uint64_t slots,
               unsigned long long *result, hipStream_t s);
+// Materializing NPJ (the reference's simple_hash_join writes (rid, rid)
+// pairs through a global cursor, small_data_optimized.cu:1731-1823): the
+// build also stores each inner tuple's rid next to its key slot (rids[slots]);
+// the probe gives every outer tuple with m matches one cursor claim of m
+// and writes (inner rid, outer rid) pairs at out[claim..) while they fit
+// `capacity` (the cursor still counts all matches: a caller that sized out
+// from npjProbe's count never overflows).
+void npjBuildRids(const data::Tuple *R, uint64_t nR, unsigned long long *table, unsigned long long *rids,
+                  uint64_t slots, hipStream_t s);
+void npjProbePairs(const data::Tuple *S, uint64_t nS, const unsigned long long *table,
+                   const unsigned long long *rids, uint64_t slots, ulonglong2 *out, uint64_t capacity,
+                   unsigned long long *cursor, hipStream_t s);
 
 // ---------------------------------------------------------- micro-benchmarks
 // Plan-time repeated-key probe (microbench.hip): S evenly spaced keys of

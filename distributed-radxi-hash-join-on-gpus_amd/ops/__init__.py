@@ -63,6 +63,11 @@ def npj_count(R: torch.Tensor, S: torch.Tensor) -> int:
     return _C().ops.npj_count(R.contiguous(), S.contiguous())
 
 
+def npj_join(R: torch.Tensor, S: torch.Tensor) -> torch.Tensor:
+    """(inner rid, outer rid) pairs of the no-partitioning hash join, [matches, 2] int64."""
+    return _C().ops.npj_join(R.contiguous(), S.contiguous())
+
+
 def _engine(inner: torch.Tensor, outer: torch.Tensor, config=None):
     C = _C()
     on_dev = inner.is_cuda

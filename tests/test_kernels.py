@@ -161,6 +161,23 @@ def test_npj_count(C, dev):
     assert C.ops.npj_count(R, S) == 150_000
 
 
+@pytest.mark.parametrize("dev", devices())
+def test_npj_join_pairs(C, dev):
+    """Materializing NPJ (duplicate inner keys: every copy pairs with every
+    outer match) against the torch pair oracle."""
+    from hpcjoin.models.npj import NoPartitionJoin
+    from hpcjoin.utils import join_pairs_reference
+    R = gen(C, 5_000, device=dev, seed=3, dist="ZIPF", domain=3_000)
+    S = gen(C, 8_000, device=dev, seed=4, dist="ZIPF", domain=4_000)
+    npj = NoPartitionJoin()
+    pairs = npj.join(R, S).cpu()
+    assert pairs.shape[0] == npj.count(R, S) > 0
+    ref = join_pairs_reference(R.cpu(), S.cpu())
+    got = pairs[torch.argsort(pairs[:, 0] * (1 << 32) + pairs[:, 1])]
+    assert torch.equal(got, ref)
+    assert npj.timings["join_ms"] > 0 and npj.throughput(R, S) > 0
+
+
 @pytest.mark.gpu
 def test_global_atomic_scatter_ablation(C, cuda):
     t = gen(C, 200_000, device="cuda")
