@@ -90,8 +90,9 @@ def build(jobs: int | None = None, verbose: bool = False, with_cli: bool = True)
     py_inc = sysconfig.get_paths()["include"]
     common_defs = [f"-D_GLIBCXX_USE_CXX11_ABI={abi}"]
     jobs_list = []
+    extra = os.environ.get("HPCJOIN_EXTRA_HIPFLAGS", "").split()  # profiling builds (e.g. -DHPCJOIN_SCATTER_PROF)
     for s in kernels:
-        f = HIP_FLAGS + common_defs
+        f = HIP_FLAGS + common_defs + extra
         jobs_list.append((s, [HIPCC, *f, "-c", str(s)], f))
     for s in core:
         f = CXX_FLAGS + common_defs

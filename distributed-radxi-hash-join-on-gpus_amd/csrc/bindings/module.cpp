@@ -1267,6 +1267,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       },
       py::arg("n"), py::arg("rid_offset"), py::arg("seed"), py::arg("device") = "cpu");
   ops.def("npj_count", &opNpjCount);
+  ops.def("scatter_profile", [](bool reset) {
+    unsigned long long v[10];
+    kernels::scatterProfile(v, reset);
+    return std::vector<unsigned long long>(v, v + 10);
+  }, py::arg("reset") = true,
+          "Claim-scatter shader-clock sums per phase (rank, barrier A, claims+prefetch, scan, staging, write bases, "
+          "barrier B, write-out), tiles, ranges; zeros unless built with -DHPCJOIN_SCATTER_PROF");
+  ops.def("scatter_profile_built", &kernels::scatterProfileBuilt);
   ops.def("npj_join", &opNpjJoin, py::arg("R"), py::arg("S"),
           "(inner rid, outer rid) pairs of the no-partitioning hash join, [matches, 2] int64");
   ops.def("wire_pack", &opWirePack, py::arg("raw"), py::arg("w"), py::arg("rid_bits"), py::arg("key_shift"),

@@ -630,6 +630,12 @@ void scanExclusiveU32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *t
 void scanExclusiveU32to64(const uint32_t *in, unsigned long long *out, uint64_t n, unsigned long long *total,
                           void *workspace, hipStream_t s);
 
+// Claim-scatter phase profile (partition.hip, built with
+// -DHPCJOIN_SCATTER_PROF): shader-clock sums per tile phase [8], tiles [8],
+// ranges [9]; all zero in a normal build.
+void scatterProfile(unsigned long long out[10], bool reset);
+bool scatterProfileBuilt();
+
 // --------------------------------------------------- no-partitioning join
 uint64_t npjTableSlots(uint64_t innerSize);
 void npjBuild(const data::Tuple *R, uint64_t nR, unsigned long long *table, uint64_t slots, hipStream_t s);

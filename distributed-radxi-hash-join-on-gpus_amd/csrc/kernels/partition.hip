@@ -624,6 +624,39 @@ struct ScatterSmem {
 // must land -- and it serialises the write-out's LDS reads element by element.
 __device__ ulonglong2 g_scatterTrash[1024];
 
+// Per-phase shader-clock breakdown of the claim scatter's tile loop, built
+// only with -DHPCJOIN_SCATTER_PROF (HPCJOIN_EXTRA_HIPFLAGS at build time;
+// tools/scatter_phases.py reads it through ops.scatter_profile()).  Wave 0
+// of every workgroup stamps s_memtime at the phase boundaries; the sums of
+// the per-phase deltas (scalar registers) are added to g_scatterProf once per
+// range, by lane 0, with vector atomics.
+//   0 rank (includes waiting for the tile's loads)  1 barrier A
+//   2 claims + prefetch issue  3 scan  4 staging  5 write bases (claims land)
+//   6 barrier B  7 write-out issue
+__device__ unsigned long long g_scatterProf[10];
+struct ScatterProf {
+#ifdef HPCJOIN_SCATTER_PROF
+  uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t last = 0, tiles = 0;
+  __device__ __forceinline__ void start() { last = __builtin_readcyclecounter(); }
+  __device__ __forceinline__ void mark(int i) {
+    const uint64_t now = __builtin_readcyclecounter();
+    acc[i] += now - last;
+    last = now;
+  }
+  __device__ __forceinline__ void flush() {
+    if (threadIdx.x != 0) return;
+    for (int i = 0; i < 8; ++i) atomicAdd(&g_scatterProf[i], (unsigned long long)acc[i]);
+    atomicAdd(&g_scatterProf[8], (unsigned long long)tiles);
+    atomicAdd(&g_scatterProf[9], 1ull);
+  }
+#else
+  __device__ __forceinline__ void start() {}
+  __device__ __forceinline__ void mark(int) {}
+  __device__ __forceinline__ void flush() {}
+#endif
+};
+
 template <class P, class = void>
 struct TwoArrayStore : std::false_type {};
 template <class P>
@@ -702,8 +735,10 @@ template <class Pol, typename CurT, int NTH, int IPT, int MODE, bool FULL, bool 
 __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict__ in, uint64_t base, uint64_t end,
                                             uint32_t count, uint32_t F, const ScatterSmem<Pol, CurT, NTH * IPT> &l,
                                             const Pol &pol, typename Pol::OutT *__restrict__ out,
-                                            typename Pol::LoadT (&v)[IPT], CurT *__restrict__ gcur) {
+                                            typename Pol::LoadT (&v)[IPT], CurT *__restrict__ gcur,
+                                            ScatterProf &pf) {
   constexpr uint32_t TILE = NTH * IPT;
+  pf.start();
   constexpr bool EARLY = earlyPrefetch<Pol, IPT>();
   const uint32_t t = threadIdx.x;
   // EARLY: sw = staged words, dr = ranks (then positions); else dr = digit << 16 | rank.
@@ -722,11 +757,13 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
       }
     }
   }
+  pf.mark(0);
   // Barriers of the tile loop order LDS only (ldsBarrier): the waves share
   // nothing through global memory here, and a full __syncthreads() would make
   // every wave wait for its prefetch of the next tile (vmcnt(0)) before the
   // write-out, so loads and stores of a workgroup would never overlap.
   ldsBarrier();  // A: counts final; previous tile's write-out done
+  pf.mark(1);
   CurT claim[MAXD];
   if constexpr (CLAIM) {
     // One device atomic per digit claims this tile's run in the group's slice,
@@ -743,7 +780,9 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
     }
   }
   if constexpr (EARLY) prefetchTile<Pol, NTH, IPT>(in, base + TILE, end - 1, v);
+  pf.mark(2);
   blockExclusiveScanLds<NTH, uint32_t, uint32_t, true>(l.cnt, l.off, (int)F, l.wave);
+  pf.mark(3);
   if constexpr (!CLAIM) {
     for (uint32_t d = t; d < F; d += NTH) {
       const CurT c = l.cursor[d];
@@ -784,6 +823,7 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
     // Prefetch the next tile while this one is streamed out.
     prefetchTile<Pol, NTH, IPT>(in, base + TILE, end - 1, v);
   }
+  pf.mark(4);
   if constexpr (CLAIM) {
 #pragma unroll
     for (int k = 0; k < MAXD; ++k) {  // padding entries get garbage bases nobody reads
@@ -792,7 +832,9 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
       l.cnt[d] = 0;
     }
   }
+  pf.mark(5);
   ldsBarrier();  // B: staged tile and write bases visible
+  pf.mark(6);
 #pragma unroll
   for (int i = 0; i < IPT; ++i) {
     const uint32_t idx = i * NTH + t;
@@ -817,6 +859,10 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
       asm volatile("" ::"v"(y), "v"(l.wbase[d]));
     }
   }
+  pf.mark(7);
+#ifdef HPCJOIN_SCATTER_PROF
+  ++pf.tiles;
+#endif
 }
 
 // Scatter [begin, end) of `in` into `out` at the cursors held in LDS
@@ -832,15 +878,17 @@ __device__ __forceinline__ void scatterRange(const typename Pol::InT *__restrict
   constexpr uint32_t TILE = NTH * IPT;
   const ScatterSmem<Pol, CurT, TILE> l(smem, F);
   typename Pol::LoadT v[IPT];
+  ScatterProf pf;
   if (begin < end) prefetchTile<Pol, NTH, IPT>(in, begin, end - 1, v);
   for (uint64_t base = begin; base < end; base += TILE) {
     if (base + TILE <= end)
       scatterTile<Pol, CurT, NTH, IPT, MODE, true, CLAIM, BOUNDED, MAXD>(in, base, end, TILE, F, l, pol, out, v,
-                                                                         gcur);
+                                                                         gcur, pf);
     else
       scatterTile<Pol, CurT, NTH, IPT, MODE, false, CLAIM, BOUNDED, MAXD>(in, base, end, (uint32_t)(end - base), F, l,
-                                                                          pol, out, v, gcur);
+                                                                          pol, out, v, gcur, pf);
   }
+  pf.flush();
   __syncthreads();
 }
 
@@ -1001,6 +1049,23 @@ static void launchNetClaim(const Pol &pol, const data::Tuple *in, uint64_t n, ui
     launchNetClaimIpt<Pol, 15>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
   else
     launchNetClaimIpt<Pol, CL_IPT_DEFAULT>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
+}
+
+void scatterProfile(unsigned long long out[10], bool reset) {
+  HIP_CHECK(hipDeviceSynchronize());
+  HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_scatterProf), 10 * sizeof(unsigned long long)));
+  if (reset) {
+    const unsigned long long z[10] = {};
+    HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_scatterProf), z, sizeof(z)));
+  }
+}
+
+bool scatterProfileBuilt() {
+#ifdef HPCJOIN_SCATTER_PROF
+  return true;
+#else
+  return false;
+#endif
 }
 
 void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift, const PartitionGeometry &g,

@@ -11,6 +11,7 @@
 #   skew=ARGS           python tools/bench_skew.py ARGS
 #   eskew=ENV/ARGS      tools/bench_skew.py ARGS with ENV (comma-separated K=V)
 #   sskew=ARGS          tools/bench_skew.py ARGS with HPCJOIN_SHARE_GPU=1 (--gpus N: N RCCL ranks on this GPU)
+#   phases=ARGS        tools/scatter_phases.py of the phase-stamped build in ab/prof (tools/README.md)
 #   py=SCRIPT,ARGS      python SCRIPT ARGS
 #   stats=ARGS          rocprofv3 --kernel-trace --stats of bench.py ARGS
 #   pstats=SCRIPT,ARGS  rocprofv3 --kernel-trace --stats of python SCRIPT ARGS
@@ -51,6 +52,7 @@ for step in "$@"; do
     skew) timeout -k 10 900 python -u tools/bench_skew.py $args > "$log" 2>&1 ;;
     eskew) envs=${arg%%/*}; sargs=${arg#*/}
            timeout -k 10 900 env ${envs//,/ } python -u tools/bench_skew.py ${sargs//,/ } > "$log" 2>&1 ;;
+    phases) timeout -k 10 600 python -u ab/prof/tools/scatter_phases.py $args > "$log" 2>&1 ;;
     sskew) HPCJOIN_SHARE_GPU=1 timeout -k 10 900 python -u tools/bench_skew.py $args > "$log" 2>&1 ;;
     sweep) f=${arg%%/*}; rest=${arg#*/}; vals=${rest%%/*}; bargs=${rest#*/}; [ "$bargs" = "$rest" ] && bargs=""
            rc=0
