@@ -46,3 +46,4 @@ def test_bench_py_cpu_contract():
               "vs_baseline", "dtype", "data", "config"):
         assert k in j, k
     assert j["correct"] is True and j["n_gpus"] == 1 and j["steps"] == 2
+    assert "value_note" in j  # which plan `value` measures (N > 1: replicated bitmaps, not the shuffle)
