@@ -55,6 +55,14 @@ ExecContext::ExecContext(Location loc, int device, comm::Communicator *comm)
                             hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(mailboxHost_, 0, sizeof(kernels::ResultMailbox));
     HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void **>(&mailboxDev_), mailboxHost_, 0));
+    // Event pools filled now (a join uses ~6 timing and a few sync events):
+    // creating them lazily put ~0.1 ms of hipEventCreate into the first join.
+    timeline_->reserveEvents(32);
+    for (int i = 0; i < 32; ++i) {
+      hipEvent_t e;
+      HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      events_.push_back(e);
+    }
     warmRuntimeCopies();
   }
 }

@@ -23,6 +23,14 @@ hipEvent_t Timeline::event() {
   return pool_[used_++];
 }
 
+void Timeline::reserveEvents(size_t n) {
+  while (pool_.size() < n) {
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreate(&e));
+    pool_.push_back(e);
+  }
+}
+
 void Timeline::reset() {
   spans_.clear();
   used_ = 0;

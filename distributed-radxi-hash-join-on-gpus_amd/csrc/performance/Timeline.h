@@ -27,6 +27,9 @@ class Timeline {
   Timeline &operator=(const Timeline &) = delete;
 
   void reset();                                   // start of a join
+  // Create n timing events up front (engine start): a first join would
+  // otherwise pay each hipEventCreate inside its span.
+  void reserveEvents(size_t n);
   void begin(const char *key, hipStream_t s = nullptr);
   void end(const char *key, hipStream_t s = nullptr);  // closes the key's open span
   // One span charged to two keys in proportion wa : wb (a fused kernel doing
