@@ -78,7 +78,19 @@ void ExecContext::warmRuntimeCopies() {
   // tens of KiB): reserved now, so a first join does not pay a pinned
   // allocation (~ms) in the middle of its network phase.
   staging_->ensure(kStagingReserve);
+  // One timed span, queried and resolved the way a join's timeline is, so the
+  // runtime's first-use work for timing events (first record / query /
+  // elapsed-time) happens here and not around the first join.
+  hipEvent_t t0 = timeline_->mark(stream_), t1 = nullptr;
   kernels::zeroWords(control_, sizeof(kernels::DeviceControl) / 8, stream_);
+  t1 = timeline_->mark(stream_);
+  if (t1) utils::waitEvent(t1, comm_, "engine start");
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  {
+    float ms = 0;
+    if (t0 && t1) HIP_CHECK(hipEventElapsedTime(&ms, t0, t1));
+  }
+  timeline_->reset();
   const char *w = std::getenv("HPCJOIN_WARM_COPIES");
   if (w && w[0] == '0') {
     HIP_CHECK(hipStreamSynchronize(stream_));
