@@ -13,7 +13,9 @@
 #include "../comm/Communicator.h"
 #include "../kernels/kernels.h"
 #include "../memory/Arena.h"
+#include "../performance/Measurements.h"
 #include "../performance/Timeline.h"
+#include "../performance/Trace.h"
 #include "../utils/Fault.h"
 #include "../utils/Hip.h"
 
@@ -65,6 +67,11 @@ ExecContext::ExecContext(Location loc, int device, comm::Communicator *comm)
     }
     warmRuntimeCopies();
   }
+  // First uses that would otherwise land in the first join: the roctx
+  // library's lazy start (a join opens its range first thing) and the
+  // measurement key table (built on the first startJoin).
+  { performance::TraceRange warm("hpcjoin::engine_start"); }
+  (void)performance::Measurements::referenceKeys();
 }
 
 // The runtime loads its copy / fill kernels on first use: the first join of
