@@ -386,74 +386,73 @@ __device__ __forceinline__ uint32_t kq4ProbeBatch(const uint64_t (&pv)[K], uint3
   return matches;
 }
 
-// Counted table (bpKeyCountedSpansKernel): entry e = one distinct key,
-//   slot 0 = stored value, slot 1 = id << 16 | esc << 15 | displaced,  count[e] apart,
-//   id = dist << 4 | tag,  dist = e - home bucket (linear probing),
-//   displaced (bit 0, home entries only) = some key of this home sits further on.
-// A probe whose home entry holds another key walks only when that entry's
-// displaced bit is set: a key absent from the span (most probes of a sparse
-// outer side) stops at its home instead of walking to the next empty entry,
-// so few waves run the divergent walk loop.
-// (stored value, id, esc) at entry e names exactly one fragment, so a probe
-// never matches a key of another home.  Escape keys (v = the empty marker)
-// are stored inline with esc = 1 and stored value 0: e = ~salt(b) is implied
-// by the home bucket, so (home, tag) names them.  Claimed by one 64-bit CAS
-// of (value, id, esc) on an empty entry; every copy (the claimer included)
-// adds its count to count[e], a separate u32 array read only on a match.
-__device__ __forceinline__ uint32_t kqCountedId(uint32_t dist, uint32_t tag) { return (dist << 4) | tag; }
-
-// 6144 entries (load <= 1/3 at 2048 keys per span, 72 KiB with the counts:
-// two 1024-thread workgroups per CU): home bucket b of 4096 sits at entry
-// b + b / 2, and linear probing wraps at 6144.  At 4096 entries (load 1/2)
-// most waves walked several entries per probe.  dist < 2048 (at most 2048
-// keys), so id = dist << 4 | tag stays within 15 bits.
-constexpr uint32_t KC_E = 6144;
-__device__ __forceinline__ uint32_t kcHome(uint32_t b) { return b + (b >> 1); }
-__device__ __forceinline__ uint32_t kcNext(uint32_t e) { return e + 1 == KC_E ? 0u : e + 1; }
+// Counted table (bpKeyCountedSpansKernel): 3072 buckets of two 8-byte
+// entries (one 16-byte ds_read_b128 reads a bucket) and a u32 count per entry
+// apart (one ds_read_b64 per bucket).  Entry = one distinct key:
+//   lo = stored value v, hi = b << 20 | tag << 16 | ovf,
+// (b, v, tag) from kqKey, a bijection of the fragment, so an entry names its
+// key wherever it sits and never equals the empty word ~0 (hi bits 1-15 are
+// zero).  A key claims the first empty entry of its home bucket (64-bit CAS),
+// then walks the following buckets (linear probing over entries); a key that
+// leaves its home sets the home's ovf bit (entry 0 of a full bucket).  A probe
+// reads the home bucket and its counts together: a hit in either entry adds
+// the count; only lanes whose home bucket overflowed walk, behind a scalar
+// any().  At 2048 keys in 3072 buckets ~5 % of keys leave their home (the
+// round-5 layout, one entry per home at 4096 homes in 6144 entries, displaced
+// ~21 %, and every probe walk re-read one 8-byte entry per step).
+constexpr uint32_t KC_B = 3072;
+constexpr uint32_t KC_E = 2 * KC_B;
+__device__ __forceinline__ uint32_t kcBucket(uint64_t frag, uint32_t s) {
+  const uint32_t h = (uint32_t)(frag >> s) * 0x9E3779B1u ^ ((uint32_t)frag & ((1u << s) - 1u)) * 0x85EBCA77u;
+  return __umulhi(h ^ (h >> 15), KC_B);
+}
+__device__ __forceinline__ uint32_t kcHi(uint32_t b, uint32_t tag) { return (b << 20) | (tag << 16); }
+constexpr uint32_t KC_EMPTY_HI = 0xFFFFFFFFu;
 
 template <int T, int K>
 __device__ __forceinline__ uint64_t kqProbeCounted(const uint64_t (&pv)[K], uint32_t valid, uint32_t s,
-                                                   const uint2 *tab2, const uint32_t *cnt) {
-  // The home entry and its count are read together for every probe (the
-  // count is needed only on a hit, but reading it unconditionally keeps the
-  // probe branch-free and takes the dependent second LDS round trip off the
-  // common path); only lanes whose home is marked displaced walk, and a wave
-  // with none skips the walk on a scalar branch.
-  uint32_t bk[K], v[K], tg[K], cv[K];
-  uint2 x[K];
+                                                   const uint4 *tab4, const uint2 *cnt2) {
+  uint32_t hb[K], v[K], hk[K];
+  uint4 x[K];
+  uint2 c[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    kqKey(pv[k], s, bk[k], v[k], tg[k]);
-    bk[k] = kcHome(bk[k]);
-    x[k] = tab2[bk[k]];
-    cv[k] = cnt[bk[k]];
+    uint32_t b, tg;
+    kqKey(pv[k], s, b, v[k], tg);
+    hk[k] = kcHi(b, tg);
+    hb[k] = kcBucket(pv[k], s);
+    x[k] = tab4[hb[k]];
+    c[k] = cnt2[hb[k]];
   }
   uint64_t matches = 0;
   bool walk[K];
   bool any = false;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const uint32_t esc = v[k] == KQ_EMPTY, vs = esc ? 0u : v[k];
-    const bool hit = x[k].x == vs && (x[k].y & ~1u) == ((kqCountedId(0, tg[k]) << 16) | (esc << 15));
+    const bool h0 = x[k].x == v[k] && (x[k].y & ~1u) == hk[k];
+    const bool h1 = x[k].z == v[k] && x[k].w == hk[k];
     const bool counted = (uint32_t)(k * T) + threadIdx.x < valid;
-    matches += hit && counted ? cv[k] : 0u;
-    walk[k] = !hit && counted && (x[k].y & 1u) != 0 && x[k].x != KQ_EMPTY;  // (an empty entry has the bit set: ~0)
+    matches += counted ? (h0 ? c[k].x : h1 ? c[k].y : 0u) : 0u;
+    walk[k] = !h0 && !h1 && counted && (x[k].y & 1u) != 0 && x[k].y != KC_EMPTY_HI;
     any |= walk[k];
   }
   if (__any(any)) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const uint32_t esc = v[k] == KQ_EMPTY, vs = esc ? 0u : v[k];
-      uint32_t e = bk[k];
+      uint32_t b = hb[k];
       bool w = walk[k];
-      for (uint32_t dist = 1; w && dist < KC_E; ++dist) {
-        e = kcNext(e);
-        const uint2 y = tab2[e];
-        if (y.x == vs && (y.y & ~1u) == ((kqCountedId(dist, tg[k]) << 16) | (esc << 15))) {
-          matches += cnt[e];
+      for (uint32_t step = 1; w && step < KC_B; ++step) {
+        b = b + 1 == KC_B ? 0u : b + 1;
+        const uint4 y = tab4[b];
+        if (y.x == v[k] && (y.y & ~1u) == hk[k]) {
+          matches += cnt2[b].x;
           break;
         }
-        w = y.x != KQ_EMPTY;
+        if (y.z == v[k] && y.w == hk[k]) {
+          matches += cnt2[b].y;
+          break;
+        }
+        w = y.y != KC_EMPTY_HI && y.w != KC_EMPTY_HI;
       }
     }
   }
@@ -600,9 +599,9 @@ static void launchKeyQuotient(const BPArgs &a, const BPSpan *spans, const uint32
 // of a key.  Their spans (bpPlanCounts -> heavySpans, same rChunk x sChunk
 // tiling) are counted here on a *counted* table (see kqProbeCounted): one
 // entry per distinct key, so copies only add to a count.  A span's <= 2048
-// inner words fill at most half of the 4096 entries.  The table also carries
-// 45-48-bit fragments (the tag in the entry) and escape keys inline, so it
-// never needs a fallback: plans whose fragments the quotient table cannot
+// inner words fill at most a third of the 6144 entries.  The table also
+// carries 45-48-bit fragments (the tag in the entry) and every 32-bit stored
+// value (the empty word is not a key's), so it never needs a fallback: plans whose fragments the quotient table cannot
 // hold, and quotient spans that filled their overflow table, count here.  A
 // hot partition's spans spread over workgroups like any others.
 //
@@ -613,7 +612,8 @@ static void launchKeyQuotient(const BPArgs &a, const BPSpan *spans, const uint32
 // Structure as bpKeyQuotientKernel (T = 1024, K = 2): spans from a work queue
 // in chunks of KS_CHUNK, spans i + 1 and i + 2 in flight while span i builds
 // and probes, the span loop unrolled by three over fixed register sets.  The
-// table is 48 KiB; 1024-thread workgroups at <= 64 VGPRs put two on a CU.
+// table is 72 KiB with the counts; 1024-thread workgroups at <= 64 VGPRs put
+// two on a CU.
 template <int T, int K, int MINW>
 __global__ __launch_bounds__(T, MINW) void bpKeyCountedSpansKernel(KsSrc<T, K, true> R, KsSrc<T, K, true> S,
                                                                     const uint32_t *__restrict__ rCounts,
@@ -622,9 +622,10 @@ __global__ __launch_bounds__(T, MINW) void bpKeyCountedSpansKernel(KsSrc<T, K, t
                                                                     uint32_t capacity, uint32_t *__restrict__ queue,
                                                                     uint32_t s, unsigned long long *__restrict__ result) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned long long *tab64 = reinterpret_cast<unsigned long long *>(smem);  // [entry] value | id << 48 | esc << 47
-  const uint2 *tab2 = reinterpret_cast<const uint2 *>(smem);
-  uint32_t *cnt = reinterpret_cast<uint32_t *>(tab64 + KC_E);          // [entry] count
+  unsigned long long *tab64 = reinterpret_cast<unsigned long long *>(smem);  // [entry] value | hi << 32
+  const uint4 *tab4 = reinterpret_cast<const uint4 *>(smem);                 // [bucket]
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(tab64 + KC_E);                // [entry] count
+  const uint2 *cnt2 = reinterpret_cast<const uint2 *>(cnt);                 // [bucket]
   BPSpan *desc = reinterpret_cast<BPSpan *>(cnt + KC_E);
   unsigned long long *wsum = reinterpret_cast<unsigned long long *>(desc + KS_CHUNK);
   uint32_t *qbase = reinterpret_cast<uint32_t *>(wsum + T / WAVE);
@@ -656,45 +657,45 @@ __global__ __launch_bounds__(T, MINW) void bpKeyCountedSpansKernel(KsSrc<T, K, t
       if ((uint32_t)(k * T) + t >= nr) continue;
       uint32_t add = 1;
       if (compacted) add = rCounts[r0 + (uint32_t)(k * T) + t];
-      uint32_t e, v, tg;
-      kqKey(rv[k], s, e, v, tg);
-      e = kcHome(e);
-      const uint32_t esc = v == KQ_EMPTY, vs = esc ? 0u : v;
-      // <= 2048 distinct keys in 6144 entries: an empty entry is always reached.
-      // The home entry first, straight-line (most keys end there); a lane
-      // whose home holds another key walks on.
-      const uint32_t home = e;
-      const uint32_t hi0 = (kqCountedId(0, tg) << 16) | (esc << 15);
-      const unsigned long long o0 = atomicCAS(&tab64[e], ~0ull, ((unsigned long long)hi0 << 32) | vs);
-      if (o0 == ~0ull || ((uint32_t)o0 == vs && ((uint32_t)(o0 >> 32) & ~1u) == hi0)) {
-        atomicAdd(&cnt[e], add);
-        used[k] = e;
-        continue;
+      uint32_t b, v, tg;
+      kqKey(rv[k], s, b, v, tg);
+      const uint32_t hi = kcHi(b, tg);
+      const unsigned long long mine = ((unsigned long long)hi << 32) | v;
+      // <= 2048 distinct keys in 6144 entries: an empty entry is always
+      // reached.  The home bucket's two entries first, straight-line (~95 % of
+      // keys end there); a lane whose home is full walks on and marks it.
+      const uint32_t e0 = 2 * kcBucket(rv[k], s);
+      auto mineOrClaimed = [&](unsigned long long o) {
+        return o == ~0ull || ((uint32_t)o == v && ((uint32_t)(o >> 32) & ~1u) == hi);
+      };
+      uint32_t e = e0;
+      bool placed = mineOrClaimed(atomicCAS(&tab64[e], ~0ull, mine));
+      if (!placed) {
+        e = e0 + 1;
+        placed = mineOrClaimed(atomicCAS(&tab64[e], ~0ull, mine));
       }
-      for (uint32_t dist = 1; dist < KC_E; ++dist) {
-        e = kcNext(e);
-        const uint32_t hi = (kqCountedId(dist, tg) << 16) | (esc << 15);
-        const unsigned long long o = atomicCAS(&tab64[e], ~0ull, ((unsigned long long)hi << 32) | vs);
-        if (o == ~0ull || ((uint32_t)o == vs && ((uint32_t)(o >> 32) & ~1u) == hi)) {
-          atomicAdd(&cnt[e], add);
-          used[k] = e;
-          atomicOr(&tab64[home], 1ull << 32);  // the home holds another key: mark it displaced
-          break;
+      if (!placed) {
+        atomicOr(&tab64[e0], 1ull << 32);  // the home bucket is full: mark it overflowed
+        for (uint32_t step = 2; step < KC_E && !placed; ++step) {
+          e = e + 1 == KC_E ? 0u : e + 1;
+          placed = mineOrClaimed(atomicCAS(&tab64[e], ~0ull, mine));
         }
       }
+      atomicAdd(&cnt[e], add);
+      used[k] = e;
     }
     __syncthreads();
     loadSpan(desc[min(i + 2, nc - 1)], rn, sn);
     // ---- probe: first batch from registers, later batches loaded inline
-    matches += kqProbeCounted<T, K>(sv, ns, s, tab2, cnt);
+    matches += kqProbeCounted<T, K>(sv, ns, s, tab4, cnt2);
     for (uint32_t b0 = BATCH; b0 < ns; b0 += BATCH) {
       uint64_t xv[K];
       S.load(s0 + b0, ns - b0, xv);
-      matches += kqProbeCounted<T, K>(xv, ns - b0, s, tab2, cnt);
+      matches += kqProbeCounted<T, K>(xv, ns - b0, s, tab4, cnt2);
     }
     __syncthreads();
     // Only the entries this span used (a few per lane instead of the whole
-    // 48 KiB table); copies of a key clear the same entry.
+    // 72 KiB table); copies of a key clear the same entry.
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       if (used[k] >= KC_E) continue;

@@ -459,11 +459,36 @@ def quotient_crowd_fragments(n, bucket=17):
     return [kq4_fragment(bucket, 0x9E370001 + 7919 * i) for i in range(n)]
 
 
+def kc_bucket(frag, s=12):
+    """The counted table's home bucket of a fragment (key_tables.hip kcBucket,
+    3072 two-entry buckets)."""
+    import numpy as np
+    frag = np.asarray(frag, dtype=np.uint64)
+    e = (frag >> np.uint64(s)) & np.uint64(KQ_M)
+    lo = frag & np.uint64((1 << s) - 1)
+    h = ((e * np.uint64(0x9E3779B1)) & np.uint64(KQ_M)) ^ ((lo * np.uint64(0x85EBCA77)) & np.uint64(KQ_M))
+    h ^= h >> np.uint64(15)
+    return (h * np.uint64(3072)) >> np.uint64(32)
+
+
+def counted_crowd_fragments(n, bucket=3071):
+    """n distinct 44-bit fragments with the same counted-table home bucket:
+    two fill it, the rest walk on past the table's end (bucket 3071 is the
+    last: the walk wraps to entry 0)."""
+    import numpy as np
+    rng = np.random.default_rng(n)
+    out = []
+    while len(out) < n:
+        cand = rng.integers(0, 1 << 44, size=1 << 22, dtype=np.uint64)
+        out = list(dict.fromkeys(out + [int(f) for f in cand[kc_bucket(cand) == bucket]]))
+    return out[:n]  # (draw order: the largest keys set the plan's 63 key bits)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,n,dup,key_count,reruns",
                          [("crowd", 20, 1, 8, 0), ("crowd", 40, 3, 8, 0), ("crowd", 100, 1, 8, 0),
                           ("crowd", 400, 1, 8, 1), ("escape", 40, 1, 8, 0), ("escape", 20, 1, 9, 0),
-                          ("escape", 300, 3, 9, 0)])
+                          ("escape", 300, 3, 9, 0), ("ccrowd", 300, 3, 9, 0), ("ccrowd", 2000, 1, 9, 0)])
 def test_key_quotient_escapes(C, kind, n, dup, key_count, reruns):
     """Quotient / counted build/probe on adversarial keys, all in one final
     partition.  crowd: n keys share one quotient-table home bucket -- 4 in its
@@ -471,7 +496,8 @@ def test_key_quotient_escapes(C, kind, n, dup, key_count, reruns):
     span); 400 fill it: the count is void and the build/probe re-runs on
     counted tables (1 re-run).  escape: keys whose counted-table value is that
     table's empty marker -- counted tables hold them inline, the quotient
-    table (no marker) as any other key.  Repeated inner keys (dup 3) are seen
+    table (no marker) as any other key.  ccrowd: n keys share the counted
+    table's last home bucket -- two in it, the rest walk, wrapping to entry 0.  Repeated inner keys (dup 3) are seen
     at plan time or by the overflow chains.  Counts equal a torch oracle every
     time; later joins of the same HashJoin start where the first ended (no
     re-run)."""
@@ -479,7 +505,8 @@ def test_key_quotient_escapes(C, kind, n, dup, key_count, reruns):
     from helpers import ref_join_count
     g = torch.Generator().manual_seed(n * 7 + dup + key_count)
     part = 0x2A5F3  # one (network, local) digit pair: the keys share a span
-    frags = quotient_crowd_fragments(n) if kind == "crowd" else quotient_escape_fragments(n, first_bucket=17)
+    frags = {"crowd": lambda: quotient_crowd_fragments(n), "ccrowd": lambda: counted_crowd_fragments(n),
+             "escape": lambda: quotient_escape_fragments(n, first_bucket=17)}[kind]()
     esc = torch.tensor(frags, dtype=torch.int64)
     esc_keys = (esc << 19) | part
     other = torch.randint(1 << 40, (1 << 62) - 1, (400_000,), generator=g, dtype=torch.int64).unique()
