@@ -316,15 +316,17 @@ def measure(C, info, ctx, comm, on_gpu, G_R, G_S, inner, outer, cfg, rel_loc, st
     # If the first join still spilled past the reserved workspace, the arena
     # adds a chunk for it here (never inside a timed join).
     ctx.reset_scratch()
-    for _ in range(max(0, warmup - 1)):
-        join.run()
-    ctx.reset_scratch()
-    barrier()
-    results = []
     # No Python garbage collection inside the timed joins (host noise only:
     # the joins allocate nothing the collector tracks beyond their result dicts).
+    # Collected before the last warmup joins, so the GPU goes from them straight
+    # into the timed ones (a collection between them left it idle for tens of
+    # ms, and the first timed join ran ~5 % slower).
     gc.collect()
     gc.disable()
+    for _ in range(max(0, warmup - 1)):
+        join.run()
+    barrier()
+    results = []
     t0 = time.perf_counter()
     for _ in range(steps):
         results.append(join.run())
