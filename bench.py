@@ -24,6 +24,14 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+T_START = time.time()
+# Multi-GPU runs: the engine's watchdog (every blocking wait on a collective or
+# a stream) fires well before the driver's own 600 s limit, so a stuck rank
+# ends the run with a message naming its rank, phase, wait site and last
+# completed collective instead of a silent kill (HPCJOIN_COMM_TIMEOUT_S
+# overrides).  Set before the ranks are spawned: they inherit it.
+if int(os.environ.get("WORLD_SIZE", "1")) > 1 or any(a.startswith("--gpus") for a in sys.argv[1:]):
+    os.environ.setdefault("HPCJOIN_COMM_TIMEOUT_S", "120")
 
 
 def _spawn_ranks_if_needed():
@@ -323,16 +331,18 @@ def measure(C, info, ctx, comm, on_gpu, G_R, G_S, inner, outer, cfg, rel_loc, st
     # ms, and the first timed join ran ~5 % slower).
     gc.collect()
     gc.disable()
-    for _ in range(max(0, warmup - 1)):
-        join.run()
-    barrier()
-    results = []
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        results.append(join.run())
-    barrier()
-    elapsed = time.perf_counter() - t0
-    gc.enable()
+    try:
+        for _ in range(max(0, warmup - 1)):
+            join.run()
+        barrier()
+        results = []
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            results.append(join.run())
+        barrier()
+        elapsed = time.perf_counter() - t0
+    finally:
+        gc.enable()
     mine = [int(elapsed * 1e9), int(first_ms * 1e6), int(setup_ms * 1e6), int(join.plan_ms * 1e6)]
     plan_ms = join.plan_ms
     if info.world > 1:
@@ -379,6 +389,10 @@ def main():
     ap.add_argument("--scale-model", default="on", choices=["on", "off"],
                     help="N = 1 only: predicted N = 2/4/8 step times of the three N > 1 paths (scale_model)")
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--budget-s", type=float, default=float(os.environ.get("HPCJOIN_BENCH_BUDGET_S", "420")),
+                    help="wall budget of the whole run: the secondary measurements (shuffle_path, general_path, "
+                         "scale_model) are skipped once half of it is spent, so the headline line is always printed "
+                         "inside the driver's limit")
     args = ap.parse_args()
 
     C = hpcjoin.require_native()
@@ -442,9 +456,21 @@ def main():
     del join
     ctx.reset_scratch()
 
+    def budget_left(what):
+        """True while less than half the wall budget is spent (same answer on
+        every rank: rank 0's clock decides)."""
+        spent = time.time() - T_START
+        ok = spent < 0.5 * args.budget_s
+        if info.world > 1:
+            ok = bool(comm.all_gather([int(ok)])[0])
+        if not ok:
+            skipped[what] = f"wall budget: {spent:.0f} s of {args.budget_s:.0f} s spent before it"
+        return ok
+
+    skipped = {}
     shuffle = None
     comm_ok = True
-    if info.world > 1 and plan.bitmap_replicated:
+    if info.world > 1 and plan.bitmap_replicated and budget_left("shuffle_path"):
         # The reference's own N > 1 algorithm on the headline workload: hash-
         # partition shuffle (claim scatter + chunked RCCL all-to-allv, the
         # MPI_Put analog) instead of the replicated bitmaps the planner prefers.
@@ -468,7 +494,7 @@ def main():
             print(f"bench.py: shuffle path failed on rank {info.rank}: {e}", file=sys.stderr, flush=True)
 
     general = None
-    if args.general == "on" and args.dist in ("unique", "uniform", "zipf") and comm_ok:
+    if args.general == "on" and args.dist in ("unique", "uniform", "zipf") and comm_ok and budget_left("general_path"):
         # The secondary measurement must not cost the headline line: a failure
         # here (the engine aborts the communicator on every rank) is reported
         # in general_path and the headline is still printed.
@@ -488,7 +514,8 @@ def main():
             print(f"bench.py: general path failed on rank {info.rank}: {e}", file=sys.stderr, flush=True)
 
     model = None
-    if args.scale_model == "on" and info.world == 1 and on_gpu and args.dist == "unique" and comm_ok:
+    if (args.scale_model == "on" and info.world == 1 and on_gpu and args.dist == "unique" and comm_ok
+            and budget_left("scale_model")):
         try:
             model = scale_model(C, info, ctx, comm, on_gpu, G_R, G_S, specs, cfg, rel_loc, args.general != "off")
         except Exception as e:  # noqa: BLE001
@@ -545,6 +572,9 @@ def main():
             "general_path": general,
             "scale_model": model,
             "engine": engine,
+            "skipped": skipped or None,
+            "wall_s": round(time.time() - T_START, 1),
+            "comm_timeout_s": float(os.environ.get("HPCJOIN_COMM_TIMEOUT_S", "600")),
             "topology": topo,
             "device": torch.cuda.get_device_name(0) if on_gpu else "cpu",
         }
@@ -569,5 +599,23 @@ def main():
         print("bench.py: general path incorrect or failed (see general_path)", file=sys.stderr, flush=True)
 
 
+def run_rank():
+    """Multi-rank runs: a failing rank (watchdog, RCCL error, wrong result)
+    prints its message and exits non-zero at once, without the teardown that
+    would wait on peers stuck in a collective; the launcher (bench.py's own
+    spawner or torchrun) then stops the other ranks."""
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        main()
+        return
+    try:
+        main()
+    except SystemExit:
+        raise
+    except BaseException as e:  # noqa: BLE001
+        print(f"bench.py: rank {os.environ.get('RANK', '?')} failed after {time.time() - T_START:.1f} s: "
+              f"{type(e).__name__}: {e}", file=sys.stderr, flush=True)
+        os._exit(4)
+
+
 if __name__ == "__main__":
-    main()
+    run_rank()

@@ -3,12 +3,28 @@
 #include <cstring>
 
 #include "../utils/Debug.h"
+#include "../utils/Fault.h"
 
 namespace hpcjoin {
 namespace comm {
 
 ProcessGroupCommunicator::ProcessGroupCommunicator(c10::intrusive_ptr<c10d::ProcessGroup> pg) : pg_(std::move(pg)) {
   utils::setDebugRank(pg_->getRank());
+}
+
+// Every collective waits at most the engine's watchdog deadline
+// (HPCJOIN_COMM_TIMEOUT_S): a peer that stopped making progress ends this
+// rank's wait with a message naming the rank, phase and last collective,
+// instead of gloo's 30-minute default.
+static void waitBounded(const c10::intrusive_ptr<c10d::Work> &work, const char *what) {
+  try {
+    work->wait(std::chrono::milliseconds(utils::commTimeoutMs()));
+  } catch (const std::exception &e) {
+    utils::fail("WATCHDOG", __FILE__, __LINE__,
+                utils::format("%s did not complete within %lu ms (%s): %s", what,
+                              (unsigned long)utils::commTimeoutMs(), utils::watchdogContext().c_str(), e.what()));
+  }
+  utils::noteCollective(what, true);
 }
 
 static at::Tensor hostWords(const uint64_t *p, size_t n) {
@@ -21,17 +37,17 @@ void ProcessGroupCommunicator::allGatherHost(const uint64_t *send, uint64_t *rec
   std::vector<at::Tensor> in{hostWords(send, count)};
   std::vector<std::vector<at::Tensor>> out(1);
   for (uint32_t r = 0; r < size(); ++r) out[0].push_back(at::empty({(int64_t)count}, at::kLong));
-  pg_->allgather(out, in)->wait();
+  waitBounded(pg_->allgather(out, in), "gloo allgather");
   for (uint32_t r = 0; r < size(); ++r) std::memcpy(recv + r * count, out[0][r].data_ptr(), count * 8);
 }
 
 void ProcessGroupCommunicator::allReduceSumHost(uint64_t *data, size_t count) {
   std::vector<at::Tensor> t{hostWords(data, count)};
-  pg_->allreduce(t)->wait();
+  waitBounded(pg_->allreduce(t), "gloo allreduce");
   std::memcpy(data, t[0].data_ptr(), count * 8);
 }
 
-void ProcessGroupCommunicator::barrier() { pg_->barrier()->wait(); }
+void ProcessGroupCommunicator::barrier() { waitBounded(pg_->barrier(), "gloo barrier"); }
 
 void ProcessGroupCommunicator::allToAllV(const uint64_t *send, const uint64_t *sendCounts,
                                          const uint64_t *sendDispls, uint64_t *recv, const uint64_t *recvCounts,
@@ -50,7 +66,7 @@ void ProcessGroupCommunicator::allToAllV(const uint64_t *send, const uint64_t *s
   }
   at::Tensor in = at::from_blob(const_cast<uint64_t *>(send) + sendDispls[0], {(int64_t)st}, at::kLong);
   at::Tensor out = at::from_blob(recv + recvDispls[0], {(int64_t)rt}, at::kLong);
-  pg_->alltoall_base(out, in, rs, ss)->wait();
+  waitBounded(pg_->alltoall_base(out, in, rs, ss), "gloo all-to-allv");
 }
 
 }  // namespace comm

@@ -27,8 +27,9 @@ void InProcessGroup::barrier() {
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(utils::commTimeoutMs());
   if (!cv_.wait_until(lk, deadline, [&] { return generation_ != gen || aborted_; })) {
     aborted_ = true;
-    reason_ = utils::format("barrier timed out after %lu ms with %u of %u ranks present",
-                            (unsigned long)utils::commTimeoutMs(), waiting_, size_);
+    reason_ = utils::format("barrier timed out after %lu ms with %u of %u ranks present (rank %d: %s)",
+                            (unsigned long)utils::commTimeoutMs(), waiting_, size_, utils::debugRank(),
+                            utils::watchdogContext().c_str());
     cv_.notify_all();
   }
   if (generation_ == gen) {  // woken by an abort, not by the last arrival

@@ -86,11 +86,13 @@ void RcclCommunicator::allGatherHost(const uint64_t *send, uint64_t *recv, size_
   RCCL_CHECK(ncclAllGather(buf + count * rank_, buf, count, ncclUint64, static_cast<ncclComm_t>(comm_), stream_));
   HIP_CHECK(hipMemcpyAsync(recv, buf, count * size_ * 8, hipMemcpyDeviceToHost, stream_));
   utils::waitStream(stream_, this, "ncclAllGather");
+  utils::noteCollective("ncclAllGather", true);
 }
 
 void RcclCommunicator::allGatherDevice(const uint64_t *send, uint64_t *recv, size_t count, hipStream_t stream) {
   checkHealth();
   RCCL_CHECK(ncclAllGather(send, recv, count, ncclUint64, static_cast<ncclComm_t>(comm_), stream));
+  utils::noteCollective("ncclAllGather (stream)", false);
 }
 
 void RcclCommunicator::allReduceSumHost(uint64_t *data, size_t count) {
@@ -100,12 +102,14 @@ void RcclCommunicator::allReduceSumHost(uint64_t *data, size_t count) {
   RCCL_CHECK(ncclAllReduce(buf, buf, count, ncclUint64, ncclSum, static_cast<ncclComm_t>(comm_), stream_));
   HIP_CHECK(hipMemcpyAsync(data, buf, count * 8, hipMemcpyDeviceToHost, stream_));
   utils::waitStream(stream_, this, "ncclAllReduce");
+  utils::noteCollective("ncclAllReduce", true);
 }
 
 void RcclCommunicator::allReduceSumDevice(uint64_t *data, size_t count, hipStream_t stream) {
   if (count == 0) return;
   checkHealth();
   RCCL_CHECK(ncclAllReduce(data, data, count, ncclUint64, ncclSum, static_cast<ncclComm_t>(comm_), stream));
+  utils::noteCollective("ncclAllReduce (stream)", false);
 }
 
 void RcclCommunicator::barrier() {
@@ -136,6 +140,7 @@ void RcclCommunicator::allToAllV(const uint64_t *send, const uint64_t *sendCount
       RCCL_CHECK(ncclRecv(recv + recvDispls[from], recvCounts[from], ncclUint64, (int)from, c, stream));
   }
   RCCL_CHECK(ncclGroupEnd());
+  utils::noteCollective("ncclSend/ncclRecv all-to-allv", false);
 }
 
 }  // namespace comm

@@ -616,6 +616,16 @@ bool HashJoin::canFuseRows() const {
 }
 
 JoinResult HashJoin::run() {
+  // Watchdog context: an injected stall (HPCJOIN_STALL) waits on this join's
+  // communicator, and a timed-out wait names the phase the join was in.
+  struct WatchScope {
+    explicit WatchScope(comm::Communicator *c) { utils::setWatchComm(c); }
+    ~WatchScope() {
+      utils::setWatchComm(nullptr);
+      utils::setPhase("between joins");
+    }
+  } watch(ctx->comm());
+  utils::setPhase("plan");
   try {
     if (passes > 1) return runPasses();
     return runImpl();

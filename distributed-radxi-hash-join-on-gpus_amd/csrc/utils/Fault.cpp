@@ -17,9 +17,16 @@ thread_local std::string t_phase;
 thread_local int t_rank = -1;
 thread_local bool t_armed = false;
 std::atomic<uint64_t> g_timeoutMs{0};
+// Watchdog context of this rank.
+thread_local const char *t_current = "setup";
+thread_local const char *t_lastDone = nullptr;
+thread_local const char *t_lastQueued = nullptr;
+thread_local uint64_t t_doneCount = 0, t_queuedCount = 0;
+thread_local comm::Communicator *t_watchComm = nullptr;
+thread_local bool t_stalled = false;
 
-bool envFault(const char *phase) {
-  const char *e = std::getenv("HPCJOIN_FAULT");
+bool envMatch(const char *var, const char *phase) {
+  const char *e = std::getenv(var);
   if (!e || !e[0]) return false;
   const char *colon = std::strchr(e, ':');
   const size_t n = colon ? (size_t)(colon - e) : std::strlen(e);
@@ -35,15 +42,46 @@ void armFault(const std::string &phase, int rank) {
 }
 
 bool faultHit(const char *phase) {
-  const bool hit = (t_armed && t_phase == phase && (t_rank < 0 || t_rank == debugRank())) || envFault(phase);
+  const bool hit =
+      (t_armed && t_phase == phase && (t_rank < 0 || t_rank == debugRank())) || envMatch("HPCJOIN_FAULT", phase);
   if (hit) t_armed = false;  // one shot
   return hit;
 }
 
+template <typename Query>
+static void waitUntil(Query query, comm::Communicator *comm, const char *what);
+
 void faultPoint(const char *phase) {
+  setPhase(phase);
   if (faultHit(phase))
     throw InjectedFault(format("[FAULT][rank %d] injected fault at phase '%s'", debugRank(), phase));
+  if (!t_stalled && envMatch("HPCJOIN_STALL", phase)) {
+    t_stalled = true;  // one shot per rank
+    const std::string what = format("injected stall at phase '%s'", phase);
+    waitUntil([] { return hipErrorNotReady; }, t_watchComm, what.c_str());
+  }
 }
+
+void setPhase(const char *phase) { t_current = phase; }
+
+void noteCollective(const char *name, bool completed) {
+  if (completed) {
+    t_lastDone = name;
+    ++t_doneCount;
+  } else {
+    t_lastQueued = name;
+    ++t_queuedCount;
+  }
+}
+
+std::string watchdogContext() {
+  std::string s = format("phase '%s', last completed collective ", t_current);
+  s += t_lastDone ? format("%s #%lu", t_lastDone, (unsigned long)t_doneCount) : std::string("none");
+  if (t_lastQueued) s += format(", last enqueued %s #%lu", t_lastQueued, (unsigned long)t_queuedCount);
+  return s;
+}
+
+void setWatchComm(comm::Communicator *comm) { t_watchComm = comm; }
 
 uint64_t commTimeoutMs() {
   uint64_t v = g_timeoutMs.load(std::memory_order_relaxed);
@@ -67,7 +105,8 @@ static void waitUntil(Query query, comm::Communicator *comm, const char *what) {
     if (comm) comm->checkHealth();
     const auto now = clk::now();
     if (now > deadline) {
-      std::string why = format("%s did not complete within %lu ms", what, (unsigned long)commTimeoutMs());
+      std::string why = format("%s did not complete within %lu ms (%s)", what, (unsigned long)commTimeoutMs(),
+                               watchdogContext().c_str());
       if (comm) comm->abort(why);
       fail("WATCHDOG", __FILE__, __LINE__, why);
     }

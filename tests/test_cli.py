@@ -47,3 +47,32 @@ def test_bench_py_cpu_contract():
         assert k in j, k
     assert j["correct"] is True and j["n_gpus"] == 1 and j["steps"] == 2
     assert "value_note" in j  # which plan `value` measures (N > 1: replicated bitmaps, not the shuffle)
+
+
+def test_bench_py_stalled_rank_exits_with_site(tmp_path):
+    """bench.py --gpus 2 (its own spawner, gloo on the CPU) with rank 1 stalled
+    at `network`: both ranks end within the watchdog timeout, the job exits
+    non-zero, and the failing rank's message names rank, phase and site."""
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="", HPCJOIN_STALL="network:1",
+               HPCJOIN_COMM_TIMEOUT_S="5")
+    env.pop("WORLD_SIZE", None)
+    import time
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=str(tmp_path))
+    assert r.returncode != 0, r.stdout + r.stderr
+    assert "WATCHDOG" in r.stderr and "phase 'network'" in r.stderr, r.stderr[-3000:]
+    assert "bench.py: rank" in r.stderr and "failed after" in r.stderr, r.stderr[-3000:]
+    assert time.time() - t0 < 200
+
+
+def test_bench_py_wall_budget_skips_secondary():
+    """A spent wall budget skips the secondary measurements (and says so)
+    instead of running past the driver's limit; the headline is printed."""
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "1",
+                        "--budget-s", "0"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    j = _last_json(r.stdout)
+    assert j["correct"] is True and j["general_path"] is None
+    assert "general_path" in j["skipped"] and "wall budget" in j["skipped"]["general_path"]

@@ -87,3 +87,41 @@ def test_fault_injection_from_env():
     env["HPCJOIN_FAULT"] = "network:5"  # other rank: no fault
     p = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stderr
+
+
+def test_stalled_rank_ends_every_rank():
+    """A rank that stops making progress at `network` (HPCJOIN_STALL) must not
+    leave the job hanging until an outer kill: with HPCJOIN_COMM_TIMEOUT_S set
+    (bench.py sets 120 s for N > 1) every rank exits non-zero within the
+    timeout, and each message names its rank, phase, wait site and last
+    completed collective."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    world, timeout_s = 3, 4
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+               HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="", HPCJOIN_STALL="network:1",
+               HPCJOIN_COMM_TIMEOUT_S=str(timeout_s))
+    script = os.path.join(ROOT, "tests", "stall_worker.py")
+    t0 = time.time()
+    procs = [subprocess.Popen([sys.executable, "-u", script], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(world)]
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=120))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    wall = time.time() - t0
+    for r, (p, (out, err)) in enumerate(zip(procs, outs)):
+        assert p.returncode != 0, (r, out, err)
+        line = next((l for l in err.splitlines() if l.startswith("RANK_FAILED")), "")
+        assert f"rank={r}" in line and "WATCHDOG" in line and f"[rank {r}]" in line, (r, err[-2000:])
+        assert "phase 'network'" in line and "last completed collective" in line, line
+        after = float(line.split("after=")[1].split("s ")[0])
+        assert after < 3 * timeout_s + 5, line  # bounded by the timeout, not by an outer kill
+    assert "injected stall at phase 'network'" in [e for _, e in outs][1]
+    assert wall < 100

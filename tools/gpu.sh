@@ -13,6 +13,7 @@
 #   sskew=ARGS          tools/bench_skew.py ARGS with HPCJOIN_SHARE_GPU=1 (--gpus N: N RCCL ranks on this GPU)
 #   phases=ARGS        tools/scatter_phases.py of the phase-stamped build in ab/prof (tools/README.md)
 #   py=SCRIPT,ARGS      python SCRIPT ARGS
+#   epy=ENV/SCRIPT,ARGS python SCRIPT ARGS with ENV (comma-separated K=V)
 #   stats=ARGS          rocprofv3 --kernel-trace --stats of bench.py ARGS
 #   pstats=SCRIPT,ARGS  rocprofv3 --kernel-trace --stats of python SCRIPT ARGS
 #   ppmc=CTRS/SCRIPT,ARGS  rocprofv3 --pmc CTRS of python SCRIPT ARGS
@@ -81,6 +82,8 @@ for step in "$@"; do
              done
              echo "abbench rc=$rc" > "$log"; (exit $rc) ;;
     py) timeout -k 10 900 python -u $args > "$log" 2>&1 ;;
+    epy) envs=${arg%%/*}; pargs=${arg#*/}
+         timeout -k 10 900 env ${envs//,/ } python -u ${pargs//,/ } > "$log" 2>&1 ;;
     stats) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/stats$n" -o run --output-format csv \
               -- python "$R/bench.py" $args) > "$log" 2>&1 ;;
     pstats) (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$OUT/stats$n" -o run --output-format csv \
