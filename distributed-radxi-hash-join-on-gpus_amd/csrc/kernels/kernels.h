@@ -163,8 +163,10 @@ void netScatterWide(const data::Tuple *in, uint64_t n, uint32_t bits, const Part
                     KeyMix mix = KeyMix(), const void *gend = nullptr, int narrowMode = -1);
 // Count-only projection (JoinPlan::fragments): the scatter writes only the
 // u32 key fragment (mixed key >> bits) -- 4 bytes per tuple instead of 8.
-// Needs fragment bits + bits <= 32 (fragWordFits).
-HJ_HD bool fragWordFits(uint32_t keyBits, uint32_t bits) { return keyBits <= 32 || keyBits <= bits; }
+// Needs a fragment of at most 32 bits above the digit (fragWordFits); with
+// keyBits <= 32 the digit rides in the staged word, above that (e.g. 6B dense
+// keys, 33 bits) the tile keeps a separate digit array.
+HJ_HD bool fragWordFits(uint32_t keyBits, uint32_t bits) { return keyBits <= 32 + bits; }
 void netScatterFrag(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g, uint32_t blockBegin,
                     uint32_t blockEnd, void *gcur, uint32_t *out, hipStream_t s, uint32_t keyBits,
                     KeyMix mix = KeyMix(), const void *gend = nullptr, int narrowMode = -1);

@@ -509,6 +509,26 @@ struct NetFragPolT : KeyLoad {
   __device__ __forceinline__ void store(OutT *o, uint64_t pos, const StageT &v) const { o[pos] = out(v); }
 };
 using NetFragPol = NetFragPolT<false>;  // ablation entry (no key mixing)
+// Fragments of keys wider than 32 bits (fragWordFits: keyBits <= 32 + bits,
+// e.g. 6B dense keys = 33 bits): the staged u32 word is the whole fragment
+// and the digit goes to the tile's u16 digit array (no early prefetch).
+template <bool MIX>
+struct NetFragDigPolT : KeyLoad {
+  using InT = ulonglong2;
+  using StageT = uint32_t;
+  using OutT = uint32_t;
+  static constexpr bool kDigArray = true;
+  uint64_t mask;
+  uint32_t bits;
+  KeyMix mix;
+  __device__ __forceinline__ uint32_t digit(const LoadT &k) const { return (uint32_t)(mixKey<MIX>(mix, k) & mask); }
+  __device__ __forceinline__ StageT stage(const LoadT &k, uint32_t) const {
+    return (uint32_t)(mixKey<MIX>(mix, k) >> bits);
+  }
+  __device__ __forceinline__ uint32_t stagedDigit(const StageT &) const { return 0; }  // digits: LDS array
+  __device__ __forceinline__ OutT out(const StageT &v) const { return v; }
+  __device__ __forceinline__ void store(OutT *o, uint64_t pos, const StageT &v) const { o[pos] = v; }
+};
 struct NetWidePol : PlainLoad<ulonglong2> {  // 16 B tuple -> 16 B tuple (full-range keys)
   using InT = ulonglong2;
   using StageT = ulonglong2;
@@ -724,7 +744,10 @@ constexpr bool earlyPrefetch() {
          IPT * sizeof(typename Pol::LoadT) <= 64;
 }
 
-// One tile.  FULL tiles (every tile but a range's tail) have no divergent
+// One tile.  The next tile's loads ([nbase, nbase + TILE), clamped to nlast)
+// are issued into v while this one is staged or written out: the caller's
+// next tile of the same range, or the first tile of its next range.
+// FULL tiles (every tile but a range's tail) have no divergent
 // control flow at all, so hipcc keeps the IPT LDS atomics, loads and stores
 // in flight with counted waits; the tail tile predicates its LDS work only.
 // BOUNDED (claim mode with estimated slices): l.cursor[d] holds the end of the
@@ -736,7 +759,7 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
                                             uint32_t count, uint32_t F, const ScatterSmem<Pol, CurT, NTH * IPT> &l,
                                             const Pol &pol, typename Pol::OutT *__restrict__ out,
                                             typename Pol::LoadT (&v)[IPT], CurT *__restrict__ gcur,
-                                            ScatterProf &pf) {
+                                            ScatterProf &pf, uint64_t nbase, uint64_t nlast) {
   constexpr uint32_t TILE = NTH * IPT;
   pf.start();
   constexpr bool EARLY = earlyPrefetch<Pol, IPT>();
@@ -779,7 +802,7 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
       if (wave0 + k * NTH < F) claim[k] = atomicAdd(d < F ? gcur + d : trash + t, (CurT)l.cnt[d]);
     }
   }
-  if constexpr (EARLY) prefetchTile<Pol, NTH, IPT>(in, base + TILE, end - 1, v);
+  if constexpr (EARLY) prefetchTile<Pol, NTH, IPT>(in, nbase, nlast, v);
   pf.mark(2);
   blockExclusiveScanLds<NTH, uint32_t, uint32_t, true>(l.cnt, l.off, (int)F, l.wave);
   pf.mark(3);
@@ -821,7 +844,7 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
       }
     }
     // Prefetch the next tile while this one is streamed out.
-    prefetchTile<Pol, NTH, IPT>(in, base + TILE, end - 1, v);
+    prefetchTile<Pol, NTH, IPT>(in, nbase, nlast, v);
   }
   pf.mark(4);
   if constexpr (CLAIM) {
@@ -883,10 +906,10 @@ __device__ __forceinline__ void scatterRange(const typename Pol::InT *__restrict
   for (uint64_t base = begin; base < end; base += TILE) {
     if (base + TILE <= end)
       scatterTile<Pol, CurT, NTH, IPT, MODE, true, CLAIM, BOUNDED, MAXD>(in, base, end, TILE, F, l, pol, out, v,
-                                                                         gcur, pf);
+                                                                         gcur, pf, base + TILE, end - 1);
     else
       scatterTile<Pol, CurT, NTH, IPT, MODE, false, CLAIM, BOUNDED, MAXD>(in, base, end, (uint32_t)(end - base), F, l,
-                                                                          pol, out, v, gcur, pf);
+                                                                          pol, out, v, gcur, pf, base + TILE, end - 1);
   }
   pf.flush();
   __syncthreads();
@@ -1135,10 +1158,15 @@ void netScatterFrag(const data::Tuple *in, uint64_t n, uint32_t bits, const Part
     pol.mix = mix;
     launchNetClaim(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
   };
-  if (mix.on)
+  const bool digitOnTop = kb <= 32;  // fragment + digit fit the staged u32
+  if (mix.on && digitOnTop)
     go(NetFragPolT<true>());
-  else
+  else if (digitOnTop)
     go(NetFragPolT<false>());
+  else if (mix.on)
+    go(NetFragDigPolT<true>());
+  else
+    go(NetFragDigPolT<false>());
 }
 
 // ------------------------------------------------ device-side sampled layout
@@ -1660,6 +1688,114 @@ __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void localScatterClaim
                                                             gcur + (uint64_t)it.stream * F);
 }
 
+// Persistent local claim scatter.  Work items are short (1B x 1B: a network
+// partition's slice of one claim group, ~120K tuples = 15 tiles) and the
+// production workgroup owns its CU (1024 threads, ~90 KB of LDS), so a
+// workgroup per item drained the tile pipeline at every item end (the last
+// tile's write-out overlapped nothing) and refilled it at the next item's
+// start (workgroup launch, LDS init, first tile's loads exposed).  Here a
+// workgroup walks the items of its XCD's contiguous run with a stride of the
+// workgroups on that XCD, and the prefetch issued while an item's last tile
+// is staged already loads the next item's first tile.  Between items only
+// the bounded slot ends are swapped (after an LDS barrier: the last
+// write-out read them).
+template <class Pol, typename CurT, int NTH, int IPT, bool BOUNDED, int MAXD>
+__global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void localScatterPersistKernel(
+    const typename Pol::InT *__restrict__ in, const LocalItem *__restrict__ items, uint32_t nItems, uint32_t F,
+    Pol pol, CurT *__restrict__ gcur, typename Pol::OutT *out, const CurT *__restrict__ gend, uint32_t perXcd) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr uint32_t TILE = NTH * IPT;
+  const uint32_t q = (nItems + NGROUPS - 1) / NGROUPS;
+  const uint32_t first = (blockIdx.x % NGROUPS) * q, last = min(nItems, first + q);  // this XCD's items
+  uint32_t cur = first + blockIdx.x / NGROUPS;
+  if (cur >= last) return;  // uniform per workgroup
+  const uint32_t FP = padDigits(F);
+  const ScatterSmem<Pol, CurT, TILE> l(smem, F);
+  LocalItem it = items[cur];
+  for (uint32_t d = threadIdx.x; d < FP; d += NTH) {
+    l.cnt[d] = 0;
+    if constexpr (BOUNDED)
+      if (d < F) l.cursor[d] = gend[(uint64_t)it.stream * F + d];
+  }
+  __syncthreads();
+  typename Pol::LoadT v[IPT];
+  ScatterProf pf;
+  prefetchTile<Pol, NTH, IPT>(in, it.begin, it.begin + it.len - 1, v);
+  for (;;) {
+    const uint32_t nxt = cur + perXcd;
+    const bool more = nxt < last;
+    const LocalItem nit = more ? items[nxt] : it;
+    const uint64_t end = it.begin + it.len;
+    CurT *gc = gcur + (uint64_t)it.stream * F;
+    for (uint64_t base = it.begin; base < end; base += TILE) {
+      const bool lastTile = base + TILE >= end;
+      const uint64_t nb = lastTile ? nit.begin : base + TILE;
+      const uint64_t nl = lastTile ? nit.begin + nit.len - 1 : end - 1;
+      if (base + TILE <= end)
+        scatterTile<Pol, CurT, NTH, IPT, 0, true, true, BOUNDED, MAXD>(in, base, end, TILE, F, l, pol, out, v, gc,
+                                                                       pf, nb, nl);
+      else
+        scatterTile<Pol, CurT, NTH, IPT, 0, false, true, BOUNDED, MAXD>(in, base, end, (uint32_t)(end - base), F, l,
+                                                                        pol, out, v, gc, pf, nb, nl);
+    }
+    if (!more) break;
+    if constexpr (BOUNDED) {
+      CurT e[MAXD];
+#pragma unroll
+      for (int k = 0; k < MAXD; ++k) {
+        const uint32_t d = threadIdx.x + k * NTH;
+        e[k] = d < F ? gend[(uint64_t)nit.stream * F + d] : (CurT)0;
+      }
+      ldsBarrier();  // every wave's last write-out has read the old slot ends
+#pragma unroll
+      for (int k = 0; k < MAXD; ++k) {
+        const uint32_t d = threadIdx.x + k * NTH;
+        if (d < F) l.cursor[d] = e[k];
+      }
+      // visible to the next tile's write-out through its barriers A and B
+    }
+    it = nit;
+    cur = nxt;
+  }
+  pf.flush();
+}
+
+// Workgroups per XCD of the persistent local scatter: what stays resident.
+template <class K>
+static uint32_t persistPerXcd(K kernel, uint32_t nth, size_t lds, uint32_t nItems) {
+  static thread_local int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  int per = 0;
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void *>(kernel), (int)nth, lds));
+  const uint32_t q = (nItems + NGROUPS - 1) / NGROUPS;
+  const uint32_t want = (uint32_t)std::max(1, per) * (uint32_t)std::max(1, cus / (int)NGROUPS);
+  return std::max<uint32_t>(1, std::min<uint32_t>(want, q));
+}
+
+template <class P, typename C, int NTH, int IPT>
+static void launchLocalClaimPersist(const void *in, const LocalItem *items, uint32_t nItems, uint32_t F, const P &pol,
+                                    void *gcur, void *out, const void *gend, hipStream_t s) {
+  const size_t lds = ScatterLayout<P, C, NTH * IPT>::bytes(F);
+  HJ_CHECK(lds <= 160 * 1024, "local scatter LDS %zu too large", lds);
+  withMaxd<NTH>(F, [&](auto maxd) {
+    constexpr int M = decltype(maxd)::value;
+    auto go = [&](auto kernel, const C *ge) {
+      const uint32_t per = persistPerXcd(kernel, NTH, lds, nItems);
+      hipLaunchKernelGGL(kernel, dim3(per * NGROUPS), dim3(NTH), lds, s, reinterpret_cast<const typename P::InT *>(in),
+                         items, nItems, F, pol, reinterpret_cast<C *>(gcur), reinterpret_cast<typename P::OutT *>(out),
+                         ge, per);
+    };
+    if (gend)
+      go(localScatterPersistKernel<P, C, NTH, IPT, true, M>, reinterpret_cast<const C *>(gend));
+    else
+      go(localScatterPersistKernel<P, C, NTH, IPT, false, M>, nullptr);
+  });
+}
+
 // One local claim-scatter launch (MAXD from F, bounded when gend is given).
 template <class P, typename C, int NTH, int IPT>
 static void launchLocalClaim(const void *in, const LocalItem *items, uint32_t nItems, uint32_t F, const P &pol,
@@ -1709,7 +1845,10 @@ void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nI
   const uint32_t F = 1u << bits;
   const uint64_t mask = F - 1;
   const uint32_t grid = ((nItems + NGROUPS - 1) / NGROUPS) * NGROUPS;
-  if (geometry != 0 && split.on && !wide && !frag && !narrow && gend) {
+  // geometry 5: the default 1024 x 8 shape as one workgroup per item (the
+  // round-5 kernel, kept for A/B); 0: persistent workgroups over the items.
+  const bool persist = geometry == 0;
+  if (geometry != 0 && geometry != 5 && split.on && !wide && !frag && !narrow && gend) {
     LocalSplitPol pol;
     pol.mask = mask;
     pol.shift = shift;
@@ -1729,7 +1868,10 @@ void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nI
     pol.mask = mask;                                                                                        \
     pol.shift = shift;                                                                                      \
     setSplit(pol, split);                                                                                   \
-    launchLocalClaim<P, C, CL_NTH, CL_IPT>(in, items, nItems, F, pol, gcur, out, gend, s);                  \
+    if (persist)                                                                                            \
+      launchLocalClaimPersist<P, C, CL_NTH, CL_IPT>(in, items, nItems, F, pol, gcur, out, gend, s);         \
+    else                                                                                                    \
+      launchLocalClaim<P, C, CL_NTH, CL_IPT>(in, items, nItems, F, pol, gcur, out, gend, s);                \
   } while (0)
   if (frag && narrow) HJ_LOCAL(LocalFragPol, uint32_t);
   else if (frag) HJ_LOCAL(LocalFragPol, unsigned long long);

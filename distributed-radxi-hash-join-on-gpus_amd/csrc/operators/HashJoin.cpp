@@ -300,8 +300,11 @@ void HashJoin::makeJoinPlan() {
   // Counting on the split layout reads only the u16 fragment column: the
   // sampled network pass can then write u32 fragments and the local pass the
   // fragment column alone (4 + 2 bytes per tuple instead of 8 + 6).
+  // No rid travels, so the rid width (which decides splitLocal) does not
+  // matter: only that the u16 column holds the fragment above both digits.
   plan.fragments = plan.sampledNetwork && !plan.materialize && !plan.wide && !plan.keyOnly && plan.twoLevel &&
-                   plan.splitLocal && kernels::fragWordFits(plan.keyBits, plan.networkBits);
+                   plan.keyBits <= plan.networkBits + plan.localBits + 16 &&
+                   kernels::fragWordFits(plan.keyBits, plan.networkBits);
   // N > 1 pipelines (also on the host path, where they run in place: same
   // logic, covered by the CPU tests).
   plan.splitHistogram = config.splitHistogram && numberOfNodes > 1;

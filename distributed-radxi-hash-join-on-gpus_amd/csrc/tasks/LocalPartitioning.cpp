@@ -1,5 +1,8 @@
 #include "LocalPartitioning.h"
 
+#include <cstdlib>
+#include <cstring>
+
 #include "../host/HostOps.h"
 #include "../memory/Arena.h"
 #include "../performance/Clock.h"
@@ -116,9 +119,18 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
     const uint64_t P = (uint64_t)owned * F;
     const uint32_t S = plan.localSampleStride;
     const uint64_t cap = kernels::localSampledCapacityBound(xp.recvTotal, P, S, align);
-    void *sout = alloc(std::max<uint64_t>(cap, 1) * ob);
+    // HPCJOIN_LP_SKEW="lo:hi" (bytes, experiments only): start the output
+    // columns that far into their allocations (HBM channel placement A/B).
+    uint64_t skewLo = 0, skewHi = 0;
+    if (const char *e = std::getenv("HPCJOIN_LP_SKEW")) {
+      skewLo = std::strtoull(e, nullptr, 0);
+      if (const char *c = std::strchr(e, ':')) skewHi = std::strtoull(c + 1, nullptr, 0);
+    }
+    void *sout = static_cast<uint8_t *>(alloc(std::max<uint64_t>(cap, 1) * ob + skewLo)) + skewLo;
     if (frag) split.hi = static_cast<uint16_t *>(sout);
-    else if (split.on) split.hi = static_cast<uint16_t *>(alloc(std::max<uint64_t>(cap, 1) * 2));
+    else if (split.on)
+      split.hi = reinterpret_cast<uint16_t *>(static_cast<uint8_t *>(alloc(std::max<uint64_t>(cap, 1) * 2 + skewHi)) +
+                                              skewHi);
     uint32_t *caps = ctx->workspace().getArray<uint32_t>(std::max<uint64_t>(P, 1));
     auto *starts = ctx->workspace().getArray<unsigned long long>(std::max<uint64_t>(P, 1));
     void *scanWs = ctx->workspace().get(kernels::scanWorkspaceBytes(std::max<uint64_t>(P, 1)));
