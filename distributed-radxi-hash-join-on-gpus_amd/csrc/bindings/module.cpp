@@ -577,6 +577,7 @@ py::dict resultToDict(const operators::JoinResult &r) {
   d["exchange_checked"] = r.exchangeChecked;
   d["passes"] = r.passes;
   d["compact_ms"] = r.compactMs;
+  d["group_passes"] = r.groupPasses;
   d["inner_received"] = r.innerReceived;
   d["wire_bytes"] = r.wireBytes;
   d["outer_received"] = r.outerReceived;
@@ -1057,6 +1058,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         d["pass_estimate_bytes"] = j.spill.passEstimate;
         d["pass_workspace_bytes"] = j.spill.passReserved;
         d["pass_peak_bytes"] = j.spill.passPeak;
+        d["group_budget_bytes"] = j.spill.groupBudget;
         return d;
       })
       .def_property_readonly("plan_ms", &operators::HashJoin::planMilliseconds)

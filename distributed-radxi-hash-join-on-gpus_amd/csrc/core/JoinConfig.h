@@ -188,6 +188,9 @@ struct JoinPlan {
   KernelVariants variants;
   uint32_t wireBits[2] = {0, 0};
   uint32_t wireRidBits[2] = {0, 0};
+  // Capacity spill of the N = 1 bitmap plan (tasks/BitmapJoin, partition-group
+  // passes): bytes the fragment windows of one pass may take; 0 = one pass.
+  uint64_t groupBudget = 0;
   std::vector<uint64_t> ridBase[2];
   uint64_t networkPartitions() const { return uint64_t(1) << networkBits; }
   uint64_t localPartitions() const { return twoLevel ? (uint64_t(1) << localBits) : 1; }

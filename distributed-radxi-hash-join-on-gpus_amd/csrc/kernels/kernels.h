@@ -170,6 +170,14 @@ HJ_HD bool fragWordFits(uint32_t keyBits, uint32_t bits) { return keyBits <= 32 
 void netScatterFrag(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g, uint32_t blockBegin,
                     uint32_t blockEnd, void *gcur, uint32_t *out, hipStream_t s, uint32_t keyBits,
                     KeyMix mix = KeyMix(), const void *gend = nullptr, int narrowMode = -1);
+// Partition-group pass of the same scatter: only tuples whose digit is in
+// [dLo, dLo + range) are written, into [G][range] bounded claim slices (gcur /
+// gend laid out by netSampledLayout with the same range); the others are read
+// and dropped.  range < 1024 (one sentinel counter in the tile's LDS arrays).
+// The final claim cursors count every kept tuple (overflow check as usual).
+void netScatterFragRange(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g, void *gcur,
+                         uint32_t *out, hipStream_t s, uint32_t keyBits, KeyMix mix, const void *gend, bool narrow,
+                         uint32_t dLo, uint32_t range);
 // Sampled network pass sized on the device (no host round trip): from the
 // sampled [G][F] group totals (netGroupTotals) to bounded claim slices
 // gstart/gcur/gend ([G][F], u32 if narrow else u64) and *capacityUsed = the
@@ -192,7 +200,10 @@ struct LayoutInput {
   unsigned long long *capacityUsed;
   bool clearSampled = false;  // zero `sampled` after reading it (DeviceControl totals)
 };
-void netSampledLayout(const LayoutInput *sides, uint32_t count, uint32_t F, bool narrow, hipStream_t s);
+// range > 0: lay out only digits [dLo, dLo + range) of the [G][F] totals, as
+// [G][range] slices (a partition-group pass, netScatterFragRange).
+void netSampledLayout(const LayoutInput *sides, uint32_t count, uint32_t F, bool narrow, hipStream_t s,
+                      uint32_t dLo = 0, uint32_t range = 0);
 // gend (optional, same layout and width as gcur): end of every group slice.
 // Positions claimed past a slice end are not written; the final gcur values
 // tell the caller each slice's demand (the sampled pass re-runs exactly on
@@ -532,8 +543,9 @@ HJ_HD uint32_t passOf(uint64_t key, uint32_t K) {
 // counts[p] += tuples of pass p (counts zeroed by the caller).
 void passCounts(const data::Tuple *in, uint64_t n, uint32_t K, unsigned long long *counts, hipStream_t s);
 // out = the tuples of pass k (any order); *cursor (zeroed by the caller) ends at their count.
+// Writes stop at `capacity` tuples (the cursor still counts every one).
 void passCompact(const data::Tuple *in, uint64_t n, uint32_t K, uint32_t k, data::Tuple *out,
-                 unsigned long long *cursor, hipStream_t s);
+                 unsigned long long *cursor, hipStream_t s, uint64_t capacity);
 
 // p[0, words) = 0 (u64 words) with the engine's own kernel.
 void zeroWords(void *p, uint64_t words, hipStream_t s);

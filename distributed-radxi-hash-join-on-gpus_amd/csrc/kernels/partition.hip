@@ -490,17 +490,35 @@ struct NetKeyPol : KeyLoad {
 // tasks/BuildProbe.cpp:101-102, and reports only the count, :115).  The
 // digit rides in the staged word's top bits (fragBits + bits <= 32, checked
 // by the launcher).
-template <bool MIX>
+//
+// FILT (partition-group passes, kernels.h netScatterFragRange): only digits
+// [dLo, dLo + range) are written, renumbered 0..range-1; every other tuple
+// gets the sentinel digit `range`, is ranked and staged behind the kept ones
+// and never stored (scatterTile: FilterOf).
+template <bool FILT>
+__device__ __forceinline__ uint32_t rangeDigit(uint32_t d, uint32_t dLo, uint32_t range) {
+  if constexpr (FILT) {
+    d -= dLo;  // wraps below dLo
+    return d < range ? d : range;
+  } else {
+    return d;
+  }
+}
+template <bool MIX, bool FILT = false>
 struct NetFragPolT : KeyLoad {
   using InT = ulonglong2;
   using StageT = uint32_t;
   using OutT = uint32_t;
   static constexpr bool kDigArray = false;
   static constexpr bool kEarly = true;  // earlyPrefetch
+  static constexpr bool kFilter = FILT;
   uint64_t mask;
   uint32_t bits;
   KeyMix mix;
-  __device__ __forceinline__ uint32_t digit(const LoadT &k) const { return (uint32_t)(mixKey<MIX>(mix, k) & mask); }
+  uint32_t dLo = 0, range = 0;
+  __device__ __forceinline__ uint32_t digit(const LoadT &k) const {
+    return rangeDigit<FILT>((uint32_t)(mixKey<MIX>(mix, k) & mask), dLo, range);
+  }
   __device__ __forceinline__ StageT stage(const LoadT &k, uint32_t d) const {
     return (uint32_t)(mixKey<MIX>(mix, k) >> bits) | (d << (32 - bits));
   }
@@ -512,16 +530,20 @@ using NetFragPol = NetFragPolT<false>;  // ablation entry (no key mixing)
 // Fragments of keys wider than 32 bits (fragWordFits: keyBits <= 32 + bits,
 // e.g. 6B dense keys = 33 bits): the staged u32 word is the whole fragment
 // and the digit goes to the tile's u16 digit array (no early prefetch).
-template <bool MIX>
+template <bool MIX, bool FILT = false>
 struct NetFragDigPolT : KeyLoad {
   using InT = ulonglong2;
   using StageT = uint32_t;
   using OutT = uint32_t;
   static constexpr bool kDigArray = true;
+  static constexpr bool kFilter = FILT;
   uint64_t mask;
   uint32_t bits;
   KeyMix mix;
-  __device__ __forceinline__ uint32_t digit(const LoadT &k) const { return (uint32_t)(mixKey<MIX>(mix, k) & mask); }
+  uint32_t dLo = 0, range = 0;
+  __device__ __forceinline__ uint32_t digit(const LoadT &k) const {
+    return rangeDigit<FILT>((uint32_t)(mixKey<MIX>(mix, k) & mask), dLo, range);
+  }
   __device__ __forceinline__ StageT stage(const LoadT &k, uint32_t) const {
     return (uint32_t)(mixKey<MIX>(mix, k) >> bits);
   }
@@ -735,6 +757,11 @@ __device__ __forceinline__ void prefetchTile(const typename Pol::InT *__restrict
 // 10.16 -> 9.62 ms) while the key-only scatter is unchanged (2.28 / 2.31) and
 // the local split scatter loses (1.45 -> 1.54).
 template <class P, class = void>
+struct FilterOf : std::false_type {};
+template <class P>
+struct FilterOf<P, std::void_t<decltype(P::kFilter)>> : std::integral_constant<bool, P::kFilter> {};
+
+template <class P, class = void>
 struct EarlyOptIn : std::false_type {};
 template <class P>
 struct EarlyOptIn<P, std::void_t<decltype(P::kEarly)>> : std::integral_constant<bool, P::kEarly> {};
@@ -767,16 +794,21 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
   // EARLY: sw = staged words, dr = ranks (then positions); else dr = digit << 16 | rank.
   uint32_t dr[IPT];
   typename Pol::StageT sw[EARLY ? IPT : 1];
+  // FILT: tuples outside the pass's digit range (sentinel digit F) are neither
+  // ranked nor staged -- a pass over a quarter of the digits does a quarter of
+  // the LDS work; the scan's entry F then stays 0 and off[F] = kept.
+  constexpr bool FILT = FilterOf<Pol>::value;
 #pragma unroll
   for (int i = 0; i < IPT; ++i) {
     const uint32_t idx = i * NTH + t;
     if (FULL || idx < count) {
       const uint32_t d = pol.digit(v[i]);
+      const bool keep = !FILT || d < F;
       if constexpr (EARLY) {
-        dr[i] = atomicAdd(&l.cnt[d], 1u);
+        if (keep) dr[i] = atomicAdd(&l.cnt[d], 1u);
         sw[i] = pol.stage(v[i], d);
       } else {
-        dr[i] = (d << 16) | atomicAdd(&l.cnt[d], 1u);
+        dr[i] = (d << 16) | (keep ? atomicAdd(&l.cnt[d], 1u) : 0u);
       }
     }
   }
@@ -804,7 +836,11 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
   }
   if constexpr (EARLY) prefetchTile<Pol, NTH, IPT>(in, nbase, nlast, v);
   pf.mark(2);
-  blockExclusiveScanLds<NTH, uint32_t, uint32_t, true>(l.cnt, l.off, (int)F, l.wave);
+  // FILT: entry F (never counted) is scanned too: off[F] = kept tuples, and
+  // the write-out stops there.
+  blockExclusiveScanLds<NTH, uint32_t, uint32_t, true>(l.cnt, l.off, (int)F + (FILT ? 1 : 0), l.wave);
+  uint32_t kept = count;
+  if constexpr (FILT) kept = (uint32_t)__builtin_amdgcn_readfirstlane((int)l.off[F]);
   pf.mark(3);
   if constexpr (!CLAIM) {
     for (uint32_t d = t; d < F; d += NTH) {
@@ -820,12 +856,12 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
       const uint32_t idx = i * NTH + t;
-      if (FULL || idx < count) dr[i] += l.off[pol.stagedDigit(sw[i])];
+      if ((FULL || idx < count) && (!FILT || pol.stagedDigit(sw[i]) < F)) dr[i] += l.off[pol.stagedDigit(sw[i])];
     }
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
       const uint32_t idx = i * NTH + t;
-      if (FULL || idx < count) l.val[dr[i]] = sw[i];
+      if ((FULL || idx < count) && (!FILT || pol.stagedDigit(sw[i]) < F)) l.val[dr[i]] = sw[i];
     }
   } else {
     uint32_t pos[IPT];
@@ -837,7 +873,7 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
       const uint32_t idx = i * NTH + t;
-      if (FULL || idx < count) {
+      if ((FULL || idx < count) && (!FILT || (dr[i] >> 16) < F)) {
         const uint32_t d = dr[i] >> 16;
         l.val[pos[i]] = pol.stage(v[i], d);
         if constexpr (Pol::kDigArray) l.dig[pos[i]] = (uint16_t)d;
@@ -861,7 +897,10 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
 #pragma unroll
   for (int i = 0; i < IPT; ++i) {
     const uint32_t idx = i * NTH + t;
-    const bool have = FULL || idx < count;
+    if constexpr (FILT) {  // whole waves past the kept tuples skip on a scalar branch
+      if ((uint32_t)i * NTH + (t & ~(uint32_t)(WAVE - 1)) >= kept) continue;
+    }
+    const bool have = FILT ? idx < kept : (FULL || idx < count);
     const uint32_t at = have ? idx : 0;  // the tail tile's element 0 exists
     const typename Pol::StageT x = l.val[at];
     uint32_t d;
@@ -1010,8 +1049,9 @@ constexpr int CL_IPT = CL_IPT_DEFAULT;
 template <class Pol, int CL_IPT, int CL_NTH = 1024>
 static void launchNetClaimIpt(const Pol &pol, const data::Tuple *in, uint64_t n, uint32_t bits,
                               const PartitionGeometry &g, uint32_t blockBegin, uint32_t blockEnd, void *gcur,
-                              void *out, hipStream_t s, const void *gend, bool narrow) {
-  const uint32_t F = 1u << bits;
+                              void *out, hipStream_t s, const void *gend, bool narrow, uint32_t digits = 0) {
+  // digits: claim slices per group (filtered range passes); else 2^bits.
+  const uint32_t F = digits ? digits : 1u << bits;
   const auto *src = reinterpret_cast<const typename Pol::InT *>(in);
   auto *dst = reinterpret_cast<typename Pol::OutT *>(out);
   const dim3 grid(blockEnd - blockBegin);
@@ -1169,6 +1209,37 @@ void netScatterFrag(const data::Tuple *in, uint64_t n, uint32_t bits, const Part
     go(NetFragDigPolT<false>());
 }
 
+void netScatterFragRange(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g, void *gcur,
+                         uint32_t *out, hipStream_t s, uint32_t keyBits, KeyMix mix, const void *gend, bool narrow,
+                         uint32_t dLo, uint32_t range) {
+  HJ_CHECK(bits >= 1 && bits <= MAX_PART_BITS, "netScatterFragRange: bits=%u out of range", bits);
+  const uint32_t kb = mix.on ? std::max(keyBits, mix.bits) : keyBits;
+  HJ_CHECK(fragWordFits(kb, bits), "netScatterFragRange: %u-bit keys above %u radix bits", kb, bits);
+  // The sentinel digit `range` needs an LDS counter of its own: range < padDigits(range).
+  HJ_CHECK(range >= 1 && range < padDigits(range) && dLo + range <= (1u << bits) && gend,
+           "netScatterFragRange: digits [%u, %u) of %u (at most %u per pass, bounded slices)", dLo, dLo + range,
+           1u << bits, padDigits(1) - 1);
+  if (n == 0) return;
+  auto go = [&](auto pol) {
+    pol.mask = (1ull << bits) - 1;
+    pol.bits = bits;
+    pol.mix = mix;
+    pol.dLo = dLo;
+    pol.range = range;
+    launchNetClaimIpt<decltype(pol), CL_IPT_DEFAULT>(pol, in, n, bits, g, 0, g.blocks, gcur, out, s, gend, narrow,
+                                                     range);
+  };
+  const bool digitOnTop = kb <= 32;
+  if (mix.on && digitOnTop)
+    go(NetFragPolT<true, true>());
+  else if (digitOnTop)
+    go(NetFragPolT<false, true>());
+  else if (mix.on)
+    go(NetFragDigPolT<true, true>());
+  else
+    go(NetFragDigPolT<false, true>());
+}
+
 // ------------------------------------------------ device-side sampled layout
 // Turns the sampled per-(XCD group, digit) counts into bounded claim slices
 // on the device, so a sampled network pass needs no host round trip between
@@ -1190,9 +1261,11 @@ struct LayoutSideArgs {
 };
 
 // Workgroup i lays out side i (one or two sides per launch).
+// Digits [dLo, dLo + F) of totals laid out as [G][Fsrc] (a partition-group
+// pass lays out its range only; F = Fsrc, dLo = 0 otherwise).
 template <typename CurT>
 __global__ __launch_bounds__(LAY_NT) void netSampledLayoutKernel(LayoutSideArgs<CurT> s0, LayoutSideArgs<CurT> s1,
-                                                                  uint32_t F) {
+                                                                  uint32_t F, uint32_t Fsrc, uint32_t dLo) {
   const LayoutSideArgs<CurT> &ls = blockIdx.x ? s1 : s0;
   const unsigned long long *__restrict__ sampled = ls.sampled;
   const SampleScale &sc = ls.sc;
@@ -1218,13 +1291,13 @@ __global__ __launch_bounds__(LAY_NT) void netSampledLayoutKernel(LayoutSideArgs<
       double c = 0;
       if (seen > 0) {
         const double scale = total / seen;
-        const double est = (double)sampled[(size_t)g * F + d] * scale;
+        const double est = (double)sampled[(size_t)g * Fsrc + dLo + d] * scale;
         // sigma of a count scaled by `scale` from k samples: scale * sqrt(k);
         // at least one sample's worth (k = 0 says little about a cell).
         const double margin = sc.sigmas * sqrt(fmax(est, scale) * scale) + sc.frac * est + sc.floor;
         c = fmin(ceil(est + margin), total);
       }
-      if (ls.clear) ls.clear[(size_t)g * F + d] = 0;  // read once (above), by this thread
+      if (ls.clear) ls.clear[(size_t)g * Fsrc + dLo + d] = 0;  // read once (above), by this thread
       cap[k] = ((unsigned long long)c + 15ull) & ~15ull;
       local += cap[k];
     }
@@ -1258,16 +1331,19 @@ static LayoutSideArgs<CurT> layoutSide(const LayoutInput &x) {
                               x.clearSampled ? const_cast<unsigned long long *>(sampled) : nullptr};
 }
 
-void netSampledLayout(const LayoutInput *sides, uint32_t count, uint32_t F, bool narrow, hipStream_t s) {
+void netSampledLayout(const LayoutInput *sides, uint32_t count, uint32_t F, bool narrow, hipStream_t s, uint32_t dLo,
+                      uint32_t range) {
   HJ_CHECK(F >= 1 && F <= (1u << MAX_PART_BITS), "netSampledLayout: F=%u", F);
   HJ_CHECK(count == 1 || count == 2, "netSampledLayout: %u sides", count);
+  const uint32_t R = range ? range : F;
+  HJ_CHECK(dLo + R <= F, "netSampledLayout: digits [%u, %u) of %u", dLo, dLo + R, F);
   const LayoutInput &b = sides[count - 1];
   if (narrow)
     hipLaunchKernelGGL(netSampledLayoutKernel<uint32_t>, dim3(count), dim3(LAY_NT), 0, s,
-                       layoutSide<uint32_t>(sides[0]), layoutSide<uint32_t>(b), F);
+                       layoutSide<uint32_t>(sides[0]), layoutSide<uint32_t>(b), R, F, dLo);
   else
     hipLaunchKernelGGL(netSampledLayoutKernel<unsigned long long>, dim3(count), dim3(LAY_NT), 0, s,
-                       layoutSide<unsigned long long>(sides[0]), layoutSide<unsigned long long>(b), F);
+                       layoutSide<unsigned long long>(sides[0]), layoutSide<unsigned long long>(b), R, F, dLo);
   HIP_CHECK_LAUNCH();
 }
 

@@ -49,7 +49,8 @@ void passCounts(const data::Tuple *in, uint64_t n, uint32_t K, unsigned long lon
 constexpr int CI = 16;
 __global__ __launch_bounds__(PT) void passCompactKernel(const ulonglong2 *__restrict__ in, uint64_t n, uint32_t K,
                                                          uint32_t k, ulonglong2 *__restrict__ out,
-                                                         unsigned long long *__restrict__ cursor) {
+                                                         unsigned long long *__restrict__ cursor,
+                                                         unsigned long long capacity) {
   __shared__ uint32_t waveTot[PT / WAVE];
   __shared__ unsigned long long base;
   const uint32_t t = threadIdx.x, lane = t & (WAVE - 1), wid = t / WAVE;
@@ -84,19 +85,24 @@ __global__ __launch_bounds__(PT) void passCompactKernel(const ulonglong2 *__rest
     uint32_t j = 0;
 #pragma unroll
     for (int i = 0; i < CI; ++i)
-      if (take & (1u << i)) out[at + j++] = v[i];
+      if (take & (1u << i)) {
+        // Never past the pass buffer: a count that drifted from the plan's
+        // (relation changed after planning) shows as cursor != count on the host.
+        if (at + j < capacity) out[at + j] = v[i];
+        ++j;
+      }
     __syncthreads();  // waveTot / base reused by the next tile
   }
 }
 
 void passCompact(const data::Tuple *in, uint64_t n, uint32_t K, uint32_t k, data::Tuple *out,
-                 unsigned long long *cursor, hipStream_t s) {
+                 unsigned long long *cursor, hipStream_t s, uint64_t capacity) {
   HJ_CHECK(K >= 1 && K <= MAX_SPILL_PASSES && k < K, "passCompact: pass %u of %u", k, K);
   if (n == 0) return;
   const uint64_t tiles = (n + (uint64_t)PT * CI - 1) / ((uint64_t)PT * CI);
   const uint32_t grid = (uint32_t)std::min<uint64_t>(2048, tiles);
   hipLaunchKernelGGL(passCompactKernel, dim3(grid), dim3(PT), 0, s, reinterpret_cast<const ulonglong2 *>(in), n, K,
-                     k, reinterpret_cast<ulonglong2 *>(out), cursor);
+                     k, reinterpret_cast<ulonglong2 *>(out), cursor, (unsigned long long)capacity);
   HIP_CHECK_LAUNCH();
 }
 

@@ -57,6 +57,10 @@ HashJoin::~HashJoin() {
   }
 }
 
+// Per-pass bytes outside the estimate's scaling (plans, histograms, cursors):
+// 256 MB, or a quarter of small budgets.
+static double spillFixedBytes(uint64_t avail) { return std::min<double>(256.0 * (1 << 20), avail / 4.0); }
+
 // Capacity spill.  A join whose workspace estimate exceeds what HBM has free
 // (or config.workspaceBudget) runs in K passes over the key-hash classes
 // kernels::passOf: pass k holds ~1/K of both relations (compacted into pass
@@ -82,41 +86,87 @@ void HashJoin::planPasses() {
       const uint64_t est = workspaceEstimate(), tuplesB = (n[0] + n[1]) * sizeof(data::Tuple);
       spill.estimate = est;
       spill.available = avail;
-      if (est > avail) {
+      if (est > avail && plan.bitmapJoin && numberOfNodes == 1) {
+        // The bitmap plan spills by partition groups instead (tasks/BitmapJoin):
+        // each group pass reads both relations once and writes only the
+        // fragments of its network partitions -- no pass buffers, no
+        // compaction, and the group count follows from the sampled totals.
+        const uint64_t fixed = 96ull << 20;  // plans, cursors, counters (the estimate's first part)
+        plan.groupBudget = avail > 2 * fixed ? avail - fixed : avail / 2;
+        spill.groupBudget = plan.groupBudget;
+      } else if (est > avail) {
         K = 2;
         while (K < kernels::MAX_SPILL_PASSES &&
-               (double)est / K * 1.6 + (double)tuplesB / K * 1.05 + (256u << 20) > (double)avail)
+               (double)est / K * 1.6 + (double)tuplesB / K * 1.05 + spillFixedBytes(avail) > (double)avail)
           ++K;
       }
     }
   }
   K = std::max<uint32_t>(1, std::min<uint32_t>(K, kernels::MAX_SPILL_PASSES));
-  {  // every rank runs the same number of passes
+  auto agreeMax = [&](uint32_t mine) {  // every rank runs the same number of passes
     std::vector<uint64_t> all(numberOfNodes);
-    const uint64_t mine = K;
-    ctx->comm()->allGatherHost(&mine, all.data(), 1);
-    for (uint64_t k : all) K = std::max<uint32_t>(K, (uint32_t)k);
-  }
+    const uint64_t m = mine;
+    ctx->comm()->allGatherHost(&m, all.data(), 1);
+    for (uint64_t k : all) mine = std::max<uint32_t>(mine, (uint32_t)k);
+    return mine;
+  };
+  K = agreeMax(K);
   passes = K;
   if (K == 1) return;
   JOIN_ASSERT(!plan.materialize, "HashJoin", "capacity spill (%u passes) runs counting joins only", K);
   data::Relation *rel[2] = {innerRelation, outerRelation};
-  std::vector<uint64_t> counts(2 * (size_t)K, 0);
-  if (ctx->onDevice()) {
-    auto *d = ctx->workspace().getArray<unsigned long long>(2 * (size_t)K);
-    ctx->zero(d, 2 * (size_t)K * 8);
-    for (int r = 0; r < 2; ++r) kernels::passCounts(rel[r]->getData(), n[r], K, d + (size_t)r * K, ctx->stream());
-    HIP_CHECK(hipMemcpyAsync(counts.data(), d, 2 * (size_t)K * 8, hipMemcpyDeviceToHost, ctx->stream()));
-    utils::waitStream(ctx->stream(), ctx->comm(), "pass counts");
-    ctx->workspace().reset();
-  } else {
-    for (int r = 0; r < 2; ++r) {
-      const data::Tuple *t = rel[r]->getData();
-      for (uint64_t i = 0; i < n[r]; ++i) ++counts[(size_t)r * K + kernels::passOf(t[i].key, K)];
+  std::vector<uint64_t> counts, global;
+  auto countPasses = [&](uint32_t k) {
+    counts.assign(2 * (size_t)k, 0);
+    if (ctx->onDevice()) {
+      auto *d = ctx->workspace().getArray<unsigned long long>(2 * (size_t)k);
+      ctx->zero(d, 2 * (size_t)k * 8);
+      for (int r = 0; r < 2; ++r) kernels::passCounts(rel[r]->getData(), n[r], k, d + (size_t)r * k, ctx->stream());
+      HIP_CHECK(hipMemcpyAsync(counts.data(), d, 2 * (size_t)k * 8, hipMemcpyDeviceToHost, ctx->stream()));
+      utils::waitStream(ctx->stream(), ctx->comm(), "pass counts");
+      ctx->workspace().reset();
+    } else {
+      for (int r = 0; r < 2; ++r) {
+        const data::Tuple *t = rel[r]->getData();
+        for (uint64_t i = 0; i < n[r]; ++i) ++counts[(size_t)r * k + kernels::passOf(t[i].key, k)];
+      }
     }
+    global = counts;
+    ctx->comm()->allReduceSumHost(global.data(), global.size());
+  };
+  countPasses(K);
+  // Key-hash classes are balanced only for spread keys: every copy of a hot
+  // key lands in one pass (Zipf, repeated inner keys).  The largest pass's
+  // buffers and its share of the workspace must fit what the planner assumed
+  // for 1/K of the data; otherwise K grows (recount) until it does.  A single
+  // key class too big for memory on its own is refused here, not by a failed
+  // allocation inside the join.
+  if (config.passes == 0 && spill.available) {
+    const double total = (double)(n[0] + n[1]) + 1.0;
+    for (;;) {
+      uint64_t worst = 0;
+      for (uint32_t k = 0; k < K; ++k) worst = std::max<uint64_t>(worst, counts[k] + counts[K + k]);
+      const double share = (double)worst / total;  // of this rank's tuples
+      const double need = (double)spill.estimate * share * 1.6 + (double)worst * sizeof(data::Tuple) * 1.05 +
+                          spillFixedBytes(spill.available);
+      const bool fits = need <= (double)spill.available;
+      // Every rank decides the same next K (the max over ranks).
+      uint32_t next = fits ? K : std::min<uint32_t>(kernels::MAX_SPILL_PASSES, K + std::max<uint32_t>(1, K / 2));
+      next = agreeMax(next);
+      if (next == K) {
+        // At the pass limit a balanced class is run anyway (best effort, the
+        // estimate's margins); a class far above 1/K is one hot key: refused.
+        HJ_CHECK(fits || share < 4.0 / kernels::MAX_SPILL_PASSES,
+                 "capacity spill: the largest key-hash class holds %lu of %lu tuples and needs %.1f GB, more than "
+                 "the %.1f GB available to one pass even at %u passes (one key too frequent to spill)",
+                 (unsigned long)worst, (unsigned long)(n[0] + n[1]), need / 1e9, spill.available / 1e9, K);
+        break;
+      }
+      K = next;
+      countPasses(K);
+    }
+    passes = K;
   }
-  std::vector<uint64_t> global(counts);
-  ctx->comm()->allReduceSumHost(global.data(), global.size());
   for (int r = 0; r < 2; ++r) {
     passCount[r].assign(counts.begin() + (size_t)r * K, counts.begin() + (size_t)(r + 1) * K);
     passGlobal[r].assign(global.begin() + (size_t)r * K, global.begin() + (size_t)(r + 1) * K);
@@ -124,7 +174,8 @@ void HashJoin::planPasses() {
     if (passBuf[r]) memory::Arena::rawFree(ctx->location(), passBuf[r]);
     passBuf[r] = static_cast<data::Tuple *>(
         memory::Arena::rawAlloc(ctx->location(), std::max<uint64_t>(cap, 1) * sizeof(data::Tuple), ctx->device()));
-    spill.passBuffers += std::max<uint64_t>(cap, 1) * sizeof(data::Tuple);
+    passCap[r] = std::max<uint64_t>(cap, 1);
+    spill.passBuffers += passCap[r] * sizeof(data::Tuple);
   }
   JOIN_DEBUG("HashJoin", "capacity spill: %u passes", K);
 }
@@ -150,8 +201,16 @@ JoinResult HashJoin::runPasses() {
       auto *cur = ctx->workspace().getArray<unsigned long long>(2);
       ctx->zero(cur, 16);
       for (int r = 0; r < 2; ++r)
-        kernels::passCompact(rel[r]->getData(), rel[r]->getLocalSize(), passes, k, passBuf[r], cur + r, ctx->stream());
+        kernels::passCompact(rel[r]->getData(), rel[r]->getLocalSize(), passes, k, passBuf[r], cur + r, ctx->stream(),
+                             passCap[r]);
+      auto *curBack = ctx->staging().getArray<unsigned long long>(2);
+      ctx->readBack(curBack, cur, 16);
       utils::waitStream(ctx->stream(), ctx->comm(), "pass compaction");
+      for (int r = 0; r < 2; ++r)
+        JOIN_ASSERT(curBack[r] == passCount[r][k], "HashJoin",
+                    "capacity spill: pass %u compacted %lu %s tuples, the plan counted %lu (relation changed since "
+                    "planning?)",
+                    k, (unsigned long)curBack[r], r ? "outer" : "inner", (unsigned long)passCount[r][k]);
     } else {
       for (int r = 0; r < 2; ++r) {
         const data::Tuple *t = rel[r]->getData();

@@ -47,6 +47,9 @@ struct JoinResult {
   uint64_t exchangeChecked = 0;    // (source, chunk, partition) runs whose content was verified (verifyExchange)
   uint32_t passes = 1;             // capacity spill: key-hash passes the join ran in (JoinConfig::passes)
   double compactMs = 0;            // capacity spill: host wall of the per-pass compaction (in joinMs)
+  // Capacity spill of the bitmap plan: partition-group passes of the last
+  // join (each reads both relations once and writes only its digit range).
+  uint32_t groupPasses = 0;
   uint64_t innerReceived = 0, outerReceived = 0;
   uint64_t wireBytes = 0;          // bytes this rank sent to peers (after the wire codec)
   uint64_t localItems = 0, buildProbeItems = 0;
@@ -158,6 +161,7 @@ class HashJoin {
   uint32_t passes = 1;
   std::vector<uint64_t> passCount[2], passGlobal[2];
   data::Tuple *passBuf[2] = {nullptr, nullptr};
+  uint64_t passCap[2] = {0, 0};  // tuples each pass buffer holds
   uint64_t planMaxKey = 0, planMaxRid = 0;
  public:
   // The capacity planner's inputs and outcome (bytes): single-pass workspace
@@ -166,6 +170,7 @@ class HashJoin {
   // and reservation (filled in by runPasses).
   struct SpillInfo {
     uint64_t estimate = 0, available = 0, passBuffers = 0, passEstimate = 0, passReserved = 0, passPeak = 0;
+    uint64_t groupBudget = 0;  // bitmap plan: fragment-window bytes of one partition-group pass (0 = none)
   } spill;
  private:
   uint64_t outputEpoch = 0;  // workspace epoch when `output` was written

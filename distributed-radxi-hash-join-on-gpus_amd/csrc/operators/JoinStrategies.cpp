@@ -316,6 +316,7 @@ bool BitmapPlan::run(uint64_t t0, JoinResult &r) {
   const uint64_t t4 = nowUs();
   ctx->timeline().resolve();  // BitmapJoin synchronised all streams
   r.bitmapJoin = true;
+  r.groupPasses = o.groupPasses;
   r.sampledNetwork = !exact;
   r.localMatches = o.localMatches;
   r.globalMatches = o.globalMatches;

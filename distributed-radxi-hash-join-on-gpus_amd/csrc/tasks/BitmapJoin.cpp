@@ -1,6 +1,7 @@
 #include "BitmapJoin.h"
 
 #include <algorithm>
+#include <cmath>
 #include <map>
 #include <tuple>
 #include <cstdlib>
@@ -157,7 +158,166 @@ static uint32_t reduceChunks(uint64_t bitmapBytes, uint32_t forced) {
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4, bitmapBytes >> 25));
 }
 
+BitmapJoin::Outcome BitmapJoin::runDeviceGroups(bool exact) {
+  const uint32_t nb = plan.networkBits, F = 1u << nb, G = CLAIM_GROUPS, bits = plan.bitmapBits;
+  const hipStream_t st = ctx->stream();
+  memory::Arena &ws = ctx->workspace();
+  const kernels::KeyMix mix{plan.keyMix ? 1u : 0u, plan.keyBits};
+  performance::Timeline &tl = ctx->timeline();
+  useControl = false;
+  auto *cnt = ws.getArray<BitmapCounters>(1);
+  ctx->zero(cnt, sizeof(BitmapCounters));
+  Side both[2] = {Side{inner, {}, nullptr, {}}, Side{outer, {}, nullptr, {}}};
+  // 1. Totals of every digit of both sides (sampled, or exact), read back once.
+  uint64_t *totals = ws.getArray<uint64_t>((uint64_t)2 * G * F);
+  kernels::SampleScale sc[2];
+  {
+    kernels::SampledInput in[2];
+    bool sampled = !exact;
+    for (int i = 0; i < 2; ++i) {
+      const uint64_t n = both[i].relation->getLocalSize();
+      const SidePlan &sp = sidePlan(n, exact, sampleStride);
+      both[i].geom = sp.geom;
+      sc[i] = sp.sc;
+      sampled = sampled && sp.stride > 1;
+      in[i] = kernels::SampledInput{both[i].relation->getData(), n, sp.geom, sp.stride, totals + (size_t)i * G * F};
+    }
+    utils::faultPoint("network");
+    tl.beginSplitAt("HLOCAL", "HILOCAL", (double)inner->getLocalSize(), "HOLOCAL", (double)outer->getLocalSize(),
+                    ev[0]);
+    if (sampled) {
+      kernels::netSampledTotals(in, 2, nb, st, mix, false);
+    } else {
+      for (int i = 0; i < 2; ++i) {
+        uint32_t *blockHist = ws.getArray<uint32_t>((uint64_t)F * in[i].geom.blocks);
+        kernels::netHistogram(in[i].data, in[i].n, nb, in[i].geom, blockHist, st, mix, 1);
+        kernels::netGroupTotals(blockHist, F, in[i].geom.blocks, in[i].totals, st);
+        if (in[i].stride > 1) sc[i] = sidePlan(in[i].n, exact, 1).sc;  // every tile counted now
+      }
+    }
+  }
+  uint64_t *back = ctx->staging().getArray<uint64_t>((uint64_t)2 * G * F);
+  ctx->readBack(back, totals, (size_t)2 * G * F * 8);
+  HIP_CHECK(hipEventRecord(ev[1], st));
+  tl.endAt("HLOCAL", ev[1]);
+  utils::waitEvent(ev[1], ctx->comm(), "bitmap group totals");
+  // 2. Slice capacities per digit (netSampledLayoutKernel's formula, plus one
+  // line per slice against rounding differences), then groups of consecutive
+  // digits whose two windows fit the budget.  A group has fewer than 1024
+  // digits (netScatterFragRange keeps one sentinel counter in LDS).
+  std::vector<uint64_t> digitCap[2];
+  for (int i = 0; i < 2; ++i) {
+    digitCap[i].assign(F, 0);
+    for (uint32_t g = 0; g < G; ++g) {
+      const double seen = sc[i].seen[g], total = sc[i].total[g];
+      if (!(seen > 0)) continue;
+      const double scale = total / seen;
+      for (uint32_t d = 0; d < F; ++d) {
+        const double est = (double)back[((size_t)i * G + g) * F + d] * scale;
+        const double margin = sc[i].sigmas * std::sqrt(std::max(est, scale) * scale) + sc[i].frac * est + sc[i].floor;
+        const uint64_t c = (uint64_t)std::min(std::ceil(est + margin), total);
+        digitCap[i][d] += ((c + 15) & ~15ull) + 16;
+      }
+    }
+  }
+  struct Group {
+    uint32_t lo = 0, n = 0;
+    uint64_t cap[2] = {0, 0};
+  };
+  std::vector<Group> groups;
+  const uint64_t budget = std::max<uint64_t>(plan.groupBudget / 4, 1);  // u32 fragments
+  const uint32_t maxRange = 512;
+  Group cur;
+  for (uint32_t d = 0; d < F; ++d) {
+    const uint64_t add = digitCap[0][d] + digitCap[1][d];
+    HJ_CHECK(add <= budget, "capacity spill: network partition %u needs %lu fragment slots, the budget holds %lu", d,
+             (unsigned long)add, (unsigned long)budget);
+    if (cur.n && (cur.cap[0] + cur.cap[1] + add > budget || cur.n == maxRange)) {
+      groups.push_back(cur);
+      cur = Group();
+      cur.lo = d;
+    }
+    ++cur.n;
+    cur.cap[0] += digitCap[0][d];
+    cur.cap[1] += digitCap[1][d];
+  }
+  groups.push_back(cur);
+  uint64_t maxCap[2] = {0, 0};
+  for (const Group &g : groups)
+    for (int i = 0; i < 2; ++i) maxCap[i] = std::max(maxCap[i], g.cap[i]);
+  // One cursor width for both sides (claims may run past a slice end by up to n).
+  const bool narrow = kernels::cursorsNarrow(maxCap[0] + inner->getLocalSize()) &&
+                      kernels::cursorsNarrow(maxCap[1] + outer->getLocalSize());
+  const size_t cb = narrow ? 4 : 8;
+  kernels::LayoutInput lay[2];
+  for (int i = 0; i < 2; ++i) {
+    Side &sd = both[i];
+    sd.frags = ws.getArray<uint32_t>(maxCap[i] + 4096);
+    lay[i].sampled = totals + (size_t)i * G * F;
+    lay[i].sc = sc[i];
+    lay[i].gstart = ws.get((size_t)G * maxRange * cb);
+    lay[i].gcur = ws.get((size_t)G * maxRange * cb);
+    lay[i].gend = ws.get((size_t)G * maxRange * cb);
+    lay[i].capacityUsed = ws.getArray<unsigned long long>(1);
+    lay[i].clearSampled = false;
+    sd.slices = BitmapSlices();
+    sd.slices.kind = BitmapSlices::Claim;
+    sd.slices.start = lay[i].gstart;
+    sd.slices.cur = lay[i].gcur;
+    sd.slices.end = lay[i].gend;
+    sd.slices.narrow = narrow;
+    sd.slices.threads = plan.variants.bmThreads;
+    sd.slices.flat = plan.variants.bmFlat;
+  }
+  // 3. One pass per group: lay out its slices, scatter its digits of both
+  // relations, join its bitmaps (the counters accumulate).
+  tl.beginAt("MIMAINPART", ev[1]);
+  for (size_t k = 0; k < groups.size(); ++k) {
+    const Group &g = groups[k];
+    kernels::netSampledLayout(lay, 2, F, narrow, st, g.lo, g.n);
+    for (int i = 0; i < 2; ++i) {
+      Side &sd = both[i];
+      sd.slices.count = g.cap[i];  // the bitmap kernels' flat-walk choice: tuples per partition
+      kernels::netScatterFragRange(sd.relation->getData(), sd.relation->getLocalSize(), nb, sd.geom,
+                                   const_cast<void *>(sd.slices.cur), sd.frags, st, plan.keyBits, mix, sd.slices.end,
+                                   narrow, g.lo, g.n);
+    }
+    if (k + 1 == groups.size()) {
+      HIP_CHECK(hipEventRecord(ev[2], st));
+      tl.endAt("MIMAINPART", ev[2]);
+      utils::faultPoint("local");
+      utils::faultPoint("build_probe");
+    }
+    kernels::bitmapJoin(4, both[0].frags, both[1].frags, both[0].slices, both[1].slices, g.n, 0, bits, cnt, st);
+  }
+  HIP_CHECK(hipEventRecord(ev[4], st));
+  tl.beginAt("BPTASKTIME", ev[2]);
+  tl.endAt("BPTASKTIME", ev[4]);
+  performance::Measurements::add("BPBUILDELEM", (double)inner->getLocalSize(), "tuples");
+  performance::Measurements::add("BPPROBEELEM", (double)outer->getLocalSize(), "tuples");
+  BitmapCounters *res = ctx->staging().getArray<BitmapCounters>(1);
+  const uint64_t tEnqueued = performance::nowUs();
+  ctx->readBack(res, cnt, sizeof(BitmapCounters));
+  ctx->synchronize();
+  Outcome o;
+  o.hostWaitMs = (performance::nowUs() - tEnqueued) / 1000.0;
+  o.enqueueUs = tEnqueued;
+  o.groupPasses = (uint32_t)groups.size();
+  float ms = 0;
+  HIP_CHECK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+  o.devSampleMs = ms;
+  HIP_CHECK(hipEventElapsedTime(&ms, ev[1], ev[2]));
+  o.devScatterMs = ms;
+  HIP_CHECK(hipEventElapsedTime(&ms, ev[2], ev[4]));
+  o.devJoinMs = ms;
+  o.localMatches = res->matches;
+  o.popcount = res->popcount;
+  agree(o, (res->dup ? kernels::BM_FLAG_DUP : 0u) | (res->overflow ? kernels::BM_FLAG_OVERFLOW : 0u));
+  return o;
+}
+
 BitmapJoin::Outcome BitmapJoin::runDevice(bool exact) {
+  if (plan.groupBudget && ctx->numberOfNodes() == 1) return runDeviceGroups(exact);
   const uint32_t F = 1u << plan.networkBits, N = ctx->numberOfNodes(), bits = plan.bitmapBits;
   const hipStream_t st = ctx->stream();
   memory::Arena &ws = ctx->workspace();

@@ -32,6 +32,16 @@
 //   dup       a repeated inner key (or a fragment out of range): the caller
 //             redoes the join on the two-level pass
 // The host path (CPU, tests) runs the same plan with exact partitioning.
+//
+// Capacity spill (N = 1, JoinPlan::groupBudget): when both sides' fragment
+// windows exceed the memory budget, the sampled totals are read back once and
+// the network partitions cut into groups whose windows fit it; each group is
+// one pass: both relations are read and only the group's digits are scattered
+// (kernels::netScatterFragRange), then the group's bitmaps join.  Reference:
+// the large-data drivers process the input per iteration with one histogram
+// for all of them (operators/gpu/kernels.cu:563-857, data/data.hpp:67-83);
+// here an iteration is a range of network partitions, so no pass buffer or
+// compaction pass exists and equal keys always meet in the same pass.
 #pragma once
 
 #include <cstdint>
@@ -56,6 +66,7 @@ class BitmapJoin {
     double devSampleMs = 0, devScatterMs = 0, devJoinMs = 0;  // hipEvents (device engine)
     uint64_t enqueueUs = 0;    // host clock when the last kernel of the join was enqueued
     double hostWaitMs = 0;     // host wait from there to the result (mailbox spin + stream sync)
+    uint32_t groupPasses = 0;  // partition-group passes (JoinPlan::groupBudget), 0 = one pass
   };
 
   // ev: 5 timing events of the caller (ev[0] already recorded at join start).
@@ -85,6 +96,9 @@ class BitmapJoin {
   void scatterSide(Side &s);
   bool sideNarrow(data::Relation *r, bool exact) const;
   Outcome runDevice(bool exact);
+  // Capacity spill (JoinPlan::groupBudget, N = 1): the network partitions in
+  // groups whose fragment windows fit the budget, one pass per group.
+  Outcome runDeviceGroups(bool exact);
   Outcome runHost();
   void agree(Outcome &o, uint64_t localFlags);
 

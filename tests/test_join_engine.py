@@ -617,21 +617,69 @@ def test_capacity_spill_passes(C, dev, passes, outer_dist, sparse):
 
 
 @pytest.mark.gpu
-def test_capacity_spill_auto_budget(C, cuda):
-    """workspace_budget below the plan's estimate: the planner picks K > 1
-    passes by itself and the join stays exact."""
+@pytest.mark.parametrize("sparse,outer_dist", [(False, "UNIQUE"), (False, "ZIPF"), (True, "UNIQUE")])
+def test_capacity_spill_auto_budget(C, cuda, sparse, outer_dist):
+    """workspace_budget below the plan's estimate: the planner spills by
+    itself and the join stays exact.  Dense unique inner keys (the bitmap
+    plan) spill by partition groups -- each group pass reads both relations
+    once and writes only its network partitions' fragments; random 63-bit
+    keys (the two-level plan) spill by key-hash passes."""
     ctx = C.ExecContext("device", 0, C.LocalCommunicator())
     G = 1 << 24
     R = C.Relation(G, G, "device", 0)
     S = C.Relation(G, G, "device", 0)
-    R.generate(C.GenSpec(seed=1234), 0)
-    S.generate(C.GenSpec(seed=4321), 0)
+    inner = C.GenSpec(seed=1234)
+    outer = C.GenSpec(distribution=getattr(C.KeyDistribution, outer_dist), seed=4321,
+                      domain=0 if outer_dist == "UNIQUE" else G, zipf_theta=0.75)
+    inner.sparse64 = outer.sparse64 = sparse
+    R.generate(inner, 0)
+    S.generate(outer, 0)
+    exp = C.Relation.expected_matches(inner, G, outer, G)
     full = C.HashJoin(R, S, ctx, C.JoinConfig())
     est = full.workspace_estimate()
+    single = full.run()["global_matches"]
+    assert single == exp
+    bitmap = full.plan.bitmap_join
     del full
     cfg = C.JoinConfig()
     cfg.workspace_budget = est // 4
     j = C.HashJoin(R, S, ctx, cfg)
-    assert j.spill_passes >= 4, (j.spill_passes, est)
-    res = j.run()
-    assert res["global_matches"] == G and res["passes"] == j.spill_passes
+    for _ in range(2):
+        res = j.run()
+        assert res["global_matches"] == exp, res
+    if bitmap:
+        assert j.spill_passes == 1 and res["group_passes"] >= 4, (res["group_passes"], est)
+        assert j.spill_info["group_budget_bytes"] > 0 and res["bitmap_join"]
+    else:
+        assert j.spill_passes >= 4 and res["passes"] == j.spill_passes, (j.spill_passes, est)
+
+
+@pytest.mark.gpu
+def test_capacity_spill_skewed_inner_key_classes(C, cuda):
+    """Zipf inner keys under a workspace budget: every copy of a
+    hot key lands in one key-hash pass, so the largest pass is far above 1/K of
+    the data.  The planner counts the passes, grows K until the largest one
+    fits, and the join stays exact; a key too frequent for any pass count is
+    refused with a clear message instead of failing an allocation."""
+    import torch
+    from helpers import ref_join_count
+    ctx = C.ExecContext("device", 0, C.LocalCommunicator())
+    G = 1 << 22
+    R = C.Relation(G, G, "device", 0)
+    S = C.Relation(G, G, "device", 0)
+    R.generate(C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=11, domain=4096, zipf_theta=0.9), 0)
+    S.generate(C.GenSpec(distribution=C.KeyDistribution.UNIFORM, seed=12, domain=4096), 0)
+    exp = ref_join_count(R.to_tensor()[:, 0], S.to_tensor()[:, 0])
+    est = C.HashJoin(R, S, ctx, C.JoinConfig()).workspace_estimate()
+    cfg = C.JoinConfig()
+    cfg.workspace_budget = est // 4
+    j = C.HashJoin(R, S, ctx, cfg)
+    assert j.spill_passes >= 4
+    assert j.run()["global_matches"] == exp
+    # Two keys only: one key-hash class holds about half the tuples at any K.
+    R2 = C.Relation(G, G, "device", 0)
+    R2.generate(C.GenSpec(distribution=C.KeyDistribution.UNIFORM, seed=13, domain=2), 0)
+    est2 = C.HashJoin(R2, S, ctx, C.JoinConfig()).workspace_estimate()
+    cfg.workspace_budget = est2 // 16
+    with pytest.raises(RuntimeError, match="too frequent to spill"):
+        C.HashJoin(R2, S, ctx, cfg)

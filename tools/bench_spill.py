@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Capacity spill benchmark: a join whose relations plus workspace exceed
 what HBM holds (or a forced workspace budget) runs in K key-hash passes
-(JoinConfig.passes, kernels/spill.hip).  One JSON line per configuration.
+(JoinConfig.passes, kernels/spill.hip) or, for the bitmap plan, in partition-
+group passes (tasks/BitmapJoin: `group_passes`).  One JSON line per configuration.
 
     python tools/bench_spill.py --size 1e9 --budget-frac 0.25      # 1B x 1B, workspace budget = estimate / 4
     python tools/bench_spill.py --size 6e9                          # 6B x 6B in HBM: 192 GB of relations
@@ -62,7 +63,7 @@ def main():
                           "single_pass_workspace_estimate_GB": round(est / 1e9, 1),
                           "hbm_free_after_relations_GB": round(free0 / 1e9, 1)}), flush=True)
         raise
-    times, res = [], None
+    times, res = [], first
     for _ in range(args.steps):
         t0 = time.perf_counter()
         res = j.run()
@@ -71,7 +72,7 @@ def main():
            "hbm_total_GB": round(total / 1e9, 1), "hbm_free_after_relations_GB": round(free0 / 1e9, 1),
            "single_pass_workspace_estimate_GB": round(est / 1e9, 1),
            "workspace_budget_GB": round(cfg.workspace_budget / 1e9, 1) if cfg.workspace_budget else None,
-           "passes": j.spill_passes, "setup_ms": round(setup_ms, 1), "first_join_ms": round(first["join_ms"], 2),
+           "passes": j.spill_passes, "group_passes": res["group_passes"] if res else None, "setup_ms": round(setup_ms, 1), "first_join_ms": round(first["join_ms"], 2),
            "ms_per_join": round(sum(times) / len(times), 2), "join_ms": [round(t, 2) for t in times],
            "compact_ms": round(res["compact_ms"], 2), "value_Gtuples_per_s": round(2 * G / (sum(times) / len(times)) / 1e6, 2),
            "matches": res["global_matches"], "expected_matches": G, "correct": res["global_matches"] == G,
