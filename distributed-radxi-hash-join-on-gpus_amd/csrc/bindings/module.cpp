@@ -691,6 +691,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("local_geometry", &core::JoinConfig::localGeometry)
       .def_readwrite("local_sample_stride", &core::JoinConfig::localSampleStride)
       .def_readwrite("output_capacity", &core::JoinConfig::outputCapacity)
+      .def_property(
+          "output_host", [](const core::JoinConfig &c) { return (uint64_t)(uintptr_t)c.outputHost; },
+          [](core::JoinConfig &c, uint64_t addr) { c.outputHost = reinterpret_cast<void *>((uintptr_t)addr); },
+          "address of a pinned host buffer of output_capacity (rid, rid) pairs (e.g. hpcjoin.pinned_pairs(n)): a "
+          "materializing join writes its pairs there instead of the workspace (0 = workspace)")
       .def_readwrite("build_target", &core::JoinConfig::buildTarget)
       .def_readwrite("r_chunk", &core::JoinConfig::rChunk)
       .def_readwrite("s_chunk", &core::JoinConfig::sChunk)
@@ -1172,14 +1177,25 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           HJ_CHECK(j.outputValid(),
                    "HashJoin.output(): the pairs of the last run were in the engine workspace, which a later join, "
                    "plan or trim_workspace on the same context has since reused; read output() right after run()");
-          if (j.context()->onDevice())
-            HIP_CHECK(hipMemcpy(out.data_ptr(), j.getOutput(), n * 16, hipMemcpyDeviceToHost));
+          if (j.context()->onDevice())  // workspace pairs, or the pinned host buffer (outputHost)
+            HIP_CHECK(hipMemcpy(out.data_ptr(), j.getOutput(), n * 16, hipMemcpyDefault));
           else
             std::memcpy(out.data_ptr(), j.getOutput(), n * 16);
         }
         return out;
       });
   m.def("result_counter", []() { return operators::HashJoin::RESULT_COUNTER; });
+  m.def(
+      "pinned_pairs",
+      [](uint64_t n) {
+        // Page-locked, device-mapped host memory for JoinConfig.output_host:
+        // the place kernel writes pairs into it over the host link.
+        void *p = nullptr;
+        HIP_CHECK(hipHostMalloc(&p, std::max<uint64_t>(n, 1) * 16, hipHostMallocMapped | hipHostMallocPortable));
+        return at::from_blob(
+            p, {(int64_t)n, 2}, [](void *q) { (void)hipHostFree(q); }, at::TensorOptions().dtype(at::kLong));
+      },
+      py::arg("pairs"), "A pinned, device-mapped host tensor [pairs, 2] (int64) for JoinConfig.output_host");
 
   auto fault = m.def_submodule("fault", "failure detection and fault injection");
   py::register_exception<utils::InjectedFault>(fault, "InjectedFault", PyExc_RuntimeError);

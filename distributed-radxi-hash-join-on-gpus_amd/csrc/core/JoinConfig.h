@@ -75,6 +75,14 @@ struct JoinConfig {
   TupleFormat format = TupleFormat::Compressed;
   bool materialize = false;   // also write (rid_inner, rid_outer) pairs
   uint64_t outputCapacity = 0;  // materialize: pair capacity (0 = auto from oracle bound)
+  // materialize: write the (rid_inner, rid_outer) pairs straight into this
+  // caller-owned pinned host buffer of outputCapacity pairs (device-mapped:
+  // the place kernel stores over the host link), not into the workspace --
+  // the output of a join may then exceed HBM, and a materializing join can
+  // spill (capacity passes append to it).  The reference's UVA driver writes
+  // its probe output to host memory the same way
+  // (operators/gpu/small_data_optimized.cu:1193-1195).
+  void *outputHost = nullptr;
   uint64_t buildTarget = 4096;  // target inner tuples per final partition (= one 256 x 16 LDS build batch)
   uint32_t rChunk = 0;          // max inner tuples per LDS table (0 = auto from LDS budget)
   uint32_t sChunk = 65536;      // max outer tuples per build/probe work item

@@ -73,7 +73,9 @@ void HashJoin::planPasses() {
   const uint64_t n[2] = {innerRelation->getLocalSize(), outerRelation->getLocalSize()};
   if (K == 0) {
     K = 1;
-    if (ctx->onDevice() && config.reserveWorkspace && !plan.materialize) {
+    // Materializing joins spill only into a host output buffer (the pairs of
+    // all passes together may exceed HBM).
+    if (ctx->onDevice() && config.reserveWorkspace && (!plan.materialize || config.outputHost)) {
       // One pass holds its pass buffers (~1/K of both relations) and its
       // join's workspace (~1/K of the estimate, with a margin: a pass join's
       // sampled local pass that overflows re-runs exactly beside its sampled
@@ -113,7 +115,10 @@ void HashJoin::planPasses() {
   K = agreeMax(K);
   passes = K;
   if (K == 1) return;
-  JOIN_ASSERT(!plan.materialize, "HashJoin", "capacity spill (%u passes) runs counting joins only", K);
+  JOIN_ASSERT(!plan.materialize || config.outputHost, "HashJoin",
+              "capacity spill (%u passes) of a materializing join needs JoinConfig.outputHost: the pairs of every "
+              "pass go to one pinned host buffer",
+              K);
   data::Relation *rel[2] = {innerRelation, outerRelation};
   std::vector<uint64_t> counts, global;
   auto countPasses = [&](uint32_t k) {
@@ -194,7 +199,14 @@ JoinResult HashJoin::runPasses() {
   core::JoinConfig sub = config;
   sub.passes = 1;
   sub.keyHashing = plan.keyMix ? core::KeyHashing::On : core::KeyHashing::Off;
+  uint64_t written = 0;  // pairs appended to config.outputHost so far (materializing spill)
   for (uint32_t k = 0; k < passes; ++k) {
+    if (plan.materialize) {
+      sub.outputHost = static_cast<ulonglong2 *>(config.outputHost) + written;
+      sub.outputCapacity = config.outputCapacity > written ? config.outputCapacity - written : 0;
+      JOIN_ASSERT(sub.outputCapacity > 0, "HashJoin", "capacity spill: the host output buffer (%lu pairs) is full "
+                  "after pass %u of %u", (unsigned long)config.outputCapacity, k, passes);
+    }
     const uint64_t tc = nowUs();
     if (ctx->onDevice()) {
       ctx->resetScratch();
@@ -229,6 +241,13 @@ JoinResult HashJoin::runPasses() {
     spill.passReserved = std::max<uint64_t>(spill.passReserved, ctx->workspace().capacity());
     const JoinResult r = pass.run();
     spill.passPeak = std::max<uint64_t>(spill.passPeak, ctx->workspace().peak());
+    if (plan.materialize) {
+      JOIN_ASSERT(!r.outputOverflow, "HashJoin",
+                  "capacity spill: pass %u of %u produced %lu pairs, the host output buffer has room for %lu", k,
+                  passes, (unsigned long)r.outputPairs, (unsigned long)sub.outputCapacity);
+      written += r.outputPairs;
+      total.outputPairs += r.outputPairs;
+    }
     total.localMatches += r.localMatches;
     total.globalMatches += r.globalMatches;
     total.innerReceived += r.innerReceived;
@@ -249,6 +268,10 @@ JoinResult HashJoin::runPasses() {
   total.joinMs = (nowUs() - t0) / 1000.0;
   total.networkMs = total.joinMs;
   result = total;
+  if (plan.materialize) {  // every pass appended to the caller's host buffer
+    output = static_cast<const ulonglong2 *>(config.outputHost);
+    outputEpoch = ctx->workspace().epoch();
+  }
   RESULT_COUNTER = result.localMatches;
   return result;
 }
@@ -513,7 +536,8 @@ std::vector<uint64_t> HashJoin::workspaceParts() const {
   // Build/probe work lists (items or spans, 32 B) and materialized pairs.
   parts[0] += (2 * P + recvTotal[1] / std::max<uint32_t>(plan.sChunk, 1) +
                recvTotal[0] / std::max<uint32_t>(plan.rChunk, 1) + 2048) * 48;
-  if (plan.materialize) parts.push_back((config.outputCapacity ? config.outputCapacity : recvTotal[1] + 1024) * 16);
+  if (plan.materialize && !config.outputHost)
+    parts.push_back((config.outputCapacity ? config.outputCapacity : recvTotal[1] + 1024) * 16);
   return parts;
 }
 

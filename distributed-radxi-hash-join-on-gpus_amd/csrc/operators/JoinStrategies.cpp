@@ -194,6 +194,10 @@ bool ExactExchange::exchange(JoinRun &run) {
 tasks::BuildProbe *LocalPhase::addBuildProbe(data::Window *inner, data::Window *outer) {
   bps.emplace_back(new tasks::BuildProbe(inner, outer, env.ctx, env.plan, env.config.outputCapacity));
   if (sink) bps.back()->setRowSink(sink);
+  if (env.config.outputHost && env.plan.materialize) {
+    JOIN_ASSERT(env.config.outputCapacity > 0, "HashJoin", "outputHost needs outputCapacity (pairs it holds)");
+    bps.back()->setHostOutput(env.config.outputHost);
+  }
   return bps.back().get();
 }
 

@@ -105,6 +105,10 @@ void BuildProbe::execute() {
     args.offA = sink->offA;
     args.offB = sink->offB;
     args.outCapacity = outputCapacity;
+  } else if (plan.materialize && hostOut) {
+    outPairs = hostOut;  // pinned host memory, written by the place kernel over the host link
+    args.outPairs = outPairs;
+    args.outCapacity = outputCapacity;
   } else if (plan.materialize) {
     if (outputCapacity == 0) outputCapacity = outerPartitionSize + 1024;
     outPairs = static_cast<ulonglong2 *>(ws.get(outputCapacity * sizeof(ulonglong2)));
@@ -269,8 +273,8 @@ bool BuildProbe::collect() {
     again = true;
   }
   if (plan.materialize && outputCount > outputCapacity) {
-    if (fused) {
-      overflowOut = true;  // the sink is the caller's: it re-runs with a larger one
+    if (fused || hostOut) {
+      overflowOut = true;  // the buffer is the caller's: it re-runs with a larger one
     } else {
       outputCapacity = outputCount;
       again = true;

@@ -49,6 +49,9 @@ class BuildProbe : public Task {
   // rows to the sink.  A sink overflow is reported, not re-run (the caller
   // owns the buffer).
   void setRowSink(const kernels::RowSink *s) { sink = s; }
+  // Pairs go to this pinned host buffer (JoinConfig::outputHost, outputCapacity
+  // pairs); an overflow is reported, not re-run.
+  void setHostOutput(void *host) { hostOut = static_cast<ulonglong2 *>(host); }
   // The quotient table chained copies of a key (repeated inner keys), or a
   // span filled its overflow table and this task re-ran on counted tables.
   bool sawDuplicateChains() const { return duplicateChains; }
@@ -83,6 +86,7 @@ class BuildProbe : public Task {
   uint32_t *dedupCounts = nullptr;
   uint64_t *dedupLen = nullptr;
   const kernels::RowSink *sink = nullptr;
+  ulonglong2 *hostOut = nullptr;
   uint64_t hostCursor = 0;
 };
 

@@ -683,3 +683,57 @@ def test_capacity_spill_skewed_inner_key_classes(C, cuda):
     cfg.workspace_budget = est2 // 16
     with pytest.raises(RuntimeError, match="too frequent to spill"):
         C.HashJoin(R2, S, ctx, cfg)
+
+
+@pytest.mark.parametrize("dev", devices())
+@pytest.mark.parametrize("passes", [0, 3])
+def test_materializing_spill_to_host_output(C, dev, passes):
+    """A materializing join under a memory budget (passes 0 = the planner's
+    choice from workspace_budget, or forced key-hash passes) writes the pairs
+    of every pass straight into a caller-owned pinned host buffer
+    (JoinConfig.output_host), the reference UVA driver's host output; the
+    pair multiset equals the join."""
+    import torch
+    G_R, G_S = 120_000, 300_000
+    loc = "device" if dev == "cuda" else "host"
+    ctx = C.ExecContext(loc, 0 if loc == "device" else -1, C.LocalCommunicator())
+    R = C.Relation(G_R, G_R, loc, 0)
+    S = C.Relation(G_S, G_S, loc, 0)
+    R.generate(C.GenSpec(distribution=C.KeyDistribution.UNIFORM, seed=91, domain=G_R // 3), 0)
+    S.generate(C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=92, domain=G_R, zipf_theta=0.9), 0)
+    Rt, St = R.to_tensor().cpu(), S.to_tensor().cpu()
+    dom = int(max(Rt[:, 0].max(), St[:, 0].max())) + 1
+    exp = int((torch.bincount(Rt[:, 0], minlength=dom) * torch.bincount(St[:, 0], minlength=dom)).sum())
+    out = C.pinned_pairs(exp + 4096) if dev == "cuda" else torch.zeros((exp + 4096, 2), dtype=torch.int64)
+    cfg = C.JoinConfig()
+    cfg.materialize = True
+    cfg.output_host = out.data_ptr()
+    cfg.output_capacity = out.shape[0]
+    if passes:
+        cfg.passes = passes
+    elif dev == "cuda":
+        probe = C.JoinConfig()
+        probe.materialize = True
+        probe.output_host = out.data_ptr()
+        probe.output_capacity = out.shape[0]
+        cfg.workspace_budget = C.HashJoin(R, S, ctx, probe).workspace_estimate() // 4
+    else:
+        pytest.skip("the automatic spill plans device workspaces only")
+    j = C.HashJoin(R, S, ctx, cfg)
+    assert j.spill_passes >= (passes or 2), j.spill_passes
+    res = j.run()
+    assert res["global_matches"] == exp == res["output_pairs"] and not res["output_overflow"]
+    if dev == "cuda":
+        torch.cuda.synchronize()
+    pairs = out[:exp].clone()
+    assert torch.equal(j.output(), pairs)
+    keyR = torch.empty(G_R, dtype=torch.int64)
+    keyR[Rt[:, 1]] = Rt[:, 0]
+    keyS = torch.empty(G_S, dtype=torch.int64)
+    keyS[St[:, 1]] = St[:, 0]
+    assert torch.equal(keyR[pairs[:, 0]], keyS[pairs[:, 1]])
+    assert torch.unique(pairs[:, 0] * G_S + pairs[:, 1]).numel() == exp
+    # Too small a buffer is refused with a clear message, not written past.
+    cfg.output_capacity = exp // 2
+    with pytest.raises(RuntimeError, match="host output buffer"):
+        C.HashJoin(R, S, ctx, cfg).run()
