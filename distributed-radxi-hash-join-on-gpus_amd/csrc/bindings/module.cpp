@@ -691,6 +691,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("local_geometry", &core::JoinConfig::localGeometry)
       .def_readwrite("local_sample_stride", &core::JoinConfig::localSampleStride)
       .def_readwrite("output_capacity", &core::JoinConfig::outputCapacity)
+      .def_readwrite("codec_extra_ps_per_tuple", &core::JoinConfig::codecExtraPsPerTuple)
       .def_property(
           "output_host", [](const core::JoinConfig &c) { return (uint64_t)(uintptr_t)c.outputHost; },
           [](core::JoinConfig &c, uint64_t addr) { c.outputHost = reinterpret_cast<void *>((uintptr_t)addr); },
@@ -1030,6 +1031,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       });
 
   py::class_<operators::HashJoin, std::shared_ptr<operators::HashJoin>>(m, "HashJoin")
+      .def_static("codec_pays", &operators::HashJoin::codecPays, py::arg("wire_bits"), py::arg("nodes"),
+                  py::arg("link_gbps_per_peer"), py::arg("extra_ps_per_tuple") = 3.5,
+                  "The wire codec's cost model: packing w-bit tuples pays at this world size and link rate")
       .def(py::init([](PyRelation &inner, PyRelation &outer, std::shared_ptr<core::ExecContext> ctx,
                        const core::JoinConfig &cfg) {
              py::gil_scoped_release nogil;

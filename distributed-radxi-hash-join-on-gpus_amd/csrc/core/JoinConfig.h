@@ -47,7 +47,7 @@ enum class HistogramMode : int {
 // Exchange wire format (kernels.h, WireCodec): bit-packed frame-of-reference
 // tuples on the xGMI links instead of full 8-byte CompressedTuples.
 enum class WireCodecMode : int {
-  Auto = 0,  // device engine, N > 1, when it saves >= 1/8 of the bytes
+  Auto = 0,  // device engine, N > 1, when the link time it saves exceeds its extra passes (HashJoin::codecPays)
   Off = 1,
   On = 2,    // whenever the tuple fits < 64 bits (also the host path: tests)
 };
@@ -140,6 +140,10 @@ struct JoinConfig {
   // reaches to one peer (0 = kDefaultLinkGBpsPerPeer; bench.py calibrates it
   // with an RCCL all-to-all).
   double linkGBpsPerPeer = 0;
+  // Wire codec cost (WireCodecMode::Auto): picoseconds per tuple the pack +
+  // unpack passes cost beyond raw words' gather of the filled runs (MI355X:
+  // ~7 ps pack + unpack vs ~3.5 ps gather per tuple, bench.py scale_model).
+  double codecExtraPsPerTuple = 3.5;
 
   std::string describe() const;
 };

@@ -161,8 +161,8 @@ void Window::exchangePacked(const uint64_t *send, uint32_t chunk) {
 
 void Window::exchangeSegmented(const uint64_t *send, uint32_t chunk, SegmentedChunk &&sc, hipEvent_t scattered) {
   const uint32_t N = plan.numberOfNodes;
-  JOIN_ASSERT(ctx->onDevice() && N > 1 && codec.w && !wide && chunk < plan.chunks, "Window",
-              "segmented exchange: device, N > 1, wire codec, compressed tuples");
+  JOIN_ASSERT(ctx->onDevice() && N > 1 && !wide && chunk < plan.chunks, "Window",
+              "segmented exchange: device, N > 1, compressed tuples");
   JOIN_ASSERT(sc.sendWords.size() == N && sc.sendDispls.size() == N && sc.recvWords.size() == N &&
                   sc.recvDispls.size() == N,
               "Window", "segmented exchange: per-peer word counts for %u ranks", N);
@@ -182,7 +182,7 @@ void Window::exchangeSegmented(const uint64_t *send, uint32_t chunk, SegmentedCh
     if (p != plan.nodeId) wireSent += sc.sendWords[p];
   }
   uint64_t *wsend = ctx->workspace().getArray<uint64_t>(std::max<uint64_t>(sTotal, 1));
-  uint64_t *wrecv = ctx->workspace().getArray<uint64_t>(std::max<uint64_t>(rTotal, 1));
+  uint64_t *wrecv = codec.w ? ctx->workspace().getArray<uint64_t>(std::max<uint64_t>(rTotal, 1)) : nullptr;
   uint64_t *dst = static_cast<uint64_t *>(data);
   hipStream_t xs = ctx->commStream();
   HIP_CHECK(hipStreamWaitEvent(xs, scattered, 0));
@@ -197,6 +197,24 @@ void Window::exchangeSegmented(const uint64_t *send, uint32_t chunk, SegmentedCh
     return d;
   };
   kernels::WireSeg *dS = upload(sc.send), *dR = upload(sc.recv), *dC = upload(sc.self);
+  if (!codec.w) {
+    // Raw words (the planner found the codec's extra pass dearer than the link
+    // bytes it saves, HashJoin::planWireCodec): the filled runs are gathered
+    // out of the claim slices and the all-to-allv lands them straight in the
+    // window -- the receive displacements ARE window offsets, no unpack pass.
+    kernels::segCopy(send, wsend, dS, (uint32_t)sc.send.size(), sG, xs);
+    kernels::segCopy(send, dst, dC, (uint32_t)sc.self.size(), cG, xs);
+    ctx->timeline().begin("MWINPUT", xs);
+    ctx->comm()->allToAllV(wsend, sc.sendWords.data(), sc.sendDispls.data(), dst, sc.recvWords.data(),
+                           sc.recvDispls.data(), Location::Device, xs);
+    ctx->timeline().end("MWINPUT", xs);
+    HIP_CHECK(hipEventRecord(done[chunk], xs));
+    performance::Measurements::add("MWINPUTCNT", 1, "calls");
+    if (segmented.size() < plan.chunks) segmented.resize(plan.chunks);
+    segmented[chunk] = std::move(sc);
+    exchanged[chunk] = true;
+    return;
+  }
   kernels::wirePack(send, wsend, dS, (uint32_t)sc.send.size(), sG, codec, xs);
   kernels::segCopy(send, dst, dC, (uint32_t)sc.self.size(), cG, xs);
   ctx->timeline().begin("MWINPUT", xs);

@@ -401,12 +401,11 @@ void HashJoin::makeJoinPlan() {
     plan.wireRidBits[0] = plan.wireRidBits[1] = 0;
     plan.pipelineOuter = false;
   }
-  // N > 1 (tasks/SampledShuffle): needs the wire codec on both relations --
-  // its pack kernel is what keeps the claim slices' gaps off the links -- and
-  // two-sided windows.
+  // N > 1 (tasks/SampledShuffle): two-sided windows; the claim slices' gaps
+  // stay off the links either through the codec's pack or, with raw words,
+  // through a gather of the filled runs (received straight into the window).
   if (numberOfNodes > 1)
-    plan.sampledNetwork = ctx->onDevice() && sampleable && !plan.wide && !plan.oneSided && plan.wireBits[0] &&
-                          plan.wireBits[1];
+    plan.sampledNetwork = ctx->onDevice() && sampleable && !plan.wide && !plan.oneSided;
   basePlan = plan;  // the two-level plan: what a bitmap plan falls back to
   bitmapExact = !(ctx->onDevice() && sampleable);
   planBitmap();
@@ -516,6 +515,7 @@ std::vector<uint64_t> HashJoin::workspaceParts() const {
     recvTotal[r] = recv;
     if (N > 1 && !plan.oneSided) parts.push_back((plan.sampledNetwork ? n[r] + n[r] / 8 : n[r]) * wordB);  // send buffer
     if (plan.wireBits[r]) parts.push_back((n[r] + recv) * ((plan.wireBits[r] + 7) / 8) + (64ull << 10));  // wire buffers
+    else if (N > 1 && plan.sampledNetwork && !plan.oneSided) parts.push_back(n[r] * 8 + (64ull << 10));  // gathered runs
     parts.push_back(recv * wordB);  // window
     if (plan.twoLevel) {
       const uint64_t ob = plan.fragments ? 2 : plan.splitLocal ? kernels::SPLIT_BYTES : (plan.wide ? 16 : 8);
@@ -604,8 +604,20 @@ void HashJoin::planBitmap() {
 // (base = the smallest rid of the sending rank's exchange chunk: a chunk is a
 // contiguous quarter of the rank's input, so positional rids need 2 bits less
 // than with one base per rank) plus the key fragment above the network digit.
-// Auto packs on a device engine with N > 1 when it saves at least 1/8 of the
-// wire bytes (w <= 56); On forces it (also on the host path).
+// Auto decides by cost on a device engine with N > 1 (codecPays): packing
+// saves (64 - w) / 8 bytes per tuple that leaves the rank, at the calibrated
+// link rate of min(N - 1, 7) peers; it costs a pack and an unpack pass in HBM
+// where raw words need only the gather of the filled runs (SampledShuffle:
+// received straight into the window).  On forces it (also on the host path).
+// The reference compresses inside its scatter at every N
+// (tasks/NetworkPartitioning.cpp:128-129); here the choice follows the links.
+bool HashJoin::codecPays(uint32_t w, uint32_t nodes, double perPeerGBps, double extraPsPerTuple) {
+  if (w == 0 || w >= 64 || nodes < 2) return false;
+  const double linkGBps = perPeerGBps * (double)std::min<uint32_t>(nodes - 1, 7);
+  const double savedPs = (64.0 - w) / 8.0 / linkGBps * 1000.0;  // bytes / (GB/s) = ns; x 1000 = ps
+  return savedPs > extraPsPerTuple;
+}
+
 void HashJoin::planWireCodec(const std::vector<uint64_t> &all, size_t stride, uint32_t chunks) {
   for (int r = 0; r < 2; ++r) {
     plan.wireBits[r] = 0;
@@ -613,13 +625,17 @@ void HashJoin::planWireCodec(const std::vector<uint64_t> &all, size_t stride, ui
     plan.ridBase[r].assign((size_t)numberOfNodes * chunks, 0);
   }
   if (plan.wide || numberOfNodes == 1 || config.wireCodec == core::WireCodecMode::Off) return;
+  const double perPeer = config.linkGBpsPerPeer > 0 ? config.linkGBpsPerPeer : kDefaultLinkGBpsPerPeer;
+  auto wants = [&](uint32_t w) {
+    if (config.wireCodec == core::WireCodecMode::On) return w < 64;
+    return ctx->onDevice() && codecPays(w, numberOfNodes, perPeer, config.codecExtraPsPerTuple);
+  };
   const uint32_t keyW = plan.keyBits > plan.networkBits ? plan.keyBits - plan.networkBits : 0;
   if (plan.keyOnly) {
     // Key-only words (keyShift 0) are the key above the network digit: only
     // those keyBits - networkBits bits travel (53 of 64 for 63-bit keys), no
     // rid and no rid base (decode then returns the word itself).
-    const bool on = config.wireCodec == core::WireCodecMode::On ? keyW < 64 : (ctx->onDevice() && keyW <= 56);
-    if (on && keyW >= 1)
+    if (keyW >= 1 && wants(keyW))
       for (int r = 0; r < 2; ++r) plan.wireBits[r] = keyW;
     return;
   }
@@ -637,8 +653,7 @@ void HashJoin::planWireCodec(const std::vector<uint64_t> &all, size_t stride, ui
     // kernel compares key fragments only): the wire carries the fragment alone.
     const uint32_t ridBits = plan.materialize ? std::max<uint32_t>(1, ceilLog2(span)) : 0;
     const uint32_t w = ridBits + keyW;
-    const bool on = config.wireCodec == core::WireCodecMode::On ? w < 64 : (ctx->onDevice() && w <= 56);
-    if (on && w >= 1 && ridBits <= plan.keyShift) {
+    if (w >= 1 && wants(w) && ridBits <= plan.keyShift) {
       plan.wireBits[r] = w;
       plan.wireRidBits[r] = ridBits;
     }

@@ -144,6 +144,13 @@ class HashJoin {
   double planMs = 0, reserveMs = 0;
   int innerKeyRepeats();
   void planWireCodec(const std::vector<uint64_t> &rankStats, size_t stride, uint32_t chunks);
+
+ public:
+  // The wire codec's cost model (planWireCodec): true when packing w-bit
+  // tuples saves more link time per tuple than its extra HBM passes cost.
+  static bool codecPays(uint32_t w, uint32_t nodes, double perPeerGBps, double extraPsPerTuple);
+
+ private:
   JoinResult runImpl();
   core::ExecContext *ctx;
   std::unique_ptr<core::ExecContext> ownedCtx;

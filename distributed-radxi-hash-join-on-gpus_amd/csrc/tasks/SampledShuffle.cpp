@@ -21,8 +21,7 @@ SampledShuffle::SampledShuffle(uint32_t numberOfNodes, uint32_t nodeId, Histogra
     : nodes(numberOfNodes), me(nodeId), ctx(ctx), plan(plan), requestedStride(std::max<uint32_t>(1, sampleStride)),
       hc(hc) {
   JOIN_ASSERT(ctx->onDevice() && nodes > 1, "SampledShuffle", "multi-rank device path only");
-  JOIN_ASSERT(!plan.wide && plan.wireBits[0] && plan.wireBits[1], "SampledShuffle",
-              "needs 8-byte tuples and the wire codec on both relations");
+  JOIN_ASSERT(!plan.wide, "SampledShuffle", "needs 8-byte tuples (packed or raw on the wire)");
   sides[0].local = hc->innerLocal();
   sides[1].local = hc->outerLocal();
   for (Side &s : sides) {
@@ -319,7 +318,7 @@ bool SampledShuffle::exchangeSide(int k) {
           tuples += n;
           if (!n || p == me) continue;
           sc.send.push_back(kernels::WireSeg{s.start[at], off, n, myBase, 0});
-          off += codec.words(n);
+          off += codec.w ? codec.words(n) : n;  // raw: the exact run
         }
       }
       sc.sendWords[p] = off - sc.sendDispls[p];
@@ -331,6 +330,7 @@ bool SampledShuffle::exchangeSide(int k) {
     uint64_t roff = 0;
     for (uint32_t src = 0; src < N; ++src) {
       x.recvDispls[(size_t)c * N + src] = cur;
+      if (!codec.w) roff = cur;  // raw: received straight into the window (same run order as the sender's)
       sc.recvDispls[src] = roff;
       const uint64_t base = plan.ridBase[k][(size_t)src * ridChunks + c];
       const uint64_t first = cur;
@@ -345,7 +345,7 @@ bool SampledShuffle::exchangeSide(int k) {
             sc.self.push_back(kernels::WireSeg{s.start[(size_t)c * GF + (size_t)g * F + q], cur, n, 0, 0});
           } else {
             sc.recv.push_back(kernels::WireSeg{cur, roff, n, base, 0});
-            roff += codec.words(n);
+            roff += codec.w ? codec.words(n) : n;
           }
           cur += n;
         }

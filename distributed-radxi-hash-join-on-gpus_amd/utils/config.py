@@ -9,9 +9,10 @@ from .._native import require_native
 _FIELDS = ["network_bits", "local_bits", "two_level", "key_shift", "materialize", "output_capacity", "build_target",
            "r_chunk", "s_chunk", "chunks", "checks", "max_partition_blocks", "sample_stride", "local_sample_stride", "local_item_tiles", "local_geometry",
            "split_local", "direct_count", "split_histogram", "pipeline_outer", "bitmap_join", "skew_split",
-           "reserve_workspace", "passes", "workspace_budget",
+           "reserve_workspace", "passes", "workspace_budget", "link_gbps_per_peer", "codec_extra_ps_per_tuple",
            # kernel-shape variants (sweeps / A-B tests; JoinConfig.variants in C++)
            "net_ipt", "net_threads", "bm_threads", "bm_flat", "reduce_chunks", "key_count", "rows_lds", "mat_variant"]
+_FLOATS = ("link_gbps_per_peer", "codec_extra_ps_per_tuple")
 _BOOLS = ("two_level", "materialize", "checks", "split_local", "direct_count", "split_histogram", "pipeline_outer",
           "bitmap_join", "skew_split", "reserve_workspace")
 
@@ -56,6 +57,8 @@ def config_from_dict(d: dict | None = None, env_prefix: str = "HPCJOIN_"):
             setattr(cfg, k, getattr(C.PlanChoice, str(v).upper()))
         elif k == "exchange":
             cfg.exchange = getattr(C.ExchangeMode, str(v).upper())
+        elif k in _FLOATS:
+            setattr(cfg, k, float(v))
         elif k in _FIELDS:
             setattr(cfg, k, int(v))
         else:

@@ -62,6 +62,11 @@ def main():
         ("sampled-hot-split", C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=79, domain=5, zipf_theta=0.99),
          G_S, {"bitmap_join": False, "chunks": 2, "key_hashing": C.KeyHashing.OFF,
                "network_histogram": C.HistogramMode.SAMPLED}),
+        # raw words (codec off: the cost model's choice on fast links), gathered
+        # runs received straight into the windows -- no unpack pass
+        ("sampled-raw-chunks2", C.GenSpec(distribution=C.KeyDistribution.UNIFORM, seed=9, domain=G_R), G_S,
+         {"bitmap_join": False, "chunks": 2, "network_histogram": C.HistogramMode.SAMPLED,
+          "wire_codec": C.WireCodecMode.OFF}),
     ]
     R = C.Relation(C.Relation.local_size_for(G_R, info.rank, info.world), G_R, "device", info.local_rank)
     R.generate(inner, C.Relation.local_offset_for(G_R, info.rank, info.world))
@@ -76,17 +81,19 @@ def main():
     Ss = C.Relation(C.Relation.local_size_for(G_R, info.rank, info.world), G_R, "device", info.local_rank)
     Ss.generate(sparse_out, C.Relation.local_offset_for(G_R, info.rank, info.world))
     cfg = C.JoinConfig()
-    cfg.wire_codec = C.WireCodecMode.ON  # auto packs only <= 56 bits (this size plans 6 network bits: 57)
     exp = C.Relation.expected_matches(sparse_in, G_R, sparse_out, G_R)
-    for mode in ("EXACT", "SAMPLED"):
+    for mode, codec in (("EXACT", "ON"), ("SAMPLED", "ON"), ("SAMPLED", "OFF")):
         cfg.network_histogram = getattr(C.HistogramMode, mode)
+        cfg.wire_codec = getattr(C.WireCodecMode, codec)
+        mode = mode if codec == "ON" else mode + "-raw"
         j = C.HashJoin(Rs, Ss, ctx, cfg)
-        assert j.plan.key_only and list(j.plan.wire_bits) == [j.plan.key_bits - j.plan.network_bits] * 2, j.plan
-        assert j.plan.sampled_network == (mode == "SAMPLED"), j.plan
+        want = [j.plan.key_bits - j.plan.network_bits] * 2 if codec == "ON" else [0, 0]
+        assert j.plan.key_only and list(j.plan.wire_bits) == want, j.plan
+        assert j.plan.sampled_network == mode.startswith("SAMPLED"), j.plan
         for _ in range(2):
             res = j.run()
             assert res["global_matches"] == exp, ("sparse-key-only", mode, res["global_matches"], exp)
-            assert res["sampled_network"] == (mode == "SAMPLED") and res["network_fallbacks"] == 0, res
+            assert res["sampled_network"] == mode.startswith("SAMPLED") and res["network_fallbacks"] == 0, res
         if info.rank == 0:
             print(f"sparse-key-only {mode}: {res['global_matches']} == {exp}, plan {j.plan}", flush=True)
         del j

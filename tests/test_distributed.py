@@ -109,15 +109,20 @@ def test_in_process_sampled_local_pass(C, cuda, n_ranks, chunks, fmt):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n_ranks,chunks,opts", [(2, 1, ""), (3, 3, "mat"), (4, 2, "zipf"), (8, 1, ""),
-                                                  (4, 2, "hot"), (3, 2, "sparse")])
+                                                  (4, 2, "hot"), (3, 2, "sparse"), (2, 1, "raw"),
+                                                  (3, 2, "rawmat"), (4, 2, "rawsparse"), (4, 2, "rawhot")])
 def test_sampled_shuffle(C, cuda, n_ranks, chunks, opts):
     """N > 1 sampled network pass (tasks/SampledShuffle): no exact pre-read of
     either relation; slices sized from a 1-in-S tile sample, exact fills
-    all-gathered per chunk, filled runs packed onto the wire.  Counts equal
-    the oracle and the exact exchange; materialized pairs are the same set."""
+    all-gathered per chunk, filled runs packed onto the wire -- or, with the
+    codec off ("raw": what the cost model picks on fast links), gathered and
+    received straight into the window with no unpack pass.  Counts equal the
+    oracle and the exact exchange; materialized pairs are the same set."""
     import torch
     G_R, G_S = 1_500_007, 2_500_009
     inner = outer = None
+    raw = opts.startswith("raw")
+    opts = opts[3:] if raw else opts
     if opts == "hot":
         G_R, G_S = 200_000, 2_000_000
         outer = C.GenSpec(distribution=C.KeyDistribution.ZIPF, seed=79, domain=5, zipf_theta=0.99)
@@ -133,7 +138,7 @@ def test_sampled_shuffle(C, cuda, n_ranks, chunks, opts):
             c.bitmap_join = False
             c.chunks = chunks
             c.materialize = opts == "mat"
-            c.wire_codec = C.WireCodecMode.ON
+            c.wire_codec = C.WireCodecMode.OFF if raw else C.WireCodecMode.ON
             if opts == "hot":
                 c.key_hashing = C.KeyHashing.OFF
 
@@ -141,6 +146,7 @@ def test_sampled_shuffle(C, cuda, n_ranks, chunks, opts):
                                  theta=0.9, outputs=pairs if opts == "mat" else None, inner=inner, outer=outer)
         for res, plan in results:
             assert plan.sampled_network == (mode == "SAMPLED")
+            assert (list(plan.wire_bits) == [0, 0]) == raw, plan
             assert res["sampled_network"] == (mode == "SAMPLED") and res["network_fallbacks"] == 0, res
             if exp is not None:
                 assert res["global_matches"] == exp
@@ -732,3 +738,40 @@ def test_ipc_ordering():
     for p, o in zip(procs, outs):
         assert p.returncode == 0, o[-4000:]
     assert obs is not None, outs[1][-4000:]
+
+
+def test_wire_codec_cost_model(C):
+    """The wire codec packs only when the link time it saves (per tuple that
+    leaves a rank: (64 - w) / 8 bytes at min(N - 1, 7) x the per-peer rate)
+    exceeds its extra HBM passes (codec_extra_ps_per_tuple, default 3.5 ps):
+    63-bit keys (w = 53) stay raw on 8 fast xGMI peers and pack on slow links
+    or few peers; dense keys (w = 20) always pack at the modelled rates."""
+    pays = C.HashJoin.codec_pays
+    assert not pays(53, 8, 64.0)        # 1.375 B / 448 GB/s = 3.1 ps < 3.5: raw
+    assert pays(53, 4, 64.0)            # 3 peers: 7.2 ps
+    assert pays(53, 8, 10.0)            # slow links (e.g. the socket-transport rehearsal)
+    assert pays(20, 8, 64.0)            # 5.5 B saved: 12.3 ps
+    assert not pays(40, 8, 200.0)       # fast links, modest saving
+    assert pays(40, 8, 200.0, 1.0)      # ... unless the codec is cheaper than modelled
+    assert not pays(64, 2, 1.0) and not pays(20, 1, 64.0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("link,packed", [(10.0, True), (1000.0, False)])
+def test_wire_codec_auto_follows_links(C, cuda, link, packed):
+    """Auto codec on the general path (53-bit key words) at N = 2 in-process
+    ranks: a slow calibrated link packs, a fast one sends raw words into the
+    window; both exact on the sampled shuffle."""
+    inner, outer = C.GenSpec(seed=1234), C.GenSpec(seed=99)
+    inner.sparse64 = outer.sparse64 = True
+
+    def cfg_fn(c):
+        c.link_gbps_per_peer = link
+        c.bitmap_join = False
+        c.network_histogram = C.HistogramMode.SAMPLED
+
+    results, exp = run_ranks(C, 2, "device", 1_000_003, 1_000_003, cfg_fn, inner=inner, outer=outer)
+    for res, plan in results:
+        assert plan.key_only and plan.sampled_network
+        assert (list(plan.wire_bits) == [plan.key_bits - plan.network_bits] * 2) == packed, plan
+        assert res["global_matches"] == exp
