@@ -131,30 +131,41 @@ def link_prediction(info, plan, results):
 def scale_model(C, info, ctx, comm, on_gpu, G_R, G_S, specs, cfg, rel_loc, general_cfg_ok):
     """Predicted N = 2/4/8 step times of the three N > 1 paths, from one
     GPU: a rank's kernel work at N is measured directly as the same join on
-    its share (G/N x G/N tuples), plus the wire pack/unpack of the (N-1)/N of
-    its tuples that leave it (measured codec rates), plus the link time the
-    plan's cost model gives for its bytes per rank at the model bandwidth,
-    minus what hides behind the other relation's network pass (the chunked
-    pipelines overlap one side's exchange with the other side's scatter).
+    its share (G/N x G/N tuples); the link bytes per rank follow from the
+    wire format the planner picks at that N (HashJoin.codec_pays: packed
+    w-bit words when the link time saved exceeds the codec's extra passes,
+    else raw 8-byte words gathered from the claim slices); the codec (pack +
+    unpack) or gather passes cost their measured rates.
       value      replicated bitmaps: all-reduce of 2 (N-1)/N x 2^keyBits / 8 B
       shuffle    hash-partition shuffle of the dense keys: w = keyBits - net bits
       general    the same shuffle of 63-bit keys (key-only words, w = 53)
-    The driver's SCALE run is the measurement this is checked against."""
+    Overlap (the chunked pipeline, chunks = 4 at N > 1): chunk k's exchange
+    runs while chunk k + 1 is scattered and, for the outer relation, while
+    chunk k - 1 is local-partitioned and probed, so a step is bounded by
+      compute = rank share + codec/gather passes, and
+      links   = first chunk's scatter + link time + last chunk's local work,
+    predicted = max(compute, links).  The driver's SCALE run is the
+    measurement this is checked against."""
     if info.world != 1 or not on_gpu:
         return None
     import math
     from hpcjoin.utils import config_from_dict
     per_peer = cfg.link_gbps_per_peer if cfg.link_gbps_per_peer > 0 else 64.0
-    # wire codec rates (ms per tuple) at the two widths, 64M tuples
+    extra_ps = cfg.codec_extra_ps_per_tuple
+    # pass rates (ms per tuple), 64M tuples: pack + unpack at the two codec
+    # widths, and the raw gather (a 64-bit "pack" is a copy of the runs)
     raw = torch.randint(0, 1 << 62, (1 << 26,), dtype=torch.int64, device="cuda")
     codec = {}
     for w in (20, 53):
         r = C.ops.bench_wire(raw, w, 0, 0, 5)
         codec[w] = (r["pack_ms"] + r["unpack_ms"]) / raw.numel()
+    gather = C.ops.bench_wire(raw, 64, 0, 0, 5)["pack_ms"] / raw.numel()
     del raw
     torch.cuda.empty_cache()
     key_bits = max(1, math.ceil(math.log2(max(G_R, 2))))
-    out = {"link_GBps_per_peer": per_peer, "source": "measured per-rank share on one GPU + codec rates + link model",
+    chunks = 4
+    out = {"link_GBps_per_peer": per_peer, "codec_extra_ps_per_tuple": extra_ps, "chunks": chunks,
+           "source": "measured per-rank share on one GPU + codec / gather rates + link model + chunk pipeline",
            "paths": {}}
     for path in ("value", "shuffle", "general"):
         if path == "general" and not general_cfg_ok:
@@ -169,21 +180,27 @@ def scale_model(C, info, ctx, comm, on_gpu, G_R, G_S, specs, cfg, rel_loc, gener
             ctx.reset_scratch()
             link_gbps = per_peer * min(N - 1, 7)
             share = (N - 1) / N
+            net_ms = m["phases_ms"]["dev_network_ms"]
             if path == "value":
-                net = 10
                 link_bytes = 2 * share * (1 << key_bits) / 8
-                codec_ms = 0.0
+                codec_ms, wire = 0.0, "bitmap all-reduce"
+                # ranges of the all-reduce overlap the outer scatter (half the network pass)
+                pred_links = net_ms / 2 + link_bytes / link_gbps / 1e6
             else:
-                net = 10
-                w = (key_bits - net) if path == "shuffle" else 53
-                link_bytes = share * (gr * w + gs * w) / 8
-                codec_ms = share * (gr + gs) * codec[20 if path == "shuffle" else 53]
+                w = (key_bits - 10) if path == "shuffle" else 53
+                packed = C.HashJoin.codec_pays(w, N, per_peer, extra_ps)
+                bits = w if packed else 64
+                link_bytes = share * (gr + gs) * bits / 8
+                codec_ms = share * (gr + gs) * (codec[20 if path == "shuffle" else 53] if packed else gather)
+                wire = f"packed {w}-bit" if packed else "raw 64-bit (gathered runs, no unpack)"
+                rest = max(0.0, m["ms_per_step"] - net_ms)
+                pred_links = net_ms / (2 * chunks) + link_bytes / link_gbps / 1e6 + rest / chunks
             link_ms = link_bytes / link_gbps / 1e6
-            hide_ms = m["phases_ms"]["dev_network_ms"] / 2  # the other relation's network pass
-            pred = m["ms_per_step"] + codec_ms + max(0.0, link_ms - hide_ms)
-            rows.append({"n_gpus": N, "rank_share_ms": m["ms_per_step"], "codec_ms": round(codec_ms, 3),
+            pred = max(m["ms_per_step"] + codec_ms, pred_links)
+            rows.append({"n_gpus": N, "rank_share_ms": m["ms_per_step"], "wire": wire, "codec_ms": round(codec_ms, 3),
                          "link_bytes_per_rank": int(link_bytes), "link_ms": round(link_ms, 3),
-                         "hidden_behind_scatter_ms": round(hide_ms, 3), "predicted_ms": round(pred, 3),
+                         "compute_bound_ms": round(m["ms_per_step"] + codec_ms, 3),
+                         "link_bound_ms": round(pred_links, 3), "predicted_ms": round(pred, 3),
                          "predicted_value": round((G_R + G_S) / pred / 1e6, 2), "rank_share_correct": m["correct"]})
         out["paths"][path] = rows
     return out
