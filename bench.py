@@ -95,7 +95,7 @@ if __name__ == "__main__":
 # read-backs): run them as blit kernels on the compute queue, not on the SDMA
 # engines.  With SDMA on, about every second process stalled one join (the
 # 4th) by 17-45 ms inside the first small copy; with it off 5/5 runs were
-# clean (profiles/r1_sdma_outlier.md).  Must be set before HIP initialises.
+# clean (profiles/archive/r1_sdma_outlier.md).  Must be set before HIP initialises.
 # Single-process runs only: multi-rank runs keep the runtime default (their
 # RCCL rehearsals over the socket transport were measured with SDMA on).
 if int(os.environ.get("WORLD_SIZE", "1")) == 1:
