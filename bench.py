@@ -51,9 +51,23 @@ def _spawn_ranks_if_needed():
     n = known.gpus
     if n <= 1:
         return
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+    # A free port below the kernel's ephemeral range: an ephemeral one can be
+    # handed out again as the local port of the ranks' own outgoing sockets
+    # (RCCL bootstrap) before rank 0 binds it (EADDRINUSE).
+    import random
+    port = 0
+    for cand in random.Random(os.getpid()).sample(range(20000, 32000), 200):
+        with socket.socket() as s:
+            try:
+                s.bind(("127.0.0.1", cand))
+            except OSError:
+                continue
+            port = cand
+            break
+    if not port:
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
     base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
                 LOCAL_WORLD_SIZE=str(n), HPCJOIN_SPAWNED="1")
     procs = []

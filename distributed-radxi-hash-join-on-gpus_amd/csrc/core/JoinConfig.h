@@ -88,7 +88,12 @@ struct JoinConfig {
   uint32_t sChunk = 65536;      // max outer tuples per build/probe work item
   uint32_t chunks = 1;          // exchange pipeline slices per relation (>1: scatter(k+1) || all-to-all(k))
   bool checks = true;           // cheap always-on invariants (all tuples written, sizes)
-  uint32_t maxPartitionBlocks = 2048;  // network-pass grid cap (~8 WGs per CU)
+  // Network-pass grid cap: 512 = two workgroups per CU, each walking a long
+  // contiguous range (1B tuples: 477 tiles per workgroup).  Same-process A/B
+  // on MI355X, 1B x 1B: general path 19.23 -> 18.99 ms, headline 9.54 -> 9.47
+  // ms against 2048 (fewer workgroup prologues / epilogues per CU;
+  // profiles/r6/README.md).
+  uint32_t maxPartitionBlocks = 512;
   KeyHashing keyHashing = KeyHashing::Auto;
   HistogramMode networkHistogram = HistogramMode::Auto;
   HistogramMode localHistogram = HistogramMode::Auto;

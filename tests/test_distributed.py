@@ -360,6 +360,21 @@ def test_pipelined_outer_chunks(C, dev, n_ranks, chunks, local):
 
 
 def _free_port():
+    """A free rendezvous port BELOW the kernel's ephemeral range (32768-60999
+    here): a port the kernel handed out as ephemeral can be handed out again
+    as the local port of any outgoing connection (RCCL's bootstrap sockets of
+    the ranks starting up) before rank 0 binds it -- an 8-rank run failed
+    that way with EADDRINUSE."""
+    import random
+    rng = random.Random(os.getpid() ^ int(time.time() * 1e6))
+    for _ in range(200):
+        port = rng.randrange(20000, 32000)
+        with socket.socket() as s:
+            try:
+                s.bind(("127.0.0.1", port))
+            except OSError:
+                continue
+            return port
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
@@ -775,3 +790,33 @@ def test_wire_codec_auto_follows_links(C, cuda, link, packed):
         assert plan.key_only and plan.sampled_network
         assert (list(plan.wire_bits) == [plan.key_bits - plan.network_bits] * 2) == packed, plan
         assert res["global_matches"] == exp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fused", [True, False])
+def test_tpch_every_output_row(C, cuda, fused):
+    """BASELINE config 5 at SF 1 (1.5M orders x 6M lineitems, 32-byte payload
+    rows): EVERY output row [o_rid, l_rid, orders payload, lineitem payload]
+    equals a torch gather oracle -- the join pairs from a sort/searchsorted
+    of the orders' keys, the payloads gathered from the same payload tensors.
+    fused: rows written by the build/probe (N = 1); else pairs + the
+    request/response late materialization (the N > 1 path)."""
+    import torch
+    from hpcjoin.models import workloads as W
+    from hpcjoin.models.tpch import TpchJoin
+    wl = W.get("tpch_sf1000").scaled(0.001)
+    t = TpchJoin(wl, fused=fused)
+    res, rows = t.run()
+    assert res["global_matches"] == wl.expected_matches() == rows.shape[0]
+    O, L = t.orders.to_tensor(), t.lineitem.to_tensor()
+    order = torch.argsort(O[:, 0])
+    keys = O[order, 0]
+    at = torch.searchsorted(keys, L[:, 0]).clamp(max=keys.numel() - 1)
+    assert torch.equal(keys[at], L[:, 0])  # every lineitem has its order
+    o_rid, l_rid = O[order, 1][at], L[:, 1]
+    exp = torch.cat([o_rid[:, None], l_rid[:, None], t.o_rows[o_rid - t.o_off], t.l_rows[l_rid - t.l_off]], 1)
+    got = rows.to(exp.device)
+    got = got[torch.argsort(got[:, 1])]
+    exp = exp[torch.argsort(exp[:, 1])]
+    assert got.shape == exp.shape == (wl.expected_matches(), 10)
+    assert torch.equal(got, exp)
