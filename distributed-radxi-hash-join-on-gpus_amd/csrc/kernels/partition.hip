@@ -1110,6 +1110,8 @@ static void launchNetClaim(const Pol &pol, const data::Tuple *in, uint64_t n, ui
   }
   if (g.ipt == 15 && narrow && bits == MAX_PART_BITS)
     launchNetClaimIpt<Pol, 15>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
+  else if (g.ipt == 12)  // 12288-tuple tiles (sweep: longer runs per digit and tile)
+    launchNetClaimIpt<Pol, 12>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
   else
     launchNetClaimIpt<Pol, CL_IPT_DEFAULT>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
 }
@@ -1922,8 +1924,30 @@ void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nI
   const uint64_t mask = F - 1;
   const uint32_t grid = ((nItems + NGROUPS - 1) / NGROUPS) * NGROUPS;
   // geometry 5: the default 1024 x 8 shape as one workgroup per item (the
-  // round-5 kernel, kept for A/B); 0: persistent workgroups over the items.
+  // round-5 kernel, kept for A/B); 0: persistent workgroups over the items;
+  // 6 / 7: persistent with 12 / 10 tuples per thread (longer runs per digit
+  // and tile, split layout only).
   const bool persist = geometry == 0;
+  if ((geometry == 6 || geometry == 7) && split.on && !wide && !frag && gend) {
+    LocalSplitPol pol;
+    pol.mask = mask;
+    pol.shift = shift;
+    setSplit(pol, split);
+    auto go = [&](auto cur, auto ipt) {
+      using C = decltype(cur);
+      launchLocalClaimPersist<LocalSplitPol, C, CL_NTH, decltype(ipt)::value>(in, items, nItems, F, pol, gcur, out,
+                                                                               gend, s);
+    };
+    if (geometry == 6) {
+      if (narrow) go(uint32_t(), std::integral_constant<int, 12>());
+      else go((unsigned long long)0, std::integral_constant<int, 12>());
+    } else {
+      if (narrow) go(uint32_t(), std::integral_constant<int, 10>());
+      else go((unsigned long long)0, std::integral_constant<int, 10>());
+    }
+    HIP_CHECK_LAUNCH();
+    return;
+  }
   if (geometry != 0 && geometry != 5 && split.on && !wide && !frag && !narrow && gend) {
     LocalSplitPol pol;
     pol.mask = mask;

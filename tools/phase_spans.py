@@ -32,11 +32,27 @@ def main():
     ap.add_argument("--ab", default="",
                     help="FIELD=v1|v2|...: one join per JoinConfig value, built on the same relations and run in "
                          "turn (same-process A/B of a config field)")
+    ap.add_argument("--after-headline", action="store_true",
+                    help="first run the dense-key headline join on the same context (as bench.py does before "
+                         "its general path), then free its relations")
+    ap.add_argument("--trim", action="store_true", help="with --after-headline: trim the workspace in between")
     ap.add_argument("--keys", default="", help="comma- or colon-separated measurement keys (default: every device span)")
     args = ap.parse_args()
     C = hpcjoin.require_native()
     ctx = C.ExecContext("device", 0, C.LocalCommunicator())
     G = int(args.size)
+    if args.after_headline:
+        Rh, Sh = C.Relation(G, G, "device", 0), C.Relation(G, G, "device", 0)
+        Rh.generate(C.GenSpec(seed=1234), 0)
+        Sh.generate(C.GenSpec(seed=4321), 0)
+        jh = C.HashJoin(Rh, Sh, ctx, C.JoinConfig())
+        for _ in range(3):
+            jh.run()
+        del jh, Rh, Sh
+        ctx.reset_scratch()
+        if args.trim:
+            ctx.trim_workspace(0)
+        torch.cuda.synchronize()
     R = C.Relation(G, G, "device", 0)
     S = C.Relation(G, G, "device", 0)
     a, b = C.GenSpec(seed=1234), C.GenSpec(seed=4321)
