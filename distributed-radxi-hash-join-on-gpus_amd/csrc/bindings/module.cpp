@@ -577,6 +577,7 @@ py::dict resultToDict(const operators::JoinResult &r) {
   d["exchange_checked"] = r.exchangeChecked;
   d["passes"] = r.passes;
   d["compact_ms"] = r.compactMs;
+  d["verify_ms"] = r.verifyMs;
   d["group_passes"] = r.groupPasses;
   d["inner_received"] = r.innerReceived;
   d["wire_bytes"] = r.wireBytes;

@@ -147,6 +147,8 @@ ExecContext::~ExecContext() {
   staging_.reset();
   windows_.reset();
   if (stream_) (void)hipStreamDestroy(stream_);
+  if (tagStream_) (void)hipStreamDestroy(tagStream_);
+  if (tagHost_) (void)hipHostFree(tagHost_);
   if (commStream_) (void)hipStreamDestroy(commStream_);
   if (decodeStream_) (void)hipStreamDestroy(decodeStream_);
 }
@@ -234,6 +236,30 @@ void ExecContext::logIpc(char op, bool cached, uint32_t peer, uint64_t generatio
   ipcLog_.push_back(IpcEvent{op, cached, peer, generation, handle ? h : 0, ptr});
 }
 
+// The 16-byte IPC tag of an allocation, read or written with the engine's own
+// copy kernels on a private non-blocking stream (no null-stream copy, nothing
+// queued on the join's streams in front of it).
+void ExecContext::tagRead(const void *devTag, uint64_t out[2]) {
+  HIP_CHECK(hipSetDevice(device_));
+  if (!tagStream_) HIP_CHECK(hipStreamCreateWithFlags(&tagStream_, hipStreamNonBlocking));
+  if (!tagHost_) HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&tagHost_), 64, hipHostMallocMapped));
+  kernels::copyToHost(tagHost_, devTag, 16, tagStream_);
+  utils::waitStream(tagStream_, nullptr, "IPC tag read");
+  out[0] = tagHost_[0];
+  out[1] = tagHost_[1];
+}
+
+void ExecContext::tagWrite(void *devTag, const uint64_t in[2]) {
+  HIP_CHECK(hipSetDevice(device_));
+  if (!tagStream_) HIP_CHECK(hipStreamCreateWithFlags(&tagStream_, hipStreamNonBlocking));
+  if (!tagHost_) HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&tagHost_), 64, hipHostMallocMapped));
+  tagHost_[2] = in[0];
+  tagHost_[3] = in[1];
+  kernels::copyFromHost(devTag, tagHost_ + 2, 16, tagStream_);
+  // Complete before the handle is published (importers read the tag).
+  utils::waitStream(tagStream_, nullptr, "IPC tag write");
+}
+
 void ExecContext::ipcExport(const void *p, uint64_t handle[8], uint64_t *offset, uint64_t *generation,
                             uint64_t *tagOffset, uint64_t *nonce) {
   static_assert(sizeof(hipIpcMemHandle_t) == 64, "unexpected hipIpcMemHandle_t size");
@@ -254,9 +280,7 @@ void ExecContext::ipcExport(const void *p, uint64_t handle[8], uint64_t *offset,
     // The tag must still be this export's: anything else is a write past
     // the end of a workspace buffer (the tag is the allocation's tail).
     uint64_t stamp[2] = {0, 0};
-    HIP_CHECK(hipSetDevice(device_));
-    HIP_CHECK(hipMemcpy(stamp, static_cast<const uint8_t *>(hit->base) + hit->tagOffset, sizeof(stamp),
-                        hipMemcpyDeviceToHost));
+    tagRead(static_cast<const uint8_t *>(hit->base) + hit->tagOffset, stamp);
     JOIN_ASSERT(stamp[0] == hit->nonce && stamp[1] == gen, "ExecContext",
                 "IPC export: the tag of allocation %p (generation %lu) was overwritten: nonce %016lx gen %lu, "
                 "expected %016lx gen %lu -- a write past the end of a workspace buffer",
@@ -273,12 +297,10 @@ void ExecContext::ipcExport(const void *p, uint64_t handle[8], uint64_t *offset,
     x.nonce = ((uint64_t)getpid() << 40) ^ (++exportSerial_ << 20) ^
               (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
     const uint64_t stamp[2] = {x.nonce, gen};
-    HIP_CHECK(hipSetDevice(device_));
-    // Complete before the handle is published: a synchronous hipMemcpy from
+    // Complete before the handle is published (a synchronous hipMemcpy from
     // pageable memory may return once the source is staged, before the DMA
-    // lands (importers then read the previous tag: seen at 8 ranks).
-    HIP_CHECK(hipMemcpyAsync(tag, stamp, sizeof(stamp), hipMemcpyHostToDevice, stream_));
-    HIP_CHECK(hipStreamSynchronize(stream_));
+    // lands: importers then read the previous tag, seen at 8 ranks).
+    tagWrite(tag, stamp);
     ipcExported_.push_back(x);
     hit = &ipcExported_.back();
   }
@@ -320,8 +342,7 @@ void *ExecContext::ipcImport(uint32_t peer, const uint64_t handle[8], uint64_t g
   HIP_CHECK(hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess));
   logIpc('O', false, peer, generation, &h, ptr);
   uint64_t stamp[2] = {0, 0};
-  HIP_CHECK(hipSetDevice(device_));
-  HIP_CHECK(hipMemcpy(stamp, static_cast<uint8_t *>(ptr) + tagOffset, sizeof(stamp), hipMemcpyDeviceToHost));
+  tagRead(static_cast<uint8_t *>(ptr) + tagOffset, stamp);
   if (stamp[0] != nonce || stamp[1] != generation) {
     (void)hipIpcCloseMemHandle(ptr);
     JOIN_ASSERT(false, "ExecContext",

@@ -143,6 +143,12 @@ class ExecContext {
   int device_;
   comm::Communicator *comm_;
   hipStream_t stream_ = nullptr;
+  // IPC tag reads / writes: a private non-blocking stream and pinned words,
+  // so the checks never wait behind work queued on the engine's streams.
+  hipStream_t tagStream_ = nullptr;
+  uint64_t *tagHost_ = nullptr;
+  void tagRead(const void *devTag, uint64_t out[2]);
+  void tagWrite(void *devTag, const uint64_t in[2]);
   hipStream_t commStream_ = nullptr;
   hipStream_t decodeStream_ = nullptr;
   std::unique_ptr<memory::Arena> workspace_;

@@ -799,8 +799,12 @@ JoinResult HashJoin::runImpl() {
                       (config.verifyExchange == core::PlanChoice::On ||
                        (config.verifyExchange == core::PlanChoice::Auto && plan.oneSided));
   if (verify) {  // both windows complete first (the outer one may still be on the links)
+    // Its own phase (verifyMs), kept out of joinMs: hashing the input and both
+    // windows again plus two collectives is a check, not join work.
+    const uint64_t tv = nowUs();
     run.outer->stop();
     result.exchangeChecked = verifyExchange(env, run).cells;
+    result.verifyMs = (nowUs() - tv) / 1000.0;
   }
   if (dev && !run.networkEventRecorded) HIP_CHECK(hipEventRecord(ev[2], ctx->stream()));
   Measurements::stopWaitingForNetworkCompletion();
@@ -835,10 +839,10 @@ JoinResult HashJoin::runImpl() {
 
 // Host phase spans and the device spans between the join's five events.
 void HashJoin::recordTimes(const JoinRun &run, uint64_t t4) {
-  result.joinMs = (t4 - run.t0) / 1000.0;
+  result.joinMs = (t4 - run.t0) / 1000.0 - result.verifyMs;
   result.histogramMs = (run.t1 - run.t0) / 1000.0;
   result.windowMs = (run.t2 - run.t1) / 1000.0;
-  result.networkMs = (run.t3 - run.t2) / 1000.0;
+  result.networkMs = (run.t3 - run.t2) / 1000.0 - result.verifyMs;
   result.localMs = (t4 - run.t3) / 1000.0;
   if (!ctx->onDevice()) return;
   float ms;

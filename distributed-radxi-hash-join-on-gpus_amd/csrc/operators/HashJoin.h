@@ -45,6 +45,8 @@ struct JoinResult {
   // joinMs - devSpanMs is what the host added around the device work.
   double enqueueMs = 0, hostWaitMs = 0, devSpanMs = 0;
   uint64_t exchangeChecked = 0;    // (source, chunk, partition) runs whose content was verified (verifyExchange)
+  double verifyMs = 0;             // host wall of that verification (excluded from joinMs / networkMs; the
+                                   // device spans devNetworkMs / devSpanMs still contain its kernels)
   uint32_t passes = 1;             // capacity spill: key-hash passes the join ran in (JoinConfig::passes)
   double compactMs = 0;            // capacity spill: host wall of the per-pass compaction (in joinMs)
   // Capacity spill of the bitmap plan: partition-group passes of the last
