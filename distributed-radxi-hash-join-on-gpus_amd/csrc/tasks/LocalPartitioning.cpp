@@ -30,9 +30,11 @@ void LocalPartitioning::execute() {
 }
 
 bool LocalPartitioning::overflowed() const {
-  if (!overflowFlag) return false;
-  HIP_CHECK(hipStreamSynchronize(ctx->stream()));  // no-op after the caller's sync
-  return *overflowBack != 0;
+  if (overflowFlag.empty()) return false;
+  ctx->synchronize();  // no-op after the caller's sync
+  for (unsigned int *b : overflowBack)
+    if (b && *b != 0) return true;
+  return false;
 }
 
 void LocalPartitioning::partition(data::Window *w, int which) {
@@ -141,10 +143,12 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
     uint32_t *dLb = ctx->workspace().getArray<uint32_t>(owned + 1);
     ctx->copy(dItems, it.data(), (uint64_t)nItems * sizeof(kernels::LocalItem), true, false);
     ctx->copy(dLb, lb.data(), (owned + 1) * 4ull, true, false);
-    if (!overflowFlag) {
-      overflowFlag = ctx->workspace().getArray<unsigned int>(1);
-      ctx->zero(overflowFlag, sizeof(unsigned int));
+    if (overflowFlag.size() <= (size_t)which) {
+      overflowFlag.resize(which + 1, nullptr);
+      overflowBack.resize(which + 1, nullptr);
     }
+    if (!overflowFlag[which]) overflowFlag[which] = ctx->workspace().getArray<unsigned int>(1);
+    ctx->zero(overflowFlag[which], sizeof(unsigned int));
     performance::Measurements::add("LPHISTELEM", (double)(xp.recvTotal / S), "tuples");
     // Back-to-back spans on one stream share their boundary events.
     hipEvent_t p0 = tl.mark(ctx->stream());
@@ -161,11 +165,10 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
     kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, gcur, false, sout, ctx->stream(), gend,
                           split, plan.localGeometry, frag);
     tl.endAt("LPPART", tl.mark(ctx->stream()));
-    kernels::claimOverflow(gcur, gend, P, overflowFlag, ctx->stream());
-    // Read back with the join's final synchronisation (the flag accumulates
-    // over sides; the last copy enqueued sees them all).
-    if (!overflowBack) overflowBack = ctx->staging().getArray<unsigned int>(1);
-    ctx->readBack(overflowBack, overflowFlag, sizeof(unsigned int));
+    kernels::claimOverflow(gcur, gend, P, overflowFlag[which], ctx->stream());
+    // Read back with the join's final synchronisation (one flag per side).
+    if (!overflowBack[which]) overflowBack[which] = ctx->staging().getArray<unsigned int>(1);
+    ctx->readBack(overflowBack[which], overflowFlag[which], sizeof(unsigned int));
     // Final claim cursors are the partition ends (valid when no slot overflowed).
     w->setPartitioned(sout, pbeg, bits, reinterpret_cast<const uint64_t *>(gcur), split.hi, std::max<uint64_t>(cap, 1));
     return;

@@ -69,8 +69,11 @@ class LocalPartitioning : public Task {
   bool forceExact;
   bool anySampled = false;
   bool innerDone = false;  // partitionSide(inner, 0) ran already: execute() does the outer side only
-  unsigned int *overflowFlag = nullptr;  // device
-  unsigned int *overflowBack = nullptr;  // pinned copy, refreshed after every sampled side
+  // Per side (`which`): a device flag raised by an overflowing sampled slot
+  // and its pinned copy, read back on the stream that ran that side (the
+  // inner side may run on a stream of its own, JoinConfig::overlapLocal).
+  std::vector<unsigned int *> overflowFlag;  // device
+  std::vector<unsigned int *> overflowBack;  // pinned
 };
 
 }  // namespace tasks
