@@ -171,6 +171,12 @@ def build_sanitized(kind: str = "address", jobs: int | None = None, verbose: boo
     kflags = HIP_FLAGS + ["-D_GLIBCXX_USE_CXX11_ABI=1"]
 
     def compile_kernel(src):
+        # The kernels are not sanitized: the main build's object of the same
+        # source, headers and flags is reused when it exists (a gfx950 compile
+        # of partition.hip takes minutes).
+        main = _obj(src, kflags, hdr)
+        if main.exists():
+            return main
         obj = odir / f"{str(src.relative_to(CSRC)).replace('/', '_')}.{hashlib.sha1(src.read_bytes() + hdr.encode()).hexdigest()[:16]}.k.o"
         if not obj.exists():
             _run([HIPCC, *kflags, "-c", str(src), "-o", str(obj) + ".tmp"], verbose)
