@@ -38,6 +38,11 @@ constexpr uint32_t BPK_SLOTS = 4;
 //    hash64 is three quarter-rate multiplies).
 // Table: the same 4-slot buckets + fill counters as bpKeyCountKernel.
 constexpr uint32_t KS_CHUNK = 32;
+// Spans a counted-table workgroup takes from its queue at a time.  Counted
+// spans are few on unique keys (the partitions just above rChunk: ~360 at
+// 1B x 1B) and each costs ~4 us: grabbing 32 at a time left 12 workgroups
+// working through them one after another (0.124 ms per join).
+constexpr uint32_t KC_GRAB = 4;
 
 __global__ __launch_bounds__(KT_EMIT_T) void bpEmitSpansKernel(const uint64_t *__restrict__ partR,
                                                          const uint64_t *__restrict__ partREnd,
@@ -631,7 +636,12 @@ __global__ __launch_bounds__(T, MINW) void bpKeyCountedSpansKernel(KsSrc<T, K, t
   uint32_t *qbase = reinterpret_cast<uint32_t *>(wsum + T / WAVE);
   constexpr uint32_t BATCH = T * K;
   const uint32_t t = threadIdx.x;
-  const uint32_t n = min(*nSpansPtr, capacity);
+  const uint32_t n = __builtin_amdgcn_readfirstlane(min(*nSpansPtr, capacity));
+  // Workgroups past the spans' chunk count have nothing to take from the
+  // queue: they leave before clearing a 72 KiB table (with no heavy spans --
+  // unique keys -- the whole launch of 512 groups cost ~0.12 ms per join).
+  // The remaining groups drain the queue (a group may take several chunks).
+  if (blockIdx.x >= (n + KC_GRAB - 1) / KC_GRAB) return;  // uniform per workgroup
   {
     uint4 *t4 = reinterpret_cast<uint4 *>(smem);  // entries (all ones) then counts (zero)
     for (uint32_t i = t; i < KC_E * 12 / 16; i += T)
@@ -705,11 +715,11 @@ __global__ __launch_bounds__(T, MINW) void bpKeyCountedSpansKernel(KsSrc<T, K, t
     __syncthreads();
   };
   for (;;) {
-    if (t == 0) *qbase = atomicAdd(queue, KS_CHUNK);
+    if (t == 0) *qbase = atomicAdd(queue, KC_GRAB);
     __syncthreads();  // (first round: also orders the table clear before any build)
     const uint32_t base = __builtin_amdgcn_readfirstlane(*qbase);
     if (base >= n) break;
-    const uint32_t nc = min(KS_CHUNK, n - base);
+    const uint32_t nc = min(KC_GRAB, n - base);
     if (t < nc) desc[t] = spans[base + t];
     __syncthreads();
     loadSpan(desc[0], ra, sa);
