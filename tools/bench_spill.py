@@ -24,7 +24,12 @@ import hpcjoin  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--size", type=float, default=1e9, help="tuples per relation")
+    ap.add_argument("--size", type=float, default=1e9, help="tuples per relation (inner; outer too unless --outer-size)")
+    ap.add_argument("--outer-size", type=float, default=0, help="outer tuples (0: --size)")
+    ap.add_argument("--outer-dist", default="unique", choices=["unique", "zipf", "uniform"],
+                    help="outer keys: unique, or Zipf / uniform over the inner key domain (BASELINE config 4: "
+                         "--size 1e9 --outer-size 16e9 --outer-dist zipf, 272 GB of relations on one GPU)")
+    ap.add_argument("--theta", type=float, default=0.75)
     ap.add_argument("--budget-frac", type=float, default=0.0,
                     help="memory budget of one pass (its pass buffers + its workspace) as a fraction of the "
                          "single-pass workspace estimate; 0: what HBM has free")
@@ -37,10 +42,16 @@ def main():
     C = hpcjoin.require_native()
     ctx = C.ExecContext("device", 0, C.LocalCommunicator())
     G = int(args.size)
+    GS = int(args.outer_size) or G
     R = C.Relation(G, G, args.input, 0)
-    S = C.Relation(G, G, args.input, 0)
-    R.generate(C.GenSpec(seed=1234), 0)
-    S.generate(C.GenSpec(seed=4321), 0)
+    S = C.Relation(GS, GS, args.input, 0)
+    inner = C.GenSpec(seed=1234)
+    outer = (C.GenSpec(seed=4321) if args.outer_dist == "unique" else
+             C.GenSpec(distribution=getattr(C.KeyDistribution, args.outer_dist.upper()), seed=4321, domain=G,
+                       zipf_theta=args.theta))
+    R.generate(inner, 0)
+    S.generate(outer, 0)
+    expected = C.Relation.expected_matches(inner, G, outer, GS)
     torch.cuda.synchronize()
     free0, total = torch.cuda.mem_get_info()
     probe = C.JoinConfig()
@@ -63,19 +74,23 @@ def main():
                           "single_pass_workspace_estimate_GB": round(est / 1e9, 1),
                           "hbm_free_after_relations_GB": round(free0 / 1e9, 1)}), flush=True)
         raise
-    times, res = [], first
+    times, res, results = [], first, []
     for _ in range(args.steps):
         t0 = time.perf_counter()
         res = j.run()
         times.append((time.perf_counter() - t0) * 1e3)
-    out = {"bench": "capacity_spill", "size": G, "input": args.input, "relations_GB": round(2 * G * 16 / 1e9, 1),
+        results.append(res)
+    out = {"bench": "capacity_spill", "size": G, "outer_size": GS, "outer_dist": args.outer_dist,
+           "input": args.input, "relations_GB": round((G + GS) * 16 / 1e9, 1),
            "hbm_total_GB": round(total / 1e9, 1), "hbm_free_after_relations_GB": round(free0 / 1e9, 1),
            "single_pass_workspace_estimate_GB": round(est / 1e9, 1),
            "workspace_budget_GB": round(cfg.workspace_budget / 1e9, 1) if cfg.workspace_budget else None,
            "passes": j.spill_passes, "group_passes": res["group_passes"] if res else None, "setup_ms": round(setup_ms, 1), "first_join_ms": round(first["join_ms"], 2),
            "ms_per_join": round(sum(times) / len(times), 2), "join_ms": [round(t, 2) for t in times],
-           "compact_ms": round(res["compact_ms"], 2), "value_Gtuples_per_s": round(2 * G / (sum(times) / len(times)) / 1e6, 2),
-           "matches": res["global_matches"], "expected_matches": G, "correct": res["global_matches"] == G,
+           "compact_ms": round(res["compact_ms"], 2),
+           "value_Gtuples_per_s": round((G + GS) / (sum(times) / len(times)) / 1e6, 2),
+           "matches": res["global_matches"], "expected_matches": expected,
+           "correct": all(r["global_matches"] == expected for r in [first] + results),
            "spill": {k: (round(v / 1e9, 2) if k.endswith("bytes") else v) for k, v in j.spill_info.items()},
            "plan": repr(j.plan)}
     del j
@@ -90,7 +105,7 @@ def main():
             r1 = jr.run()
             t.append((time.perf_counter() - t0) * 1e3)
         out["single_pass_ms"] = round(sum(t) / len(t), 2)
-        out["single_pass_correct"] = r1["global_matches"] == G
+        out["single_pass_correct"] = r1["global_matches"] == expected
         del jr
     print(json.dumps(out), flush=True)
     del ctx
