@@ -361,7 +361,7 @@ double timeDevice(const std::function<void(hipStream_t)> &fn, int iters) {
 // Times the network scatter kernel alone (cursors precomputed) in one of the
 // ablation modes; returns ms per call.
 double benchScatter(const at::Tensor &tuples, int64_t bits, int64_t mode, int iters, int64_t maxBlocks,
-                    int64_t geometry) {
+                    int64_t geometry, int64_t roundLp) {
   checkTuples(tuples, "tuples");
   setDevice(tuples);
   const uint64_t n = tuples.size(0);
@@ -370,7 +370,13 @@ double benchScatter(const at::Tensor &tuples, int64_t bits, int64_t mode, int it
   at::Tensor blockHist = at::empty({(int64_t)F * g.blocks}, like(tuples, at::kInt));
   at::Tensor totals = at::empty({(int64_t)F}, like(tuples));
   at::Tensor cursors = at::empty({(int64_t)F * g.blocks}, like(tuples));
-  at::Tensor out = at::empty({(int64_t)n}, like(tuples));
+  // mode 3 (round-interleaved slices): slice i = g * F + d starts at logical
+  // i << lv; the write-out sends logical [i | j | o] to physical [j | i | o].
+  uint32_t rs[3] = {(uint32_t)roundLp, 0, 0};
+  while ((1u << rs[2]) < 8 * F) ++rs[2];
+  while ((double)(1ull << rs[1]) < 1.05 * (double)n / (8.0 * F) + 64) ++rs[1];
+  JOIN_ASSERT(mode != 3 || rs[1] + rs[2] <= 32, "benchScatter", "mode 3 logical space past 32 bits");
+  at::Tensor out = at::empty({mode == 3 ? (int64_t)1 << (rs[1] + rs[2]) : (int64_t)n}, like(tuples));
   kernels::netHistogram(ptr<data::Tuple>(tuples), n, bits, g, ptr<uint32_t>(blockHist), nullptr);
   kernels::digitTotals(ptr<uint32_t>(blockHist), F, g.blocks, g.blocks, 1, ptr<uint64_t>(totals), nullptr);
   at::Tensor base = (at::cumsum(totals, 0) - totals).contiguous();
@@ -379,13 +385,17 @@ double benchScatter(const at::Tensor &tuples, int64_t bits, int64_t mode, int it
   at::Tensor gcur32 = at::empty({8 * (int64_t)F}, like(tuples, at::kInt));
   kernels::netGroupCursors(ptr<uint32_t>(blockHist), F, g.blocks, g.blocks, ptr<uint64_t>(base), gcur32.data_ptr(),
                            true, nullptr);
+  if (mode == 3)
+    gcur32 = (at::arange(8 * (int64_t)F, like(tuples, at::kLong)) * ((int64_t)1 << rs[1])).to(at::kInt).contiguous();
   at::Tensor work = gcur32.clone();
+  at::Tensor meta = at::tensor({(int32_t)rs[0], (int32_t)rs[1], (int32_t)rs[2], 0}, like(tuples, at::kInt));
   HIP_CHECK(hipDeviceSynchronize());
   return timeDevice(
       [&](hipStream_t s) {
         HIP_CHECK(hipMemcpyAsync(work.data_ptr(), gcur32.data_ptr(), 8 * F * 4, hipMemcpyDeviceToDevice, s));
         kernels::scatterAblation(ptr<data::Tuple>(tuples), n, bits, 32, g, ptr<uint64_t>(cursors), ptr<uint64_t>(out),
-                                 (int)mode, (int)geometry, s, work.data_ptr());
+                                 (int)mode, (int)geometry, s, work.data_ptr(),
+                                 mode == 3 ? static_cast<const uint32_t *>(meta.data_ptr()) : nullptr);
       },
       iters);
 }
@@ -557,6 +567,7 @@ py::dict resultToDict(const operators::JoinResult &r) {
   d["reruns"] = r.reruns;
   d["sampled_network"] = r.sampledNetwork;
   d["network_fallbacks"] = r.networkFallbacks;
+  d["round_windows"] = r.roundWindows;
   d["sampled_local"] = r.sampledLocal;
   d["bitmap_join"] = r.bitmapJoin;
   d["local_fallbacks"] = r.localFallbacks;
@@ -691,6 +702,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("local_item_tiles", &core::JoinConfig::localItemTiles)
       .def_readwrite("local_geometry", &core::JoinConfig::localGeometry)
       .def_readwrite("local_sample_stride", &core::JoinConfig::localSampleStride)
+      .def_readwrite("round_lp", &core::JoinConfig::roundLp)
       .def_readwrite("output_capacity", &core::JoinConfig::outputCapacity)
       .def_readwrite("codec_extra_ps_per_tuple", &core::JoinConfig::codecExtraPsPerTuple)
       .def_property(
@@ -1387,7 +1399,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   ops.def("bench_host_link", &benchHostLink, py::arg("bytes") = (uint64_t)1 << 30, py::arg("device") = 0,
           py::arg("iters") = 5);
   ops.def("bench_scatter_ms", &benchScatter, py::arg("tuples"), py::arg("bits"), py::arg("mode") = 0,
-          py::arg("iters") = 10, py::arg("max_blocks") = 2048, py::arg("geometry") = 0);
+          py::arg("iters") = 10, py::arg("max_blocks") = 2048, py::arg("geometry") = 0, py::arg("round_lp") = 6);
   ops.def("bench_histogram_ms", &benchHistogram, py::arg("tuples"), py::arg("bits"), py::arg("iters") = 10);
   ops.def("partition_tile", []() { return kernels::PART_TILE; });
+  // Round-interleaved window slots (kernels::RoundMap), for the layout tests.
+  ops.def(
+      "round_slot",
+      [](uint64_t logical, uint32_t lp, uint32_t lv, uint32_t lns) {
+        kernels::RoundMap m;
+        m.lp = lp;
+        m.lv = lv;
+        m.lns = lns;
+        return m(logical);
+      },
+      py::arg("logical"), py::arg("lp"), py::arg("lv"), py::arg("lns"));
+  ops.def("round_slots", &kernels::roundSlots, py::arg("max_cap"), py::arg("lp"), py::arg("lns"));
 }

@@ -46,6 +46,7 @@ JoinPlan makePlan(const JoinConfig &cfg, uint32_t numberOfNodes, uint64_t global
   p.localHistogram = cfg.localHistogram;
   p.sampleStride = std::max<uint32_t>(1, cfg.sampleStride);
   p.localSampleStride = std::max<uint32_t>(1, cfg.localSampleStride);
+  p.roundLp = std::min<uint32_t>(cfg.roundLp, 16);
   p.sChunk = std::max<uint32_t>(1024, cfg.sChunk);
 
   const uint32_t maxBits = Configuration::GPU_MAX_FANOUT_BITS - 1;  // 1024-way per pass

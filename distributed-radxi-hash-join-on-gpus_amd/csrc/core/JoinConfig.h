@@ -99,6 +99,10 @@ struct JoinConfig {
   HistogramMode localHistogram = HistogramMode::Auto;
   uint32_t sampleStride = 64;   // sampled network pass: histogram 1 tile in sampleStride (per-slot counts ~1e5+)
   uint32_t localSampleStride = 16;  // sampled local pass: 1 tile in localSampleStride of every work item
+  // Single-rank sampled network windows: claim slices in rounds of
+  // 2^roundLp-slot pieces (kernels::RoundMap) when the slices are even enough
+  // to fit; 0 = linear slices.
+  uint32_t roundLp = 9;
   WireCodecMode wireCodec = WireCodecMode::Auto;
   bool splitLocal = true;       // device: split local pass output (u32 rid + u16 fragment columns) when they fit
   // N > 1, LPT: a network partition above one rank's fair share of |R| + |S|
@@ -189,6 +193,7 @@ struct JoinPlan {
   HistogramMode localHistogram = HistogramMode::Exact;  // resolved per window size by LocalPartitioning
   uint32_t sampleStride = 64;
   uint32_t localSampleStride = 16;
+  uint32_t roundLp = 0;  // round-interleaved sampled network window (JoinConfig::roundLp; 0 = linear)
   AssignmentPolicy assignment = AssignmentPolicy::LPT;
   // Wire codec per relation (0 = inner, 1 = outer): bits per tuple (0 = off),
   // rid bits, and the rid base of every (rank, exchange chunk), rank-major.

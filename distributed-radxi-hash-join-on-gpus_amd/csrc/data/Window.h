@@ -102,6 +102,10 @@ class Window {
   void assertAllTuplesWritten();
 
   void *getData() { return data; }
+  // Slot map of a sampled single-rank network window (kernels::RoundMap):
+  // the plan's segment offsets are logical positions; identity by default.
+  void setRoundMap(const kernels::RoundMap &m) { roundMap_ = m; }
+  const kernels::RoundMap &roundMap() const { return roundMap_; }
   uint32_t tupleBytes() const { return elemBytes ? elemBytes : (wide ? 16 : 8); }
   bool holdsFragments() const { return elemBytes == 4; }
   bool isWide() const { return wide; }
@@ -134,6 +138,7 @@ class Window {
   histograms::AssignmentMap *assignment;
   core::ExecContext *ctx;
   bool wide;
+  kernels::RoundMap roundMap_;
   uint32_t elemBytes = 0;  // 0: the tuple format's size
   bool open = false;
   std::vector<hipEvent_t> ready, done;

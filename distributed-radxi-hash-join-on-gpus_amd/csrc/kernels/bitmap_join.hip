@@ -45,7 +45,18 @@ template <typename CurT>
 struct ClaimSrc {
   const CurT *start, *cur, *end;
   uint32_t F;
+  const uint32_t *roundMeta;  // BitmapSlices::roundMeta
   __device__ __forceinline__ uint32_t groups() const { return CLAIM_GROUPS; }
+  // Slot map of the fragment window (RoundMap), decided by the layout kernel.
+  __device__ __forceinline__ RoundMap roundMap() const {
+    RoundMap m;
+    if (roundMeta) {
+      m.lp = roundMeta[0];
+      m.lv = roundMeta[1];
+      m.lns = roundMeta[2];
+    }
+    return m;
+  }
   __device__ __forceinline__ void get(uint32_t d, uint32_t g, uint64_t &b, uint64_t &len, uint32_t &flags) const {
     const size_t i = (size_t)g * F + d;
     const uint64_t s0 = start[i], c = cur[i], e = end[i];
@@ -62,6 +73,7 @@ struct TableSrc {
   const uint64_t *len;
   uint32_t G;
   __device__ __forceinline__ uint32_t groups() const { return G; }
+  __device__ __forceinline__ RoundMap roundMap() const { return RoundMap(); }
   __device__ __forceinline__ void get(uint32_t d, uint32_t g, uint64_t &b, uint64_t &n, uint32_t &) const {
     const size_t i = (size_t)d * G + g;
     b = start[i];
@@ -95,10 +107,11 @@ __device__ __forceinline__ void visitSlice64(const uint64_t *__restrict__ src, u
 // The walk of long slices (N = 1 at 1B: 1.40 ms for the join kernel vs 1.49
 // with the flat walk below, whose address select costs more than the two
 // latencies per slice start it saves when slices are long).
+// src[b, b + len) in logical positions (b a multiple of 4), at rm's slots.
 template <int NTH, int U, typename Fn>
-__device__ __forceinline__ void visitSlice32(const uint32_t *__restrict__ src, uint64_t len, Fn &&fn) {
+__device__ __forceinline__ void visitSlice32(const uint32_t *__restrict__ src, uint64_t b, uint64_t len,
+                                             const RoundMap &rm, Fn &&fn) {
   const uint32_t t = threadIdx.x;
-  const u32x4 *v = reinterpret_cast<const u32x4 *>(src);
   const uint64_t nv = len >> 2;
   constexpr uint64_t STEP = (uint64_t)NTH * U;
   u32x4 cur[U], nxt[U];
@@ -106,7 +119,7 @@ __device__ __forceinline__ void visitSlice32(const uint32_t *__restrict__ src, u
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       const uint64_t i = i0 + (uint64_t)k * NTH + t;
-      if (i < nv) x[k] = __builtin_nontemporal_load(v + i);
+      if (i < nv) x[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src + rm(b + (i << 2))));
     }
   };
   if (nv) load(cur, 0);
@@ -126,7 +139,7 @@ __device__ __forceinline__ void visitSlice32(const uint32_t *__restrict__ src, u
     for (int k = 0; k < U; ++k) cur[k] = nxt[k];
   }
   const uint32_t rem = (uint32_t)(len & 3);
-  if (t < rem) fn((uint64_t)src[(nv << 2) + t]);
+  if (t < rem) fn((uint64_t)src[rm(b + (nv << 2) + t)]);
 }
 
 // fn(fragment) for every u32 fragment of partition d: its
@@ -165,6 +178,7 @@ __device__ __forceinline__ void visitClaim(const uint32_t *__restrict__ src, con
     sAdj[t] = (sBase[t] >> 2) - pre;
   }
   __syncthreads();
+  const RoundMap rm = cs.roundMap();  // vector i of the stream: slot rm(4 (i + a)) / 4
   static_assert(G == 8, "visitClaim: the slice map is written out for 8 XCD groups");
   const uint64_t p1 = uniform64(sPre[1]), p2 = uniform64(sPre[2]), p3 = uniform64(sPre[3]),
                  p4 = uniform64(sPre[4]), p5 = uniform64(sPre[5]), p6 = uniform64(sPre[6]),
@@ -184,7 +198,7 @@ __device__ __forceinline__ void visitClaim(const uint32_t *__restrict__ src, con
     a += i >= p5 ? d5 : 0;
     a += i >= p6 ? d6 : 0;
     a += i >= p7 ? d7 : 0;
-    return v + (i + a);
+    return v + (rm((i + a) << 2) >> 2);
   };
   constexpr uint64_t STEP = (uint64_t)NTH * U;
   u32x4 cur[U], nxt[U];
@@ -214,7 +228,7 @@ __device__ __forceinline__ void visitClaim(const uint32_t *__restrict__ src, con
   if (t < 4 * G) {
     const uint32_t g = t >> 2, j = t & 3;
     const uint64_t len = sLen[g];
-    if (j < (uint32_t)(len & 3)) fn((uint64_t)src[sBase[g] + (len & ~3ull) + j]);
+    if (j < (uint32_t)(len & 3)) fn((uint64_t)src[rm(sBase[g] + (len & ~3ull) + j)]);
   }
 }
 
@@ -229,10 +243,11 @@ __device__ __forceinline__ void visitPartition(const E *__restrict__ src, const 
       visitClaim<NTH, U>(src, ss, d, flags, fn);
       return;
     }
+    const RoundMap rm = ss.roundMap();
     for (uint32_t g = 0; g < ss.groups(); ++g) {
       uint64_t b, len;
       ss.get(d, g, b, len, flags);
-      visitSlice32<NTH, U>(src + b, len, fn);
+      visitSlice32<NTH, U>(src, b, len, rm, fn);
     }
   } else {
     for (uint32_t g = 0; g < ss.groups(); ++g) {
@@ -474,13 +489,13 @@ static S makeSrc(const BitmapSlices &b, uint32_t F);
 template <>
 ClaimSrc<uint32_t> makeSrc(const BitmapSlices &b, uint32_t F) {
   return ClaimSrc<uint32_t>{static_cast<const uint32_t *>(b.start), static_cast<const uint32_t *>(b.cur),
-                            static_cast<const uint32_t *>(b.end), F};
+                            static_cast<const uint32_t *>(b.end), F, b.roundMeta};
 }
 template <>
 ClaimSrc<unsigned long long> makeSrc(const BitmapSlices &b, uint32_t F) {
   return ClaimSrc<unsigned long long>{static_cast<const unsigned long long *>(b.start),
                                       static_cast<const unsigned long long *>(b.cur),
-                                      static_cast<const unsigned long long *>(b.end), F};
+                                      static_cast<const unsigned long long *>(b.end), F, b.roundMeta};
 }
 template <>
 TableSrc makeSrc(const BitmapSlices &b, uint32_t) {

@@ -143,6 +143,26 @@ void netCursors(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uint32_t
 // one device atomic per digit per tile, so the workgroups of an XCD append to
 // ONE stream per digit and output lines fill inside that XCD's L2.
 constexpr uint32_t CLAIM_GROUPS = 8;
+// Round-interleaved claim slices (single-rank network windows).  A linear
+// window puts every slice's run contiguously, so a tile's write-out -- runs
+// for all G x F slices -- lands on G x F different pages spread over the whole
+// window and the scatter's translation misses run at ~0.1 per tuple
+// (rocprofv3 TCP_UTCL1_TRANSLATION_MISS, 8.9e7 per 1e9-tuple call).  Here
+// slice i (= g * F + d, the claim-cursor index) owns logical positions
+// L = i << lv | k, and L lives at physical slot
+//   (k >> lp) << (lns + lp) | i << lp | (k & (2^lp - 1))   (lns = log2(G * F)):
+// round j holds the j-th 2^lp-slot piece of every slice, so writers that
+// advance through their slices at similar rates all write inside one or two
+// rounds (a few MB) at any moment.  lp = lv = 0 is the identity (linear).
+// Physical slots used: ceil(max slice capacity / 2^lp) rounds of 2^(lns + lp).
+struct RoundMap {
+  uint32_t lp = 0, lv = 0, lns = 0, pad = 0;
+  HJ_HD uint64_t operator()(uint64_t L) const {
+    const uint64_t k = L & ((1ull << lv) - 1);
+    return ((k >> lp) << (lns + lp)) | ((L >> lv) << lp) | (k & ((1ull << lp) - 1));
+  }
+  HJ_HD bool on() const { return lv != 0; }
+};
 // 32-bit cursors whenever every output position fits (half the atomics' bytes).
 inline bool cursorsNarrow(uint64_t outSize) { return outSize < (1ull << 32); }
 // gcur[c][g][d] (u32 if narrow else u64): start of group g's slice of digit d in chunk c.
@@ -157,7 +177,7 @@ void netGroupCursors(const uint32_t *blockHist, uint32_t F, uint32_t blocks, uin
 void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift, const PartitionGeometry &g,
                 uint32_t blockBegin, uint32_t blockEnd, void *gcur, uint64_t *out, hipStream_t s,
                 uint32_t keyBits = 64, KeyMix mix = KeyMix(), const void *gend = nullptr, int narrowMode = -1,
-                bool withRids = true);
+                bool withRids = true, const uint32_t *roundMeta = nullptr);
 void netScatterWide(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g,
                     uint32_t blockBegin, uint32_t blockEnd, void *gcur, data::Tuple *out, hipStream_t s,
                     KeyMix mix = KeyMix(), const void *gend = nullptr, int narrowMode = -1);
@@ -169,7 +189,8 @@ void netScatterWide(const data::Tuple *in, uint64_t n, uint32_t bits, const Part
 HJ_HD bool fragWordFits(uint32_t keyBits, uint32_t bits) { return keyBits <= 32 + bits; }
 void netScatterFrag(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g, uint32_t blockBegin,
                     uint32_t blockEnd, void *gcur, uint32_t *out, hipStream_t s, uint32_t keyBits,
-                    KeyMix mix = KeyMix(), const void *gend = nullptr, int narrowMode = -1);
+                    KeyMix mix = KeyMix(), const void *gend = nullptr, int narrowMode = -1,
+                    const uint32_t *roundMeta = nullptr);
 // Partition-group pass of the same scatter: only tuples whose digit is in
 // [dLo, dLo + range) are written, into [G][range] bounded claim slices (gcur /
 // gend laid out by netSampledLayout with the same range); the others are read
@@ -199,7 +220,31 @@ struct LayoutInput {
   void *gstart, *gcur, *gend;
   unsigned long long *capacityUsed;
   bool clearSampled = false;  // zero `sampled` after reading it (DeviceControl totals)
+  // Round-interleaved slices (RoundMap), decided on the device: with
+  // roundMeta set, slices of 2^roundLp-slot pieces are used when the largest
+  // slice needs lv <= roundMaxLv bits and the rounds fit roundCapacity slots;
+  // roundMeta[0..2] = {lp, lv, lns} then (else zeros: linear slices).  Both
+  // the scatter (netScatter / netScatterFrag roundMeta) and the read-back
+  // take the map from there.  Needs G * F a power of two.
+  uint32_t *roundMeta = nullptr;
+  uint32_t roundLp = 0, roundMaxLv = 0;
+  uint64_t roundCapacity = 0;
 };
+// Piece size (log2 slots) of a round-interleaved window of elemBytes-wide
+// words: JoinConfig::roundLp is given for 8-byte words; 4-byte fragment
+// windows use pieces of the same bytes.  0 = linear slices.
+inline uint32_t roundLpFor(uint32_t roundLp, uint32_t elemBytes) {
+  return roundLp ? roundLp + (elemBytes == 4 ? 1 : 0) : 0;
+}
+// Slots a round-interleaved window needs for slices of at most maxCap tuples.
+HJ_HD uint64_t roundSlots(uint64_t maxCap, uint32_t lp, uint32_t lns) {
+  return ((maxCap + (1ull << lp) - 1) >> lp) << (lns + lp);
+}
+// Window slots of a sampled single-rank pass: the linear bound, or (roundLp >
+// 0) at least what round-interleaved slices need when every slice's sampled
+// estimate lands within 5 sigma of its group's mean (even data; skewed data
+// then gets linear slices inside the same window).
+uint64_t sampledWindowCapacity(const SampleScale &sc, uint32_t F, uint32_t roundLp);
 // range > 0: lay out only digits [dLo, dLo + range) of the [G][F] totals, as
 // [G][range] slices (a partition-group pass, netScatterFragRange).
 void netSampledLayout(const LayoutInput *sides, uint32_t count, uint32_t F, bool narrow, hipStream_t s,
@@ -213,10 +258,12 @@ void netSampledLayout(const LayoutInput *sides, uint32_t count, uint32_t F, bool
 // geometry: 0 = 256x16 (default), 1 = 512x16, 2 = 1024x8, 3 = 1024x16,
 // 4 = 256x16 with a separate LDS digit array, 5 = 256x8.
 // geometries 6..9 = claim mode (256x16, 512x16, 1024x16, 1024x8) using gcur
-// (u32 group cursors [8][F], re-initialised by the caller before each call).
+// (u32 group cursors [8][F], re-initialised by the caller before each call);
+// mode 3 = the real scatter into round-interleaved slices (device roundMeta,
+// RoundMap; gcur then holds logical slice starts).
 void scatterAblation(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift, const PartitionGeometry &g,
                      const uint64_t *cursors, uint64_t *out, int mode, int geometry, hipStream_t s,
-                     void *gcur = nullptr);
+                     void *gcur = nullptr, const uint32_t *roundMeta = nullptr);
 
 // Ablation baseline: one global atomic per tuple, no LDS staging
 // (reference histogram_build_global / reorder_global, kernels.cu:256-298).
@@ -242,8 +289,10 @@ constexpr uint32_t LOCAL_ITEM_MAX = LOCAL_ITEM_TILES * PART_TILE;  // 65536
 // digit = (word >> shift) & (2^bits - 1).  For compressed tuples word = value,
 // shift = keyShift; for wide tuples word = key, shift = networkBits; for u32
 // key fragments (frag) word = fragment, shift = 0.
+// rm: the network window's slot map (RoundMap; items are logical positions).
 void localHistogram(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift,
-                    uint32_t bits, uint32_t *itemHist, hipStream_t s, uint32_t sampleStride = 1, bool frag = false);
+                    uint32_t bits, uint32_t *itemHist, hipStream_t s, uint32_t sampleStride = 1, bool frag = false,
+                    RoundMap rm = RoundMap());
 // gcur[stream][F] (u32 if narrow else u64) claim slices + partBegin[owned*F+1].
 void localCursors(const uint32_t *itemHist, const uint32_t *lpItemBegin, uint32_t owned, uint32_t bits,
                   const uint64_t *lpBase, const LocalItem *items, void *gcur, bool narrow, uint64_t *partBegin,
@@ -276,7 +325,8 @@ constexpr uint32_t SPLIT_BYTES = 6;
 // the u16 column of fragment >> bits alone (out; split.hi unused).
 void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift,
                   uint32_t bits, void *gcur, bool narrow, void *out, hipStream_t s, const void *gend = nullptr,
-                  SplitLayout split = SplitLayout(), uint32_t geometry = 0, bool frag = false);
+                  SplitLayout split = SplitLayout(), uint32_t geometry = 0, bool frag = false,
+                  RoundMap rm = RoundMap());
 // Sampled local pass (no exact local histogram): itemHist from
 // localHistogram(sampleStride) -> per-final-partition capacities (estimate +
 // 8 sigma + 2% + 64) -> gapped partition-major layout: gcur = partBegin =
@@ -569,6 +619,9 @@ struct BitmapSlices {
   // inner side's slices): 0 / -1 = auto.
   uint32_t threads = 0;
   int32_t flat = -1;
+  // Claim: device {lp, lv, lns, 0} of a round-interleaved fragment window
+  // (RoundMap, LayoutInput::roundMeta); null = linear slices.
+  const uint32_t *roundMeta = nullptr;
 };
 // u32 words of one partition's bitmap (a power of two >= 4).
 uint32_t bitmapWords(uint32_t bits);

@@ -733,13 +733,15 @@ __device__ __forceinline__ void loadTile(const typename Pol::InT *__restrict__ s
 
 // Next tile into registers, branch-free: indices past the range end read its
 // last element (loaded, never ranked), so every tile issues exactly IPT loads.
+// im: slot map of the input (RoundMap; identity unless the local pass reads a
+// round-interleaved network window).
 template <class Pol, int NTH, int IPT>
 __device__ __forceinline__ void prefetchTile(const typename Pol::InT *__restrict__ in, uint64_t nbase, uint64_t last,
-                                             typename Pol::LoadT (&v)[IPT]) {
+                                             typename Pol::LoadT (&v)[IPT], const RoundMap &im = RoundMap()) {
 #pragma unroll
   for (int i = 0; i < IPT; ++i) {
     const uint64_t idx = nbase + (uint64_t)(i * NTH + threadIdx.x);
-    v[i] = Pol::load(in + (idx < last ? idx : last));
+    v[i] = Pol::load(in + im(idx < last ? idx : last));
   }
 }
 
@@ -786,7 +788,8 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
                                             uint32_t count, uint32_t F, const ScatterSmem<Pol, CurT, NTH * IPT> &l,
                                             const Pol &pol, typename Pol::OutT *__restrict__ out,
                                             typename Pol::LoadT (&v)[IPT], CurT *__restrict__ gcur,
-                                            ScatterProf &pf, uint64_t nbase, uint64_t nlast) {
+                                            ScatterProf &pf, uint64_t nbase, uint64_t nlast,
+                                            const RoundMap &im = RoundMap(), const RoundMap &om = RoundMap()) {
   constexpr uint32_t TILE = NTH * IPT;
   pf.start();
   constexpr bool EARLY = earlyPrefetch<Pol, IPT>();
@@ -834,7 +837,7 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
       if (wave0 + k * NTH < F) claim[k] = atomicAdd(d < F ? gcur + d : trash + t, (CurT)l.cnt[d]);
     }
   }
-  if constexpr (EARLY) prefetchTile<Pol, NTH, IPT>(in, nbase, nlast, v);
+  if constexpr (EARLY) prefetchTile<Pol, NTH, IPT>(in, nbase, nlast, v, im);
   pf.mark(2);
   // FILT: entry F (never counted) is scanned too: off[F] = kept tuples, and
   // the write-out stops there.
@@ -880,7 +883,7 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
       }
     }
     // Prefetch the next tile while this one is streamed out.
-    prefetchTile<Pol, NTH, IPT>(in, nbase, nlast, v);
+    prefetchTile<Pol, NTH, IPT>(in, nbase, nlast, v, im);
   }
   pf.mark(4);
   if constexpr (CLAIM) {
@@ -912,7 +915,7 @@ __device__ __forceinline__ void scatterTile(const typename Pol::InT *__restrict_
       const CurT pos = (CurT)(l.wbase[d] + (CurT)idx);
       bool ok = have;
       if constexpr (BOUNDED) ok = ok && pos < l.cursor[d];
-      storeSel(pol, out, (uint64_t)pos, x, ok, t);
+      storeSel(pol, out, om((uint64_t)pos), x, ok, t);
     } else if constexpr (MODE == 1) {
       if (have) out[base + idx] = pol.out(x);
       asm volatile("" ::"v"(l.wbase[d]));
@@ -936,19 +939,21 @@ template <class Pol, typename CurT, int NTH, int IPT, int MODE, bool CLAIM = fal
           int MAXD = 1>
 __device__ __forceinline__ void scatterRange(const typename Pol::InT *__restrict__ in, uint64_t begin, uint64_t end,
                                              uint32_t F, unsigned char *smem, const Pol &pol,
-                                             typename Pol::OutT *__restrict__ out, CurT *gcur = nullptr) {
+                                             typename Pol::OutT *__restrict__ out, CurT *gcur = nullptr,
+                                             const RoundMap &im = RoundMap(), const RoundMap &om = RoundMap()) {
   constexpr uint32_t TILE = NTH * IPT;
   const ScatterSmem<Pol, CurT, TILE> l(smem, F);
   typename Pol::LoadT v[IPT];
   ScatterProf pf;
-  if (begin < end) prefetchTile<Pol, NTH, IPT>(in, begin, end - 1, v);
+  if (begin < end) prefetchTile<Pol, NTH, IPT>(in, begin, end - 1, v, im);
   for (uint64_t base = begin; base < end; base += TILE) {
     if (base + TILE <= end)
       scatterTile<Pol, CurT, NTH, IPT, MODE, true, CLAIM, BOUNDED, MAXD>(in, base, end, TILE, F, l, pol, out, v,
-                                                                         gcur, pf, base + TILE, end - 1);
+                                                                         gcur, pf, base + TILE, end - 1, im, om);
     else
       scatterTile<Pol, CurT, NTH, IPT, MODE, false, CLAIM, BOUNDED, MAXD>(in, base, end, (uint32_t)(end - base), F, l,
-                                                                          pol, out, v, gcur, pf, base + TILE, end - 1);
+                                                                          pol, out, v, gcur, pf, base + TILE, end - 1,
+                                                                          im, om);
   }
   pf.flush();
   __syncthreads();
@@ -987,9 +992,16 @@ __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void netScatterKernel(
 template <class Pol, typename CurT, int NTH, int IPT, int MODE, bool BOUNDED, int MAXD>
 __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void netScatterClaimKernel(
     const typename Pol::InT *__restrict__ in, uint64_t n, uint32_t tpb, uint32_t F, Pol pol, uint32_t blockBegin,
-    CurT *__restrict__ gcur, typename Pol::OutT *out, const CurT *__restrict__ gend = nullptr) {
+    CurT *__restrict__ gcur, typename Pol::OutT *out, const CurT *__restrict__ gend = nullptr,
+    const uint32_t *__restrict__ roundMeta = nullptr) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t blk = blockBegin + blockIdx.x;
+  RoundMap om;  // output slot map, decided by the layout kernel (RoundMap)
+  if (roundMeta) {
+    om.lp = roundMeta[0];
+    om.lv = roundMeta[1];
+    om.lns = roundMeta[2];
+  }
   const uint32_t FP = padDigits(F);
   CurT *sliceEnd = reinterpret_cast<CurT *>(smem);  // the per-workgroup cursor array is unused in claim mode
   uint32_t *cnt = reinterpret_cast<uint32_t *>(reinterpret_cast<CurT *>(smem) + 2 * FP);
@@ -1002,7 +1014,8 @@ __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void netScatterClaimKe
   __syncthreads();
   const uint64_t begin = (uint64_t)blk * tpb * PART_TILE;
   const uint64_t end = min(n, begin + (uint64_t)tpb * PART_TILE);
-  scatterRange<Pol, CurT, NTH, IPT, MODE, true, BOUNDED, MAXD>(in, begin, end, F, smem, pol, out, gcur + grp);
+  scatterRange<Pol, CurT, NTH, IPT, MODE, true, BOUNDED, MAXD>(in, begin, end, F, smem, pol, out, gcur + grp,
+                                                               RoundMap(), om);
 }
 
 // Calls fn(std::integral_constant<int, MAXD>) with MAXD = padDigits(F) / NTH:
@@ -1049,7 +1062,8 @@ constexpr int CL_IPT = CL_IPT_DEFAULT;
 template <class Pol, int CL_IPT, int CL_NTH = 1024>
 static void launchNetClaimIpt(const Pol &pol, const data::Tuple *in, uint64_t n, uint32_t bits,
                               const PartitionGeometry &g, uint32_t blockBegin, uint32_t blockEnd, void *gcur,
-                              void *out, hipStream_t s, const void *gend, bool narrow, uint32_t digits = 0) {
+                              void *out, hipStream_t s, const void *gend, bool narrow, uint32_t digits = 0,
+                              const uint32_t *roundMeta = nullptr) {
   // digits: claim slices per group (filtered range passes); else 2^bits.
   const uint32_t F = digits ? digits : 1u << bits;
   const auto *src = reinterpret_cast<const typename Pol::InT *>(in);
@@ -1063,10 +1077,11 @@ static void launchNetClaimIpt(const Pol &pol, const data::Tuple *in, uint64_t n,
     auto *gc = reinterpret_cast<C *>(gcur);
     if (gend)
       hipLaunchKernelGGL((netScatterClaimKernel<Pol, C, CL_NTH, CL_IPT, 0, true, M>), grid, dim3(CL_NTH), lds, s, src,
-                         n, g.tilesPerBlock, F, pol, blockBegin, gc, dst, reinterpret_cast<const C *>(gend));
+                         n, g.tilesPerBlock, F, pol, blockBegin, gc, dst, reinterpret_cast<const C *>(gend),
+                         roundMeta);
     else
       hipLaunchKernelGGL((netScatterClaimKernel<Pol, C, CL_NTH, CL_IPT, 0, false, M>), grid, dim3(CL_NTH), lds, s,
-                         src, n, g.tilesPerBlock, F, pol, blockBegin, gc, dst, nullptr);
+                         src, n, g.tilesPerBlock, F, pol, blockBegin, gc, dst, nullptr, roundMeta);
   };
   withMaxd<CL_NTH>(F, [&](auto maxd) {
     if (narrow)
@@ -1087,33 +1102,34 @@ static void launchNetClaimIpt(const Pol &pol, const data::Tuple *in, uint64_t n,
 template <class Pol>
 static void launchNetClaim(const Pol &pol, const data::Tuple *in, uint64_t n, uint32_t bits,
                            const PartitionGeometry &g, uint32_t blockBegin, uint32_t blockEnd, void *gcur,
-                           void *out, hipStream_t s, const void *gend, bool narrow) {
+                           void *out, hipStream_t s, const void *gend, bool narrow,
+                           const uint32_t *roundMeta = nullptr) {
   // PartitionGeometry::nth = 512 (KernelVariants::netThreads): half-width
   // workgroups with the same per-thread tile, so two or three share a CU and
   // one's rank/scan/claim phases overlap another's loads and stores.
   if (g.nth == 512) {
     if constexpr (sizeof(typename Pol::StageT) == 4) {
       if (g.ipt == 16) {
-        launchNetClaimIpt<Pol, 16, 512>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
+        launchNetClaimIpt<Pol, 16, 512>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow, 0, roundMeta);
         return;
       }
     }
     launchNetClaimIpt<Pol, CL_IPT_DEFAULT, 512>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend,
-                                                narrow);
+                                                narrow, 0, roundMeta);
     return;
   }
   if constexpr (sizeof(typename Pol::StageT) == 4) {
     if (g.ipt == 16) {
-      launchNetClaimIpt<Pol, 16>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
+      launchNetClaimIpt<Pol, 16>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow, 0, roundMeta);
       return;
     }
   }
   if (g.ipt == 15 && narrow && bits == MAX_PART_BITS)
-    launchNetClaimIpt<Pol, 15>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
+    launchNetClaimIpt<Pol, 15>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow, 0, roundMeta);
   else if (g.ipt == 12)  // 12288-tuple tiles (sweep: longer runs per digit and tile)
-    launchNetClaimIpt<Pol, 12>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
+    launchNetClaimIpt<Pol, 12>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow, 0, roundMeta);
   else
-    launchNetClaimIpt<Pol, CL_IPT_DEFAULT>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
+    launchNetClaimIpt<Pol, CL_IPT_DEFAULT>(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow, 0, roundMeta);
 }
 
 void scatterProfile(unsigned long long out[10], bool reset) {
@@ -1135,7 +1151,7 @@ bool scatterProfileBuilt() {
 
 void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift, const PartitionGeometry &g,
                 uint32_t blockBegin, uint32_t blockEnd, void *gcur, uint64_t *out, hipStream_t s, uint32_t keyBits,
-                KeyMix mix, const void *gend, int narrowMode, bool withRids) {
+                KeyMix mix, const void *gend, int narrowMode, bool withRids, const uint32_t *roundMeta) {
   const bool narrow = narrowMode < 0 ? cursorsNarrow(n) : narrowMode != 0;
   HJ_CHECK(bits >= 1 && bits <= MAX_PART_BITS, "netScatter: bits=%u out of range", bits);
   HJ_CHECK(blockBegin <= blockEnd && blockEnd <= g.blocks, "netScatter: block range [%u,%u) of %u", blockBegin,
@@ -1147,7 +1163,7 @@ void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keySh
       kpol.mask = (1ull << bits) - 1;
       kpol.bits = bits;
       kpol.mix = mix;
-      launchNetClaim(kpol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
+      launchNetClaim(kpol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow, roundMeta);
     };
     if (mix.on)
       go(NetKeyPol<true>());
@@ -1161,11 +1177,11 @@ void netScatter(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keySh
   pol.keyShift = keyShift;
   pol.mix = mix;
   if (digitFitsOnTop(bits, keyShift, mix.on ? std::max(keyBits, mix.bits) : keyBits)) {
-    launchNetClaim(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
+    launchNetClaim(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow, roundMeta);
   } else {
     NetCompressedDigPol dpol;
     static_cast<NetCompressedPol &>(dpol) = pol;
-    launchNetClaim(dpol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
+    launchNetClaim(dpol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow, roundMeta);
   }
 }
 
@@ -1185,7 +1201,7 @@ void netScatterWide(const data::Tuple *in, uint64_t n, uint32_t bits, const Part
 
 void netScatterFrag(const data::Tuple *in, uint64_t n, uint32_t bits, const PartitionGeometry &g, uint32_t blockBegin,
                     uint32_t blockEnd, void *gcur, uint32_t *out, hipStream_t s, uint32_t keyBits, KeyMix mix,
-                    const void *gend, int narrowMode) {
+                    const void *gend, int narrowMode, const uint32_t *roundMeta) {
   const bool narrow = narrowMode < 0 ? cursorsNarrow(n) : narrowMode != 0;
   HJ_CHECK(bits >= 1 && bits <= MAX_PART_BITS, "netScatterFrag: bits=%u out of range", bits);
   const uint32_t kb = mix.on ? std::max(keyBits, mix.bits) : keyBits;
@@ -1198,7 +1214,7 @@ void netScatterFrag(const data::Tuple *in, uint64_t n, uint32_t bits, const Part
     pol.mask = (1ull << bits) - 1;
     pol.bits = bits;
     pol.mix = mix;
-    launchNetClaim(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow);
+    launchNetClaim(pol, in, n, bits, g, blockBegin, blockEnd, gcur, out, s, gend, narrow, roundMeta);
   };
   const bool digitOnTop = kb <= 32;  // fragment + digit fit the staged u32
   if (mix.on && digitOnTop)
@@ -1260,6 +1276,9 @@ struct LayoutSideArgs {
   CurT *gstart, *gcur, *gend;
   unsigned long long *capacityUsed;
   unsigned long long *clear;  // = sampled when it is DeviceControl scratch, else nullptr
+  uint32_t *roundMeta;        // LayoutInput::roundMeta
+  uint32_t roundLp, roundMaxLv;
+  unsigned long long roundCapacity;
 };
 
 // Workgroup i lays out side i (one or two sides per launch).
@@ -1276,6 +1295,7 @@ __global__ __launch_bounds__(LAY_NT) void netSampledLayoutKernel(LayoutSideArgs<
   CurT *__restrict__ gend = ls.gend;
   unsigned long long *__restrict__ capacityUsed = ls.capacityUsed;
   __shared__ unsigned long long wt[LAY_NT / WAVE];
+  __shared__ unsigned long long maxCapS;
   constexpr uint32_t G = NGROUPS;
   const uint32_t n = F * G;
   const uint32_t per = (n + LAY_NT - 1) / LAY_NT, t = threadIdx.x;
@@ -1304,6 +1324,30 @@ __global__ __launch_bounds__(LAY_NT) void netSampledLayoutKernel(LayoutSideArgs<
       local += cap[k];
     }
   }
+  // Round-interleaved slices (RoundMap) when the largest slice allows them.
+  uint32_t lv = 0, lns = 0;
+  unsigned long long roundUsed = 0;
+  if (ls.roundMeta) {  // uniform per workgroup
+    if (t == 0) maxCapS = 0;
+    __syncthreads();
+    unsigned long long m = 0;
+#pragma unroll
+    for (int k = 0; k < MAXPER; ++k) m = cap[k] > m ? cap[k] : m;
+    atomicMax(&maxCapS, m);
+    __syncthreads();
+    const unsigned long long maxCap = maxCapS;
+    while ((1u << lns) < n) ++lns;
+    uint32_t v = ls.roundLp;
+    while ((1ull << v) < maxCap) ++v;
+    roundUsed = roundSlots(maxCap, ls.roundLp, lns);
+    if ((1u << lns) == n && v <= ls.roundMaxLv && roundUsed <= ls.roundCapacity) lv = v;
+    if (t == 0) {
+      ls.roundMeta[0] = lv ? ls.roundLp : 0;
+      ls.roundMeta[1] = lv;
+      ls.roundMeta[2] = lv ? lns : 0;
+      ls.roundMeta[3] = 0;
+    }
+  }
   const unsigned long long incl = waveInclusiveScan<unsigned long long>(local);
   const int lane = t & (WAVE - 1), wid = t / WAVE;
   if (lane == WAVE - 1) wt[wid] = incl;
@@ -1315,13 +1359,14 @@ __global__ __launch_bounds__(LAY_NT) void netSampledLayoutKernel(LayoutSideArgs<
     const uint32_t j = j0 + k;
     if (k < (int)per && j < n) {
       const uint32_t i = (j % G) * F + j / G;
-      gstart[i] = (CurT)run;
-      gcur[i] = (CurT)run;
-      gend[i] = (CurT)(run + cap[k]);
+      const unsigned long long b = lv ? (unsigned long long)i << lv : run;
+      gstart[i] = (CurT)b;
+      gcur[i] = (CurT)b;
+      gend[i] = (CurT)(b + cap[k]);
       run += cap[k];
     }
   }
-  if (t == LAY_NT - 1) *capacityUsed = run;
+  if (t == LAY_NT - 1) *capacityUsed = lv ? roundUsed : run;
 }
 
 template <typename CurT>
@@ -1330,7 +1375,8 @@ static LayoutSideArgs<CurT> layoutSide(const LayoutInput &x) {
   return LayoutSideArgs<CurT>{sampled, x.sc,
                               static_cast<CurT *>(x.gstart), static_cast<CurT *>(x.gcur), static_cast<CurT *>(x.gend),
                               x.capacityUsed,
-                              x.clearSampled ? const_cast<unsigned long long *>(sampled) : nullptr};
+                              x.clearSampled ? const_cast<unsigned long long *>(sampled) : nullptr,
+                              x.roundMeta, x.roundLp, x.roundMaxLv, (unsigned long long)x.roundCapacity};
 }
 
 void netSampledLayout(const LayoutInput *sides, uint32_t count, uint32_t F, bool narrow, hipStream_t s, uint32_t dLo,
@@ -1339,6 +1385,10 @@ void netSampledLayout(const LayoutInput *sides, uint32_t count, uint32_t F, bool
   HJ_CHECK(count == 1 || count == 2, "netSampledLayout: %u sides", count);
   const uint32_t R = range ? range : F;
   HJ_CHECK(dLo + R <= F, "netSampledLayout: digits [%u, %u) of %u", dLo, dLo + R, F);
+  for (uint32_t k = 0; k < count; ++k)
+    HJ_CHECK(!sides[k].roundMeta || (range == 0 && sides[k].roundLp >= 1 && sides[k].roundLp <= 16),
+             "netSampledLayout: round slices need a whole-range layout and 1 <= lp <= 16 (lp %u, range %u)",
+             sides[k].roundLp, range);
   const LayoutInput &b = sides[count - 1];
   if (narrow)
     hipLaunchKernelGGL(netSampledLayoutKernel<uint32_t>, dim3(count), dim3(LAY_NT), 0, s,
@@ -1380,6 +1430,22 @@ SampleScale sampleScale(const PartitionGeometry &g, uint64_t n, uint32_t sampleS
   return sc;
 }
 
+uint64_t sampledWindowCapacity(const SampleScale &sc, uint32_t F, uint32_t roundLp) {
+  const uint64_t bound = sampledLayoutCapacityBound(sc, F);
+  if (!roundLp) return bound;
+  double maxCap = 0;
+  for (uint32_t g = 0; g < NGROUPS; ++g) {
+    if (sc.total[g] <= 0) continue;
+    const double scale = sc.seen[g] > 0 ? sc.total[g] / sc.seen[g] : 1.0;
+    const double est = sc.total[g] / F;
+    const double sigma = std::sqrt(std::max(est, scale) * scale);
+    maxCap = std::max(maxCap, est + (sc.sigmas + 5.0) * sigma + sc.frac * est + sc.floor + 16.0);
+  }
+  uint32_t lns = 0;
+  while ((1u << lns) < NGROUPS * F) ++lns;
+  return std::max<uint64_t>(bound, roundSlots((uint64_t)std::ceil(maxCap), roundLp, lns));
+}
+
 uint64_t sampledLayoutCapacityBound(const SampleScale &sc, uint32_t F) {
   // Per group: sum_d est_d = total_g; sum_d sqrt(max(est_d,scale) * scale) <=
   // sqrt(F * scale * (total_g + F * scale)) (Cauchy-Schwarz); + ceil and the 16-tuple
@@ -1395,7 +1461,8 @@ uint64_t sampledLayoutCapacityBound(const SampleScale &sc, uint32_t F) {
 }
 
 void scatterAblation(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t keyShift, const PartitionGeometry &g,
-                     const uint64_t *cursors, uint64_t *out, int mode, int geometry, hipStream_t s, void *gcur) {
+                     const uint64_t *cursors, uint64_t *out, int mode, int geometry, hipStream_t s, void *gcur,
+                     const uint32_t *roundMeta) {
   NetCompressedPol pol;
   pol.mask = (1ull << bits) - 1;
   pol.bits = bits;
@@ -1411,6 +1478,10 @@ void scatterAblation(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t 
       hipLaunchKernelGGL((netScatterClaimKernel<NetCompressedPol, uint32_t, NTH, IPT, 1, false, M>), dim3(g.blocks), \
                          dim3(NTH), lds, s, reinterpret_cast<const ulonglong2 *>(in), n, g.tilesPerBlock,         \
                          1u << bits, pol, 0u, gc, out);                                                           \
+    else if (mode == 3)                                                                                           \
+      hipLaunchKernelGGL((netScatterClaimKernel<NetCompressedPol, uint32_t, NTH, IPT, 0, false, M>), dim3(g.blocks), \
+                         dim3(NTH), lds, s, reinterpret_cast<const ulonglong2 *>(in), n, g.tilesPerBlock,         \
+                         1u << bits, pol, 0u, gc, out, nullptr, roundMeta);                                       \
     else                                                                                                          \
       hipLaunchKernelGGL((netScatterClaimKernel<NetCompressedPol, uint32_t, NTH, IPT, 0, false, M>), dim3(g.blocks), \
                          dim3(NTH), lds, s, reinterpret_cast<const ulonglong2 *>(in), n, g.tilesPerBlock,         \
@@ -1433,6 +1504,7 @@ void scatterAblation(const data::Tuple *in, uint64_t n, uint32_t bits, uint32_t 
   // before this one is ranked) ran 2 % slower in the 1B join (network pass
   // 8.78 vs 8.60 ms): the pass is bound by the scattered writes, not by load
   // latency.
+  HJ_CHECK(mode != 3 || (geometry >= 6 && geometry <= 9 && roundMeta), "scatterAblation: mode 3 needs a claim geometry");
   NetFragPol fpol;
   fpol.mask = (1ull << bits) - 1;
   fpol.bits = bits;
@@ -1510,7 +1582,7 @@ template <int WIDE>
 __global__ __launch_bounds__(NT) void localHistogramKernel(const void *__restrict__ in,
                                                            const LocalItem *__restrict__ items, uint32_t shift,
                                                            uint32_t bits, uint32_t *__restrict__ itemHist,
-                                                           uint32_t stride) {
+                                                           uint32_t stride, RoundMap rm) {
   extern __shared__ __attribute__((aligned(16))) uint32_t hsh[];
   const uint32_t F = 1u << bits;
   const uint64_t mask = F - 1;
@@ -1524,7 +1596,7 @@ __global__ __launch_bounds__(NT) void localHistogramKernel(const void *__restric
 #pragma unroll
     for (int i = 0; i < (int)PART_ITEMS; ++i) {
       const uint32_t idx = base + i * NT + threadIdx.x;
-      w[i] = idx < it.len ? localWord<WIDE>(in, it.begin + idx) : 0;
+      w[i] = idx < it.len ? localWord<WIDE>(in, rm(it.begin + idx)) : 0;
     }
 #pragma unroll
     for (int i = 0; i < (int)PART_ITEMS; ++i) {
@@ -1538,7 +1610,7 @@ __global__ __launch_bounds__(NT) void localHistogramKernel(const void *__restric
 }
 
 void localHistogram(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift,
-                    uint32_t bits, uint32_t *itemHist, hipStream_t s, uint32_t sampleStride, bool frag) {
+                    uint32_t bits, uint32_t *itemHist, hipStream_t s, uint32_t sampleStride, bool frag, RoundMap rm) {
   HJ_CHECK(bits <= MAX_PART_BITS, "localHistogram: bits=%u out of range", bits);
   HJ_CHECK(sampleStride >= 1, "localHistogram: sampleStride must be >= 1");
   HJ_CHECK(!(wide && frag), "localHistogram: fragments are not wide tuples");
@@ -1546,13 +1618,13 @@ void localHistogram(const void *in, bool wide, const LocalItem *items, uint32_t 
   const size_t lds = size_t(4) << bits << 2;
   if (frag)
     hipLaunchKernelGGL(localHistogramKernel<2>, dim3(nItems), dim3(NT), lds, s, in, items, shift, bits, itemHist,
-                       sampleStride);
+                       sampleStride, rm);
   else if (wide)
     hipLaunchKernelGGL(localHistogramKernel<1>, dim3(nItems), dim3(NT), lds, s, in, items, shift, bits, itemHist,
-                       sampleStride);
+                       sampleStride, rm);
   else
     hipLaunchKernelGGL(localHistogramKernel<0>, dim3(nItems), dim3(NT), lds, s, in, items, shift, bits, itemHist,
-                       sampleStride);
+                       sampleStride, rm);
   HIP_CHECK_LAUNCH();
 }
 
@@ -1747,7 +1819,7 @@ void claimOverflow(unsigned long long *gcur, const unsigned long long *gend, uin
 template <class Pol, typename CurT, int NTH, int IPT, bool BOUNDED, int MAXD>
 __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void localScatterClaimKernel(
     const typename Pol::InT *__restrict__ in, const LocalItem *__restrict__ items, uint32_t nItems, uint32_t F,
-    Pol pol, CurT *__restrict__ gcur, typename Pol::OutT *out, const CurT *__restrict__ gend) {
+    Pol pol, CurT *__restrict__ gcur, typename Pol::OutT *out, const CurT *__restrict__ gend, RoundMap im) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t q = (nItems + NGROUPS - 1) / NGROUPS;
   const uint32_t item = (blockIdx.x % NGROUPS) * q + blockIdx.x / NGROUPS;  // XCD-contiguous items
@@ -1763,7 +1835,7 @@ __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void localScatterClaim
   }
   __syncthreads();
   scatterRange<Pol, CurT, NTH, IPT, 0, true, BOUNDED, MAXD>(in, it.begin, it.begin + it.len, F, smem, pol, out,
-                                                            gcur + (uint64_t)it.stream * F);
+                                                            gcur + (uint64_t)it.stream * F, im);
 }
 
 // Persistent local claim scatter.  Work items are short (1B x 1B: a network
@@ -1780,7 +1852,8 @@ __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void localScatterClaim
 template <class Pol, typename CurT, int NTH, int IPT, bool BOUNDED, int MAXD>
 __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void localScatterPersistKernel(
     const typename Pol::InT *__restrict__ in, const LocalItem *__restrict__ items, uint32_t nItems, uint32_t F,
-    Pol pol, CurT *__restrict__ gcur, typename Pol::OutT *out, const CurT *__restrict__ gend, uint32_t perXcd) {
+    Pol pol, CurT *__restrict__ gcur, typename Pol::OutT *out, const CurT *__restrict__ gend, uint32_t perXcd,
+    RoundMap im) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr uint32_t TILE = NTH * IPT;
   const uint32_t q = (nItems + NGROUPS - 1) / NGROUPS;
@@ -1798,7 +1871,7 @@ __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void localScatterPersi
   __syncthreads();
   typename Pol::LoadT v[IPT];
   ScatterProf pf;
-  prefetchTile<Pol, NTH, IPT>(in, it.begin, it.begin + it.len - 1, v);
+  prefetchTile<Pol, NTH, IPT>(in, it.begin, it.begin + it.len - 1, v, im);
   for (;;) {
     const uint32_t nxt = cur + perXcd;
     const bool more = nxt < last;
@@ -1811,10 +1884,10 @@ __global__ __launch_bounds__(NTH, ScatterOcc<NTH>::value) void localScatterPersi
       const uint64_t nl = lastTile ? nit.begin + nit.len - 1 : end - 1;
       if (base + TILE <= end)
         scatterTile<Pol, CurT, NTH, IPT, 0, true, true, BOUNDED, MAXD>(in, base, end, TILE, F, l, pol, out, v, gc,
-                                                                       pf, nb, nl);
+                                                                       pf, nb, nl, im);
       else
         scatterTile<Pol, CurT, NTH, IPT, 0, false, true, BOUNDED, MAXD>(in, base, end, (uint32_t)(end - base), F, l,
-                                                                        pol, out, v, gc, pf, nb, nl);
+                                                                        pol, out, v, gc, pf, nb, nl, im);
     }
     if (!more) break;
     if constexpr (BOUNDED) {
@@ -1856,7 +1929,7 @@ static uint32_t persistPerXcd(K kernel, uint32_t nth, size_t lds, uint32_t nItem
 
 template <class P, typename C, int NTH, int IPT>
 static void launchLocalClaimPersist(const void *in, const LocalItem *items, uint32_t nItems, uint32_t F, const P &pol,
-                                    void *gcur, void *out, const void *gend, hipStream_t s) {
+                                    void *gcur, void *out, const void *gend, hipStream_t s, RoundMap rm) {
   const size_t lds = ScatterLayout<P, C, NTH * IPT>::bytes(F);
   HJ_CHECK(lds <= 160 * 1024, "local scatter LDS %zu too large", lds);
   withMaxd<NTH>(F, [&](auto maxd) {
@@ -1865,7 +1938,7 @@ static void launchLocalClaimPersist(const void *in, const LocalItem *items, uint
       const uint32_t per = persistPerXcd(kernel, NTH, lds, nItems);
       hipLaunchKernelGGL(kernel, dim3(per * NGROUPS), dim3(NTH), lds, s, reinterpret_cast<const typename P::InT *>(in),
                          items, nItems, F, pol, reinterpret_cast<C *>(gcur), reinterpret_cast<typename P::OutT *>(out),
-                         ge, per);
+                         ge, per, rm);
     };
     if (gend)
       go(localScatterPersistKernel<P, C, NTH, IPT, true, M>, reinterpret_cast<const C *>(gend));
@@ -1877,7 +1950,7 @@ static void launchLocalClaimPersist(const void *in, const LocalItem *items, uint
 // One local claim-scatter launch (MAXD from F, bounded when gend is given).
 template <class P, typename C, int NTH, int IPT>
 static void launchLocalClaim(const void *in, const LocalItem *items, uint32_t nItems, uint32_t F, const P &pol,
-                             void *gcur, void *out, const void *gend, hipStream_t s) {
+                             void *gcur, void *out, const void *gend, hipStream_t s, RoundMap rm) {
   const size_t lds = ScatterLayout<P, C, NTH * IPT>::bytes(F);
   HJ_CHECK(lds <= 160 * 1024, "local scatter LDS %zu too large", lds);
   const uint32_t grid = ((nItems + NGROUPS - 1) / NGROUPS) * NGROUPS;
@@ -1887,11 +1960,11 @@ static void launchLocalClaim(const void *in, const LocalItem *items, uint32_t nI
       hipLaunchKernelGGL((localScatterClaimKernel<P, C, NTH, IPT, true, M>), dim3(grid), dim3(NTH), lds, s,
                          reinterpret_cast<const typename P::InT *>(in), items, nItems, F, pol,
                          reinterpret_cast<C *>(gcur), reinterpret_cast<typename P::OutT *>(out),
-                         reinterpret_cast<const C *>(gend));
+                         reinterpret_cast<const C *>(gend), rm);
     else
       hipLaunchKernelGGL((localScatterClaimKernel<P, C, NTH, IPT, false, M>), dim3(grid), dim3(NTH), lds, s,
                          reinterpret_cast<const typename P::InT *>(in), items, nItems, F, pol,
-                         reinterpret_cast<C *>(gcur), reinterpret_cast<typename P::OutT *>(out), nullptr);
+                         reinterpret_cast<C *>(gcur), reinterpret_cast<typename P::OutT *>(out), nullptr, rm);
   });
 }
 
@@ -1908,13 +1981,14 @@ static void setSplit(LocalSplitPol &p, const SplitLayout &sl) {
 // output, 64-bit cursors, bounded slots) for the geometry sweep.
 template <int NTH, int IPT>
 static void launchLocalSplitGeom(const void *in, const LocalItem *items, uint32_t nItems, uint32_t F,
-                                 const LocalSplitPol &pol, void *gcur, void *out, const void *gend, hipStream_t s) {
-  launchLocalClaim<LocalSplitPol, unsigned long long, NTH, IPT>(in, items, nItems, F, pol, gcur, out, gend, s);
+                                 const LocalSplitPol &pol, void *gcur, void *out, const void *gend, hipStream_t s,
+                                 RoundMap rm) {
+  launchLocalClaim<LocalSplitPol, unsigned long long, NTH, IPT>(in, items, nItems, F, pol, gcur, out, gend, s, rm);
 }
 
 void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift, uint32_t bits,
                   void *gcur, bool narrow, void *out, hipStream_t s, const void *gend, SplitLayout split,
-                  uint32_t geometry, bool frag) {
+                  uint32_t geometry, bool frag, RoundMap rm) {
   HJ_CHECK(!(wide && split.on), "localScatter: the split layout needs compressed input");
   HJ_CHECK(!split.on || frag || split.hi, "localScatter: split layout without a fragment column");
   HJ_CHECK(!(frag && wide), "localScatter: fragments are not wide tuples");
@@ -1936,7 +2010,7 @@ void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nI
     auto go = [&](auto cur, auto ipt) {
       using C = decltype(cur);
       launchLocalClaimPersist<LocalSplitPol, C, CL_NTH, decltype(ipt)::value>(in, items, nItems, F, pol, gcur, out,
-                                                                               gend, s);
+                                                                               gend, s, rm);
     };
     if (geometry == 6) {
       if (narrow) go(uint32_t(), std::integral_constant<int, 12>());
@@ -1954,10 +2028,10 @@ void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nI
     pol.shift = shift;
     setSplit(pol, split);
     switch (geometry) {
-      case 1: launchLocalSplitGeom<512, 8>(in, items, nItems, F, pol, gcur, out, gend, s); break;
-      case 2: launchLocalSplitGeom<512, 16>(in, items, nItems, F, pol, gcur, out, gend, s); break;
-      case 3: launchLocalSplitGeom<256, 16>(in, items, nItems, F, pol, gcur, out, gend, s); break;
-      default: launchLocalSplitGeom<1024, 16>(in, items, nItems, F, pol, gcur, out, gend, s); break;
+      case 1: launchLocalSplitGeom<512, 8>(in, items, nItems, F, pol, gcur, out, gend, s, rm); break;
+      case 2: launchLocalSplitGeom<512, 16>(in, items, nItems, F, pol, gcur, out, gend, s, rm); break;
+      case 3: launchLocalSplitGeom<256, 16>(in, items, nItems, F, pol, gcur, out, gend, s, rm); break;
+      default: launchLocalSplitGeom<1024, 16>(in, items, nItems, F, pol, gcur, out, gend, s, rm); break;
     }
     HIP_CHECK_LAUNCH();
     return;
@@ -1969,9 +2043,9 @@ void localScatter(const void *in, bool wide, const LocalItem *items, uint32_t nI
     pol.shift = shift;                                                                                      \
     setSplit(pol, split);                                                                                   \
     if (persist)                                                                                            \
-      launchLocalClaimPersist<P, C, CL_NTH, CL_IPT>(in, items, nItems, F, pol, gcur, out, gend, s);         \
+      launchLocalClaimPersist<P, C, CL_NTH, CL_IPT>(in, items, nItems, F, pol, gcur, out, gend, s, rm);     \
     else                                                                                                    \
-      launchLocalClaim<P, C, CL_NTH, CL_IPT>(in, items, nItems, F, pol, gcur, out, gend, s);                \
+      launchLocalClaim<P, C, CL_NTH, CL_IPT>(in, items, nItems, F, pol, gcur, out, gend, s, rm);            \
   } while (0)
   if (frag && narrow) HJ_LOCAL(LocalFragPol, uint32_t);
   else if (frag) HJ_LOCAL(LocalFragPol, unsigned long long);

@@ -256,6 +256,7 @@ JoinResult HashJoin::runPasses() {
     total.localItems += r.localItems;
     total.buildProbeItems += r.buildProbeItems;
     total.networkFallbacks += r.networkFallbacks;
+    total.roundWindows += r.roundWindows;
     total.localFallbacks += r.localFallbacks;
     total.reruns += r.reruns;
     total.devNetworkMs += r.devNetworkMs;
@@ -494,13 +495,18 @@ std::vector<uint64_t> HashJoin::workspaceParts() const {
   const uint64_t n[2] = {innerRelation->getLocalSize(), outerRelation->getLocalSize()};
   const uint64_t g[2] = {innerRelation->getGlobalSize(), outerRelation->getGlobalSize()};
   std::vector<uint64_t> parts(1, 64ull << 20);
-  auto sampledCap = [&](uint64_t m) {
+  // Round-interleaved network windows (SampledNetworkPartitioning::roundLp) need a little more room.
+  const uint32_t roundLp =
+      plan.twoLevel && !plan.wide ? kernels::roundLpFor(plan.roundLp, plan.fragments ? 4 : 8) : 0;
+  auto sampledCap = [&](uint64_t m, uint32_t lp = 0) {
     const kernels::PartitionGeometry geom = kernels::partitionGeometry(m, config.maxPartitionBlocks);
     const uint32_t stride = kernels::sampleStrideFor(geom, m, F, std::max<uint32_t>(1, config.sampleStride));
-    return kernels::sampledLayoutCapacityBound(kernels::sampleScale(geom, m, stride, false), F);
+    return kernels::sampledWindowCapacity(kernels::sampleScale(geom, m, stride, false), F, lp);
   };
   if (plan.bitmapJoin) {
-    for (int r = 0; r < 2; ++r) parts.push_back((sampledCap(n[r]) + 64) * 4);  // u32 fragments in claim slices
+    // u32 fragments in claim slices (round-interleaved unless a partition-group pass)
+    const uint32_t lp = plan.groupBudget ? 0 : kernels::roundLpFor(plan.roundLp, 4);
+    for (int r = 0; r < 2; ++r) parts.push_back((sampledCap(n[r], lp) + 64) * 4);
     if (plan.bitmapReplicated) parts.push_back(2ull * F * kernels::bitmapWords(plan.bitmapBits) * 4);
     return parts;
   }
@@ -511,7 +517,8 @@ std::vector<uint64_t> HashJoin::workspaceParts() const {
   for (int r = 0; r < 2; ++r) {
     // N > 1: the fair share plus a quarter (LPT balances partitions; skew
     // beyond that falls back to allocation inside the first join).
-    const uint64_t recv = N == 1 ? (plan.sampledNetwork ? sampledCap(n[r]) : n[r]) : g[r] / N + g[r] / (4 * N) + (1 << 20);
+    const uint64_t recv =
+        N == 1 ? (plan.sampledNetwork ? sampledCap(n[r], roundLp) : n[r]) : g[r] / N + g[r] / (4 * N) + (1 << 20);
     recvTotal[r] = recv;
     if (N > 1 && !plan.oneSided) parts.push_back((plan.sampledNetwork ? n[r] + n[r] / 8 : n[r]) * wordB);  // send buffer
     if (plan.wireBits[r]) parts.push_back((n[r] + recv) * ((plan.wireBits[r] + 7) / 8) + (64ull << 10));  // wire buffers
@@ -822,6 +829,7 @@ JoinResult HashJoin::runImpl() {
   result.innerReceived = run.inner->computeLocalWindowSize();
   result.outerReceived = run.outer->computeLocalWindowSize();
   result.sampledNetwork = run.sampled;
+  result.roundWindows = (run.inner->roundMap().on() ? 1u : 0u) + (run.outer->roundMap().on() ? 1u : 0u);
   result.directScatter = run.inner->directScatter() || run.outer->directScatter();
   Measurements::storeLocalPartitioningDetails(result.innerReceived + result.outerReceived, result.localItems);
   Measurements::storeBuildProbeDetails(result.innerReceived, result.outerReceived, result.buildProbeItems);

@@ -43,16 +43,17 @@ BitmapJoin::Outcome BitmapJoin::run(bool exact) { return ctx->onDevice() ? runDe
 const BitmapJoin::SidePlan &BitmapJoin::sidePlan(uint64_t n, bool exact, uint32_t stride) const {
   struct Key {
     uint64_t n;
-    uint32_t maxBlocks, bits, stride, ipt, nth;
+    uint32_t maxBlocks, bits, stride, ipt, nth, lp;
     bool exact;
     bool operator<(const Key &o) const {
-      return std::tie(n, maxBlocks, bits, stride, ipt, nth, exact) <
-             std::tie(o.n, o.maxBlocks, o.bits, o.stride, o.ipt, o.nth, o.exact);
+      return std::tie(n, maxBlocks, bits, stride, ipt, nth, lp, exact) <
+             std::tie(o.n, o.maxBlocks, o.bits, o.stride, o.ipt, o.nth, o.lp, o.exact);
     }
   };
   thread_local std::map<Key, SidePlan> cache;
   const uint32_t F = 1u << plan.networkBits;
-  const Key k{n, maxBlocks, plan.networkBits, stride, plan.variants.netIpt, plan.variants.netThreads, exact};
+  const Key k{n, maxBlocks, plan.networkBits, stride, plan.variants.netIpt, plan.variants.netThreads, plan.roundLp,
+              exact};
   auto it = cache.find(k);
   if (it != cache.end()) return it->second;
   if (cache.size() > 64) cache.clear();
@@ -62,7 +63,7 @@ const BitmapJoin::SidePlan &BitmapJoin::sidePlan(uint64_t n, bool exact, uint32_
   sp.geom.nth = plan.variants.netThreads;
   sp.stride = exact ? 1 : kernels::sampleStrideFor(sp.geom, n, F, stride);
   sp.sc = kernels::sampleScale(sp.geom, n, sp.stride, exact);
-  sp.cap = kernels::sampledLayoutCapacityBound(sp.sc, F);
+  sp.cap = kernels::sampledWindowCapacity(sp.sc, F, kernels::roundLpFor(plan.roundLp, 4));
   return cache.emplace(k, sp).first->second;
 }
 
@@ -120,11 +121,26 @@ void BitmapJoin::layoutSides(Side *sides, uint32_t count, bool exact, bool narro
     }
   }
   const size_t cb = narrow ? 4 : 8;
+  // Round-interleaved fragment windows (kernels::RoundMap): the slots follow
+  // from the layout kernel's map, which every reader takes from roundMeta.
+  const uint32_t lp = kernels::roundLpFor(plan.roundLp, 4);
+  uint32_t lns = 0;
+  while ((1u << lns) < G * F) ++lns;
   for (uint32_t i = 0; i < count; ++i) {
     lay[i].gstart = ws.get((size_t)G * F * cb);
     lay[i].gcur = ws.get((size_t)G * F * cb);
     lay[i].gend = ws.get((size_t)G * F * cb);
     lay[i].capacityUsed = ws.getArray<unsigned long long>(1);
+    if (lp) {
+      // Logical positions reach (G * F << lv) + n (claims past a slice end).
+      const uint64_t n = sides[i].relation->getLocalSize(), limit = narrow ? (1ull << 32) : (1ull << 62);
+      uint32_t maxLv = 0;
+      while (maxLv < 40 && ((uint64_t)G * F << (maxLv + 1)) + n < limit) ++maxLv;
+      lay[i].roundMeta = ws.getArray<uint32_t>(4);
+      lay[i].roundLp = lp;
+      lay[i].roundMaxLv = maxLv;
+      lay[i].roundCapacity = sides[i].cap;
+    }
     Side &s = sides[i];
     s.slices = BitmapSlices();
     s.slices.kind = BitmapSlices::Claim;
@@ -135,6 +151,7 @@ void BitmapJoin::layoutSides(Side *sides, uint32_t count, bool exact, bool narro
     s.slices.count = s.relation->getLocalSize();
     s.slices.threads = plan.variants.bmThreads;
     s.slices.flat = plan.variants.bmFlat;
+    s.slices.roundMeta = lay[i].roundMeta;
     s.frags = ws.getArray<uint32_t>(std::max<uint64_t>(s.cap, 16));
   }
   kernels::netSampledLayout(lay, count, F, narrow, st);
@@ -145,7 +162,7 @@ void BitmapJoin::scatterSide(Side &s) {
   const kernels::KeyMix mix{plan.keyMix ? 1u : 0u, plan.keyBits};
   kernels::netScatterFrag(s.relation->getData(), s.relation->getLocalSize(), plan.networkBits, s.geom, 0,
                           s.geom.blocks, const_cast<void *>(s.slices.cur), s.frags, ctx->stream(), plan.keyBits, mix,
-                          s.slices.end, s.slices.narrow ? 1 : 0);
+                          s.slices.end, s.slices.narrow ? 1 : 0, s.slices.roundMeta);
 }
 
 // Partition ranges of the replicated plan's all-reduce: one per 32 MiB of

@@ -62,6 +62,8 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
   const uint32_t tb = w->tupleBytes();
   elements += xp.recvTotal;
 
+  JOIN_ASSERT(!w->roundMap().on() || (ctx->onDevice() && plan.twoLevel), "LocalPartitioning",
+              "round-interleaved windows are read by the device two-level pass only");
   if (!plan.twoLevel && xp.windowIsPartitionMajor()) {
     uint64_t *pb = ctx->workspace().getArray<uint64_t>(owned + 1);
     ctx->copy(pb, xp.lpBase.data(), (owned + 1) * 8, ctx->onDevice(), false);
@@ -153,7 +155,8 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
     // Back-to-back spans on one stream share their boundary events.
     hipEvent_t p0 = tl.mark(ctx->stream());
     tl.beginAt("LPHISTCOMP", p0);
-    kernels::localHistogram(w->getData(), wide, dItems, nItems, shift, bits, itemHist, ctx->stream(), S, frag);
+    kernels::localHistogram(w->getData(), wide, dItems, nItems, shift, bits, itemHist, ctx->stream(), S, frag,
+                            w->roundMap());
     hipEvent_t p1 = tl.mark(ctx->stream());
     tl.endAt("LPHISTCOMP", p1);
     tl.beginAt("LPOFFSET", p1);
@@ -163,7 +166,7 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
     tl.endAt("LPOFFSET", p2);
     tl.beginAt("LPPART", p2);
     kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, gcur, false, sout, ctx->stream(), gend,
-                          split, plan.localGeometry, frag);
+                          split, plan.localGeometry, frag, w->roundMap());
     tl.endAt("LPPART", tl.mark(ctx->stream()));
     kernels::claimOverflow(gcur, gend, P, overflowFlag[which], ctx->stream());
     // Read back with the join's final synchronisation (one flag per side).
@@ -194,7 +197,8 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
     performance::Measurements::add("LPHISTELEM", (double)xp.recvTotal, "tuples");
     hipEvent_t p0 = tl.mark(ctx->stream());
     tl.beginAt("LPHISTCOMP", p0);
-    kernels::localHistogram(w->getData(), wide, dItems, nItems, shift, bits, itemHist, ctx->stream(), 1, frag);
+    kernels::localHistogram(w->getData(), wide, dItems, nItems, shift, bits, itemHist, ctx->stream(), 1, frag,
+                            w->roundMap());
     hipEvent_t p1 = tl.mark(ctx->stream());
     tl.endAt("LPHISTCOMP", p1);
     tl.beginAt("LPOFFSET", p1);
@@ -203,7 +207,7 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
     tl.endAt("LPOFFSET", p2);
     tl.beginAt("LPPART", p2);
     kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, gcur, narrow, out, ctx->stream(), nullptr,
-                          split, 0, frag);
+                          split, 0, frag, w->roundMap());
     tl.endAt("LPPART", tl.mark(ctx->stream()));
   } else {
     uint64_t *itemCursors = ctx->workspace().getArray<uint64_t>(std::max<uint64_t>(1, (uint64_t)nItems * F));

@@ -33,14 +33,15 @@ SampledNetworkPartitioning::~SampledNetworkPartitioning() = default;  // events 
 const SampledNetworkPartitioning::SidePlan &SampledNetworkPartitioning::sidePlan(uint64_t n) const {
   struct Key {
     uint64_t n;
-    uint32_t maxBlocks, bits, stride, ipt, nth;
+    uint32_t maxBlocks, bits, stride, ipt, nth, lp;
     bool operator<(const Key &o) const {
-      return std::tie(n, maxBlocks, bits, stride, ipt, nth) < std::tie(o.n, o.maxBlocks, o.bits, o.stride, o.ipt, o.nth);
+      return std::tie(n, maxBlocks, bits, stride, ipt, nth, lp) <
+             std::tie(o.n, o.maxBlocks, o.bits, o.stride, o.ipt, o.nth, o.lp);
     }
   };
   thread_local std::map<Key, SidePlan> cache;
   const uint32_t F = 1u << plan.networkBits;
-  const Key k{n, maxBlocks, plan.networkBits, sampleStride, plan.variants.netIpt, plan.variants.netThreads};
+  const Key k{n, maxBlocks, plan.networkBits, sampleStride, plan.variants.netIpt, plan.variants.netThreads, roundLp()};
   auto it = cache.find(k);
   if (it != cache.end()) return it->second;
   if (cache.size() > 64) cache.clear();
@@ -50,7 +51,7 @@ const SampledNetworkPartitioning::SidePlan &SampledNetworkPartitioning::sidePlan
   sp.geom.nth = plan.variants.netThreads;
   sp.stride = kernels::sampleStrideFor(sp.geom, n, F, sampleStride);
   sp.sc = kernels::sampleScale(sp.geom, n, sp.stride, sp.stride == 1);
-  sp.bound = kernels::sampledLayoutCapacityBound(sp.sc, F);
+  sp.bound = kernels::sampledWindowCapacity(sp.sc, F, roundLp());
   return cache.emplace(k, sp).first->second;
 }
 
@@ -94,6 +95,12 @@ void SampledNetworkPartitioning::sample() {
   ctx->timeline().end("HLOCAL", st);
 }
 
+// Round-interleaved slices (kernels::RoundMap) for windows the local pass
+// reads (two-level plans; the wide scatter keeps linear slices).
+uint32_t SampledNetworkPartitioning::roundLp() const {
+  return plan.twoLevel && !plan.wide ? kernels::roundLpFor(plan.roundLp, plan.fragments ? 4 : 8) : 0;
+}
+
 void SampledNetworkPartitioning::layout() {
   layoutSide(0);
   layoutSide(1);
@@ -127,12 +134,29 @@ void SampledNetworkPartitioning::layoutSide(int k) {
   s.window.reset(new data::Window(x, s.capacityTotal, ctx, plan.wide, plan.fragments ? 4u : 0u));
   // Slice starts, claim cursors and slice ends ([G][F] each, adjacent: one
   // read-back after the scatter), laid out on the device from the totals.
+  // The round map's 4 words follow (read back with them).
   const size_t cb = s.narrow ? 4 : 8, per = (size_t)G * F * cb;
-  s.gstart = ctx->workspace().get(3 * per);
+  s.gstart = ctx->workspace().get(3 * per + 16);
   s.gcur = static_cast<uint8_t *>(s.gstart) + per;
   s.gend = static_cast<uint8_t *>(s.gstart) + 2 * per;
-  kernels::netSampledLayout(s.groupTotalsDev, F, s.sc, s.gstart, s.gcur, s.gend, s.narrow,
-                            ctx->workspace().getArray<unsigned long long>(1), ctx->stream());
+  s.roundMeta = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(s.gstart) + 3 * per);
+  kernels::LayoutInput in{s.groupTotalsDev, s.sc, s.gstart, s.gcur, s.gend,
+                          ctx->workspace().getArray<unsigned long long>(1)};
+  if (const uint32_t lp = roundLp()) {
+    // Logical positions reach (G * F << lv) + n (claims past a slice end).
+    uint32_t lns = 0;
+    while ((1u << lns) < G * F) ++lns;
+    const uint64_t limit = s.narrow ? (1ull << 32) : (1ull << 62);
+    uint32_t maxLv = 0;
+    while (maxLv < 40 && ((uint64_t)G * F << (maxLv + 1)) + n < limit) ++maxLv;
+    in.roundMeta = s.roundMeta;
+    in.roundLp = lp;
+    in.roundMaxLv = maxLv;
+    in.roundCapacity = s.capacityTotal;
+  } else {
+    ctx->zero(s.roundMeta, 16);
+  }
+  kernels::netSampledLayout(&in, 1, F, s.narrow, ctx->stream());
 }
 
 bool SampledNetworkPartitioning::scatter() {
@@ -154,15 +178,17 @@ void SampledNetworkPartitioning::scatterSide(int k) {
   ctx->timeline().begin(key, ctx->stream());
   if (plan.fragments)  // count-only: u32 key fragments (key >> networkBits), no rid
     kernels::netScatterFrag(s.relation->getData(), n, plan.networkBits, s.geom, 0, s.geom.blocks, s.gcur,
-                            static_cast<uint32_t *>(s.window->getData()), ctx->stream(), plan.keyBits, mix, s.gend, nm);
+                            static_cast<uint32_t *>(s.window->getData()), ctx->stream(), plan.keyBits, mix, s.gend, nm,
+                            s.roundMeta);
   else if (plan.wide)
     kernels::netScatterWide(s.relation->getData(), n, plan.networkBits, s.geom, 0, s.geom.blocks, s.gcur,
                             static_cast<data::Tuple *>(s.window->getData()), ctx->stream(), mix, s.gend, nm);
   else
     kernels::netScatter(s.relation->getData(), n, plan.networkBits, plan.keyShift, s.geom, 0, s.geom.blocks, s.gcur,
-                        static_cast<uint64_t *>(s.window->getData()), ctx->stream(), plan.keyBits, mix, s.gend, nm, !plan.keyOnly);
+                        static_cast<uint64_t *>(s.window->getData()), ctx->stream(), plan.keyBits, mix, s.gend, nm,
+                        !plan.keyOnly, s.roundMeta);
   ctx->timeline().end(key, ctx->stream());
-  const size_t bytes = 3 * (size_t)G * F * (s.narrow ? 4 : 8);  // starts, final cursors, ends
+  const size_t bytes = 3 * (size_t)G * F * (s.narrow ? 4 : 8) + 16;  // starts, final cursors, ends, round map
   s.cursorsBack = ctx->staging().get(bytes);
   ctx->readBack(s.cursorsBack, s.gstart, bytes);
   if (!s.cursorsReady) s.cursorsReady = ctx->acquireEvent();
@@ -180,16 +206,30 @@ bool SampledNetworkPartitioning::finishSide(int k) {
   const uint64_t *c64 = static_cast<const uint64_t *>(s.cursorsBack);
   auto at = [&](size_t i) -> uint64_t { return s.narrow ? c32[i] : c64[i]; };
   bool ok = true;
-  uint64_t sum = 0, maxEnd = 0;
+  uint64_t sum = 0, maxEnd = 0, maxCap = 0;
   for (size_t i = 0; i < m; ++i) {
     s.start[i] = at(i);
     s.fill[i] = at(m + i) - s.start[i];  // final claim cursor - slice start
     sum += s.fill[i];
     maxEnd = std::max<uint64_t>(maxEnd, at(2 * m + i));
+    maxCap = std::max<uint64_t>(maxCap, at(2 * m + i) - s.start[i]);
     if (s.fill[i] > at(2 * m + i) - s.start[i]) ok = false;
+  }
+  const uint32_t *meta = reinterpret_cast<const uint32_t *>(static_cast<const uint8_t *>(s.cursorsBack) +
+                                                            3 * m * (s.narrow ? 4 : 8));
+  kernels::RoundMap rm;
+  rm.lp = meta[0];
+  rm.lv = meta[1];
+  rm.lns = meta[2];
+  if (rm.on()) {
+    HJ_CHECK(rm.lv >= rm.lp && maxCap <= (1ull << rm.lv) && (1ull << rm.lns) == m,
+             "sampled network layout: round map lp=%u lv=%u lns=%u for slices of %lu over %zu slices", rm.lp, rm.lv,
+             rm.lns, (unsigned long)maxCap, m);
+    maxEnd = kernels::roundSlots(maxCap, rm.lp, rm.lns);
   }
   HJ_CHECK(maxEnd <= s.capacityTotal, "sampled network layout: slices end at %lu, window holds %lu",
            (unsigned long)maxEnd, (unsigned long)s.capacityTotal);
+  s.window->setRoundMap(rm);
   HJ_CHECK(sum == s.relation->getLocalSize(), "sampled network pass claimed %lu of %lu tuples", (unsigned long)sum,
            (unsigned long)s.relation->getLocalSize());
   if (!ok) return false;

@@ -55,6 +55,7 @@ class SampledNetworkPartitioning {
   data::Window *innerWindow() { return sides[0].window.get(); }
   data::Window *outerWindow() { return sides[1].window.get(); }
   uint64_t capacity(int side) const { return sides[side].capacityTotal; }
+  uint32_t roundLp() const;
 
  private:
   struct SidePlan {
@@ -77,6 +78,7 @@ class SampledNetworkPartitioning {
     std::vector<uint64_t> start;  // [groups][F] slice start (tuples), read back with the cursors
     std::vector<uint64_t> fill;   // [groups][F] claimed after the scatter
     void *gstart = nullptr, *gcur = nullptr, *gend = nullptr;  // device [groups][F] each, adjacent
+    uint32_t *roundMeta = nullptr;                              // device {lp, lv, lns, 0} after gend
     bool narrow = true;
     uint64_t capacityTotal = 0;  // window slots: the layout's capacity bound
   };

@@ -7,7 +7,7 @@ import os
 from .._native import require_native
 
 _FIELDS = ["network_bits", "local_bits", "two_level", "key_shift", "materialize", "output_capacity", "build_target",
-           "r_chunk", "s_chunk", "chunks", "checks", "max_partition_blocks", "sample_stride", "local_sample_stride", "local_item_tiles", "local_geometry",
+           "r_chunk", "s_chunk", "chunks", "checks", "max_partition_blocks", "sample_stride", "local_sample_stride", "round_lp", "local_item_tiles", "local_geometry",
            "split_local", "direct_count", "split_histogram", "pipeline_outer", "bitmap_join", "skew_split",
            "reserve_workspace", "passes", "workspace_budget", "link_gbps_per_peer", "codec_extra_ps_per_tuple",
            # kernel-shape variants (sweeps / A-B tests; JoinConfig.variants in C++)

@@ -15,6 +15,7 @@
 #   py=SCRIPT,ARGS      python SCRIPT ARGS
 #   epy=ENV/SCRIPT,ARGS python SCRIPT ARGS with ENV (comma-separated K=V)
 #   stats=ARGS          rocprofv3 --kernel-trace --stats of bench.py ARGS
+#   estats=ENV/ARGS     the same with ENV exported (comma-separated K=V)
 #   pstats=SCRIPT,ARGS  rocprofv3 --kernel-trace --stats of python SCRIPT ARGS
 #   ppmc=CTRS/SCRIPT,ARGS  rocprofv3 --pmc CTRS of python SCRIPT ARGS
 #   pmc=CTRS/ARGS       rocprofv3 --pmc CTRS (comma-separated) of bench.py ARGS
@@ -86,6 +87,9 @@ for step in "$@"; do
          timeout -k 10 900 env ${envs//,/ } python -u ${pargs//,/ } > "$log" 2>&1 ;;
     stats) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/stats$n" -o run --output-format csv \
               -- python "$R/bench.py" $args) > "$log" 2>&1 ;;
+    estats) envs=${arg%%/*}; bargs=${arg#*/}
+            (cd /tmp && export ${envs//,/ } && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/stats$n" \
+               -o run --output-format csv -- python "$R/bench.py" ${bargs//,/ }) > "$log" 2>&1 ;;
     pstats) (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$OUT/stats$n" -o run --output-format csv \
               -- python "$R/"$args) > "$log" 2>&1 ;;
     ppmc) ctrs=${arg%%/*}; sargs=${arg#*/}; (cd /tmp && timeout -s KILL 600 rocprofv3 --kernel-trace --pmc ${ctrs//,/ } \
