@@ -202,8 +202,8 @@ void Window::exchangeSegmented(const uint64_t *send, uint32_t chunk, SegmentedCh
     // bytes it saves, HashJoin::planWireCodec): the filled runs are gathered
     // out of the claim slices and the all-to-allv lands them straight in the
     // window -- the receive displacements ARE window offsets, no unpack pass.
-    kernels::segCopy(send, wsend, dS, (uint32_t)sc.send.size(), sG, xs);
-    kernels::segCopy(send, dst, dC, (uint32_t)sc.self.size(), cG, xs);
+    kernels::segCopy(send, wsend, dS, (uint32_t)sc.send.size(), sG, xs, sc.sendMap);
+    kernels::segCopy(send, dst, dC, (uint32_t)sc.self.size(), cG, xs, sc.sendMap);
     ctx->timeline().begin("MWINPUT", xs);
     ctx->comm()->allToAllV(wsend, sc.sendWords.data(), sc.sendDispls.data(), dst, sc.recvWords.data(),
                            sc.recvDispls.data(), Location::Device, xs);
@@ -215,8 +215,8 @@ void Window::exchangeSegmented(const uint64_t *send, uint32_t chunk, SegmentedCh
     exchanged[chunk] = true;
     return;
   }
-  kernels::wirePack(send, wsend, dS, (uint32_t)sc.send.size(), sG, codec, xs);
-  kernels::segCopy(send, dst, dC, (uint32_t)sc.self.size(), cG, xs);
+  kernels::wirePack(send, wsend, dS, (uint32_t)sc.send.size(), sG, codec, xs, sc.sendMap);
+  kernels::segCopy(send, dst, dC, (uint32_t)sc.self.size(), cG, xs, sc.sendMap);
   ctx->timeline().begin("MWINPUT", xs);
   ctx->comm()->allToAllV(wsend, sc.sendWords.data(), sc.sendDispls.data(), wrecv, sc.recvWords.data(),
                          sc.recvDispls.data(), Location::Device, xs);

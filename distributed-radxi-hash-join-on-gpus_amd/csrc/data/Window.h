@@ -85,6 +85,7 @@ class Window {
   struct SegmentedChunk {
     std::vector<kernels::WireSeg> send, recv, self;
     std::vector<uint64_t> sendWords, sendDispls, recvWords, recvDispls;
+    kernels::RoundMap sendMap;  // slot map of the send buffer (send / self `raw` are logical positions)
   };
   void exchangeSegmented(const uint64_t *sendBuffer, uint32_t chunk, SegmentedChunk &&sc, hipEvent_t scattered);
   // Bit-pack tuples on the wire (kernels.h, WireCodec); ridBase[rank * C + c]
@@ -106,6 +107,10 @@ class Window {
   // the plan's segment offsets are logical positions; identity by default.
   void setRoundMap(const kernels::RoundMap &m) { roundMap_ = m; }
   const kernels::RoundMap &roundMap() const { return roundMap_; }
+  // N > 1: the send buffer feeding this window had round-interleaved slices
+  // (informational: the window itself is linear).
+  void setSendRounded(bool on) { sendRounded_ = on; }
+  bool sendRounded() const { return sendRounded_; }
   uint32_t tupleBytes() const { return elemBytes ? elemBytes : (wide ? 16 : 8); }
   bool holdsFragments() const { return elemBytes == 4; }
   bool isWide() const { return wide; }
@@ -139,6 +144,7 @@ class Window {
   core::ExecContext *ctx;
   bool wide;
   kernels::RoundMap roundMap_;
+  bool sendRounded_ = false;
   uint32_t elemBytes = 0;  // 0: the tuple format's size
   bool open = false;
   std::vector<hipEvent_t> ready, done;

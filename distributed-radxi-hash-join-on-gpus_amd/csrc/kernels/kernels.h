@@ -679,14 +679,16 @@ struct WireSeg {
   uint64_t group0;  // first global group index of this segment (prefix of ceil(n/64))
 };
 // segs is a device array (nSegs entries, ascending group0); totalGroups = sum ceil(n/64).
+// rm: slot map of `raw` (RoundMap of a round-interleaved send buffer; seg.raw
+// is then a logical position).
 void wirePack(const uint64_t *raw, uint64_t *wire, const WireSeg *segs, uint32_t nSegs, uint64_t totalGroups,
-              const WireCodec &c, hipStream_t s);
+              const WireCodec &c, hipStream_t s, RoundMap rm = RoundMap());
 void wireUnpack(const uint64_t *wire, uint64_t *raw, const WireSeg *segs, uint32_t nSegs, uint64_t totalGroups,
                 const WireCodec &c, hipStream_t s);
 // Raw segmented gather: dst[seg.wire + t] = src[seg.raw + t] for t < seg.n
 // (same segment list format; offsets in 8-byte words, nothing past seg.n written).
 void segCopy(const uint64_t *src, uint64_t *dst, const WireSeg *segs, uint32_t nSegs, uint64_t totalGroups,
-             hipStream_t s);
+             hipStream_t s, RoundMap rm = RoundMap());
 
 // ------------------------------------------------------------------- scans
 size_t scanWorkspaceBytes(uint64_t n);

@@ -70,7 +70,8 @@ template <bool kLds>
 __global__ __launch_bounds__(WIRE_THREADS) void wirePackKernel(const uint64_t *__restrict__ raw,
                                                                uint64_t *__restrict__ wire,
                                                                const WireSeg *__restrict__ gsegs, uint32_t nSegs,
-                                                               uint64_t totalGroups, uint64_t per, WireCodec c) {
+                                                               uint64_t totalGroups, uint64_t per, WireCodec c,
+                                                               RoundMap rm) {
   __shared__ WireSeg lds[kLds ? WIRE_MAX_SEGS_LDS : 1];
   const WireSeg *segs = stageSegs<kLds>(gsegs, nSegs, lds);
   const uint32_t lane = threadIdx.x & (WAVE - 1);
@@ -83,7 +84,7 @@ __global__ __launch_bounds__(WIRE_THREADS) void wirePackKernel(const uint64_t *_
   for (; r.gi < r.ge; ++r.gi) {
     const WireSeg &sg = r.seg(segs, nSegs);
     const uint64_t g = r.gi - sg.group0, t = g * 64 + lane;
-    const uint64_t e = t < sg.n ? (c.encode(raw[sg.raw + t], sg.base) & wmask) : 0ull;
+    const uint64_t e = t < sg.n ? (c.encode(raw[rm(sg.raw + t)], sg.base) & wmask) : 0ull;
     uint64_t word = 0;
     for (uint32_t k = 0; k < K; ++k) {
       const uint32_t idx = a + k;
@@ -124,13 +125,14 @@ __global__ __launch_bounds__(WIRE_THREADS) void wireUnpackKernel(const uint64_t 
   }
 }
 
-// Raw gather: dst[seg.wire + t] = src[seg.raw + t] (a rank's own runs, which
-// never touch the wire, into its window).
+// Raw gather: dst[seg.wire + t] = src[rm(seg.raw + t)] (a rank's own runs,
+// which never touch the wire, into its window; or every run into the raw send
+// buffer).
 template <bool kLds>
 __global__ __launch_bounds__(WIRE_THREADS) void segCopyKernel(const uint64_t *__restrict__ src,
                                                               uint64_t *__restrict__ dst,
                                                               const WireSeg *__restrict__ gsegs, uint32_t nSegs,
-                                                              uint64_t totalGroups, uint64_t per) {
+                                                              uint64_t totalGroups, uint64_t per, RoundMap rm) {
   __shared__ WireSeg lds[kLds ? WIRE_MAX_SEGS_LDS : 1];
   const WireSeg *segs = stageSegs<kLds>(gsegs, nSegs, lds);
   const uint32_t lane = threadIdx.x & (WAVE - 1);
@@ -138,7 +140,7 @@ __global__ __launch_bounds__(WIRE_THREADS) void segCopyKernel(const uint64_t *__
   for (; r.gi < r.ge; ++r.gi) {
     const WireSeg &sg = r.seg(segs, nSegs);
     const uint64_t t = (r.gi - sg.group0) * 64 + lane;
-    if (t < sg.n) dst[sg.wire + t] = __builtin_nontemporal_load(src + sg.raw + t);
+    if (t < sg.n) dst[sg.wire + t] = __builtin_nontemporal_load(src + rm(sg.raw + t));
   }
 }
 
@@ -158,16 +160,16 @@ WireLaunch wireLaunch(uint64_t totalGroups) {
 }  // namespace
 
 void wirePack(const uint64_t *raw, uint64_t *wire, const WireSeg *segs, uint32_t nSegs, uint64_t totalGroups,
-              const WireCodec &c, hipStream_t s) {
+              const WireCodec &c, hipStream_t s, RoundMap rm) {
   if (totalGroups == 0) return;
   HJ_CHECK(c.w >= 1 && c.w <= 64 && nSegs >= 1, "wirePack: w=%u nSegs=%u", c.w, nSegs);
   const WireLaunch l = wireLaunch(totalGroups);
   if (nSegs <= WIRE_MAX_SEGS_LDS)
     hipLaunchKernelGGL(wirePackKernel<true>, dim3(l.blocks), dim3(WIRE_THREADS), 0, s, raw, wire, segs, nSegs,
-                       totalGroups, l.per, c);
+                       totalGroups, l.per, c, rm);
   else
     hipLaunchKernelGGL(wirePackKernel<false>, dim3(l.blocks), dim3(WIRE_THREADS), 0, s, raw, wire, segs, nSegs,
-                       totalGroups, l.per, c);
+                       totalGroups, l.per, c, rm);
   HIP_CHECK_LAUNCH();
 }
 
@@ -186,16 +188,16 @@ void wireUnpack(const uint64_t *wire, uint64_t *raw, const WireSeg *segs, uint32
 }
 
 void segCopy(const uint64_t *src, uint64_t *dst, const WireSeg *segs, uint32_t nSegs, uint64_t totalGroups,
-             hipStream_t s) {
+             hipStream_t s, RoundMap rm) {
   if (totalGroups == 0) return;
   HJ_CHECK(nSegs >= 1, "segCopy: no segments for %lu groups", (unsigned long)totalGroups);
   const WireLaunch l = wireLaunch(totalGroups);
   if (nSegs <= WIRE_MAX_SEGS_LDS)
     hipLaunchKernelGGL(segCopyKernel<true>, dim3(l.blocks), dim3(WIRE_THREADS), 0, s, src, dst, segs, nSegs,
-                       totalGroups, l.per);
+                       totalGroups, l.per, rm);
   else
     hipLaunchKernelGGL(segCopyKernel<false>, dim3(l.blocks), dim3(WIRE_THREADS), 0, s, src, dst, segs, nSegs,
-                       totalGroups, l.per);
+                       totalGroups, l.per, rm);
   HIP_CHECK_LAUNCH();
 }
 

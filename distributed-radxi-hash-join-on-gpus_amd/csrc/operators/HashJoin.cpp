@@ -520,7 +520,9 @@ std::vector<uint64_t> HashJoin::workspaceParts() const {
     const uint64_t recv =
         N == 1 ? (plan.sampledNetwork ? sampledCap(n[r], roundLp) : n[r]) : g[r] / N + g[r] / (4 * N) + (1 << 20);
     recvTotal[r] = recv;
-    if (N > 1 && !plan.oneSided) parts.push_back((plan.sampledNetwork ? n[r] + n[r] / 8 : n[r]) * wordB);  // send buffer
+    // send buffer (sampled: slice margins; round-interleaved slices up to half again, SampledShuffle)
+    if (N > 1 && !plan.oneSided)
+      parts.push_back((plan.sampledNetwork ? n[r] + (plan.roundLp ? n[r] / 2 : n[r] / 8) : n[r]) * wordB);
     if (plan.wireBits[r]) parts.push_back((n[r] + recv) * ((plan.wireBits[r] + 7) / 8) + (64ull << 10));  // wire buffers
     else if (N > 1 && plan.sampledNetwork && !plan.oneSided) parts.push_back(n[r] * 8 + (64ull << 10));  // gathered runs
     parts.push_back(recv * wordB);  // window
@@ -829,7 +831,8 @@ JoinResult HashJoin::runImpl() {
   result.innerReceived = run.inner->computeLocalWindowSize();
   result.outerReceived = run.outer->computeLocalWindowSize();
   result.sampledNetwork = run.sampled;
-  result.roundWindows = (run.inner->roundMap().on() ? 1u : 0u) + (run.outer->roundMap().on() ? 1u : 0u);
+  result.roundWindows = (run.inner->roundMap().on() || run.inner->sendRounded() ? 1u : 0u) +
+                        (run.outer->roundMap().on() || run.outer->sendRounded() ? 1u : 0u);
   result.directScatter = run.inner->directScatter() || run.outer->directScatter();
   Measurements::storeLocalPartitioningDetails(result.innerReceived + result.outerReceived, result.localItems);
   Measurements::storeBuildProbeDetails(result.innerReceived, result.outerReceived, result.buildProbeItems);

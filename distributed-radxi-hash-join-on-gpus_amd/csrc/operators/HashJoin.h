@@ -58,7 +58,7 @@ struct JoinResult {
   uint64_t innerLocal = 0, outerLocal = 0;
   bool sampledNetwork = false;     // network pass sized from a sampled histogram (N == 1)
   uint32_t networkFallbacks = 0;   // sampled pass overflowed -> exact re-run inside this join
-  uint32_t roundWindows = 0;       // network windows with round-interleaved slices (kernels::RoundMap)
+  uint32_t roundWindows = 0;       // network windows (N > 1: send buffers) with round-interleaved slices (kernels::RoundMap)
   bool sampledLocal = false;       // local pass sized from a sampled histogram
   bool bitmapJoin = false;         // single-level bitmap join counted the matches (no local pass)
   uint32_t localFallbacks = 0;     // sampled local pass overflowed -> exact re-run

@@ -115,8 +115,29 @@ void SampledShuffle::sampleAndAssign() {
         s.estimate[(size_t)c * F + d] = (uint64_t)std::llround(sum);
       }
     s.capTotal = cur;
+    // Round-interleaved send buffer (kernels::RoundMap): slice i = (c G + g) F
+    // + d starts at logical i << lv; taken when its slots stay within half
+    // again the linear total (uneven slices keep linear ones).
+    s.rm = kernels::RoundMap();
+    uint64_t logical = cur;
+    if (const uint32_t lp = kernels::roundLpFor(plan.roundLp, 8)) {
+      uint64_t maxCap = 0;
+      for (uint64_t c : s.cap) maxCap = std::max(maxCap, c);
+      uint32_t lns = 0, lv = lp;
+      while ((1ull << lns) < cells) ++lns;
+      while ((1ull << lv) < maxCap) ++lv;
+      const uint64_t slots = kernels::roundSlots(maxCap, lp, lns);
+      if (maxCap && lns + lv < 48 && slots <= cur + cur / 2 + (1ull << 20)) {
+        s.rm.lp = lp;
+        s.rm.lv = lv;
+        s.rm.lns = lns;
+        for (size_t i = 0; i < cells; ++i) s.start[i] = (uint64_t)i << lv;
+        s.capTotal = slots;
+        logical = (uint64_t)cells << lv;
+      }
+    }
     // Claims may run past a slice end by up to n before the overflow is seen.
-    s.narrow = kernels::cursorsNarrow(cur + n);
+    s.narrow = kernels::cursorsNarrow(logical + n);
   }
   hc->assignFromEstimates(sides[0].estimate.data(), sides[1].estimate.data());
 }
@@ -182,6 +203,7 @@ void SampledShuffle::layoutSide(int k) {
   s.windowCap.resize(nodes);
   for (uint32_t r = 0; r < nodes; ++r) s.windowCap[r] = receiveCapacity(k, r);
   s.window.reset(new data::Window(x, s.windowCap[me], ctx, false));
+  s.window->setSendRounded(s.rm.on());
   kernels::WireCodec codec;
   codec.w = plan.wireBits[k];
   codec.ridBits = plan.wireRidBits[k];
@@ -201,6 +223,16 @@ void SampledShuffle::scatterSide(int k) {
   const size_t perChunk = (size_t)G * F * (s.narrow ? 4 : 8);
   s.send = ctx->workspace().getArray<uint64_t>(std::max<uint64_t>(s.capTotal, 1));
   s.cursorsBack = ctx->staging().get(perChunk * s.chunks);
+  s.roundMeta = nullptr;
+  if (s.rm.on()) {
+    uint32_t *m = static_cast<uint32_t *>(ctx->staging().get(16));
+    m[0] = s.rm.lp;
+    m[1] = s.rm.lv;
+    m[2] = s.rm.lns;
+    m[3] = 0;
+    s.roundMeta = ctx->workspace().getArray<uint32_t>(4);
+    ctx->copy(s.roundMeta, m, 16, true, false);
+  }
   s.scattered.assign(s.chunks, nullptr);
   s.window->start();
   const char *key = k == 0 ? "MIMAINPART" : "MOMAINPART";
@@ -211,7 +243,7 @@ void SampledShuffle::scatterSide(int k) {
     const uint8_t *ge = static_cast<const uint8_t *>(s.gend) + c * perChunk;
     if (b1 > b0)
       kernels::netScatter(s.relation->getData(), n, plan.networkBits, plan.keyShift, g, b0, b1, gc, s.send,
-                          ctx->stream(), plan.keyBits, mix, ge, s.narrow ? 1 : 0, !plan.keyOnly);
+                          ctx->stream(), plan.keyBits, mix, ge, s.narrow ? 1 : 0, !plan.keyOnly, s.roundMeta);
     ctx->readBack(static_cast<uint8_t *>(s.cursorsBack) + c * perChunk, gc, perChunk);
     s.scattered[c] = ctx->acquireEvent();
     HIP_CHECK(hipEventRecord(s.scattered[c], ctx->stream()));
@@ -300,6 +332,7 @@ bool SampledShuffle::exchangeSide(int k) {
   uint64_t cur = 0;  // window tuples laid out so far
   for (uint32_t c = 0; c < C; ++c) {
     data::Window::SegmentedChunk sc;
+    sc.sendMap = s.rm;
     sc.sendWords.assign(N, 0);
     sc.sendDispls.assign(N, 0);
     sc.recvWords.assign(N, 0);

@@ -86,7 +86,9 @@ class SampledShuffle {
     std::vector<uint64_t> end64;
     void *gcur = nullptr, *gend = nullptr;
     bool narrow = true;
-    uint64_t capTotal = 0;
+    uint64_t capTotal = 0;               // send buffer slots
+    kernels::RoundMap rm;                // round-interleaved send buffer (kernels::RoundMap), else identity
+    uint32_t *roundMeta = nullptr;       // device copy of rm for the scatter
     uint64_t *send = nullptr;            // claim slices (8-byte words)
     void *cursorsBack = nullptr;         // [C][G][F] final claim cursors (pinned staging)
     std::vector<hipEvent_t> scattered;   // [C]

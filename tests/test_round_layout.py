@@ -76,3 +76,32 @@ def test_round_windows_exact(C, cuda, dist, bitmap):
             assert res["round_windows"] == 0
         if not bitmap and lp and dist != "ZIPF":
             assert res["round_windows"] == 2, res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("raw,sparse", [(True, False), (False, False), (True, True)])
+def test_round_send_buffers_shuffle(C, cuda, raw, sparse):
+    """N > 1 sampled shuffle (2 in-process ranks): the claim slices of each
+    rank's send buffer are round-interleaved (both relations report it) and
+    the runs are gathered (raw words) or packed (codec) through the same slot
+    map; counts equal the oracle and the linear send buffers'."""
+    from test_distributed import run_ranks
+    G = 8_000_000
+    got = {}
+    for lp in (9, 0):
+        def cfg_fn(c, lp=lp):
+            c.network_histogram = C.HistogramMode.SAMPLED
+            c.bitmap_join = False
+            c.chunks = 1
+            c.round_lp = lp
+            c.wire_codec = C.WireCodecMode.OFF if raw else C.WireCodecMode.ON
+        inner, outer = C.GenSpec(seed=1234), C.GenSpec(seed=99)
+        inner.sparse64 = outer.sparse64 = sparse
+        results, exp = run_ranks(C, 2, "device", G, G, cfg_fn, inner=inner, outer=outer)
+        for res, plan in results:
+            assert plan.sampled_network and res["network_fallbacks"] == 0, res
+            assert res["round_windows"] == (2 if lp else 0), res
+            if exp is not None:
+                assert res["global_matches"] == exp
+        got[lp] = results[0][0]["global_matches"]
+    assert got[9] == got[0]
