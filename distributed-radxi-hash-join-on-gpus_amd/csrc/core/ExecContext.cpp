@@ -166,8 +166,10 @@ void ExecContext::synchronize() const {
   utils::waitStream(stream_, comm_, "compute stream");
 }
 
-void ExecContext::copy(void *dst, const void *src, uint64_t bytes, bool toDevice, bool fromDevice) const {
+void ExecContext::copy(void *dst, const void *src, uint64_t bytes, bool toDevice, bool fromDevice,
+                       hipStream_t s) const {
   if (bytes == 0) return;
+  if (!s) s = stream_;
   if (!onDevice()) {
     std::memcpy(dst, src, bytes);
     return;
@@ -188,10 +190,10 @@ void ExecContext::copy(void *dst, const void *src, uint64_t bytes, bool toDevice
   // kernels over the host link (no copy engine: bench_skew's first join paid
   // ~5-10 ms in its local pass for the first SDMA upload of a process).
   if (toDevice && !fromDevice && staging_->owns(src)) {
-    kernels::copyFromHost(dst, src, bytes, stream_);
+    kernels::copyFromHost(dst, src, bytes, s);
     return;
   }
-  HIP_CHECK(hipMemcpyAsync(dst, src, bytes, k, stream_));
+  HIP_CHECK(hipMemcpyAsync(dst, src, bytes, k, s));
 }
 
 void ExecContext::readBack(void *dst, const void *src, uint64_t bytes, hipStream_t s) const {

@@ -57,7 +57,8 @@ class ExecContext {
   performance::Timeline &timeline() { return *timeline_; }  // sub-phase spans of the current join (.perf keys)
 
   void synchronize() const;                 // compute + comm streams
-  void copy(void *dst, const void *src, uint64_t bytes, bool toDevice, bool fromDevice) const;  // async on stream()
+  // Async on s (default: stream()).
+  void copy(void *dst, const void *src, uint64_t bytes, bool toDevice, bool fromDevice, hipStream_t s = nullptr) const;
   // Device -> host read-back on stream s (default: stream()).  Into the
   // pinned staging arena it is one of the engine's own kernels writing the
   // mapped host memory (no copy engine, no runtime blit kernel); elsewhere a

@@ -111,6 +111,11 @@ class Window {
   // (informational: the window itself is linear).
   void setSendRounded(bool on) { sendRounded_ = on; }
   bool sendRounded() const { return sendRounded_; }
+  // An event recorded behind every kernel that writes the window's data (the
+  // sampled single-rank scatter), or null: the local pass may then start its
+  // histogram on another stream as soon as this event has fired.
+  void setDataReady(hipEvent_t e) { dataReady_ = e; }
+  hipEvent_t dataReady() const { return dataReady_; }
   uint32_t tupleBytes() const { return elemBytes ? elemBytes : (wide ? 16 : 8); }
   bool holdsFragments() const { return elemBytes == 4; }
   bool isWide() const { return wide; }
@@ -145,6 +150,7 @@ class Window {
   bool wide;
   kernels::RoundMap roundMap_;
   bool sendRounded_ = false;
+  hipEvent_t dataReady_ = nullptr;
   uint32_t elemBytes = 0;  // 0: the tuple format's size
   bool open = false;
   std::vector<hipEvent_t> ready, done;

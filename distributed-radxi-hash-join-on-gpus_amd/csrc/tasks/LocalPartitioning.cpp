@@ -143,27 +143,44 @@ void LocalPartitioning::partitionImpl(data::Window *w, int which) {
     uint64_t *pbeg = ctx->workspace().getArray<uint64_t>(std::max<uint64_t>(P, 1));
     kernels::LocalItem *dItems = ctx->workspace().getArray<kernels::LocalItem>(std::max<uint32_t>(nItems, 1));
     uint32_t *dLb = ctx->workspace().getArray<uint32_t>(owned + 1);
-    ctx->copy(dItems, it.data(), (uint64_t)nItems * sizeof(kernels::LocalItem), true, false);
-    ctx->copy(dLb, lb.data(), (owned + 1) * 4ull, true, false);
     if (overflowFlag.size() <= (size_t)which) {
       overflowFlag.resize(which + 1, nullptr);
       overflowBack.resize(which + 1, nullptr);
     }
     if (!overflowFlag[which]) overflowFlag[which] = ctx->workspace().getArray<unsigned int>(1);
-    ctx->zero(overflowFlag[which], sizeof(unsigned int));
+    // HPCJOIN_LP_PREP=1 (A/B only): the sampled histogram and the slot
+    // layout, which read only this window, run on the decode stream (idle at
+    // N = 1) next to whatever the compute stream still does -- the outer
+    // network scatter for the inner side, the inner local scatter for the
+    // outer side -- once the window's data is complete (Window::dataReady).
+    // Measured neutral (18.97 vs 18.93 ms per 1B x 1B general join: the
+    // overlapped histograms slow the scatters beside them by as much as they
+    // hide, profiles/r6/ab/lp_prep_stream_r7q.jsonl), so off by default.
+    const char *pe = std::getenv("HPCJOIN_LP_PREP");
+    const bool prep = w->dataReady() && ctx->numberOfNodes() == 1 && pe && pe[0] == '1';
+    const hipStream_t ps = prep ? ctx->decodeStream() : ctx->stream();
+    if (prep) HIP_CHECK(hipStreamWaitEvent(ps, w->dataReady(), 0));
+    ctx->copy(dItems, it.data(), (uint64_t)nItems * sizeof(kernels::LocalItem), true, false, ps);
+    ctx->copy(dLb, lb.data(), (owned + 1) * 4ull, true, false, ps);
+    ctx->zero(overflowFlag[which], sizeof(unsigned int), ps);
     performance::Measurements::add("LPHISTELEM", (double)(xp.recvTotal / S), "tuples");
     // Back-to-back spans on one stream share their boundary events.
-    hipEvent_t p0 = tl.mark(ctx->stream());
+    hipEvent_t p0 = tl.mark(ps);
     tl.beginAt("LPHISTCOMP", p0);
-    kernels::localHistogram(w->getData(), wide, dItems, nItems, shift, bits, itemHist, ctx->stream(), S, frag,
-                            w->roundMap());
-    hipEvent_t p1 = tl.mark(ctx->stream());
+    kernels::localHistogram(w->getData(), wide, dItems, nItems, shift, bits, itemHist, ps, S, frag, w->roundMap());
+    hipEvent_t p1 = tl.mark(ps);
     tl.endAt("LPHISTCOMP", p1);
     tl.beginAt("LPOFFSET", p1);
     kernels::localSampledLayout(itemHist, dLb, dItems, owned, bits, S, caps, starts, scanWs, gcur, gend, pbeg, cap,
-                                ctx->stream(), align);
-    hipEvent_t p2 = tl.mark(ctx->stream());
+                                ps, align);
+    hipEvent_t p2 = tl.mark(ps);
     tl.endAt("LPOFFSET", p2);
+    if (prep) {
+      hipEvent_t done = ctx->acquireEvent();
+      HIP_CHECK(hipEventRecord(done, ps));
+      HIP_CHECK(hipStreamWaitEvent(ctx->stream(), done, 0));
+      p2 = tl.mark(ctx->stream());
+    }
     tl.beginAt("LPPART", p2);
     kernels::localScatter(w->getData(), wide, dItems, nItems, shift, bits, gcur, false, sout, ctx->stream(), gend,
                           split, plan.localGeometry, frag, w->roundMap());

@@ -193,6 +193,7 @@ void SampledNetworkPartitioning::scatterSide(int k) {
   ctx->readBack(s.cursorsBack, s.gstart, bytes);
   if (!s.cursorsReady) s.cursorsReady = ctx->acquireEvent();
   HIP_CHECK(hipEventRecord(s.cursorsReady, ctx->stream()));
+  s.window->setDataReady(s.cursorsReady);
 }
 
 bool SampledNetworkPartitioning::finishSide(int k) {
