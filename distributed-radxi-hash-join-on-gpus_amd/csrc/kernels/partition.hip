@@ -1609,6 +1609,46 @@ __global__ __launch_bounds__(NT) void localHistogramKernel(const void *__restric
     itemHist[(uint64_t)blockIdx.x * F + d] = hsh[d] + hsh[F + d] + hsh[2 * F + d] + hsh[3 * F + d];
 }
 
+// 8-byte words whose digit lies inside one 32-bit half (HALF 0 = low word,
+// 1 = high word; shift is then relative to that half): every thread loads
+// only that half, and both of a batch's two sampled tiles are in flight
+// before the first is counted (an item of the 1B x 1B general path holds two
+// sampled tiles: one HBM round trip instead of two).
+template <int HALF>
+__global__ __launch_bounds__(NT) void localHistogramHalfKernel(const uint32_t *__restrict__ in,
+                                                               const LocalItem *__restrict__ items, uint32_t shift,
+                                                               uint32_t bits, uint32_t *__restrict__ itemHist,
+                                                               uint32_t stride, RoundMap rm) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t hsh[];
+  const uint32_t F = 1u << bits, mask = F - 1;
+  const int wid = threadIdx.x / WAVE;
+  for (uint32_t i = threadIdx.x; i < 4 * F; i += NT) hsh[i] = 0;
+  __syncthreads();
+  const LocalItem it = items[blockIdx.x];
+  uint32_t *wh = hsh + wid * F;
+  const uint32_t step = PART_TILE * stride;
+  for (uint32_t base = 0; base < it.len; base += 2 * step) {
+    uint32_t w[2][PART_ITEMS];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < (int)PART_ITEMS; ++i) {
+        const uint32_t idx = base + t * step + i * NT + threadIdx.x;
+        w[t][i] = idx < it.len ? __builtin_nontemporal_load(in + 2 * rm(it.begin + idx) + HALF) : 0u;
+      }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < (int)PART_ITEMS; ++i) {
+        const uint32_t idx = base + t * step + i * NT + threadIdx.x;
+        if (idx < it.len) atomicAdd(&wh[(w[t][i] >> shift) & mask], 1u);
+      }
+  }
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < F; d += NT)
+    itemHist[(uint64_t)blockIdx.x * F + d] = hsh[d] + hsh[F + d] + hsh[2 * F + d] + hsh[3 * F + d];
+}
+
 void localHistogram(const void *in, bool wide, const LocalItem *items, uint32_t nItems, uint32_t shift,
                     uint32_t bits, uint32_t *itemHist, hipStream_t s, uint32_t sampleStride, bool frag, RoundMap rm) {
   HJ_CHECK(bits <= MAX_PART_BITS, "localHistogram: bits=%u out of range", bits);
@@ -1616,7 +1656,16 @@ void localHistogram(const void *in, bool wide, const LocalItem *items, uint32_t 
   HJ_CHECK(!(wide && frag), "localHistogram: fragments are not wide tuples");
   if (nItems == 0) return;
   const size_t lds = size_t(4) << bits << 2;
-  if (frag)
+  const char *hv = std::getenv("HPCJOIN_LH_HALF");  // "0": the whole-word kernel (A/B)
+  if (!wide && !frag && (shift + bits <= 32 || shift >= 32) && !(hv && hv[0] == '0')) {
+    const auto *w = static_cast<const uint32_t *>(in);
+    if (shift >= 32)
+      hipLaunchKernelGGL(localHistogramHalfKernel<1>, dim3(nItems), dim3(NT), lds, s, w, items, shift - 32, bits,
+                         itemHist, sampleStride, rm);
+    else
+      hipLaunchKernelGGL(localHistogramHalfKernel<0>, dim3(nItems), dim3(NT), lds, s, w, items, shift, bits,
+                         itemHist, sampleStride, rm);
+  } else if (frag)
     hipLaunchKernelGGL(localHistogramKernel<2>, dim3(nItems), dim3(NT), lds, s, in, items, shift, bits, itemHist,
                        sampleStride, rm);
   else if (wide)
