@@ -394,6 +394,8 @@ def measure(C, info, ctx, comm, on_gpu, G_R, G_S, inner, outer, cfg, rel_loc, st
         "plan": repr(join.plan),
         "sampled_network": bool(results[-1]["sampled_network"]),
         "network_fallbacks": sum(r["network_fallbacks"] for r in [first] + results),
+        # two-level plans: network windows (N > 1: send buffers) with round-interleaved slices
+        "round_windows": results[-1].get("round_windows", 0),
         "phases_ms": {k: round(sum(r[k] for r in results) / len(results), 3) for k in PHASES},
         "results": results,
         "join": join,
