@@ -1437,9 +1437,11 @@ uint64_t sampledWindowCapacity(const SampleScale &sc, uint32_t F, uint32_t round
   for (uint32_t g = 0; g < NGROUPS; ++g) {
     if (sc.total[g] <= 0) continue;
     const double scale = sc.seen[g] > 0 ? sc.total[g] / sc.seen[g] : 1.0;
-    const double est = sc.total[g] / F;
-    const double sigma = std::sqrt(std::max(est, scale) * scale);
-    maxCap = std::max(maxCap, est + (sc.sigmas + 5.0) * sigma + sc.frac * est + sc.floor + 16.0);
+    // The largest slice: its sampled estimate up to 5 sigma above the mean,
+    // plus the layout kernel's margin taken at that estimate.
+    const double mean = sc.total[g] / F;
+    const double hi = mean + 5.0 * std::sqrt(std::max(mean, scale) * scale);
+    maxCap = std::max(maxCap, hi + sc.sigmas * std::sqrt(std::max(hi, scale) * scale) + sc.frac * hi + sc.floor + 16.0);
   }
   uint32_t lns = 0;
   while ((1u << lns) < NGROUPS * F) ++lns;

@@ -105,3 +105,28 @@ def test_round_send_buffers_shuffle(C, cuda, raw, sparse):
                 assert res["global_matches"] == exp
         got[lp] = results[0][0]["global_matches"]
     assert got[9] == got[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [8, 11])
+@pytest.mark.parametrize("sparse", [False, True])
+def test_round_windows_network_bits(C, cuda, bits, sparse):
+    """Round-interleaved windows at other fan-outs (G * F = 2048 or 16384
+    slices per round): same count as linear slices, both windows rounded on
+    the two-level plan."""
+    G_R = 1 << 22
+    ctx = C.ExecContext("device", 0, C.LocalCommunicator())
+    inner, outer = C.GenSpec(seed=5), C.GenSpec(seed=6)
+    inner.sparse64 = outer.sparse64 = sparse
+    R = C.Relation(G_R, G_R, "device", 0)
+    S = C.Relation(G_R, G_R, "device", 0)
+    R.generate(inner, 0)
+    S.generate(outer, 0)
+    for lp in (9, 0):
+        cfg = _cfg(C, lp, False)
+        cfg.network_bits = bits
+        j = C.HashJoin(R, S, ctx, cfg)
+        assert j.plan.network_bits == bits, j.plan
+        res = j.run()
+        info = {k: res[k] for k in ("global_matches", "round_windows", "network_fallbacks", "sampled_network")}
+        assert res["global_matches"] == G_R and res["round_windows"] == (2 if lp else 0), (info, repr(j.plan))
